@@ -1,0 +1,119 @@
+/*
+ * mando.h — C-ABI of libmando, the MI355X-native consensus core for Mandalorion's D module.
+ *
+ * Every entry point is extern "C", takes plain pointers and sizes, returns int (0 = ok, < 0 = error
+ * code) and never throws.  mando_last_error() returns a thread-local message for the last failure.
+ * Device memory lives inside an opaque mando_ctx (one per GPU, not re-entrant; several ctxs may run
+ * concurrently).  The Python host binds these with ctypes (mandalorion_amd/_lib.py); the bindings a
+ * reference maintainer would add are shown in INTEGRATION.md.
+ *
+ * Reference interfaces replaced (paths relative to the upstream Mandalorion tree):
+ *   mando_poa_batch / mando_poa_batch_device
+ *       replaces the abPOA CLI call `abpoa -M 5 -r 0 [-S] root.fasta > root.consensus.fasta`
+ *       and the read-back of its FASTA  — utils/SpliceDefineConsensus.py:911-926
+ *       (abPOA v1.4.1, pinned by setup.sh:17-20).
+ *   mando_orient_batch
+ *       replaces `mp.Aligner(seq=first, preset='map-ont')` + the per-read `map()` primary-hit /
+ *       strand loop — utils/SpliceDefineConsensus.py:895-907.
+ *   mando_mt_permutation
+ *       replaces `np.random.choice(np.arange(n), min(n, k), replace=False)` on the process-global
+ *       legacy RandomState — utils/SpliceDefineConsensus.py:505, :818, :884.
+ */
+#ifndef MANDO_H
+#define MANDO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MANDO_ABI_VERSION 1
+
+enum mando_status {
+    MANDO_OK = 0,
+    MANDO_E_ARG = -1,         /* bad argument (null pointer, negative size, inconsistent offsets) */
+    MANDO_E_HIP = -2,         /* HIP runtime error (message in mando_last_error) */
+    MANDO_E_NOMEM = -3,       /* device or host allocation failed */
+    MANDO_E_CAP = -4,         /* caller-provided output buffer too small */
+    MANDO_E_UNSUPPORTED = -5, /* requested mode not implemented on this build */
+    MANDO_E_INTERNAL = -6,    /* kernel reported an inconsistent state */
+    MANDO_E_NODEV = -7        /* no HIP device visible */
+};
+
+typedef struct mando_ctx mando_ctx;
+
+/* abPOA-equivalent parameters.  Defaults (mando_poa_default_params) are the reference's
+ * `abpoa -M 5 -r 0`: match 5, mismatch 4, convex gaps (4,2) and (24,1), adaptive band
+ * w = band_b + (int)(band_f * qlen) with band_b 10, band_f 0.01; seeding (-S) off, k 19, w 10,
+ * min_w 500. */
+typedef struct {
+    int32_t match, mismatch;
+    int32_t gap_open1, gap_ext1, gap_open2, gap_ext2;
+    int32_t band_b;
+    float band_f;
+    int32_t seeding, k, w, min_w;
+} mando_poa_params;
+
+const char *mando_last_error(void);
+int mando_abi_version(void);
+void mando_poa_default_params(mando_poa_params *p);
+
+/* Number of visible HIP devices (0 on a machine without a GPU; never fails for that reason). */
+int mando_device_count(int *out);
+
+int mando_ctx_create(int device_ordinal, mando_ctx **out);
+void mando_ctx_destroy(mando_ctx *ctx);
+
+/* Batched POA consensus, host buffers.
+ *   n_groups groups; group g = reads [grp_off[g], grp_off[g+1]) in FINAL abPOA input order
+ *   (post-subsample, post-orientation, duplicates kept).  Read r = seqs[seq_off[r] .. seq_off[r+1])
+ *   as ASCII (ACGTN, any case; other bytes are treated as N).
+ *   seeding_per_group may be NULL (all 0); a nonzero entry requests the -S path.
+ *   On success cons_off[0..n_groups] holds offsets into cons_out (ASCII ACGTN, no separators) and,
+ *   when cells_out is non-NULL, cells_out[g] the number of banded DP cells evaluated for group g.
+ *   Returns MANDO_E_CAP (and the required size in cons_off[n_groups]) when cons_cap is too small. */
+int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *seqs,
+                    const int64_t *seq_off, const int64_t *grp_off, int64_t n_groups,
+                    const uint8_t *seeding_per_group, uint8_t *cons_out, int64_t cons_cap,
+                    int64_t *cons_off, int64_t *cells_out);
+
+/* Same computation with every input already resident in device memory (HBM) — the form the
+ * benchmark times.  d_seqs holds 2-bit-free encoded bases (0..4 = ACGTN), d_seq_off/d_grp_off are
+ * device int64 arrays as above, outputs are device arrays: d_cons (capacity cons_cap bytes, encoded
+ * 0..4), d_cons_len[n_groups] (int32), d_cells[n_groups] (int64), d_status[n_groups] (int32).
+ * Asynchronous on the ctx's stream; mando_ctx_sync() waits. */
+int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *d_seqs,
+                           const int64_t *d_seq_off, const int64_t *d_grp_off, int64_t n_groups,
+                           int64_t max_read_len, int64_t max_group_bases, uint8_t *d_cons,
+                           const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
+                           int32_t *d_status);
+int mando_ctx_sync(mando_ctx *ctx);
+
+/* Device-time of the most recent POA / orientation launch on the ctx stream, from HIP events
+ * recorded around the kernel on that stream (milliseconds). */
+float mando_last_kernel_ms(mando_ctx *ctx);
+/* Number of kernel launches issued by the most recent batch call (the roofline divides by it). */
+int mando_last_kernel_launches(mando_ctx *ctx);
+
+/* Read orientation (mappy map-ont strand / primary-hit replacement).  For each group the
+ * reference sequence is the group's first read.  For every read r, n_hits[r] in {0,1} is the
+ * number of primary hits and hit_strands[r*max_hits] is +1 / -1.  seqs as in mando_poa_batch. */
+int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_off,
+                       const int64_t *grp_off, int64_t n_groups, int8_t *hit_strands,
+                       int32_t max_hits, int32_t *n_hits);
+
+/* Device self-test of the wave-level primitives the kernels use (scan / reduce); *bad = number of
+ * mismatching lanes (0 = pass). */
+int mando_selftest(mando_ctx *ctx, int *bad);
+
+/* numpy legacy RandomState(seed).permutation(n)[:k] replayed `n_draws` times in sequence from one
+ * fresh MT19937 state: draw d uses n = ns[d], k = ks[d]; outputs concatenated in out (int64). */
+int mando_mt_permutation(uint32_t seed, const int64_t *ns, const int64_t *ks, int64_t n_draws,
+                         int64_t *out, int64_t out_cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MANDO_H */

@@ -1,0 +1,187 @@
+"""ctypes binding of libmando.so (the C-ABI declared in include/mando.h).
+
+The product path is HIP-only: if the shared library is missing, or no gfx950 device is visible,
+every compute entry point raises instead of falling back to a CPU implementation.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmando.so")
+
+# Every symbol include/mando.h declares (tests check the library exports all of them).
+EXPORTED = (
+    "mando_last_error",
+    "mando_abi_version",
+    "mando_poa_default_params",
+    "mando_device_count",
+    "mando_ctx_create",
+    "mando_ctx_destroy",
+    "mando_poa_batch",
+    "mando_poa_batch_device",
+    "mando_ctx_sync",
+    "mando_last_kernel_ms",
+    "mando_last_kernel_launches",
+    "mando_orient_batch",
+    "mando_selftest",
+    "mando_mt_permutation",
+)
+
+STATUS = {
+    0: "MANDO_OK",
+    -1: "MANDO_E_ARG",
+    -2: "MANDO_E_HIP",
+    -3: "MANDO_E_NOMEM",
+    -4: "MANDO_E_CAP",
+    -5: "MANDO_E_UNSUPPORTED",
+    -6: "MANDO_E_INTERNAL",
+    -7: "MANDO_E_NODEV",
+}
+
+
+class MandoError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class PoaParams(ctypes.Structure):
+    """mando_poa_params — defaults are the reference's `abpoa -M 5 -r 0`."""
+
+    _fields_ = [
+        ("match", ctypes.c_int32),
+        ("mismatch", ctypes.c_int32),
+        ("gap_open1", ctypes.c_int32),
+        ("gap_ext1", ctypes.c_int32),
+        ("gap_open2", ctypes.c_int32),
+        ("gap_ext2", ctypes.c_int32),
+        ("band_b", ctypes.c_int32),
+        ("band_f", ctypes.c_float),
+        ("seeding", ctypes.c_int32),
+        ("k", ctypes.c_int32),
+        ("w", ctypes.c_int32),
+        ("min_w", ctypes.c_int32),
+    ]
+
+    @classmethod
+    def defaults(cls) -> "PoaParams":
+        p = cls()
+        load().mando_poa_default_params(ctypes.byref(p))
+        return p
+
+
+_lib = None
+_lock = threading.Lock()
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+
+
+def load(path: str | None = None):
+    """Load libmando.so and declare argument types.  Raises if the library is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise MandoError(-7, f"{p} not built (run __graft_entry__.build() or make -C mandalorion_amd/csrc)")
+        lib = ctypes.CDLL(p)
+        lib.mando_last_error.restype = ctypes.c_char_p
+        lib.mando_last_error.argtypes = []
+        lib.mando_abi_version.restype = ctypes.c_int
+        lib.mando_poa_default_params.argtypes = [_P]
+        lib.mando_poa_default_params.restype = None
+        lib.mando_device_count.argtypes = [_P]
+        lib.mando_ctx_create.argtypes = [ctypes.c_int, _P]
+        lib.mando_ctx_destroy.argtypes = [_P]
+        lib.mando_ctx_destroy.restype = None
+        lib.mando_ctx_sync.argtypes = [_P]
+        lib.mando_poa_batch.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]
+        lib.mando_poa_batch_device.argtypes = [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]
+        lib.mando_last_kernel_ms.argtypes = [_P]
+        lib.mando_last_kernel_ms.restype = ctypes.c_float
+        lib.mando_last_kernel_launches.argtypes = [_P]
+        lib.mando_orient_batch.argtypes = [_P, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
+        lib.mando_mt_permutation.argtypes = [ctypes.c_uint32, _P, _P, _I64, _P, _I64]
+        if hasattr(lib, "mando_selftest"):
+            lib.mando_selftest.argtypes = [_P, _P]
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().mando_last_error()
+        raise MandoError(rc, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(load().mando_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def ptr(a: np.ndarray | None) -> int | None:
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+class Context:
+    """One mando_ctx per device (HIP stream + device buffers)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        check(self.lib.mando_ctx_create(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self.lib.mando_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self) -> None:
+        check(self.lib.mando_ctx_sync(self.handle))
+
+    def last_kernel_ms(self) -> float:
+        return float(self.lib.mando_last_kernel_ms(self.handle))
+
+    def last_kernel_launches(self) -> int:
+        return int(self.lib.mando_last_kernel_launches(self.handle))
+
+    def selftest(self) -> int:
+        bad = ctypes.c_int(-1)
+        check(self.lib.mando_selftest(self.handle, ctypes.byref(bad)))
+        return bad.value
+
+
+_ctx_cache: dict[int, Context] = {}
+
+
+def context(device: int = 0) -> Context:
+    c = _ctx_cache.get(device)
+    if c is None or c.handle is None:
+        c = Context(device)
+        _ctx_cache[device] = c
+    return c

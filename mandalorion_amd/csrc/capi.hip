@@ -1,0 +1,407 @@
+// capi.hip — C-ABI of libmando (declared in include/mando.h): contexts, device buffers, batch
+// planning for the POA kernel (capacity estimates, LPT work order, overflow re-runs).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/mando.h"
+#include "poa_kernel.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return fail(MANDO_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));   \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t need) {
+        if (need <= bytes && p) return MANDO_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t nb = std::max<size_t>(need, 256);
+        hipError_t e = hipMalloc(&p, nb);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(MANDO_E_NOMEM, std::string("hipMalloc(") + std::to_string(nb) +
+                                           "): " + hipGetErrorString(e));
+        }
+        bytes = nb;
+        return MANDO_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T *as() const {
+        return reinterpret_cast<T *>(p);
+    }
+};
+
+uint8_t g_enc[256];
+struct EncInit {
+    EncInit() {
+        for (int i = 0; i < 256; ++i) g_enc[i] = 4;
+        g_enc['A'] = g_enc['a'] = 0;
+        g_enc['C'] = g_enc['c'] = 1;
+        g_enc['G'] = g_enc['g'] = 2;
+        g_enc['T'] = g_enc['t'] = 3;
+    }
+} g_enc_init;
+const char g_dec[5] = {'A', 'C', 'G', 'T', 'N'};
+
+}  // namespace
+
+struct mando_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int last_launches = 0;
+    bool timed = false;
+    DevBuf ws, counter;
+    DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
+    DevBuf o_hits, o_strand;
+    ~mando_ctx() {
+        for (DevBuf *b : {&ws, &counter, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
+                          &cons_len, &cells, &status, &o_hits, &o_strand})
+            b->release();
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+struct GroupStat {
+    int64_t nreads = 0, first_len = 0, sum = 0, maxlen = 0;
+};
+
+mando::PoaCaps plan_caps(const mando_poa_params &p, int64_t max_first, int64_t max_sum,
+                         int64_t max_len, int64_t max_reads, int attempt) {
+    mando::PoaCaps c;
+    const double grow = (double)(1 << attempt);
+    int64_t rest = std::max<int64_t>(0, max_sum - max_first);
+    int64_t nc = max_first + 2 + (int64_t)(0.06 * grow * (double)rest) + 256;
+    nc = std::min<int64_t>(nc, max_sum + 2 + 64);
+    nc = std::max<int64_t>(nc, max_first + 2 + 64);
+    c.NC = (int32_t)nc;
+    c.DCAP = attempt == 0 ? 16 : (attempt == 1 ? 64 : 255);
+    c.BIGCAP = (int32_t)std::max<int64_t>(max_reads + 8, 16);
+    c.QC = (int32_t)std::max<int64_t>(max_len, 1);
+    const int64_t w = p.band_b + (int64_t)(p.band_f * (float)max_len);
+    const int64_t rowb = ((2 * w + 1 + 96) + 3) & ~int64_t(3);
+    c.TBC = nc * rowb * (int64_t)(attempt + 1);
+    c.KPC = 3 * c.TBC / (attempt == 0 ? 2 : 1);
+    c.SVC = c.TBC / (attempt == 0 ? 2 : 1) * 3;
+    return c;
+}
+
+int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps &caps,
+                 const uint8_t *d_seq, const int64_t *d_seq_off, const int64_t *d_grp_off,
+                 const int32_t *d_gorder, int64_t n_groups, uint8_t *d_cons,
+                 const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
+                 int32_t *d_status, int max_slots) {
+    mando::PoaKArgs a{};
+    a.seq = d_seq;
+    a.seq_off = d_seq_off;
+    a.grp_off = d_grp_off;
+    a.gorder = d_gorder;
+    a.n_groups = (int32_t)n_groups;
+    a.cons = d_cons;
+    a.cons_off = d_cons_off;
+    a.cons_len = d_cons_len;
+    a.cells = d_cells;
+    a.status = d_status;
+    a.caps = caps;
+    a.lay = mando::make_layout(caps);
+    a.slot_bytes = a.lay.total;
+    a.match = p.match;
+    a.mismatch = p.mismatch;
+    a.o1 = p.gap_open1;
+    a.e1 = p.gap_ext1;
+    a.o2 = p.gap_open2;
+    a.e2 = p.gap_ext2;
+    a.band_b = p.band_b;
+    a.band_f = p.band_f;
+    // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    const size_t budget = std::max<size_t>((size_t)1 << 30, (size_t)(0.5 * (double)free_b) + ctx->ws.bytes);
+    int64_t slots = std::min<int64_t>(n_groups, max_slots);
+    while (slots > 1 && (size_t)(slots * a.slot_bytes) > budget) slots /= 2;
+    if (slots < 1) slots = 1;
+    int rc = ctx->ws.ensure((size_t)(slots * a.slot_bytes));
+    if (rc) return rc;
+    rc = ctx->counter.ensure(256);
+    if (rc) return rc;
+    a.ws = ctx->ws.as<char>();
+    a.counter = ctx->counter.as<int32_t>();
+    HIP_TRY(hipMemsetAsync(a.counter, 0, sizeof(int32_t), ctx->stream));
+    HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    HIP_TRY(mando::launch_poa(a, (int)slots, ctx->stream));
+    HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    ctx->timed = true;
+    return MANDO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *mando_last_error(void) { return g_err.c_str(); }
+
+int mando_abi_version(void) { return MANDO_ABI_VERSION; }
+
+void mando_poa_default_params(mando_poa_params *p) {
+    if (!p) return;
+    p->match = 5;
+    p->mismatch = 4;
+    p->gap_open1 = 4;
+    p->gap_ext1 = 2;
+    p->gap_open2 = 24;
+    p->gap_ext2 = 1;
+    p->band_b = 10;
+    p->band_f = 0.01f;
+    p->seeding = 0;
+    p->k = 19;
+    p->w = 10;
+    p->min_w = 500;
+}
+
+int mando_device_count(int *out) {
+    if (!out) return fail(MANDO_E_ARG, "null out");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return MANDO_OK;
+}
+
+int mando_ctx_create(int device_ordinal, mando_ctx **out) {
+    if (!out) return fail(MANDO_E_ARG, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(MANDO_E_NODEV, "no HIP device visible (libmando requires an MI355X / gfx950)");
+    if (device_ordinal < 0 || device_ordinal >= n)
+        return fail(MANDO_E_ARG, "device ordinal out of range");
+    HIP_TRY(hipSetDevice(device_ordinal));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device_ordinal));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(MANDO_E_NODEV, std::string("device is ") + prop.gcnArchName + ", libmando is built for gfx950");
+    mando_ctx *c = new mando_ctx();
+    c->device = device_ordinal;
+    c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return fail(MANDO_E_HIP, "stream/event creation failed");
+    }
+    *out = c;
+    return MANDO_OK;
+}
+
+void mando_ctx_destroy(mando_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    delete ctx;
+}
+
+int mando_ctx_sync(mando_ctx *ctx) {
+    if (!ctx) return fail(MANDO_E_ARG, "null ctx");
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MANDO_OK;
+}
+
+float mando_last_kernel_ms(mando_ctx *ctx) {
+    if (!ctx || !ctx->timed) return -1.0f;
+    float ms = -1.0f;
+    if (hipEventSynchronize(ctx->ev1) != hipSuccess) return -1.0f;
+    if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return -1.0f;
+    return ms;
+}
+
+int mando_last_kernel_launches(mando_ctx *ctx) { return ctx ? ctx->last_launches : 0; }
+
+int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *d_seqs,
+                           const int64_t *d_seq_off, const int64_t *d_grp_off, int64_t n_groups,
+                           int64_t max_read_len, int64_t max_group_bases, uint8_t *d_cons,
+                           const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
+                           int32_t *d_status) {
+    if (!ctx || !params || !d_seqs || !d_seq_off || !d_grp_off || !d_cons || !d_cons_off ||
+        !d_cons_len || !d_cells || !d_status || n_groups < 0 || max_read_len < 0)
+        return fail(MANDO_E_ARG, "mando_poa_batch_device: bad argument");
+    if (params->seeding) return fail(MANDO_E_UNSUPPORTED, "-S seeding path not implemented yet");
+    if (n_groups == 0) return MANDO_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    mando::PoaCaps caps = plan_caps(*params, max_read_len, max_group_bases, max_read_len,
+                                    std::max<int64_t>(1, max_group_bases / std::max<int64_t>(1, max_read_len / 4)), 0);
+    ctx->last_launches = 1;
+    return launch_batch(ctx, *params, caps, d_seqs, d_seq_off, d_grp_off, nullptr, n_groups,
+                        d_cons, d_cons_off, d_cons_len, d_cells, d_status, ctx->n_cu * 8);
+}
+
+int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *seqs,
+                    const int64_t *seq_off, const int64_t *grp_off, int64_t n_groups,
+                    const uint8_t *seeding_per_group, uint8_t *cons_out, int64_t cons_cap,
+                    int64_t *cons_off, int64_t *cells_out) {
+    if (!ctx || !params || !seq_off || !grp_off || !cons_off || n_groups < 0 || cons_cap < 0)
+        return fail(MANDO_E_ARG, "mando_poa_batch: bad argument");
+    if (n_groups == 0) {
+        cons_off[0] = 0;
+        return MANDO_OK;
+    }
+    if (params->seeding) return fail(MANDO_E_UNSUPPORTED, "-S seeding path not implemented yet");
+    if (seeding_per_group)
+        for (int64_t g = 0; g < n_groups; ++g)
+            if (seeding_per_group[g])
+                return fail(MANDO_E_UNSUPPORTED, "-S seeding path not implemented yet");
+    const int64_t n_reads = grp_off[n_groups] - grp_off[0];
+    if (grp_off[0] != 0 || n_reads < 0) return fail(MANDO_E_ARG, "grp_off must start at 0");
+    for (int64_t g = 0; g < n_groups; ++g)
+        if (grp_off[g + 1] < grp_off[g]) return fail(MANDO_E_ARG, "grp_off not monotone");
+    for (int64_t r = 0; r < n_reads; ++r)
+        if (seq_off[r + 1] < seq_off[r]) return fail(MANDO_E_ARG, "seq_off not monotone");
+    const int64_t total = seq_off[n_reads] - seq_off[0];
+    if (total > 0 && !seqs) return fail(MANDO_E_ARG, "null seqs");
+    HIP_TRY(hipSetDevice(ctx->device));
+
+    // encode + per-group statistics
+    std::vector<uint8_t> enc((size_t)std::max<int64_t>(total, 1));
+    for (int64_t i = 0; i < total; ++i) enc[(size_t)i] = g_enc[seqs[seq_off[0] + i]];
+    std::vector<int64_t> soff((size_t)n_reads + 1);
+    for (int64_t r = 0; r <= n_reads; ++r) soff[(size_t)r] = seq_off[r] - seq_off[0];
+    std::vector<GroupStat> gs((size_t)n_groups);
+    int64_t max_first = 0, max_sum = 0, max_len = 0, max_nreads = 0;
+    std::vector<int64_t> ccap((size_t)n_groups + 1, 0);
+    for (int64_t g = 0; g < n_groups; ++g) {
+        GroupStat &s = gs[(size_t)g];
+        s.nreads = grp_off[g + 1] - grp_off[g];
+        for (int64_t r = grp_off[g]; r < grp_off[g + 1]; ++r) {
+            const int64_t L = soff[(size_t)r + 1] - soff[(size_t)r];
+            if (L > 0 && s.first_len == 0) s.first_len = L;
+            s.sum += L;
+            s.maxlen = std::max(s.maxlen, L);
+        }
+        max_first = std::max(max_first, s.first_len);
+        max_sum = std::max(max_sum, s.sum);
+        max_len = std::max(max_len, s.maxlen);
+        max_nreads = std::max(max_nreads, s.nreads);
+        ccap[(size_t)g + 1] = ccap[(size_t)g] + 2 * s.maxlen + 256;
+    }
+    // LPT order: most DP work first
+    std::vector<int32_t> order((size_t)n_groups);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+        const GroupStat &a = gs[(size_t)x], &b = gs[(size_t)y];
+        return (double)(a.sum - a.first_len) * (double)a.first_len >
+               (double)(b.sum - b.first_len) * (double)b.first_len;
+    });
+
+    int rc;
+    if ((rc = ctx->seq.ensure(enc.size())) || (rc = ctx->seq_off.ensure(soff.size() * 8)) ||
+        (rc = ctx->grp_off.ensure(((size_t)n_groups + 1) * 8)) ||
+        (rc = ctx->gorder.ensure((size_t)n_groups * 4)) ||
+        (rc = ctx->cons_off.ensure(((size_t)n_groups + 1) * 8)) ||
+        (rc = ctx->cons.ensure((size_t)ccap[(size_t)n_groups])) ||
+        (rc = ctx->cons_len.ensure((size_t)n_groups * 4)) ||
+        (rc = ctx->cells.ensure((size_t)n_groups * 8)) ||
+        (rc = ctx->status.ensure((size_t)n_groups * 4)))
+        return rc;
+    std::vector<int64_t> goff((size_t)n_groups + 1);
+    for (int64_t g = 0; g <= n_groups; ++g) goff[(size_t)g] = grp_off[g];
+    HIP_TRY(hipMemcpyAsync(ctx->seq.p, enc.data(), enc.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->seq_off.p, soff.data(), soff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->grp_off.p, goff.data(), goff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->cons_off.p, ccap.data(), ccap.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+
+    std::vector<int32_t> st((size_t)n_groups), clen((size_t)n_groups);
+    std::vector<int64_t> cells((size_t)n_groups);
+    std::vector<int32_t> todo = order;
+    std::vector<uint8_t> cons_enc((size_t)ccap[(size_t)n_groups]);
+    ctx->last_launches = 0;
+    for (int attempt = 0; attempt < 4 && !todo.empty(); ++attempt) {
+        int64_t mf = 0, ms = 0, ml = 0, mr = 0;
+        for (int32_t g : todo) {
+            mf = std::max(mf, gs[(size_t)g].first_len);
+            ms = std::max(ms, gs[(size_t)g].sum);
+            ml = std::max(ml, gs[(size_t)g].maxlen);
+            mr = std::max(mr, gs[(size_t)g].nreads);
+        }
+        mando::PoaCaps caps = plan_caps(*params, mf, ms, ml, mr, attempt);
+        HIP_TRY(hipMemcpyAsync(ctx->gorder.p, todo.data(), todo.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+        rc = launch_batch(ctx, *params, caps, ctx->seq.as<uint8_t>(), ctx->seq_off.as<int64_t>(),
+                          ctx->grp_off.as<int64_t>(), ctx->gorder.as<int32_t>(), (int64_t)todo.size(),
+                          ctx->cons.as<uint8_t>(), ctx->cons_off.as<int64_t>(),
+                          ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
+                          ctx->status.as<int32_t>(), ctx->n_cu * 8);
+        if (rc) return rc;
+        ctx->last_launches += 1;
+        HIP_TRY(hipMemcpyAsync(st.data(), ctx->status.p, st.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(clen.data(), ctx->cons_len.p, clen.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(cells.data(), ctx->cells.p, cells.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(cons_enc.data(), ctx->cons.p, cons_enc.size(), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        std::vector<int32_t> again;
+        for (int32_t g : todo) {
+            if (st[(size_t)g] == mando::kStCap) again.push_back(g);
+            else if (st[(size_t)g] != mando::kStOk)
+                return fail(MANDO_E_INTERNAL, "POA kernel reported status " + std::to_string(st[(size_t)g]) +
+                                                  " for group " + std::to_string(g));
+        }
+        todo.swap(again);
+    }
+    if (!todo.empty())
+        return fail(MANDO_E_INTERNAL, "POA workspace capacity still exceeded after retries");
+
+    int64_t used = 0;
+    cons_off[0] = 0;
+    for (int64_t g = 0; g < n_groups; ++g) {
+        const int64_t L = clen[(size_t)g];
+        if (cons_out && used + L <= cons_cap) {
+            const uint8_t *src = cons_enc.data() + ccap[(size_t)g];
+            for (int64_t t = 0; t < L; ++t) cons_out[used + t] = (uint8_t)g_dec[src[t] > 4 ? 4 : src[t]];
+        }
+        used += L;
+        cons_off[g + 1] = used;
+        if (cells_out) cells_out[g] = cells[(size_t)g];
+    }
+    if (used > cons_cap || (!cons_out && used > 0)) return fail(MANDO_E_CAP, "cons_out too small");
+    return MANDO_OK;
+}
+
+int mando_selftest(mando_ctx *ctx, int *bad) {
+    if (!ctx || !bad) return fail(MANDO_E_ARG, "bad argument");
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc = ctx->counter.ensure(256);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->counter.p, 0, 4, ctx->stream));
+    HIP_TRY(mando::run_wave_selftest(ctx->counter.as<int>(), ctx->stream));
+    HIP_TRY(hipMemcpyAsync(bad, ctx->counter.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MANDO_OK;
+}
+
+}  // extern "C"

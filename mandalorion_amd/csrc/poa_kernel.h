@@ -1,0 +1,117 @@
+// poa_kernel.h — internal interface between the C-ABI layer (capi.hip) and the POA kernel
+// (poa_kernel.hip).  Not part of the public ABI (that is include/mando.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mando {
+
+constexpr int kWave = 64;
+constexpr int kCPL = 2;                  // DP cells per lane per chunk
+constexpr int kChunk = kWave * kCPL;     // 128 band columns per chunk
+constexpr int kRing = 8;                 // rows of H/E1/E2 kept in LDS
+constexpr int kRowRing = 64;             // rows of band info kept in LDS
+constexpr int kPreInline = 5;            // predecessor rows stored inline in a row descriptor
+constexpr int kDescInts = 8;             // ints per row descriptor
+constexpr int kRowInfoInts = 8;          // ints per row record in HBM
+constexpr int kNegInf = -(1 << 28);      // "minus infinity" sentinel of the DP (never overflows)
+constexpr int kSrc = 0, kSink = 1;
+// aligned-node group table: [A C G T N] member per base, [5] head (first row of the group's
+// contiguous block), [6] member count
+constexpr int kGtabInts = 8;
+
+// traceback byte layout (one byte per DP cell)
+constexpr int kTbTypeMask = 7;           // 0 M, 1 E1, 2 E2, 3 F1, 4 F2 : source of H
+constexpr int kTbE1Open = 1 << 3;        // E1out[i][j] came from H[i][j]-oe1 (open preferred on ties)
+constexpr int kTbE2Open = 1 << 4;
+constexpr int kTbF1OpenNext = 1 << 5;    // F1[i][j+1] opens from H0[i][j]
+constexpr int kTbF2OpenNext = 1 << 6;
+
+// per-group status codes written by the kernel (match include/mando.h)
+constexpr int kStOk = 0, kStCap = -4, kStInternal = -6, kStUnsupported = -5;
+
+struct PoaCaps {
+    int32_t NC;      // node capacity per group
+    int32_t DCAP;    // in/out edge capacity per ordinary node
+    int32_t BIGCAP;  // in-edge capacity of the sink / out-edge capacity of the source
+    int32_t QC;      // max read length
+    int64_t TBC;     // traceback bytes per read
+    int64_t KPC;     // predecessor-index bytes per read (multi-predecessor rows)
+    int64_t SVC;     // spilled H/E1/E2 ints per read
+};
+
+struct SlotLayout {
+    int64_t base, gid, gtab, in_n, out_n, in_id, out_id, out_w, sink_in, src_out, src_out_w;
+    int64_t order0, order1, pos, remrow, desc, rinfo, tb, kp, sv, qnode, qtgt, qflag, qnb, qoff, qmslot,
+        ins, insmm, score, nxt;
+    int64_t total;
+};
+
+__host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+__host__ __device__ inline SlotLayout make_layout(const PoaCaps &c) {
+    SlotLayout L;
+    int64_t o = 0;
+    const int64_t nc = c.NC, dc = c.DCAP;
+    L.base = o; o = align256(o + nc);
+    L.gid = o; o = align256(o + 4 * nc);
+    L.gtab = o; o = align256(o + 4 * kGtabInts * nc);
+    L.in_n = o; o = align256(o + 4 * nc);
+    L.out_n = o; o = align256(o + 4 * nc);
+    L.in_id = o; o = align256(o + 4 * nc * dc);
+    L.out_id = o; o = align256(o + 4 * nc * dc);
+    L.out_w = o; o = align256(o + 4 * nc * dc);
+    L.sink_in = o; o = align256(o + 4 * (int64_t)c.BIGCAP);
+    L.src_out = o; o = align256(o + 4 * (int64_t)c.BIGCAP);
+    L.src_out_w = o; o = align256(o + 4 * (int64_t)c.BIGCAP);
+    L.order0 = o; o = align256(o + 4 * nc);
+    L.order1 = o; o = align256(o + 4 * nc);
+    L.pos = o; o = align256(o + 4 * nc);
+    L.remrow = o; o = align256(o + 4 * nc);
+    L.desc = o; o = align256(o + 4 * kDescInts * (nc + kWave));
+    L.rinfo = o; o = align256(o + 4 * kRowInfoInts * nc);
+    L.tb = o; o = align256(o + c.TBC);
+    L.kp = o; o = align256(o + c.KPC);
+    L.sv = o; o = align256(o + 4 * c.SVC);
+    const int64_t qc = c.QC + kWave;
+    L.qnode = o; o = align256(o + 4 * qc);
+    L.qtgt = o; o = align256(o + 4 * qc);
+    L.qflag = o; o = align256(o + 4 * qc);
+    L.qnb = o; o = align256(o + 4 * qc);
+    L.qoff = o; o = align256(o + 4 * qc);
+    L.qmslot = o; o = align256(o + 4 * qc);
+    L.ins = o; o = align256(o + 4 * nc);
+    L.insmm = o; o = align256(o + 4 * nc);
+    L.score = o; o = align256(o + 4 * nc);
+    L.nxt = o; o = align256(o + 4 * nc);
+    L.total = o;
+    return L;
+}
+
+struct PoaKArgs {
+    const uint8_t *seq;      // encoded bases 0..4
+    const int64_t *seq_off;  // per read
+    const int64_t *grp_off;  // per group, n_groups+1
+    const int32_t *gorder;   // processing order (may be null: identity)
+    int32_t n_groups;
+    uint8_t *cons;           // encoded consensus output
+    const int64_t *cons_off; // per group capacity offsets, n_groups+1
+    int32_t *cons_len;
+    int64_t *cells;
+    int32_t *status;
+    int32_t *counter;        // work-queue head (zeroed before launch)
+    char *ws;
+    int64_t slot_bytes;
+    PoaCaps caps;
+    SlotLayout lay;
+    int32_t match, mismatch, o1, e1, o2, e2, band_b;
+    float band_f;
+};
+
+// Launch the persistent POA kernel on `stream` with `n_slots` one-wave workgroups.
+hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream);
+
+// Device self-test of the wave primitives (scan/reduce); returns number of mismatches in *bad.
+hipError_t run_wave_selftest(int *d_bad, hipStream_t stream);
+
+}  // namespace mando

@@ -1,0 +1,74 @@
+"""Batched partial-order-alignment consensus on the GPU (libmando `mando_poa_batch`).
+
+Drop-in for the reference's per-isoform abPOA call
+(/root/reference/utils/SpliceDefineConsensus.py:911-926): each group is the ordered list of
+oriented reads that the reference would have written to `root.fasta`; the result per group is the
+sequence abPOA's `-r 0` FASTA record would hold.  Unlike the reference, all groups of all loci go to
+the device in one call.
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+
+
+def pack_groups(groups: Sequence[Sequence[str | bytes]]):
+    """Concatenate groups of reads into (seqs bytes, seq_off int64, grp_off int64)."""
+    parts: list[bytes] = []
+    lens: list[int] = []
+    grp = [0]
+    for g in groups:
+        for s in g:
+            b = s.encode() if isinstance(s, str) else bytes(s)
+            parts.append(b)
+            lens.append(len(b))
+        grp.append(len(lens))
+    seq_off = np.zeros(len(lens) + 1, dtype=np.int64)
+    if lens:
+        np.cumsum(np.asarray(lens, dtype=np.int64), out=seq_off[1:])
+    return b"".join(parts), seq_off, np.asarray(grp, dtype=np.int64)
+
+
+def poa_consensus_batch(
+    groups: Sequence[Sequence[str | bytes]],
+    params: _lib.PoaParams | None = None,
+    seeding: Sequence[bool] | None = None,
+    device: int = 0,
+    return_cells: bool = False,
+):
+    """Consensus of every group (list of str).  Raises MandoError if the HIP path is unavailable."""
+    ctx = _lib.context(device)
+    p = params or _lib.PoaParams.defaults()
+    seqs, seq_off, grp_off = pack_groups(groups)
+    n = len(groups)
+    seed_arr = None
+    if seeding is not None:
+        seed_arr = np.asarray([1 if s else 0 for s in seeding], dtype=np.uint8)
+    cap = int(seq_off[-1]) * 2 + 1024
+    cons = np.zeros(cap, dtype=np.uint8)
+    cons_off = np.zeros(n + 1, dtype=np.int64)
+    cells = np.zeros(max(n, 1), dtype=np.int64)
+    sbuf = np.frombuffer(seqs, dtype=np.uint8) if seqs else np.zeros(1, dtype=np.uint8)
+    _lib.check(
+        ctx.lib.mando_poa_batch(
+            ctx.handle,
+            _lib.ctypes.byref(p),
+            _lib.ptr(sbuf),
+            _lib.ptr(seq_off),
+            _lib.ptr(grp_off),
+            n,
+            _lib.ptr(seed_arr),
+            _lib.ptr(cons),
+            cap,
+            _lib.ptr(cons_off),
+            _lib.ptr(cells),
+        )
+    )
+    raw = cons.tobytes()
+    out = [raw[cons_off[i] : cons_off[i + 1]].decode() for i in range(n)]
+    if return_cells:
+        return out, cells[:n].copy()
+    return out

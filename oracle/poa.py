@@ -1,0 +1,79 @@
+"""ctypes loader for oracle/poa_ref.c — TEST INFRASTRUCTURE ONLY (checker, never the product).
+
+Mirrors mando_poa_batch: groups of ASCII reads in abPOA input order -> consensus strings + DP cell
+counts.  Builds oracle/build/libpoa_ref.so with `make -C oracle` when it is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libpoa_ref.so")
+
+
+class Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("match", "mismatch", "gap_open1", "gap_ext1", "gap_open2", "gap_ext2", "band_b")] + \
+               [("band_f", ctypes.c_float)] + \
+               [(n, ctypes.c_int32) for n in ("seeding", "k", "w", "min_w")]
+
+    @classmethod
+    def defaults(cls) -> "Params":
+        return cls(5, 4, 4, 2, 24, 1, 10, 0.01, 0, 19, 10, 500)
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = ctypes.CDLL(LIB)
+        P = ctypes.c_void_p
+        lib.poa_ref_batch.argtypes = [P, P, P, P, ctypes.c_int64, P, P, ctypes.c_int64, P, P]
+        lib.poa_ref_batch.restype = ctypes.c_int
+        _lib = lib
+    return _lib
+
+
+def consensus_batch(groups: Sequence[Sequence[str]], params: Params | None = None,
+                    return_cells: bool = False):
+    lib = load()
+    p = params or Params.defaults()
+    parts, lens, grp = [], [], [0]
+    for g in groups:
+        for s in g:
+            b = s.encode() if isinstance(s, str) else bytes(s)
+            parts.append(b)
+            lens.append(len(b))
+        grp.append(len(lens))
+    seqs = np.frombuffer(b"".join(parts) or b"\0", dtype=np.uint8)
+    seq_off = np.zeros(len(lens) + 1, dtype=np.int64)
+    if lens:
+        np.cumsum(lens, out=seq_off[1:])
+    grp_off = np.asarray(grp, dtype=np.int64)
+    n = len(groups)
+    cap = int(seq_off[-1]) * 2 + 1024
+    out = np.zeros(cap, dtype=np.uint8)
+    cons_off = np.zeros(n + 1, dtype=np.int64)
+    cells = np.zeros(max(n, 1), dtype=np.int64)
+    rc = lib.poa_ref_batch(ctypes.addressof(p), seqs.ctypes.data, seq_off.ctypes.data,
+                           grp_off.ctypes.data, n, None, out.ctypes.data, cap,
+                           cons_off.ctypes.data, cells.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"poa_ref_batch failed: {rc}")
+    raw = out.tobytes()
+    cons = [raw[cons_off[i]:cons_off[i + 1]].decode() for i in range(n)]
+    return (cons, cells[:n].copy()) if return_cells else cons

@@ -1,0 +1,61 @@
+"""HIP POA kernel == CPU restatement (oracle/poa_ref.c), byte for byte, plus identical DP cell counts.
+
+Runs through the C-ABI (libmando mando_poa_batch).  Exact equality is the bar: consensus bytes are
+integer/index work."""
+import numpy as np
+import pytest
+
+from mandalorion_amd import poa, synth
+from oracle import poa as opoa
+from tests import poa_cases
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(groups):
+    got, gcells = poa.poa_consensus_batch(groups, return_cells=True)
+    want, wcells = opoa.consensus_batch(groups, return_cells=True)
+    bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert not bad, f"{len(bad)} groups differ, first {bad[:5]}"
+    assert np.array_equal(gcells, wcells)
+    return got
+
+
+def test_wave_primitives_selftest(gpu_ctx):
+    assert gpu_ctx.selftest() == 0
+
+
+def test_edge_cases_match_oracle():
+    _check(poa_cases.edge_groups())
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_small_noisy_groups_match_oracle(seed):
+    _check(poa_cases.noisy_groups(40, (50, 700), (2, 25), seed=seed)[1])
+
+
+def test_r2c2_3kb_groups_match_oracle():
+    _check(poa_cases.noisy_groups(24, (2000, 4000), (10, 30), seed=77)[1])
+
+
+def test_pacbio_like_and_noisy_mix():
+    _, a = synth.read_groups(8, (1000, 2500), (5, 15), seed=4, model=synth.PACBIO)
+    _, b = synth.read_groups(8, (500, 1500), (5, 15), seed=5, model=dict(sub=0.04, ins=0.03, dele=0.03))
+    _check(a + b)
+
+
+def test_many_groups_one_launch_is_order_independent():
+    _, groups = poa_cases.noisy_groups(300, (100, 400), (3, 8), seed=123)
+    full = poa.poa_consensus_batch(groups)
+    part = poa.poa_consensus_batch(groups[::-1])[::-1]
+    assert full == part
+    want = opoa.consensus_batch(groups)
+    assert full == want
+
+
+def test_wide_band_and_far_predecessors():
+    rng = np.random.default_rng(8)
+    t = synth.random_template(rng, 1500).tobytes().decode()
+    ins = synth.random_template(rng, 300).tobytes().decode()
+    groups = [[t, t[:700] + ins + t[700:], t, t[:400] + t[700:], t[:700] + ins + t[700:], t]]
+    _check(groups)
