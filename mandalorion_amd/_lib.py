@@ -87,7 +87,7 @@ def load(path: str | None = None):
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = path or LIB_PATH
+        p = path or os.environ.get("MANDO_LIB") or LIB_PATH
         if not os.path.exists(p):
             raise MandoError(-7, f"{p} not built (run __graft_entry__.build() or make -C mandalorion_amd/csrc)")
         lib = ctypes.CDLL(p)

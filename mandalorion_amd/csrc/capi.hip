@@ -78,11 +78,11 @@ struct mando_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_launches = 0;
     bool timed = false;
-    DevBuf ws, counter;
+    DevBuf ws, counter, prof;
     DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
     DevBuf o_hits, o_strand;
     ~mando_ctx() {
-        for (DevBuf *b : {&ws, &counter, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
+        for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
                           &cons_len, &cells, &status, &o_hits, &o_strand})
             b->release();
         if (ev0) (void)hipEventDestroy(ev0);
@@ -158,10 +158,33 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.ws = ctx->ws.as<char>();
     a.counter = ctx->counter.as<int32_t>();
     HIP_TRY(hipMemsetAsync(a.counter, 0, sizeof(int32_t), ctx->stream));
+    const char *pe = getenv("MANDO_PROF");
+    const bool prof = pe && pe[0] == '1';
+    if (prof) {
+        rc = ctx->prof.ensure((size_t)slots * mando::kProfPhases * 8);
+        if (rc) return rc;
+        HIP_TRY(hipMemsetAsync(ctx->prof.p, 0, (size_t)slots * mando::kProfPhases * 8, ctx->stream));
+        a.prof = ctx->prof.as<int64_t>();
+    }
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
     HIP_TRY(mando::launch_poa(a, (int)slots, ctx->stream));
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->timed = true;
+    if (prof) {
+        std::vector<int64_t> h((size_t)slots * mando::kProfPhases);
+        HIP_TRY(hipMemcpyAsync(h.data(), ctx->prof.p, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        double tot[mando::kProfPhases] = {0};
+        for (int64_t s = 0; s < slots; ++s)
+            for (int k = 0; k < mando::kProfPhases; ++k) tot[k] += (double)h[(size_t)(s * mando::kProfPhases + k)];
+        const double reads = std::max(1.0, tot[6]), rows = std::max(1.0, tot[5]);
+        fprintf(stderr, "[mando prof] slots=%lld reads=%.0f rows/read=%.0f | cycles per read: desc %.0f dp %.0f (%.1f/row) backtrack %.0f update %.0f | consensus/slot %.0f\n",
+                (long long)slots, reads, rows / reads, tot[0] / reads, tot[1] / reads, tot[1] / rows,
+                tot[2] / reads, tot[3] / reads, tot[4] / (double)slots);
+        if (tot[8] + tot[9] + tot[10] + tot[11] > 0)
+            fprintf(stderr, "[mando prof] per DP row: band %.0f  pre-loop %.0f  compute %.0f  store+argmax %.0f\n",
+                    tot[8] / rows, tot[9] / rows, tot[10] / rows, tot[11] / rows);
+    }
     return MANDO_OK;
 }
 

@@ -9,7 +9,7 @@ namespace mando {
 constexpr int kWave = 64;
 constexpr int kCPL = 2;                  // DP cells per lane per chunk
 constexpr int kChunk = kWave * kCPL;     // 128 band columns per chunk
-constexpr int kRing = 8;                 // rows of H/E1/E2 kept in LDS
+constexpr int kRing = 4;                 // rows of H/E1/E2 kept in LDS
 constexpr int kRowRing = 64;             // rows of band info kept in LDS
 constexpr int kPreInline = 5;            // predecessor rows stored inline in a row descriptor
 constexpr int kDescInts = 8;             // ints per row descriptor
@@ -26,6 +26,10 @@ constexpr int kTbE1Open = 1 << 3;        // E1out[i][j] came from H[i][j]-oe1 (o
 constexpr int kTbE2Open = 1 << 4;
 constexpr int kTbF1OpenNext = 1 << 5;    // F1[i][j+1] opens from H0[i][j]
 constexpr int kTbF2OpenNext = 1 << 6;
+
+// phases timed when PoaKArgs::prof is set (MANDO_PROF=1)
+constexpr int kProfPhases = 16;  // 0 desc, 1 dp, 2 backtrack, 3 update, 4 consensus, 5 rows, 6 reads,
+                                 // 8.. in-row segments (MANDO_STAMPS builds only)
 
 // per-group status codes written by the kernel (match include/mando.h)
 constexpr int kStOk = 0, kStCap = -4, kStInternal = -6, kStUnsupported = -5;
@@ -100,6 +104,7 @@ struct PoaKArgs {
     int64_t *cells;
     int32_t *status;
     int32_t *counter;        // work-queue head (zeroed before launch)
+    int64_t *prof;           // optional per-slot phase cycle counters (kProfPhases per slot) or null
     char *ws;
     int64_t slot_bytes;
     PoaCaps caps;

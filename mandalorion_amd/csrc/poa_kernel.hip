@@ -25,12 +25,19 @@
 
 namespace mando {
 
+// Workspace pointers carry the global address space explicitly: they are re-read from LDS per
+// phase, and a generic pointer would make every access a flat_* op, which also counts on lgkmcnt and
+// so would stall every LDS wait behind this wave's outstanding traceback stores.
+#define GLB __attribute__((address_space(1)))
+typedef GLB int gint;
+typedef GLB uint8_t gu8;
+
 struct Slot {
-    uint8_t *base;
-    int *gid, *gtab, *in_n, *out_n, *in_id, *out_id, *out_w, *sink_in, *src_out, *src_out_w;
-    int *order, *order2, *pos, *remrow, *desc, *rinfo;
-    uint8_t *tb, *kp;
-    int *sv, *qnode, *qtgt, *qflag, *qnb, *qoff, *qmslot, *ins, *insmm, *score, *nxt;
+    gu8 *base;
+    gint *gid, *gtab, *in_n, *out_n, *in_id, *out_id, *out_w, *sink_in, *src_out, *src_out_w;
+    gint *order, *order2, *pos, *remrow, *desc, *rinfo;
+    gu8 *tb, *kp;
+    gint *sv, *qnode, *qtgt, *qflag, *qnb, *qoff, *qmslot, *ins, *insmm, *score, *nxt;
 };
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
@@ -65,6 +72,36 @@ __device__ __forceinline__ int wave_max(int v) {
     return v;
 }
 
+// DPP forms (gfx9 DPP: row_shr:1/2/4/8, row_bcast:15/31, wave_shr:1) — VALU-latency wave scans
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int dpp_mov(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, BM, false);
+}
+
+// inclusive prefix max over the wave; lanes see `ident` from outside the wave
+__device__ __forceinline__ int dpp_incl_max(int v, int ident) {
+    v = max(v, dpp_mov<0x111, 0xf, 0xf>(ident, v));
+    v = max(v, dpp_mov<0x112, 0xf, 0xf>(ident, v));
+    v = max(v, dpp_mov<0x114, 0xf, 0xf>(ident, v));
+    v = max(v, dpp_mov<0x118, 0xf, 0xf>(ident, v));
+    v = max(v, dpp_mov<0x142, 0xa, 0xf>(ident, v));
+    v = max(v, dpp_mov<0x143, 0xc, 0xf>(ident, v));
+    return v;
+}
+
+__device__ __forceinline__ int dpp_incl_sum(int v) {
+    v += dpp_mov<0x111, 0xf, 0xf>(0, v);
+    v += dpp_mov<0x112, 0xf, 0xf>(0, v);
+    v += dpp_mov<0x114, 0xf, 0xf>(0, v);
+    v += dpp_mov<0x118, 0xf, 0xf>(0, v);
+    v += dpp_mov<0x142, 0xa, 0xf>(0, v);
+    v += dpp_mov<0x143, 0xc, 0xf>(0, v);
+    return v;
+}
+
+// lane l receives lane l-1's value; lane 0 receives `fill`
+__device__ __forceinline__ int dpp_shr1(int v, int fill) { return dpp_mov<0x138, 0xf, 0xf>(fill, v); }
+
 __device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
     return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
 }
@@ -73,16 +110,16 @@ __device__ __forceinline__ int score_of(int a, int b, int match, int mismatch) {
     return (a == 4 || b == 4) ? 0 : (a == b ? match : -mismatch);
 }
 
-__device__ __forceinline__ int *in_list(const Slot &s, const PoaKArgs &a, int v) {
+__device__ __forceinline__ gint *in_list(const Slot &s, const PoaKArgs &a, int v) {
     return v == kSink ? s.sink_in : s.in_id + (int64_t)v * a.caps.DCAP;
 }
 __device__ __forceinline__ int in_cap(const PoaKArgs &a, int v) {
     return v == kSink ? a.caps.BIGCAP : a.caps.DCAP;
 }
-__device__ __forceinline__ int *out_list(const Slot &s, const PoaKArgs &a, int v) {
+__device__ __forceinline__ gint *out_list(const Slot &s, const PoaKArgs &a, int v) {
     return v == kSrc ? s.src_out : s.out_id + (int64_t)v * a.caps.DCAP;
 }
-__device__ __forceinline__ int *out_wlist(const Slot &s, const PoaKArgs &a, int v) {
+__device__ __forceinline__ gint *out_wlist(const Slot &s, const PoaKArgs &a, int v) {
     return v == kSrc ? s.src_out_w : s.out_w + (int64_t)v * a.caps.DCAP;
 }
 __device__ __forceinline__ int out_cap(const PoaKArgs &a, int v) {
@@ -92,19 +129,106 @@ __device__ __forceinline__ int out_cap(const PoaKArgs &a, int v) {
 // wave-level barrier that also orders this wave's global/LDS memory traffic
 __device__ __forceinline__ void wave_sync() { __syncthreads(); }
 
+// same-wave RAW through HBM (spilled rows, far row records): drain this wave's stores first
+__device__ __forceinline__ void hbm_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
 struct RowRec {
     int beg, end, am, soff;
 };
 
+constexpr int kQLds = 8192;      // reads up to this length are staged in LDS (4-bit bases)
+constexpr int kStage = 2 * kChunk;  // staging slot width (a 130-column window never aliases)
+
 struct SharedState {
-    int ring[kRing][3][kChunk];
-    int4 rrow[kRowRing];
+    int ring[kRing][3][kChunk];  // H, E1out, E2out of the last kRing narrow rows, col & 127
+    int stage[3][kStage];        // one predecessor window copied from HBM, col & 255
+    int4 rrow[kRowRing];         // beg, end, argmax, spill offset of the last kRowRing rows
+    int desc[kWave][kDescInts];  // descriptors of the current 64-row batch
+    int4 prec[kWave];            // rare-case predecessor records {row, beg, end, argmax}
+    int psoff[kWave];            // ... and their spill offsets
+    uint8_t qnib[kQLds / 2];     // read bases, two 4-bit codes per byte
+    Slot slot;                   // this wave's workspace arrays (read per phase, see slot_of)
+    PoaKArgs args;               // kernel arguments (read per phase, see args_of)
 };
+
+// Each phase re-reads the few workspace pointers it needs from LDS behind a compiler barrier, so
+// the ~30 loop-invariant 64-bit pointers are not kept live (and spilled) across the whole
+// persistent loop; unused fields of the copy are dead and never loaded.
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+    const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffff));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <class T>
+__device__ __forceinline__ T *uniptr(T *p) {
+    return (T *)(uintptr_t)uni64((int64_t)(uintptr_t)p);
+}
+
+// LDS-loaded values are divergent as far as the compiler knows: readfirstlane every field so
+// pointer arithmetic, capacity checks and loop bounds stay on the scalar unit.
+__device__ __forceinline__ Slot slot_of(SharedState &sh) {
+    asm volatile("" ::: "memory");
+    Slot s = sh.slot;
+    s.base = uniptr(s.base);
+    s.gid = uniptr(s.gid);
+    s.gtab = uniptr(s.gtab);
+    s.in_n = uniptr(s.in_n);
+    s.out_n = uniptr(s.out_n);
+    s.in_id = uniptr(s.in_id);
+    s.out_id = uniptr(s.out_id);
+    s.out_w = uniptr(s.out_w);
+    s.sink_in = uniptr(s.sink_in);
+    s.src_out = uniptr(s.src_out);
+    s.src_out_w = uniptr(s.src_out_w);
+    s.order = uniptr(s.order);
+    s.order2 = uniptr(s.order2);
+    s.pos = uniptr(s.pos);
+    s.remrow = uniptr(s.remrow);
+    s.desc = uniptr(s.desc);
+    s.rinfo = uniptr(s.rinfo);
+    s.tb = uniptr(s.tb);
+    s.kp = uniptr(s.kp);
+    s.sv = uniptr(s.sv);
+    s.qnode = uniptr(s.qnode);
+    s.qtgt = uniptr(s.qtgt);
+    s.qflag = uniptr(s.qflag);
+    s.qnb = uniptr(s.qnb);
+    s.qoff = uniptr(s.qoff);
+    s.qmslot = uniptr(s.qmslot);
+    s.ins = uniptr(s.ins);
+    s.insmm = uniptr(s.insmm);
+    s.score = uniptr(s.score);
+    s.nxt = uniptr(s.nxt);
+    return s;
+}
+__device__ __forceinline__ PoaKArgs args_of(SharedState &sh) {
+    asm volatile("" ::: "memory");
+    PoaKArgs a = sh.args;
+    a.caps.NC = bcast0(a.caps.NC);
+    a.caps.DCAP = bcast0(a.caps.DCAP);
+    a.caps.BIGCAP = bcast0(a.caps.BIGCAP);
+    a.caps.QC = bcast0(a.caps.QC);
+    a.caps.TBC = uni64(a.caps.TBC);
+    a.caps.KPC = uni64(a.caps.KPC);
+    a.caps.SVC = uni64(a.caps.SVC);
+    a.match = bcast0(a.match);
+    a.mismatch = bcast0(a.mismatch);
+    a.o1 = bcast0(a.o1);
+    a.e1 = bcast0(a.e1);
+    a.o2 = bcast0(a.o2);
+    a.e2 = bcast0(a.e2);
+    a.band_b = bcast0(a.band_b);
+    a.band_f = __int_as_float(bcast0(__float_as_int(a.band_f)));
+    a.prof = uniptr(a.prof);
+    return a;
+}
 
 // ---------------------------------------------------------------------------------------------
 // first read: a chain SRC -> n0 -> ... -> n(L-1) -> SINK
 // ---------------------------------------------------------------------------------------------
-__device__ int init_chain(const PoaKArgs &a, Slot &s, const uint8_t *q, int L, int lane, int &n) {
+__device__ int init_chain(SharedState &sh, const uint8_t *q, int L, int lane, int &n) {
+    const PoaKArgs a = args_of(sh);
+    Slot s = slot_of(sh);
     if (L + 2 > a.caps.NC) return kStCap;
     for (int t = lane; t < L; t += kWave) {
         int v = 2 + t;
@@ -147,7 +271,9 @@ __device__ int init_chain(const PoaKArgs &a, Slot &s, const uint8_t *q, int L, i
 // row descriptors + remain (heaviest out-edge path length to the sink), 64-row chunks from the end
 // desc[r] = {node, base | far<<8 | pre_n<<16, remain, pre_row[0..4]}
 // ---------------------------------------------------------------------------------------------
-__device__ void build_desc(const PoaKArgs &a, Slot &s, int n, int lane) {
+__device__ void build_desc(SharedState &sh, int n, int lane) {
+    const PoaKArgs a = args_of(sh);
+    Slot s = slot_of(sh);
     const int nch = (n + kWave - 1) / kWave;
     int prev_val = 0;
     for (int c = nch - 1; c >= 0; --c) {
@@ -161,13 +287,13 @@ __device__ void build_desc(const PoaKArgs &a, Slot &s, int n, int lane) {
             v = s.order[r];
             vb = s.base[v];
             pn = s.in_n[v];
-            const int *il = in_list(s, a, v);
+            const gint *il = in_list(s, a, v);
 #pragma unroll
             for (int k = 0; k < kPreInline; ++k)
                 if (k < pn) pre[k] = s.pos[il[k]];
             const int on = s.out_n[v];
-            const int *ol = out_list(s, a, v);
-            const int *ow = out_wlist(s, a, v);
+            const gint *ol = out_list(s, a, v);
+            const gint *ow = out_wlist(s, a, v);
             int bw = -2147483647 - 1, maxd = 0;
             for (int k = 0; k < on; ++k) {
                 int po = s.pos[ol[k]];
@@ -208,7 +334,7 @@ __device__ void build_desc(const PoaKArgs &a, Slot &s, int n, int lane) {
         }
         if (valid) {
             s.remrow[r] = val;
-            int *d = s.desc + (int64_t)r * kDescInts;
+            gint *d = s.desc + (int64_t)r * kDescInts;
             d[0] = v;
             d[1] = vb | (far << 8) | (pn << 16);
             d[2] = val;
@@ -226,266 +352,410 @@ __device__ __forceinline__ int pre_row_slow(const PoaKArgs &a, const Slot &s, in
 }
 
 __device__ __forceinline__ RowRec load_rowrec(const SharedState &sh, const Slot &s, int r, int p) {
-    RowRec rr;
+    int4 x;
     if (r - p < kRowRing) {
-        int4 x = sh.rrow[p % kRowRing];
-        rr.beg = x.x;
-        rr.end = x.y;
-        rr.am = x.z;
-        rr.soff = x.w;
+        x = sh.rrow[p % kRowRing];
     } else {
-        const int *ri = s.rinfo + (int64_t)p * kRowInfoInts;
-        rr.beg = ri[0];
-        rr.end = ri[1];
-        rr.am = ri[2];
-        rr.soff = ri[3];
+        // rare: record of a row more than kRowRing rows back (written by this wave long ago);
+        // consumed (readfirstlane) inside the branch so the common path never waits on vmcnt
+        hbm_fence();
+        const gint *g = s.rinfo + (int64_t)p * kRowInfoInts;
+        x = make_int4(bcast0(g[0]), bcast0(g[1]), bcast0(g[2]), bcast0(g[3]));
     }
+    RowRec rr;
+    rr.beg = x.x;
+    rr.end = x.y;
+    rr.am = x.z;
+    rr.soff = x.w;
     return rr;
 }
 
-// H (plane 0), E1out (1), E2out (2) of row p at column col, kNegInf outside its band
-__device__ __forceinline__ int row_val(const SharedState &sh, const Slot &s, int r, int p,
-                                       const RowRec &rr, int plane, int col) {
-    if (col < rr.beg || col > rr.end) return kNegInf;
-    const int width = rr.end - rr.beg + 1;
-    if (r - p < kRing && width <= kChunk) return sh.ring[p % kRing][plane][col & (kChunk - 1)];
-    return s.sv[(int64_t)rr.soff + (int64_t)plane * width + (col - rr.beg)];
+// A row's band is processed in 128-column chunks starting at the even column cb0 = beg & ~1.
+// "Narrow" rows (one chunk) keep H/E1/E2 in the LDS ring, indexed by absolute column & 127; rows
+// that are wider, or that have a successor >= kRing rows later, are (also) spilled to HBM as three
+// planes of nchunk*128 ints starting at column cb0.  A predecessor outside the ring is staged for
+// the current chunk into sh.stage (columns cb-1 .. cb+128, indexed & 255) before it is read, so the
+// arithmetic only ever reads LDS.
+__device__ __forceinline__ bool row_narrow(int beg, int end) { return end - (beg & ~1) < kChunk; }
+__device__ __forceinline__ int row_spill_width(int beg, int end) {
+    return ((end - (beg & ~1)) / kChunk + 1) * kChunk;
+}
+__device__ __forceinline__ bool pre_in_ring(int r, int p, const RowRec &pr) {
+    return (r - p < kRing) && row_narrow(pr.beg, pr.end);
+}
+
+// predecessor row k of the current row (descriptor `dl` in the LDS batch)
+__device__ __forceinline__ int pre_row_k(const PoaKArgs &a, const Slot &s, const int *dl, int node, int k) {
+    if (k >= kPreInline) {
+        hbm_fence();
+        return bcast0(s.pos[in_list(s, a, node)[k]]);
+    }
+    return dl[3 + k];
+}
+
+// copy row p's spilled H/E1/E2 for columns [cb-1, cb+128] into the staging slot
+__device__ __forceinline__ void stage_pre(SharedState &sh, const Slot &s, const RowRec &pr, int cb, int lane) {
+    hbm_fence();
+    const int cb0 = pr.beg & ~1;
+    const int wa = row_spill_width(pr.beg, pr.end);
+    const gint *sp = s.sv + pr.soff;
+    for (int t = lane; t < kChunk + 2; t += kWave) {
+        const int col = cb - 1 + t;
+        const int c = min(max(col - cb0, 0), wa - 1);
+        const int h = sp[c], x1 = sp[wa + c], x2 = sp[2 * wa + c];
+        const int ix = col & (kStage - 1);
+        sh.stage[0][ix] = h;
+        sh.stage[1][ix] = x1;
+        sh.stage[2][ix] = x2;
+    }
+}
+
+struct DpState {
+    int64_t tb_used, kp_used, sv_used, cells;
+    uint64_t seg[4];
+};
+
+#ifdef MANDO_STAMPS
+#define STAMP(var) uint64_t var; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+#else
+#define STAMP(var) const uint64_t var = 0
+#endif
+
+__device__ __forceinline__ int qbase(const SharedState &sh, int j) {
+    return (sh.qnib[j >> 1] >> ((j & 1) << 2)) & 0xf;
+}
+
+// Rare-case predecessor records (more than kPreInline predecessors, or a predecessor whose record
+// left the LDS row ring): gathered from HBM into sh.prec / sh.psoff.  The loads are consumed inside
+// this uniform branch, so the common path never carries an outstanding load into an s_waitcnt.
+__device__ __forceinline__ void pre_records_slow(const PoaKArgs &a, const Slot &s, SharedState &sh, int r,
+                                                 int node, int pn, const int *dl, int lane) {
+    hbm_fence();
+    for (int k = lane; k < pn; k += kWave) {
+        const int p = (k < kPreInline) ? dl[3 + k] : s.pos[in_list(s, a, node)[k]];
+        int4 x;
+        if (r - p < kRowRing) {
+            x = sh.rrow[p % kRowRing];
+        } else {
+            const gint *g = s.rinfo + (int64_t)p * kRowInfoInts;
+            x = make_int4(g[0], g[1], g[2], g[3]);
+        }
+        sh.prec[k] = make_int4(p, x.x, x.y, x.z);
+        sh.psoff[k] = x.w;
+    }
+}
+
+__device__ __forceinline__ bool in_band(int col, int b, int e) {
+    return (unsigned)(col - b) <= (unsigned)(e - b);
+}
+
+// One DP row r.  Predecessor k's record lives in lane k (pP row, pB/pE band, pA argmax, pS spill
+// offset); the common case (every predecessor in the LDS ring) reads values with 4 LDS ops per
+// predecessor and no global memory traffic except the traceback stores.
+__device__ __forceinline__ int dp_row(const PoaKArgs &a, Slot &s, SharedState &sh, int qlen, int w,
+                                      int r, int lane, DpState &ds) {
+    const int e1 = a.e1, e2 = a.e2, oe1 = a.o1 + a.e1, oe2 = a.o2 + a.e2;
+    const int IDENT = -(1 << 30);
+    STAMP(ts0);
+    const int *dl = &sh.desc[r & (kWave - 1)][0];
+    const int node = dl[0];
+    const int d1 = dl[1];
+    const int rem = dl[2];
+    const int vb = d1 & 0xff, far = (d1 >> 8) & 0xff, pn = d1 >> 16;
+    if (pn > kWave) return kStUnsupported;
+    // ---- predecessor records, lane-parallel
+    int pP = 0, pB = 0, pE = -1, pA = 0, pS = -1;
+    bool slow = pn > kPreInline;
+    if (!slow) {
+        if (lane < pn) pP = dl[3 + lane];
+        slow = __ballot(lane < pn && r - pP >= kRowRing) != 0;
+    }
+    if (slow) {
+        pre_records_slow(a, s, sh, r, node, pn, dl, lane);
+        if (lane < pn) {
+            const int4 x = sh.prec[lane];
+            pP = x.x;
+            pB = x.y;
+            pE = x.z;
+            pA = x.w;
+            pS = sh.psoff[lane];
+        }
+    } else if (lane < pn) {
+        const int4 x = sh.rrow[pP % kRowRing];
+        pB = x.x;
+        pE = x.y;
+        pA = x.z;
+        pS = x.w;
+    }
+    // ---- band
+    int beg, end;
+    if (r == 0) {
+        beg = 0;
+        end = min(qlen, max(0, qlen - rem) + w);
+    } else {
+        int posL = 2147483647, posR = -2147483647 - 1;
+        for (int k = 0; k < pn; ++k) {
+            const int am = readlane(pA, k) + 1;
+            posL = min(posL, am);
+            posR = max(posR, am);
+        }
+        const int x = qlen - rem;
+        beg = max(0, min(posL, x) - w);
+        end = min(qlen, max(posR, x) + w);
+    }
+    const bool pring = (r - pP < kRing) && row_narrow(pB, pE);
+    const bool all_ring = __ballot(lane < pn && !pring) == 0;
+    const int cb0 = beg & ~1;
+    const int span = end - cb0 + 1;
+    const int nchunk = (span + kChunk - 1) / kChunk;
+    const bool narrow = nchunk == 1;
+    const bool spill = far || !narrow;
+    const int wa = nchunk * kChunk;
+    const int tbw = (span + 3) & ~3;
+    const bool multi = pn > 1;
+    if (ds.tb_used + tbw > a.caps.TBC) return kStCap;
+    if (multi && ds.kp_used + 3 * tbw > a.caps.KPC) return kStCap;
+    if (spill && ds.sv_used + 3 * (int64_t)wa > a.caps.SVC) return kStCap;
+    // 32-bit offsets from the slot's arrays (the stores then use a scalar base + vector offset)
+    const int tbbase = (int)ds.tb_used - cb0;       // traceback byte of column j: tb[tbbase + j]
+    const int kpbase = (int)ds.kp_used - 3 * cb0;   // predecessor bytes of column j: kp[kpbase + 3j]
+    const int soff = spill ? (int)ds.sv_used : -1;
+    const int svbase = (int)ds.sv_used - cb0;       // plane pl, column j: sv[svbase + pl*wa + j]
+    ds.tb_used += tbw;
+    if (multi) ds.kp_used += 3 * tbw;
+    if (spill) ds.sv_used += 3 * (int64_t)wa;
+    ds.cells += end - beg + 1;
+    STAMP(ts1);
+    uint64_t ts2 = ts1, ts3 = ts1;
+
+    int best = -2147483647 - 1, besti = beg;
+    int carry1 = kNegInf + oe1 + e1 * (beg - 1);
+    int carry2 = kNegInf + oe2 + e2 * (beg - 1);
+    int *ringrow = &sh.ring[r % kRing][0][0];
+
+    for (int c = 0; c < nchunk; ++c) {
+        const int cb = cb0 + c * kChunk;
+        const int j0 = cb + 2 * lane, j1 = j0 + 1;
+        const bool va = j0 >= beg && j0 <= end, vbb = j1 <= end;
+        int Ha, Hb, E1a, E1b, E2a, E2b;
+        int tpair = 0;
+        if (r == 0) {
+            // source row: H[0][0] = 0, H[0][j] = max(-(o1+e1 j), -(o2+e2 j))
+            Ha = (j0 == 0) ? 0 : max(-(a.o1 + e1 * j0), -(a.o2 + e2 * j0));
+            Hb = max(-(a.o1 + e1 * j1), -(a.o2 + e2 * j1));
+            E1a = Ha - oe1;
+            E1b = Hb - oe1;
+            E2a = Ha - oe2;
+            E2b = Hb - oe2;
+        } else {
+            const int qa = (j0 >= 1 && j0 <= qlen) ? qbase(sh, j0 - 1) : 4;
+            const int qb = (j0 < qlen) ? qbase(sh, j0) : 4;
+            int Mva, Mvb, X1a, X1b, X2a, X2b;
+            int mka = 0, mkb = 0, k1a = 0, k1b = 0, k2a = 0, k2b = 0;
+            const int ia = (j0 - 1) & (kChunk - 1), ib = j0 & (kChunk - 1);
+            if (all_ring && pn == 1) {
+                // the common row: one predecessor, in the ring
+                const int p0 = readlane(pP, 0), b0 = readlane(pB, 0), e0 = readlane(pE, 0);
+                const int *rp = &sh.ring[p0 % kRing][0][0];
+                const int hA = rp[ia], hB = rp[ib];
+                const int2 x1 = *reinterpret_cast<const int2 *>(rp + kChunk + ib);
+                const int2 x2 = *reinterpret_cast<const int2 *>(rp + 2 * kChunk + ib);
+                const bool inA = in_band(j0 - 1, b0, e0), inB = in_band(j0, b0, e0),
+                           inC = in_band(j1, b0, e0);
+                Mva = inA ? hA : kNegInf;
+                Mvb = inB ? hB : kNegInf;
+                X1a = inB ? x1.x : kNegInf;
+                X2a = inB ? x2.x : kNegInf;
+                X1b = inC ? x1.y : kNegInf;
+                X2b = inC ? x2.y : kNegInf;
+            } else {
+                Mva = Mvb = X1a = X1b = X2a = X2b = kNegInf;
+#pragma unroll 1
+                for (int k = 0; k < pn; ++k) {
+                    const int pk = readlane(pP, k), bk = readlane(pB, k), ek = readlane(pE, k);
+                    const int *rp;
+                    int mask;
+                    if (all_ring || (r - pk < kRing && row_narrow(bk, ek))) {
+                        rp = &sh.ring[pk % kRing][0][0];
+                        mask = kChunk - 1;
+                    } else {
+                        RowRec pr;
+                        pr.beg = bk;
+                        pr.end = ek;
+                        pr.am = 0;
+                        pr.soff = readlane(pS, k);
+                        stage_pre(sh, s, pr, cb, lane);
+                        rp = &sh.stage[0][0];
+                        mask = kStage - 1;
+                    }
+                    const int pl = mask + 1;  // plane stride
+                    const int hA = rp[(j0 - 1) & mask], hB = rp[j0 & mask];
+                    const int2 x1 = *reinterpret_cast<const int2 *>(rp + pl + (j0 & mask));
+                    const int2 x2 = *reinterpret_cast<const int2 *>(rp + 2 * pl + (j0 & mask));
+                    const bool inA = in_band(j0 - 1, bk, ek), inB = in_band(j0, bk, ek),
+                               inC = in_band(j1, bk, ek);
+                    const int vA = inA ? hA : kNegInf, vB = inB ? hB : kNegInf;
+                    const int v1a = inB ? x1.x : kNegInf, v2a = inB ? x2.x : kNegInf;
+                    const int v1b = inC ? x1.y : kNegInf, v2b = inC ? x2.y : kNegInf;
+                    if (vA > Mva) { Mva = vA; mka = k; }
+                    if (vB > Mvb) { Mvb = vB; mkb = k; }
+                    if (v1a > X1a) { X1a = v1a; k1a = k; }
+                    if (v1b > X1b) { X1b = v1b; k1b = k; }
+                    if (v2a > X2a) { X2a = v2a; k2a = k; }
+                    if (v2b > X2b) { X2b = v2b; k2b = k; }
+                }
+            }
+            {
+                STAMP(tx);
+                ts2 = tx;
+            }
+            const int Ma = Mva + score_of(vb, qa, a.match, a.mismatch);
+            const int Mb = Mvb + score_of(vb, qb, a.match, a.mismatch);
+            const int H0a = max(Ma, max(X1a, X2a));
+            const int H0b = max(Mb, max(X1b, X2b));
+            // horizontal gaps: F[j] = max(C, max_{k<j} H0[k] + e*k) - oe - e*(j-1)
+            const int G1a = va ? H0a + e1 * j0 : IDENT;
+            const int G1b = vbb ? H0b + e1 * j1 : IDENT;
+            const int G2a = va ? H0a + e2 * j0 : IDENT;
+            const int G2b = vbb ? H0b + e2 * j1 : IDENT;
+            const int inc1 = dpp_incl_max(max(G1a, G1b), IDENT);
+            const int inc2 = dpp_incl_max(max(G2a, G2b), IDENT);
+            const int ex1 = dpp_shr1(inc1, IDENT);
+            const int ex2 = dpp_shr1(inc2, IDENT);
+            const int P1a = max(ex1, carry1), P1b = max(P1a, G1a);
+            const int P2a = max(ex2, carry2), P2b = max(P2a, G2a);
+            if (nchunk > 1) {
+                carry1 = max(carry1, readlane(inc1, kWave - 1));
+                carry2 = max(carry2, readlane(inc2, kWave - 1));
+            }
+            const int F1a = P1a - oe1 - e1 * (j0 - 1), F1b = P1b - oe1 - e1 * (j1 - 1);
+            const int F2a = P2a - oe2 - e2 * (j0 - 1), F2b = P2b - oe2 - e2 * (j1 - 1);
+            Ha = max(H0a, max(F1a, F2a));
+            Hb = max(H0b, max(F1b, F2b));
+            auto src_type = [&](int H, int M, int X1, int X2, int F1, int k1, int k2) -> int {
+                if (M == H) return 0;
+                const bool t1 = X1 == H, t2 = X2 == H;
+                if (t1 && t2) return (k1 <= k2) ? 1 : 2;
+                if (t1) return 1;
+                if (t2) return 2;
+                return (F1 == H) ? 3 : 4;
+            };
+            const int tya = src_type(Ha, Ma, X1a, X2a, F1a, k1a, k2a);
+            const int tyb = src_type(Hb, Mb, X1b, X2b, F1b, k1b, k2b);
+            E1a = max(X1a - e1, Ha - oe1);
+            E1b = max(X1b - e1, Hb - oe1);
+            E2a = max(X2a - e2, Ha - oe2);
+            E2b = max(X2b - e2, Hb - oe2);
+            const int ta = tya | ((Ha - oe1 >= X1a - e1) ? kTbE1Open : 0) |
+                           ((Ha - oe2 >= X2a - e2) ? kTbE2Open : 0) |
+                           ((G1a >= P1a) ? kTbF1OpenNext : 0) | ((G2a >= P2a) ? kTbF2OpenNext : 0);
+            const int tb2 = tyb | ((Hb - oe1 >= X1b - e1) ? kTbE1Open : 0) |
+                            ((Hb - oe2 >= X2b - e2) ? kTbE2Open : 0) |
+                            ((G1b >= P1b) ? kTbF1OpenNext : 0) | ((G2b >= P2b) ? kTbF2OpenNext : 0);
+            tpair = ta | (tb2 << 8);
+            if ((va || vbb) && multi) {
+                GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + 3 * j0));
+                kq[0] = (uint16_t)(mka | (k1a << 8));
+                kq[1] = (uint16_t)(k2a | (mkb << 8));
+                kq[2] = (uint16_t)(k1b | (k2b << 8));
+            }
+            {
+                STAMP(tx);
+                ts3 = tx;
+            }
+        }
+        if (va || vbb) *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)tpair;
+        if (narrow) {
+            const int ibk = j0 & (kChunk - 1);
+            *reinterpret_cast<int2 *>(ringrow + ibk) = make_int2(Ha, Hb);
+            *reinterpret_cast<int2 *>(ringrow + kChunk + ibk) = make_int2(E1a, E1b);
+            *reinterpret_cast<int2 *>(ringrow + 2 * kChunk + ibk) = make_int2(E2a, E2b);
+        }
+        if (spill) {
+            gint *sv = s.sv + svbase;
+            sv[j0] = Ha;
+            sv[j1] = Hb;
+            sv[wa + j0] = E1a;
+            sv[wa + j1] = E1b;
+            sv[2 * wa + j0] = E2a;
+            sv[2 * wa + j1] = E2b;
+        }
+        // leftmost argmax of H in one max-reduction: value (clamped; real values are far inside
+        // +-2^23, out-of-band garbage never wins) in the high bits, 127 - column-in-chunk below
+        const int ca = va ? (min(max(Ha, -(1 << 23)), (1 << 23)) << 7) | (127 - 2 * lane)
+                          : (-2147483647 - 1);
+        const int cbk = vbb ? (min(max(Hb, -(1 << 23)), (1 << 23)) << 7) | (126 - 2 * lane)
+                            : (-2147483647 - 1);
+        const int mp = readlane(dpp_incl_max(max(ca, cbk), -2147483647 - 1), kWave - 1);
+        const int m = mp >> 7;
+        if (m > best) {
+            best = m;
+            besti = cb + 127 - (mp & 127);
+        }
+    }
+    {
+        STAMP(ts4);
+        ds.seg[0] += ts1 - ts0;
+        ds.seg[1] += ts2 - ts1;
+        ds.seg[2] += ts3 - ts2;
+        ds.seg[3] += ts4 - ts3;
+    }
+    if (lane == 0) {
+        sh.rrow[r % kRowRing] = make_int4(beg, end, besti, soff);
+        gint *ri = s.rinfo + (int64_t)r * kRowInfoInts;
+        ri[0] = beg;
+        ri[1] = end;
+        ri[2] = besti;
+        ri[3] = soff;
+        ri[4] = tbbase;
+        ri[5] = kpbase;
+        ri[6] = node;
+        ri[7] = pn;
+    }
+    return kStOk;
 }
 
 // ---------------------------------------------------------------------------------------------
-// banded DP over all rows of the current graph for read q (qlen) — writes traceback bytes and
-// returns the start row of the backtrack in *bi (or -1)
+// banded DP over all rows of the current graph for read q (qlen): writes the traceback bytes and
+// returns the start row of the backtrack in bi_out (or -1)
 // ---------------------------------------------------------------------------------------------
-__device__ int run_dp(const PoaKArgs &a, Slot &s, SharedState &sh, const uint8_t *q, int qlen,
+__device__ int run_dp(SharedState &sh, const uint8_t *q, int qlen,
                       int n, int lane, int64_t &cells, int &bi_out) {
+    const PoaKArgs a = args_of(sh);
+    Slot s = slot_of(sh);
+    if (qlen > kQLds) return kStUnsupported;
     const int w = a.band_b + (int)(a.band_f * (float)qlen);
-    const int e1 = a.e1, e2 = a.e2, oe1 = a.o1 + a.e1, oe2 = a.o2 + a.e2;
-    const int IDENT = -(1 << 30);
-    int64_t tb_used = 0, kp_used = 0, sv_used = 0;
-    int dreg[kDescInts];
+    DpState ds{0, 0, 0, 0, {0, 0, 0, 0}};
+    // stage the read in LDS (4-bit codes): on gfx9 vmcnt orders loads behind every earlier store,
+    // so a global load per row would wait for the previous rows' traceback stores to land
+    for (int t = 2 * lane; t < qlen; t += 2 * kWave) {
+        const int lo = q[t], hi = (t + 1 < qlen) ? q[t + 1] : 4;
+        sh.qnib[t >> 1] = (uint8_t)(lo | (hi << 4));
+    }
     for (int r = 0; r < n - 1; ++r) {
         if ((r & (kWave - 1)) == 0) {
+            // next 64 descriptors -> LDS (one global round trip per 64 rows)
             const int rr0 = r + lane;
             if (rr0 < n) {
-                const int4 *dp4 = reinterpret_cast<const int4 *>(s.desc + (int64_t)rr0 * kDescInts);
-                int4 x = dp4[0], y = dp4[1];
-                dreg[0] = x.x; dreg[1] = x.y; dreg[2] = x.z; dreg[3] = x.w;
-                dreg[4] = y.x; dreg[5] = y.y; dreg[6] = y.z; dreg[7] = y.w;
-            }
-        }
-        const int rl = r & (kWave - 1);
-        const int node = readlane(dreg[0], rl);
-        const int d1 = readlane(dreg[1], rl);
-        const int rem = readlane(dreg[2], rl);
-        const int vb = d1 & 0xff;
-        const int far = (d1 >> 8) & 0xff;
-        const int pn = d1 >> 16;
-        int dpre[kPreInline];
+                const gint *dg = s.desc + (int64_t)rr0 * kDescInts;
+                int *dl = &sh.desc[lane][0];
 #pragma unroll
-        for (int k = 0; k < kPreInline; ++k) dpre[k] = readlane(dreg[3 + k], rl);
-
-        // --- band
-        int beg, end;
-        if (r == 0) {
-            beg = 0;
-            end = min(qlen, max(0, qlen - rem) + w);
-        } else {
-            int posL = 2147483647, posR = -2147483647 - 1;
-            for (int k = 0; k < pn; ++k) {
-                int p;
-                if (k < kPreInline) {
-                    p = dpre[0];
-#pragma unroll
-                    for (int kk = 1; kk < kPreInline; ++kk)
-                        if (k == kk) p = dpre[kk];
-                } else {
-                    p = bcast0(pre_row_slow(a, s, node, k));
-                }
-                RowRec pr = load_rowrec(sh, s, r, p);
-                posL = min(posL, pr.am + 1);
-                posR = max(posR, pr.am + 1);
-            }
-            const int x = qlen - rem;
-            beg = max(0, min(posL, x) - w);
-            end = min(qlen, max(posR, x) + w);
-        }
-        const int width = end - beg + 1;
-        const bool wide = width > kChunk;
-        const bool spill = far || wide;
-        const int64_t tbw = (width + 3) & ~3;
-        const bool multi = pn > 1;
-        if (tb_used + tbw > a.caps.TBC) return kStCap;
-        if (multi && kp_used + 3 * tbw > a.caps.KPC) return kStCap;
-        if (spill && sv_used + 3 * (int64_t)width > a.caps.SVC) return kStCap;
-        const int64_t tboff = tb_used, kpoff = multi ? kp_used : -1;
-        const int soff = spill ? (int)sv_used : -1;
-        tb_used += tbw;
-        if (multi) kp_used += 3 * tbw;
-        if (spill) sv_used += 3 * (int64_t)width;
-        cells += width;
-
-        int best = -2147483647 - 1, besti = beg;
-        int carry1 = kNegInf + oe1 + e1 * (beg - 1);
-        int carry2 = kNegInf + oe2 + e2 * (beg - 1);
-        int *ringrow = &sh.ring[r % kRing][0][0];
-
-        for (int cb = beg; cb <= end; cb += kChunk) {
-            const int j0 = cb + 2 * lane, j1 = j0 + 1;
-            const bool va = j0 <= end, vbb = j1 <= end;
-            int Ha, Hb, E1a, E1b, E2a, E2b;
-            uint8_t ta = 0, tbb = 0;
-            int mka = 0, mkb = 0, k1a = 0, k1b = 0, k2a = 0, k2b = 0;
-            if (r == 0) {
-                // source row: H[0][0] = 0, H[0][j] = max(-(o1+e1 j), -(o2+e2 j))
-                Ha = (j0 == 0) ? 0 : max(-(a.o1 + e1 * j0), -(a.o2 + e2 * j0));
-                Hb = max(-(a.o1 + e1 * j1), -(a.o2 + e2 * j1));
-                E1a = Ha - oe1;
-                E1b = Hb - oe1;
-                E2a = Ha - oe2;
-                E2b = Hb - oe2;
-            } else {
-                int Mva = kNegInf, Mvb = kNegInf, X1a = kNegInf, X1b = kNegInf, X2a = kNegInf,
-                    X2b = kNegInf;
-                for (int k = 0; k < pn; ++k) {
-                    int p;
-                    if (k < kPreInline) {
-                        p = dpre[0];
-#pragma unroll
-                        for (int kk = 1; kk < kPreInline; ++kk)
-                            if (k == kk) p = dpre[kk];
-                    } else {
-                        p = bcast0(pre_row_slow(a, s, node, k));
-                    }
-                    const RowRec pr = load_rowrec(sh, s, r, p);
-                    const int hA = row_val(sh, s, r, p, pr, 0, j0 - 1);
-                    const int hB = row_val(sh, s, r, p, pr, 0, j0);
-                    const int e1A = row_val(sh, s, r, p, pr, 1, j0);
-                    const int e1B = row_val(sh, s, r, p, pr, 1, j1);
-                    const int e2A = row_val(sh, s, r, p, pr, 2, j0);
-                    const int e2B = row_val(sh, s, r, p, pr, 2, j1);
-                    if (hA > Mva) { Mva = hA; mka = k; }
-                    if (hB > Mvb) { Mvb = hB; mkb = k; }
-                    if (e1A > X1a) { X1a = e1A; k1a = k; }
-                    if (e1B > X1b) { X1b = e1B; k1b = k; }
-                    if (e2A > X2a) { X2a = e2A; k2a = k; }
-                    if (e2B > X2b) { X2b = e2B; k2b = k; }
-                }
-                const int qa = (j0 >= 1 && j0 <= qlen) ? q[j0 - 1] : 4;
-                const int qb = (j0 >= 0 && j0 < qlen) ? q[j0] : 4;
-                const int Ma = Mva + score_of(vb, qa, a.match, a.mismatch);
-                const int Mb = Mvb + score_of(vb, qb, a.match, a.mismatch);
-                const int H0a = max(Ma, max(X1a, X2a));
-                const int H0b = max(Mb, max(X1b, X2b));
-                // horizontal gaps: F[j] = max(C, max_{k<j} H0[k] + e*k) - oe - e*(j-1)
-                const int G1a = va ? H0a + e1 * j0 : IDENT;
-                const int G1b = vbb ? H0b + e1 * j1 : IDENT;
-                const int G2a = va ? H0a + e2 * j0 : IDENT;
-                const int G2b = vbb ? H0b + e2 * j1 : IDENT;
-                const int inc1 = wave_incl_max(max(G1a, G1b), lane);
-                const int inc2 = wave_incl_max(max(G2a, G2b), lane);
-                int ex1 = __shfl_up(inc1, 1, kWave);
-                int ex2 = __shfl_up(inc2, 1, kWave);
-                if (lane == 0) { ex1 = IDENT; ex2 = IDENT; }
-                const int P1a = max(ex1, carry1), P1b = max(P1a, G1a);
-                const int P2a = max(ex2, carry2), P2b = max(P2a, G2a);
-                carry1 = max(carry1, readlane(inc1, kWave - 1));
-                carry2 = max(carry2, readlane(inc2, kWave - 1));
-                const int F1a = P1a - oe1 - e1 * (j0 - 1), F1b = P1b - oe1 - e1 * (j1 - 1);
-                const int F2a = P2a - oe2 - e2 * (j0 - 1), F2b = P2b - oe2 - e2 * (j1 - 1);
-                Ha = max(H0a, max(F1a, F2a));
-                Hb = max(H0b, max(F1b, F2b));
-                auto src_type = [&](int H, int M, int X1, int X2, int F1, int k1, int k2) -> int {
-                    if (M == H) return 0;
-                    const bool t1 = X1 == H, t2 = X2 == H;
-                    if (t1 && t2) return (k1 <= k2) ? 1 : 2;
-                    if (t1) return 1;
-                    if (t2) return 2;
-                    return (F1 == H) ? 3 : 4;
-                };
-                const int tya = src_type(Ha, Ma, X1a, X2a, F1a, k1a, k2a);
-                const int tyb = src_type(Hb, Mb, X1b, X2b, F1b, k1b, k2b);
-                E1a = max(X1a - e1, Ha - oe1);
-                E1b = max(X1b - e1, Hb - oe1);
-                E2a = max(X2a - e2, Ha - oe2);
-                E2b = max(X2b - e2, Hb - oe2);
-                ta = (uint8_t)(tya | ((Ha - oe1 >= X1a - e1) ? kTbE1Open : 0) |
-                               ((Ha - oe2 >= X2a - e2) ? kTbE2Open : 0) |
-                               ((G1a >= P1a) ? kTbF1OpenNext : 0) | ((G2a >= P2a) ? kTbF2OpenNext : 0));
-                tbb = (uint8_t)(tyb | ((Hb - oe1 >= X1b - e1) ? kTbE1Open : 0) |
-                                ((Hb - oe2 >= X2b - e2) ? kTbE2Open : 0) |
-                                ((G1b >= P1b) ? kTbF1OpenNext : 0) | ((G2b >= P2b) ? kTbF2OpenNext : 0));
-            }
-            // store traceback / predecessor indices / row values
-            if (va) {
-                const int64_t c0 = j0 - beg;
-                s.tb[tboff + c0] = ta;
-                if (multi) {
-                    uint8_t *kpp = s.kp + kpoff + 3 * c0;
-                    kpp[0] = (uint8_t)mka;
-                    kpp[1] = (uint8_t)k1a;
-                    kpp[2] = (uint8_t)k2a;
-                }
-                if (!wide) {
-                    ringrow[0 * kChunk + (j0 & (kChunk - 1))] = Ha;
-                    ringrow[1 * kChunk + (j0 & (kChunk - 1))] = E1a;
-                    ringrow[2 * kChunk + (j0 & (kChunk - 1))] = E2a;
-                }
-                if (spill) {
-                    int *svp = s.sv + soff;
-                    svp[c0] = Ha;
-                    svp[width + c0] = E1a;
-                    svp[2 * width + c0] = E2a;
-                }
-            }
-            if (vbb) {
-                const int64_t c1 = j1 - beg;
-                s.tb[tboff + c1] = tbb;
-                if (multi) {
-                    uint8_t *kpp = s.kp + kpoff + 3 * c1;
-                    kpp[0] = (uint8_t)mkb;
-                    kpp[1] = (uint8_t)k1b;
-                    kpp[2] = (uint8_t)k2b;
-                }
-                if (!wide) {
-                    ringrow[0 * kChunk + (j1 & (kChunk - 1))] = Hb;
-                    ringrow[1 * kChunk + (j1 & (kChunk - 1))] = E1b;
-                    ringrow[2 * kChunk + (j1 & (kChunk - 1))] = E2b;
-                }
-                if (spill) {
-                    int *svp = s.sv + soff;
-                    svp[c1] = Hb;
-                    svp[width + c1] = E1b;
-                    svp[2 * width + c1] = E2b;
-                }
-            }
-            // leftmost argmax of H over the row
-            int lb = -2147483647 - 1, lp = j0;
-            if (va) { lb = Ha; lp = j0; }
-            if (vbb && Hb > lb) { lb = Hb; lp = j1; }
-            const int m = wave_max(lb);
-            const unsigned long long hit = __ballot(lb == m && va);
-            const int first = __ffsll((long long)hit) - 1;
-            const int mpos = __shfl(lp, first < 0 ? 0 : first, kWave);
-            if (m > best) {
-                best = m;
-                besti = mpos;
+                for (int k = 0; k < kDescInts; ++k) dl[k] = dg[k];
             }
         }
-        if (lane == 0) {
-            sh.rrow[r % kRowRing] = make_int4(beg, end, besti, soff);
-            int *ri = s.rinfo + (int64_t)r * kRowInfoInts;
-            ri[0] = beg;
-            ri[1] = end;
-            ri[2] = besti;
-            ri[3] = soff;
-            ri[4] = (int)tboff;
-            ri[5] = (int)kpoff;
-        }
-        // make this row's LDS/HBM values visible to the next rows' loads (same wave)
-        wave_sync();
+        const int st = dp_row(a, s, sh, qlen, w, r, lane, ds);
+        if (st != kStOk) return st;
     }
+    cells += ds.cells;
+#ifdef MANDO_STAMPS
+    if (a.prof && lane == 0) {
+        int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
+        for (int k = 0; k < 4; ++k) pf[8 + k] += (int64_t)ds.seg[k];
+    }
+#endif
 
     // best predecessor of the sink at column qlen (first in in-edge order on ties)
+    hbm_fence();
     const int sr = n - 1;
     const int nin = s.in_n[kSink];
     int bs = -2147483647 - 1, bi = -1;
@@ -493,9 +763,15 @@ __device__ int run_dp(const PoaKArgs &a, Slot &s, SharedState &sh, const uint8_t
         const int p = bcast0(s.pos[s.sink_in[k]]);
         const RowRec pr = load_rowrec(sh, s, sr, p);
         if (qlen < pr.beg || qlen > pr.end) continue;
-        const int h = bcast0(row_val(sh, s, sr, p, pr, 0, qlen));
-        if (h > bs) {
-            bs = h;
+        int hv;
+        if (pre_in_ring(sr, p, pr)) {
+            hv = sh.ring[p % kRing][0][qlen & (kChunk - 1)];
+        } else {
+            hv = s.sv[pr.soff + (qlen - (pr.beg & ~1))];
+        }
+        hv = bcast0(hv);
+        if (hv > bs) {
+            bs = hv;
             bi = p;
         }
     }
@@ -505,32 +781,32 @@ __device__ int run_dp(const PoaKArgs &a, Slot &s, SharedState &sh, const uint8_t
 
 // ---------------------------------------------------------------------------------------------
 // backtrack (lane 0): fills qnode[q] = aligned node or -1 (insertion) for q in [0, qlen)
+// row record: rinfo[r] = {beg, end, argmax, soff, tbbase, kpbase, node, pre_n}
 // ---------------------------------------------------------------------------------------------
-__device__ int backtrack(const PoaKArgs &a, Slot &s, int bi, int qlen, int n) {
+__device__ int backtrack(SharedState &sh, int bi, int qlen, int n) {
+    const PoaKArgs a = args_of(sh);
+    Slot s = slot_of(sh);
     int i = bi, j = qlen, st = 0;  // 0 H, 1 E1, 2 E2, 3 F1, 4 F2
     int guard = n + qlen + 8;
     while (i > 0 && j > 0) {
         if (--guard < 0) return kStInternal;
-        const int *ri = s.rinfo + (int64_t)i * kRowInfoInts;
-        const int rb = ri[0];
-        const int64_t tboff = ri[4], kpoff = ri[5];
-        const int c = j - rb;
-        const int t = s.tb[tboff + c];
-        const int *d = s.desc + (int64_t)i * kDescInts;
-        const int node = d[0];
-        const int pn = d[1] >> 16;
+        const gint *rb = s.rinfo + (int64_t)i * kRowInfoInts;
+        const int64_t tbbase = rb[4], kpbase = rb[5];
+        const int node = rb[6], pn = rb[7];
+        const int t = s.tb[tbbase + j];
         if (st == 0) {
             const int ty = t & kTbTypeMask;
             if (ty <= 2) {
-                const int k = (pn > 1) ? s.kp[kpoff + 3 * c + ty] : 0;
-                const int p = (k < kPreInline) ? d[3 + k] : pre_row_slow(a, s, node, k);
+                const int k = (pn > 1) ? s.kp[kpbase + 3 * (int64_t)j + ty] : 0;
+                const int p = (k < kPreInline) ? s.desc[(int64_t)i * kDescInts + 3 + k]
+                                               : s.pos[in_list(s, a, node)[k]];
                 if (ty == 0) {
                     s.qnode[j - 1] = node;
                     i = p;
                     --j;
                 } else {
-                    const int *pri = s.rinfo + (int64_t)p * kRowInfoInts;
-                    const int tp = s.tb[(int64_t)pri[4] + (j - pri[0])];
+                    const int ptb = s.rinfo[(int64_t)p * kRowInfoInts + 4];
+                    const int tp = s.tb[(int64_t)ptb + j];
                     st = (tp & (ty == 1 ? kTbE1Open : kTbE2Open)) ? 0 : ty;
                     i = p;
                 }
@@ -539,17 +815,18 @@ __device__ int backtrack(const PoaKArgs &a, Slot &s, int bi, int qlen, int n) {
             st = ty;  // 3 or 4: handled below in the same step
         }
         if (st == 1 || st == 2) {
-            const int k = (pn > 1) ? s.kp[kpoff + 3 * c + st] : 0;
-            const int p = (k < kPreInline) ? d[3 + k] : pre_row_slow(a, s, node, k);
-            const int *pri = s.rinfo + (int64_t)p * kRowInfoInts;
-            const int tp = s.tb[(int64_t)pri[4] + (j - pri[0])];
+            const int k = (pn > 1) ? s.kp[kpbase + 3 * (int64_t)j + st] : 0;
+            const int p = (k < kPreInline) ? s.desc[(int64_t)i * kDescInts + 3 + k]
+                                           : s.pos[in_list(s, a, node)[k]];
+            const int ptb = s.rinfo[(int64_t)p * kRowInfoInts + 4];
+            const int tp = s.tb[(int64_t)ptb + j];
             st = (tp & (st == 1 ? kTbE1Open : kTbE2Open)) ? 0 : st;
             i = p;
             continue;
         }
         // F1 / F2: query base j-1 is an insertion at row i
         s.qnode[j - 1] = -1;
-        const int tprev = s.tb[tboff + c - 1];
+        const int tprev = s.tb[tbbase + j - 1];
         st = (tprev & (st == 3 ? kTbF1OpenNext : kTbF2OpenNext)) ? 0 : st;
         --j;
     }
@@ -562,8 +839,8 @@ __device__ int backtrack(const PoaKArgs &a, Slot &s, int bi, int qlen, int n) {
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int add_edge(const PoaKArgs &a, Slot &s, int from, int to, bool check,
                                         bool from_new, bool to_new) {
-    int *ol = out_list(s, a, from);
-    int *ow = out_wlist(s, a, from);
+    gint *ol = out_list(s, a, from);
+    gint *ow = out_wlist(s, a, from);
     if (check) {
         const int on = s.out_n[from];
         for (int k = 0; k < on; ++k)
@@ -577,7 +854,7 @@ __device__ __forceinline__ int add_edge(const PoaKArgs &a, Slot &s, int from, in
     ol[on] = to;
     ow[on] = 1;
     s.out_n[from] = on + 1;
-    int *il = in_list(s, a, to);
+    gint *il = in_list(s, a, to);
     const int inn = to_new ? 0 : s.in_n[to];
     if (inn >= in_cap(a, to)) return kStCap;
     il[inn] = from;
@@ -585,8 +862,10 @@ __device__ __forceinline__ int add_edge(const PoaKArgs &a, Slot &s, int from, in
     return kStOk;
 }
 
-__device__ int update_graph(const PoaKArgs &a, Slot &s, const uint8_t *q, int qlen, int &n,
+__device__ int update_graph(SharedState &sh, const uint8_t *q, int qlen, int &n,
                             int &ng, int lane) {
+    const PoaKArgs a = args_of(sh);
+    Slot s = slot_of(sh);
     // Path kinds per query position: 0 = existing node (matched, or a reused aligned node),
     // 1 = new node aligned to the DP row's node (mismatch), 2 = new inserted node.
     // Topological order invariant kept here: every aligned group occupies a contiguous block of
@@ -641,7 +920,7 @@ __device__ int update_graph(const PoaKArgs &a, Slot &s, const uint8_t *q, int ql
             if (kind == 2) s.gid[tgt] = -1;
         }
         if (kind == 1) {
-            int *gt = s.gtab + (int64_t)g * kGtabInts;
+            gint *gt = s.gtab + (int64_t)g * kGtabInts;
             if (needgrp) {
 #pragma unroll
                 for (int t = 0; t < 5; ++t) gt[t] = -1;
@@ -655,12 +934,8 @@ __device__ int update_graph(const PoaKArgs &a, Slot &s, const uint8_t *q, int ql
             gt[b] = tgt;
             s.gid[tgt] = g;
         }
-        int prev_t = __shfl_up(tgt, 1, kWave);
-        int prev_n = __shfl_up(isnew, 1, kWave);
-        if (lane == 0) {
-            prev_t = last;
-            prev_n = last_new;
-        }
+        const int prev_t = dpp_shr1(tgt, last);
+        const int prev_n = dpp_shr1(isnew, last_new);
         int e = kStOk;
         if (valid) e = add_edge(a, s, prev_t, tgt, !prev_n, prev_n != 0, isnew != 0);
         if (__ballot(e != kStOk)) err = kStCap;
@@ -695,7 +970,7 @@ __device__ int update_graph(const PoaKArgs &a, Slot &s, const uint8_t *q, int ql
         const int R_in = __shfl(aslot, nl, kWave);
         const int nq = above ? c * kWave + nl : nxt_q;
         const int R = above ? R_in : nxt_R;
-        const int prev_kind = __shfl_up(kind, 1, kWave);
+        const int prev_kind = dpp_shr1(kind, 0);
         if (valid && kind == 2) {
             const bool run_start = (qi == 0) || (lane == 0 ? s.qflag[qi - 1] != 2 : prev_kind != 2);
             s.qnb[qi] = R;
@@ -716,7 +991,7 @@ __device__ int update_graph(const PoaKArgs &a, Slot &s, const uint8_t *q, int ql
         const int r = c * kWave + lane;
         const bool valid = r < n_old;
         const int tot = valid ? s.ins[r] + s.insmm[r] : 0;
-        const int inc = wave_incl_sum(tot, lane) + carry;
+        const int inc = dpp_incl_sum(tot) + carry;
         carry = readlane(inc, kWave - 1);
         if (valid) {
             const int v = s.order[r];
@@ -749,9 +1024,10 @@ __device__ int update_graph(const PoaKArgs &a, Slot &s, const uint8_t *q, int ql
         s.ins[t] = 0;
         s.insmm[t] = 0;
     }
-    int *tmp = s.order;
-    s.order = s.order2;
-    s.order2 = tmp;
+    if (lane == 0) {
+        sh.slot.order = s.order2;
+        sh.slot.order2 = s.order;
+    }
     wave_sync();
     return kStOk;
 }
@@ -759,8 +1035,10 @@ __device__ int update_graph(const PoaKArgs &a, Slot &s, const uint8_t *q, int ql
 // ---------------------------------------------------------------------------------------------
 // heaviest bundling (lane 0): reverse topological sweep, then walk from the source
 // ---------------------------------------------------------------------------------------------
-__device__ int consensus(const PoaKArgs &a, Slot &s, int n, uint8_t *out, int64_t cap,
+__device__ int consensus(SharedState &sh, int n, uint8_t *out, int64_t cap,
                          int &len) {
+    const PoaKArgs a = args_of(sh);
+    Slot s = slot_of(sh);
     for (int r = n - 1; r >= 0; --r) {
         const int v = s.order[r];
         if (v == kSink) {
@@ -769,8 +1047,8 @@ __device__ int consensus(const PoaKArgs &a, Slot &s, int n, uint8_t *out, int64_
             continue;
         }
         const int on = s.out_n[v];
-        const int *ol = out_list(s, a, v);
-        const int *ow = out_wlist(s, a, v);
+        const gint *ol = out_list(s, a, v);
+        const gint *ow = out_wlist(s, a, v);
         int maxw = -1, maxr = -1;
         for (int k = 0; k < on; ++k) {
             const int ro = s.pos[ol[k]];
@@ -798,39 +1076,47 @@ __device__ int consensus(const PoaKArgs &a, Slot &s, int n, uint8_t *out, int64_
     return l <= cap ? kStOk : kStCap;
 }
 
-__global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs a) {
+__global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
     __shared__ SharedState sh;
     const int lane = lane_id();
+    if (lane == 0) sh.args = ka;
+    wave_sync();
+    const PoaKArgs &a = ka;
     char *ws = a.ws + (int64_t)blockIdx.x * a.slot_bytes;
     Slot s;
-    s.base = (uint8_t *)(ws + a.lay.base);
-    s.gid = (int *)(ws + a.lay.gid);
-    s.gtab = (int *)(ws + a.lay.gtab);
-    s.in_n = (int *)(ws + a.lay.in_n);
-    s.out_n = (int *)(ws + a.lay.out_n);
-    s.in_id = (int *)(ws + a.lay.in_id);
-    s.out_id = (int *)(ws + a.lay.out_id);
-    s.out_w = (int *)(ws + a.lay.out_w);
-    s.sink_in = (int *)(ws + a.lay.sink_in);
-    s.src_out = (int *)(ws + a.lay.src_out);
-    s.src_out_w = (int *)(ws + a.lay.src_out_w);
-    s.pos = (int *)(ws + a.lay.pos);
-    s.remrow = (int *)(ws + a.lay.remrow);
-    s.desc = (int *)(ws + a.lay.desc);
-    s.rinfo = (int *)(ws + a.lay.rinfo);
-    s.tb = (uint8_t *)(ws + a.lay.tb);
-    s.kp = (uint8_t *)(ws + a.lay.kp);
-    s.sv = (int *)(ws + a.lay.sv);
-    s.qnode = (int *)(ws + a.lay.qnode);
-    s.qtgt = (int *)(ws + a.lay.qtgt);
-    s.qflag = (int *)(ws + a.lay.qflag);
-    s.qnb = (int *)(ws + a.lay.qnb);
-    s.qoff = (int *)(ws + a.lay.qoff);
-    s.ins = (int *)(ws + a.lay.ins);
-    s.insmm = (int *)(ws + a.lay.insmm);
-    s.qmslot = (int *)(ws + a.lay.qmslot);
-    s.score = (int *)(ws + a.lay.score);
-    s.nxt = (int *)(ws + a.lay.nxt);
+    s.base = (gu8 *)(ws + a.lay.base);
+    s.gid = (gint *)(ws + a.lay.gid);
+    s.gtab = (gint *)(ws + a.lay.gtab);
+    s.in_n = (gint *)(ws + a.lay.in_n);
+    s.out_n = (gint *)(ws + a.lay.out_n);
+    s.in_id = (gint *)(ws + a.lay.in_id);
+    s.out_id = (gint *)(ws + a.lay.out_id);
+    s.out_w = (gint *)(ws + a.lay.out_w);
+    s.sink_in = (gint *)(ws + a.lay.sink_in);
+    s.src_out = (gint *)(ws + a.lay.src_out);
+    s.src_out_w = (gint *)(ws + a.lay.src_out_w);
+    s.pos = (gint *)(ws + a.lay.pos);
+    s.remrow = (gint *)(ws + a.lay.remrow);
+    s.desc = (gint *)(ws + a.lay.desc);
+    s.rinfo = (gint *)(ws + a.lay.rinfo);
+    s.tb = (gu8 *)(ws + a.lay.tb);
+    s.kp = (gu8 *)(ws + a.lay.kp);
+    s.sv = (gint *)(ws + a.lay.sv);
+    s.qnode = (gint *)(ws + a.lay.qnode);
+    s.qtgt = (gint *)(ws + a.lay.qtgt);
+    s.qflag = (gint *)(ws + a.lay.qflag);
+    s.qnb = (gint *)(ws + a.lay.qnb);
+    s.qoff = (gint *)(ws + a.lay.qoff);
+    s.ins = (gint *)(ws + a.lay.ins);
+    s.insmm = (gint *)(ws + a.lay.insmm);
+    s.qmslot = (gint *)(ws + a.lay.qmslot);
+    s.score = (gint *)(ws + a.lay.score);
+    s.nxt = (gint *)(ws + a.lay.nxt);
+    s.order = (gint *)(ws + a.lay.order0);
+    s.order2 = (gint *)(ws + a.lay.order1);
+    if (lane == 0) sh.slot = s;
+    wave_sync();
+    int64_t *prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
 
     for (;;) {
         int gi = 0;
@@ -838,8 +1124,11 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs a) {
         gi = bcast0(gi);
         if (gi >= a.n_groups) break;
         const int g = a.gorder ? a.gorder[gi] : gi;
-        s.order = (int *)(ws + a.lay.order0);
-        s.order2 = (int *)(ws + a.lay.order1);
+        if (lane == 0) {
+            sh.slot.order = (gint *)(ws + a.lay.order0);
+            sh.slot.order2 = (gint *)(ws + a.lay.order1);
+        }
+        wave_sync();
         const int64_t r0 = a.grp_off[g], r1 = a.grp_off[g + 1];
         int st = kStOk;
         int n = 0, ng = 0;
@@ -850,7 +1139,7 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs a) {
         if (first < r1) {
             const uint8_t *q0 = a.seq + a.seq_off[first];
             const int L0 = (int)(a.seq_off[first + 1] - a.seq_off[first]);
-            st = init_chain(a, s, q0, L0, lane, n);
+            st = init_chain(sh, q0, L0, lane, n);
             wave_sync();
             for (int64_t rd = first + 1; rd < r1 && st == kStOk; ++rd) {
                 const int qlen = (int)(a.seq_off[rd + 1] - a.seq_off[rd]);
@@ -860,31 +1149,49 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs a) {
                     break;
                 }
                 const uint8_t *q = a.seq + a.seq_off[rd];
-                build_desc(a, s, n, lane);
+                uint64_t t0 = prof ? clock64() : 0;
+                build_desc(sh, n, lane);
+                uint64_t t1 = prof ? clock64() : 0;
                 int bi = -1;
-                st = run_dp(a, s, sh, q, qlen, n, lane, cells, bi);
+                st = run_dp(sh, q, qlen, n, lane, cells, bi);
+                uint64_t t2 = prof ? clock64() : 0;
+                if (prof && lane == 0) {
+                    prof[0] += (int64_t)(t1 - t0);
+                    prof[1] += (int64_t)(t2 - t1);
+                    prof[5] += n;
+                    prof[6] += 1;
+                }
                 if (st != kStOk) break;
                 if (bi < 0) {
                     st = kStInternal;
                     break;
                 }
                 wave_sync();
+                uint64_t t3 = prof ? clock64() : 0;
                 int bst = kStOk;
-                if (lane == 0) bst = backtrack(a, s, bi, qlen, n);
+                if (lane == 0) bst = backtrack(sh, bi, qlen, n);
                 st = bcast0(bst);
                 if (st != kStOk) break;
                 wave_sync();
-                st = update_graph(a, s, q, qlen, n, ng, lane);
+                uint64_t t4 = prof ? clock64() : 0;
+                st = update_graph(sh, q, qlen, n, ng, lane);
                 wave_sync();
+                uint64_t t5 = prof ? clock64() : 0;
+                if (prof && lane == 0) {
+                    prof[2] += (int64_t)(t4 - t3);
+                    prof[3] += (int64_t)(t5 - t4);
+                }
             }
             if (st == kStOk) {
+                uint64_t t6 = prof ? clock64() : 0;
                 int cst = kStOk, len = 0;
                 if (lane == 0) {
                     const int64_t cap = a.cons_off[g + 1] - a.cons_off[g];
-                    cst = consensus(a, s, n, a.cons + a.cons_off[g], cap, len);
+                    cst = consensus(sh, n, a.cons + a.cons_off[g], cap, len);
                 }
                 st = bcast0(cst);
                 clen = bcast0(len);
+                if (prof && lane == 0) prof[4] += (int64_t)(clock64() - t6);
             }
         }
         if (lane == 0) {
@@ -923,6 +1230,11 @@ __global__ __launch_bounds__(kWave) void wave_selftest_kernel(int *bad) {
         for (int l = 0; l < kWave; ++l)
             allmax = max(allmax, (int)((l * 2654435761u + trial * 40503u) % 1000u) - 500);
         if (wave_max(v) != allmax) ++errs;
+        // DPP forms used by the DP / graph update
+        if (dpp_incl_max(v, -2147483647 - 1) != rmax) ++errs;
+        if (dpp_incl_sum(v) != rsum) ++errs;
+        const int prevv = lane == 0 ? 12345 : (int)(((lane - 1) * 2654435761u + trial * 40503u) % 1000u) - 500;
+        if (dpp_shr1(v, 12345) != prevv) ++errs;
     }
     atomicAdd(bad, errs);
 }

@@ -84,3 +84,63 @@ def read_groups(n_groups: int, length: int | tuple[int, int], depth: int | tuple
         templates.append(t)
         groups.append(rs)
     return templates, groups
+
+
+# ---------------------------------------------------------------------------------------------
+# fast multithreaded generator (libmando_synth.so) for benchmark-scale data
+# ---------------------------------------------------------------------------------------------
+def _synth_lib():
+    import ctypes
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmando_synth.so")
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    lib.mando_synth_groups.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_double, P, P, P, P, P, P, ctypes.c_int]
+    lib.mando_synth_free.argtypes = [P]
+    return lib
+
+
+def fast_groups(n_groups: int, length: tuple[int, int], depth: tuple[int, int], seed: int = DATA_SEED,
+                model: dict = R2C2, threads: int = 0, with_templates: bool = False):
+    """Packed groups: (seqs uint8 array, seq_off int64, grp_off int64[, templates list])."""
+    import ctypes
+
+    lib = _synth_lib()
+    out = ctypes.c_void_p()
+    so = ctypes.c_void_p()
+    nr = ctypes.c_int64()
+    go = ctypes.c_void_p()
+    tp = ctypes.c_void_p()
+    to = ctypes.c_void_p()
+    rc = lib.mando_synth_groups(seed, n_groups, length[0], length[1], depth[0], depth[1],
+                                model["sub"], model["ins"], model["dele"], ctypes.byref(out),
+                                ctypes.byref(so), ctypes.byref(nr), ctypes.byref(go),
+                                ctypes.byref(tp) if with_templates else None,
+                                ctypes.byref(to) if with_templates else None, threads)
+    if rc != 0:
+        raise RuntimeError(f"mando_synth_groups failed: {rc}")
+    n = nr.value
+    seq_off = np.ctypeslib.as_array(ctypes.cast(so, ctypes.POINTER(ctypes.c_int64)), shape=(n + 1,)).copy()
+    grp_off = np.ctypeslib.as_array(ctypes.cast(go, ctypes.POINTER(ctypes.c_int64)), shape=(n_groups + 1,)).copy()
+    total = int(seq_off[-1])
+    seqs = np.ctypeslib.as_array(ctypes.cast(out, ctypes.POINTER(ctypes.c_uint8)), shape=(max(total, 1),)).copy()
+    templates = None
+    if with_templates:
+        toff = np.ctypeslib.as_array(ctypes.cast(to, ctypes.POINTER(ctypes.c_int64)), shape=(n_groups + 1,)).copy()
+        traw = ctypes.string_at(tp, int(toff[-1]))
+        templates = [traw[toff[i]:toff[i + 1]].decode() for i in range(n_groups)]
+        lib.mando_synth_free(tp)
+        lib.mando_synth_free(to)
+    for p in (out, so, go):
+        lib.mando_synth_free(p)
+    return (seqs, seq_off, grp_off, templates) if with_templates else (seqs, seq_off, grp_off)
+
+
+def unpack_groups(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, groups=None):
+    """Packed -> list of lists of str (optionally only the listed group indices)."""
+    raw = seqs.tobytes()
+    idx = range(len(grp_off) - 1) if groups is None else groups
+    return [[raw[seq_off[r]:seq_off[r + 1]].decode() for r in range(grp_off[g], grp_off[g + 1])] for g in idx]
