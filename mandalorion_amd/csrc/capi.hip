@@ -114,6 +114,11 @@ mando::PoaCaps plan_caps(const mando_poa_params &p, int64_t max_first, int64_t m
     c.TBC = nc * rowb * (int64_t)(attempt + 1);
     c.KPC = 3 * c.TBC / (attempt == 0 ? 2 : 1);
     c.SVC = c.TBC / (attempt == 0 ? 2 : 1) * 3;
+    // the kernel keeps its per-read usage counters in 32 bits
+    const int64_t lim = int64_t(1) << 30;
+    c.TBC = std::min(c.TBC, lim);
+    c.KPC = std::min(c.KPC, lim);
+    c.SVC = std::min(c.SVC, lim / 4);
     return c;
 }
 
@@ -178,6 +183,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         for (int64_t s = 0; s < slots; ++s)
             for (int k = 0; k < mando::kProfPhases; ++k) tot[k] += (double)h[(size_t)(s * mando::kProfPhases + k)];
         const double reads = std::max(1.0, tot[6]), rows = std::max(1.0, tot[5]);
+        fprintf(stderr, "[mando prof] fast rows %.1f%%\n", 100.0 * tot[7] / rows);
         fprintf(stderr, "[mando prof] slots=%lld reads=%.0f rows/read=%.0f | cycles per read: desc %.0f dp %.0f (%.1f/row) backtrack %.0f update %.0f | consensus/slot %.0f\n",
                 (long long)slots, reads, rows / reads, tot[0] / reads, tot[1] / reads, tot[1] / rows,
                 tot[2] / reads, tot[3] / reads, tot[4] / (double)slots);

@@ -23,6 +23,8 @@
 //     in-register pointer jumping.
 #include "poa_kernel.h"
 
+#include <type_traits>
+
 namespace mando {
 
 // Workspace pointers carry the global address space explicitly: they are re-read from LDS per
@@ -410,8 +412,19 @@ __device__ __forceinline__ void stage_pre(SharedState &sh, const Slot &s, const 
     }
 }
 
+// Scoring: the reference always runs `abpoa -M 5` with default gaps, so that case is compiled with
+// constants (no quarter-rate multiplies, fewer live scalars); any other parameter set uses the
+// runtime-valued variant of the same kernel.
+struct DefaultScores {
+    static constexpr int match = 5, mismatch = 4, o1 = 4, e1 = 2, o2 = 24, e2 = 1;
+};
+struct RuntimeScores {
+    int match, mismatch, o1, e1, o2, e2;
+};
+
 struct DpState {
-    int64_t tb_used, kp_used, sv_used, cells;
+    int tb_used, kp_used, sv_used;
+    int64_t cells;
     uint64_t seg[4];
 };
 
@@ -452,9 +465,10 @@ __device__ __forceinline__ bool in_band(int col, int b, int e) {
 // One DP row r.  Predecessor k's record lives in lane k (pP row, pB/pE band, pA argmax, pS spill
 // offset); the common case (every predecessor in the LDS ring) reads values with 4 LDS ops per
 // predecessor and no global memory traffic except the traceback stores.
-__device__ __forceinline__ int dp_row(const PoaKArgs &a, Slot &s, SharedState &sh, int qlen, int w,
-                                      int r, int lane, DpState &ds) {
-    const int e1 = a.e1, e2 = a.e2, oe1 = a.o1 + a.e1, oe2 = a.o2 + a.e2;
+template <class SC>
+__device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
+                                      int w, int r, int lane, DpState &ds) {
+    const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
     const int IDENT = -(1 << 30);
     STAMP(ts0);
     const int *dl = &sh.desc[r & (kWave - 1)][0];
@@ -513,9 +527,9 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, Slot &s, SharedState &s
     const int wa = nchunk * kChunk;
     const int tbw = (span + 3) & ~3;
     const bool multi = pn > 1;
-    if (ds.tb_used + tbw > a.caps.TBC) return kStCap;
-    if (multi && ds.kp_used + 3 * tbw > a.caps.KPC) return kStCap;
-    if (spill && ds.sv_used + 3 * (int64_t)wa > a.caps.SVC) return kStCap;
+    if (ds.tb_used + tbw > (int)a.caps.TBC) return kStCap;
+    if (multi && ds.kp_used + 3 * tbw > (int)a.caps.KPC) return kStCap;
+    if (spill && ds.sv_used + 3 * wa > (int)a.caps.SVC) return kStCap;
     // 32-bit offsets from the slot's arrays (the stores then use a scalar base + vector offset)
     const int tbbase = (int)ds.tb_used - cb0;       // traceback byte of column j: tb[tbbase + j]
     const int kpbase = (int)ds.kp_used - 3 * cb0;   // predecessor bytes of column j: kp[kpbase + 3j]
@@ -523,7 +537,7 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, Slot &s, SharedState &s
     const int svbase = (int)ds.sv_used - cb0;       // plane pl, column j: sv[svbase + pl*wa + j]
     ds.tb_used += tbw;
     if (multi) ds.kp_used += 3 * tbw;
-    if (spill) ds.sv_used += 3 * (int64_t)wa;
+    if (spill) ds.sv_used += 3 * wa;
     ds.cells += end - beg + 1;
     STAMP(ts1);
     uint64_t ts2 = ts1, ts3 = ts1;
@@ -541,8 +555,8 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, Slot &s, SharedState &s
         int tpair = 0;
         if (r == 0) {
             // source row: H[0][0] = 0, H[0][j] = max(-(o1+e1 j), -(o2+e2 j))
-            Ha = (j0 == 0) ? 0 : max(-(a.o1 + e1 * j0), -(a.o2 + e2 * j0));
-            Hb = max(-(a.o1 + e1 * j1), -(a.o2 + e2 * j1));
+            Ha = (j0 == 0) ? 0 : max(-(sc.o1 + e1 * j0), -(sc.o2 + e2 * j0));
+            Hb = max(-(sc.o1 + e1 * j1), -(sc.o2 + e2 * j1));
             E1a = Ha - oe1;
             E1b = Hb - oe1;
             E2a = Ha - oe2;
@@ -609,8 +623,8 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, Slot &s, SharedState &s
                 STAMP(tx);
                 ts2 = tx;
             }
-            const int Ma = Mva + score_of(vb, qa, a.match, a.mismatch);
-            const int Mb = Mvb + score_of(vb, qb, a.match, a.mismatch);
+            const int Ma = Mva + score_of(vb, qa, sc.match, sc.mismatch);
+            const int Mb = Mvb + score_of(vb, qb, sc.match, sc.mismatch);
             const int H0a = max(Ma, max(X1a, X2a));
             const int H0b = max(Mb, max(X1b, X2b));
             // horizontal gaps: F[j] = max(C, max_{k<j} H0[k] + e*k) - oe - e*(j-1)
@@ -715,23 +729,205 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, Slot &s, SharedState &s
     return kStOk;
 }
 
+// Loop-carried state of the row loop: the previous row's band record (forwarded in registers, so
+// the common predecessor r-1 costs no LDS round trip) and the next row's prefetched descriptor and
+// predecessor records (read from LDS one row ahead, off the critical path).
+struct RowPipe {
+    int prv_r, prv_beg, prv_end, prv_am;
+    int node, d1, rem, p0, p1;
+    int4 x0, x1;
+};
+
+__device__ __forceinline__ void prefetch_row(const SharedState &sh, int r, RowPipe &rp) {
+    const int *dl = &sh.desc[r & (kWave - 1)][0];
+    rp.node = dl[0];
+    rp.d1 = dl[1];
+    rp.rem = dl[2];
+    rp.p0 = dl[3];
+    rp.p1 = dl[4];
+    rp.x0 = sh.rrow[max(rp.p0, 0) % kRowRing];
+    rp.x1 = sh.rrow[max(rp.p1, 0) % kRowRing];
+}
+
+// Fast path for the common row: 1 or 2 predecessors, both in the LDS ring, band <= 128 columns,
+// both records in the row ring.  All row-control values stay in VGPRs (every lane computes them),
+// so the row costs a single scalar round trip (the fast-path test) plus the argmax broadcast.
+// Returns false (having changed nothing) when the row must take the general path.
+template <class SC>
+__device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
+                                           int w, int r, int lane, DpState &ds, RowPipe &pp) {
+    const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
+    const int IDENT = -(1 << 30);
+    const int node = pp.node, d1 = pp.d1, rem = pp.rem, p0 = pp.p0, p1 = pp.p1;
+    const int vb = d1 & 0xff, pn = d1 >> 16;
+    const int4 x0 = (p0 == pp.prv_r) ? make_int4(pp.prv_beg, pp.prv_end, pp.prv_am, 0) : pp.x0;
+    const int4 x1 = (p1 == pp.prv_r) ? make_int4(pp.prv_beg, pp.prv_end, pp.prv_am, 0) : pp.x1;
+    const bool two = pn == 2;
+    const int am0 = x0.z + 1, am1 = two ? x1.z + 1 : am0;
+    const int xr = qlen - rem;
+    const int beg = max(0, min(min(am0, am1), xr) - w);
+    const int end = min(qlen, max(max(am0, am1), xr) + w);
+    const int cb0 = beg & ~1;
+    const int span = end - cb0 + 1;
+    const int tbw = (span + 3) & ~3;
+    const bool ring0 = (r - p0 < kRing) && row_narrow(x0.x, x0.y);
+    const bool ring1 = !two || ((r - p1 < kRing) && row_narrow(x1.x, x1.y));
+    // far / multi come from the descriptor (prefetched a row earlier): cheap scalar tests
+    const int d1s = bcast0(d1);
+    const bool far = ((d1s >> 8) & 0xff) != 0;
+    const bool multi = (d1s >> 16) > 1;
+    const bool ok = pn >= 1 && pn <= 2 && span <= kChunk && ring0 && ring1 &&
+                    ds.tb_used + tbw + kChunk <= (int)a.caps.TBC &&
+                    (!multi || ds.kp_used + 3 * (tbw + kChunk) <= (int)a.caps.KPC) &&
+                    (!far || ds.sv_used + 3 * kChunk <= (int)a.caps.SVC);
+    if (!__builtin_amdgcn_readfirstlane((int)ok)) return false;
+
+    const int tbbase = (int)ds.tb_used - cb0;
+    const int kpbase = (int)ds.kp_used - 3 * cb0;
+    const int soff = far ? (int)ds.sv_used : -1;
+    const int svbase = (int)ds.sv_used - cb0;
+    const int j0 = cb0 + 2 * lane, j1 = j0 + 1;
+    const bool va = j0 >= beg && j0 <= end, vbb = j1 <= end;
+    // branch-free query lookups (clamped index, then select)
+    const int qa0 = qbase(sh, min(max(j0 - 1, 0), qlen - 1)), qb0 = qbase(sh, min(j0, qlen - 1));
+    const int qa = (j0 >= 1 && j0 <= qlen) ? qa0 : 4;
+    const int qb = (j0 < qlen) ? qb0 : 4;
+    const int ia = (j0 - 1) & (kChunk - 1), ib = j0 & (kChunk - 1);
+    // predecessor 0
+    const int *r0p = &sh.ring[p0 % kRing][0][0];
+    const int h0A = r0p[ia], h0B = r0p[ib];
+    const int2 y01 = *reinterpret_cast<const int2 *>(r0p + kChunk + ib);
+    const int2 y02 = *reinterpret_cast<const int2 *>(r0p + 2 * kChunk + ib);
+    // predecessor 1 (read unconditionally, masked when absent)
+    const int *r1p = &sh.ring[max(p1, 0) % kRing][0][0];
+    const int h1A = r1p[ia], h1B = r1p[ib];
+    const int2 y11 = *reinterpret_cast<const int2 *>(r1p + kChunk + ib);
+    const int2 y12 = *reinterpret_cast<const int2 *>(r1p + 2 * kChunk + ib);
+    const bool i0A = in_band(j0 - 1, x0.x, x0.y), i0B = in_band(j0, x0.x, x0.y), i0C = in_band(j1, x0.x, x0.y);
+    const bool i1A = two && in_band(j0 - 1, x1.x, x1.y), i1B = two && in_band(j0, x1.x, x1.y),
+               i1C = two && in_band(j1, x1.x, x1.y);
+    const int a0 = i0A ? h0A : kNegInf, b0 = i0B ? h0B : kNegInf;
+    const int a1 = i1A ? h1A : kNegInf, b1 = i1B ? h1B : kNegInf;
+    const int u0 = i0B ? y01.x : kNegInf, u1 = i1B ? y11.x : kNegInf;
+    const int v0 = i0C ? y01.y : kNegInf, v1 = i1C ? y11.y : kNegInf;
+    const int w0 = i0B ? y02.x : kNegInf, w1 = i1B ? y12.x : kNegInf;
+    const int z0 = i0C ? y02.y : kNegInf, z1 = i1C ? y12.y : kNegInf;
+    // first predecessor attaining the max (strict > keeps the earlier one)
+    const int Mva = max(a0, a1), Mvb = max(b0, b1);
+    const int mka = a1 > a0, mkb = b1 > b0;
+    const int X1a = max(u0, u1), X1b = max(v0, v1), X2a = max(w0, w1), X2b = max(z0, z1);
+    const int k1a = u1 > u0, k1b = v1 > v0, k2a = w1 > w0, k2b = z1 > z0;
+
+    const int Ma = Mva + score_of(vb, qa, sc.match, sc.mismatch);
+    const int Mb = Mvb + score_of(vb, qb, sc.match, sc.mismatch);
+    const int H0a = max(Ma, max(X1a, X2a));
+    const int H0b = max(Mb, max(X1b, X2b));
+    const int G1a = va ? H0a + e1 * j0 : IDENT;
+    const int G1b = vbb ? H0b + e1 * j1 : IDENT;
+    const int G2a = va ? H0a + e2 * j0 : IDENT;
+    const int G2b = vbb ? H0b + e2 * j1 : IDENT;
+    const int inc1 = dpp_incl_max(max(G1a, G1b), IDENT);
+    const int inc2 = dpp_incl_max(max(G2a, G2b), IDENT);
+    const int carry1 = kNegInf + oe1 + e1 * (beg - 1);
+    const int carry2 = kNegInf + oe2 + e2 * (beg - 1);
+    const int P1a = max(dpp_shr1(inc1, IDENT), carry1), P1b = max(P1a, G1a);
+    const int P2a = max(dpp_shr1(inc2, IDENT), carry2), P2b = max(P2a, G2a);
+    const int F1a = P1a - oe1 - e1 * (j0 - 1), F1b = P1b - oe1 - e1 * (j1 - 1);
+    const int F2a = P2a - oe2 - e2 * (j0 - 1), F2b = P2b - oe2 - e2 * (j1 - 1);
+    const int Ha = max(H0a, max(F1a, F2a));
+    const int Hb = max(H0b, max(F1b, F2b));
+    auto src_type = [&](int H, int M, int X1, int X2, int F1, int k1, int k2) -> int {
+        if (M == H) return 0;
+        const bool t1 = X1 == H, t2 = X2 == H;
+        if (t1 && t2) return (k1 <= k2) ? 1 : 2;
+        if (t1) return 1;
+        if (t2) return 2;
+        return (F1 == H) ? 3 : 4;
+    };
+    const int tya = src_type(Ha, Ma, X1a, X2a, F1a, k1a, k2a);
+    const int tyb = src_type(Hb, Mb, X1b, X2b, F1b, k1b, k2b);
+    const int E1a = max(X1a - e1, Ha - oe1), E1b = max(X1b - e1, Hb - oe1);
+    const int E2a = max(X2a - e2, Ha - oe2), E2b = max(X2b - e2, Hb - oe2);
+    const int ta = tya | ((Ha - oe1 >= X1a - e1) ? kTbE1Open : 0) | ((Ha - oe2 >= X2a - e2) ? kTbE2Open : 0) |
+                   ((G1a >= P1a) ? kTbF1OpenNext : 0) | ((G2a >= P2a) ? kTbF2OpenNext : 0);
+    const int tb2 = tyb | ((Hb - oe1 >= X1b - e1) ? kTbE1Open : 0) | ((Hb - oe2 >= X2b - e2) ? kTbE2Open : 0) |
+                    ((G1b >= P1b) ? kTbF1OpenNext : 0) | ((G2b >= P2b) ? kTbF2OpenNext : 0);
+    // stores: the traceback pair of every lane (lanes past `end` write into slack the next row
+    // overwrites; the caller's capacity test keeps one chunk of slack), ring row, optional planes
+    *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)(ta | (tb2 << 8));
+    if (multi) {
+        GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + 3 * j0));
+        kq[0] = (uint16_t)(mka | (k1a << 8));
+        kq[1] = (uint16_t)(k2a | (mkb << 8));
+        kq[2] = (uint16_t)(k1b | (k2b << 8));
+    }
+    int *ringrow = &sh.ring[r % kRing][0][0];
+    *reinterpret_cast<int2 *>(ringrow + ib) = make_int2(Ha, Hb);
+    *reinterpret_cast<int2 *>(ringrow + kChunk + ib) = make_int2(E1a, E1b);
+    *reinterpret_cast<int2 *>(ringrow + 2 * kChunk + ib) = make_int2(E2a, E2b);
+    if (far) {
+        gint *sv = s.sv + svbase;
+        sv[j0] = Ha;
+        sv[j1] = Hb;
+        sv[kChunk + j0] = E1a;
+        sv[kChunk + j1] = E1b;
+        sv[2 * kChunk + j0] = E2a;
+        sv[2 * kChunk + j1] = E2b;
+    }
+    // leftmost argmax (value << 7 | 127 - column-in-chunk)
+    const int ca = va ? (min(max(Ha, -(1 << 23)), (1 << 23)) << 7) | (127 - 2 * lane) : (-2147483647 - 1);
+    const int cbk = vbb ? (min(max(Hb, -(1 << 23)), (1 << 23)) << 7) | (126 - 2 * lane) : (-2147483647 - 1);
+    const int mp = readlane(dpp_incl_max(max(ca, cbk), -2147483647 - 1), kWave - 1);
+    const int besti = cb0 + 127 - (mp & 127);
+    // bookkeeping (scalar)
+    const int begs = bcast0(beg), ends = bcast0(end), tbws = bcast0(tbw);
+    ds.tb_used += tbws;
+    if (multi) ds.kp_used += 3 * tbws;
+    if (far) ds.sv_used += 3 * kChunk;
+    ds.cells += ends - begs + 1;
+    if (lane == 0) {
+        sh.rrow[r % kRowRing] = make_int4(beg, end, besti, soff);
+        gint *ri = s.rinfo + (int64_t)r * kRowInfoInts;
+        ri[0] = beg;
+        ri[1] = end;
+        ri[2] = besti;
+        ri[3] = soff;
+        ri[4] = tbbase;
+        ri[5] = kpbase;
+        ri[6] = node;
+        ri[7] = pn;
+    }
+    pp.prv_r = r;
+    pp.prv_beg = beg;
+    pp.prv_end = end;
+    pp.prv_am = besti;
+    return true;
+}
+
 // ---------------------------------------------------------------------------------------------
 // banded DP over all rows of the current graph for read q (qlen): writes the traceback bytes and
 // returns the start row of the backtrack in bi_out (or -1)
 // ---------------------------------------------------------------------------------------------
-__device__ int run_dp(SharedState &sh, const uint8_t *q, int qlen,
+template <class SC>
+__device__ int run_dp(SharedState &sh, const SC &sc, const uint8_t *q, int qlen,
                       int n, int lane, int64_t &cells, int &bi_out) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
     if (qlen > kQLds) return kStUnsupported;
     const int w = a.band_b + (int)(a.band_f * (float)qlen);
     DpState ds{0, 0, 0, 0, {0, 0, 0, 0}};
+    const int TBC = (int)a.caps.TBC, KPC = (int)a.caps.KPC, SVC = (int)a.caps.SVC;
+    (void)TBC; (void)KPC; (void)SVC;
     // stage the read in LDS (4-bit codes): on gfx9 vmcnt orders loads behind every earlier store,
     // so a global load per row would wait for the previous rows' traceback stores to land
     for (int t = 2 * lane; t < qlen; t += 2 * kWave) {
         const int lo = q[t], hi = (t + 1 < qlen) ? q[t + 1] : 4;
         sh.qnib[t >> 1] = (uint8_t)(lo | (hi << 4));
     }
+    int nfast = 0;
+    RowPipe pp;
+    pp.prv_r = -1;
+    pp.prv_beg = pp.prv_end = pp.prv_am = 0;
     for (int r = 0; r < n - 1; ++r) {
         if ((r & (kWave - 1)) == 0) {
             // next 64 descriptors -> LDS (one global round trip per 64 rows)
@@ -742,11 +938,23 @@ __device__ int run_dp(SharedState &sh, const uint8_t *q, int qlen,
 #pragma unroll
                 for (int k = 0; k < kDescInts; ++k) dl[k] = dg[k];
             }
+            prefetch_row(sh, r, pp);
         }
-        const int st = dp_row(a, s, sh, qlen, w, r, lane, ds);
-        if (st != kStOk) return st;
+        const bool fastok = r > 0 && dp_row_fast(a, sc, s, sh, qlen, w, r, lane, ds, pp);
+        nfast += fastok;
+        if (!fastok) {
+            const int st = dp_row(a, sc, s, sh, qlen, w, r, lane, ds);
+            if (st != kStOk) return st;
+            const int4 x = sh.rrow[r % kRowRing];
+            pp.prv_r = r;
+            pp.prv_beg = x.x;
+            pp.prv_end = x.y;
+            pp.prv_am = x.z;
+        }
+        if (((r + 1) & (kWave - 1)) != 0) prefetch_row(sh, r + 1, pp);
     }
     cells += ds.cells;
+    if (a.prof && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 7] += nfast;
 #ifdef MANDO_STAMPS
     if (a.prof && lane == 0) {
         int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
@@ -1076,6 +1284,7 @@ __device__ int consensus(SharedState &sh, int n, uint8_t *out, int64_t cap,
     return l <= cap ? kStOk : kStCap;
 }
 
+template <class SC>
 __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
     __shared__ SharedState sh;
     const int lane = lane_id();
@@ -1153,7 +1362,12 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
                 build_desc(sh, n, lane);
                 uint64_t t1 = prof ? clock64() : 0;
                 int bi = -1;
-                st = run_dp(sh, q, qlen, n, lane, cells, bi);
+                SC sc;
+                if constexpr (!std::is_same<SC, DefaultScores>::value) {
+                    const PoaKArgs aa = args_of(sh);
+                    sc = SC{aa.match, aa.mismatch, aa.o1, aa.e1, aa.o2, aa.e2};
+                }
+                st = run_dp<SC>(sh, sc, q, qlen, n, lane, cells, bi);
                 uint64_t t2 = prof ? clock64() : 0;
                 if (prof && lane == 0) {
                     prof[0] += (int64_t)(t1 - t0);
@@ -1204,7 +1418,13 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
 }
 
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream) {
-    hipLaunchKernelGGL(poa_kernel, dim3(n_slots), dim3(kWave), 0, stream, a);
+    const bool dflt = a.match == DefaultScores::match && a.mismatch == DefaultScores::mismatch &&
+                      a.o1 == DefaultScores::o1 && a.e1 == DefaultScores::e1 && a.o2 == DefaultScores::o2 &&
+                      a.e2 == DefaultScores::e2;
+    if (dflt)
+        hipLaunchKernelGGL(poa_kernel<DefaultScores>, dim3(n_slots), dim3(kWave), 0, stream, a);
+    else
+        hipLaunchKernelGGL(poa_kernel<RuntimeScores>, dim3(n_slots), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 
