@@ -187,6 +187,10 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         fprintf(stderr, "[mando prof] slots=%lld reads=%.0f rows/read=%.0f | cycles per read: desc %.0f dp %.0f (%.1f/row) backtrack %.0f update %.0f | consensus/slot %.0f\n",
                 (long long)slots, reads, rows / reads, tot[0] / reads, tot[1] / reads, tot[1] / rows,
                 tot[2] / reads, tot[3] / reads, tot[4] / (double)slots);
+        if (tot[12] > 0)
+            fprintf(stderr, "[mando prof] backtrack per read: refills %.1f (%.0f cyc each) blocks %.1f walk %.0f cyc/block\n",
+                    tot[13] / reads, tot[12] / std::max(1.0, tot[13]), tot[14] / reads,
+                    (tot[2] - tot[12]) / std::max(1.0, tot[14]));
         if (tot[8] + tot[9] + tot[10] + tot[11] > 0)
             fprintf(stderr, "[mando prof] per DP row: band %.0f  pre-loop %.0f  compute %.0f  store+argmax %.0f\n",
                     tot[8] / rows, tot[9] / rows, tot[10] / rows, tot[11] / rows);

@@ -80,15 +80,34 @@ __device__ __forceinline__ int dpp_mov(int old, int v) {
     return __builtin_amdgcn_update_dpp(old, v, CTRL, RM, BM, false);
 }
 
-// inclusive prefix max over the wave; lanes see `ident` from outside the wave
-__device__ __forceinline__ int dpp_incl_max(int v, int ident) {
-    v = max(v, dpp_mov<0x111, 0xf, 0xf>(ident, v));
-    v = max(v, dpp_mov<0x112, 0xf, 0xf>(ident, v));
-    v = max(v, dpp_mov<0x114, 0xf, 0xf>(ident, v));
-    v = max(v, dpp_mov<0x118, 0xf, 0xf>(ident, v));
-    v = max(v, dpp_mov<0x142, 0xa, 0xf>(ident, v));
-    v = max(v, dpp_mov<0x143, 0xc, 0xf>(ident, v));
+// inclusive prefix max over the wave.  A lane without a DPP source keeps its own value (the
+// identity of max), so every step is one v_max_i32_dpp.  Written as inline asm: the compiler does
+// not fold update_dpp + max and serialises two scans through one temporary.  The s_nop pads cover
+// the 2-wait-state VALU-write -> DPP-read hazard (the asm is opaque to the hazard recognizer).
+#define MANDO_DPP_MAX(r, ctl) "v_max_i32_dpp " r ", " r ", " r " " ctl "\n"
+#define MANDO_ROW_SHR1 "row_shr:1 row_mask:0xf bank_mask:0xf"
+#define MANDO_ROW_SHR2 "row_shr:2 row_mask:0xf bank_mask:0xf"
+#define MANDO_ROW_SHR4 "row_shr:4 row_mask:0xf bank_mask:0xf"
+#define MANDO_ROW_SHR8 "row_shr:8 row_mask:0xf bank_mask:0xf"
+#define MANDO_BCAST15 "row_bcast:15 row_mask:0xa bank_mask:0xf"
+#define MANDO_BCAST31 "row_bcast:31 row_mask:0xc bank_mask:0xf"
+__device__ __forceinline__ int dpp_incl_max(int v, int /*ident*/) {
+    asm volatile("s_nop 1\n" MANDO_DPP_MAX("%0", MANDO_ROW_SHR1) "s_nop 1\n" MANDO_DPP_MAX("%0", MANDO_ROW_SHR2)
+                 "s_nop 1\n" MANDO_DPP_MAX("%0", MANDO_ROW_SHR4) "s_nop 1\n" MANDO_DPP_MAX("%0", MANDO_ROW_SHR8)
+                 "s_nop 1\n" MANDO_DPP_MAX("%0", MANDO_BCAST15) "s_nop 1\n" MANDO_DPP_MAX("%0", MANDO_BCAST31)
+                 : "+v"(v));
     return v;
+}
+// two independent scans interleaved step by step (each hides part of the other's hazard)
+__device__ __forceinline__ void dpp_incl_max2(int &a, int &b) {
+    asm volatile("s_nop 1\n"
+                 MANDO_DPP_MAX("%0", MANDO_ROW_SHR1) MANDO_DPP_MAX("%1", MANDO_ROW_SHR1) "s_nop 0\n"
+                 MANDO_DPP_MAX("%0", MANDO_ROW_SHR2) MANDO_DPP_MAX("%1", MANDO_ROW_SHR2) "s_nop 0\n"
+                 MANDO_DPP_MAX("%0", MANDO_ROW_SHR4) MANDO_DPP_MAX("%1", MANDO_ROW_SHR4) "s_nop 0\n"
+                 MANDO_DPP_MAX("%0", MANDO_ROW_SHR8) MANDO_DPP_MAX("%1", MANDO_ROW_SHR8) "s_nop 0\n"
+                 MANDO_DPP_MAX("%0", MANDO_BCAST15) MANDO_DPP_MAX("%1", MANDO_BCAST15) "s_nop 0\n"
+                 MANDO_DPP_MAX("%0", MANDO_BCAST31) MANDO_DPP_MAX("%1", MANDO_BCAST31)
+                 : "+v"(a), "+v"(b));
 }
 
 __device__ __forceinline__ int dpp_incl_sum(int v) {
@@ -140,15 +159,21 @@ struct RowRec {
 
 constexpr int kQLds = 8192;      // reads up to this length are staged in LDS (4-bit bases)
 constexpr int kStage = 2 * kChunk;  // staging slot width (a 130-column window never aliases)
+constexpr int kTbWin = (kRing * kChunk + kStage) * 3 * 4;
 
-struct SharedState {
-    int ring[kRing][3][kChunk];  // H, E1out, E2out of the last kRing narrow rows, col & 127
-    int stage[3][kStage];        // one predecessor window copied from HBM, col & 255
+struct alignas(16) SharedState {
+    union {
+        struct {
+            int ring[kRing][3][kChunk];  // H, E1out, E2out of the last kRing narrow rows, col & 127
+            int stage[3][kStage];        // one predecessor window copied from HBM, col & 255
+        };
+        uint8_t tbwin[(kRing * kChunk + kStage) * 3 * 4];  // backtrack: traceback byte window
+    };
     int4 rrow[kRowRing];         // beg, end, argmax, spill offset of the last kRowRing rows
     int desc[kWave][kDescInts];  // descriptors of the current 64-row batch
     int4 prec[kWave];            // rare-case predecessor records {row, beg, end, argmax}
     int psoff[kWave];            // ... and their spill offsets
-    uint8_t qnib[kQLds / 2];     // read bases, two 4-bit codes per byte
+    alignas(16) uint8_t qnib[kQLds / 2];  // read bases, two 4-bit codes per byte
     Slot slot;                   // this wave's workspace arrays (read per phase, see slot_of)
     PoaKArgs args;               // kernel arguments (read per phase, see args_of)
 };
@@ -228,7 +253,7 @@ __device__ __forceinline__ PoaKArgs args_of(SharedState &sh) {
 // ---------------------------------------------------------------------------------------------
 // first read: a chain SRC -> n0 -> ... -> n(L-1) -> SINK
 // ---------------------------------------------------------------------------------------------
-__device__ int init_chain(SharedState &sh, const uint8_t *q, int L, int lane, int &n) {
+__device__ __forceinline__ int init_chain(SharedState &sh, const uint8_t *q, int L, int lane, int &n) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
     if (L + 2 > a.caps.NC) return kStCap;
@@ -273,7 +298,7 @@ __device__ int init_chain(SharedState &sh, const uint8_t *q, int L, int lane, in
 // row descriptors + remain (heaviest out-edge path length to the sink), 64-row chunks from the end
 // desc[r] = {node, base | far<<8 | pre_n<<16, remain, pre_row[0..4]}
 // ---------------------------------------------------------------------------------------------
-__device__ void build_desc(SharedState &sh, int n, int lane) {
+__device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
     const int nch = (n + kWave - 1) / kWave;
@@ -632,8 +657,8 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
             const int G1b = vbb ? H0b + e1 * j1 : IDENT;
             const int G2a = va ? H0a + e2 * j0 : IDENT;
             const int G2b = vbb ? H0b + e2 * j1 : IDENT;
-            const int inc1 = dpp_incl_max(max(G1a, G1b), IDENT);
-            const int inc2 = dpp_incl_max(max(G2a, G2b), IDENT);
+            int inc1 = max(G1a, G1b), inc2 = max(G2a, G2b);
+            dpp_incl_max2(inc1, inc2);
             const int ex1 = dpp_shr1(inc1, IDENT);
             const int ex2 = dpp_shr1(inc2, IDENT);
             const int P1a = max(ex1, carry1), P1b = max(P1a, G1a);
@@ -826,8 +851,8 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
     const int G1b = vbb ? H0b + e1 * j1 : IDENT;
     const int G2a = va ? H0a + e2 * j0 : IDENT;
     const int G2b = vbb ? H0b + e2 * j1 : IDENT;
-    const int inc1 = dpp_incl_max(max(G1a, G1b), IDENT);
-    const int inc2 = dpp_incl_max(max(G2a, G2b), IDENT);
+    int inc1 = max(G1a, G1b), inc2 = max(G2a, G2b);
+    dpp_incl_max2(inc1, inc2);
     const int carry1 = kNegInf + oe1 + e1 * (beg - 1);
     const int carry2 = kNegInf + oe2 + e2 * (beg - 1);
     const int P1a = max(dpp_shr1(inc1, IDENT), carry1), P1b = max(P1a, G1a);
@@ -909,7 +934,7 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
 // returns the start row of the backtrack in bi_out (or -1)
 // ---------------------------------------------------------------------------------------------
 template <class SC>
-__device__ int run_dp(SharedState &sh, const SC &sc, const uint8_t *q, int qlen,
+__device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8_t *q, int qlen,
                       int n, int lane, int64_t &cells, int &bi_out) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
@@ -988,57 +1013,231 @@ __device__ int run_dp(SharedState &sh, const SC &sc, const uint8_t *q, int qlen,
 }
 
 // ---------------------------------------------------------------------------------------------
-// backtrack (lane 0): fills qnode[q] = aligned node or -1 (insertion) for q in [0, qlen)
+// backtrack: fills qnode[q] = aligned node or -1 (insertion) for q in [0, qlen)
 // row record: rinfo[r] = {beg, end, argmax, soff, tbbase, kpbase, node, pre_n}
+//
+// The walk is inherently serial, so its cost is the latency chain per step.  Walking HBM directly
+// costs three dependent global loads per step (row record -> traceback byte -> predecessor byte).
+// Instead the wave copies a window of up to 64 rows -- their records, predecessor lists and the
+// contiguous traceback / predecessor-byte ranges the DP allocated for them -- into LDS with a few
+// wide loads, and the walk then touches LDS only.  Rows are allocated in DP order, so the rows
+// [i-63, i] occupy one contiguous byte range of each array.
+// E states are resolved lazily: state E at row i means "at E_out[i][j]", and the open/extend bit
+// is read from row i itself, so every step reads only the current row's window entry.
 // ---------------------------------------------------------------------------------------------
-__device__ int backtrack(SharedState &sh, int bi, int qlen, int n) {
+constexpr int kKpWin = kQLds / 2;  // predecessor-byte window (shares the read's LDS staging buffer)
+constexpr int kKpNone = -2147483647 - 1;
+
+struct BtWin {
+    int lo, hi, glob;  // rows [lo, hi] are in the window; glob: single row read from HBM
+};
+
+__device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i, int lane, BtWin &w) {
+    const int rr = i - lane;
+    const bool valid = rr >= 0;
+    int4 ra = make_int4(0, -1, 0, 0), rb = make_int4(0, 0, 0, 0), da = make_int4(0, 0, 0, 0),
+         db = make_int4(0, 0, 0, 0);
+    if (valid) {
+        const GLB int4 *ri = reinterpret_cast<const GLB int4 *>(s.rinfo + (int64_t)rr * kRowInfoInts);
+        const GLB int4 *di = reinterpret_cast<const GLB int4 *>(s.desc + (int64_t)rr * kDescInts);
+        ra = make_int4(ri[0].x, ri[0].y, ri[0].z, ri[0].w);
+        rb = make_int4(ri[1].x, ri[1].y, ri[1].z, ri[1].w);
+        da = make_int4(di[0].x, di[0].y, di[0].z, di[0].w);
+        db = make_int4(di[1].x, di[1].y, di[1].z, di[1].w);
+    }
+    const int beg = ra.x, end = ra.y, tbbase = rb.x, kpbase = rb.y, node = rb.z, pn = rb.w;
+    const int cb0 = beg & ~1;
+    const int tbw = (end - cb0 + 1 + 3) & ~3;
+    const bool multi = valid && pn > 1;
+    const int tstart = tbbase + cb0, tend = tstart + tbw;
+    const int kstart = kpbase + 3 * cb0, kend = kstart + 3 * tbw;
+    const int TE = readlane(tend, 0);
+    const unsigned long long mm = __ballot(multi);
+    const int fm = mm ? __ffsll((long long)mm) - 1 : 0;
+    const int KE = readlane(kend, fm);
+    const bool fit = valid && TE - (tstart & ~15) <= kTbWin && (!multi || KE - (kstart & ~15) <= kKpWin);
+    const unsigned long long nf = ~__ballot(fit);
+    const int cnt = nf ? __ffsll((long long)nf) - 1 : kWave;
+    int *md = &sh.desc[lane][0];
+    if (cnt == 0) {
+        // row i alone does not fit: read it from HBM
+        if (lane == 0) {
+            md[0] = tbbase;
+            md[1] = multi ? kpbase : kKpNone;
+            md[2] = node;
+            md[3] = da.w;
+            md[4] = db.x;
+            md[5] = db.y;
+            md[6] = db.z;
+            md[7] = db.w;
+        }
+        w.lo = w.hi = i;
+        w.glob = 1;
+        wave_sync();
+        return;
+    }
+    const int rs16 = readlane(tstart, cnt - 1) & ~15;
+    const unsigned long long mw = mm & ((cnt == kWave) ? ~0ull : ((1ull << cnt) - 1));
+    const int lm = mw ? 63 - __clzll((long long)mw) : 0;
+    const int ks16 = readlane(kstart, lm) & ~15;
+    const int tsz = TE - rs16, ksz = mw ? KE - ks16 : 0;
+    // wide copies: all loads first, then the LDS stores (one HBM round trip)
+    constexpr int kTU = kTbWin / (16 * kWave), kKU = kKpWin / (16 * kWave);
+    const GLB int4 *tg = reinterpret_cast<const GLB int4 *>(s.tb + rs16);
+    const GLB int4 *kg = reinterpret_cast<const GLB int4 *>(s.kp + ks16);
+    int4 tv[kTU], kv[kKU];
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+        const int x = u * kWave + lane;
+        if (x * 16 < tsz) tv[u] = make_int4(tg[x].x, tg[x].y, tg[x].z, tg[x].w);
+    }
+#pragma unroll
+    for (int u = 0; u < kKU; ++u) {
+        const int x = u * kWave + lane;
+        if (x * 16 < ksz) kv[u] = make_int4(kg[x].x, kg[x].y, kg[x].z, kg[x].w);
+    }
+    int4 *tl = reinterpret_cast<int4 *>(sh.tbwin);
+    int4 *kl = reinterpret_cast<int4 *>(sh.qnib);
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+        const int x = u * kWave + lane;
+        if (x * 16 < tsz) tl[x] = tv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kKU; ++u) {
+        const int x = u * kWave + lane;
+        if (x * 16 < ksz) kl[x] = kv[u];
+    }
+    if (lane < cnt) {
+        md[0] = tbbase - rs16;
+        md[1] = multi ? kpbase - ks16 : kKpNone;
+        md[2] = node;
+        md[3] = da.w;
+        md[4] = db.x;
+        md[5] = db.y;
+        md[6] = db.z;
+        md[7] = db.w;
+    }
+    w.lo = i - cnt + 1;
+    w.hi = i;
+    w.glob = 0;
+    wave_sync();
+}
+
+// One walk step read straight from HBM (rows too wide for the window, > kPreInline predecessors).
+__device__ __forceinline__ void bt_step_global(const PoaKArgs &a, const Slot &s, int &i, int &j, int &st) {
+    const gint *rb = s.rinfo + (int64_t)i * kRowInfoInts;
+    const int tbbase = rb[4], kpbase = rb[5], node = rb[6], pn = rb[7];
+    const int t = s.tb[tbbase + j];
+    if (st == 1 || st == 2) {
+        if (t & (st == 1 ? kTbE1Open : kTbE2Open)) {
+            st = 0;
+            return;
+        }
+    }
+    const int ty = st == 0 ? (t & kTbTypeMask) : st;
+    if (ty <= 2) {
+        const int k = (pn > 1) ? s.kp[kpbase + 3 * j + ty] : 0;
+        const int p = (k < kPreInline) ? s.desc[(int64_t)i * kDescInts + 3 + k] : s.pos[in_list(s, a, node)[k]];
+        if (ty == 0) {
+            s.qnode[j - 1] = node;
+            --j;
+        }
+        st = ty;
+        i = p;
+        return;
+    }
+    s.qnode[j - 1] = -1;
+    const int tprev = s.tb[tbbase + j - 1];
+    st = (tprev & (ty == 3 ? kTbF1OpenNext : kTbF2OpenNext)) ? 0 : ty;
+    --j;
+}
+
+// One walk step from the LDS window, branch-free (every lane computes the same step).  A step that
+// cannot be served from the window sets `stall` and changes nothing; finished walks are no-ops.
+__device__ __forceinline__ void bt_step_lds(const SharedState &sh, const Slot &s, int wlo, int whi, int &i,
+                                            int &j, int &st, int &stall) {
+    const bool live = i > 0 && j > 0 && !stall;
+    const bool inwin = i >= wlo;
+    const int idx = min(max(whi - i, 0), kWave - 1);
+    const int4 m0 = *reinterpret_cast<const int4 *>(&sh.desc[idx][0]);
+    const int4 m1 = *reinterpret_cast<const int4 *>(&sh.desc[idx][4]);
+    const int woff = m0.x, kof = m0.y, node = m0.z;
+    const int tix = max(woff + j, 1);
+    const int t = sh.tbwin[tix], tprev = sh.tbwin[tix - 1];
+    const bool multi = kof != kKpNone;
+    const int kix = multi ? kof + 3 * j : 0;
+    const int k0 = sh.qnib[kix], k1 = sh.qnib[kix + 1], k2 = sh.qnib[kix + 2];
+    const bool isE = st == 1 || st == 2;
+    const bool open = isE && (t & (st == 1 ? kTbE1Open : kTbE2Open));
+    const int ty = st == 0 ? (t & kTbTypeMask) : st;
+    const bool mv = !open && ty <= 2;
+    const int k = multi ? (ty == 0 ? k0 : (ty == 1 ? k1 : k2)) : 0;
+    const int p = k == 0 ? m0.w : (k == 1 ? m1.x : (k == 2 ? m1.y : (k == 3 ? m1.z : m1.w)));
+    const bool blocked = !inwin || (mv && k >= kPreInline);
+    const bool go = live && !blocked;
+    stall |= (int)(live && blocked);
+    const bool isF = !open && ty >= 3;
+    const bool wr = go && ((mv && ty == 0) || isF);
+    if (wr) s.qnode[j - 1] = mv ? node : -1;
+    const int fopen = tprev & (ty == 3 ? kTbF1OpenNext : kTbF2OpenNext);
+    const int nst = open ? 0 : (mv ? ty : (fopen ? 0 : ty));
+    const int ni = mv ? p : i;
+    const int nj = j - (int)((mv && ty == 0) || isF);
+    i = go ? ni : i;
+    j = go ? nj : j;
+    st = go ? nst : st;
+}
+
+__device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int n, int lane) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
-    int i = bi, j = qlen, st = 0;  // 0 H, 1 E1, 2 E2, 3 F1, 4 F2
-    int guard = n + qlen + 8;
+    int i = bi, j = qlen, st = 0;  // 0 H, 1 E1 (at E1out[i][j]), 2 E2, 3 F1, 4 F2
+    constexpr int kUnroll = 8;
+    int guard = (2 * (n + qlen) + 8) / kUnroll + 2 * (n + qlen) + 8;
+    BtWin w{1, 0, 0};
+    int glob_row = -1;
     while (i > 0 && j > 0) {
         if (--guard < 0) return kStInternal;
-        const gint *rb = s.rinfo + (int64_t)i * kRowInfoInts;
-        const int64_t tbbase = rb[4], kpbase = rb[5];
-        const int node = rb[6], pn = rb[7];
-        const int t = s.tb[tbbase + j];
-        if (st == 0) {
-            const int ty = t & kTbTypeMask;
-            if (ty <= 2) {
-                const int k = (pn > 1) ? s.kp[kpbase + 3 * (int64_t)j + ty] : 0;
-                const int p = (k < kPreInline) ? s.desc[(int64_t)i * kDescInts + 3 + k]
-                                               : s.pos[in_list(s, a, node)[k]];
-                if (ty == 0) {
-                    s.qnode[j - 1] = node;
-                    i = p;
-                    --j;
-                } else {
-                    const int ptb = s.rinfo[(int64_t)p * kRowInfoInts + 4];
-                    const int tp = s.tb[(int64_t)ptb + j];
-                    st = (tp & (ty == 1 ? kTbE1Open : kTbE2Open)) ? 0 : ty;
-                    i = p;
-                }
-                continue;
-            }
-            st = ty;  // 3 or 4: handled below in the same step
-        }
-        if (st == 1 || st == 2) {
-            const int k = (pn > 1) ? s.kp[kpbase + 3 * (int64_t)j + st] : 0;
-            const int p = (k < kPreInline) ? s.desc[(int64_t)i * kDescInts + 3 + k]
-                                           : s.pos[in_list(s, a, node)[k]];
-            const int ptb = s.rinfo[(int64_t)p * kRowInfoInts + 4];
-            const int tp = s.tb[(int64_t)ptb + j];
-            st = (tp & (st == 1 ? kTbE1Open : kTbE2Open)) ? 0 : st;
-            i = p;
+        if (i == glob_row) {
+            bt_step_global(a, s, i, j, st);
+            i = bcast0(i);
+            j = bcast0(j);
+            st = bcast0(st);
             continue;
         }
-        // F1 / F2: query base j-1 is an insertion at row i
-        s.qnode[j - 1] = -1;
-        const int tprev = s.tb[tbbase + j - 1];
-        st = (tprev & (st == 3 ? kTbF1OpenNext : kTbF2OpenNext)) ? 0 : st;
-        --j;
+        if (i < w.lo || i > w.hi) {
+            const uint64_t c0 = a.prof ? clock64() : 0;
+            bt_refill(sh, s, i, lane, w);
+            if (a.prof && lane == 0) {
+                int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
+                pf[12] += (int64_t)(clock64() - c0);
+                pf[13] += 1;
+            }
+            if (w.glob) {
+                glob_row = i;
+                w.lo = 1;
+                w.hi = 0;
+                continue;
+            }
+        }
+        int stall = 0;
+        int vi = i, vj = j, vst = st;
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) bt_step_lds(sh, s, w.lo, w.hi, vi, vj, vst, stall);
+        if (a.prof && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 14] += 1;
+        i = bcast0(vi);
+        j = bcast0(vj);
+        st = bcast0(vst);
+        if (bcast0(stall) && i >= w.lo && i <= w.hi && i > 0 && j > 0) {
+            // in the window but more than kPreInline predecessors: one step from HBM
+            bt_step_global(a, s, i, j, st);
+            i = bcast0(i);
+            j = bcast0(j);
+            st = bcast0(st);
+        }
     }
-    for (int t = 0; t < j; ++t) s.qnode[t] = -1;
+    for (int t = lane; t < j; t += kWave) s.qnode[t] = -1;
     return kStOk;
 }
 
@@ -1070,7 +1269,7 @@ __device__ __forceinline__ int add_edge(const PoaKArgs &a, Slot &s, int from, in
     return kStOk;
 }
 
-__device__ int update_graph(SharedState &sh, const uint8_t *q, int qlen, int &n,
+__device__ __forceinline__ int update_graph(SharedState &sh, const uint8_t *q, int qlen, int &n,
                             int &ng, int lane) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
@@ -1243,7 +1442,7 @@ __device__ int update_graph(SharedState &sh, const uint8_t *q, int qlen, int &n,
 // ---------------------------------------------------------------------------------------------
 // heaviest bundling (lane 0): reverse topological sweep, then walk from the source
 // ---------------------------------------------------------------------------------------------
-__device__ int consensus(SharedState &sh, int n, uint8_t *out, int64_t cap,
+__device__ __forceinline__ int consensus(SharedState &sh, int n, uint8_t *out, int64_t cap,
                          int &len) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
@@ -1382,9 +1581,7 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
                 }
                 wave_sync();
                 uint64_t t3 = prof ? clock64() : 0;
-                int bst = kStOk;
-                if (lane == 0) bst = backtrack(sh, bi, qlen, n);
-                st = bcast0(bst);
+                st = backtrack(sh, bi, qlen, n, lane);
                 if (st != kStOk) break;
                 wave_sync();
                 uint64_t t4 = prof ? clock64() : 0;
