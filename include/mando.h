@@ -112,6 +112,65 @@ int mando_selftest(mando_ctx *ctx, int *bad);
 int mando_mt_permutation(uint32_t seed, const int64_t *ns, const int64_t *ks, int64_t n_draws,
                          int64_t *out, int64_t out_cap);
 
+/* ------------------------------------------------------------------------------------------------
+ * Per-locus read clustering (host C++, one locus per worker thread).  Replaces the clustering half of
+ * process_locus (/root/reference/defineIsoforms.py:55-91 -> SpliceDefineConsensus.py:278-868) and the
+ * subsample draw of determine_consensus (SpliceDefineConsensus.py:884-888).  Every locus replays the
+ * numpy legacy RNG stream of RandomState(seed), which is what each forked locus worker of the
+ * reference sees when its parent seeded numpy (defineIsoforms.py:130).
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct {
+    double cutoff;              /* -c, find_peaks proportion cutoff (0.1) */
+    int32_t splice_site_width;  /* -w (1) */
+    int32_t minimum_read_count; /* -m (2) */
+    int32_t upstream_buffer;    /* -u (10) */
+    int32_t downstream_buffer;  /* -d (50) */
+    const char *junctions;      /* -j, comma separated ("gtag,gcag,atac,ctac,ctgc,gtat") */
+    uint32_t seed;              /* numpy global RNG seed every locus starts from */
+    int32_t threads;            /* host worker threads (0 = all hardware threads) */
+    int32_t poa_subsample;      /* determine_consensus subsample size (100) */
+} mando_cluster_params;
+
+typedef struct mando_cluster_result mando_cluster_result;
+
+/* Flat, read-only view of a clustering result (arrays owned by the result). */
+typedef struct {
+    int64_t n_loci;
+    const int32_t *locus_status;   /* 0 ok; -10 ZeroDivisionError, -11 KeyError (strand), -12 parse,
+                                      -13 I/O, -15 ValueError -- the reference's locus exceptions */
+    const char *text;              /* all locus files, concatenated */
+    int64_t text_len;
+    int64_t n_records;             /* PSL lines, locus by locus in file order */
+    const int64_t *name_off;       /* qName (col 9) of each record: text + name_off[r], name_len[r] */
+    const int32_t *name_len;
+    const int64_t *seq_off;        /* sequence (col 23) */
+    const int32_t *seq_len;
+    const int64_t *rec_locus;
+    int64_t n_isoforms;            /* locus by locus, IsoDict order inside a locus */
+    const int64_t *iso_locus;
+    const int64_t *mem_off;        /* n_isoforms+1: member records (IsoDict read order) */
+    const int64_t *mem;
+    const int64_t *sub_off;        /* n_isoforms+1: determine_consensus subsample, draw order */
+    const int64_t *sub;
+    int64_t n_peaks;               /* accepted splice-site bins (make_genome_bins + find_peaks rows) */
+    const int64_t *peak_locus;
+    const int64_t *peak_start;
+    const int64_t *peak_end;
+    const char *peak_type;         /* '5' / '3' */
+    const char *peak_side;         /* 'l' / 'r' */
+    const double *peak_prop;       /* round(prop, 3), -1 for annotated ('A') bins */
+} mando_cluster_view;
+
+void mando_cluster_default_params(mando_cluster_params *p);
+/* psl_paths[i]: locus file tmp_SS/<chrom~start~end>.psl; chroms[i]: its chrom.  Annotated splice
+ * bounds inside the locus (defineIsoforms.py:140-150) as 4 lists per locus (left '5', left '3',
+ * right '5', right '3'): ann_pos[ann_off[4i+s] .. ann_off[4i+s+1]); both may be NULL. */
+int mando_cluster_loci(const mando_cluster_params *params, const char *const *psl_paths,
+                       const char *const *chroms, int64_t n_loci, const int64_t *ann_pos,
+                       const int64_t *ann_off, mando_cluster_result **out);
+int mando_cluster_view_get(const mando_cluster_result *res, mando_cluster_view *view);
+void mando_cluster_free(mando_cluster_result *res);
+
 #ifdef __cplusplus
 }
 #endif

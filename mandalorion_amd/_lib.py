@@ -30,6 +30,10 @@ EXPORTED = (
     "mando_orient_batch",
     "mando_selftest",
     "mando_mt_permutation",
+    "mando_cluster_default_params",
+    "mando_cluster_loci",
+    "mando_cluster_view_get",
+    "mando_cluster_free",
 )
 
 STATUS = {
@@ -75,6 +79,56 @@ class PoaParams(ctypes.Structure):
         return p
 
 
+class ClusterParams(ctypes.Structure):
+    """mando_cluster_params — defaults are Mando.py's D-module arguments (Mando.py:382-399)."""
+
+    _fields_ = [
+        ("cutoff", ctypes.c_double),
+        ("splice_site_width", ctypes.c_int32),
+        ("minimum_read_count", ctypes.c_int32),
+        ("upstream_buffer", ctypes.c_int32),
+        ("downstream_buffer", ctypes.c_int32),
+        ("junctions", ctypes.c_char_p),
+        ("seed", ctypes.c_uint32),
+        ("threads", ctypes.c_int32),
+        ("poa_subsample", ctypes.c_int32),
+    ]
+
+    @classmethod
+    def defaults(cls) -> "ClusterParams":
+        p = cls()
+        load().mando_cluster_default_params(ctypes.byref(p))
+        return p
+
+
+class ClusterView(ctypes.Structure):
+    _fields_ = [
+        ("n_loci", ctypes.c_int64),
+        ("locus_status", ctypes.POINTER(ctypes.c_int32)),
+        ("text", ctypes.c_void_p),
+        ("text_len", ctypes.c_int64),
+        ("n_records", ctypes.c_int64),
+        ("name_off", ctypes.POINTER(ctypes.c_int64)),
+        ("name_len", ctypes.POINTER(ctypes.c_int32)),
+        ("seq_off", ctypes.POINTER(ctypes.c_int64)),
+        ("seq_len", ctypes.POINTER(ctypes.c_int32)),
+        ("rec_locus", ctypes.POINTER(ctypes.c_int64)),
+        ("n_isoforms", ctypes.c_int64),
+        ("iso_locus", ctypes.POINTER(ctypes.c_int64)),
+        ("mem_off", ctypes.POINTER(ctypes.c_int64)),
+        ("mem", ctypes.POINTER(ctypes.c_int64)),
+        ("sub_off", ctypes.POINTER(ctypes.c_int64)),
+        ("sub", ctypes.POINTER(ctypes.c_int64)),
+        ("n_peaks", ctypes.c_int64),
+        ("peak_locus", ctypes.POINTER(ctypes.c_int64)),
+        ("peak_start", ctypes.POINTER(ctypes.c_int64)),
+        ("peak_end", ctypes.POINTER(ctypes.c_int64)),
+        ("peak_type", ctypes.POINTER(ctypes.c_char)),
+        ("peak_side", ctypes.POINTER(ctypes.c_char)),
+        ("peak_prop", ctypes.POINTER(ctypes.c_double)),
+    ]
+
+
 _lib = None
 _lock = threading.Lock()
 _P = ctypes.c_void_p
@@ -108,6 +162,12 @@ def load(path: str | None = None):
         lib.mando_last_kernel_launches.argtypes = [_P]
         lib.mando_orient_batch.argtypes = [_P, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
         lib.mando_mt_permutation.argtypes = [ctypes.c_uint32, _P, _P, _I64, _P, _I64]
+        lib.mando_cluster_default_params.argtypes = [_P]
+        lib.mando_cluster_default_params.restype = None
+        lib.mando_cluster_loci.argtypes = [_P, _P, _P, _I64, _P, _P, _P]
+        lib.mando_cluster_view_get.argtypes = [_P, _P]
+        lib.mando_cluster_free.argtypes = [_P]
+        lib.mando_cluster_free.restype = None
         if hasattr(lib, "mando_selftest"):
             lib.mando_selftest.argtypes = [_P, _P]
         if path is None:

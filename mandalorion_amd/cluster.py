@@ -1,0 +1,147 @@
+"""Per-locus read clustering (libmando `mando_cluster_loci`, host C++ threads).
+
+Replaces the clustering half of the reference's `process_locus`
+(/root/reference/defineIsoforms.py:55-91: collect_reads, make_genome_bins, find_peaks,
+sort_reads_into_splice_junctions, define_start_end_sites) plus the subsample draw of
+`determine_consensus` (/root/reference/utils/SpliceDefineConsensus.py:884-888).  Each locus replays the
+numpy RNG stream of `RandomState(seed)`, i.e. what every forked locus worker of the reference sees when
+the parent seeded numpy before `mp.Pool` (defineIsoforms.py:130).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+STATUS = {0: "ok", -10: "ZeroDivisionError", -11: "KeyError", -12: "parse error", -13: "I/O error",
+          -14: "IndexError", -15: "ValueError"}
+
+
+@dataclass
+class Peak:
+    start: int
+    end: int
+    type: str
+    side: str
+    prop: float  # -1.0 for annotated bins ('A')
+
+    @property
+    def prop_str(self) -> str:
+        """str(proportion) as the reference writes it (toWrite[5])."""
+        return "A" if self.prop < 0 else repr(float(self.prop))
+
+
+def _arr(p, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(p, shape=(n,)).copy()
+
+
+class ClusterResult:
+    """Owns a mando_cluster_result; arrays are copied out, the text buffer is viewed in place."""
+
+    def __init__(self, handle: ctypes.c_void_p):
+        self._lib = _lib.load()
+        self._h = handle
+        v = _lib.ClusterView()
+        _lib.check(self._lib.mando_cluster_view_get(handle, ctypes.byref(v)))
+        self.n_loci = v.n_loci
+        self.n_records = v.n_records
+        self.locus_status = _arr(v.locus_status, v.n_loci, np.int32)
+        self.text = (np.ctypeslib.as_array(ctypes.cast(v.text, ctypes.POINTER(ctypes.c_uint8)), shape=(v.text_len,))
+                     if v.text_len else np.zeros(0, dtype=np.uint8))
+        n = v.n_records
+        self.name_off = _arr(v.name_off, n, np.int64)
+        self.name_len = _arr(v.name_len, n, np.int32)
+        self.seq_off = _arr(v.seq_off, n, np.int64)
+        self.seq_len = _arr(v.seq_len, n, np.int32)
+        self.rec_locus = _arr(v.rec_locus, n, np.int64)
+        ni = v.n_isoforms
+        self.iso_locus = _arr(v.iso_locus, ni, np.int64)
+        self.mem_off = _arr(v.mem_off, ni + 1, np.int64)
+        self.mem = _arr(v.mem, int(self.mem_off[-1]), np.int64)
+        self.sub_off = _arr(v.sub_off, ni + 1, np.int64)
+        self.sub = _arr(v.sub, int(self.sub_off[-1]), np.int64)
+        npk = v.n_peaks
+        self.peak_locus = _arr(v.peak_locus, npk, np.int64)
+        self.peak_start = _arr(v.peak_start, npk, np.int64)
+        self.peak_end = _arr(v.peak_end, npk, np.int64)
+        self.peak_type = bytes(_arr(v.peak_type, npk, np.uint8)).decode() if npk else ""
+        self.peak_side = bytes(_arr(v.peak_side, npk, np.uint8)).decode() if npk else ""
+        self.peak_prop = _arr(v.peak_prop, npk, np.float64)
+        self._raw = self.text.tobytes() if v.text_len else b""
+
+    def close(self):
+        if self._h is not None:
+            self._lib.mando_cluster_free(self._h)
+            self._h = None
+            self.text = np.zeros(0, dtype=np.uint8)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def n_isoforms(self) -> int:
+        return len(self.iso_locus)
+
+    def name(self, r: int) -> str:
+        a = int(self.name_off[r])
+        return self._raw[a:a + int(self.name_len[r])].decode()
+
+    def seq(self, r: int) -> str:
+        a = int(self.seq_off[r])
+        return self._raw[a:a + int(self.seq_len[r])].decode()
+
+    def members(self, i: int) -> np.ndarray:
+        return self.mem[self.mem_off[i]:self.mem_off[i + 1]]
+
+    def subsample(self, i: int) -> np.ndarray:
+        return self.sub[self.sub_off[i]:self.sub_off[i + 1]]
+
+    def peaks(self, locus: int) -> list[Peak]:
+        idx = np.nonzero(self.peak_locus == locus)[0]
+        return [Peak(int(self.peak_start[k]), int(self.peak_end[k]), self.peak_type[k], self.peak_side[k],
+                     float(self.peak_prop[k])) for k in idx]
+
+
+def cluster_loci(paths: list[str], chroms: list[str], ann: list[list[list[int]]] | None = None,
+                 cutoff: float = 0.1, splice_site_width: int = 1, minimum_read_count: int = 2,
+                 upstream_buffer: int = 10, downstream_buffer: int = 50,
+                 junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", seed: int = 0, threads: int = 0,
+                 poa_subsample: int = 100) -> ClusterResult:
+    """Cluster every locus file.  ann[i] = [left '5', left '3', right '5', right '3'] position lists."""
+    lib = _lib.load()
+    p = _lib.ClusterParams()
+    lib.mando_cluster_default_params(ctypes.byref(p))
+    p.cutoff = cutoff
+    p.splice_site_width = splice_site_width
+    p.minimum_read_count = minimum_read_count
+    p.upstream_buffer = upstream_buffer
+    p.downstream_buffer = downstream_buffer
+    jb = junctions.encode()
+    p.junctions = jb
+    p.seed = seed & 0xFFFFFFFF
+    p.threads = threads
+    p.poa_subsample = poa_subsample
+    n = len(paths)
+    cpaths = (ctypes.c_char_p * max(n, 1))(*[x.encode() for x in paths])
+    cchroms = (ctypes.c_char_p * max(n, 1))(*[x.encode() for x in chroms])
+    ann_pos = ann_off = None
+    if ann is not None:
+        flat, off = [], [0]
+        for i in range(n):
+            for s in range(4):
+                flat.extend(int(v) for v in ann[i][s])
+                off.append(len(flat))
+        ann_pos = np.asarray(flat if flat else [0], dtype=np.int64)
+        ann_off = np.asarray(off, dtype=np.int64)
+    h = ctypes.c_void_p()
+    _lib.check(lib.mando_cluster_loci(ctypes.byref(p), cpaths, cchroms, n, _lib.ptr(ann_pos), _lib.ptr(ann_off),
+                                      ctypes.byref(h)))
+    return ClusterResult(h)

@@ -1,0 +1,1039 @@
+// cluster.cpp — per-locus read clustering of the D module (host C++, one locus per worker thread).
+//
+// Restates, function by function, the clustering half of the reference's process_locus
+// (/root/reference/defineIsoforms.py:55-91) so that a locus produces the same splice-site peaks, the
+// same isoform groups in the same order, and the same RNG draws as the reference under a seeded
+// parent:
+//   collect_reads                      SpliceDefineConsensus.py:278-331
+//   make_genome_bins                   :392-438
+//   find_peaks / scan_for_best_bin     :232-275, :163-197
+//   determine_cov / myround            :200-224, :227-229
+//   characterize_splicing_event        :499-550   (RNG draw #1 per accepted candidate)
+//   getCSaroundSS                      :107-161   (tokenised once per read, then O(log L) per query)
+//   sort_reads_into_splice_junctions   :714-769
+//   group_mono_exon_transcripts        :772-794
+//   define_start_end_sites / find_ends :797-868, :554-711   (RNG draw #2 per identity)
+//   determine_consensus subsample      :884-888   (RNG draw #3 per isoform)
+// Python semantics reproduced on purpose: dict insertion order, stable sorts,
+// round-half-even myround, correctly rounded round(x, 3), negative-slice wrap in getCSaroundSS,
+// the dead branch of make_genome_bins, `identity.split('_')[1]`, `previous_end = end`, tuple order of
+// the mono-exon sort, and the ZeroDivisionError / KeyError cases (reported as a locus status).
+//
+// The reference spends 82 % of clustering in the per-base Python walk of getCSaroundSS;
+// here each cs string is tokenised once into (status, genome position) records and every junction
+// query is a binary search plus a 20-record window, so clustering is a small host cost next to the
+// GPU consensus and is not moved to the device (DESIGN.md "Clustering").
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/mando.h"
+#include "mt19937.h"
+
+namespace {
+
+using std::string;
+using std::string_view;
+using std::vector;
+
+// locus status codes (mando_cluster_view::locus_status)
+constexpr int kLocusOk = 0;
+constexpr int kLocusZeroDivision = -10;  // characterize_splicing_event: leftCS['Total'] == 0
+constexpr int kLocusKeyError = -11;      // scan_for_best_bin: strand column not '+' / '-'
+constexpr int kLocusParse = -12;         // malformed PSL line / cs string
+constexpr int kLocusIO = -13;            // file unreadable
+[[maybe_unused]] constexpr int kLocusIndexError = -14;  // host side: zero reads orient (IndexError)
+constexpr int kLocusValueError = -15;    // max() of an empty sequence in find_ends
+
+struct LocusError {
+    int code;
+};
+
+// ---------------------------------------------------------------------------------------------
+// parsing helpers
+// ---------------------------------------------------------------------------------------------
+int64_t to_i64(string_view s) {
+    // Python int(): optional surrounding whitespace, optional sign, decimal digits
+    size_t a = 0, b = s.size();
+    while (a < b && (s[a] == ' ' || s[a] == '\t' || s[a] == '\r' || s[a] == '\n')) ++a;
+    while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t' || s[b - 1] == '\r' || s[b - 1] == '\n')) --b;
+    if (a == b) throw LocusError{kLocusParse};
+    bool neg = false;
+    if (s[a] == '+' || s[a] == '-') {
+        neg = s[a] == '-';
+        ++a;
+    }
+    if (a == b) throw LocusError{kLocusParse};
+    int64_t v = 0;
+    for (size_t i = a; i < b; ++i) {
+        const char c = s[i];
+        if (c == '_' ) continue;
+        if (c < '0' || c > '9') throw LocusError{kLocusParse};
+        v = v * 10 + (c - '0');
+    }
+    return neg ? -v : v;
+}
+
+double to_f64(string_view s) {
+    string t(s);
+    char *end = nullptr;
+    const double v = strtod(t.c_str(), &end);  // glibc strtod is correctly rounded, like float()
+    if (end == t.c_str()) throw LocusError{kLocusParse};
+    return v;
+}
+
+// str.split(',')[:-1] of a PSL list column
+void split_list(string_view s, vector<int64_t> &out) {
+    out.clear();
+    size_t a = 0;
+    vector<string_view> parts;
+    while (true) {
+        const size_t c = s.find(',', a);
+        if (c == string_view::npos) {
+            parts.push_back(s.substr(a));
+            break;
+        }
+        parts.push_back(s.substr(a, c - a));
+        a = c + 1;
+    }
+    for (size_t i = 0; i + 1 < parts.size(); ++i) out.push_back(to_i64(parts[i]));
+}
+
+// Python round(x) (half-even) of x / 10 for integer x, times 10 (myround, SDC:227-229)
+inline int64_t myround(int64_t x) {
+    // x / 10 is exact at the .5 ties (k + 0.5 is representable), so the float round is half-even on
+    // the exact quotient.
+    int64_t q = x >= 0 ? x / 10 : -((-x + 9) / 10);
+    int64_t r = x - 10 * q;
+    if (r > 5 || (r == 5 && (q & 1))) ++q;
+    return 10 * q;
+}
+
+// Python round(x, 3): correctly rounded decimal, then back to double (glibc printf is exact)
+inline double py_round3(double x) {
+    char buf[64];
+    snprintf(buf, sizeof buf, "%.3f", x);
+    return strtod(buf, nullptr);
+}
+
+// ---------------------------------------------------------------------------------------------
+// records
+// ---------------------------------------------------------------------------------------------
+struct Record {
+    string_view name, dirn, chrom, cs, seq;
+    int64_t qsize = 0, qstart = 0, qend = 0, tstart = 0, tend = 0;
+    vector<int64_t> bsize, bstart;
+    double accuracy = 0;
+    int64_t global = 0;  // index in the batch
+};
+
+// line.strip().split('\t')
+void split_tabs(string_view line, vector<string_view> &f) {
+    f.clear();
+    size_t a = 0, b = line.size();
+    while (a < b && isspace((unsigned char)line[a])) ++a;
+    while (b > a && isspace((unsigned char)line[b - 1])) --b;
+    line = line.substr(a, b - a);
+    size_t p = 0;
+    while (true) {
+        const size_t t = line.find('\t', p);
+        if (t == string_view::npos) {
+            f.push_back(line.substr(p));
+            break;
+        }
+        f.push_back(line.substr(p, t - p));
+        p = t + 1;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// getCSaroundSS: tokenised cs string
+// ---------------------------------------------------------------------------------------------
+struct CsIndex {
+    vector<char> st;          // '=', '+', '-', '*', '|' (intron record)
+    vector<int64_t> pos;      // genome position after the record
+    vector<int32_t> intron;   // record index -> index into motif (introns only), else -1
+    vector<std::array<char, 4>> motif;
+    bool built = false;
+};
+
+bool is_op(char c) { return c == '\\' || c == '=' || c == '+' || c == '-' || c == '*' || c == '~'; }
+
+void build_cs(string_view cs, int64_t begin, CsIndex &ix) {
+    ix.st.clear();
+    ix.pos.clear();
+    ix.intron.clear();
+    ix.motif.clear();
+    int64_t g = begin;
+    size_t i = 0;
+    // re.split keeps text before the first operator as element 0, which the zip drops
+    while (i < cs.size() && !is_op(cs[i])) ++i;
+    while (i < cs.size()) {
+        const char op = cs[i++];
+        size_t j = i;
+        while (j < cs.size() && !is_op(cs[j])) ++j;
+        const string_view e = cs.substr(i, j - i);
+        i = j;
+        switch (op) {
+            case '=':
+            case '-':
+                for (size_t k = 0; k < e.size(); ++k) {
+                    ++g;
+                    ix.st.push_back(op);
+                    ix.pos.push_back(g);
+                    ix.intron.push_back(-1);
+                }
+                break;
+            case '+':
+                for (size_t k = 0; k < e.size(); ++k) {
+                    ix.st.push_back('+');
+                    ix.pos.push_back(g);
+                    ix.intron.push_back(-1);
+                }
+                break;
+            case '*':
+                for (size_t k = 0; k < e.size(); k += 2) {
+                    ++g;
+                    ix.st.push_back('*');
+                    ix.pos.push_back(g);
+                    ix.intron.push_back(-1);
+                }
+                break;
+            case '~': {
+                if (e.size() < 4) throw LocusError{kLocusParse};
+                g += to_i64(e.substr(2, e.size() - 4));
+                // record '|' + entry + '|'; bases = item[1:3] + item[-3:-1]
+                std::array<char, 4> m{e[0], e[1], e[e.size() - 2], e[e.size() - 1]};
+                ix.intron.push_back((int32_t)ix.motif.size());
+                ix.motif.push_back(m);
+                ix.st.push_back('|');
+                ix.pos.push_back(g);
+                break;
+            }
+            default:  // '\\' never occurs in a cs string; it would start an ignored record
+                break;
+        }
+    }
+    ix.built = true;
+}
+
+struct CsResult {
+    string bases;        // 4 chars, "nnnn" when no intron in the window
+    int cnt_l[6] = {0};  // '*','+','-','=','|' counts of `left` and Total
+    int cnt_r[6] = {0};
+    bool has_l = false, has_r = false;
+};
+
+inline int st_slot(char c) {
+    switch (c) {
+        case '*': return 0;
+        case '+': return 1;
+        case '-': return 2;
+        case '=': return 3;
+        default: return 4;  // '|'
+    }
+}
+
+void cs_around(const CsIndex &ix, int64_t start, int64_t end, CsResult &r) {
+    r.bases = "nnnn";
+    r.has_l = r.has_r = false;
+    std::fill(r.cnt_l, r.cnt_l + 6, 0);
+    std::fill(r.cnt_r, r.cnt_r + 6, 0);
+    const int64_t n = (int64_t)ix.st.size();
+    // last advancing record with start <= pos <= end ('+' records never set spliceIndex)
+    int64_t k = (int64_t)(std::upper_bound(ix.pos.begin(), ix.pos.end(), end) - ix.pos.begin()) - 1;
+    while (k >= 0 && ix.st[(size_t)k] == '+') --k;
+    if (k < 0 || ix.pos[(size_t)k] < start) return;
+    const int64_t si = k + 1;  // len(record) after appending record k
+    const int64_t lo = std::max<int64_t>(si - 10, 0), hi = std::min<int64_t>(si + 10, n);
+    int64_t idx = -1;
+    for (int64_t t = hi - 1; t >= lo; --t)
+        if (ix.st[(size_t)t] == '|') {
+            idx = t;
+            break;
+        }
+    if (idx < 0) return;
+    const auto &m = ix.motif[(size_t)ix.intron[(size_t)idx]];
+    r.bases.assign(m.begin(), m.end());
+    // left = record[idx-5:idx] with Python slice normalisation
+    int64_t a = idx - 5, b = idx;
+    if (a < 0) a += n;
+    if (a < 0) a = 0;
+    for (int64_t t = a; t < b && t < n; ++t) {
+        r.cnt_l[st_slot(ix.st[(size_t)t])]++;
+        r.cnt_l[5]++;
+        r.has_l = true;
+    }
+    // right = record[idx+1:idx+6]
+    for (int64_t t = idx + 1; t < std::min<int64_t>(idx + 6, n); ++t) {
+        r.cnt_r[st_slot(ix.st[(size_t)t])]++;
+        r.cnt_r[5]++;
+        r.has_r = true;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ordered dict helper (Python dict: insertion order)
+// ---------------------------------------------------------------------------------------------
+template <class V>
+struct OrderedMap {
+    vector<int64_t> keys;
+    vector<V> vals;
+    std::unordered_map<int64_t, size_t> idx;
+    V &at(int64_t k) {
+        auto it = idx.find(k);
+        if (it != idx.end()) return vals[it->second];
+        idx.emplace(k, keys.size());
+        keys.push_back(k);
+        vals.emplace_back();
+        return vals.back();
+    }
+    const V *find(int64_t k) const {
+        auto it = idx.find(k);
+        return it == idx.end() ? nullptr : &vals[it->second];
+    }
+};
+
+struct HistEntry {
+    int32_t rec;  // record index within the locus
+};
+
+struct Peak {
+    int64_t start, end;
+    char type, side;
+    double prop;  // -1 for annotated ('A')
+};
+
+struct Params {
+    double cutoff;
+    int w, min_count, up, down, sub_k;
+    vector<string> junctions;
+    uint32_t seed;
+};
+
+// ---------------------------------------------------------------------------------------------
+// one locus
+// ---------------------------------------------------------------------------------------------
+struct LocusOut {
+    int status = kLocusOk;
+    vector<Peak> peaks;
+    vector<vector<int32_t>> iso_members;  // record indices (locus-local), IsoDict order
+    vector<vector<int32_t>> iso_sub;      // subsample, in draw order
+};
+
+struct LocusIn {
+    string_view text;
+    string chrom;
+    vector<int64_t> ann[4];  // left '5', left '3', right '5', right '3'
+    int64_t rec_base = 0;
+};
+
+class LocusRunner {
+  public:
+    LocusRunner(const Params &p, const LocusIn &in, vector<Record> &recs, LocusOut &out)
+        : P(p), in(in), recs(recs), out(out), mt(p.seed) {}
+
+    void run() {
+        collect_reads();
+        std::unordered_set<int64_t> areas_l, areas_r;
+        vector<Peak> a_l, a_r, n_l, n_r;
+        make_genome_bins(in.ann[0], in.ann[1], 'l', areas_l, a_l);
+        make_genome_bins(in.ann[2], in.ann[3], 'r', areas_r, a_r);
+        find_peaks(hist_l, true, 'l', areas_l, n_l);
+        find_peaks(hist_r, false, 'r', areas_r, n_r);
+        // spliceDict (defineIsoforms.py:71-83): per-side counters, later rows overwrite
+        int counter[2] = {0, 0};
+        for (auto *tw : {&a_l, &a_r, &n_l, &n_r}) {
+            for (const Peak &pk : *tw) {
+                const int s = pk.side == 'l' ? 0 : 1;
+                counter[s] += 1;
+                const int32_t lab = (int32_t)labels.size();
+                labels.push_back(string(1, pk.type) + pk.side + std::to_string(counter[s]));
+                for (int64_t b = pk.start; b <= pk.end; ++b) splice[b] = lab;
+                out.peaks.push_back(pk);
+            }
+        }
+        sort_reads();
+        define_start_end_sites();
+        // determine_consensus subsample draw per isoform (SDC:884-888)
+        vector<int64_t> perm, pick;
+        for (auto &mem : out.iso_members) {
+            const int64_t n = (int64_t)mem.size();
+            mando::mt_choice(mt, n, std::min<int64_t>(n, P.sub_k), perm, pick);
+            vector<int32_t> sub;
+            sub.reserve(pick.size());
+            for (int64_t t : pick) sub.push_back(mem[(size_t)t]);
+            out.iso_sub.push_back(std::move(sub));
+        }
+    }
+
+  private:
+    const Params &P;
+    const LocusIn &in;
+    vector<Record> &recs;
+    LocusOut &out;
+    mando::MT19937 mt;
+
+    // collect_reads state
+    std::unordered_map<int64_t, int32_t> histo_cov;
+    OrderedMap<vector<HistEntry>> hist_l, hist_r;
+    vector<vector<int64_t>> cov_sets;                    // per record (rounded, unique, sorted)
+    std::unordered_map<string_view, int32_t> cs_dict;     // name -> last record
+    vector<CsIndex> cs_ix;
+    // spliceDict
+    std::unordered_map<int64_t, int32_t> splice;
+    vector<string> labels;
+    // sort_reads output
+    struct Pos {
+        int64_t start, end;
+        int32_t rec;
+        int64_t lx, rx;
+    };
+    std::map<string, int> ident_index_unused;
+    vector<string> ident_order;
+    std::unordered_map<string, vector<Pos>> se_dict;
+    vector<string> mono_order;
+    std::unordered_map<string, vector<Pos>> se_mono;
+
+    void collect_reads() {
+        const size_t n = recs.size();
+        cov_sets.resize(n);
+        cs_ix.resize(n);
+        for (size_t r = 0; r < n; ++r) {
+            Record &R = recs[r];
+            if (R.chrom != string_view(in.chrom)) continue;
+            cs_dict[R.name] = (int32_t)r;
+            std::unordered_set<int64_t> cs;
+            vector<int64_t> low, up;
+            int64_t y = -1;
+            bool y_set = false;
+            for (size_t x = 0; x < R.bsize.size(); ++x) {
+                const int64_t bs = R.bstart[x], sz = R.bsize[x], be = bs + sz;
+                for (int64_t t = 0; t < sz; t += 10) {
+                    cs.insert(myround(bs + t));
+                    y = t;
+                    y_set = true;
+                }
+                if (!y_set) throw LocusError{kLocusParse};  // NameError in the reference
+                for (int64_t t = y; t < sz; ++t) cs.insert(myround(bs + t));
+                if (bs != R.tstart) up.push_back(bs);
+                if (be != R.tend) low.push_back(be);
+            }
+            vector<int64_t> v(cs.begin(), cs.end());
+            std::sort(v.begin(), v.end());
+            for (int64_t b : v) histo_cov[b] += 1;
+            cov_sets[r] = std::move(v);
+            if (R.accuracy < 0.9) continue;
+            for (int64_t b : low) hist_l.at(b).push_back({(int32_t)r});
+            for (int64_t b : up) hist_r.at(b).push_back({(int32_t)r});
+        }
+    }
+
+    void make_genome_bins(const vector<int64_t> &b5, const vector<int64_t> &b3, char side,
+                          std::unordered_set<int64_t> &areas, vector<Peak> &tw) {
+        for (int ti = 0; ti < 2; ++ti) {
+            const char type = ti == 0 ? '5' : '3';
+            vector<int64_t> pl = ti == 0 ? b5 : b3;
+            std::stable_sort(pl.begin(), pl.end());
+            std::unordered_set<size_t> covered;
+            for (size_t i1 = 0; i1 < pl.size(); ++i1) {
+                if (covered.count(i1)) continue;
+                // sub_list starts with pl[i1] and the inner loop re-adds it (index2 = index1), so
+                // min(splice_dists) == 0 and the multi-bin branch (SDC:412-426) never runs
+                int64_t mx = pl[i1], mn = pl[i1];
+                for (size_t i2 = i1; i2 < pl.size(); ++i2) {
+                    if (pl[i2] - mx <= P.w) {
+                        mx = std::max(mx, pl[i2]);
+                        mn = std::min(mn, pl[i2]);
+                        covered.insert(i2);
+                    } else {
+                        break;
+                    }
+                }
+                Peak pk{mn - P.w, mx + P.w, type, side, -1.0};
+                tw.push_back(pk);
+                for (int64_t b = pk.start; b <= pk.end; ++b) areas.insert(b);
+            }
+        }
+    }
+
+    bool characterize(int64_t left, int64_t right, const vector<int32_t> &names) {
+        const int64_t n = (int64_t)names.size();
+        vector<int64_t> perm, pick;
+        mando::mt_choice(mt, n, std::min<int64_t>(n, 500), perm, pick);
+        int64_t allowed = 0, all = 0;
+        int64_t lc[6] = {0}, rc[6] = {0};
+        CsResult res;
+        for (int64_t t : pick) {
+            const string_view nm = recs[(size_t)names[(size_t)t]].name;
+            const int32_t ri = cs_dict.at(nm);
+            CsIndex &ix = cs_ix[(size_t)ri];
+            if (!ix.built) build_cs(recs[(size_t)ri].cs, recs[(size_t)ri].tstart, ix);
+            cs_around(ix, left, right, res);
+            all += 1;
+            for (const string &j : P.junctions)
+                if (res.bases == j) {
+                    allowed += 1;
+                    break;
+                }
+            if (res.has_l)
+                for (int s = 0; s < 6; ++s) lc[s] += res.cnt_l[s];
+            if (res.has_r)
+                for (int s = 0; s < 6; ++s) rc[s] += res.cnt_r[s];
+        }
+        if (all == 0) throw LocusError{kLocusZeroDivision};
+        bool basepass = (double)allowed / (double)all > 0.85;
+        if (!basepass) return false;
+        if (lc[5] == 0 || rc[5] == 0) throw LocusError{kLocusZeroDivision};
+        const double la = (double)lc[3] / (double)lc[5], ra = (double)rc[3] / (double)rc[5];
+        return la > 0.85 && ra > 0.85;
+    }
+
+    void find_peaks(OrderedMap<vector<HistEntry>> &dd, bool reverse, char side,
+                    std::unordered_set<int64_t> &areas, vector<Peak> &tw) {
+        vector<int64_t> dist{0};
+        for (int s = 1; s <= P.w; ++s) {
+            dist.push_back(s);
+            dist.push_back(-s);
+        }
+        vector<size_t> cand;
+        for (size_t i = 0; i < dd.keys.size(); ++i)
+            if ((int64_t)dd.vals[i].size() >= P.min_count) cand.push_back(i);
+        std::stable_sort(cand.begin(), cand.end(),
+                         [&](size_t a, size_t b) { return dd.vals[a].size() > dd.vals[b].size(); });
+        for (size_t ci : cand) {
+            const int64_t entry = dd.keys[ci];
+            if (areas.count(entry)) continue;
+            // scan_for_best_bin
+            int64_t best = 0, center = 0;
+            int64_t bdir_p = 0, bdir_m = 0;
+            vector<int32_t> best_names;
+            std::unordered_map<int64_t, int32_t> best_cov;
+            for (int64_t x : dist) {
+                bool called = false;
+                for (int64_t y : dist)
+                    if (areas.count(entry + x + y)) {
+                        called = true;
+                        break;
+                    }
+                if (called) continue;
+                int64_t cnt = 0, dp = 0, dm = 0;
+                vector<int32_t> names;
+                std::unordered_map<int64_t, int32_t> covc;
+                for (int64_t y : dist) {
+                    const vector<HistEntry> *lst = dd.find(entry + x + y);
+                    if (!lst) continue;
+                    for (const HistEntry &h : *lst) {
+                        cnt += 1;
+                        const string_view d = recs[(size_t)h.rec].dirn;
+                        if (d == "+")
+                            dp += 1;
+                        else if (d == "-")
+                            dm += 1;
+                        else
+                            throw LocusError{kLocusKeyError};
+                        names.push_back(h.rec);
+                        for (int64_t cp : cov_sets[(size_t)h.rec]) covc[cp] += 1;
+                    }
+                }
+                if (cnt > best) {
+                    best = cnt;
+                    best_names = std::move(names);
+                    center = entry + x;
+                    best_cov = std::move(covc);
+                    bdir_p = dp;
+                    bdir_m = dm;
+                }
+            }
+            // determine_cov
+            vector<int64_t> area2;
+            for (auto &kv : best_cov)
+                if (kv.second > 1) area2.push_back(kv.first);
+            if (reverse)
+                std::sort(area2.begin(), area2.end(), std::greater<int64_t>());
+            else
+                std::sort(area2.begin(), area2.end());
+            int64_t cov = 0;
+            int counter = 0;
+            for (int64_t bf : area2) {
+                const bool count = reverse ? bf < center : bf > center;
+                if (!count) continue;
+                if (counter <= 3) {
+                    counter += 1;
+                    auto it = histo_cov.find(myround(bf));
+                    if (it != histo_cov.end()) cov = std::max<int64_t>(cov, it->second);
+                } else {
+                    break;
+                }
+            }
+            if (cov <= 0) continue;
+            const double prop = py_round3((double)best / (double)cov);
+            if (!(prop > P.cutoff)) continue;
+            char type = 0;
+            if (bdir_p < bdir_m)
+                type = reverse ? '3' : '5';
+            else if (bdir_p > bdir_m)
+                type = reverse ? '5' : '3';
+            if (!type) continue;
+            if (characterize(center - P.w, center + P.w, best_names)) {
+                Peak pk{center - P.w, center + P.w, type, side, prop};
+                tw.push_back(pk);
+                for (int64_t b = pk.start; b <= pk.end; ++b) areas.insert(b);
+            }
+        }
+    }
+
+    void sort_reads() {
+        for (size_t r = 0; r < recs.size(); ++r) {
+            const Record &R = recs[r];
+            const int64_t lx = R.qstart, rx = R.qsize - R.qend;  // direction forced '+'
+            bool failed = false;
+            string ident(R.chrom);
+            ident += '_';
+            const bool chrom_known = R.chrom == string_view(in.chrom);
+            for (size_t x = 0; x + 1 < R.bsize.size(); ++x) {
+                const int64_t ls = R.bstart[x] + R.bsize[x], rs = R.bstart[x + 1];
+                if (rs - ls > 50) {
+                    if (!chrom_known) {
+                        failed = true;
+                        break;
+                    }
+                    auto a = splice.find(ls), b = splice.find(rs);
+                    if (a == splice.end() || b == splice.end()) {
+                        failed = true;
+                        break;
+                    }
+                    ident += labels[(size_t)a->second];
+                    ident += '-';
+                    ident += labels[(size_t)b->second];
+                    ident += '~';
+                }
+            }
+            if (failed) continue;
+            // identity.split('_')[1] != ''
+            const size_t u1 = ident.find('_');
+            const size_t u2 = ident.find('_', u1 + 1);
+            const bool spliced = (u2 == string::npos ? ident.size() : u2) > u1 + 1;
+            Pos p{R.tstart, R.tend, (int32_t)r, lx, rx};
+            if (spliced) {
+                auto it = se_dict.find(ident);
+                if (it == se_dict.end()) {
+                    ident_order.push_back(ident);
+                    se_dict[ident].push_back(p);
+                } else {
+                    it->second.push_back(p);
+                }
+            } else {
+                auto it = se_mono.find(ident);
+                if (it == se_mono.end()) {
+                    mono_order.push_back(ident);
+                    se_mono[ident].push_back(p);
+                } else {
+                    it->second.push_back(p);
+                }
+            }
+        }
+    }
+
+    // position tuple order: (start, end, (name, seq), left_extra, right_extra, '+')
+    bool pos_less(const Pos &a, const Pos &b) const {
+        if (a.start != b.start) return a.start < b.start;
+        if (a.end != b.end) return a.end < b.end;
+        const Record &A = recs[(size_t)a.rec], &B = recs[(size_t)b.rec];
+        if (A.name != B.name) return A.name < B.name;
+        if (A.seq != B.seq) return A.seq < B.seq;
+        if (a.lx != b.lx) return a.lx < b.lx;
+        return a.rx < b.rx;
+    }
+
+    void group_mono() {
+        for (const string &id : mono_order) {
+            vector<Pos> ps = se_mono[id];
+            std::stable_sort(ps.begin(), ps.end(), [&](const Pos &a, const Pos &b) { return pos_less(a, b); });
+            int64_t prev_end = 0;
+            int counter = 0;
+            string nid = id + "M0";
+            for (const Pos &p : ps) {
+                if (p.start > prev_end) {
+                    counter += 1;
+                    nid = id + "M" + std::to_string(counter);
+                    prev_end = std::max(p.end, prev_end);
+                } else {
+                    prev_end = p.end;
+                }
+                auto it = se_dict.find(nid);
+                if (it == se_dict.end()) {
+                    ident_order.push_back(nid);
+                    se_dict[nid].push_back(p);
+                } else {
+                    it->second.push_back(p);
+                }
+            }
+        }
+    }
+
+    // find_ends for one identity (SDC:554-711); peaks map position -> owning position
+    void find_ends(const vector<int64_t> &starts, const vector<int64_t> &ends,
+                   std::unordered_map<int64_t, int64_t> &sp, std::unordered_map<int64_t, int64_t> &ep) {
+        const int64_t up = P.up, down = P.down, mc = P.min_count;
+        std::unordered_map<int64_t, int64_t> sc, ec;
+        for (int64_t p : starts) sc[p] += 1;
+        for (int64_t p : ends) ec[p] += 1;
+        auto cnt = [](const std::unordered_map<int64_t, int64_t> &m, int64_t k) -> int64_t {
+            auto it = m.find(k);
+            return it == m.end() ? 0 : it->second;
+        };
+        vector<int64_t> ss = starts;
+        std::sort(ss.begin(), ss.end());
+        for (int64_t position : ss) {
+            if (sp.count(position - up)) continue;
+            int64_t wc = 0;
+            for (int64_t i = 0; i < 10; ++i) wc += cnt(sc, position + i);
+            if (wc < mc) continue;
+            int64_t ob_min = INT64_MAX, ob_max = INT64_MIN;
+            for (int64_t s = -up; s < down; ++s) {
+                sp[position + s] = position;
+                ob_min = std::min(ob_min, position + s);
+                ob_max = std::max(ob_max, position + s);
+            }
+            if (ob_min == INT64_MAX) throw LocusError{kLocusValueError};
+            int64_t best_bin = INT64_MIN;
+            for (int64_t i = ob_min; i < ob_max; ++i) {
+                int64_t b = 0;
+                for (int64_t s = 0; s < 10; ++s) b += cnt(sc, i + s);
+                best_bin = std::max(best_bin, b);
+            }
+            if (best_bin == INT64_MIN) throw LocusError{kLocusValueError};
+            extend(sp, sc, position, position - up, -1, best_bin, mc);
+            extend(sp, sc, position, position + down - 1, +1, best_bin, mc);
+        }
+        vector<int64_t> es = ends;
+        std::sort(es.begin(), es.end(), std::greater<int64_t>());
+        for (int64_t position : es) {
+            if (ep.count(position + up - 1)) continue;
+            int64_t wc = 0;
+            for (int64_t i = 0; i < 10; ++i) wc += cnt(ec, position - i);
+            if (wc < mc) continue;
+            int64_t ob_min = INT64_MAX, ob_max = INT64_MIN;
+            for (int64_t s = -down; s < up; ++s) {
+                ep[position + s] = position;
+                ob_min = std::min(ob_min, position + s);
+                ob_max = std::max(ob_max, position + s);
+            }
+            if (ob_min == INT64_MAX) throw LocusError{kLocusValueError};
+            int64_t best_bin = INT64_MIN;
+            for (int64_t i = ob_min; i < ob_max; ++i) {
+                int64_t b = 0;
+                for (int64_t s = 0; s < 10; ++s) b += cnt(ec, i + s);
+                best_bin = std::max(best_bin, b);
+            }
+            if (best_bin == INT64_MIN) throw LocusError{kLocusValueError};
+            extend(ep, ec, position, position - down, -1, best_bin, mc);
+            extend(ep, ec, position, position + up - 1, +1, best_bin, mc);
+        }
+    }
+
+    // one extension loop of find_ends (SDC:598-620 and mirrors): windows of 10 beyond `adjacent`
+    static void extend(std::unordered_map<int64_t, int64_t> &peaks, const std::unordered_map<int64_t, int64_t> &cnt,
+                       int64_t position, int64_t adjacent, int dir, int64_t best_bin, int64_t mc) {
+        bool extended = true;
+        while (extended) {
+            int64_t wc = 0;
+            int64_t adj[10];
+            for (int i = 1; i <= 10; ++i) {
+                adj[i - 1] = adjacent + dir * i;
+                auto it = cnt.find(adj[i - 1]);
+                if (it != cnt.end()) wc += it->second;
+            }
+            if (best_bin > wc && wc >= mc) {
+                for (int i = 0; i < 10; ++i) {
+                    if (!peaks.count(adj[i]))
+                        peaks[adj[i]] = position;
+                    else
+                        extended = false;
+                }
+            } else {
+                extended = false;
+            }
+            adjacent = adj[9];
+        }
+    }
+
+    void define_start_end_sites() {
+        group_mono();
+        vector<string> ids = ident_order;
+        std::sort(ids.begin(), ids.end());
+        int isoform_counter = 0;
+        std::map<std::tuple<string, int64_t, int64_t>, int> iso_of;
+        vector<int64_t> perm, pick;
+        for (const string &id : ids) {
+            const vector<Pos> &ps = se_dict[id];
+            const int64_t n = (int64_t)ps.size();
+            mando::mt_choice(mt, n, std::min<int64_t>(n, 10000), perm, pick);
+            vector<int64_t> starts, ends;
+            for (int64_t t : pick) {
+                starts.push_back(ps[(size_t)t].start);
+                ends.push_back(ps[(size_t)t].end);
+            }
+            std::unordered_map<int64_t, int64_t> sp, ep;
+            find_ends(starts, ends, sp, ep);
+            for (const Pos &p : ps) {
+                auto a = sp.find(p.start), b = ep.find(p.end);
+                if (a == sp.end() || b == ep.end()) continue;
+                auto key = std::make_tuple(id, a->second, b->second);
+                auto it = iso_of.find(key);
+                int iso;
+                if (it == iso_of.end()) {
+                    iso = isoform_counter++;
+                    iso_of.emplace(key, iso);
+                    out.iso_members.emplace_back();
+                } else {
+                    iso = it->second;
+                }
+                out.iso_members[(size_t)iso].push_back(p.rec);
+            }
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// batch
+// ---------------------------------------------------------------------------------------------
+void parse_locus(string_view text, int64_t base, vector<Record> &recs) {
+    size_t p = 0;
+    vector<string_view> f;
+    while (p < text.size()) {
+        size_t e = text.find('\n', p);
+        if (e == string_view::npos) e = text.size();
+        const string_view line = text.substr(p, e - p);
+        p = e + 1;
+        split_tabs(line, f);
+        if (f.size() < 24) throw LocusError{kLocusParse};
+        Record R;
+        R.dirn = f[8];
+        R.name = f[9];
+        R.qsize = to_i64(f[10]);
+        R.qstart = to_i64(f[11]);
+        R.qend = to_i64(f[12]);
+        R.chrom = f[13];
+        R.tstart = to_i64(f[15]);
+        R.tend = to_i64(f[16]);
+        split_list(f[18], R.bsize);
+        split_list(f[20], R.bstart);
+        if (R.bsize.size() != R.bstart.size()) throw LocusError{kLocusParse};
+        R.accuracy = to_f64(f[21]);
+        R.cs = f[22];
+        R.seq = f[23];
+        R.global = base + (int64_t)recs.size();
+        recs.push_back(std::move(R));
+    }
+}
+
+}  // namespace
+
+struct mando_cluster_result {
+    string text;
+    vector<int64_t> name_off, seq_off, rec_locus;
+    vector<int32_t> name_len, seq_len;
+    vector<int64_t> iso_locus, mem_off, mem, sub_off, sub;
+    vector<int64_t> peak_locus, peak_start, peak_end;
+    vector<char> peak_type, peak_side;
+    vector<double> peak_prop;
+    vector<int32_t> locus_status;
+};
+
+namespace {
+thread_local string g_cluster_err;
+}
+
+extern "C" {
+
+void mando_cluster_default_params(mando_cluster_params *p) {
+    if (!p) return;
+    p->cutoff = 0.1;
+    p->splice_site_width = 1;
+    p->minimum_read_count = 2;
+    p->upstream_buffer = 10;
+    p->downstream_buffer = 50;
+    p->junctions = "gtag,gcag,atac,ctac,ctgc,gtat";
+    p->seed = 0;
+    p->threads = 0;
+    p->poa_subsample = 100;
+}
+
+int mando_cluster_loci(const mando_cluster_params *prm, const char *const *psl_paths, const char *const *chroms,
+                       int64_t n_loci, const int64_t *ann_pos, const int64_t *ann_off,
+                       mando_cluster_result **out) {
+    if (!prm || !out || n_loci < 0 || (n_loci > 0 && (!psl_paths || !chroms))) return MANDO_E_ARG;
+    *out = nullptr;
+    Params P;
+    P.cutoff = prm->cutoff;
+    P.w = prm->splice_site_width;
+    P.min_count = prm->minimum_read_count;
+    P.up = prm->upstream_buffer;
+    P.down = prm->downstream_buffer;
+    P.sub_k = prm->poa_subsample > 0 ? prm->poa_subsample : 100;
+    P.seed = prm->seed;
+    if (prm->junctions) {
+        string j(prm->junctions);
+        size_t a = 0;
+        while (true) {
+            const size_t c = j.find(',', a);
+            P.junctions.push_back(j.substr(a, c == string::npos ? string::npos : c - a));
+            if (c == string::npos) break;
+            a = c + 1;
+        }
+    }
+    auto res = std::make_unique<mando_cluster_result>();
+    // read every locus file into one buffer (sizes first, then parallel reads)
+    vector<int64_t> fsize((size_t)n_loci, 0), foff((size_t)n_loci + 1, 0);
+    for (int64_t i = 0; i < n_loci; ++i) {
+        FILE *fh = fopen(psl_paths[i], "rb");
+        if (!fh) {
+            fsize[(size_t)i] = -1;
+            continue;
+        }
+        fseek(fh, 0, SEEK_END);
+        fsize[(size_t)i] = ftell(fh);
+        fclose(fh);
+    }
+    for (int64_t i = 0; i < n_loci; ++i) foff[(size_t)i + 1] = foff[(size_t)i] + std::max<int64_t>(0, fsize[(size_t)i]);
+    res->text.resize((size_t)foff[(size_t)n_loci]);
+    int nth = prm->threads > 0 ? prm->threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n_loci));
+    vector<LocusIn> ins((size_t)n_loci);
+    vector<vector<Record>> recs((size_t)n_loci);
+    vector<LocusOut> outs((size_t)n_loci);
+    // heaviest loci first
+    vector<int64_t> order((size_t)n_loci);
+    for (int64_t i = 0; i < n_loci; ++i) order[(size_t)i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return fsize[(size_t)a] > fsize[(size_t)b]; });
+    std::atomic<int64_t> next{0};
+    auto worker = [&]() {
+        while (true) {
+            const int64_t k = next.fetch_add(1);
+            if (k >= n_loci) break;
+            const int64_t i = order[(size_t)k];
+            LocusOut &lo = outs[(size_t)i];
+            try {
+                if (fsize[(size_t)i] < 0) throw LocusError{kLocusIO};
+                char *dst = &res->text[(size_t)foff[(size_t)i]];
+                FILE *fh = fopen(psl_paths[i], "rb");
+                if (!fh) throw LocusError{kLocusIO};
+                const size_t got = fread(dst, 1, (size_t)fsize[(size_t)i], fh);
+                fclose(fh);
+                if ((int64_t)got != fsize[(size_t)i]) throw LocusError{kLocusIO};
+                LocusIn &li = ins[(size_t)i];
+                li.text = string_view(dst, got);
+                li.chrom = chroms[i];
+                if (ann_pos && ann_off)
+                    for (int s = 0; s < 4; ++s) {
+                        const int64_t a = ann_off[4 * i + s], b = ann_off[4 * i + s + 1];
+                        li.ann[s].assign(ann_pos + a, ann_pos + b);
+                    }
+                parse_locus(li.text, 0, recs[(size_t)i]);
+                LocusRunner run(P, li, recs[(size_t)i], lo);
+                run.run();
+            } catch (const LocusError &e) {
+                lo = LocusOut();
+                lo.status = e.code;
+            } catch (const std::exception &) {
+                lo = LocusOut();
+                lo.status = kLocusParse;
+            }
+        }
+    };
+    vector<std::thread> th;
+    for (int t = 0; t < nth; ++t) th.emplace_back(worker);
+    for (auto &t : th) t.join();
+    // flatten
+    const char *base = res->text.data();
+    vector<int64_t> rec_base((size_t)n_loci + 1, 0);
+    for (int64_t i = 0; i < n_loci; ++i) rec_base[(size_t)i + 1] = rec_base[(size_t)i] + (int64_t)recs[(size_t)i].size();
+    const int64_t nr = rec_base[(size_t)n_loci];
+    res->name_off.resize((size_t)nr);
+    res->name_len.resize((size_t)nr);
+    res->seq_off.resize((size_t)nr);
+    res->seq_len.resize((size_t)nr);
+    res->rec_locus.resize((size_t)nr);
+    for (int64_t i = 0; i < n_loci; ++i)
+        for (size_t r = 0; r < recs[(size_t)i].size(); ++r) {
+            const Record &R = recs[(size_t)i][r];
+            const size_t g = (size_t)(rec_base[(size_t)i] + (int64_t)r);
+            res->name_off[g] = R.name.data() - base;
+            res->name_len[g] = (int32_t)R.name.size();
+            res->seq_off[g] = R.seq.data() - base;
+            res->seq_len[g] = (int32_t)R.seq.size();
+            res->rec_locus[g] = i;
+        }
+    res->mem_off.push_back(0);
+    res->sub_off.push_back(0);
+    res->locus_status.resize((size_t)n_loci);
+    for (int64_t i = 0; i < n_loci; ++i) {
+        const LocusOut &lo = outs[(size_t)i];
+        res->locus_status[(size_t)i] = lo.status;
+        for (size_t k = 0; k < lo.iso_members.size(); ++k) {
+            res->iso_locus.push_back(i);
+            for (int32_t r : lo.iso_members[k]) res->mem.push_back(rec_base[(size_t)i] + r);
+            res->mem_off.push_back((int64_t)res->mem.size());
+            for (int32_t r : lo.iso_sub[k]) res->sub.push_back(rec_base[(size_t)i] + r);
+            res->sub_off.push_back((int64_t)res->sub.size());
+        }
+        for (const Peak &pk : lo.peaks) {
+            res->peak_locus.push_back(i);
+            res->peak_start.push_back(pk.start);
+            res->peak_end.push_back(pk.end);
+            res->peak_type.push_back(pk.type);
+            res->peak_side.push_back(pk.side);
+            res->peak_prop.push_back(pk.prop);
+        }
+    }
+    *out = res.release();
+    return MANDO_OK;
+}
+
+int mando_cluster_view_get(const mando_cluster_result *r, mando_cluster_view *v) {
+    if (!r || !v) return MANDO_E_ARG;
+    v->n_loci = (int64_t)r->locus_status.size();
+    v->locus_status = r->locus_status.data();
+    v->text = r->text.data();
+    v->text_len = (int64_t)r->text.size();
+    v->n_records = (int64_t)r->name_off.size();
+    v->name_off = r->name_off.data();
+    v->name_len = r->name_len.data();
+    v->seq_off = r->seq_off.data();
+    v->seq_len = r->seq_len.data();
+    v->rec_locus = r->rec_locus.data();
+    v->n_isoforms = (int64_t)r->iso_locus.size();
+    v->iso_locus = r->iso_locus.data();
+    v->mem_off = r->mem_off.data();
+    v->mem = r->mem.data();
+    v->sub_off = r->sub_off.data();
+    v->sub = r->sub.data();
+    v->n_peaks = (int64_t)r->peak_locus.size();
+    v->peak_locus = r->peak_locus.data();
+    v->peak_start = r->peak_start.data();
+    v->peak_end = r->peak_end.data();
+    v->peak_type = r->peak_type.data();
+    v->peak_side = r->peak_side.data();
+    v->peak_prop = r->peak_prop.data();
+    return MANDO_OK;
+}
+
+void mando_cluster_free(mando_cluster_result *r) { delete r; }
+
+}  // extern "C"
