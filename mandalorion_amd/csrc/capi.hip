@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/mando.h"
+#include "orient_kernel.h"
 #include "poa_kernel.h"
 
 namespace {
@@ -80,10 +81,10 @@ struct mando_ctx {
     bool timed = false;
     DevBuf ws, counter, prof;
     DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
-    DevBuf o_hits, o_strand;
+    DevBuf o_hits, o_strand, o_status;
     ~mando_ctx() {
         for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
-                          &cons_len, &cells, &status, &o_hits, &o_strand})
+                          &cons_len, &cells, &status, &o_hits, &o_strand, &o_status})
             b->release();
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -434,6 +435,71 @@ int mando_selftest(mando_ctx *ctx, int *bad) {
     HIP_TRY(mando::run_wave_selftest(ctx->counter.as<int>(), ctx->stream));
     HIP_TRY(hipMemcpyAsync(bad, ctx->counter.p, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MANDO_OK;
+}
+
+int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_off, const int64_t *grp_off,
+                       int64_t n_groups, int8_t *hit_strands, int32_t max_hits, int32_t *n_hits) {
+    if (!ctx || n_groups < 0 || max_hits < 1 || max_hits > 8 || (n_groups > 0 && (!seq_off || !grp_off)))
+        return fail(MANDO_E_ARG, "mando_orient_batch: bad argument (max_hits must be 1..8)");
+    if (n_groups == 0) return MANDO_OK;
+    if (grp_off[0] != 0) return fail(MANDO_E_ARG, "grp_off must start at 0");
+    for (int64_t g = 0; g < n_groups; ++g)
+        if (grp_off[g + 1] < grp_off[g]) return fail(MANDO_E_ARG, "grp_off not monotone");
+    const int64_t n_reads = grp_off[n_groups];
+    for (int64_t r = 0; r < n_reads; ++r)
+        if (seq_off[r + 1] < seq_off[r]) return fail(MANDO_E_ARG, "seq_off not monotone");
+    const int64_t total = seq_off[n_reads] - seq_off[0];
+    if (total > 0 && !seqs) return fail(MANDO_E_ARG, "null seqs");
+    if (n_reads > 0 && (!hit_strands || !n_hits)) return fail(MANDO_E_ARG, "null outputs");
+    if (n_groups > INT32_MAX) return fail(MANDO_E_ARG, "too many groups");
+    HIP_TRY(hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = ctx->seq.ensure((size_t)std::max<int64_t>(total, 1) + 16)) != MANDO_OK) return rc;
+    if ((rc = ctx->seq_off.ensure(sizeof(int64_t) * (size_t)(n_reads + 1))) != MANDO_OK) return rc;
+    if ((rc = ctx->grp_off.ensure(sizeof(int64_t) * (size_t)(n_groups + 1))) != MANDO_OK) return rc;
+    if ((rc = ctx->o_strand.ensure((size_t)std::max<int64_t>(n_reads, 1) * (size_t)max_hits)) != MANDO_OK) return rc;
+    if ((rc = ctx->o_hits.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(n_reads, 1))) != MANDO_OK) return rc;
+    if ((rc = ctx->o_status.ensure(sizeof(int32_t) * (size_t)n_groups)) != MANDO_OK) return rc;
+    if ((rc = ctx->counter.ensure(sizeof(int32_t))) != MANDO_OK) return rc;
+    std::vector<int64_t> so((size_t)n_reads + 1);
+    for (int64_t r = 0; r <= n_reads; ++r) so[(size_t)r] = seq_off[r] - seq_off[0];
+    if (total > 0) HIP_TRY(hipMemcpyAsync(ctx->seq.p, seqs + seq_off[0], (size_t)total, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->seq_off.p, so.data(), so.size() * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->grp_off.p, grp_off, sizeof(int64_t) * (size_t)(n_groups + 1), hipMemcpyHostToDevice,
+                           ctx->stream));
+    HIP_TRY(hipMemsetAsync(ctx->o_hits.p, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(n_reads, 1), ctx->stream));
+    HIP_TRY(hipMemsetAsync(ctx->counter.p, 0, sizeof(int32_t), ctx->stream));
+    mando::OrientArgs a;
+    a.seq = ctx->seq.as<uint8_t>();
+    a.seq_off = ctx->seq_off.as<int64_t>();
+    a.grp_off = ctx->grp_off.as<int64_t>();
+    a.n_groups = (int32_t)n_groups;
+    a.hits = ctx->o_strand.as<int8_t>();
+    a.n_hits = ctx->o_hits.as<int32_t>();
+    a.max_hits = max_hits;
+    a.status = ctx->o_status.as<int32_t>();
+    a.counter = ctx->counter.as<int32_t>();
+    const int slots = (int)std::min<int64_t>(n_groups, (int64_t)ctx->n_cu * 2);
+    HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    HIP_TRY(mando::launch_orient(a, slots, ctx->stream));
+    HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    ctx->timed = true;
+    ctx->last_launches = 1;
+    std::vector<int32_t> st((size_t)n_groups);
+    HIP_TRY(hipMemcpyAsync(st.data(), ctx->o_status.p, sizeof(int32_t) * (size_t)n_groups, hipMemcpyDeviceToHost,
+                           ctx->stream));
+    if (n_reads > 0) {
+        HIP_TRY(hipMemcpyAsync(hit_strands, ctx->o_strand.p, (size_t)n_reads * (size_t)max_hits, hipMemcpyDeviceToHost,
+                               ctx->stream));
+        HIP_TRY(hipMemcpyAsync(n_hits, ctx->o_hits.p, sizeof(int32_t) * (size_t)n_reads, hipMemcpyDeviceToHost,
+                               ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (int64_t g = 0; g < n_groups; ++g)
+        if (st[(size_t)g] != 0)
+            return fail(MANDO_E_UNSUPPORTED, "orientation: group " + std::to_string(g) + " has a read with more than " +
+                                                 std::to_string(mando::kOrientCap) + " minimizers or anchors");
     return MANDO_OK;
 }
 

@@ -1,0 +1,36 @@
+"""Read orientation on the GPU (libmando `mando_orient_batch`, HIP).
+
+Drop-in for the mappy calls of determine_consensus
+(/root/reference/utils/SpliceDefineConsensus.py:895-907): per isoform group, the reference is the
+group's first subsampled read and every subsampled read (the first included) gets the ordered list of
+strands of its primary hits.  The host then replays the reference's rebinding quirk
+(mandalorion_amd.define.assemble).  Specification: oracle/orient_ref.c (parity with mappy unpinned).
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+
+
+def orient_batch(groups: Sequence[Sequence[str | bytes]], device: int = 0, max_hits: int = 4) -> list[list[list[int]]]:
+    from .poa import pack_groups
+
+    ctx = _lib.context(device)
+    seqs, seq_off, grp_off = pack_groups(groups)
+    n = int(seq_off.shape[0]) - 1
+    hits = np.zeros(max(n, 1) * max_hits, dtype=np.int8)
+    nh = np.zeros(max(n, 1), dtype=np.int32)
+    sbuf = np.frombuffer(seqs, dtype=np.uint8) if seqs else np.zeros(1, dtype=np.uint8)
+    _lib.check(ctx.lib.mando_orient_batch(ctx.handle, _lib.ptr(sbuf), _lib.ptr(seq_off), _lib.ptr(grp_off),
+                                          len(groups), _lib.ptr(hits), max_hits, _lib.ptr(nh)))
+    out, r = [], 0
+    for g in groups:
+        gl = []
+        for _ in g:
+            gl.append([int(x) for x in hits[r * max_hits:r * max_hits + int(nh[r])]])
+            r += 1
+        out.append(gl)
+    return out

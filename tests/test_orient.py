@@ -1,0 +1,65 @@
+"""Orientation: the HIP kernel vs the CPU restatement (oracle/orient_ref.c), and both vs the true strand
+of synthetic reads.  PARITY UNPINNED against mappy (absent; no reference test or fixture exists for this
+step) — the GPU/CPU comparison is bit-exact on the full hit lists."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from mandalorion_amd import synth
+
+
+def _groups(n_groups, seed, flip_p=0.3, lens=(2500, 3500), depth=(5, 30), unrelated=True):
+    _, groups = synth.read_groups(n_groups, lens, depth, seed=seed)
+    rng = np.random.default_rng(seed + 100)
+    out, truth = [], []
+    for g in groups:
+        f = [bool(rng.random() < flip_p) and i > 0 for i in range(len(g))]
+        gg = [synth.revcomp(s) if x else s for s, x in zip(g, f)]
+        t = [[-1] if x else [1] for x in f]
+        if unrelated:
+            gg.append("".join(rng.choice(list("ACGT"), int(rng.integers(500, 3000)))))
+            t.append([])
+        out.append(gg)
+        truth.append(t)
+    return out, truth
+
+
+def test_oracle_recovers_true_strand():
+    from oracle import orient as oref
+
+    groups, truth = _groups(12, 5)
+    assert oref.orient_batch(groups) == truth
+
+
+def test_oracle_edge_cases():
+    from oracle import orient as oref
+
+    short = ["ACGT", "ACGTACGTAC", "N" * 50]
+    g = [["ACGTTGCA" * 40] + short, short]
+    res = oref.orient_batch(g)
+    assert res[0][1:] == [[], [], []]
+    assert res[1] == [[], [], []]
+
+
+@pytest.mark.gpu
+def test_orient_gpu_matches_oracle(gpu_ctx):
+    from mandalorion_amd import orient
+    from oracle import orient as oref
+
+    groups, truth = _groups(40, 11)
+    groups += _groups(10, 12, lens=(300, 900), depth=(2, 6))[0]
+    groups += [["ACGT", "A" * 40, "ACGTACGTACGTACGTAC"], ["N" * 100, "ACGTTGCA" * 30]]
+    got = orient.orient_batch(groups)
+    assert got == oref.orient_batch(groups)
+    assert got[:40] == truth
+
+
+@pytest.mark.gpu
+def test_orient_gpu_long_reads(gpu_ctx):
+    from mandalorion_amd import orient
+    from oracle import orient as oref
+
+    groups, truth = _groups(6, 21, lens=(7000, 9000), depth=(5, 12))
+    got = orient.orient_batch(groups)
+    assert got == oref.orient_batch(groups) == truth
