@@ -1,0 +1,113 @@
+"""`Mando.py`-compatible entry point of this build (python -m mandalorion_amd.mando ... or ./Mando.py).
+
+Keeps the reference's command-line surface (/root/reference/Mando.py:22-205) so a pipeline that calls
+`Mando.py -M D ...` can switch over unchanged.  Only the D module (defining isoforms) is built here:
+it runs mandalorion_amd.define (clustering on host C++ threads, orientation and POA consensus on the
+GPU) with exactly the arguments Mando.py passes to defineIsoforms.py (Mando.py:382-399).  The other
+modules (A alignment, P SAM->PSL, F filtering, Q quantification) are outside this build's scope
+ and are reported and skipped.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+from time import localtime, strftime
+
+VERSION = "mandalorion_amd 0.1.0 (D module on MI355X; CLI of Mandalorion v4.2.0)"
+
+
+def parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description="Mandalorion isoform identification (MI355X D module)")
+    ap.add_argument("-p", "--path", type=str, default=".", help="output directory")
+    ap.add_argument("-u", "--upstream_buffer", type=str, default="10")
+    ap.add_argument("-d", "--downstream_buffer", type=str, default="50")
+    ap.add_argument("-g", "--genome_annotation", type=str, default="None", help="GTF (annotated splice sites)")
+    ap.add_argument("-G", "--genome_sequence", type=str)
+    ap.add_argument("-r", "--minimum_ratio", type=str, default="0.01")
+    ap.add_argument("-i", "--minimum_internal_ratio", type=str, default="1")
+    ap.add_argument("-R", "--minimum_reads", type=str, default="3")
+    ap.add_argument("-f", "--Consensus_reads", type=str, help="reads: file, comma list, or .fofn")
+    ap.add_argument("-O", "--overhangs", type=str, default="0,40,0,40")
+    ap.add_argument("-t", "--minimap2_threads", type=str, default="8")
+    ap.add_argument("-I", "--minimum_isoform_length", type=str, default="200")
+    ap.add_argument("-n", "--minimum_feature_count", type=str, default="2")
+    ap.add_argument("-w", "--splice_site_window", type=str, default="1")
+    ap.add_argument("-A", "--Acutoff", type=str, default="0.5")
+    ap.add_argument("-W", "--white_list_polyA", type=str, default="0")
+    ap.add_argument("-m", "--multi_exon_only", default="0", action="store_const", const="1")
+    ap.add_argument("-j", "--junctions", default="gtag,gcag,atac,ctac,ctgc,gtat", type=str)
+    ap.add_argument("-M", "--Modules", default="APDFQ")
+    ap.add_argument("-P", "--pacbio", default=False, action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--mm2_path", default=None, type=str, help=argparse.SUPPRESS)
+    ap.add_argument("--seed", type=int, default=int(os.environ.get("MANDO_RNG_SEED", "0")),
+                    help="numpy RNG state every locus starts from (the reference's parent process state)")
+    ap.add_argument("-v", "--version", action="version", version=VERSION)
+    return ap
+
+
+def main(argv: list[str] | None = None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    ap = parser()
+    if not argv:
+        ap.print_help()
+        return 0
+    a = ap.parse_args(argv)
+    path = a.path + "/"
+    temp_path = path + "/tmp/"
+    files = a.Consensus_reads or ""
+    if ".fofn" in files:
+        fasta_list = [l.strip() for l in open(files)]
+    else:
+        fasta_list = files.split(",") if files else []
+    os.makedirs(path, exist_ok=True)
+    with open(path + "/Mando.log", "a") as log:
+        log.write(f'\nMandalorion "{VERSION}" was run on {strftime("%Y-%m-%d %H:%M:%S", localtime())}\n'
+                  f"with the following parameters\n{str(a).replace('Namespace(', '').replace(')', '')}\n")
+    os.makedirs(temp_path, exist_ok=True)
+    for mod in a.Modules:
+        if mod != "D":
+            print(f"\tmodule {mod}: not part of this build (D module only), skipped")
+            continue
+        print("\n      Module D - defining isoforms (MI355X)\n")
+        clean_sorted = temp_path + "/mm2Alignments.clean.sorted.psl"
+        ok = True
+        if not os.path.exists(clean_sorted) or os.path.getsize(clean_sorted) == 0:
+            print("\tclean sorted psl file missing or empty")
+            ok = False
+        for f in fasta_list:
+            if not os.path.exists(f) or os.path.getsize(f) == 0:
+                print("\t", f, "missing or empty")
+                ok = False
+        if not ok:
+            continue
+        from . import define
+
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+
+            if torch.cuda.is_available():
+                torch.cuda.set_device(local)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
+        define.define_isoforms(temp_path, cutoff=0.1, genome_file=a.genome_annotation,
+                               splice_site_width=int(a.splice_site_window),
+                               minimum_read_count=int(a.minimum_feature_count),
+                               white_list_polyA=a.white_list_polyA.split(","), threads=int(a.minimap2_threads),
+                               junctions=a.junctions, upstream_buffer=int(a.upstream_buffer),
+                               downstream_buffer=int(a.downstream_buffer), seed=a.seed, device=local,
+                               rank=rank, world=world, verbose=True)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

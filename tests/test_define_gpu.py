@@ -1,0 +1,43 @@
+"""End-to-end D module on the GPU: clustering (host C++) -> orientation (HIP) -> batched POA (HIP) ->
+writer, against the same driver with the CPU restatements (oracle/) injected for orientation and POA.
+The written Isoform_Consensi.fasta / reads2isoforms.txt must be byte-identical; reads2isoforms.txt must
+also equal the reference's own (tests/golden/cluster_vectors.json, independent of consensus)."""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+
+import pytest
+
+from mandalorion_amd import define, simdata
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "cluster_vectors.json")))
+P = GOLD["params"]
+
+
+def _run(d, gtf, **kw):
+    return define.define_isoforms(d, cutoff=P["cutoff"], genome_file=gtf, splice_site_width=P["splice_site_width"],
+                                  minimum_read_count=P["minimum_read_count"],
+                                  white_list_polyA=P["white_list_polyA"].split(","), threads=8,
+                                  junctions=P["junctions"], upstream_buffer=P["upstream_buffer"],
+                                  downstream_buffer=P["downstream_buffer"], seed=0, **kw)
+
+
+@pytest.mark.gpu
+def test_define_gpu_equals_cpu_restatement(gpu_ctx, tmp_path):
+    from oracle import orient as oref
+    from oracle import poa as opoa
+
+    d = str(tmp_path)
+    loci = simdata.make_dataset(simdata.fixture_specs())
+    info = simdata.write_dataset(loci, d)
+    st = _run(d, info["gtf"])
+    read = lambda f: open(os.path.join(d, f), "rb").read()
+    gpu_fa, gpu_r2i = read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")
+    assert hashlib.sha256(gpu_r2i).hexdigest() == GOLD["seeds"]["0"]["reads2isoforms_sha256"]
+    assert st["poa_groups"] > 20
+    _run(d, info["gtf"], orient_fn=lambda g: oref.orient_batch(g),
+         consensus_fn=lambda g, s: opoa.consensus_batch(g))
+    assert read("Isoform_Consensi.fasta") == gpu_fa
+    assert read("reads2isoforms.txt") == gpu_r2i
