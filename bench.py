@@ -87,22 +87,32 @@ def _cpu_worker(args):
     return done_reads, done_groups, time.perf_counter() - t0
 
 
+def _cpu_init():
+    from oracle import poa as opoa
+
+    opoa.load()
+
+
 def cpu_baseline(seqs, seq_off, grp_off, seconds, procs):
-    """oracle/poa_ref.c (C restatement of abPOA, 1 thread per process) on a time-bounded sample."""
+    """oracle/poa_ref.c (C restatement of abPOA, 1 thread per process) on a time-bounded sample.
+
+    Runs before the GPU is initialised, in `spawn` workers (no inherited HIP state); each process gets
+    far more groups than it can finish (~0.2 s per 50x3kb group) and stops at the shared deadline."""
     from mandalorion_amd import synth
 
     n_groups = len(grp_off) - 1
-    per = max(4, int(seconds * 10))  # enough groups per process to outlast the time budget (~0.2 s each)
+    per = max(8, int(seconds * 12))
     want = min(n_groups, procs * per)
     pick = list(range(0, n_groups, max(1, n_groups // want)))[:want]  # evenly strided sample
     groups = synth.unpack_groups(seqs, seq_off, grp_off, pick)
     chunks = [groups[i::procs] for i in range(procs)]
-    deadline = time.perf_counter() + seconds
-    t0 = time.perf_counter()
-    ctx = mp.get_context("fork")
-    with ctx.Pool(procs) as pool:
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs, initializer=_cpu_init) as pool:
+        pool.map(_cpu_init_probe, range(procs))  # workers up and the oracle loaded before the clock
+        t0 = time.perf_counter()
+        deadline = t0 + seconds
         res = pool.map(_cpu_worker, [(c, deadline) for c in chunks])
-    wall = time.perf_counter() - t0
+        wall = time.perf_counter() - t0
     reads = sum(r[0] for r in res)
     ngr = sum(r[1] for r in res)
     return {
@@ -115,11 +125,25 @@ def cpu_baseline(seqs, seq_off, grp_off, seconds, procs):
     }
 
 
+def _cpu_init_probe(_):
+    return os.getpid()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    from mandalorion_amd import synth
+
+    seqs, seq_off, grp_off = synth.fast_groups(args.groups, (args.len_lo, args.len_hi),
+                                               (args.depth, args.depth), seed=synth.DATA_SEED + rank,
+                                               threads=16)
+    # CPU baseline first, on rank 0 of a 1-GPU run, before anything touches the GPU
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(seqs, seq_off, grp_off, args.cpu_seconds, procs)
     import torch
 
     torch.cuda.set_device(local)
@@ -130,12 +154,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from mandalorion_amd import _lib, synth
+    from mandalorion_amd import _lib
 
     ctx = _lib.context(local)
-    seqs, seq_off, grp_off = synth.fast_groups(args.groups, (args.len_lo, args.len_hi),
-                                               (args.depth, args.depth), seed=synth.DATA_SEED + rank,
-                                               threads=16)
     order = lpt_order(seq_off, grp_off)
     seqs, seq_off, grp_off = reorder(seqs, seq_off, grp_off, order)
     n_groups = len(grp_off) - 1
@@ -247,9 +268,8 @@ def main():
             "traffic": traffic,
         },
     }
-    if rank == 0 and not args.no_cpu_baseline:
-        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(seqs, seq_off, grp_off, args.cpu_seconds, procs)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -1,6 +1,6 @@
 """Dev helper: per-phase cycle breakdown of the POA kernel (MANDO_PROF=1) on a config-3-shaped batch."""
 import os, sys, time
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["MANDO_PROF"] = "1"
 from mandalorion_amd import synth, poa
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 500
