@@ -94,6 +94,8 @@ struct mando_ctx {
 
 namespace {
 
+constexpr int kMaxWavesPerCu = 16;  // upper bound on resident POA waves per CU
+
 struct GroupStat {
     int64_t nreads = 0, first_len = 0, sum = 0, maxlen = 0;
 };
@@ -127,7 +129,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
                  const uint8_t *d_seq, const int64_t *d_seq_off, const int64_t *d_grp_off,
                  const int32_t *d_gorder, int64_t n_groups, uint8_t *d_cons,
                  const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
-                 int32_t *d_status, int max_slots) {
+                 int32_t *d_status, int max_per_cu) {
     mando::PoaKArgs a{};
     a.seq = d_seq;
     a.seq_off = d_seq_off;
@@ -150,11 +152,16 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.e2 = p.gap_ext2;
     a.band_b = p.band_b;
     a.band_f = p.band_f;
+    a.qlds = mando::poa_qlds_bytes(caps.QC);
     // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     const size_t budget = std::max<size_t>((size_t)1 << 30, (size_t)(0.5 * (double)free_b) + ctx->ws.bytes);
-    int64_t slots = std::min<int64_t>(n_groups, max_slots);
+    // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
+    int cap = max_per_cu;
+    if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
+    const int per_cu = mando::poa_blocks_per_cu(a, cap);
+    int64_t slots = std::min<int64_t>(n_groups, (int64_t)ctx->n_cu * per_cu);
     while (slots > 1 && (size_t)(slots * a.slot_bytes) > budget) slots /= 2;
     if (slots < 1) slots = 1;
     int rc = ctx->ws.ensure((size_t)(slots * a.slot_bytes));
@@ -294,7 +301,7 @@ int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const
                                     std::max<int64_t>(1, max_group_bases / std::max<int64_t>(1, max_read_len / 4)), 0);
     ctx->last_launches = 1;
     return launch_batch(ctx, *params, caps, d_seqs, d_seq_off, d_grp_off, nullptr, n_groups,
-                        d_cons, d_cons_off, d_cons_len, d_cells, d_status, ctx->n_cu * 8);
+                        d_cons, d_cons_off, d_cons_len, d_cells, d_status, kMaxWavesPerCu);
 }
 
 int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *seqs,
@@ -390,7 +397,7 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
                           ctx->grp_off.as<int64_t>(), ctx->gorder.as<int32_t>(), (int64_t)todo.size(),
                           ctx->cons.as<uint8_t>(), ctx->cons_off.as<int64_t>(),
                           ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
-                          ctx->status.as<int32_t>(), ctx->n_cu * 8);
+                          ctx->status.as<int32_t>(), kMaxWavesPerCu);
         if (rc) return rc;
         ctx->last_launches += 1;
         HIP_TRY(hipMemcpyAsync(st.data(), ctx->status.p, st.size() * 4, hipMemcpyDeviceToHost, ctx->stream));

@@ -10,7 +10,7 @@ constexpr int kWave = 64;
 constexpr int kCPL = 2;                  // DP cells per lane per chunk
 constexpr int kChunk = kWave * kCPL;     // 128 band columns per chunk
 constexpr int kRing = 4;                 // rows of H/E1/E2 kept in LDS
-constexpr int kRowRing = 64;             // rows of band info kept in LDS
+constexpr int kRowRing = 32;             // rows of band info kept in LDS
 constexpr int kPreInline = 5;            // predecessor rows stored inline in a row descriptor
 constexpr int kDescInts = 8;             // ints per row descriptor
 constexpr int kRowInfoInts = 8;          // ints per row record in HBM
@@ -111,7 +111,17 @@ struct PoaKArgs {
     SlotLayout lay;
     int32_t match, mismatch, o1, e1, o2, e2, band_b;
     float band_f;
+    int32_t qlds;            // dynamic LDS bytes for the read (4-bit codes): >= (longest read + 1) / 2
 };
+
+// dynamic LDS the POA kernel needs for reads up to max_len
+inline int poa_qlds_bytes(int64_t max_len) {
+    const int64_t b = ((((max_len + 1) / 2) + 15) & ~int64_t(15)) + 16;
+    return (int)(b < 1040 ? 1040 : b);  // >= 1 KB: the backtrack's predecessor-byte window reuses it
+}
+
+// Resident workgroups per CU for these arguments (LDS / register limited), at most cap.
+int poa_blocks_per_cu(const PoaKArgs &a, int cap);
 
 // Launch the persistent POA kernel on `stream` with `n_slots` one-wave workgroups.
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream);

@@ -157,26 +157,37 @@ struct RowRec {
     int beg, end, am, soff;
 };
 
-constexpr int kQLds = 8192;      // reads up to this length are staged in LDS (4-bit bases)
-constexpr int kStage = 2 * kChunk;  // staging slot width (a 130-column window never aliases)
-constexpr int kTbWin = (kRing * kChunk + kStage) * 3 * 4;
+constexpr int kDescBatch = 32;        // row descriptors staged in LDS per refill
+constexpr int kTbWin = 4096;          // backtrack: traceback byte window
+constexpr int kBtRows = 64;           // backtrack: rows per window
+constexpr int kKpWinMax = 2048;       // backtrack: predecessor-byte window (in the read buffer)
 
+// DP phase: the H/E1/E2 ring, carried from row to row
+struct DpLds {
+    int ring[kRing][3][kChunk];  // H, E1out, E2out of the last kRing narrow rows, col & 127
+};
+// backtrack phase (the DP state is dead by then); the predecessor-byte window uses the read's
+// dynamic buffer, which the next read's DP re-stages
+struct BtLds {
+    uint8_t tb[kTbWin];
+    int md[kBtRows][8];  // per window row: tb offset, kp offset, node, predecessors 0..4
+};
+
+// LDS per wave: ~8.4 KB static + the read (4-bit codes, dynamic: sized by the batch's longest read),
+// so 16 waves fit per CU (4 per SIMD) for reads up to ~3.5 kb.
 struct alignas(16) SharedState {
     union {
-        struct {
-            int ring[kRing][3][kChunk];  // H, E1out, E2out of the last kRing narrow rows, col & 127
-            int stage[3][kStage];        // one predecessor window copied from HBM, col & 255
-        };
-        uint8_t tbwin[(kRing * kChunk + kStage) * 3 * 4];  // backtrack: traceback byte window
+        DpLds dp;
+        BtLds bt;
     };
-    int4 rrow[kRowRing];         // beg, end, argmax, spill offset of the last kRowRing rows
-    int desc[kWave][kDescInts];  // descriptors of the current 64-row batch
-    int4 prec[kWave];            // rare-case predecessor records {row, beg, end, argmax}
-    int psoff[kWave];            // ... and their spill offsets
-    alignas(16) uint8_t qnib[kQLds / 2];  // read bases, two 4-bit codes per byte
-    Slot slot;                   // this wave's workspace arrays (read per phase, see slot_of)
-    PoaKArgs args;               // kernel arguments (read per phase, see args_of)
+    int4 rrow[kRowRing];            // beg, end, argmax, spill offset of the last kRowRing rows
+    int desc[kDescBatch][kDescInts];  // descriptors of the current row batch
+    Slot slot;                      // this wave's workspace arrays (read per phase, see slot_of)
+    PoaKArgs args;                  // kernel arguments (read per phase, see args_of)
 };
+static_assert(sizeof(BtLds) <= sizeof(DpLds), "backtrack window must fit the DP scratch");
+
+extern __shared__ __attribute__((aligned(16))) uint8_t g_qnib[];  // dynamic: the read, 4-bit codes
 
 // Each phase re-reads the few workspace pointers it needs from LDS behind a compiler barrier, so
 // the ~30 loop-invariant 64-bit pointers are not kept live (and spilled) across the whole
@@ -400,9 +411,8 @@ __device__ __forceinline__ RowRec load_rowrec(const SharedState &sh, const Slot 
 // A row's band is processed in 128-column chunks starting at the even column cb0 = beg & ~1.
 // "Narrow" rows (one chunk) keep H/E1/E2 in the LDS ring, indexed by absolute column & 127; rows
 // that are wider, or that have a successor >= kRing rows later, are (also) spilled to HBM as three
-// planes of nchunk*128 ints starting at column cb0.  A predecessor outside the ring is staged for
-// the current chunk into sh.stage (columns cb-1 .. cb+128, indexed & 255) before it is read, so the
-// arithmetic only ever reads LDS.
+// planes of nchunk*128 ints starting at column cb0; a (rare) predecessor outside the ring is read
+// from those planes.
 __device__ __forceinline__ bool row_narrow(int beg, int end) { return end - (beg & ~1) < kChunk; }
 __device__ __forceinline__ int row_spill_width(int beg, int end) {
     return ((end - (beg & ~1)) / kChunk + 1) * kChunk;
@@ -418,23 +428,6 @@ __device__ __forceinline__ int pre_row_k(const PoaKArgs &a, const Slot &s, const
         return bcast0(s.pos[in_list(s, a, node)[k]]);
     }
     return dl[3 + k];
-}
-
-// copy row p's spilled H/E1/E2 for columns [cb-1, cb+128] into the staging slot
-__device__ __forceinline__ void stage_pre(SharedState &sh, const Slot &s, const RowRec &pr, int cb, int lane) {
-    hbm_fence();
-    const int cb0 = pr.beg & ~1;
-    const int wa = row_spill_width(pr.beg, pr.end);
-    const gint *sp = s.sv + pr.soff;
-    for (int t = lane; t < kChunk + 2; t += kWave) {
-        const int col = cb - 1 + t;
-        const int c = min(max(col - cb0, 0), wa - 1);
-        const int h = sp[c], x1 = sp[wa + c], x2 = sp[2 * wa + c];
-        const int ix = col & (kStage - 1);
-        sh.stage[0][ix] = h;
-        sh.stage[1][ix] = x1;
-        sh.stage[2][ix] = x2;
-    }
 }
 
 // Scoring: the reference always runs `abpoa -M 5` with default gaps, so that case is compiled with
@@ -460,17 +453,18 @@ struct DpState {
 #endif
 
 __device__ __forceinline__ int qbase(const SharedState &sh, int j) {
-    return (sh.qnib[j >> 1] >> ((j & 1) << 2)) & 0xf;
+    return (g_qnib[j >> 1] >> ((j & 1) << 2)) & 0xf;
 }
 
 // Rare-case predecessor records (more than kPreInline predecessors, or a predecessor whose record
-// left the LDS row ring): gathered from HBM into sh.prec / sh.psoff.  The loads are consumed inside
-// this uniform branch, so the common path never carries an outstanding load into an s_waitcnt.
+// left the LDS row ring): lane k gathers predecessor k's record from HBM.  The loads are consumed
+// inside this uniform branch, so the common path never carries an outstanding load into an s_waitcnt.
 __device__ __forceinline__ void pre_records_slow(const PoaKArgs &a, const Slot &s, SharedState &sh, int r,
-                                                 int node, int pn, const int *dl, int lane) {
+                                                 int node, int pn, const int *dl, int lane, int &pP, int &pB,
+                                                 int &pE, int &pA, int &pS) {
     hbm_fence();
-    for (int k = lane; k < pn; k += kWave) {
-        const int p = (k < kPreInline) ? dl[3 + k] : s.pos[in_list(s, a, node)[k]];
+    if (lane < pn) {
+        const int p = (lane < kPreInline) ? dl[3 + lane] : s.pos[in_list(s, a, node)[lane]];
         int4 x;
         if (r - p < kRowRing) {
             x = sh.rrow[p % kRowRing];
@@ -478,9 +472,13 @@ __device__ __forceinline__ void pre_records_slow(const PoaKArgs &a, const Slot &
             const gint *g = s.rinfo + (int64_t)p * kRowInfoInts;
             x = make_int4(g[0], g[1], g[2], g[3]);
         }
-        sh.prec[k] = make_int4(p, x.x, x.y, x.z);
-        sh.psoff[k] = x.w;
+        pP = p;
+        pB = x.x;
+        pE = x.y;
+        pA = x.z;
+        pS = x.w;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // consume here (see above)
 }
 
 __device__ __forceinline__ bool in_band(int col, int b, int e) {
@@ -496,7 +494,7 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
     const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
     const int IDENT = -(1 << 30);
     STAMP(ts0);
-    const int *dl = &sh.desc[r & (kWave - 1)][0];
+    const int *dl = &sh.desc[r & (kDescBatch - 1)][0];
     const int node = dl[0];
     const int d1 = dl[1];
     const int rem = dl[2];
@@ -510,15 +508,7 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
         slow = __ballot(lane < pn && r - pP >= kRowRing) != 0;
     }
     if (slow) {
-        pre_records_slow(a, s, sh, r, node, pn, dl, lane);
-        if (lane < pn) {
-            const int4 x = sh.prec[lane];
-            pP = x.x;
-            pB = x.y;
-            pE = x.z;
-            pA = x.w;
-            pS = sh.psoff[lane];
-        }
+        pre_records_slow(a, s, sh, r, node, pn, dl, lane, pP, pB, pE, pA, pS);
     } else if (lane < pn) {
         const int4 x = sh.rrow[pP % kRowRing];
         pB = x.x;
@@ -570,7 +560,7 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
     int best = -2147483647 - 1, besti = beg;
     int carry1 = kNegInf + oe1 + e1 * (beg - 1);
     int carry2 = kNegInf + oe2 + e2 * (beg - 1);
-    int *ringrow = &sh.ring[r % kRing][0][0];
+    int *ringrow = &sh.dp.ring[r % kRing][0][0];
 
     for (int c = 0; c < nchunk; ++c) {
         const int cb = cb0 + c * kChunk;
@@ -595,7 +585,7 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
             if (all_ring && pn == 1) {
                 // the common row: one predecessor, in the ring
                 const int p0 = readlane(pP, 0), b0 = readlane(pB, 0), e0 = readlane(pE, 0);
-                const int *rp = &sh.ring[p0 % kRing][0][0];
+                const int *rp = &sh.dp.ring[p0 % kRing][0][0];
                 const int hA = rp[ia], hB = rp[ib];
                 const int2 x1 = *reinterpret_cast<const int2 *>(rp + kChunk + ib);
                 const int2 x2 = *reinterpret_cast<const int2 *>(rp + 2 * kChunk + ib);
@@ -612,25 +602,29 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
 #pragma unroll 1
                 for (int k = 0; k < pn; ++k) {
                     const int pk = readlane(pP, k), bk = readlane(pB, k), ek = readlane(pE, k);
-                    const int *rp;
-                    int mask;
+                    int hA, hB;
+                    int2 x1, x2;
                     if (all_ring || (r - pk < kRing && row_narrow(bk, ek))) {
-                        rp = &sh.ring[pk % kRing][0][0];
-                        mask = kChunk - 1;
+                        const int *rp = &sh.dp.ring[pk % kRing][0][0];
+                        const int iA = (j0 - 1) & (kChunk - 1), iB = j0 & (kChunk - 1);
+                        hA = rp[iA];
+                        hB = rp[iB];
+                        x1 = *reinterpret_cast<const int2 *>(rp + kChunk + iB);
+                        x2 = *reinterpret_cast<const int2 *>(rp + 2 * kChunk + iB);
                     } else {
-                        RowRec pr;
-                        pr.beg = bk;
-                        pr.end = ek;
-                        pr.am = 0;
-                        pr.soff = readlane(pS, k);
-                        stage_pre(sh, s, pr, cb, lane);
-                        rp = &sh.stage[0][0];
-                        mask = kStage - 1;
+                        // predecessor outside the ring: its spill planes in HBM (columns clamped to
+                        // the spilled width; out-of-band values are masked below)
+                        hbm_fence();
+                        const int pc0 = bk & ~1, wa_k = row_spill_width(bk, ek);
+                        const gint *sp = s.sv + readlane(pS, k);
+                        const int cA = min(max(j0 - 1 - pc0, 0), wa_k - 1), cB = min(max(j0 - pc0, 0), wa_k - 1),
+                                  cC = min(max(j1 - pc0, 0), wa_k - 1);
+                        hA = sp[cA];
+                        hB = sp[cB];
+                        x1 = make_int2(sp[wa_k + cB], sp[wa_k + cC]);
+                        x2 = make_int2(sp[2 * wa_k + cB], sp[2 * wa_k + cC]);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // consume inside the branch
                     }
-                    const int pl = mask + 1;  // plane stride
-                    const int hA = rp[(j0 - 1) & mask], hB = rp[j0 & mask];
-                    const int2 x1 = *reinterpret_cast<const int2 *>(rp + pl + (j0 & mask));
-                    const int2 x2 = *reinterpret_cast<const int2 *>(rp + 2 * pl + (j0 & mask));
                     const bool inA = in_band(j0 - 1, bk, ek), inB = in_band(j0, bk, ek),
                                inC = in_band(j1, bk, ek);
                     const int vA = inA ? hA : kNegInf, vB = inB ? hB : kNegInf;
@@ -764,7 +758,7 @@ struct RowPipe {
 };
 
 __device__ __forceinline__ void prefetch_row(const SharedState &sh, int r, RowPipe &rp) {
-    const int *dl = &sh.desc[r & (kWave - 1)][0];
+    const int *dl = &sh.desc[r & (kDescBatch - 1)][0];
     rp.node = dl[0];
     rp.d1 = dl[1];
     rp.rem = dl[2];
@@ -819,12 +813,12 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
     const int qb = (j0 < qlen) ? qb0 : 4;
     const int ia = (j0 - 1) & (kChunk - 1), ib = j0 & (kChunk - 1);
     // predecessor 0
-    const int *r0p = &sh.ring[p0 % kRing][0][0];
+    const int *r0p = &sh.dp.ring[p0 % kRing][0][0];
     const int h0A = r0p[ia], h0B = r0p[ib];
     const int2 y01 = *reinterpret_cast<const int2 *>(r0p + kChunk + ib);
     const int2 y02 = *reinterpret_cast<const int2 *>(r0p + 2 * kChunk + ib);
     // predecessor 1 (read unconditionally, masked when absent)
-    const int *r1p = &sh.ring[max(p1, 0) % kRing][0][0];
+    const int *r1p = &sh.dp.ring[max(p1, 0) % kRing][0][0];
     const int h1A = r1p[ia], h1B = r1p[ib];
     const int2 y11 = *reinterpret_cast<const int2 *>(r1p + kChunk + ib);
     const int2 y12 = *reinterpret_cast<const int2 *>(r1p + 2 * kChunk + ib);
@@ -886,7 +880,7 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
         kq[1] = (uint16_t)(k2a | (mkb << 8));
         kq[2] = (uint16_t)(k1b | (k2b << 8));
     }
-    int *ringrow = &sh.ring[r % kRing][0][0];
+    int *ringrow = &sh.dp.ring[r % kRing][0][0];
     *reinterpret_cast<int2 *>(ringrow + ib) = make_int2(Ha, Hb);
     *reinterpret_cast<int2 *>(ringrow + kChunk + ib) = make_int2(E1a, E1b);
     *reinterpret_cast<int2 *>(ringrow + 2 * kChunk + ib) = make_int2(E2a, E2b);
@@ -938,7 +932,7 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
                       int n, int lane, int64_t &cells, int &bi_out) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
-    if (qlen > kQLds) return kStUnsupported;
+    if (qlen > 2 * a.qlds) return kStUnsupported;  // the launch sizes the read buffer for the batch
     const int w = a.band_b + (int)(a.band_f * (float)qlen);
     DpState ds{0, 0, 0, 0, {0, 0, 0, 0}};
     const int TBC = (int)a.caps.TBC, KPC = (int)a.caps.KPC, SVC = (int)a.caps.SVC;
@@ -947,17 +941,17 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
     // so a global load per row would wait for the previous rows' traceback stores to land
     for (int t = 2 * lane; t < qlen; t += 2 * kWave) {
         const int lo = q[t], hi = (t + 1 < qlen) ? q[t + 1] : 4;
-        sh.qnib[t >> 1] = (uint8_t)(lo | (hi << 4));
+        g_qnib[t >> 1] = (uint8_t)(lo | (hi << 4));
     }
     int nfast = 0;
     RowPipe pp;
     pp.prv_r = -1;
     pp.prv_beg = pp.prv_end = pp.prv_am = 0;
     for (int r = 0; r < n - 1; ++r) {
-        if ((r & (kWave - 1)) == 0) {
-            // next 64 descriptors -> LDS (one global round trip per 64 rows)
+        if ((r & (kDescBatch - 1)) == 0) {
+            // next kDescBatch descriptors -> LDS (one global round trip per batch)
             const int rr0 = r + lane;
-            if (rr0 < n) {
+            if (lane < kDescBatch && rr0 < n) {
                 const gint *dg = s.desc + (int64_t)rr0 * kDescInts;
                 int *dl = &sh.desc[lane][0];
 #pragma unroll
@@ -976,7 +970,7 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
             pp.prv_end = x.y;
             pp.prv_am = x.z;
         }
-        if (((r + 1) & (kWave - 1)) != 0) prefetch_row(sh, r + 1, pp);
+        if (((r + 1) & (kDescBatch - 1)) != 0) prefetch_row(sh, r + 1, pp);
     }
     cells += ds.cells;
     if (a.prof && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 7] += nfast;
@@ -998,7 +992,7 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
         if (qlen < pr.beg || qlen > pr.end) continue;
         int hv;
         if (pre_in_ring(sr, p, pr)) {
-            hv = sh.ring[p % kRing][0][qlen & (kChunk - 1)];
+            hv = sh.dp.ring[p % kRing][0][qlen & (kChunk - 1)];
         } else {
             hv = s.sv[pr.soff + (qlen - (pr.beg & ~1))];
         }
@@ -1025,14 +1019,13 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
 // E states are resolved lazily: state E at row i means "at E_out[i][j]", and the open/extend bit
 // is read from row i itself, so every step reads only the current row's window entry.
 // ---------------------------------------------------------------------------------------------
-constexpr int kKpWin = kQLds / 2;  // predecessor-byte window (shares the read's LDS staging buffer)
 constexpr int kKpNone = -2147483647 - 1;
 
 struct BtWin {
     int lo, hi, glob;  // rows [lo, hi] are in the window; glob: single row read from HBM
 };
 
-__device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i, int lane, BtWin &w) {
+__device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i, int lane, BtWin &w, int kpwin) {
     const int rr = i - lane;
     const bool valid = rr >= 0;
     int4 ra = make_int4(0, -1, 0, 0), rb = make_int4(0, 0, 0, 0), da = make_int4(0, 0, 0, 0),
@@ -1055,10 +1048,10 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
     const unsigned long long mm = __ballot(multi);
     const int fm = mm ? __ffsll((long long)mm) - 1 : 0;
     const int KE = readlane(kend, fm);
-    const bool fit = valid && TE - (tstart & ~15) <= kTbWin && (!multi || KE - (kstart & ~15) <= kKpWin);
+    const bool fit = valid && TE - (tstart & ~15) <= kTbWin && (!multi || KE - (kstart & ~15) <= kpwin);
     const unsigned long long nf = ~__ballot(fit);
     const int cnt = nf ? __ffsll((long long)nf) - 1 : kWave;
-    int *md = &sh.desc[lane][0];
+    int *md = &sh.bt.md[lane][0];
     if (cnt == 0) {
         // row i alone does not fit: read it from HBM
         if (lane == 0) {
@@ -1082,7 +1075,7 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
     const int ks16 = readlane(kstart, lm) & ~15;
     const int tsz = TE - rs16, ksz = mw ? KE - ks16 : 0;
     // wide copies: all loads first, then the LDS stores (one HBM round trip)
-    constexpr int kTU = kTbWin / (16 * kWave), kKU = kKpWin / (16 * kWave);
+    constexpr int kTU = kTbWin / (16 * kWave), kKU = kKpWinMax / (16 * kWave);
     const GLB int4 *tg = reinterpret_cast<const GLB int4 *>(s.tb + rs16);
     const GLB int4 *kg = reinterpret_cast<const GLB int4 *>(s.kp + ks16);
     int4 tv[kTU], kv[kKU];
@@ -1096,8 +1089,8 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
         const int x = u * kWave + lane;
         if (x * 16 < ksz) kv[u] = make_int4(kg[x].x, kg[x].y, kg[x].z, kg[x].w);
     }
-    int4 *tl = reinterpret_cast<int4 *>(sh.tbwin);
-    int4 *kl = reinterpret_cast<int4 *>(sh.qnib);
+    int4 *tl = reinterpret_cast<int4 *>(sh.bt.tb);
+    int4 *kl = reinterpret_cast<int4 *>(g_qnib);
 #pragma unroll
     for (int u = 0; u < kTU; ++u) {
         const int x = u * kWave + lane;
@@ -1160,14 +1153,14 @@ __device__ __forceinline__ void bt_step_lds(const SharedState &sh, const Slot &s
     const bool live = i > 0 && j > 0 && !stall;
     const bool inwin = i >= wlo;
     const int idx = min(max(whi - i, 0), kWave - 1);
-    const int4 m0 = *reinterpret_cast<const int4 *>(&sh.desc[idx][0]);
-    const int4 m1 = *reinterpret_cast<const int4 *>(&sh.desc[idx][4]);
+    const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][0]);
+    const int4 m1 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][4]);
     const int woff = m0.x, kof = m0.y, node = m0.z;
     const int tix = max(woff + j, 1);
-    const int t = sh.tbwin[tix], tprev = sh.tbwin[tix - 1];
+    const int t = sh.bt.tb[tix], tprev = sh.bt.tb[tix - 1];
     const bool multi = kof != kKpNone;
     const int kix = multi ? kof + 3 * j : 0;
-    const int k0 = sh.qnib[kix], k1 = sh.qnib[kix + 1], k2 = sh.qnib[kix + 2];
+    const int k0 = g_qnib[kix], k1 = g_qnib[kix + 1], k2 = g_qnib[kix + 2];
     const bool isE = st == 1 || st == 2;
     const bool open = isE && (t & (st == 1 ? kTbE1Open : kTbE2Open));
     const int ty = st == 0 ? (t & kTbTypeMask) : st;
@@ -1197,6 +1190,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
     int guard = (2 * (n + qlen) + 8) / kUnroll + 2 * (n + qlen) + 8;
     BtWin w{1, 0, 0};
     int glob_row = -1;
+    const int kpwin = min(kKpWinMax, a.qlds & ~15);  // predecessor bytes reuse the read's buffer
     while (i > 0 && j > 0) {
         if (--guard < 0) return kStInternal;
         if (i == glob_row) {
@@ -1208,7 +1202,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
         }
         if (i < w.lo || i > w.hi) {
             const uint64_t c0 = a.prof ? clock64() : 0;
-            bt_refill(sh, s, i, lane, w);
+            bt_refill(sh, s, i, lane, w, kpwin);
             if (a.prof && lane == 0) {
                 int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
                 pf[12] += (int64_t)(clock64() - c0);
@@ -1614,14 +1608,25 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
     }
 }
 
+int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
+    int nb = 0;
+    const bool dflt = a.match == DefaultScores::match && a.mismatch == DefaultScores::mismatch &&
+                      a.o1 == DefaultScores::o1 && a.e1 == DefaultScores::e1 && a.o2 == DefaultScores::o2 &&
+                      a.e2 == DefaultScores::e2;
+    hipError_t e = dflt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, poa_kernel<DefaultScores>, kWave, a.qlds)
+                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, poa_kernel<RuntimeScores>, kWave, a.qlds);
+    if (e != hipSuccess || nb < 1) nb = 8;
+    return nb < cap ? nb : cap;
+}
+
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream) {
     const bool dflt = a.match == DefaultScores::match && a.mismatch == DefaultScores::mismatch &&
                       a.o1 == DefaultScores::o1 && a.e1 == DefaultScores::e1 && a.o2 == DefaultScores::o2 &&
                       a.e2 == DefaultScores::e2;
     if (dflt)
-        hipLaunchKernelGGL(poa_kernel<DefaultScores>, dim3(n_slots), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL(poa_kernel<DefaultScores>, dim3(n_slots), dim3(kWave), a.qlds, stream, a);
     else
-        hipLaunchKernelGGL(poa_kernel<RuntimeScores>, dim3(n_slots), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL(poa_kernel<RuntimeScores>, dim3(n_slots), dim3(kWave), a.qlds, stream, a);
     return hipGetLastError();
 }
 
