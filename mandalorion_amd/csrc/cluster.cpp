@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -61,6 +62,19 @@ constexpr int kLocusValueError = -15;    // max() of an empty sequence in find_e
 
 struct LocusError {
     int code;
+};
+
+// optional phase timing (MANDO_CLUSTER_PROF=1): nanoseconds summed over loci / threads
+std::atomic<int64_t> g_ph[8];
+const char *kPhName[8] = {"parse", "collect", "peaks", "characterize", "sort_reads", "start_end", "subsample", "io"};
+inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+struct PhTimer {
+    int ph;
+    int64_t t0;
+    explicit PhTimer(int p) : ph(p), t0(now_ns()) {}
+    ~PhTimer() { g_ph[ph] += now_ns() - t0; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -163,22 +177,40 @@ void split_tabs(string_view line, vector<string_view> &f) {
 // ---------------------------------------------------------------------------------------------
 // getCSaroundSS: tokenised cs string
 // ---------------------------------------------------------------------------------------------
+// Run-length view of getCSaroundSS's `record` list: one run per cs operation.  Record t of the
+// reference list is record (t - rec0) of the run containing it; run k covers records
+// [rec0, rec0 + n) whose genome positions (after the per-record increment) are g0 + step * (i + 1).
+struct CsRun {
+    int32_t rec0, n;
+    int64_t g0;
+    int32_t step;  // 1 for '=', '-', '*'; 0 for '+'; the intron length for '~' (n == 1)
+    char st;       // '=', '+', '-', '*', '|'
+    std::array<char, 4> motif;
+};
 struct CsIndex {
-    vector<char> st;          // '=', '+', '-', '*', '|' (intron record)
-    vector<int64_t> pos;      // genome position after the record
-    vector<int32_t> intron;   // record index -> index into motif (introns only), else -1
-    vector<std::array<char, 4>> motif;
+    vector<CsRun> runs;
+    vector<int32_t> adv;       // indices of advancing runs (step > 0), in order
+    vector<int64_t> adv_first; // genome position of each advancing run's first record
+    int32_t nrec = 0;
     bool built = false;
 };
 
-bool is_op(char c) { return c == '\\' || c == '=' || c == '+' || c == '-' || c == '*' || c == '~'; }
+struct OpTable {
+    bool t[256];
+    OpTable() {
+        for (auto &x : t) x = false;
+        for (unsigned char c : {'\\', '=', '+', '-', '*', '~'}) t[c] = true;
+    }
+};
+const OpTable kOps;
+inline bool is_op(char c) { return kOps.t[(unsigned char)c]; }
 
 void build_cs(string_view cs, int64_t begin, CsIndex &ix) {
-    ix.st.clear();
-    ix.pos.clear();
-    ix.intron.clear();
-    ix.motif.clear();
+    ix.runs.clear();
+    ix.adv.clear();
+    ix.adv_first.clear();
     int64_t g = begin;
+    int32_t rec = 0;
     size_t i = 0;
     // re.split keeps text before the first operator as element 0, which the zip drops
     while (i < cs.size() && !is_op(cs[i])) ++i;
@@ -188,47 +220,57 @@ void build_cs(string_view cs, int64_t begin, CsIndex &ix) {
         while (j < cs.size() && !is_op(cs[j])) ++j;
         const string_view e = cs.substr(i, j - i);
         i = j;
+        CsRun r{rec, 0, g, 0, op, {0, 0, 0, 0}};
         switch (op) {
             case '=':
             case '-':
-                for (size_t k = 0; k < e.size(); ++k) {
-                    ++g;
-                    ix.st.push_back(op);
-                    ix.pos.push_back(g);
-                    ix.intron.push_back(-1);
-                }
+                r.n = (int32_t)e.size();
+                r.step = 1;
                 break;
             case '+':
-                for (size_t k = 0; k < e.size(); ++k) {
-                    ix.st.push_back('+');
-                    ix.pos.push_back(g);
-                    ix.intron.push_back(-1);
-                }
+                r.n = (int32_t)e.size();
+                r.step = 0;
                 break;
             case '*':
-                for (size_t k = 0; k < e.size(); k += 2) {
-                    ++g;
-                    ix.st.push_back('*');
-                    ix.pos.push_back(g);
-                    ix.intron.push_back(-1);
-                }
+                r.n = (int32_t)((e.size() + 1) / 2);  // entry[::2]
+                r.step = 1;
+                r.st = '*';
                 break;
             case '~': {
                 if (e.size() < 4) throw LocusError{kLocusParse};
-                g += to_i64(e.substr(2, e.size() - 4));
-                // record '|' + entry + '|'; bases = item[1:3] + item[-3:-1]
-                std::array<char, 4> m{e[0], e[1], e[e.size() - 2], e[e.size() - 1]};
-                ix.intron.push_back((int32_t)ix.motif.size());
-                ix.motif.push_back(m);
-                ix.st.push_back('|');
-                ix.pos.push_back(g);
+                r.n = 1;
+                r.step = (int32_t)to_i64(e.substr(2, e.size() - 4));
+                r.st = '|';
+                r.motif = {e[0], e[1], e[e.size() - 2], e[e.size() - 1]};
                 break;
             }
-            default:  // '\\' never occurs in a cs string; it would start an ignored record
-                break;
+            default:  // '\\' never occurs in a cs string
+                continue;
         }
+        if (r.n == 0) continue;
+        if (r.step > 0 || r.st == '|') {
+            ix.adv.push_back((int32_t)ix.runs.size());
+            ix.adv_first.push_back(g + r.step);
+        }
+        g += (int64_t)r.step * r.n;
+        rec += r.n;
+        ix.runs.push_back(r);
     }
+    ix.nrec = rec;
     ix.built = true;
+}
+
+// run containing record t (0 <= t < nrec)
+inline int run_of(const CsIndex &ix, int32_t t) {
+    int lo = 0, hi = (int)ix.runs.size() - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (ix.runs[(size_t)mid].rec0 <= t)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
 }
 
 struct CsResult {
@@ -248,43 +290,85 @@ inline int st_slot(char c) {
     }
 }
 
+// count statuses of records [a, b) into cnt (and cnt[5] += b - a)
+inline void count_range(const CsIndex &ix, int32_t a, int32_t b, int *cnt) {
+    if (a >= b) return;
+    int k = run_of(ix, a);
+    while (a < b) {
+        const CsRun &R = ix.runs[(size_t)k];
+        const int32_t e = std::min(b, R.rec0 + R.n);
+        cnt[st_slot(R.st)] += e - a;
+        cnt[5] += e - a;
+        a = e;
+        ++k;
+    }
+}
+
 void cs_around(const CsIndex &ix, int64_t start, int64_t end, CsResult &r) {
     r.bases = "nnnn";
     r.has_l = r.has_r = false;
     std::fill(r.cnt_l, r.cnt_l + 6, 0);
     std::fill(r.cnt_r, r.cnt_r + 6, 0);
-    const int64_t n = (int64_t)ix.st.size();
+    const int32_t n = ix.nrec;
     // last advancing record with start <= pos <= end ('+' records never set spliceIndex)
-    int64_t k = (int64_t)(std::upper_bound(ix.pos.begin(), ix.pos.end(), end) - ix.pos.begin()) - 1;
-    while (k >= 0 && ix.st[(size_t)k] == '+') --k;
-    if (k < 0 || ix.pos[(size_t)k] < start) return;
-    const int64_t si = k + 1;  // len(record) after appending record k
+    const int64_t ka = (int64_t)(std::upper_bound(ix.adv_first.begin(), ix.adv_first.end(), end) - ix.adv_first.begin()) - 1;
+    if (ka < 0) return;
+    const CsRun &R = ix.runs[(size_t)ix.adv[(size_t)ka]];
+    const int64_t i_in = R.n == 1 ? 0 : std::min<int64_t>(R.n - 1, (end - R.g0) / R.step - 1);
+    const int64_t pos = R.g0 + (int64_t)R.step * (i_in + 1);
+    if (pos < start) return;
+    const int64_t si = R.rec0 + i_in + 1;  // len(record) after appending that record
     const int64_t lo = std::max<int64_t>(si - 10, 0), hi = std::min<int64_t>(si + 10, n);
+    // last intron record in [lo, hi)
     int64_t idx = -1;
-    for (int64_t t = hi - 1; t >= lo; --t)
-        if (ix.st[(size_t)t] == '|') {
-            idx = t;
-            break;
-        }
+    const CsRun *IR = nullptr;
+    if (lo < hi) {
+        for (int k = run_of(ix, (int32_t)(hi - 1)); k >= 0 && ix.runs[(size_t)k].rec0 + ix.runs[(size_t)k].n > lo; --k)
+            if (ix.runs[(size_t)k].st == '|') {
+                idx = ix.runs[(size_t)k].rec0;
+                IR = &ix.runs[(size_t)k];
+                break;
+            }
+    }
     if (idx < 0) return;
-    const auto &m = ix.motif[(size_t)ix.intron[(size_t)idx]];
-    r.bases.assign(m.begin(), m.end());
+    r.bases.assign(IR->motif.begin(), IR->motif.end());
     // left = record[idx-5:idx] with Python slice normalisation
     int64_t a = idx - 5, b = idx;
     if (a < 0) a += n;
     if (a < 0) a = 0;
-    for (int64_t t = a; t < b && t < n; ++t) {
-        r.cnt_l[st_slot(ix.st[(size_t)t])]++;
-        r.cnt_l[5]++;
+    if (a < b) {
+        count_range(ix, (int32_t)a, (int32_t)std::min<int64_t>(b, n), r.cnt_l);
         r.has_l = true;
     }
     // right = record[idx+1:idx+6]
-    for (int64_t t = idx + 1; t < std::min<int64_t>(idx + 6, n); ++t) {
-        r.cnt_r[st_slot(ix.st[(size_t)t])]++;
-        r.cnt_r[5]++;
+    const int64_t ra = idx + 1, rb = std::min<int64_t>(idx + 6, n);
+    if (ra < rb) {
+        count_range(ix, (int32_t)ra, (int32_t)rb, r.cnt_r);
         r.has_r = true;
     }
 }
+
+// Position set (peak_areas): a byte map over the locus span, a hash set for anything outside it
+struct PosSet {
+    int64_t lo = 0;
+    vector<uint8_t> bits;
+    std::unordered_set<int64_t> extra;
+    void init(int64_t a, int64_t b) {
+        lo = a;
+        bits.assign(b >= a ? (size_t)(b - a + 1) : 0, 0);
+    }
+    bool has(int64_t p) const {
+        const uint64_t k = (uint64_t)(p - lo);
+        return k < bits.size() ? bits[k] != 0 : extra.count(p) != 0;
+    }
+    void add(int64_t p) {
+        const uint64_t k = (uint64_t)(p - lo);
+        if (k < bits.size())
+            bits[k] = 1;
+        else
+            extra.insert(p);
+    }
+};
 
 // ---------------------------------------------------------------------------------------------
 // ordered dict helper (Python dict: insertion order)
@@ -348,13 +432,21 @@ class LocusRunner {
         : P(p), in(in), recs(recs), out(out), mt(p.seed) {}
 
     void run() {
-        collect_reads();
-        std::unordered_set<int64_t> areas_l, areas_r;
+        {
+            PhTimer t(1);
+            collect_reads();
+        }
+        PosSet areas_l, areas_r;
+        areas_l.init(span_lo - 64, span_hi + 64);
+        areas_r.init(span_lo - 64, span_hi + 64);
         vector<Peak> a_l, a_r, n_l, n_r;
         make_genome_bins(in.ann[0], in.ann[1], 'l', areas_l, a_l);
         make_genome_bins(in.ann[2], in.ann[3], 'r', areas_r, a_r);
-        find_peaks(hist_l, true, 'l', areas_l, n_l);
-        find_peaks(hist_r, false, 'r', areas_r, n_r);
+        {
+            PhTimer t(2);
+            find_peaks(hist_l, true, 'l', areas_l, n_l);
+            find_peaks(hist_r, false, 'r', areas_r, n_r);
+        }
         // spliceDict (defineIsoforms.py:71-83): per-side counters, later rows overwrite
         int counter[2] = {0, 0};
         for (auto *tw : {&a_l, &a_r, &n_l, &n_r}) {
@@ -367,8 +459,14 @@ class LocusRunner {
                 out.peaks.push_back(pk);
             }
         }
-        sort_reads();
-        define_start_end_sites();
+        {
+            PhTimer t(4);
+            sort_reads();
+        }
+        {
+            PhTimer t(5);
+            define_start_end_sites();
+        }
         // determine_consensus subsample draw per isoform (SDC:884-888)
         vector<int64_t> perm, pick;
         for (auto &mem : out.iso_members) {
@@ -389,7 +487,10 @@ class LocusRunner {
     mando::MT19937 mt;
 
     // collect_reads state
-    std::unordered_map<int64_t, int32_t> histo_cov;
+    int64_t bin_lo = INT64_MAX, bin_hi = INT64_MIN, nbins = 0;
+    int64_t span_lo = 0, span_hi = -1;  // genome span of the locus' records  // rounded positions (multiples of 10)
+    vector<int32_t> hcov;     // histo_cov, dense over [bin_lo, bin_hi] step 10
+    vector<int32_t> ccount;   // scratch: coverage counts of the winning bin's reads
     OrderedMap<vector<HistEntry>> hist_l, hist_r;
     vector<vector<int64_t>> cov_sets;                    // per record (rounded, unique, sorted)
     std::unordered_map<string_view, int32_t> cs_dict;     // name -> last record
@@ -413,38 +514,61 @@ class LocusRunner {
         const size_t n = recs.size();
         cov_sets.resize(n);
         cs_ix.resize(n);
+        vector<int64_t> v;
         for (size_t r = 0; r < n; ++r) {
             Record &R = recs[r];
             if (R.chrom != string_view(in.chrom)) continue;
+            if (span_hi < span_lo) {
+                span_lo = R.tstart;
+                span_hi = R.tend;
+            }
+            span_lo = std::min(span_lo, R.tstart);
+            span_hi = std::max(span_hi, R.tend);
             cs_dict[R.name] = (int32_t)r;
-            std::unordered_set<int64_t> cs;
+            v.clear();
             vector<int64_t> low, up;
             int64_t y = -1;
             bool y_set = false;
             for (size_t x = 0; x < R.bsize.size(); ++x) {
                 const int64_t bs = R.bstart[x], sz = R.bsize[x], be = bs + sz;
                 for (int64_t t = 0; t < sz; t += 10) {
-                    cs.insert(myround(bs + t));
+                    v.push_back(myround(bs + t));
                     y = t;
                     y_set = true;
                 }
                 if (!y_set) throw LocusError{kLocusParse};  // NameError in the reference
-                for (int64_t t = y; t < sz; ++t) cs.insert(myround(bs + t));
+                int64_t last = INT64_MIN;
+                for (int64_t t = y; t < sz; ++t) {
+                    const int64_t b = myround(bs + t);
+                    if (b != last) v.push_back(b);
+                    last = b;
+                }
                 if (bs != R.tstart) up.push_back(bs);
                 if (be != R.tend) low.push_back(be);
             }
-            vector<int64_t> v(cs.begin(), cs.end());
             std::sort(v.begin(), v.end());
-            for (int64_t b : v) histo_cov[b] += 1;
-            cov_sets[r] = std::move(v);
+            v.erase(std::unique(v.begin(), v.end()), v.end());
+            if (!v.empty()) {
+                bin_lo = std::min(bin_lo, v.front());
+                bin_hi = std::max(bin_hi, v.back());
+            }
+            cov_sets[r] = v;
             if (R.accuracy < 0.9) continue;
             for (int64_t b : low) hist_l.at(b).push_back({(int32_t)r});
             for (int64_t b : up) hist_r.at(b).push_back({(int32_t)r});
         }
+        // dense per-locus coverage histogram over 10-nt bins (histo_cov)
+        if (bin_lo <= bin_hi) {
+            nbins = (bin_hi - bin_lo) / 10 + 1;
+            hcov.assign((size_t)nbins, 0);
+            ccount.assign((size_t)nbins, 0);
+            for (size_t r = 0; r < n; ++r)
+                for (int64_t b : cov_sets[r]) hcov[(size_t)((b - bin_lo) / 10)] += 1;
+        }
     }
 
     void make_genome_bins(const vector<int64_t> &b5, const vector<int64_t> &b3, char side,
-                          std::unordered_set<int64_t> &areas, vector<Peak> &tw) {
+                          PosSet &areas, vector<Peak> &tw) {
         for (int ti = 0; ti < 2; ++ti) {
             const char type = ti == 0 ? '5' : '3';
             vector<int64_t> pl = ti == 0 ? b5 : b3;
@@ -466,12 +590,13 @@ class LocusRunner {
                 }
                 Peak pk{mn - P.w, mx + P.w, type, side, -1.0};
                 tw.push_back(pk);
-                for (int64_t b = pk.start; b <= pk.end; ++b) areas.insert(b);
+                for (int64_t b = pk.start; b <= pk.end; ++b) areas.add(b);
             }
         }
     }
 
     bool characterize(int64_t left, int64_t right, const vector<int32_t> &names) {
+        PhTimer tm(3);
         const int64_t n = (int64_t)names.size();
         vector<int64_t> perm, pick;
         mando::mt_choice(mt, n, std::min<int64_t>(n, 500), perm, pick);
@@ -504,7 +629,7 @@ class LocusRunner {
     }
 
     void find_peaks(OrderedMap<vector<HistEntry>> &dd, bool reverse, char side,
-                    std::unordered_set<int64_t> &areas, vector<Peak> &tw) {
+                    PosSet &areas, vector<Peak> &tw) {
         vector<int64_t> dist{0};
         for (int s = 1; s <= P.w; ++s) {
             dist.push_back(s);
@@ -517,23 +642,20 @@ class LocusRunner {
                          [&](size_t a, size_t b) { return dd.vals[a].size() > dd.vals[b].size(); });
         for (size_t ci : cand) {
             const int64_t entry = dd.keys[ci];
-            if (areas.count(entry)) continue;
-            // scan_for_best_bin
-            int64_t best = 0, center = 0;
+            if (areas.has(entry)) continue;
+            // scan_for_best_bin: the winning shift by read count (strict >, first wins); the
+            // coverage counts are only needed for the winner
+            int64_t best = 0, center = 0, bx = 0;
             int64_t bdir_p = 0, bdir_m = 0;
-            vector<int32_t> best_names;
-            std::unordered_map<int64_t, int32_t> best_cov;
             for (int64_t x : dist) {
                 bool called = false;
                 for (int64_t y : dist)
-                    if (areas.count(entry + x + y)) {
+                    if (areas.has(entry + x + y)) {
                         called = true;
                         break;
                     }
                 if (called) continue;
                 int64_t cnt = 0, dp = 0, dm = 0;
-                vector<int32_t> names;
-                std::unordered_map<int64_t, int32_t> covc;
                 for (int64_t y : dist) {
                     const vector<HistEntry> *lst = dd.find(entry + x + y);
                     if (!lst) continue;
@@ -546,39 +668,49 @@ class LocusRunner {
                             dm += 1;
                         else
                             throw LocusError{kLocusKeyError};
-                        names.push_back(h.rec);
-                        for (int64_t cp : cov_sets[(size_t)h.rec]) covc[cp] += 1;
                     }
                 }
                 if (cnt > best) {
                     best = cnt;
-                    best_names = std::move(names);
                     center = entry + x;
-                    best_cov = std::move(covc);
+                    bx = x;
                     bdir_p = dp;
                     bdir_m = dm;
                 }
             }
-            // determine_cov
-            vector<int64_t> area2;
-            for (auto &kv : best_cov)
-                if (kv.second > 1) area2.push_back(kv.first);
-            if (reverse)
-                std::sort(area2.begin(), area2.end(), std::greater<int64_t>());
-            else
-                std::sort(area2.begin(), area2.end());
+            vector<int32_t> best_names;
             int64_t cov = 0;
-            int counter = 0;
-            for (int64_t bf : area2) {
-                const bool count = reverse ? bf < center : bf > center;
-                if (!count) continue;
-                if (counter <= 3) {
-                    counter += 1;
-                    auto it = histo_cov.find(myround(bf));
-                    if (it != histo_cov.end()) cov = std::max<int64_t>(cov, it->second);
-                } else {
-                    break;
+            if (best > 0) {
+                for (int64_t y : dist) {
+                    const vector<HistEntry> *lst = dd.find(entry + bx + y);
+                    if (!lst) continue;
+                    for (const HistEntry &h : *lst) {
+                        best_names.push_back(h.rec);
+                        for (int64_t cp : cov_sets[(size_t)h.rec]) ccount[(size_t)((cp - bin_lo) / 10)] += 1;
+                    }
                 }
+                // determine_cov: the first 4 bins with count > 1 strictly beyond the centre (downward
+                // for the left side), max of their histo_cov
+                int counter = 0;
+                if (reverse) {
+                    int64_t k = center - 1 - bin_lo;
+                    k = k < 0 ? -1 : std::min<int64_t>(k / 10, nbins - 1);
+                    for (; k >= 0 && counter < 4; --k)
+                        if (ccount[(size_t)k] > 1) {
+                            ++counter;
+                            cov = std::max<int64_t>(cov, hcov[(size_t)k]);
+                        }
+                } else {
+                    int64_t k = center + 1 - bin_lo;
+                    k = k <= 0 ? 0 : (k + 9) / 10;
+                    for (; k < nbins && counter < 4; ++k)
+                        if (ccount[(size_t)k] > 1) {
+                            ++counter;
+                            cov = std::max<int64_t>(cov, hcov[(size_t)k]);
+                        }
+                }
+                for (int32_t rr : best_names)
+                    for (int64_t cp : cov_sets[(size_t)rr]) ccount[(size_t)((cp - bin_lo) / 10)] = 0;
             }
             if (cov <= 0) continue;
             const double prop = py_round3((double)best / (double)cov);
@@ -592,7 +724,7 @@ class LocusRunner {
             if (characterize(center - P.w, center + P.w, best_names)) {
                 Peak pk{center - P.w, center + P.w, type, side, prop};
                 tw.push_back(pk);
-                for (int64_t b = pk.start; b <= pk.end; ++b) areas.insert(b);
+                for (int64_t b = pk.start; b <= pk.end; ++b) areas.add(b);
             }
         }
     }
@@ -945,7 +1077,10 @@ int mando_cluster_loci(const mando_cluster_params *prm, const char *const *psl_p
                         const int64_t a = ann_off[4 * i + s], b = ann_off[4 * i + s + 1];
                         li.ann[s].assign(ann_pos + a, ann_pos + b);
                     }
-                parse_locus(li.text, 0, recs[(size_t)i]);
+                {
+                    PhTimer t(0);
+                    parse_locus(li.text, 0, recs[(size_t)i]);
+                }
                 LocusRunner run(P, li, recs[(size_t)i], lo);
                 run.run();
             } catch (const LocusError &e) {
@@ -957,9 +1092,17 @@ int mando_cluster_loci(const mando_cluster_params *prm, const char *const *psl_p
             }
         }
     };
+    const char *pe = getenv("MANDO_CLUSTER_PROF");
+    const bool prof = pe && pe[0] == '1';
+    for (auto &x : g_ph) x = 0;
     vector<std::thread> th;
     for (int t = 0; t < nth; ++t) th.emplace_back(worker);
     for (auto &t : th) t.join();
+    if (prof) {
+        fprintf(stderr, "[mando cluster] thread-seconds:");
+        for (int k = 0; k < 8; ++k) fprintf(stderr, " %s %.3f", kPhName[k], (double)g_ph[k].load() * 1e-9);
+        fprintf(stderr, "\n");
+    }
     // flatten
     const char *base = res->text.data();
     vector<int64_t> rec_base((size_t)n_loci + 1, 0);

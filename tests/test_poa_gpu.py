@@ -59,3 +59,15 @@ def test_wide_band_and_far_predecessors():
     ins = synth.random_template(rng, 300).tobytes().decode()
     groups = [[t, t[:700] + ins + t[700:], t, t[:400] + t[700:], t[:700] + ins + t[700:], t]]
     _check(groups)
+
+
+def test_long_reads_beyond_8kb():
+    """Reads of 8-12 kb (config-5 lengths; the read buffer is sized per batch in dynamic LDS)."""
+    _check(poa_cases.noisy_groups(4, (8000, 12000), (4, 8), seed=31)[1])
+
+
+def test_mixed_lengths_one_batch():
+    """Short and long groups in one launch: LDS sizing and occupancy follow the longest read."""
+    _, a = poa_cases.noisy_groups(30, (200, 900), (3, 10), seed=41)
+    _, b = poa_cases.noisy_groups(2, (9000, 10000), (3, 5), seed=42)
+    _check(a + b)
