@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--e2e-loci", type=int, default=2000,
+                    help="also time the whole D module (define_isoforms: PSL files -> FASTA) on this many "
+                         "synthetic 50-read loci; 0 = skip (reported as d_module, never as value)")
     return ap.parse_args()
 
 
@@ -123,6 +126,30 @@ def cpu_baseline(seqs, seq_off, grp_off, seconds, procs):
         "sample": f"{ngr} groups x {groups[0] and len(groups[0])} reads of this workload through oracle/poa_ref.c "
                   f"(C restatement of abPOA v1.4.1, scalar), {procs} processes, {wall:.1f} s wall",
     }
+
+
+def d_module_e2e(n_loci, device):
+    """Whole D module (mandalorion_amd.define.define_isoforms, i.e. `Mando.py -M D`): locus PSL files on
+    disk -> clustering (host C++) -> orientation + POA (GPU) -> Isoform_Consensi.fasta.  Reported as
+    PSL records / wall second, the BASELINE.md end-to-end metric, on a config-3-shaped sample."""
+    import shutil
+    import tempfile
+
+    from mandalorion_amd import define, synth
+
+    d = tempfile.mkdtemp(prefix="mando_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        n = synth.write_loci(os.path.join(d, "tmp_SS"), n_loci, threads=16)
+        define.define_isoforms(d, threads=16, device=device)  # warm (context, kernels, page cache)
+        t0 = time.perf_counter()
+        st = define.define_isoforms(d, threads=16, device=device)
+        wall = time.perf_counter() - t0
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"records": n, "loci": st["loci"], "isoforms": st["isoforms"], "poa_groups": st["poa_groups"],
+            "wall_s": wall, "reads_per_s": n / wall, "t_cluster": st["t_cluster"], "t_orient": st["t_orient"],
+            "t_poa": st["t_poa"], "host_threads": 16,
+            "input": f"{n_loci} synthetic loci x 50 R2C2 reads (5-12 exons of 150-400 nt), PSL files on disk"}
 
 
 def _cpu_init_probe(_):
@@ -270,6 +297,8 @@ def main():
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu
+    if rank == 0 and world == 1 and args.e2e_loci > 0:
+        out["d_module"] = d_module_e2e(args.e2e_loci, local)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -144,3 +144,25 @@ def unpack_groups(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, gr
     raw = seqs.tobytes()
     idx = range(len(grp_off) - 1) if groups is None else groups
     return [[raw[seq_off[r]:seq_off[r + 1]].decode() for r in range(grp_off[g], grp_off[g + 1])] for g in idx]
+
+
+def write_loci(tmp_ss: str, n_loci: int, reads: tuple[int, int] = (50, 50), exons: tuple[int, int] = (5, 12),
+               exon_len: tuple[int, int] = (150, 400), intron_len: tuple[int, int] = (300, 3000),
+               isoforms: tuple[int, int] = (1, 3), seed: int = DATA_SEED, model: dict = R2C2,
+               threads: int = 0) -> int:
+    """Benchmark-scale locus PSL files (libmando_synth mando_synth_loci, same format as simdata.py) into
+    tmp_ss; returns the number of PSL records written."""
+    import ctypes
+    import os
+
+    lib = _synth_lib()
+    lib.mando_synth_loci.restype = ctypes.c_int64
+    lib.mando_synth_loci.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int64] + [ctypes.c_int32] * 10 + \
+        [ctypes.c_double] * 3 + [ctypes.c_int]
+    os.makedirs(tmp_ss, exist_ok=True)
+    n = lib.mando_synth_loci(tmp_ss.encode(), seed, n_loci, reads[0], reads[1], exons[0], exons[1], exon_len[0],
+                             exon_len[1], intron_len[0], intron_len[1], isoforms[0], isoforms[1], model["sub"],
+                             model["ins"], model["dele"], threads)
+    if n < 0:
+        raise RuntimeError(f"mando_synth_loci failed: {n}")
+    return int(n)
