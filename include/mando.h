@@ -171,6 +171,13 @@ int mando_cluster_loci(const mando_cluster_params *params, const char *const *ps
 int mando_cluster_view_get(const mando_cluster_result *res, mando_cluster_view *view);
 void mando_cluster_free(mando_cluster_result *res);
 
+/* Host helper of the D driver (FASTA / read-group assembly without per-read interpreter work):
+ * segment i = src[sel[i]] + starts[i], lens[i] bytes (sel may be NULL: src[0]), reverse-complemented
+ * like mappy.revcomp when rc && rc[i], written at out + out_off[i]. */
+int mando_pack_segments(const uint8_t *const *src, const int8_t *sel, const int64_t *starts,
+                        const int64_t *lens, const int8_t *rc, int64_t n, uint8_t *out,
+                        const int64_t *out_off, int32_t threads);
+
 #ifdef __cplusplus
 }
 #endif

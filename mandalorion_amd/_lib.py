@@ -34,6 +34,7 @@ EXPORTED = (
     "mando_cluster_loci",
     "mando_cluster_view_get",
     "mando_cluster_free",
+    "mando_pack_segments",
 )
 
 STATUS = {
@@ -168,6 +169,7 @@ def load(path: str | None = None):
         lib.mando_cluster_view_get.argtypes = [_P, _P]
         lib.mando_cluster_free.argtypes = [_P]
         lib.mando_cluster_free.restype = None
+        lib.mando_pack_segments.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, ctypes.c_int32]
         if hasattr(lib, "mando_selftest"):
             lib.mando_selftest.argtypes = [_P, _P]
         if path is None:
@@ -192,6 +194,28 @@ def ptr(a: np.ndarray | None) -> int | None:
         return None
     assert a.flags["C_CONTIGUOUS"]
     return a.ctypes.data
+
+
+def pack_segments(srcs: list[np.ndarray], starts: np.ndarray, lens: np.ndarray, sel: np.ndarray | None = None,
+                  rc: np.ndarray | None = None, threads: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Concatenate byte segments of the uint8 arrays in srcs (see mando_pack_segments); returns
+    (bytes uint8 array, offsets int64 with n+1 entries)."""
+    lib = load()
+    n = int(len(starts))
+    lens = np.ascontiguousarray(lens, dtype=np.int64)
+    off = np.zeros(n + 1, dtype=np.int64)
+    if n:
+        np.cumsum(lens, out=off[1:])
+    out = np.empty(max(int(off[-1]), 1), dtype=np.uint8)
+    if n == 0:
+        return out[:0], off
+    keep = [np.ascontiguousarray(s, dtype=np.uint8) for s in srcs]
+    ptrs = (ctypes.c_void_p * len(keep))(*[k.ctypes.data for k in keep])
+    starts = np.ascontiguousarray(starts, dtype=np.int64)
+    sel_a = None if sel is None else np.ascontiguousarray(sel, dtype=np.int8)
+    rc_a = None if rc is None else np.ascontiguousarray(rc, dtype=np.int8)
+    check(lib.mando_pack_segments(ptrs, ptr(sel_a), ptr(starts), ptr(lens), ptr(rc_a), n, ptr(out), ptr(off), threads))
+    return out[:int(off[-1])], off
 
 
 class Context:

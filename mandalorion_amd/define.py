@@ -36,60 +36,107 @@ def revcomp(s: str) -> str:
     return s.encode().translate(COMP)[::-1].decode()
 
 
-def gpu_orient(groups: Sequence[Sequence[str]], device: int = 0, max_hits: int = 4) -> list[list[list[int]]]:
-    """Per group, per read: the strands (+1/-1) of its primary hits against the group's first read."""
+def gpu_orient(seqs, seq_off, grp_off, device: int = 0, max_hits: int = 4):
+    """Per read: the strands (+1/-1) of its primary hits against its group's first read (HIP)."""
     from . import orient
 
-    return orient.orient_batch(groups, device=device, max_hits=max_hits)
+    return orient.orient_packed(seqs, seq_off, grp_off, device=device, max_hits=max_hits)
 
 
-def gpu_consensus(groups: Sequence[Sequence[str]], seeding: Sequence[bool], device: int = 0) -> list[str]:
+def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0):
     from . import poa
 
-    if not groups:
-        return []
-    return poa.poa_consensus_batch(groups, seeding=seeding, device=device)
+    return poa.poa_consensus_packed(seqs, seq_off, grp_off, seeding=seeding, device=device)
 
 
 def _roots(out_tmp: str) -> list[str]:
     roots = set()
     for f in os.listdir(out_tmp):
         if os.path.isfile(os.path.join(out_tmp, f)) and ".psl" in f:
-            root = f.split(".psl")[0]
-            root.split("~")  # chrom~start~end (a '~' in a chrom name breaks the reference too)
-            roots.add(root)
+            roots.add(f.split(".psl")[0])  # chrom~start~end (a '~' in a chrom breaks the reference too)
     return sorted(roots, key=lambda x: (x.split("~")[0], int(x.split("~")[1])))
 
 
-def assemble(res: cluster.ClusterResult, iso_idx: Sequence[int], strands: list[list[list[int]]]):
-    """determine_consensus (SpliceDefineConsensus.py:876-931) minus the POA call, per isoform.
+class Assembly:
+    """determine_consensus (SpliceDefineConsensus.py:876-931) minus the POA call, for every isoform at
+    once, on arrays.  Emissions: every primary hit of a subsampled read writes the read once, in hit
+    order, re-bound by the hits before it (SDC:902-907); the isoform's sequences are its emissions."""
 
-    Returns (direct, poa_groups, poa_seeding, poa_owner): direct[i] is the consensus when no POA run
-    is needed (<=2 oriented sequences), else None and the isoform's group is in poa_groups."""
-    direct: list[str | None] = []
-    groups, seeding, owner, firsts = [], [], [], []
-    for gi, i in enumerate(iso_idx):
-        sub = res.subsample(i)
-        seqs, lens = [], []
-        for r, st in zip(sub, strands[gi]):
-            s = res.seq(int(r))
-            lens.append(len(s))
-            for strand in st:  # every primary hit writes the (re-bound) sequence once (SDC:902-907)
-                if strand == -1:
-                    s = revcomp(s)
-                seqs.append(s)
-        if not seqs:
-            raise IndexError(f"isoform {i}: no subsampled read maps to the first one "
+    def __init__(self, res: cluster.ClusterResult, hits: np.ndarray, n_hits: np.ndarray):
+        sub_off = res.sub_off
+        n_iso = len(sub_off) - 1
+        n_sub = int(sub_off[-1])
+        hits = np.asarray(hits).reshape(n_sub, -1) if n_sub else np.zeros((0, 1), np.int8)
+        nh = np.asarray(n_hits, dtype=np.int64)[:n_sub]
+        H = hits.shape[1]
+        valid = np.arange(H)[None, :] < nh[:, None]
+        signs = np.cumprod(np.where(valid, hits.astype(np.int64), 1), axis=1)
+        self.e_read = np.repeat(np.arange(n_sub), nh)            # emission -> subsample slot
+        self.e_sign = signs[valid]                                # row-major = hit order per read
+        iso_of_sub = np.repeat(np.arange(n_iso), np.diff(sub_off))
+        self.e_iso = iso_of_sub[self.e_read] if n_sub else np.zeros(0, np.int64)
+        self.n_emit = np.bincount(self.e_iso, minlength=n_iso) if n_iso else np.zeros(0, np.int64)
+        empty = np.nonzero(self.n_emit == 0)[0]
+        if len(empty):
+            raise IndexError(f"isoform {int(empty[0])}: no subsampled read maps to the first one "
                              "(the reference raises IndexError at SpliceDefineConsensus.py:912)")
-        if len(seqs) <= 2:
-            direct.append(seqs[0])
-        else:
-            direct.append(None)
-            groups.append(seqs)
-            seeding.append(bool(np.median(lens) >= 8000))
-            owner.append(gi)
-            firsts.append(seqs[0])
-    return direct, groups, seeding, owner, firsts
+        self.first_emit = np.searchsorted(self.e_iso, np.arange(n_iso))
+        self.direct = self.n_emit <= 2
+        self.poa_iso = np.nonzero(~self.direct)[0]
+        self.e_rec = res.sub[self.e_read] if n_sub else np.zeros(0, np.int64)
+        # -S when the median subsample length (all subsampled reads, mapped or not) is >= 8000
+        lens = res.seq_len[res.sub].astype(np.int64) if n_sub else np.zeros(0, np.int64)
+        self.seeding = np.array([np.median(lens[sub_off[i]:sub_off[i + 1]]) >= 8000 for i in self.poa_iso],
+                                dtype=np.uint8)
+        self.res = res
+
+    def poa_input(self):
+        sel = ~self.direct[self.e_iso]
+        rec = self.e_rec[sel]
+        seqs, off = _lib.pack_segments([self.res.text], self.res.seq_off[rec], self.res.seq_len[rec],
+                                       rc=(self.e_sign[sel] == -1).astype(np.int8))
+        grp = np.zeros(len(self.poa_iso) + 1, dtype=np.int64)
+        np.cumsum(self.n_emit[self.poa_iso], out=grp[1:])
+        return seqs, off, grp
+
+
+def _fasta_and_r2i(names_src, name_start, name_len, mem_off, cons_src, cons_sel, cons_start, cons_len, cons_rc,
+                   counter0: int = 0):
+    """Isoform_Consensi.fasta and reads2isoforms.txt bytes for isoforms in output order
+    (defineIsoforms.py:155-166): '>Isoform{k}_{n}\n{consensus}\n' and '{name}\tIsoform{k}_{n}\n'."""
+    n_iso = len(mem_off) - 1
+    n_mem = np.diff(mem_off)
+    labels = [f"Isoform{counter0 + i + 1}_{int(n_mem[i])}" for i in range(n_iso)]
+    head = "".join(f">{l}\n" for l in labels).encode()
+    suf = "".join(f"\t{l}\n" for l in labels).encode()
+    aux = np.frombuffer(head + b"\n" + suf or b"\0", dtype=np.uint8)
+    hl = np.array([len(l) + 2 for l in labels], dtype=np.int64)
+    hs = np.zeros(n_iso, dtype=np.int64)
+    if n_iso:
+        hs[1:] = np.cumsum(hl)[:-1]
+    nl_pos = len(head)
+    sl = hl.copy()  # "\t" + label + "\n" has the same length as ">" + label + "\n"
+    ss = nl_pos + 1 + hs
+    # FASTA: [header (aux)] [consensus (its source)] ["\n" (aux)] per isoform; sources: 0 aux, 1.. cons
+    srcs = [aux] + list(cons_src)
+    sel = np.empty(3 * n_iso, dtype=np.int8)
+    st = np.empty(3 * n_iso, dtype=np.int64)
+    ln = np.empty(3 * n_iso, dtype=np.int64)
+    rc = np.zeros(3 * n_iso, dtype=np.int8)
+    sel[0::3], st[0::3], ln[0::3] = 0, hs, hl
+    sel[1::3], st[1::3], ln[1::3], rc[1::3] = 1 + np.asarray(cons_sel), cons_start, cons_len, cons_rc
+    sel[2::3], st[2::3], ln[2::3] = 0, nl_pos, 1
+    fasta, _ = _lib.pack_segments(srcs, st, ln, sel=sel, rc=rc)
+    # reads2isoforms: [name (names_src)] [suffix (aux)] per member
+    m = int(mem_off[-1])
+    iso_of_mem = np.repeat(np.arange(n_iso), n_mem)
+    sel = np.empty(2 * m, dtype=np.int8)
+    st = np.empty(2 * m, dtype=np.int64)
+    ln = np.empty(2 * m, dtype=np.int64)
+    sel[0::2], st[0::2], ln[0::2] = 1, name_start, name_len
+    sel[1::2], st[1::2], ln[1::2] = 0, ss[iso_of_mem], sl[iso_of_mem]
+    r2i, _ = _lib.pack_segments([aux, names_src], st, ln, sel=sel)
+    return fasta, r2i
 
 
 def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", splice_site_width: int = 1,
@@ -98,10 +145,11 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                     downstream_buffer: int = 50, seed: int = 0, device: int = 0,
                     orient_fn: Callable | None = None, consensus_fn: Callable | None = None,
                     rank: int = 0, world: int = 1, comm=None, verbose: bool = False) -> dict:
-    """Runs the D module on <path>/tmp_SS/*.psl.  orient_fn / consensus_fn default to the HIP path."""
+    """Runs the D module on <path>/tmp_SS/*.psl.  orient_fn(seqs, seq_off, grp_off) -> (hits, n_hits) and
+    consensus_fn(seqs, seq_off, grp_off, seeding) -> (cons bytes, cons_off) default to the HIP path."""
     t0 = time.perf_counter()
-    orient_fn = orient_fn or (lambda g: gpu_orient(g, device=device))
-    consensus_fn = consensus_fn or (lambda g, s: gpu_consensus(g, s, device=device))
+    orient_fn = orient_fn or (lambda s, o, g: gpu_orient(s, o, g, device=device))
+    consensus_fn = consensus_fn or (lambda s, o, g, sd: gpu_consensus(s, o, g, sd, device=device))
     out_path = path + "/"
     out_tmp = out_path + "/tmp_SS"
     wl = list(white_list_polyA)
@@ -138,37 +186,54 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         raise RuntimeError(f"locus {my_roots[i]}: {cluster.STATUS.get(int(res.locus_status[i]), res.locus_status[i])} "
                            "(the reference's locus worker raises here)")
     t2 = time.perf_counter()
-    n_iso = res.n_isoforms
-    iso_idx = list(range(n_iso))
-    og = [[res.seq(int(r)) for r in res.subsample(i)] for i in iso_idx]
-    strands = orient_fn(og)
+    # orientation: every subsampled read against its isoform's first subsampled read
+    o_seqs, o_off = _lib.pack_segments([res.text], res.seq_off[res.sub], res.seq_len[res.sub])
+    hits, n_hits = orient_fn(o_seqs, o_off, res.sub_off)
     t3 = time.perf_counter()
-    direct, groups, seeding, owner, firsts = assemble(res, iso_idx, strands)
-    cons = consensus_fn(groups, seeding)
-    for k, gi in enumerate(owner):
-        direct[gi] = cons[k] if cons[k] else firsts[k]
+    asm = Assembly(res, hits, n_hits)
+    p_seqs, p_off, p_grp = asm.poa_input()
+    cons, cons_off = consensus_fn(p_seqs, p_off, p_grp, asm.seeding)
     t4 = time.perf_counter()
-    # per-locus records for the writer: (root index, [(consensus, [names])...])
-    per_locus: dict[int, list] = {mine[li]: [] for li in range(len(my_roots))}
-    for i in iso_idx:
-        li = int(res.iso_locus[i])
-        per_locus[mine[li]].append((direct[i], [res.name(int(r)) for r in res.members(i)]))
+    # consensus of every isoform as a byte segment: POA output, else (<=2 sequences, or an empty POA
+    # result) the first emission, re-bound (SDC:911-926)
+    n_iso = res.n_isoforms
+    fe = asm.first_emit
+    c_sel = np.zeros(n_iso, dtype=np.int8)                      # 0: read text, 1: POA output
+    c_start = res.seq_off[asm.e_rec[fe]] if n_iso else np.zeros(0, np.int64)
+    c_len = res.seq_len[asm.e_rec[fe]].astype(np.int64) if n_iso else np.zeros(0, np.int64)
+    c_rc = (asm.e_sign[fe] == -1).astype(np.int8) if n_iso else np.zeros(0, np.int8)
+    plen = np.diff(cons_off)
+    use = plen > 0
+    pi = asm.poa_iso[use]
+    c_sel[pi] = 1
+    c_start[pi] = cons_off[:-1][use]
+    c_len[pi] = plen[use]
+    c_rc[pi] = 0
+    mem_off = res.mem_off
+    payload = dict(iso_root=np.asarray([mine[int(l)] for l in res.iso_locus], dtype=np.int64),
+                   cons=[res.text, cons], c_sel=c_sel, c_start=c_start, c_len=c_len, c_rc=c_rc,
+                   names=res.text, n_start=res.name_off[res.mem], n_len=res.name_len[res.mem].astype(np.int64),
+                   mem_off=mem_off)
     if world > 1:
-        per_locus = _gather(per_locus, rank, world, comm)
-    stats = {"loci": len(roots), "isoforms": n_iso, "poa_groups": len(groups),
-             "records": int(res.n_records), "poa_reads": int(sum(len(g) for g in groups)),
+        payload = _gather(payload, rank, world)
+    stats = {"loci": len(roots), "isoforms": n_iso, "poa_groups": int(len(asm.poa_iso)),
+             "records": int(res.n_records), "poa_reads": int(p_grp[-1]),
              "t_ingest": t1 - t0, "t_cluster": t2 - t1, "t_orient": t3 - t2, "t_poa": t4 - t3}
     if rank == 0:
-        counter = 0
-        with open(out_path + "/Isoform_Consensi.fasta", "w") as out, open(out_path + "/reads2isoforms.txt", "w") as r2i:
-            for ri in range(len(roots)):
-                for consensus, names in per_locus.get(ri, []):
-                    counter += 1
-                    nm = "Isoform" + str(counter) + "_" + str(len(names))
-                    out.write(">%s\n%s\n" % (nm, consensus))
-                    for n in names:
-                        r2i.write("%s\t%s\n" % (n, nm))
-        stats["written_isoforms"] = counter
+        order = np.argsort(payload["iso_root"], kind="stable")   # sorted roots x IsoDict order
+        mo = payload["mem_off"]
+        cnt = np.diff(mo)[order]
+        new_off = np.zeros(len(order) + 1, dtype=np.int64)
+        np.cumsum(cnt, out=new_off[1:])
+        midx = np.concatenate([np.arange(mo[i], mo[i + 1]) for i in order]) if len(order) else np.zeros(0, np.int64)
+        fasta, r2i = _fasta_and_r2i(payload["names"], payload["n_start"][midx], payload["n_len"][midx], new_off,
+                                    payload["cons"], payload["c_sel"][order], payload["c_start"][order],
+                                    payload["c_len"][order], payload["c_rc"][order])
+        with open(out_path + "/Isoform_Consensi.fasta", "wb") as fh:
+            fh.write(fasta.tobytes())
+        with open(out_path + "/reads2isoforms.txt", "wb") as fh:
+            fh.write(r2i.tobytes())
+        stats["written_isoforms"] = int(len(order))
     stats["t_total"] = time.perf_counter() - t0
     res.close()
     if verbose and rank == 0:
@@ -176,56 +241,95 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     return stats
 
 
-def _gather(per_locus: dict, rank: int, world: int, comm) -> dict:
+def _compact(payload: dict) -> dict:
+    """Copy the referenced bytes out of the (large) locus text, so a rank ships only its results."""
+    cons_text = payload["cons"][0]
+    tsel = payload["c_sel"] == 0
+    ct, co = _lib.pack_segments([cons_text], payload["c_start"][tsel], payload["c_len"][tsel],
+                                rc=payload["c_rc"][tsel])
+    c_start = payload["c_start"].copy()
+    c_rc = payload["c_rc"].copy()
+    c_start[tsel] = co[:-1]
+    c_rc[tsel] = 0
+    names, noff = _lib.pack_segments([payload["names"]], payload["n_start"], payload["n_len"])
+    return dict(iso_root=payload["iso_root"], cons=[ct, payload["cons"][1]], c_sel=payload["c_sel"], c_start=c_start,
+                c_len=payload["c_len"], c_rc=c_rc, names=names, n_start=noff[:-1], n_len=payload["n_len"],
+                mem_off=payload["mem_off"])
+
+
+_FIELDS = ("iso_root", "c_sel", "c_start", "c_len", "c_rc", "n_start", "n_len", "mem_off")
+
+
+def _gather(payload: dict, rank: int, world: int) -> dict:
     """Reassembly on rank 0: one all-gather of byte counts, one of padded byte buffers (RCCL over xGMI
-    with the nccl backend, gloo on CPU)."""
+    with the nccl backend, gloo on CPU).  Each rank ships its isoforms' root indices, consensus bytes
+    and member names."""
     import torch
     import torch.distributed as dist
 
-    blob = _serialize(per_locus)
+    p = _compact(payload)
+    arrays = [np.ascontiguousarray(p[f]) for f in _FIELDS] + [p["cons"][0], p["cons"][1], p["names"]]
+    hdr = np.array([a.nbytes for a in arrays] + [a.dtype.num for a in arrays], dtype=np.int64)
+    blob = np.concatenate([hdr.view(np.uint8)] + [a.view(np.uint8).ravel() for a in arrays])
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
-    n = torch.tensor([len(blob)], dtype=torch.int64, device=dev)
+    n = torch.tensor([blob.size], dtype=torch.int64, device=dev)
     ns = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(ns, n)
     mx = int(max(int(x.item()) for x in ns))
     buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    if blob:
-        buf[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    buf[:blob.size] = torch.from_numpy(blob).to(dev)
     bufs = [torch.zeros_like(buf) for _ in range(world)]
     dist.all_gather(bufs, buf)
-    merged: dict[int, list] = {}
-    if rank == 0:
-        for k in range(world):
-            raw = bytes(bufs[k][: int(ns[k].item())].cpu().numpy())
-            merged.update(_deserialize(raw))
+    if rank != 0:
+        return payload
+    parts = []
+    na = len(arrays)
+    for k in range(world):
+        raw = bufs[k][: int(ns[k].item())].cpu().numpy()
+        h = raw[: 16 * na].view(np.int64)
+        sizes, kinds = h[:na], h[na:]
+        pos = 16 * na
+        arrs = []
+        for sz, kd in zip(sizes, kinds):
+            arrs.append(raw[pos:pos + sz].view(_dtype_of(int(kd))))
+            pos += int(sz)
+        parts.append(arrs)
+    # merge: concatenate fields, rebasing offsets into concatenated byte buffers
+    out = {f: [] for f in _FIELDS}
+    cons_t, cons_p, names = [], [], []
+    bt = bp = bn = bm = 0
+    for arrs in parts:
+        d = dict(zip(_FIELDS, arrs[:len(_FIELDS)]))
+        ct, cp, nm = arrs[len(_FIELDS):]
+        cs = d["c_start"].copy()
+        cs[d["c_sel"] == 0] += bt
+        cs[d["c_sel"] == 1] += bp
+        out["iso_root"].append(d["iso_root"])
+        out["c_sel"].append(d["c_sel"])
+        out["c_start"].append(cs)
+        out["c_len"].append(d["c_len"])
+        out["c_rc"].append(d["c_rc"])
+        out["n_start"].append(d["n_start"] + bn)
+        out["n_len"].append(d["n_len"])
+        out["mem_off"].append(d["mem_off"][1:] + bm if len(out["mem_off"]) else d["mem_off"] + bm)
+        bm += int(d["mem_off"][-1])
+        bt += ct.size
+        bp += cp.size
+        bn += nm.size
+        cons_t.append(ct)
+        cons_p.append(cp)
+        names.append(nm)
+    merged = {f: np.concatenate(v) for f, v in out.items()}
+    merged["cons"] = [np.concatenate(cons_t), np.concatenate(cons_p)]
+    merged["names"] = np.concatenate(names)
     return merged
 
 
-def _serialize(per_locus: dict) -> bytes:
-    parts = []
-    for ri, isos in per_locus.items():
-        parts.append(f"L\t{ri}\t{len(isos)}\n")
-        for consensus, names in isos:
-            parts.append(f"I\t{consensus}\t{len(names)}\n")
-            parts.append("\t".join(names) + "\n")
-    return "".join(parts).encode()
-
-
-def _deserialize(raw: bytes) -> dict:
-    out: dict[int, list] = {}
-    lines = raw.decode().split("\n")
-    i = 0
-    while i < len(lines) and lines[i]:
-        _, ri, niso = lines[i].split("\t")
-        i += 1
-        isos = []
-        for _ in range(int(niso)):
-            _, consensus, nn = lines[i].split("\t")
-            names = lines[i + 1].split("\t") if int(nn) else []
-            isos.append((consensus, names))
-            i += 2
-        out[int(ri)] = isos
-    return out
+def _dtype_of(num: int):
+    for t in (np.int64, np.int32, np.int8, np.uint8):
+        if np.dtype(t).num == num:
+            return np.dtype(t)
+    raise ValueError(num)
 
 
 def parser() -> argparse.ArgumentParser:

@@ -34,3 +34,19 @@ def orient_batch(groups: Sequence[Sequence[str | bytes]], device: int = 0, max_h
             r += 1
         out.append(gl)
     return out
+
+
+def orient_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, device: int = 0, max_hits: int = 4):
+    """Packed form: returns (hits int8 [n_reads, max_hits], n_hits int32 [n_reads])."""
+    ctx = _lib.context(device)
+    n = int(len(seq_off)) - 1
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
+    if seqs.size == 0:
+        seqs = np.zeros(1, dtype=np.uint8)
+    hits = np.zeros((max(n, 1), max_hits), dtype=np.int8)
+    nh = np.zeros(max(n, 1), dtype=np.int32)
+    if len(grp_off) > 1:
+        _lib.check(ctx.lib.mando_orient_batch(ctx.handle, _lib.ptr(seqs), _lib.ptr(np.ascontiguousarray(seq_off, np.int64)),
+                                              _lib.ptr(np.ascontiguousarray(grp_off, np.int64)), len(grp_off) - 1,
+                                              _lib.ptr(hits), max_hits, _lib.ptr(nh)))
+    return hits[:n], nh[:n]

@@ -72,3 +72,26 @@ def poa_consensus_batch(
     if return_cells:
         return out, cells[:n].copy()
     return out
+
+
+def poa_consensus_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, seeding=None,
+                         device: int = 0, params: _lib.PoaParams | None = None):
+    """Packed form (no per-read Python objects): uint8 reads + int64 offsets in, consensus bytes
+    (uint8) + int64 offsets (n_groups+1) out."""
+    ctx = _lib.context(device)
+    p = params or _lib.PoaParams.defaults()
+    n = int(len(grp_off)) - 1
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
+    if seqs.size == 0:
+        seqs = np.zeros(1, dtype=np.uint8)
+    seq_off = np.ascontiguousarray(seq_off, dtype=np.int64)
+    grp_off = np.ascontiguousarray(grp_off, dtype=np.int64)
+    seed_arr = None if seeding is None else np.ascontiguousarray(np.asarray(seeding, dtype=np.uint8))
+    cap = int(seq_off[-1] - seq_off[0]) * 2 + 1024
+    cons = np.zeros(cap, dtype=np.uint8)
+    cons_off = np.zeros(n + 1, dtype=np.int64)
+    if n > 0:
+        _lib.check(ctx.lib.mando_poa_batch(ctx.handle, _lib.ctypes.byref(p), _lib.ptr(seqs), _lib.ptr(seq_off),
+                                           _lib.ptr(grp_off), n, _lib.ptr(seed_arr), _lib.ptr(cons), cap,
+                                           _lib.ptr(cons_off), None))
+    return cons, cons_off

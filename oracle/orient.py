@@ -66,3 +66,21 @@ def minimizers(s: str) -> np.ndarray:
     out = np.zeros(max(len(s), 1), dtype=np.uint64)
     n = lib.orient_ref_minimizers(b.ctypes.data, len(s), out.ctypes.data, len(out))
     return out[:max(n, 0)]
+
+
+def orient_packed(seqs, seq_off, grp_off, max_hits: int = 4):
+    """Packed form (mirrors mandalorion_amd.orient.orient_packed)."""
+    lib = load()
+    n = len(seq_off) - 1
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
+    if seqs.size == 0:
+        seqs = np.zeros(1, dtype=np.uint8)
+    so = np.ascontiguousarray(seq_off, dtype=np.int64)
+    go = np.ascontiguousarray(grp_off, dtype=np.int64)
+    hits = np.zeros((max(n, 1), max_hits), dtype=np.int8)
+    nh = np.zeros(max(n, 1), dtype=np.int32)
+    rc = lib.orient_ref_batch(seqs.ctypes.data, so.ctypes.data, go.ctypes.data, len(go) - 1, hits.ctypes.data,
+                              max_hits, nh.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"orient_ref_batch failed: {rc}")
+    return hits[:n], nh[:n]

@@ -77,3 +77,24 @@ def consensus_batch(groups: Sequence[Sequence[str]], params: Params | None = Non
     raw = out.tobytes()
     cons = [raw[cons_off[i]:cons_off[i + 1]].decode() for i in range(n)]
     return (cons, cells[:n].copy()) if return_cells else cons
+
+
+def consensus_packed(seqs, seq_off, grp_off, params: Params | None = None):
+    """Packed form of consensus_batch (mirrors mandalorion_amd.poa.poa_consensus_packed)."""
+    lib = load()
+    p = params or Params.defaults()
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
+    if seqs.size == 0:
+        seqs = np.zeros(1, dtype=np.uint8)
+    seq_off = np.ascontiguousarray(seq_off, dtype=np.int64)
+    grp_off = np.ascontiguousarray(grp_off, dtype=np.int64)
+    n = len(grp_off) - 1
+    cap = int(seq_off[-1] - seq_off[0]) * 2 + 1024
+    out = np.zeros(cap, dtype=np.uint8)
+    cons_off = np.zeros(n + 1, dtype=np.int64)
+    if n > 0:
+        rc = lib.poa_ref_batch(ctypes.addressof(p), seqs.ctypes.data, seq_off.ctypes.data, grp_off.ctypes.data, n,
+                               None, out.ctypes.data, cap, cons_off.ctypes.data, None)
+        if rc != 0:
+            raise RuntimeError(f"poa_ref_batch failed: {rc}")
+    return out, cons_off

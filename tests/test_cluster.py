@@ -17,7 +17,9 @@ import socket
 
 import pytest
 
-from mandalorion_amd import cluster, define, gtf, simdata
+import numpy as np
+
+from mandalorion_amd import _lib, cluster, define, gtf, simdata
 
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "cluster_vectors.json")))
 P = GOLD["params"]
@@ -35,13 +37,21 @@ def dataset(tmp_path_factory):
     return d, roots, info
 
 
-def _stub_orient(groups):
-    return [[[1] for _ in g] for g in groups]
+def _stub_orient(seqs, seq_off, grp_off):
+    """mappy stand-in of the fixture run: every read one forward primary hit."""
+    n = len(seq_off) - 1
+    return np.ones((n, 1), dtype=np.int8), np.ones(n, dtype=np.int32)
 
 
-def _stub_consensus(groups, seeding):
-    _stub_consensus.calls = list(zip(groups, seeding))
-    return [g[0] for g in groups]
+def _first_of_groups(seqs, seq_off, grp_off):
+    """abpoa stand-in of the fixture run: the group's first input sequence."""
+    first = grp_off[:-1]
+    return _lib.pack_segments([seqs], seq_off[first], seq_off[first + 1] - seq_off[first])
+
+
+def _stub_consensus(seqs, seq_off, grp_off, seeding):
+    _stub_consensus.calls = [(int(grp_off[i + 1] - grp_off[i]), bool(seeding[i])) for i in range(len(grp_off) - 1)]
+    return _first_of_groups(seqs, seq_off, grp_off)
 
 
 def _ann(info, roots):
@@ -86,6 +96,7 @@ def test_define_driver_files_byte_identical(dataset, seed, tmp_path):
     assert sha("reads2isoforms.txt") == exp["reads2isoforms_sha256"]
     assert stats["poa_groups"] == len(exp["abpoa_calls"])
     assert [s for _, s in _stub_consensus.calls] == [c["seeding"] for c in exp["abpoa_calls"]]
+    assert [n for n, _ in _stub_consensus.calls] == [len(c["names"]) for c in exp["abpoa_calls"]]
 
 
 def test_rebinding_and_fallbacks(dataset):
@@ -95,17 +106,35 @@ def test_rebinding_and_fallbacks(dataset):
     d, roots, _ = dataset
     res = cluster.cluster_loci([os.path.join(d, "tmp_SS", roots[0] + ".psl")], [roots[0].split("~")[0]], seed=0)
     sub = res.subsample(0)
-    assert len(sub) >= 3
+    n = len(sub)
+    assert n >= 3 and res.n_isoforms >= 1
+    nsub = int(res.sub_off[-1])
     s0 = res.seq(int(sub[0]))
-    st = [[1, -1]] + [[] for _ in sub[1:]]
-    direct, groups, seeding, owner, firsts = define.assemble(res, [0], [st])
-    # [s0, revcomp(s0)] -> two sequences -> direct consensus = s0
-    assert direct[0] == s0 and groups == []
-    st = [[-1]] + [[1] for _ in sub[1:]]
-    direct, groups, _, _, _ = define.assemble(res, [0], [st])
-    assert direct == [None] and groups[0][0] == define.revcomp(s0) and len(groups[0]) == len(sub)
+
+    def run(hits_rows):
+        hits = np.zeros((nsub, 4), dtype=np.int8)
+        nh = np.ones(nsub, dtype=np.int32)
+        for r, row in enumerate(hits_rows):
+            hits[r, :len(row)] = row
+            nh[r] = len(row)
+        hits[len(hits_rows):, 0] = 1
+        return define.Assembly(res, hits, nh)
+
+    # read 0 maps twice (+, -), the others not at all -> [s0, revcomp(s0)] -> direct consensus = s0
+    a = run([[1, -1]] + [[] for _ in sub[1:]])
+    assert bool(a.direct[0]) and a.n_emit[0] == 2 and list(a.e_sign[:2]) == [1, -1]
+    # read 0 on '-': the first sequence is its reverse complement; everything goes to the POA
+    a = run([[-1]] + [[1] for _ in sub[1:]])
+    assert not a.direct[0]
+    seqs, off, grp = a.poa_input()
+    assert bytes(seqs[off[0]:off[1]]).decode() == define.revcomp(s0) and grp[1] == n
+    # second hit of a '-' read flips it back (re-binding): [-1, -1] -> revcomp, then forward again
+    a = run([[-1, -1]] + [[1] for _ in sub[1:]])
+    seqs, off, _ = a.poa_input()
+    assert bytes(seqs[off[0]:off[1]]).decode() == define.revcomp(s0)
+    assert bytes(seqs[off[1]:off[2]]).decode() == s0
     with pytest.raises(IndexError):
-        define.assemble(res, [0], [[[] for _ in sub]])
+        run([[] for _ in sub])
 
 
 def _free_port():
@@ -127,7 +156,8 @@ def _rank_main(rank, world, port, d, gtf_path, seed, q):
                                     white_list_polyA=P["white_list_polyA"].split(","), threads=2,
                                     junctions=P["junctions"], upstream_buffer=P["upstream_buffer"],
                                     downstream_buffer=P["downstream_buffer"], seed=seed, orient_fn=_stub_orient,
-                                    consensus_fn=lambda g, s: [x[0] for x in g], rank=rank, world=world)
+                                    consensus_fn=lambda s, o, g, sd: _first_of_groups(s, o, g), rank=rank,
+                                    world=world)
         q.put((rank, st["loci"], st["isoforms"]))
     finally:
         dist.destroy_process_group()

@@ -37,7 +37,7 @@ def test_define_gpu_equals_cpu_restatement(gpu_ctx, tmp_path):
     gpu_fa, gpu_r2i = read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")
     assert hashlib.sha256(gpu_r2i).hexdigest() == GOLD["seeds"]["0"]["reads2isoforms_sha256"]
     assert st["poa_groups"] > 20
-    _run(d, info["gtf"], orient_fn=lambda g: oref.orient_batch(g),
-         consensus_fn=lambda g, s: opoa.consensus_batch(g))
+    _run(d, info["gtf"], orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
+         consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g))
     assert read("Isoform_Consensi.fasta") == gpu_fa
     assert read("reads2isoforms.txt") == gpu_r2i
