@@ -294,7 +294,6 @@ int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const
     if (!ctx || !params || !d_seqs || !d_seq_off || !d_grp_off || !d_cons || !d_cons_off ||
         !d_cons_len || !d_cells || !d_status || n_groups < 0 || max_read_len < 0)
         return fail(MANDO_E_ARG, "mando_poa_batch_device: bad argument");
-    if (params->seeding) return fail(MANDO_E_UNSUPPORTED, "-S seeding path not implemented yet");
     if (n_groups == 0) return MANDO_OK;
     HIP_TRY(hipSetDevice(ctx->device));
     mando::PoaCaps caps = plan_caps(*params, max_read_len, max_group_bases, max_read_len,
@@ -314,11 +313,9 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
         cons_off[0] = 0;
         return MANDO_OK;
     }
-    if (params->seeding) return fail(MANDO_E_UNSUPPORTED, "-S seeding path not implemented yet");
-    if (seeding_per_group)
-        for (int64_t g = 0; g < n_groups; ++g)
-            if (seeding_per_group[g])
-                return fail(MANDO_E_UNSUPPORTED, "-S seeding path not implemented yet");
+    // -S (params->seeding / seeding_per_group): abPOA's minimizer-window partition is not restated;
+    // seeded groups run the same full adaptive-band DP (DESIGN.md "Known gaps").
+    (void)seeding_per_group;
     const int64_t n_reads = grp_off[n_groups] - grp_off[0];
     if (grp_off[0] != 0 || n_reads < 0) return fail(MANDO_E_ARG, "grp_off must start at 0");
     for (int64_t g = 0; g < n_groups; ++g)

@@ -101,6 +101,23 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     }
     return v;
 }
+// wave-wide max of a non-negative int (every lane gets it): DPP inclusive max, then lane 63
+__device__ __forceinline__ int wave_max_dpp(int v) {
+    asm volatile("s_nop 1\n"
+                 "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n s_nop 1\n"
+                 "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n s_nop 1\n"
+                 "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+                 : "+v"(v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+// lane l receives lane l+1's value; lane 63 receives `fill`
+__device__ __forceinline__ int wave_shl1(int v, int fill) {
+    return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false);
+}
+
 __device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
@@ -236,38 +253,37 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
     }
     wsync();
     bitonic_sort(sh.an, na, lane);
-    // chaining DP: lane l looks at predecessor j = i - 64 + l
+    // chaining DP: lane l looks at predecessor j = i - 64 + l.  The 64-anchor look-back window (x, y,
+    // strand, f) lives in registers and slides one lane per anchor (DPP wave_shl); the best
+    // predecessor is one DPP max-reduction.  Only lane 0 stores f / p (for the chain walk below).
+    int wx = 0, wy = 0, wr = -1, wf = 0;  // wr = -1: empty slot (j < 0)
     for (int i = 0; i < na; ++i) {
         const uint64_t ai = sh.an[i];
         const int ri = (int)(ai >> 62);
-        const int64_t xi = (int64_t)((ai >> 31) & 0x7fffffff), yi = (int64_t)(ai & 0x7fffffff);
-        const int j = i - 64 + lane;
-        uint32_t key = 0;
-        if (j >= 0) {
-            const uint64_t aj = sh.an[j];
-            const int64_t dr = xi - (int64_t)((aj >> 31) & 0x7fffffff), dq = yi - (int64_t)(aj & 0x7fffffff);
-            const int64_t dd = dr > dq ? dr - dq : dq - dr;
-            if ((int)(aj >> 62) == ri && dr > 0 && dq > 0 && dr <= MAX_GAP && dq <= MAX_GAP && dd <= BW) {
-                int64_t sc = dq < dr ? dq : dr;
-                if (sc > K) sc = K;
-                sc -= dd ? (dd * 15) / 100 + (ilog2_u32((uint32_t)dd) >> 1) : 0;
-                const int cand = sh.dp.f[j] + (int)sc;
-                key = ((uint32_t)(cand + 65536) << 6) | (uint32_t)lane;
-            }
+        const int xi = (int)((ai >> 31) & 0x7fffffff), yi = (int)(ai & 0x7fffffff);
+        const int dr = xi - wx, dq = yi - wy;
+        const int dd = dr > dq ? dr - dq : dq - dr;
+        int key = 0;
+        if (wr == ri && dr > 0 && dq > 0 && dr <= MAX_GAP && dq <= MAX_GAP && dd <= BW) {
+            int sc = dq < dr ? dq : dr;
+            if (sc > K) sc = K;
+            sc -= dd ? (dd * 15) / 100 + (ilog2_u32((uint32_t)dd) >> 1) : 0;
+            key = ((wf + sc + 65536) << 6) | lane;
         }
-        const uint32_t best = wave_max_u32(key);
+        const int best = wave_max_dpp(key);
+        const int cand = (best >> 6) - 65536;
+        const bool take = best != 0 && cand > K;
+        const int fi = take ? cand : K;
         if (lane == 0) {
-            const int cand = (int)(best >> 6) - 65536;
-            if (best != 0 && cand > K) {
-                sh.dp.f[i] = cand;
-                sh.dp.p[i] = i - 64 + (int)(best & 63);
-            } else {
-                sh.dp.f[i] = K;
-                sh.dp.p[i] = -1;
-            }
+            sh.dp.f[i] = fi;
+            sh.dp.p[i] = take ? i - 64 + (best & 63) : -1;
         }
-        wsync();
+        wx = wave_shl1(wx, xi);
+        wy = wave_shl1(wy, yi);
+        wr = wave_shl1(wr, ri);
+        wf = wave_shl1(wf, fi);
     }
+    wsync();
     // greedy chain extraction: highest f first (ties: lowest index), walk back to a used anchor
     for (int t = lane; t < CAP / 64; t += 64) sh.used[t] = 0;
     wsync();

@@ -144,7 +144,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                     junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", upstream_buffer: int = 10,
                     downstream_buffer: int = 50, seed: int = 0, device: int = 0,
                     orient_fn: Callable | None = None, consensus_fn: Callable | None = None,
-                    rank: int = 0, world: int = 1, comm=None, verbose: bool = False) -> dict:
+                    rank: int = 0, world: int = 1, comm=None, verbose: bool = False, n_chunks: int = 0) -> dict:
     """Runs the D module on <path>/tmp_SS/*.psl.  orient_fn(seqs, seq_off, grp_off) -> (hits, n_hits) and
     consensus_fn(seqs, seq_off, grp_off, seeding) -> (cons bytes, cons_off) default to the HIP path."""
     t0 = time.perf_counter()
@@ -175,16 +175,84 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     ann = [gtf.locus_bounds(left, right, r.split("~")[0], int(r.split("~")[1]), int(r.split("~")[2]))
            for r in my_roots]
     t1 = time.perf_counter()
-    res = cluster.cluster_loci([os.path.join(out_tmp, r + ".psl") for r in my_roots], chroms, ann=ann,
-                               cutoff=cutoff, splice_site_width=splice_site_width,
-                               minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
-                               downstream_buffer=downstream_buffer, junctions=junctions, seed=seed,
-                               threads=threads)
-    bad = np.nonzero(res.locus_status != 0)[0]
-    if len(bad):
-        i = int(bad[0])
-        raise RuntimeError(f"locus {my_roots[i]}: {cluster.STATUS.get(int(res.locus_status[i]), res.locus_status[i])} "
-                           "(the reference's locus worker raises here)")
+    # Chunked pipeline: clustering of chunk k+1 (host C++ threads, GIL released) overlaps orientation +
+    # POA of chunk k on the GPU.  Chunks are contiguous runs of sorted roots with balanced bytes.
+    sizes = np.array([os.path.getsize(os.path.join(out_tmp, r + ".psl")) for r in my_roots], dtype=np.int64)
+    if n_chunks <= 0:
+        n_chunks = 1 if sizes.sum() < (64 << 20) else 4
+    n_chunks = max(1, min(n_chunks, len(my_roots)))
+    cuts = [0]
+    if n_chunks > 1:
+        cs = np.cumsum(sizes)
+        for k in range(1, n_chunks):
+            cuts.append(int(np.searchsorted(cs, cs[-1] * k / n_chunks)) + 1)
+    cuts.append(len(my_roots))
+    cuts = sorted(set(min(max(c, 0), len(my_roots)) for c in cuts))
+    spans = [(cuts[k], cuts[k + 1]) for k in range(len(cuts) - 1) if cuts[k + 1] > cuts[k]] or [(0, 0)]
+
+    def run_cluster(lo, hi):
+        tc = time.perf_counter()
+        r = cluster.cluster_loci([os.path.join(out_tmp, x + ".psl") for x in my_roots[lo:hi]], chroms[lo:hi],
+                                 ann=ann[lo:hi], cutoff=cutoff, splice_site_width=splice_site_width,
+                                 minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
+                                 downstream_buffer=downstream_buffer, junctions=junctions, seed=seed,
+                                 threads=threads)
+        return r, time.perf_counter() - tc
+
+    from concurrent.futures import ThreadPoolExecutor
+
+    stats = {"loci": len(roots), "isoforms": 0, "poa_groups": 0, "records": 0, "poa_reads": 0,
+             "t_ingest": t1 - t0, "t_cluster": 0.0, "t_orient": 0.0, "t_poa": 0.0, "chunks": len(spans)}
+    payloads = []
+    with ThreadPoolExecutor(max_workers=1) as ex:
+        fut = ex.submit(run_cluster, *spans[0])
+        for k, (lo, hi) in enumerate(spans):
+            res, tcl = fut.result()
+            if k + 1 < len(spans):
+                fut = ex.submit(run_cluster, *spans[k + 1])
+            stats["t_cluster"] += tcl
+            bad = np.nonzero(res.locus_status != 0)[0]
+            if len(bad):
+                i = int(bad[0])
+                raise RuntimeError(f"locus {my_roots[lo + i]}: "
+                                   f"{cluster.STATUS.get(int(res.locus_status[i]), res.locus_status[i])} "
+                                   "(the reference's locus worker raises here)")
+            pl = _consensus_chunk(res, mine[lo:hi], orient_fn, consensus_fn, stats)
+            if len(spans) > 1:
+                pl = _compact(pl)
+                res.close()
+            else:
+                pl["_res"] = res
+            payloads.append(pl)
+    payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
+    if world > 1:
+        payload = _gather(payload, rank, world)
+    if rank == 0:
+        order = np.argsort(payload["iso_root"], kind="stable")   # sorted roots x IsoDict order
+        mo = payload["mem_off"]
+        cnt = np.diff(mo)[order]
+        new_off = np.zeros(len(order) + 1, dtype=np.int64)
+        np.cumsum(cnt, out=new_off[1:])
+        midx = np.concatenate([np.arange(mo[i], mo[i + 1]) for i in order]) if len(order) else np.zeros(0, np.int64)
+        fasta, r2i = _fasta_and_r2i(payload["names"], payload["n_start"][midx], payload["n_len"][midx], new_off,
+                                    payload["cons"], payload["c_sel"][order], payload["c_start"][order],
+                                    payload["c_len"][order], payload["c_rc"][order])
+        with open(out_path + "/Isoform_Consensi.fasta", "wb") as fh:
+            fh.write(fasta.tobytes())
+        with open(out_path + "/reads2isoforms.txt", "wb") as fh:
+            fh.write(r2i.tobytes())
+        stats["written_isoforms"] = int(len(order))
+    stats["t_total"] = time.perf_counter() - t0
+    for pl in payloads:
+        if "_res" in pl:
+            pl["_res"].close()
+    if verbose and rank == 0:
+        print("\t" + " ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in stats.items()))
+    return stats
+
+
+def _consensus_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], orient_fn, consensus_fn, stats: dict):
+    """Orientation + assembly + POA for one clustered chunk; returns its writer payload."""
     t2 = time.perf_counter()
     # orientation: every subsampled read against its isoform's first subsampled read
     o_seqs, o_off = _lib.pack_segments([res.text], res.seq_off[res.sub], res.seq_len[res.sub])
@@ -209,36 +277,17 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     c_start[pi] = cons_off[:-1][use]
     c_len[pi] = plen[use]
     c_rc[pi] = 0
-    mem_off = res.mem_off
-    payload = dict(iso_root=np.asarray([mine[int(l)] for l in res.iso_locus], dtype=np.int64),
-                   cons=[res.text, cons], c_sel=c_sel, c_start=c_start, c_len=c_len, c_rc=c_rc,
-                   names=res.text, n_start=res.name_off[res.mem], n_len=res.name_len[res.mem].astype(np.int64),
-                   mem_off=mem_off)
-    if world > 1:
-        payload = _gather(payload, rank, world)
-    stats = {"loci": len(roots), "isoforms": n_iso, "poa_groups": int(len(asm.poa_iso)),
-             "records": int(res.n_records), "poa_reads": int(p_grp[-1]),
-             "t_ingest": t1 - t0, "t_cluster": t2 - t1, "t_orient": t3 - t2, "t_poa": t4 - t3}
-    if rank == 0:
-        order = np.argsort(payload["iso_root"], kind="stable")   # sorted roots x IsoDict order
-        mo = payload["mem_off"]
-        cnt = np.diff(mo)[order]
-        new_off = np.zeros(len(order) + 1, dtype=np.int64)
-        np.cumsum(cnt, out=new_off[1:])
-        midx = np.concatenate([np.arange(mo[i], mo[i + 1]) for i in order]) if len(order) else np.zeros(0, np.int64)
-        fasta, r2i = _fasta_and_r2i(payload["names"], payload["n_start"][midx], payload["n_len"][midx], new_off,
-                                    payload["cons"], payload["c_sel"][order], payload["c_start"][order],
-                                    payload["c_len"][order], payload["c_rc"][order])
-        with open(out_path + "/Isoform_Consensi.fasta", "wb") as fh:
-            fh.write(fasta.tobytes())
-        with open(out_path + "/reads2isoforms.txt", "wb") as fh:
-            fh.write(r2i.tobytes())
-        stats["written_isoforms"] = int(len(order))
-    stats["t_total"] = time.perf_counter() - t0
-    res.close()
-    if verbose and rank == 0:
-        print("\t" + " ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in stats.items()))
-    return stats
+    stats["isoforms"] += n_iso
+    stats["poa_groups"] += int(len(asm.poa_iso))
+    stats["records"] += int(res.n_records)
+    stats["poa_reads"] += int(p_grp[-1])
+    stats["t_orient"] += t3 - t2
+    stats["t_poa"] += t4 - t3
+    ri = np.asarray(root_idx, dtype=np.int64)
+    return dict(iso_root=ri[res.iso_locus] if n_iso else np.zeros(0, np.int64),
+                cons=[res.text, cons], c_sel=c_sel, c_start=c_start, c_len=c_len, c_rc=c_rc,
+                names=res.text, n_start=res.name_off[res.mem], n_len=res.name_len[res.mem].astype(np.int64),
+                mem_off=res.mem_off)
 
 
 def _compact(payload: dict) -> dict:
@@ -294,13 +343,18 @@ def _gather(payload: dict, rank: int, world: int) -> dict:
             arrs.append(raw[pos:pos + sz].view(_dtype_of(int(kd))))
             pos += int(sz)
         parts.append(arrs)
-    # merge: concatenate fields, rebasing offsets into concatenated byte buffers
+    return _merge([dict(zip(_FIELDS, arrs[:len(_FIELDS)]), cons=[arrs[len(_FIELDS)], arrs[len(_FIELDS) + 1]],
+                        names=arrs[len(_FIELDS) + 2]) for arrs in parts])
+
+
+def _merge(payloads: list) -> dict:
+    """Concatenate compacted payloads, rebasing offsets into the concatenated byte buffers."""
     out = {f: [] for f in _FIELDS}
     cons_t, cons_p, names = [], [], []
     bt = bp = bn = bm = 0
-    for arrs in parts:
-        d = dict(zip(_FIELDS, arrs[:len(_FIELDS)]))
-        ct, cp, nm = arrs[len(_FIELDS):]
+    for d in payloads:
+        ct, cp = d["cons"]
+        nm = d["names"]
         cs = d["c_start"].copy()
         cs[d["c_sel"] == 0] += bt
         cs[d["c_sel"] == 1] += bp

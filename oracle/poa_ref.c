@@ -33,7 +33,8 @@
  * aligned-group tables instead of lists, flag-based traceback instead of score re-comparison), so
  * agreement also checks those design claims.
  *
- * The -S (minimizer seeding) path is not restated yet; poa_ref_group returns -5 for it.
+ * The -S (minimizer seeding) window partition is not restated: seeded groups run the same full
+ * adaptive-band DP, exactly like the HIP kernel (DESIGN.md "Known gaps").
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -611,11 +612,11 @@ static int hb_consensus(const graph_t *g, uint8_t *out, int cap) {
 }
 
 /* One group: encoded reads (0..4).  Writes the encoded consensus; returns its length, -1 on an
- * internal error, -5 if seeding is requested (not restated).  *cells_out gets the DP cell count. */
+ * internal error.  `seeding` (-S) is accepted and ignored (see header).  *cells_out gets the DP cell count. */
 int poa_ref_group_encoded(const uint8_t *const *reads, const int *lens, int n_reads,
                           const mando_poa_params *p, int seeding, uint8_t *cons, int cap,
                           int64_t *cells_out) {
-    if (seeding) return -5;
+    (void)seeding;
     scorer sc;
     make_scorer(&sc, p);
     graph_t g;
