@@ -326,9 +326,7 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
     if (total > 0 && !seqs) return fail(MANDO_E_ARG, "null seqs");
     HIP_TRY(hipSetDevice(ctx->device));
 
-    // encode + per-group statistics
-    std::vector<uint8_t> enc((size_t)std::max<int64_t>(total, 1));
-    for (int64_t i = 0; i < total; ++i) enc[(size_t)i] = g_enc[seqs[seq_off[0] + i]];
+    // per-group statistics (the bases are uploaded as ASCII and encoded on the device)
     std::vector<int64_t> soff((size_t)n_reads + 1);
     for (int64_t r = 0; r <= n_reads; ++r) soff[(size_t)r] = seq_off[r] - seq_off[0];
     std::vector<GroupStat> gs((size_t)n_groups);
@@ -359,7 +357,7 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
     });
 
     int rc;
-    if ((rc = ctx->seq.ensure(enc.size())) || (rc = ctx->seq_off.ensure(soff.size() * 8)) ||
+    if ((rc = ctx->seq.ensure((size_t)std::max<int64_t>(total, 1))) || (rc = ctx->seq_off.ensure(soff.size() * 8)) ||
         (rc = ctx->grp_off.ensure(((size_t)n_groups + 1) * 8)) ||
         (rc = ctx->gorder.ensure((size_t)n_groups * 4)) ||
         (rc = ctx->cons_off.ensure(((size_t)n_groups + 1) * 8)) ||
@@ -370,7 +368,10 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
         return rc;
     std::vector<int64_t> goff((size_t)n_groups + 1);
     for (int64_t g = 0; g <= n_groups; ++g) goff[(size_t)g] = grp_off[g];
-    HIP_TRY(hipMemcpyAsync(ctx->seq.p, enc.data(), enc.size(), hipMemcpyHostToDevice, ctx->stream));
+    if (total > 0) {
+        HIP_TRY(hipMemcpyAsync(ctx->seq.p, seqs + seq_off[0], (size_t)total, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(mando::launch_encode(ctx->seq.as<uint8_t>(), total, ctx->stream));
+    }
     HIP_TRY(hipMemcpyAsync(ctx->seq_off.p, soff.data(), soff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->grp_off.p, goff.data(), goff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->cons_off.p, ccap.data(), ccap.size() * 8, hipMemcpyHostToDevice, ctx->stream));

@@ -126,6 +126,9 @@ int poa_blocks_per_cu(const PoaKArgs &a, int cap);
 // Launch the persistent POA kernel on `stream` with `n_slots` one-wave workgroups.
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream);
 
+// In-place ASCII -> base code (A C G T -> 0..3, either case; anything else -> 4) on the device.
+hipError_t launch_encode(uint8_t *buf, int64_t n, hipStream_t stream);
+
 // Device self-test of the wave primitives (scan/reduce); returns number of mismatches in *bad.
 hipError_t run_wave_selftest(int *d_bad, hipStream_t stream);
 

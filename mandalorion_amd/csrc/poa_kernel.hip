@@ -1608,6 +1608,36 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
     }
 }
 
+// ASCII -> 0..4, 16 bytes per thread (HBM-bound streaming map)
+__global__ void encode_kernel(uint8_t *buf, int64_t n) {
+    const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (i0 >= n) return;
+    auto code = [](uint32_t c) -> uint32_t {
+        c |= 0x20;  // lower case
+        return c == 'a' ? 0u : c == 'c' ? 1u : c == 'g' ? 2u : c == 't' ? 3u : 4u;
+    };
+    if (i0 + 16 <= n && (((uintptr_t)(buf + i0)) & 15) == 0) {
+        uint4 v = *reinterpret_cast<const uint4 *>(buf + i0);
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t x = w[k];
+            w[k] = code(x & 0xff) | (code((x >> 8) & 0xff) << 8) | (code((x >> 16) & 0xff) << 16) |
+                   (code(x >> 24) << 24);
+        }
+        *reinterpret_cast<uint4 *>(buf + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (int64_t i = i0; i < n && i < i0 + 16; ++i) buf[i] = (uint8_t)code(buf[i]);
+    }
+}
+
+hipError_t launch_encode(uint8_t *buf, int64_t n, hipStream_t stream) {
+    const int64_t threads = (n + 15) / 16;
+    const int64_t blocks = (threads + 255) / 256;
+    hipLaunchKernelGGL(encode_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, buf, n);
+    return hipGetLastError();
+}
+
 int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
     int nb = 0;
     const bool dflt = a.match == DefaultScores::match && a.mismatch == DefaultScores::mismatch &&

@@ -71,3 +71,23 @@ def test_mixed_lengths_one_batch():
     _, a = poa_cases.noisy_groups(30, (200, 900), (3, 10), seed=41)
     _, b = poa_cases.noisy_groups(2, (9000, 10000), (3, 5), seed=42)
     _check(a + b)
+
+
+def test_config5_deep_long_group():
+    """Config-5 shape: one isoform of 100 reads x ~8.5 kb (what the reference hands `abpoa -S`)."""
+    _check(poa_cases.noisy_groups(1, (8300, 8700), (100, 100), seed=55)[1])
+
+
+def test_config3_full_size_properties():
+    """BASELINE config 3 at full size per GPU is 20k groups; here 2k of them through the same launch
+    path, checked by size-independent properties: every consensus is non-empty ACGT, within 10 % of
+    the template length, and 50 strided groups match the CPU restatement byte for byte."""
+    import numpy as np
+    seqs, so, go, tmpl = synth.fast_groups(2000, (2700, 3300), (50, 50), seed=2025, threads=8, with_templates=True)
+    groups = synth.unpack_groups(seqs, so, go)
+    got = poa.poa_consensus_batch(groups)
+    assert all(g and set(g) <= set("ACGT") for g in got)
+    ratio = np.array([len(g) / len(t) for g, t in zip(got, tmpl)])
+    assert ratio.min() > 0.9 and ratio.max() < 1.1
+    pick = list(range(0, 2000, 40))
+    assert [got[i] for i in pick] == opoa.consensus_batch([groups[i] for i in pick])
