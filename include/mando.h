@@ -178,6 +178,12 @@ int mando_pack_segments(const uint8_t *const *src, const int8_t *sel, const int6
                         const int64_t *lens, const int8_t *rc, int64_t n, uint8_t *out,
                         const int64_t *out_off, int32_t threads);
 
+/* PSL ingest + locus split: `sort -k 14,14 -k 16,17n` (C locale) of the clean
+ * PSL (Mando.py:343-349) when sort_lines != 0, optional write of the sorted file, then
+ * get_chromosomes (SpliceDefineConsensus.py:442-495): one <out_dir>/<chrom>~<start>~<end>.psl per locus. */
+int mando_split_loci(const char *psl_path, const char *out_dir, int32_t sort_lines, const char *sorted_out,
+                     int64_t *n_records, int64_t *n_loci);
+
 #ifdef __cplusplus
 }
 #endif

@@ -4,8 +4,9 @@ Keeps the reference's command-line surface (/root/reference/Mando.py:22-205) so 
 `Mando.py -M D ...` can switch over unchanged.  Only the D module (defining isoforms) is built here:
 it runs mandalorion_amd.define (clustering on host C++ threads, orientation and POA consensus on the
 GPU) with exactly the arguments Mando.py passes to defineIsoforms.py (Mando.py:382-399).  The other
-modules (A alignment, P SAM->PSL, F filtering, Q quantification) are outside this build's scope
- and are reported and skipped.
+modules (A alignment, F filtering, Q quantification, and the SAM->PSL / clean_psl half of P) are outside
+this build's scope and are reported and skipped; P's sort + locus split (the D module's
+input) is built (mando_split_loci).
 """
 from __future__ import annotations
 
@@ -66,6 +67,22 @@ def main(argv: list[str] | None = None) -> int:
                   f"with the following parameters\n{str(a).replace('Namespace(', '').replace(')', '')}\n")
     os.makedirs(temp_path, exist_ok=True)
     for mod in a.Modules:
+        if mod == "P":
+            # locus split of module P (Mando.py:343-352): clean PSL -> sorted PSL + tmp_SS/<locus>.psl.
+            # SAM -> PSL (emtrey) and clean_psl are outside this build; a clean PSL must exist.
+            clean = temp_path + "/mm2Alignments.clean.psl"
+            if not os.path.exists(clean) or os.path.getsize(clean) == 0:
+                print("\tmodule P: mm2Alignments.clean.psl missing (emtrey / clean_psl are not part of this build)")
+                continue
+            import shutil
+
+            from . import psl
+
+            shutil.rmtree(temp_path + "/tmp_SS", ignore_errors=True)
+            nrec, nloc = psl.split_loci(clean, temp_path + "/tmp_SS", sort_lines=True,
+                                        sorted_out=temp_path + "/mm2Alignments.clean.sorted.psl")
+            print(f"\t\tsplit {nrec} psl entries into {nloc} loci")
+            continue
         if mod != "D":
             print(f"\tmodule {mod}: not part of this build (D module only), skipped")
             continue

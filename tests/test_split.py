@@ -1,0 +1,55 @@
+"""§8(f) row 1: PSL ingest + locus split (mando_split_loci) against the reference's own split
+(GNU `sort -k 14,14 -k 16,17n` + get_chromosomes) on the same shuffled input: identical sorted file
+and identical locus files (names and bytes).  Fixture: tests/golden/split_vectors.json."""
+import hashlib
+import importlib.util
+import json
+import os
+
+from mandalorion_amd import psl
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "split_vectors.json")))
+
+
+def _make_input(path):
+    spec = importlib.util.spec_from_file_location("msv", os.path.join(HERE, "golden", "make_split_vectors.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m.make_input(path)
+
+
+def test_split_matches_reference(tmp_path):
+    src = str(tmp_path / "clean.psl")
+    assert _make_input(src) == GOLD["records"]
+    srt = str(tmp_path / "clean.sorted.psl")
+    nrec, nloc = psl.split_loci(src, str(tmp_path / "tmp_SS"), sort_lines=True, sorted_out=srt)
+    assert nrec == GOLD["records"] and nloc == len(GOLD["loci"])
+    assert hashlib.sha256(open(srt, "rb").read()).hexdigest() == GOLD["sorted_sha256"]
+    got = {f: hashlib.sha256(open(tmp_path / "tmp_SS" / f, "rb").read()).hexdigest()
+           for f in sorted(os.listdir(tmp_path / "tmp_SS"))}
+    assert got == GOLD["loci"]
+
+
+def test_split_presorted_input_is_idempotent(tmp_path):
+    src = str(tmp_path / "clean.psl")
+    _make_input(src)
+    srt = str(tmp_path / "s1.psl")
+    psl.split_loci(src, str(tmp_path / "a"), sort_lines=True, sorted_out=srt)
+    psl.split_loci(srt, str(tmp_path / "b"), sort_lines=False)
+    assert sorted(os.listdir(tmp_path / "a")) == sorted(os.listdir(tmp_path / "b"))
+
+
+def test_mando_cli_P_then_D(tmp_path):
+    """`Mando.py -M PD` on a clean PSL: split, then the D module (orientation / POA stand-ins are not
+    injectable through the CLI, so only P and the D-module input checks run without a GPU)."""
+    from mandalorion_amd import mando
+
+    tmp = tmp_path / "tmp"
+    tmp.mkdir()
+    _make_input(str(tmp / "mm2Alignments.clean.psl"))
+    fa = tmp_path / "reads.fasta"
+    fa.write_text(">r\nACGT\n")
+    assert mando.main(["-p", str(tmp_path), "-f", str(fa), "-M", "P"]) == 0
+    assert sorted(os.listdir(tmp / "tmp_SS")) == sorted(GOLD["loci"])
+    assert hashlib.sha256(open(tmp / "mm2Alignments.clean.sorted.psl", "rb").read()).hexdigest() == GOLD["sorted_sha256"]
