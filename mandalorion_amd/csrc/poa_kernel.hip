@@ -698,11 +698,11 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
             }
         }
         if (va || vbb) *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)tpair;
-        if (narrow) {
+        if (narrow) {  // out-of-band columns hold -inf (see dp_row_fast)
             const int ibk = j0 & (kChunk - 1);
-            *reinterpret_cast<int2 *>(ringrow + ibk) = make_int2(Ha, Hb);
-            *reinterpret_cast<int2 *>(ringrow + kChunk + ibk) = make_int2(E1a, E1b);
-            *reinterpret_cast<int2 *>(ringrow + 2 * kChunk + ibk) = make_int2(E2a, E2b);
+            *reinterpret_cast<int2 *>(ringrow + ibk) = make_int2(va ? Ha : kNegInf, vbb ? Hb : kNegInf);
+            *reinterpret_cast<int2 *>(ringrow + kChunk + ibk) = make_int2(va ? E1a : kNegInf, vbb ? E1b : kNegInf);
+            *reinterpret_cast<int2 *>(ringrow + 2 * kChunk + ibk) = make_int2(va ? E2a : kNegInf, vbb ? E2b : kNegInf);
         }
         if (spill) {
             gint *sv = s.sv + svbase;
@@ -812,25 +812,38 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
     const int qa = (j0 >= 1 && j0 <= qlen) ? qa0 : 4;
     const int qb = (j0 < qlen) ? qb0 : 4;
     const int ia = (j0 - 1) & (kChunk - 1), ib = j0 & (kChunk - 1);
-    // predecessor 0
+    // Ring rows hold -inf outside their band (every writer masks its out-of-band columns), so when
+    // the columns this row reads, [beg-1, end], lie inside a predecessor's 128-column chunk, the ring
+    // values need no band masks.  A single predecessor is read twice (max and first-index ties are
+    // unchanged by a duplicate).  Otherwise the masked form below handles chunk aliasing.
+    const int pc0 = x0.x & ~1, pc1 = x1.x & ~1;
+    const bool nm0 = beg - 1 >= pc0 && end <= pc0 + kChunk - 1;
+    const bool nm1 = !two || (beg - 1 >= pc1 && end <= pc1 + kChunk - 1);
+    const bool nomask = __builtin_amdgcn_readfirstlane((int)(nm0 && nm1)) != 0;
     const int *r0p = &sh.dp.ring[p0 % kRing][0][0];
+    const int *r1p = two ? &sh.dp.ring[max(p1, 0) % kRing][0][0] : r0p;
     const int h0A = r0p[ia], h0B = r0p[ib];
     const int2 y01 = *reinterpret_cast<const int2 *>(r0p + kChunk + ib);
     const int2 y02 = *reinterpret_cast<const int2 *>(r0p + 2 * kChunk + ib);
-    // predecessor 1 (read unconditionally, masked when absent)
-    const int *r1p = &sh.dp.ring[max(p1, 0) % kRing][0][0];
     const int h1A = r1p[ia], h1B = r1p[ib];
     const int2 y11 = *reinterpret_cast<const int2 *>(r1p + kChunk + ib);
     const int2 y12 = *reinterpret_cast<const int2 *>(r1p + 2 * kChunk + ib);
-    const bool i0A = in_band(j0 - 1, x0.x, x0.y), i0B = in_band(j0, x0.x, x0.y), i0C = in_band(j1, x0.x, x0.y);
-    const bool i1A = two && in_band(j0 - 1, x1.x, x1.y), i1B = two && in_band(j0, x1.x, x1.y),
-               i1C = two && in_band(j1, x1.x, x1.y);
-    const int a0 = i0A ? h0A : kNegInf, b0 = i0B ? h0B : kNegInf;
-    const int a1 = i1A ? h1A : kNegInf, b1 = i1B ? h1B : kNegInf;
-    const int u0 = i0B ? y01.x : kNegInf, u1 = i1B ? y11.x : kNegInf;
-    const int v0 = i0C ? y01.y : kNegInf, v1 = i1C ? y11.y : kNegInf;
-    const int w0 = i0B ? y02.x : kNegInf, w1 = i1B ? y12.x : kNegInf;
-    const int z0 = i0C ? y02.y : kNegInf, z1 = i1C ? y12.y : kNegInf;
+    int a0, b0, a1, b1, u0, u1, v0, v1, w0, w1, z0, z1;
+    if (nomask) {
+        a0 = h0A, b0 = h0B, a1 = h1A, b1 = h1B;
+        u0 = y01.x, u1 = y11.x, v0 = y01.y, v1 = y11.y;
+        w0 = y02.x, w1 = y12.x, z0 = y02.y, z1 = y12.y;
+    } else {
+        const bool i0A = in_band(j0 - 1, x0.x, x0.y), i0B = in_band(j0, x0.x, x0.y), i0C = in_band(j1, x0.x, x0.y);
+        const bool i1A = two && in_band(j0 - 1, x1.x, x1.y), i1B = two && in_band(j0, x1.x, x1.y),
+                   i1C = two && in_band(j1, x1.x, x1.y);
+        a0 = i0A ? h0A : kNegInf, b0 = i0B ? h0B : kNegInf;
+        a1 = i1A ? h1A : kNegInf, b1 = i1B ? h1B : kNegInf;
+        u0 = i0B ? y01.x : kNegInf, u1 = i1B ? y11.x : kNegInf;
+        v0 = i0C ? y01.y : kNegInf, v1 = i1C ? y11.y : kNegInf;
+        w0 = i0B ? y02.x : kNegInf, w1 = i1B ? y12.x : kNegInf;
+        z0 = i0C ? y02.y : kNegInf, z1 = i1C ? y12.y : kNegInf;
+    }
     // first predecessor attaining the max (strict > keeps the earlier one)
     const int Mva = max(a0, a1), Mvb = max(b0, b1);
     const int mka = a1 > a0, mkb = b1 > b0;
@@ -881,9 +894,9 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
         kq[2] = (uint16_t)(k1b | (k2b << 8));
     }
     int *ringrow = &sh.dp.ring[r % kRing][0][0];
-    *reinterpret_cast<int2 *>(ringrow + ib) = make_int2(Ha, Hb);
-    *reinterpret_cast<int2 *>(ringrow + kChunk + ib) = make_int2(E1a, E1b);
-    *reinterpret_cast<int2 *>(ringrow + 2 * kChunk + ib) = make_int2(E2a, E2b);
+    *reinterpret_cast<int2 *>(ringrow + ib) = make_int2(va ? Ha : kNegInf, vbb ? Hb : kNegInf);
+    *reinterpret_cast<int2 *>(ringrow + kChunk + ib) = make_int2(va ? E1a : kNegInf, vbb ? E1b : kNegInf);
+    *reinterpret_cast<int2 *>(ringrow + 2 * kChunk + ib) = make_int2(va ? E2a : kNegInf, vbb ? E2b : kNegInf);
     if (far) {
         gint *sv = s.sv + svbase;
         sv[j0] = Ha;
