@@ -184,6 +184,16 @@ int mando_pack_segments(const uint8_t *const *src, const int8_t *sel, const int6
 int mando_split_loci(const char *psl_path, const char *out_dir, int32_t sort_lines, const char *sorted_out,
                      int64_t *n_records, int64_t *n_loci);
 
+/* SAM -> PSL, replacing `python3 emtrey.py -i sam -o psl -m -t T`
+ * (emtrey.py:31-193, called at Mando.py:336-341): one PSL line per mapped SAM record, input order, with
+ * the accuracy / cs / read-sequence columns when mando_mode != 0.  threads <= 0: all cores. */
+int mando_sam_to_psl(const char *sam_path, const char *psl_path, int32_t mando_mode, int32_t threads,
+                     int64_t *n_records);
+
+/* clean_psl (SpliceDefineConsensus.py:14-92, called at Mando.py:343): target gaps < 10 nt merged into
+ * their blocks; primary != 0 keeps only the first line per read name. */
+int mando_clean_psl(const char *in_path, const char *out_path, int32_t primary, int64_t *n_records);
+
 #ifdef __cplusplus
 }
 #endif

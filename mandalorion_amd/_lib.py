@@ -36,6 +36,8 @@ EXPORTED = (
     "mando_cluster_free",
     "mando_pack_segments",
     "mando_split_loci",
+    "mando_sam_to_psl",
+    "mando_clean_psl",
 )
 
 STATUS = {
@@ -171,6 +173,8 @@ def load(path: str | None = None):
         lib.mando_cluster_free.argtypes = [_P]
         lib.mando_cluster_free.restype = None
         lib.mando_split_loci.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _P, _P]
+        lib.mando_sam_to_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, _P]
+        lib.mando_clean_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, _P]
         lib.mando_pack_segments.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, ctypes.c_int32]
         if hasattr(lib, "mando_selftest"):
             lib.mando_selftest.argtypes = [_P, _P]

@@ -44,6 +44,7 @@
 
 #include "../../include/mando.h"
 #include "mt19937.h"
+#include "revcomp.h"
 
 namespace {
 
@@ -1181,18 +1182,11 @@ void mando_cluster_free(mando_cluster_result *r) { delete r; }
 
 // Host helper of the D driver: concatenates n byte segments into out (at out_off[i], caller-computed
 // exclusive prefix sums of lens).  Segment i is src[sel[i]] + starts[i], lens[i] bytes, reverse-
-// complemented (mappy.revcomp: ACGTN either case, other bytes kept) when rc && rc[i].  Threaded.
+// complemented like mappy.revcomp (revcomp.h) when rc && rc[i].  Threaded.
 int mando_pack_segments(const uint8_t *const *src, const int8_t *sel, const int64_t *starts, const int64_t *lens,
                         const int8_t *rc, int64_t n, uint8_t *out, const int64_t *out_off, int32_t threads) {
     if (n < 0 || (n > 0 && (!src || !starts || !lens || !out || !out_off))) return MANDO_E_ARG;
-    static const struct Comp {
-        uint8_t t[256];
-        Comp() {
-            for (int i = 0; i < 256; ++i) t[i] = (uint8_t)i;
-            const char *a = "ACGTNacgtn", *b = "TGCANtgcan";
-            for (int i = 0; a[i]; ++i) t[(uint8_t)a[i]] = (uint8_t)b[i];
-        }
-    } comp;
+    const mando::CompTable &comp = mando::comp_table();
     int nth = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
     nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n / 256));
     auto work = [&](int64_t a, int64_t b) {

@@ -28,11 +28,12 @@ import numpy as np
 
 from . import _lib, cluster, gtf
 
-COMP = bytes.maketrans(b"ACGTNacgtn", b"TGCANtgcan")
+# mappy.revcomp's complement table (minimap2 seq_comp_table; csrc/revcomp.h): IUPAC, either case
+COMP = bytes.maketrans(b"ACGTURYKMBVDHSWNacgturykmbvdhswn", b"TGCAAYRMKVBHDSWNtgcaayrmkvbhdswn")
 
 
 def revcomp(s: str) -> str:
-    """mappy.revcomp (ACGTN, either case)."""
+    """mappy.revcomp."""
     return s.encode().translate(COMP)[::-1].decode()
 
 

@@ -3,10 +3,10 @@
 Keeps the reference's command-line surface (/root/reference/Mando.py:22-205) so a pipeline that calls
 `Mando.py -M D ...` can switch over unchanged.  Only the D module (defining isoforms) is built here:
 it runs mandalorion_amd.define (clustering on host C++ threads, orientation and POA consensus on the
-GPU) with exactly the arguments Mando.py passes to defineIsoforms.py (Mando.py:382-399).  The other
-modules (A alignment, F filtering, Q quantification, and the SAM->PSL / clean_psl half of P) are outside
-this build's scope and are reported and skipped; P's sort + locus split (the D module's
-input) is built (mando_split_loci).
+GPU) with exactly the arguments Mando.py passes to defineIsoforms.py (Mando.py:382-399).  Module P
+(SAM -> PSL, clean_psl, sort + locus split: the D module's input) runs natively (mandalorion_amd.psl).
+The other modules (A alignment, F filtering, Q quantification) are outside this build's scope
+ and are reported and skipped.  Without a SAM, P starts from an existing clean PSL.
 """
 from __future__ import annotations
 
@@ -68,16 +68,22 @@ def main(argv: list[str] | None = None) -> int:
     os.makedirs(temp_path, exist_ok=True)
     for mod in a.Modules:
         if mod == "P":
-            # locus split of module P (Mando.py:343-352): clean PSL -> sorted PSL + tmp_SS/<locus>.psl.
-            # SAM -> PSL (emtrey) and clean_psl are outside this build; a clean PSL must exist.
-            clean = temp_path + "/mm2Alignments.clean.psl"
-            if not os.path.exists(clean) or os.path.getsize(clean) == 0:
-                print("\tmodule P: mm2Alignments.clean.psl missing (emtrey / clean_psl are not part of this build)")
-                continue
+            # module P (Mando.py:323-358): SAM -> PSL (emtrey -m), clean_psl, sort + locus split, all native
             import shutil
 
             from . import psl
 
+            sam = temp_path + "/mm2Alignments.sam"
+            clean = temp_path + "/mm2Alignments.clean.psl"
+            if os.path.exists(sam) and os.path.getsize(sam) > 0:
+                print("\tconverting sam output to psl format")
+                psl.sam_to_psl(sam, temp_path + "/mm2Alignments.psl", mando=True, threads=int(a.minimap2_threads))
+                print("\tcleaning psl file of small Indels")
+                psl.clean_psl(temp_path + "/mm2Alignments.psl", clean, True)
+            elif not os.path.exists(clean) or os.path.getsize(clean) == 0:
+                print("\tno or empty SAM file was provided. File conversions and parsing not performed")
+                continue
+            print("\tsorting clean psl file and splitting it into loci")
             shutil.rmtree(temp_path + "/tmp_SS", ignore_errors=True)
             nrec, nloc = psl.split_loci(clean, temp_path + "/tmp_SS", sort_lines=True,
                                         sorted_out=temp_path + "/mm2Alignments.clean.sorted.psl")

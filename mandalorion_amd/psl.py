@@ -1,6 +1,7 @@
-"""PSL ingest + locus split (libmando `mando_split_loci`): the part of module P that produces the D
-module's input, i.e. `sort -k 14,14 -k 16,17n` of the clean PSL (/root/reference/Mando.py:343-349) and
-get_chromosomes (/root/reference/utils/SpliceDefineConsensus.py:442-495), in one native pass."""
+"""Module P natively (libmando): SAM -> PSL (`mando_sam_to_psl`, emtrey.py -m), clean_psl
+(`mando_clean_psl`, /root/reference/utils/SpliceDefineConsensus.py:14-92) and the locus split that produces
+the D module's input (`mando_split_loci`: `sort -k 14,14 -k 16,17n` of the clean PSL,
+/root/reference/Mando.py:343-349, and get_chromosomes, SpliceDefineConsensus.py:442-495)."""
 from __future__ import annotations
 
 import ctypes
@@ -18,3 +19,21 @@ def split_loci(clean_psl: str, tmp_ss: str, sort_lines: bool = True, sorted_out:
                                             sorted_out.encode() if sorted_out else None, ctypes.byref(nr),
                                             ctypes.byref(nl)))
     return nr.value, nl.value
+
+
+def sam_to_psl(sam: str, psl: str, mando: bool = True, threads: int = 0) -> int:
+    """emtrey.py -i sam -o psl [-m] (/root/reference/emtrey.py:31-193); returns PSL lines written.
+    Raises MandoError where emtrey raises (unknown chromosome, missing cs tag in -m mode, zero-length
+    alignment, malformed CIGAR)."""
+    n = ctypes.c_int64()
+    _lib.check(_lib.load().mando_sam_to_psl(sam.encode(), psl.encode(), 1 if mando else 0, int(threads),
+                                            ctypes.byref(n)))
+    return n.value
+
+
+def clean_psl(psl_file: str, clean_psl_file: str, primary: bool) -> int:
+    """SpliceDefineConsensus.clean_psl (same argument order); returns lines written."""
+    n = ctypes.c_int64()
+    _lib.check(_lib.load().mando_clean_psl(psl_file.encode(), clean_psl_file.encode(), 1 if primary else 0,
+                                           ctypes.byref(n)))
+    return n.value
