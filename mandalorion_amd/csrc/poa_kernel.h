@@ -20,12 +20,18 @@ constexpr int kSrc = 0, kSink = 1;
 // contiguous block), [6] member count
 constexpr int kGtabInts = 8;
 
-// traceback byte layout (one byte per DP cell)
-constexpr int kTbTypeMask = 7;           // 0 M, 1 E1, 2 E2, 3 F1, 4 F2 : source of H
-constexpr int kTbE1Open = 1 << 3;        // E1out[i][j] came from H[i][j]-oe1 (open preferred on ties)
-constexpr int kTbE2Open = 1 << 4;
-constexpr int kTbF1OpenNext = 1 << 5;    // F1[i][j+1] opens from H0[i][j]
-constexpr int kTbF2OpenNext = 1 << 6;
+// traceback byte layout (one byte per DP cell).  Raw "differs" bits rather than a resolved source
+// type, so both the 32-bit and the packed 16-bit rows produce it with compares only; the backtrack
+// resolves the source with abPOA's priority (M, then E1/E2 -- the lower predecessor index first on
+// an E1/E2 tie --, then F1, then F2).  Gap bits are set for "extends" (open preferred on ties).
+constexpr int kTbNM = 1 << 0;            // M[i][j] != H[i][j]
+constexpr int kTbNX1 = 1 << 1;           // E1in[i][j] != H[i][j]
+constexpr int kTbNX2 = 1 << 2;           // E2in[i][j] != H[i][j]
+constexpr int kTbNF1 = 1 << 3;           // F1[i][j] != H[i][j]
+constexpr int kTbE1Ext = 1 << 4;         // E1out[i][j] extends E1in (H[i][j]-oe1 < E1in-e1)
+constexpr int kTbE2Ext = 1 << 5;
+constexpr int kTbF1ExtNext = 1 << 6;     // F1[i][j+1] extends F1[i][j] (G1[j] < P1[j])
+constexpr int kTbF2ExtNext = 1 << 7;
 
 // phases timed when PoaKArgs::prof is set (MANDO_PROF=1)
 constexpr int kProfPhases = 16;  // 0 desc, 1 dp, 2 backtrack, 3 update, 4 consensus, 5 rows, 6 reads,
@@ -111,12 +117,16 @@ struct PoaKArgs {
     SlotLayout lay;
     int32_t match, mismatch, o1, e1, o2, e2, band_b;
     float band_f;
-    int32_t qlds;            // dynamic LDS bytes for the read (4-bit codes): >= (longest read + 1) / 2
+    int32_t qlds;            // dynamic LDS bytes for the read stream (see poa_qlds_bytes)
 };
 
-// dynamic LDS the POA kernel needs for reads up to max_len
+// Columns a row can touch past the read: one 128-column chunk beyond `end` (<= qlen) plus slack.
+constexpr int kQPad = 132;
+
+// dynamic LDS the POA kernel needs for reads up to max_len: the read as 4-bit codes shifted by one
+// (nibble j = base j-1, nibble 0 and everything past the read = 4), padded by kQPad columns
 inline int poa_qlds_bytes(int64_t max_len) {
-    const int64_t b = ((((max_len + 1) / 2) + 15) & ~int64_t(15)) + 16;
+    const int64_t b = ((((max_len + kQPad + 2) / 2) + 15) & ~int64_t(15)) + 16;
     return (int)(b < 1040 ? 1040 : b);  // >= 1 KB: the backtrack's predecessor-byte window reuses it
 }
 

@@ -452,7 +452,9 @@ struct DpState {
 #define STAMP(var) const uint64_t var = 0
 #endif
 
-__device__ __forceinline__ int qbase(const SharedState &sh, int j) {
+// code of the query base consumed by column j (base j-1): nibble j of the shifted stream, 4 for
+// column 0 and every column past the read
+__device__ __forceinline__ int qcol(const SharedState &sh, int j) {
     return (g_qnib[j >> 1] >> ((j & 1) << 2)) & 0xf;
 }
 
@@ -479,6 +481,25 @@ __device__ __forceinline__ void pre_records_slow(const PoaKArgs &a, const Slot &
         pS = x.w;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // consume here (see above)
+}
+
+// traceback byte of one cell (layout in poa_kernel.h)
+__device__ __forceinline__ int tb_bits(int H, int M, int X1, int X2, int F1, int oe1, int e1, int oe2, int e2, int G1,
+                                       int P1, int G2, int P2) {
+    return (M != H ? kTbNM : 0) | (X1 != H ? kTbNX1 : 0) | (X2 != H ? kTbNX2 : 0) | (F1 != H ? kTbNF1 : 0) |
+           (H - oe1 < X1 - e1 ? kTbE1Ext : 0) | (H - oe2 < X2 - e2 ? kTbE2Ext : 0) | (G1 < P1 ? kTbF1ExtNext : 0) |
+           (G2 < P2 ? kTbF2ExtNext : 0);
+}
+
+// source of H[i][j] from its traceback byte: 0 M, 1 E1, 2 E2, 3 F1, 4 F2 (k1/k2: predecessor index
+// of the E1/E2 maxima, 0 on single-predecessor rows)
+__device__ __forceinline__ int tb_type(int t, int k1, int k2) {
+    if (!(t & kTbNM)) return 0;
+    const bool x1 = !(t & kTbNX1), x2 = !(t & kTbNX2);
+    if (x1 && x2) return k1 <= k2 ? 1 : 2;
+    if (x1) return 1;
+    if (x2) return 2;
+    return (t & kTbNF1) ? 4 : 3;
 }
 
 __device__ __forceinline__ bool in_band(int col, int b, int e) {
@@ -577,8 +598,7 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
             E2a = Ha - oe2;
             E2b = Hb - oe2;
         } else {
-            const int qa = (j0 >= 1 && j0 <= qlen) ? qbase(sh, j0 - 1) : 4;
-            const int qb = (j0 < qlen) ? qbase(sh, j0) : 4;
+            const int qa = qcol(sh, j0), qb = qcol(sh, j1);
             int Mva, Mvb, X1a, X1b, X2a, X2b;
             int mka = 0, mkb = 0, k1a = 0, k1b = 0, k2a = 0, k2b = 0;
             const int ia = (j0 - 1) & (kChunk - 1), ib = j0 & (kChunk - 1);
@@ -665,26 +685,12 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
             const int F2a = P2a - oe2 - e2 * (j0 - 1), F2b = P2b - oe2 - e2 * (j1 - 1);
             Ha = max(H0a, max(F1a, F2a));
             Hb = max(H0b, max(F1b, F2b));
-            auto src_type = [&](int H, int M, int X1, int X2, int F1, int k1, int k2) -> int {
-                if (M == H) return 0;
-                const bool t1 = X1 == H, t2 = X2 == H;
-                if (t1 && t2) return (k1 <= k2) ? 1 : 2;
-                if (t1) return 1;
-                if (t2) return 2;
-                return (F1 == H) ? 3 : 4;
-            };
-            const int tya = src_type(Ha, Ma, X1a, X2a, F1a, k1a, k2a);
-            const int tyb = src_type(Hb, Mb, X1b, X2b, F1b, k1b, k2b);
             E1a = max(X1a - e1, Ha - oe1);
             E1b = max(X1b - e1, Hb - oe1);
             E2a = max(X2a - e2, Ha - oe2);
             E2b = max(X2b - e2, Hb - oe2);
-            const int ta = tya | ((Ha - oe1 >= X1a - e1) ? kTbE1Open : 0) |
-                           ((Ha - oe2 >= X2a - e2) ? kTbE2Open : 0) |
-                           ((G1a >= P1a) ? kTbF1OpenNext : 0) | ((G2a >= P2a) ? kTbF2OpenNext : 0);
-            const int tb2 = tyb | ((Hb - oe1 >= X1b - e1) ? kTbE1Open : 0) |
-                            ((Hb - oe2 >= X2b - e2) ? kTbE2Open : 0) |
-                            ((G1b >= P1b) ? kTbF1OpenNext : 0) | ((G2b >= P2b) ? kTbF2OpenNext : 0);
+            const int ta = tb_bits(Ha, Ma, X1a, X2a, F1a, oe1, e1, oe2, e2, G1a, P1a, G2a, P2a);
+            const int tb2 = tb_bits(Hb, Mb, X1b, X2b, F1b, oe1, e1, oe2, e2, G1b, P1b, G2b, P2b);
             tpair = ta | (tb2 << 8);
             if ((va || vbb) && multi) {
                 GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + 3 * j0));
@@ -807,10 +813,9 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
     const int svbase = (int)ds.sv_used - cb0;
     const int j0 = cb0 + 2 * lane, j1 = j0 + 1;
     const bool va = j0 >= beg && j0 <= end, vbb = j1 <= end;
-    // branch-free query lookups (clamped index, then select)
-    const int qa0 = qbase(sh, min(max(j0 - 1, 0), qlen - 1)), qb0 = qbase(sh, min(j0, qlen - 1));
-    const int qa = (j0 >= 1 && j0 <= qlen) ? qa0 : 4;
-    const int qb = (j0 < qlen) ? qb0 : 4;
+    // query codes of both columns: one byte of the shifted, padded stream
+    const int qbyte = g_qnib[j0 >> 1];
+    const int qa = qbyte & 0xf, qb = qbyte >> 4;
     const int ia = (j0 - 1) & (kChunk - 1), ib = j0 & (kChunk - 1);
     // Ring rows hold -inf outside their band (every writer masks its out-of-band columns), so when
     // the columns this row reads, [beg-1, end], lie inside a predecessor's 128-column chunk, the ring
@@ -868,22 +873,10 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
     const int F2a = P2a - oe2 - e2 * (j0 - 1), F2b = P2b - oe2 - e2 * (j1 - 1);
     const int Ha = max(H0a, max(F1a, F2a));
     const int Hb = max(H0b, max(F1b, F2b));
-    auto src_type = [&](int H, int M, int X1, int X2, int F1, int k1, int k2) -> int {
-        if (M == H) return 0;
-        const bool t1 = X1 == H, t2 = X2 == H;
-        if (t1 && t2) return (k1 <= k2) ? 1 : 2;
-        if (t1) return 1;
-        if (t2) return 2;
-        return (F1 == H) ? 3 : 4;
-    };
-    const int tya = src_type(Ha, Ma, X1a, X2a, F1a, k1a, k2a);
-    const int tyb = src_type(Hb, Mb, X1b, X2b, F1b, k1b, k2b);
     const int E1a = max(X1a - e1, Ha - oe1), E1b = max(X1b - e1, Hb - oe1);
     const int E2a = max(X2a - e2, Ha - oe2), E2b = max(X2b - e2, Hb - oe2);
-    const int ta = tya | ((Ha - oe1 >= X1a - e1) ? kTbE1Open : 0) | ((Ha - oe2 >= X2a - e2) ? kTbE2Open : 0) |
-                   ((G1a >= P1a) ? kTbF1OpenNext : 0) | ((G2a >= P2a) ? kTbF2OpenNext : 0);
-    const int tb2 = tyb | ((Hb - oe1 >= X1b - e1) ? kTbE1Open : 0) | ((Hb - oe2 >= X2b - e2) ? kTbE2Open : 0) |
-                    ((G1b >= P1b) ? kTbF1OpenNext : 0) | ((G2b >= P2b) ? kTbF2OpenNext : 0);
+    const int ta = tb_bits(Ha, Ma, X1a, X2a, F1a, oe1, e1, oe2, e2, G1a, P1a, G2a, P2a);
+    const int tb2 = tb_bits(Hb, Mb, X1b, X2b, F1b, oe1, e1, oe2, e2, G1b, P1b, G2b, P2b);
     // stores: the traceback pair of every lane (lanes past `end` write into slack the next row
     // overwrites; the caller's capacity test keeps one chunk of slack), ring row, optional planes
     *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)(ta | (tb2 << 8));
@@ -945,15 +938,16 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
                       int n, int lane, int64_t &cells, int &bi_out) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
-    if (qlen > 2 * a.qlds) return kStUnsupported;  // the launch sizes the read buffer for the batch
+    if ((qlen + kQPad + 2) / 2 > a.qlds) return kStUnsupported;  // the launch sizes the read buffer
     const int w = a.band_b + (int)(a.band_f * (float)qlen);
     DpState ds{0, 0, 0, 0, {0, 0, 0, 0}};
     const int TBC = (int)a.caps.TBC, KPC = (int)a.caps.KPC, SVC = (int)a.caps.SVC;
     (void)TBC; (void)KPC; (void)SVC;
     // stage the read in LDS (4-bit codes): on gfx9 vmcnt orders loads behind every earlier store,
     // so a global load per row would wait for the previous rows' traceback stores to land
-    for (int t = 2 * lane; t < qlen; t += 2 * kWave) {
-        const int lo = q[t], hi = (t + 1 < qlen) ? q[t + 1] : 4;
+    // (shifted by one column: nibble j = base j-1; nibble 0 and the kQPad columns past the read = 4)
+    for (int t = 2 * lane; t < qlen + kQPad; t += 2 * kWave) {
+        const int lo = (t >= 1 && t <= qlen) ? q[t - 1] : 4, hi = (t < qlen) ? q[t] : 4;
         g_qnib[t >> 1] = (uint8_t)(lo | (hi << 4));
     }
     int nfast = 0;
@@ -1136,14 +1130,16 @@ __device__ __forceinline__ void bt_step_global(const PoaKArgs &a, const Slot &s,
     const int tbbase = rb[4], kpbase = rb[5], node = rb[6], pn = rb[7];
     const int t = s.tb[tbbase + j];
     if (st == 1 || st == 2) {
-        if (t & (st == 1 ? kTbE1Open : kTbE2Open)) {
+        if (!(t & (st == 1 ? kTbE1Ext : kTbE2Ext))) {
             st = 0;
             return;
         }
     }
-    const int ty = st == 0 ? (t & kTbTypeMask) : st;
+    const bool multi = pn > 1;
+    const int ty = st == 0 ? tb_type(t, multi ? s.kp[kpbase + 3 * j + 1] : 0, multi ? s.kp[kpbase + 3 * j + 2] : 0)
+                           : st;
     if (ty <= 2) {
-        const int k = (pn > 1) ? s.kp[kpbase + 3 * j + ty] : 0;
+        const int k = multi ? s.kp[kpbase + 3 * j + ty] : 0;
         const int p = (k < kPreInline) ? s.desc[(int64_t)i * kDescInts + 3 + k] : s.pos[in_list(s, a, node)[k]];
         if (ty == 0) {
             s.qnode[j - 1] = node;
@@ -1155,7 +1151,7 @@ __device__ __forceinline__ void bt_step_global(const PoaKArgs &a, const Slot &s,
     }
     s.qnode[j - 1] = -1;
     const int tprev = s.tb[tbbase + j - 1];
-    st = (tprev & (ty == 3 ? kTbF1OpenNext : kTbF2OpenNext)) ? 0 : ty;
+    st = (tprev & (ty == 3 ? kTbF1ExtNext : kTbF2ExtNext)) ? ty : 0;
     --j;
 }
 
@@ -1175,8 +1171,8 @@ __device__ __forceinline__ void bt_step_lds(const SharedState &sh, const Slot &s
     const int kix = multi ? kof + 3 * j : 0;
     const int k0 = g_qnib[kix], k1 = g_qnib[kix + 1], k2 = g_qnib[kix + 2];
     const bool isE = st == 1 || st == 2;
-    const bool open = isE && (t & (st == 1 ? kTbE1Open : kTbE2Open));
-    const int ty = st == 0 ? (t & kTbTypeMask) : st;
+    const bool open = isE && !(t & (st == 1 ? kTbE1Ext : kTbE2Ext));
+    const int ty = st == 0 ? tb_type(t, multi ? k1 : 0, multi ? k2 : 0) : st;
     const bool mv = !open && ty <= 2;
     const int k = multi ? (ty == 0 ? k0 : (ty == 1 ? k1 : k2)) : 0;
     const int p = k == 0 ? m0.w : (k == 1 ? m1.x : (k == 2 ? m1.y : (k == 3 ? m1.z : m1.w)));
@@ -1186,7 +1182,7 @@ __device__ __forceinline__ void bt_step_lds(const SharedState &sh, const Slot &s
     const bool isF = !open && ty >= 3;
     const bool wr = go && ((mv && ty == 0) || isF);
     if (wr) s.qnode[j - 1] = mv ? node : -1;
-    const int fopen = tprev & (ty == 3 ? kTbF1OpenNext : kTbF2OpenNext);
+    const int fopen = !(tprev & (ty == 3 ? kTbF1ExtNext : kTbF2ExtNext));
     const int nst = open ? 0 : (mv ? ty : (fopen ? 0 : ty));
     const int ni = mv ? p : i;
     const int nj = j - (int)((mv && ty == 0) || isF);
