@@ -153,6 +153,8 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.band_b = p.band_b;
     a.band_f = p.band_f;
     a.qlds = mando::poa_qlds_bytes(caps.QC);
+    a.dbg = 0;
+    if (const char *ev = getenv("MANDO_POA_DBG")) a.dbg = atoi(ev);
     // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
@@ -191,10 +193,23 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         for (int64_t s = 0; s < slots; ++s)
             for (int k = 0; k < mando::kProfPhases; ++k) tot[k] += (double)h[(size_t)(s * mando::kProfPhases + k)];
         const double reads = std::max(1.0, tot[6]), rows = std::max(1.0, tot[5]);
-        fprintf(stderr, "[mando prof] fast rows %.1f%%\n", 100.0 * tot[7] / rows);
+        fprintf(stderr, "[mando prof] fast rows %.1f%%, reads re-aligned in 32-bit mode %.0f\n", 100.0 * tot[7] / rows,
+                tot[15]);
         fprintf(stderr, "[mando prof] slots=%lld reads=%.0f rows/read=%.0f | cycles per read: desc %.0f dp %.0f (%.1f/row) backtrack %.0f update %.0f | consensus/slot %.0f\n",
                 (long long)slots, reads, rows / reads, tot[0] / reads, tot[1] / reads, tot[1] / rows,
                 tot[2] / reads, tot[3] / reads, tot[4] / (double)slots);
+        if (a.dbg & 16) {
+            for (int64_t s = 0; s < slots; ++s) {
+                const int64_t *f = &h[(size_t)(s * mando::kProfPhases)];
+                if (f[8] == 0) continue;
+                fprintf(stderr, "[mando dbg] slot %lld row %lld lane %lld beg %lld end %lld am %lld | tb fast %04llx gen %04llx | H %08llx %08llx | E1 %08llx %08llx | E2 %08llx %08llx | am2 %lld qlen %lld n %lld\n",
+                        (long long)s, (long long)f[8] - 1, (long long)(f[9] & 0xff), (long long)((f[9] >> 8) & 0xffff),
+                        (long long)((f[9] >> 24) & 0xffff), (long long)(f[9] >> 40), (long long)(f[10] >> 16),
+                        (long long)(f[10] & 0xffff), (long long)((uint64_t)f[11] >> 32), (long long)(f[11] & 0xffffffff),
+                        (long long)((uint64_t)f[12] >> 32), (long long)(f[12] & 0xffffffff), (long long)((uint64_t)f[13] >> 32),
+                        (long long)(f[13] & 0xffffffff), (long long)f[14], (long long)(f[15] & 0xfffff), (long long)(f[15] >> 20));
+            }
+        }
         if (tot[12] > 0)
             fprintf(stderr, "[mando prof] backtrack per read: refills %.1f (%.0f cyc each) blocks %.1f walk %.0f cyc/block\n",
                     tot[13] / reads, tot[12] / std::max(1.0, tot[13]), tot[14] / reads,

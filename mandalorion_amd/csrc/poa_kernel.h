@@ -39,6 +39,7 @@ constexpr int kProfPhases = 16;  // 0 desc, 1 dp, 2 backtrack, 3 update, 4 conse
 
 // per-group status codes written by the kernel (match include/mando.h)
 constexpr int kStOk = 0, kStCap = -4, kStInternal = -6, kStUnsupported = -5;
+constexpr int kStRetry32 = -100;  // kernel-internal: re-run the read's DP in 32-bit mode
 
 struct PoaCaps {
     int32_t NC;      // node capacity per group
@@ -118,6 +119,7 @@ struct PoaKArgs {
     int32_t match, mismatch, o1, e1, o2, e2, band_b;
     float band_f;
     int32_t qlds;            // dynamic LDS bytes for the read stream (see poa_qlds_bytes)
+    int32_t dbg;             // MANDO_POA_DBG: bit 0 no 16-bit mode, bit 1 no 16-bit fast rows
 };
 
 // Columns a row can touch past the read: one 128-column chunk beyond `end` (<= qlen) plus slack.

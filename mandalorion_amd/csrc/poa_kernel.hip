@@ -164,7 +164,10 @@ constexpr int kKpWinMax = 2048;       // backtrack: predecessor-byte window (in 
 
 // DP phase: the H/E1/E2 ring, carried from row to row
 struct DpLds {
-    int ring[kRing][3][kChunk];  // H, E1out, E2out of the last kRing narrow rows, col & 127
+    union {
+        int ring[kRing][3][kChunk];      // H, E1out, E2out of the last kRing narrow rows, col & 127
+        short ring16[kRing][3][kChunk];  // the same in 16-bit mode (run_dp<SC, true>)
+    };
 };
 // backtrack phase (the DP state is dead by then); the predecessor-byte window uses the read's
 // dynamic buffer, which the next read's DP re-stages
@@ -258,6 +261,7 @@ __device__ __forceinline__ PoaKArgs args_of(SharedState &sh) {
     a.band_b = bcast0(a.band_b);
     a.band_f = __int_as_float(bcast0(__float_as_int(a.band_f)));
     a.prof = uniptr(a.prof);
+    a.dbg = bcast0(a.dbg);
     return a;
 }
 
@@ -442,7 +446,9 @@ struct RuntimeScores {
 
 struct DpState {
     int tb_used, kp_used, sv_used;
-    int64_t cells;
+    int r16bad;     // 16-bit mode left its safe range: re-align the read in 32-bit mode
+    uint32_t r16acc;  // per-lane min of (H - kR16Low) over valid fast-row columns (16-bit mode)
+    int cells;  // DP cells of this read (< 2^31: a read's band cells)
     uint64_t seg[4];
 };
 
@@ -506,10 +512,45 @@ __device__ __forceinline__ bool in_band(int col, int b, int e) {
     return (unsigned)(col - b) <= (unsigned)(e - b);
 }
 
+// Ring access for the generic row in both modes.  16-bit mode stores values clamped to int16
+// (-inf = -32768); the 32-bit mode stores kNegInf.  Columns are absolute & 127.
+__device__ __forceinline__ int clamp16(int v) { return min(max(v, -32768), 32767); }
+template <bool R16>
+__device__ __forceinline__ int ring_get(const SharedState &sh, int row, int plane, int col) {
+    if constexpr (R16) return sh.dp.ring16[row][plane][col];
+    else return sh.dp.ring[row][plane][col];
+}
+// (col, col+1) of one plane; col even
+template <bool R16>
+__device__ __forceinline__ int2 ring_get2(const SharedState &sh, int row, int plane, int col) {
+    if constexpr (R16) {
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(&sh.dp.ring16[row][plane][col]);
+        return make_int2((int)(short)(w & 0xffff), (int)w >> 16);
+    } else {
+        return *reinterpret_cast<const int2 *>(&sh.dp.ring[row][plane][col]);
+    }
+}
+template <bool R16>
+__device__ __forceinline__ void ring_put2(SharedState &sh, int row, int plane, int col, int a, bool va, int b,
+                                          bool vb) {
+    if constexpr (R16) {
+        const uint32_t lo = (uint32_t)(va ? clamp16(a) : -32768) & 0xffff;
+        const uint32_t hi = (uint32_t)(vb ? clamp16(b) : -32768) << 16;
+        *reinterpret_cast<uint32_t *>(&sh.dp.ring16[row][plane][col]) = lo | hi;
+    } else {
+        *reinterpret_cast<int2 *>(&sh.dp.ring[row][plane][col]) = make_int2(va ? a : kNegInf, vb ? b : kNegInf);
+    }
+}
+
+// 16-bit mode: a finite H must never be confused with a -inf-derived one (those stay below
+// kR16Low; every value moves by a bounded step per cell, so one that drifts between the classes
+// passes through [kR16Low, kR16High) and is caught); the read is then re-aligned in 32-bit mode.
+constexpr int kR16Low = -31000, kR16High = -28000;
+
 // One DP row r.  Predecessor k's record lives in lane k (pP row, pB/pE band, pA argmax, pS spill
 // offset); the common case (every predecessor in the LDS ring) reads values with 4 LDS ops per
 // predecessor and no global memory traffic except the traceback stores.
-template <class SC>
+template <class SC, bool R16>
 __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
                                       int w, int r, int lane, DpState &ds) {
     const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
@@ -581,8 +622,6 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
     int best = -2147483647 - 1, besti = beg;
     int carry1 = kNegInf + oe1 + e1 * (beg - 1);
     int carry2 = kNegInf + oe2 + e2 * (beg - 1);
-    int *ringrow = &sh.dp.ring[r % kRing][0][0];
-
     for (int c = 0; c < nchunk; ++c) {
         const int cb = cb0 + c * kChunk;
         const int j0 = cb + 2 * lane, j1 = j0 + 1;
@@ -605,10 +644,10 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
             if (all_ring && pn == 1) {
                 // the common row: one predecessor, in the ring
                 const int p0 = readlane(pP, 0), b0 = readlane(pB, 0), e0 = readlane(pE, 0);
-                const int *rp = &sh.dp.ring[p0 % kRing][0][0];
-                const int hA = rp[ia], hB = rp[ib];
-                const int2 x1 = *reinterpret_cast<const int2 *>(rp + kChunk + ib);
-                const int2 x2 = *reinterpret_cast<const int2 *>(rp + 2 * kChunk + ib);
+                const int pr = p0 % kRing;
+                const int hA = ring_get<R16>(sh, pr, 0, ia), hB = ring_get<R16>(sh, pr, 0, ib);
+                const int2 x1 = ring_get2<R16>(sh, pr, 1, ib);
+                const int2 x2 = ring_get2<R16>(sh, pr, 2, ib);
                 const bool inA = in_band(j0 - 1, b0, e0), inB = in_band(j0, b0, e0),
                            inC = in_band(j1, b0, e0);
                 Mva = inA ? hA : kNegInf;
@@ -625,12 +664,12 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
                     int hA, hB;
                     int2 x1, x2;
                     if (all_ring || (r - pk < kRing && row_narrow(bk, ek))) {
-                        const int *rp = &sh.dp.ring[pk % kRing][0][0];
+                        const int pr = pk % kRing;
                         const int iA = (j0 - 1) & (kChunk - 1), iB = j0 & (kChunk - 1);
-                        hA = rp[iA];
-                        hB = rp[iB];
-                        x1 = *reinterpret_cast<const int2 *>(rp + kChunk + iB);
-                        x2 = *reinterpret_cast<const int2 *>(rp + 2 * kChunk + iB);
+                        hA = ring_get<R16>(sh, pr, 0, iA);
+                        hB = ring_get<R16>(sh, pr, 0, iB);
+                        x1 = ring_get2<R16>(sh, pr, 1, iB);
+                        x2 = ring_get2<R16>(sh, pr, 2, iB);
                     } else {
                         // predecessor outside the ring: its spill planes in HBM (columns clamped to
                         // the spilled width; out-of-band values are masked below)
@@ -705,10 +744,16 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
         }
         if (va || vbb) *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)tpair;
         if (narrow) {  // out-of-band columns hold -inf (see dp_row_fast)
-            const int ibk = j0 & (kChunk - 1);
-            *reinterpret_cast<int2 *>(ringrow + ibk) = make_int2(va ? Ha : kNegInf, vbb ? Hb : kNegInf);
-            *reinterpret_cast<int2 *>(ringrow + kChunk + ibk) = make_int2(va ? E1a : kNegInf, vbb ? E1b : kNegInf);
-            *reinterpret_cast<int2 *>(ringrow + 2 * kChunk + ibk) = make_int2(va ? E2a : kNegInf, vbb ? E2b : kNegInf);
+            const int ibk = j0 & (kChunk - 1), rr = r % kRing;
+            ring_put2<R16>(sh, rr, 0, ibk, Ha, va, Hb, vbb);
+            ring_put2<R16>(sh, rr, 1, ibk, E1a, va, E1b, vbb);
+            ring_put2<R16>(sh, rr, 2, ibk, E2a, va, E2b, vbb);
+        }
+        if constexpr (R16) {
+            // finite values must stay clear of the -inf band (see kR16Low)
+            const bool bad = (va && Ha >= kR16Low && Ha < kR16High) || (vbb && Hb >= kR16Low && Hb < kR16High) ||
+                             (va && Ha > 32767 - 256) || (vbb && Hb > 32767 - 256);
+            if (__ballot(bad)) ds.r16bad = 1;
         }
         if (spill) {
             gint *sv = s.sv + svbase;
@@ -929,18 +974,249 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
     return true;
 }
 
+// ---- packed 16-bit lane pairs: .lo = column j0 = cb0 + 2*lane, .hi = column j0 + 1 ------------
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s16x2(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__host__ __device__ constexpr uint32_t pk2(int v) { return ((uint32_t)v & 0xffffu) * 0x10001u; }
+constexpr uint32_t kNeg2 = 0x80008000u;  // (-32768, -32768): -inf of the 16-bit mode
+__device__ __forceinline__ uint32_t pk_adds(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_add_sat(as_s16x2(a), as_s16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_subs(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_sub_sat(as_s16x2(a), as_s16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_max(as_s16x2(a), as_s16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_umax(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_max(as_u16x2(a), as_u16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_umin(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_min(as_u16x2(a), as_u16x2(b)));
+}
+// 0xffff in the halves where x < 0
+__device__ __forceinline__ uint32_t pk_neg_mask(uint32_t x) { return as_u32(as_s16x2(x) >> (s16x2){15, 15}); }
+// bit K set in the halves where h != x (h >= x or x is -inf; one saturating subtract + min)
+template <int K>
+__device__ __forceinline__ uint32_t pk_ne_bit(uint32_t h, uint32_t x) {
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(r) : "v"(pk_subs(h, x)));  // (splat 1; the compiler would use compares)
+    return K ? as_u32(as_u16x2(r) << (u16x2){K, K}) : r;
+}
+// bit K set in the halves where a < b
+template <int K>
+__device__ __forceinline__ uint32_t pk_lt_bit(uint32_t a, uint32_t b) {
+    return as_u32((as_u16x2(pk_subs(a, b)) >> (u16x2){15 - K, 15 - K}) & (u16x2){1u << K, 1u << K});
+}
+// (m & x) | (~m & y) as one v_bfi_b32 (left to itself the compiler turns mask-selects into
+// per-half compares + cndmasks + a perm)
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(y));
+    return r;
+}
+// inclusive prefix max over the wave of both halves (unsigned; 0 is the identity, so DPP lanes
+// without a source read 0 via bound_ctrl)
+__device__ __forceinline__ uint32_t pk_scan_umax(uint32_t u) {
+    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x111, 0xf, 0xf, true));
+    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x112, 0xf, 0xf, true));
+    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x114, 0xf, 0xf, true));
+    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x118, 0xf, 0xf, true));
+    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x142, 0xa, 0xf, true));
+    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x143, 0xc, 0xf, true));
+    return u;
+}
+
+// 16-bit mode is exact when every finite value fits with room to spare (see kR16Low) and the
+// biased score table fits in bytes.
+template <class SC>
+__device__ __forceinline__ bool r16_eligible(const SC &sc, int qlen) {
+    return sc.match >= 0 && sc.mismatch >= 0 && sc.match + sc.mismatch <= 255 && sc.e1 >= 0 && sc.e2 >= 0 &&
+           sc.o1 >= 0 && sc.o2 >= 0 && (sc.e1 + sc.e2) * kChunk + sc.o1 + sc.o2 <= 2000 &&
+           (int64_t)sc.match * qlen <= 30000;
+}
+
+// The fast row in 16-bit mode (same band / bookkeeping as dp_row_fast, values as lane pairs: one
+// packed op per two cells).  Gap states use cb0-relative G (G = H0 + e*(j - cb0)), which keeps the
+// -inf-derived G values near -32768; the scans run on both gap states at once, sign-flipped to
+// unsigned so that DPP's zero fill is the identity.  The score of both columns comes from one
+// v_perm_b32 over a per-row byte table of (score + mismatch).
+template <class SC>
+__device__ __forceinline__ bool dp_row_fast16(const PoaKArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
+                                             int w, int r, int lane, DpState &ds, RowPipe &pp) {
+    const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
+    const int node = pp.node, d1 = pp.d1, rem = pp.rem, p0 = pp.p0, p1 = pp.p1;
+    const int pn = d1 >> 16;
+    const int4 x0 = (p0 == pp.prv_r) ? make_int4(pp.prv_beg, pp.prv_end, pp.prv_am, 0) : pp.x0;
+    const int4 x1 = (p1 == pp.prv_r) ? make_int4(pp.prv_beg, pp.prv_end, pp.prv_am, 0) : pp.x1;
+    const bool two = pn == 2;
+    const int am0 = x0.z + 1, am1 = two ? x1.z + 1 : am0;
+    const int xr = qlen - rem;
+    const int beg = max(0, min(min(am0, am1), xr) - w);
+    const int end = min(qlen, max(max(am0, am1), xr) + w);
+    const int cb0 = beg & ~1;
+    const int span = end - cb0 + 1;
+    const int tbw = (span + 3) & ~3;
+    const bool ring0 = (r - p0 < kRing) && row_narrow(x0.x, x0.y);
+    const bool ring1 = !two || ((r - p1 < kRing) && row_narrow(x1.x, x1.y));
+    const int d1s = bcast0(d1);
+    const bool far = ((d1s >> 8) & 0xff) != 0;
+    const bool multi = (d1s >> 16) > 1;
+    const bool ok = pn >= 1 && pn <= 2 && span <= kChunk && ring0 && ring1 &&
+                    ds.tb_used + tbw + kChunk <= (int)a.caps.TBC &&
+                    (!multi || ds.kp_used + 3 * (tbw + kChunk) <= (int)a.caps.KPC) &&
+                    (!far || ds.sv_used + 3 * kChunk <= (int)a.caps.SVC);
+    if (!__builtin_amdgcn_readfirstlane((int)ok)) return false;
+
+    const int tbbase = (int)ds.tb_used - cb0;
+    const int kpbase = (int)ds.kp_used - 3 * cb0;
+    const int soff = far ? (int)ds.sv_used : -1;
+    const int svbase = (int)ds.sv_used - cb0;
+    const int j0 = cb0 + 2 * lane;
+    const uint32_t J = (uint32_t)j0 * 0x10001u + 0x10000u;         // (j0, j0 + 1)
+    const uint32_t LJ = (uint32_t)(2 * lane) * 0x10001u + 0x10000u;  // (j0, j0 + 1) - cb0
+    // halves outside [beg, end]
+    const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(beg))) |
+                                     as_u32(as_s16x2(pk2(end)) - as_s16x2(J)));
+    // scores of both columns: biased table byte per query code (match+mismatch, 0, N: mismatch)
+    const int qbyte = g_qnib[j0 >> 1];
+    const uint32_t sel = (uint32_t)(qbyte & 0xf) | (((uint32_t)qbyte & 0xf0u) << 12) | 0x0C000C00u;
+    const int vbs = d1s & 0xff;
+    const uint32_t tlo = vbs < 4 ? (uint32_t)(sc.match + sc.mismatch) << (8 * vbs) : (uint32_t)sc.mismatch * 0x01010101u;
+    const uint32_t S = __builtin_amdgcn_perm((uint32_t)sc.mismatch, tlo, sel);
+    // predecessor values: H at (j0-1, j0), E1/E2 at (j0, j0+1), from the 16-bit ring
+    const int iw = (j0 >> 1) & (kChunk / 2 - 1), iwp = (iw - 1) & (kChunk / 2 - 1);
+    const uint32_t *w0 = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[p0 % kRing][0][0]);
+    uint32_t Hd = __builtin_amdgcn_alignbit(w0[iw], w0[iwp], 16);
+    uint32_t X1 = w0[kChunk / 2 + iw], X2 = w0[kChunk + iw];
+    const int pc0 = x0.x & ~1, pc1 = x1.x & ~1;
+    const bool nm0 = beg - 1 >= pc0 && end <= pc0 + kChunk - 1;
+    const bool nm1 = !two || (beg - 1 >= pc1 && end <= pc1 + kChunk - 1);
+    const bool nomask = __builtin_amdgcn_readfirstlane((int)(nm0 && nm1)) != 0;
+    if ((a.dbg & 4) && !nomask) return false;
+    if ((a.dbg & 8) && far) return false;
+    if (!nomask) {
+        const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0): per half, no borrow
+        const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(x0.x))) |
+                                        as_u32(as_s16x2(pk2(x0.y)) - as_s16x2(JD)));
+        const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(x0.x))) |
+                                        as_u32(as_s16x2(pk2(x0.y)) - as_s16x2(J)));
+        Hd = bfi(md, kNeg2, Hd);
+        X1 = bfi(me, kNeg2, X1);
+        X2 = bfi(me, kNeg2, X2);
+    }
+    uint32_t MK = 0, K1 = 0, K2 = 0;
+    if (two) {
+        const uint32_t *w1 = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[max(p1, 0) % kRing][0][0]);
+        uint32_t Hd1 = __builtin_amdgcn_alignbit(w1[iw], w1[iwp], 16);
+        uint32_t X11 = w1[kChunk / 2 + iw], X21 = w1[kChunk + iw];
+        if (!nomask) {
+            const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0): per half, no borrow
+            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(x1.x))) |
+                                            as_u32(as_s16x2(pk2(x1.y)) - as_s16x2(JD)));
+            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(x1.x))) |
+                                            as_u32(as_s16x2(pk2(x1.y)) - as_s16x2(J)));
+            Hd1 = bfi(md, kNeg2, Hd1);
+            X11 = bfi(me, kNeg2, X11);
+            X21 = bfi(me, kNeg2, X21);
+        }
+        // first predecessor attaining the max (strict > keeps the earlier one)
+        MK = pk_lt_bit<0>(Hd, Hd1);
+        K1 = pk_lt_bit<0>(X1, X11);
+        K2 = pk_lt_bit<0>(X2, X21);
+        Hd = pk_max(Hd, Hd1);
+        X1 = pk_max(X1, X11);
+        X2 = pk_max(X2, X21);
+    }
+    const uint32_t M = pk_subs(pk_adds(Hd, S), pk2(sc.mismatch));
+    const uint32_t H0 = bfi(inv, kNeg2, pk_max(M, pk_max(X1, X2)));
+    // gap states, cb0-relative: G = H0 + e*(j - cb0), F = P - (oe + e*(j - 1 - cb0))
+    const uint32_t LJ1 = as_u32(as_u16x2(LJ) * (u16x2){(unsigned short)e1, (unsigned short)e1});
+    const uint32_t LJ2 = as_u32(as_u16x2(LJ) * (u16x2){(unsigned short)e2, (unsigned short)e2});
+    const uint32_t G1 = pk_adds(H0, LJ1), G2 = pk_adds(H0, LJ2);
+    const uint32_t Ga = __builtin_amdgcn_perm(G2, G1, 0x05040100u);  // (G1a, G2a)
+    const uint32_t Gb = __builtin_amdgcn_perm(G2, G1, 0x07060302u);  // (G1b, G2b)
+    const uint32_t inc = pk_scan_umax(pk_max(Ga, Gb) ^ kNeg2);
+    const uint32_t Pa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x138, 0xf, 0xf, true) ^ kNeg2;
+    const uint32_t Pb = pk_max(Pa, Ga);
+    const uint32_t P1 = __builtin_amdgcn_perm(Pb, Pa, 0x05040100u);  // (P1a, P1b)
+    const uint32_t P2 = __builtin_amdgcn_perm(Pb, Pa, 0x07060302u);  // (P2a, P2b)
+    const uint32_t F1 = pk_subs(P1, LJ1 + pk2(oe1 - e1)), F2 = pk_subs(P2, LJ2 + pk2(oe2 - e2));
+    const uint32_t H = pk_max(H0, pk_max(F1, F2));
+    const uint32_t X1e = pk_subs(X1, pk2(e1)), Ho1 = pk_subs(H, pk2(oe1));
+    const uint32_t X2e = pk_subs(X2, pk2(e2)), Ho2 = pk_subs(H, pk2(oe2));
+    const uint32_t E1 = pk_max(X1e, Ho1), E2 = pk_max(X2e, Ho2);
+    // traceback bytes (layout in poa_kernel.h), both columns
+    const uint32_t tb = pk_ne_bit<0>(H, M) | pk_ne_bit<1>(H, X1) | pk_ne_bit<2>(H, X2) | pk_ne_bit<3>(H, F1) |
+                        pk_lt_bit<4>(Ho1, X1e) | pk_lt_bit<5>(Ho2, X2e) | pk_lt_bit<6>(G1, P1) |
+                        pk_lt_bit<7>(G2, P2);
+    *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)__builtin_amdgcn_perm(0u, tb, 0x0C0C0200u);
+    if (multi) {
+        GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + 3 * j0));
+        kq[0] = (uint16_t)__builtin_amdgcn_perm(K1, MK, 0x0C0C0400u);  // mk(a), k1(a)
+        kq[1] = (uint16_t)__builtin_amdgcn_perm(MK, K2, 0x0C0C0600u);  // k2(a), mk(b)
+        kq[2] = (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u);  // k1(b), k2(b)
+    }
+    const uint32_t Hs = bfi(inv, kNeg2, H);
+    uint32_t *wr = reinterpret_cast<uint32_t *>(&sh.dp.ring16[r % kRing][0][0]);
+    wr[iw] = Hs;
+    wr[kChunk / 2 + iw] = bfi(inv, kNeg2, E1);
+    wr[kChunk + iw] = bfi(inv, kNeg2, E2);
+    if (far) {  // 32-bit spill planes (read by the generic row and the sink lookup)
+        gint *sv = s.sv + svbase;
+        sv[j0] = (int)(short)(H & 0xffff);
+        sv[j0 + 1] = (int)H >> 16;
+        sv[kChunk + j0] = (int)(short)(E1 & 0xffff);
+        sv[kChunk + j0 + 1] = (int)E1 >> 16;
+        sv[2 * kChunk + j0] = (int)(short)(E2 & 0xffff);
+        sv[2 * kChunk + j0 + 1] = (int)E2 >> 16;
+    }
+    ds.r16acc = pk_umin(ds.r16acc, as_u32(as_u16x2(Hs) - as_u16x2(pk2(kR16Low))));  // wraps below kR16Low
+    // leftmost argmax (value << 7 | 127 - column-in-chunk); invalid halves hold -32768
+    const int ca = ((int)(short)(Hs & 0xffff) << 7) | (127 - 2 * lane);
+    const int cbk = (((int)Hs >> 16) << 7) | (126 - 2 * lane);
+    const int mp = readlane(dpp_incl_max(max(ca, cbk), -2147483647 - 1), kWave - 1);
+    const int besti = cb0 + 127 - (mp & 127);
+    const int begs = bcast0(beg), ends = bcast0(end), tbws = bcast0(tbw);
+    ds.tb_used += tbws;
+    if (multi) ds.kp_used += 3 * tbws;
+    if (far) ds.sv_used += 3 * kChunk;
+    ds.cells += ends - begs + 1;
+    if (lane == 0) {
+        sh.rrow[r % kRowRing] = make_int4(beg, end, besti, soff);
+        gint *ri = s.rinfo + (int64_t)r * kRowInfoInts;
+        ri[0] = beg;
+        ri[1] = end;
+        ri[2] = besti;
+        ri[3] = soff;
+        ri[4] = tbbase;
+        ri[5] = kpbase;
+        ri[6] = node;
+        ri[7] = pn;
+    }
+    pp.prv_r = r;
+    pp.prv_beg = beg;
+    pp.prv_end = end;
+    pp.prv_am = besti;
+    return true;
+}
+
 // ---------------------------------------------------------------------------------------------
 // banded DP over all rows of the current graph for read q (qlen): writes the traceback bytes and
 // returns the start row of the backtrack in bi_out (or -1)
 // ---------------------------------------------------------------------------------------------
-template <class SC>
+template <class SC, bool R16>
 __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8_t *q, int qlen,
                       int n, int lane, int64_t &cells, int &bi_out) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
     if ((qlen + kQPad + 2) / 2 > a.qlds) return kStUnsupported;  // the launch sizes the read buffer
     const int w = a.band_b + (int)(a.band_f * (float)qlen);
-    DpState ds{0, 0, 0, 0, {0, 0, 0, 0}};
+    DpState ds{0, 0, 0, 0, 0xffffffffu, 0, {0, 0, 0, 0}};
     const int TBC = (int)a.caps.TBC, KPC = (int)a.caps.KPC, SVC = (int)a.caps.SVC;
     (void)TBC; (void)KPC; (void)SVC;
     // stage the read in LDS (4-bit codes): on gfx9 vmcnt orders loads behind every earlier store,
@@ -966,10 +1242,59 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
             }
             prefetch_row(sh, r, pp);
         }
-        const bool fastok = r > 0 && dp_row_fast(a, sc, s, sh, qlen, w, r, lane, ds, pp);
+        bool fastok;
+        if constexpr (R16) {
+            const DpState ds0 = ds;
+            fastok = r > 0 && !(a.dbg & 2) && dp_row_fast16(a, sc, s, sh, qlen, w, r, lane, ds, pp);
+#ifdef MANDO_DEBUG_R16
+            if (fastok && (a.dbg & 16) && a.prof) {
+                // debug: recompute the row with the generic 16-bit-ring row and record the first
+                // difference (row, lane, fast tb|H, generic tb|H, band) in prof[8..15] of this slot
+                hbm_fence();
+                const int4 rec = sh.rrow[r % kRowRing];
+                const int tbb = (int)ds0.tb_used - (rec.x & ~1);
+                const int j0 = (rec.x & ~1) + 2 * lane;
+                const uint32_t *wr = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[r % kRing][0][0]);
+                const int iw = (j0 >> 1) & (kChunk / 2 - 1);
+                const uint32_t fH = wr[iw], fE1 = wr[kChunk / 2 + iw], fE2 = wr[kChunk + iw];
+                const int ftb = *reinterpret_cast<const GLB uint16_t *>(s.tb + (tbb + j0));
+                const DpState ds1 = ds;
+                ds = ds0;
+                dp_row<SC, R16>(a, sc, s, sh, qlen, w, r, lane, ds);
+                hbm_fence();
+                const int4 rec2 = sh.rrow[r % kRowRing];
+                const uint32_t gH = wr[iw], gE1 = wr[kChunk / 2 + iw], gE2 = wr[kChunk + iw];
+                const int gtb = *reinterpret_cast<const GLB uint16_t *>(s.tb + (tbb + j0));
+                const bool va = j0 >= rec.x && j0 <= rec.y, vb2 = j0 + 1 <= rec.y;
+                const int vm = (va ? 0xff : 0) | (vb2 ? 0xff00 : 0);
+                const uint32_t hm = (va ? 0xffffu : 0) | (vb2 ? 0xffff0000u : 0);
+                const bool bad = ((ftb ^ gtb) & vm) || ((fH ^ gH) & hm) || ((fE1 ^ gE1) & hm) || ((fE2 ^ gE2) & hm) ||
+                                 rec.z != rec2.z;
+                const unsigned long long bm = __ballot(bad);
+                int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
+                if (bm && pf[8] == 0) {
+                    const int bl = __ffsll((long long)bm) - 1;
+                    if (lane == bl) {
+                        pf[8] = 1 + r;
+                        pf[9] = lane | ((int64_t)rec.x << 8) | ((int64_t)rec.y << 24) | ((int64_t)rec.z << 40);
+                        pf[10] = ((int64_t)ftb << 16) | gtb;
+                        pf[11] = ((int64_t)fH << 32) | gH;
+                        pf[12] = ((int64_t)fE1 << 32) | gE1;
+                        pf[13] = ((int64_t)fE2 << 32) | gE2;
+                        pf[14] = rec2.z;
+                        pf[15] = (int64_t)qlen | ((int64_t)n << 20);
+                    }
+                }
+                ds = ds1;
+                (void)ds1;
+            }
+#endif
+        } else {
+            fastok = r > 0 && dp_row_fast(a, sc, s, sh, qlen, w, r, lane, ds, pp);
+        }
         nfast += fastok;
         if (!fastok) {
-            const int st = dp_row(a, sc, s, sh, qlen, w, r, lane, ds);
+            const int st = dp_row<SC, R16>(a, sc, s, sh, qlen, w, r, lane, ds);
             if (st != kStOk) return st;
             const int4 x = sh.rrow[r % kRowRing];
             pp.prv_r = r;
@@ -978,6 +1303,11 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
             pp.prv_am = x.z;
         }
         if (((r + 1) & (kDescBatch - 1)) != 0) prefetch_row(sh, r + 1, pp);
+    }
+    if constexpr (R16) {
+        const uint32_t m = min(ds.r16acc & 0xffffu, ds.r16acc >> 16);
+        const unsigned long long nearinf = __ballot(m < (uint32_t)(kR16High - kR16Low));
+        if (nearinf || bcast0(ds.r16bad)) return kStRetry32;
     }
     cells += ds.cells;
     if (a.prof && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 7] += nfast;
@@ -999,7 +1329,7 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
         if (qlen < pr.beg || qlen > pr.end) continue;
         int hv;
         if (pre_in_ring(sr, p, pr)) {
-            hv = sh.dp.ring[p % kRing][0][qlen & (kChunk - 1)];
+            hv = ring_get<R16>(sh, p % kRing, 0, qlen & (kChunk - 1));
         } else {
             hv = s.sv[pr.soff + (qlen - (pr.beg & ~1))];
         }
@@ -1212,7 +1542,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
         if (i < w.lo || i > w.hi) {
             const uint64_t c0 = a.prof ? clock64() : 0;
             bt_refill(sh, s, i, lane, w, kpwin);
-            if (a.prof && lane == 0) {
+            if (a.prof && !(a.dbg & 16) && lane == 0) {
                 int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
                 pf[12] += (int64_t)(clock64() - c0);
                 pf[13] += 1;
@@ -1228,7 +1558,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
         int vi = i, vj = j, vst = st;
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) bt_step_lds(sh, s, w.lo, w.hi, vi, vj, vst, stall);
-        if (a.prof && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 14] += 1;
+        if (a.prof && !(a.dbg & 16) && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 14] += 1;
         i = bcast0(vi);
         j = bcast0(vj);
         st = bcast0(vst);
@@ -1569,7 +1899,13 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
                     const PoaKArgs aa = args_of(sh);
                     sc = SC{aa.match, aa.mismatch, aa.o1, aa.e1, aa.o2, aa.e2};
                 }
-                st = run_dp<SC>(sh, sc, q, qlen, n, lane, cells, bi);
+                // 16-bit mode when the read's score range allows it; a read that leaves the safe
+                // range is re-aligned in 32-bit mode (the graph is untouched until update_graph)
+                st = (r16_eligible(sc, qlen) && !(args_of(sh).dbg & 1)) ? run_dp<SC, true>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
+                if (st == kStRetry32) {
+                    if (prof && !(args_of(sh).dbg & 16) && lane == 0) prof[15] += 1;
+                    st = run_dp<SC, false>(sh, sc, q, qlen, n, lane, cells, bi);
+                }
                 uint64_t t2 = prof ? clock64() : 0;
                 if (prof && lane == 0) {
                     prof[0] += (int64_t)(t1 - t0);
