@@ -214,6 +214,9 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
             fprintf(stderr, "[mando prof] backtrack per read: refills %.1f (%.0f cyc each) blocks %.1f walk %.0f cyc/block\n",
                     tot[13] / reads, tot[12] / std::max(1.0, tot[13]), tot[14] / reads,
                     (tot[2] - tot[12]) / std::max(1.0, tot[14]));
+        if (getenv("MANDO_BT_STATS"))
+            fprintf(stderr, "[mando prof] run stops per read: window %.1f multi %.1f non-adjacent %.1f not-M %.1f\n",
+                    tot[8] / reads, tot[9] / reads, tot[10] / reads, tot[11] / reads);
         if (tot[8] + tot[9] + tot[10] + tot[11] > 0)
             fprintf(stderr, "[mando prof] per DP row: band %.0f  pre-loop %.0f  compute %.0f  store+argmax %.0f\n",
                     tot[8] / rows, tot[9] / rows, tot[10] / rows, tot[11] / rows);

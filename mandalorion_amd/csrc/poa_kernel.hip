@@ -186,6 +186,7 @@ struct alignas(16) SharedState {
     int4 rrow[kRowRing];            // beg, end, argmax, spill offset of the last kRowRing rows
     int desc[kDescBatch][kDescInts];  // descriptors of the current row batch
     Slot slot;                      // this wave's workspace arrays (read per phase, see slot_of)
+    gint *order0, *order1;          // the two topological-order buffers (slot.order swaps them)
     PoaKArgs args;                  // kernel arguments (read per phase, see args_of)
 };
 static_assert(sizeof(BtLds) <= sizeof(DpLds), "backtrack window must fit the DP scratch");
@@ -262,6 +263,17 @@ __device__ __forceinline__ PoaKArgs args_of(SharedState &sh) {
     a.band_f = __int_as_float(bcast0(__float_as_int(a.band_f)));
     a.prof = uniptr(a.prof);
     a.dbg = bcast0(a.dbg);
+    a.seq = uniptr(a.seq);
+    a.seq_off = uniptr(a.seq_off);
+    a.grp_off = uniptr(a.grp_off);
+    a.gorder = uniptr(a.gorder);
+    a.counter = uniptr(a.counter);
+    a.cons = uniptr(a.cons);
+    a.cons_off = uniptr(a.cons_off);
+    a.cons_len = uniptr(a.cons_len);
+    a.cells = uniptr(a.cells);
+    a.status = uniptr(a.status);
+    a.n_groups = bcast0(a.n_groups);
     return a;
 }
 
@@ -378,7 +390,10 @@ __device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane) {
             s.remrow[r] = val;
             gint *d = s.desc + (int64_t)r * kDescInts;
             d[0] = v;
-            d[1] = vb | (far << 8) | (pn << 16);
+            // bit 15: the row's predecessor structure allows the fast row (1-2 predecessors, all
+            // within the LDS ring); the band-dependent tests are made per read
+            const int sfast = (pn == 1 || pn == 2) && r - pre[0] < kRing && (pn == 1 || r - pre[1] < kRing);
+            d[1] = vb | (far << 8) | (sfast << 15) | (pn << 16);
             d[2] = val;
 #pragma unroll
             for (int k = 0; k < kPreInline; ++k) d[3 + k] = pre[k];
@@ -560,7 +575,7 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
     const int node = dl[0];
     const int d1 = dl[1];
     const int rem = dl[2];
-    const int vb = d1 & 0xff, far = (d1 >> 8) & 0xff, pn = d1 >> 16;
+    const int vb = d1 & 0xff, far = (d1 >> 8) & 1, pn = d1 >> 16;
     if (pn > kWave) return kStUnsupported;
     // ---- predecessor records, lane-parallel
     int pP = 0, pB = 0, pE = -1, pA = 0, pS = -1;
@@ -844,7 +859,7 @@ __device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slo
     const bool ring1 = !two || ((r - p1 < kRing) && row_narrow(x1.x, x1.y));
     // far / multi come from the descriptor (prefetched a row earlier): cheap scalar tests
     const int d1s = bcast0(d1);
-    const bool far = ((d1s >> 8) & 0xff) != 0;
+    const bool far = ((d1s >> 8) & 1) != 0;
     const bool multi = (d1s >> 16) > 1;
     const bool ok = pn >= 1 && pn <= 2 && span <= kChunk && ring0 && ring1 &&
                     ds.tb_used + tbw + kChunk <= (int)a.caps.TBC &&
@@ -1040,91 +1055,68 @@ __device__ __forceinline__ bool r16_eligible(const SC &sc, int qlen) {
            (int64_t)sc.match * qlen <= 30000;
 }
 
-// The fast row in 16-bit mode (same band / bookkeeping as dp_row_fast, values as lane pairs: one
-// packed op per two cells).  Gap states use cb0-relative G (G = H0 + e*(j - cb0)), which keeps the
-// -inf-derived G values near -32768; the scans run on both gap states at once, sign-flipped to
-// unsigned so that DPP's zero fill is the identity.  The score of both columns comes from one
-// v_perm_b32 over a per-row byte table of (score + mismatch).
-template <class SC>
-__device__ __forceinline__ bool dp_row_fast16(const PoaKArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
-                                             int w, int r, int lane, DpState &ds, RowPipe &pp) {
-    const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
-    const int node = pp.node, d1 = pp.d1, rem = pp.rem, p0 = pp.p0, p1 = pp.p1;
-    const int pn = d1 >> 16;
-    const int4 x0 = (p0 == pp.prv_r) ? make_int4(pp.prv_beg, pp.prv_end, pp.prv_am, 0) : pp.x0;
-    const int4 x1 = (p1 == pp.prv_r) ? make_int4(pp.prv_beg, pp.prv_end, pp.prv_am, 0) : pp.x1;
-    const bool two = pn == 2;
-    const int am0 = x0.z + 1, am1 = two ? x1.z + 1 : am0;
-    const int xr = qlen - rem;
-    const int beg = max(0, min(min(am0, am1), xr) - w);
-    const int end = min(qlen, max(max(am0, am1), xr) + w);
-    const int cb0 = beg & ~1;
-    const int span = end - cb0 + 1;
-    const int tbw = (span + 3) & ~3;
-    const bool ring0 = (r - p0 < kRing) && row_narrow(x0.x, x0.y);
-    const bool ring1 = !two || ((r - p1 < kRing) && row_narrow(x1.x, x1.y));
-    const int d1s = bcast0(d1);
-    const bool far = ((d1s >> 8) & 0xff) != 0;
-    const bool multi = (d1s >> 16) > 1;
-    const bool ok = pn >= 1 && pn <= 2 && span <= kChunk && ring0 && ring1 &&
-                    ds.tb_used + tbw + kChunk <= (int)a.caps.TBC &&
-                    (!multi || ds.kp_used + 3 * (tbw + kChunk) <= (int)a.caps.KPC) &&
-                    (!far || ds.sv_used + 3 * kChunk <= (int)a.caps.SVC);
-    if (!__builtin_amdgcn_readfirstlane((int)ok)) return false;
+// ---- 16-bit mode with scalar row control -------------------------------------------------------
+// Everything that is uniform per row (descriptor, predecessor band records, band, fast-path
+// tests, allocation) lives in SGPRs: descriptors come straight from HBM through the scalar cache
+// (s_load, invalidated once per read: build_desc wrote them with vector stores), the previous row's
+// record is forwarded in SGPRs, and other predecessors' records are read from the LDS row ring and
+// broadcast.  The vector unit only does the two cells per lane.
+typedef __attribute__((address_space(4))) const int cint;
 
-    const int tbbase = (int)ds.tb_used - cb0;
-    const int kpbase = (int)ds.kp_used - 3 * cb0;
-    const int soff = far ? (int)ds.sv_used : -1;
-    const int svbase = (int)ds.sv_used - cb0;
+struct Row16 {
+    int r, node, vb, pn, beg, end, cb0, tbw;
+    int p0slot, p1slot;        // ring rows of the predecessors (p % kRing)
+    int b0, e0, b1, e1;        // their bands
+    int two, far, multi, nomask;  // 0/1 (ints: LLVM keeps uniform bools as 64-bit lane masks)
+};
+
+template <class SC>
+__device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *sv, gint *rinfo, SharedState &sh,
+                                         int lane, const Row16 &R, DpState &ds) {
+    const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
+    const int beg = R.beg, end = R.end, cb0 = R.cb0;
+    const int tbbase = ds.tb_used - cb0;
+    const int kpbase = ds.kp_used - 3 * cb0;
+    const int soff = R.far ? ds.sv_used : -1;
+    const int svbase = ds.sv_used - cb0;
     const int j0 = cb0 + 2 * lane;
     const uint32_t J = (uint32_t)j0 * 0x10001u + 0x10000u;         // (j0, j0 + 1)
     const uint32_t LJ = (uint32_t)(2 * lane) * 0x10001u + 0x10000u;  // (j0, j0 + 1) - cb0
-    // halves outside [beg, end]
     const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(beg))) |
                                      as_u32(as_s16x2(pk2(end)) - as_s16x2(J)));
-    // scores of both columns: biased table byte per query code (match+mismatch, 0, N: mismatch)
     const int qbyte = g_qnib[j0 >> 1];
     const uint32_t sel = (uint32_t)(qbyte & 0xf) | (((uint32_t)qbyte & 0xf0u) << 12) | 0x0C000C00u;
-    const int vbs = d1s & 0xff;
-    const uint32_t tlo = vbs < 4 ? (uint32_t)(sc.match + sc.mismatch) << (8 * vbs) : (uint32_t)sc.mismatch * 0x01010101u;
+    const uint32_t tlo =
+        R.vb < 4 ? (uint32_t)(sc.match + sc.mismatch) << (8 * R.vb) : (uint32_t)sc.mismatch * 0x01010101u;
     const uint32_t S = __builtin_amdgcn_perm((uint32_t)sc.mismatch, tlo, sel);
-    // predecessor values: H at (j0-1, j0), E1/E2 at (j0, j0+1), from the 16-bit ring
     const int iw = (j0 >> 1) & (kChunk / 2 - 1), iwp = (iw - 1) & (kChunk / 2 - 1);
-    const uint32_t *w0 = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[p0 % kRing][0][0]);
+    const uint32_t *w0 = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[R.p0slot][0][0]);
     uint32_t Hd = __builtin_amdgcn_alignbit(w0[iw], w0[iwp], 16);
     uint32_t X1 = w0[kChunk / 2 + iw], X2 = w0[kChunk + iw];
-    const int pc0 = x0.x & ~1, pc1 = x1.x & ~1;
-    const bool nm0 = beg - 1 >= pc0 && end <= pc0 + kChunk - 1;
-    const bool nm1 = !two || (beg - 1 >= pc1 && end <= pc1 + kChunk - 1);
-    const bool nomask = __builtin_amdgcn_readfirstlane((int)(nm0 && nm1)) != 0;
-    if ((a.dbg & 4) && !nomask) return false;
-    if ((a.dbg & 8) && far) return false;
-    if (!nomask) {
-        const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0): per half, no borrow
-        const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(x0.x))) |
-                                        as_u32(as_s16x2(pk2(x0.y)) - as_s16x2(JD)));
-        const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(x0.x))) |
-                                        as_u32(as_s16x2(pk2(x0.y)) - as_s16x2(J)));
+    const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0)
+    if (!R.nomask) {
+        const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(R.b0))) |
+                                        as_u32(as_s16x2(pk2(R.e0)) - as_s16x2(JD)));
+        const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(R.b0))) |
+                                        as_u32(as_s16x2(pk2(R.e0)) - as_s16x2(J)));
         Hd = bfi(md, kNeg2, Hd);
         X1 = bfi(me, kNeg2, X1);
         X2 = bfi(me, kNeg2, X2);
     }
     uint32_t MK = 0, K1 = 0, K2 = 0;
-    if (two) {
-        const uint32_t *w1 = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[max(p1, 0) % kRing][0][0]);
+    if (R.two) {
+        const uint32_t *w1 = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[R.p1slot][0][0]);
         uint32_t Hd1 = __builtin_amdgcn_alignbit(w1[iw], w1[iwp], 16);
         uint32_t X11 = w1[kChunk / 2 + iw], X21 = w1[kChunk + iw];
-        if (!nomask) {
-            const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0): per half, no borrow
-            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(x1.x))) |
-                                            as_u32(as_s16x2(pk2(x1.y)) - as_s16x2(JD)));
-            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(x1.x))) |
-                                            as_u32(as_s16x2(pk2(x1.y)) - as_s16x2(J)));
+        if (!R.nomask) {
+            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(R.b1))) |
+                                            as_u32(as_s16x2(pk2(R.e1)) - as_s16x2(JD)));
+            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(R.b1))) |
+                                            as_u32(as_s16x2(pk2(R.e1)) - as_s16x2(J)));
             Hd1 = bfi(md, kNeg2, Hd1);
             X11 = bfi(me, kNeg2, X11);
             X21 = bfi(me, kNeg2, X21);
         }
-        // first predecessor attaining the max (strict > keeps the earlier one)
         MK = pk_lt_bit<0>(Hd, Hd1);
         K1 = pk_lt_bit<0>(X1, X11);
         K2 = pk_lt_bit<0>(X2, X21);
@@ -1134,75 +1126,190 @@ __device__ __forceinline__ bool dp_row_fast16(const PoaKArgs &a, const SC &sc, S
     }
     const uint32_t M = pk_subs(pk_adds(Hd, S), pk2(sc.mismatch));
     const uint32_t H0 = bfi(inv, kNeg2, pk_max(M, pk_max(X1, X2)));
-    // gap states, cb0-relative: G = H0 + e*(j - cb0), F = P - (oe + e*(j - 1 - cb0))
     const uint32_t LJ1 = as_u32(as_u16x2(LJ) * (u16x2){(unsigned short)e1, (unsigned short)e1});
     const uint32_t LJ2 = as_u32(as_u16x2(LJ) * (u16x2){(unsigned short)e2, (unsigned short)e2});
     const uint32_t G1 = pk_adds(H0, LJ1), G2 = pk_adds(H0, LJ2);
-    const uint32_t Ga = __builtin_amdgcn_perm(G2, G1, 0x05040100u);  // (G1a, G2a)
-    const uint32_t Gb = __builtin_amdgcn_perm(G2, G1, 0x07060302u);  // (G1b, G2b)
+    const uint32_t Ga = __builtin_amdgcn_perm(G2, G1, 0x05040100u);
+    const uint32_t Gb = __builtin_amdgcn_perm(G2, G1, 0x07060302u);
     const uint32_t inc = pk_scan_umax(pk_max(Ga, Gb) ^ kNeg2);
     const uint32_t Pa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x138, 0xf, 0xf, true) ^ kNeg2;
     const uint32_t Pb = pk_max(Pa, Ga);
-    const uint32_t P1 = __builtin_amdgcn_perm(Pb, Pa, 0x05040100u);  // (P1a, P1b)
-    const uint32_t P2 = __builtin_amdgcn_perm(Pb, Pa, 0x07060302u);  // (P2a, P2b)
+    const uint32_t P1 = __builtin_amdgcn_perm(Pb, Pa, 0x05040100u);
+    const uint32_t P2 = __builtin_amdgcn_perm(Pb, Pa, 0x07060302u);
     const uint32_t F1 = pk_subs(P1, LJ1 + pk2(oe1 - e1)), F2 = pk_subs(P2, LJ2 + pk2(oe2 - e2));
     const uint32_t H = pk_max(H0, pk_max(F1, F2));
     const uint32_t X1e = pk_subs(X1, pk2(e1)), Ho1 = pk_subs(H, pk2(oe1));
     const uint32_t X2e = pk_subs(X2, pk2(e2)), Ho2 = pk_subs(H, pk2(oe2));
     const uint32_t E1 = pk_max(X1e, Ho1), E2 = pk_max(X2e, Ho2);
-    // traceback bytes (layout in poa_kernel.h), both columns
-    const uint32_t tb = pk_ne_bit<0>(H, M) | pk_ne_bit<1>(H, X1) | pk_ne_bit<2>(H, X2) | pk_ne_bit<3>(H, F1) |
-                        pk_lt_bit<4>(Ho1, X1e) | pk_lt_bit<5>(Ho2, X2e) | pk_lt_bit<6>(G1, P1) |
-                        pk_lt_bit<7>(G2, P2);
-    *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)__builtin_amdgcn_perm(0u, tb, 0x0C0C0200u);
-    if (multi) {
-        GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + 3 * j0));
-        kq[0] = (uint16_t)__builtin_amdgcn_perm(K1, MK, 0x0C0C0400u);  // mk(a), k1(a)
-        kq[1] = (uint16_t)__builtin_amdgcn_perm(MK, K2, 0x0C0C0600u);  // k2(a), mk(b)
-        kq[2] = (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u);  // k1(b), k2(b)
+    const uint32_t tbv = pk_ne_bit<0>(H, M) | pk_ne_bit<1>(H, X1) | pk_ne_bit<2>(H, X2) | pk_ne_bit<3>(H, F1) |
+                         pk_lt_bit<4>(Ho1, X1e) | pk_lt_bit<5>(Ho2, X2e) | pk_lt_bit<6>(G1, P1) |
+                         pk_lt_bit<7>(G2, P2);
+    *reinterpret_cast<GLB uint16_t *>(tb + (tbbase + j0)) = (uint16_t)__builtin_amdgcn_perm(0u, tbv, 0x0C0C0200u);
+    if (R.multi) {
+        GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(kp + (kpbase + 3 * j0));
+        kq[0] = (uint16_t)__builtin_amdgcn_perm(K1, MK, 0x0C0C0400u);
+        kq[1] = (uint16_t)__builtin_amdgcn_perm(MK, K2, 0x0C0C0600u);
+        kq[2] = (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u);
     }
     const uint32_t Hs = bfi(inv, kNeg2, H);
-    uint32_t *wr = reinterpret_cast<uint32_t *>(&sh.dp.ring16[r % kRing][0][0]);
+    uint32_t *wr = reinterpret_cast<uint32_t *>(&sh.dp.ring16[R.r & (kRing - 1)][0][0]);
     wr[iw] = Hs;
     wr[kChunk / 2 + iw] = bfi(inv, kNeg2, E1);
     wr[kChunk + iw] = bfi(inv, kNeg2, E2);
-    if (far) {  // 32-bit spill planes (read by the generic row and the sink lookup)
-        gint *sv = s.sv + svbase;
-        sv[j0] = (int)(short)(H & 0xffff);
-        sv[j0 + 1] = (int)H >> 16;
-        sv[kChunk + j0] = (int)(short)(E1 & 0xffff);
-        sv[kChunk + j0 + 1] = (int)E1 >> 16;
-        sv[2 * kChunk + j0] = (int)(short)(E2 & 0xffff);
-        sv[2 * kChunk + j0 + 1] = (int)E2 >> 16;
+    if (R.far) {
+        gint *svp = sv + svbase;
+        svp[j0] = (int)(short)(H & 0xffff);
+        svp[j0 + 1] = (int)H >> 16;
+        svp[kChunk + j0] = (int)(short)(E1 & 0xffff);
+        svp[kChunk + j0 + 1] = (int)E1 >> 16;
+        svp[2 * kChunk + j0] = (int)(short)(E2 & 0xffff);
+        svp[2 * kChunk + j0 + 1] = (int)E2 >> 16;
     }
-    ds.r16acc = pk_umin(ds.r16acc, as_u32(as_u16x2(Hs) - as_u16x2(pk2(kR16Low))));  // wraps below kR16Low
-    // leftmost argmax (value << 7 | 127 - column-in-chunk); invalid halves hold -32768
+    ds.r16acc = pk_umin(ds.r16acc, as_u32(as_u16x2(Hs) - as_u16x2(pk2(kR16Low))));
     const int ca = ((int)(short)(Hs & 0xffff) << 7) | (127 - 2 * lane);
     const int cbk = (((int)Hs >> 16) << 7) | (126 - 2 * lane);
     const int mp = readlane(dpp_incl_max(max(ca, cbk), -2147483647 - 1), kWave - 1);
     const int besti = cb0 + 127 - (mp & 127);
-    const int begs = bcast0(beg), ends = bcast0(end), tbws = bcast0(tbw);
-    ds.tb_used += tbws;
-    if (multi) ds.kp_used += 3 * tbws;
-    if (far) ds.sv_used += 3 * kChunk;
-    ds.cells += ends - begs + 1;
+    ds.tb_used += R.tbw;
+    if (R.multi) ds.kp_used += 3 * R.tbw;
+    if (R.far) ds.sv_used += 3 * kChunk;
+    ds.cells += end - beg + 1;
     if (lane == 0) {
-        sh.rrow[r % kRowRing] = make_int4(beg, end, besti, soff);
-        gint *ri = s.rinfo + (int64_t)r * kRowInfoInts;
+        sh.rrow[R.r & (kRowRing - 1)] = make_int4(beg, end, besti, soff);
+        gint *ri = rinfo + (int64_t)R.r * kRowInfoInts;
         ri[0] = beg;
         ri[1] = end;
         ri[2] = besti;
         ri[3] = soff;
         ri[4] = tbbase;
         ri[5] = kpbase;
-        ri[6] = node;
-        ri[7] = pn;
+        ri[6] = R.node;
+        ri[7] = R.pn;
     }
-    pp.prv_r = r;
-    pp.prv_beg = beg;
-    pp.prv_end = end;
-    pp.prv_am = besti;
-    return true;
+    return besti;
+}
+
+// The row loop of 16-bit mode (same rows, same results as run_dp<SC, true>).  The per-row
+// control is written for the scalar unit: tests accumulate as sign bits into one word
+// (`bad < 0` = take the generic row) rather than as bools, which the compiler would keep as
+// 64-bit lane masks.
+template <class SC>
+__device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen, int n, int lane, int w,
+                                        DpState &ds, int &nfast) {
+    gu8 *tb, *kp;
+    gint *sv, *rinfo, *desc;
+    int tb_lim, kp_lim, sv_lim;
+    {
+        const Slot s = slot_of(sh);
+        const PoaKArgs a = args_of(sh);
+        tb = s.tb;
+        kp = s.kp;
+        sv = s.sv;
+        rinfo = s.rinfo;
+        desc = s.desc;
+        // a fast row allocates at most tbw + one chunk of slack
+        tb_lim = (int)a.caps.TBC - 2 * (kChunk + 4);
+        kp_lim = (int)a.caps.KPC - 6 * (kChunk + 4);
+        sv_lim = (int)a.caps.SVC - 3 * kChunk;
+    }
+    __builtin_amdgcn_s_dcache_inv();  // descriptors were just written by build_desc (vector stores)
+    int prv_r = -1, prv_beg = 0, prv_end = 0, prv_am = 0;
+    cint *dq = (cint *)(desc + kDescInts);
+    int nd_node = dq[0], nd_d1 = dq[1], nd_rem = dq[2], nd_p0 = dq[3], nd_p1 = dq[4];
+    for (int r = 0; r < n - 1; ++r) {
+        if ((r & (kDescBatch - 1)) == 0) {
+            // descriptors -> LDS for the generic row (one global round trip per batch)
+            const int rr0 = r + lane;
+            if (lane < kDescBatch && rr0 < n) {
+                const gint *dg = desc + (int64_t)rr0 * kDescInts;
+                int *dl = &sh.desc[lane][0];
+#pragma unroll
+                for (int k = 0; k < kDescInts; ++k) dl[k] = dg[k];
+            }
+        }
+        int bad = -1;
+        Row16 R;
+        if (r > 0) {
+            const int node = nd_node, d1 = nd_d1, rem = nd_rem, p0 = nd_p0, p1 = nd_p1;
+            if (r + 1 < n - 1) {  // next row's descriptor, in flight during this row
+                cint *dn = (cint *)(desc + (r + 1) * kDescInts);
+                nd_node = dn[0];
+                nd_d1 = dn[1];
+                nd_rem = dn[2];
+                nd_p0 = dn[3];
+                nd_p1 = dn[4];
+            }
+            if (d1 & 0x8000) {  // 1-2 predecessors, all in the LDS ring (build_desc)
+                int am0, am1;
+                if (p0 == prv_r) {
+                    R.b0 = prv_beg;
+                    R.e0 = prv_end;
+                    am0 = prv_am;
+                } else {
+                    const int4 x = sh.rrow[p0 & (kRowRing - 1)];
+                    R.b0 = bcast0(x.x);
+                    R.e0 = bcast0(x.y);
+                    am0 = bcast0(x.z);
+                }
+                R.two = (d1 >> 16) == 2;
+                if (R.two) {
+                    if (p1 == prv_r) {
+                        R.b1 = prv_beg;
+                        R.e1 = prv_end;
+                        am1 = prv_am;
+                    } else {
+                        const int4 x = sh.rrow[p1 & (kRowRing - 1)];
+                        R.b1 = bcast0(x.x);
+                        R.e1 = bcast0(x.y);
+                        am1 = bcast0(x.z);
+                    }
+                } else {
+                    R.b1 = R.b0;
+                    R.e1 = R.e0;
+                    am1 = am0;
+                }
+                const int xr = qlen - rem;
+                R.beg = max(0, min(min(am0, am1) + 1, xr) - w);
+                R.end = min(qlen, max(max(am0, am1) + 1, xr) + w);
+                R.cb0 = R.beg & ~1;
+                const int span = R.end - R.cb0 + 1;
+                R.tbw = (span + 3) & ~3;
+                const int pc0 = R.b0 & ~1, pc1 = R.b1 & ~1;
+                // each term is negative exactly when its test fails
+                bad = (kChunk - span) | (kChunk - 1 - (R.e0 - pc0)) | (kChunk - 1 - (R.e1 - pc1)) |
+                      (tb_lim - ds.tb_used) | (kp_lim - ds.kp_used) | (sv_lim - ds.sv_used);
+                R.nomask = ((R.beg - 1 - pc0) | (pc0 + kChunk - 1 - R.end) | (R.beg - 1 - pc1) |
+                            (pc1 + kChunk - 1 - R.end)) >= 0;
+                R.r = r;
+                R.node = node;
+                R.vb = d1 & 0xff;
+                R.pn = d1 >> 16;
+                R.far = (d1 >> 8) & 1;
+                R.multi = R.two;
+                R.p0slot = p0 & (kRing - 1);
+                R.p1slot = (R.two ? p1 : p0) & (kRing - 1);
+            }
+        }
+        if (bad >= 0) {
+            const int besti = row16_vec(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
+            prv_r = r;
+            prv_beg = R.beg;
+            prv_end = R.end;
+            prv_am = besti;
+            ++nfast;
+        } else {
+            Slot s = slot_of(sh);
+            const PoaKArgs a = args_of(sh);
+            const int st = dp_row<SC, true>(a, sc, s, sh, qlen, w, r, lane, ds);
+            if (st != kStOk) return st;
+            const int4 x = sh.rrow[r & (kRowRing - 1)];
+            prv_r = r;
+            prv_beg = bcast0(x.x);
+            prv_end = bcast0(x.y);
+            prv_am = bcast0(x.z);
+        }
+    }
+    return kStOk;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1227,6 +1334,10 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
         g_qnib[t >> 1] = (uint8_t)(lo | (hi << 4));
     }
     int nfast = 0;
+    if constexpr (R16) {
+        const int st = run_dp16(sh, sc, qlen, n, lane, w, ds, nfast);
+        if (st != kStOk) return st;
+    } else {
     RowPipe pp;
     pp.prv_r = -1;
     pp.prv_beg = pp.prv_end = pp.prv_am = 0;
@@ -1243,53 +1354,7 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
             prefetch_row(sh, r, pp);
         }
         bool fastok;
-        if constexpr (R16) {
-            const DpState ds0 = ds;
-            fastok = r > 0 && !(a.dbg & 2) && dp_row_fast16(a, sc, s, sh, qlen, w, r, lane, ds, pp);
-#ifdef MANDO_DEBUG_R16
-            if (fastok && (a.dbg & 16) && a.prof) {
-                // debug: recompute the row with the generic 16-bit-ring row and record the first
-                // difference (row, lane, fast tb|H, generic tb|H, band) in prof[8..15] of this slot
-                hbm_fence();
-                const int4 rec = sh.rrow[r % kRowRing];
-                const int tbb = (int)ds0.tb_used - (rec.x & ~1);
-                const int j0 = (rec.x & ~1) + 2 * lane;
-                const uint32_t *wr = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[r % kRing][0][0]);
-                const int iw = (j0 >> 1) & (kChunk / 2 - 1);
-                const uint32_t fH = wr[iw], fE1 = wr[kChunk / 2 + iw], fE2 = wr[kChunk + iw];
-                const int ftb = *reinterpret_cast<const GLB uint16_t *>(s.tb + (tbb + j0));
-                const DpState ds1 = ds;
-                ds = ds0;
-                dp_row<SC, R16>(a, sc, s, sh, qlen, w, r, lane, ds);
-                hbm_fence();
-                const int4 rec2 = sh.rrow[r % kRowRing];
-                const uint32_t gH = wr[iw], gE1 = wr[kChunk / 2 + iw], gE2 = wr[kChunk + iw];
-                const int gtb = *reinterpret_cast<const GLB uint16_t *>(s.tb + (tbb + j0));
-                const bool va = j0 >= rec.x && j0 <= rec.y, vb2 = j0 + 1 <= rec.y;
-                const int vm = (va ? 0xff : 0) | (vb2 ? 0xff00 : 0);
-                const uint32_t hm = (va ? 0xffffu : 0) | (vb2 ? 0xffff0000u : 0);
-                const bool bad = ((ftb ^ gtb) & vm) || ((fH ^ gH) & hm) || ((fE1 ^ gE1) & hm) || ((fE2 ^ gE2) & hm) ||
-                                 rec.z != rec2.z;
-                const unsigned long long bm = __ballot(bad);
-                int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
-                if (bm && pf[8] == 0) {
-                    const int bl = __ffsll((long long)bm) - 1;
-                    if (lane == bl) {
-                        pf[8] = 1 + r;
-                        pf[9] = lane | ((int64_t)rec.x << 8) | ((int64_t)rec.y << 24) | ((int64_t)rec.z << 40);
-                        pf[10] = ((int64_t)ftb << 16) | gtb;
-                        pf[11] = ((int64_t)fH << 32) | gH;
-                        pf[12] = ((int64_t)fE1 << 32) | gE1;
-                        pf[13] = ((int64_t)fE2 << 32) | gE2;
-                        pf[14] = rec2.z;
-                        pf[15] = (int64_t)qlen | ((int64_t)n << 20);
-                    }
-                }
-                ds = ds1;
-                (void)ds1;
-            }
-#endif
-        } else {
+        {
             fastok = r > 0 && dp_row_fast(a, sc, s, sh, qlen, w, r, lane, ds, pp);
         }
         nfast += fastok;
@@ -1303,6 +1368,7 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
             pp.prv_am = x.z;
         }
         if (((r + 1) & (kDescBatch - 1)) != 0) prefetch_row(sh, r + 1, pp);
+    }
     }
     if constexpr (R16) {
         const uint32_t m = min(ds.r16acc & 0xffffu, ds.r16acc >> 16);
@@ -1551,6 +1617,48 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
                 glob_row = i;
                 w.lo = 1;
                 w.hi = 0;
+                continue;
+            }
+        }
+        if (st == 0) {
+            // Diagonal run, wave-parallel: lane k checks cell (i-k, j-k) -- an M step whose source
+            // predecessor (the only one, or the one its predecessor byte names) is the row right
+            // above.  Every step before the first lane that fails is taken at once (runs end at
+            // indels and at graph rows out of order, typically tens of cells apart).
+            const int ri = i - lane, cj = j - lane;
+            bool okk = false;
+            int nd = 0;
+            if (ri >= w.lo && ri > 0 && cj > 0) {
+                const int idx = w.hi - ri;
+                const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][0]);
+                const int t = sh.bt.tb[m0.x + cj];
+                int pr = m0.w;
+                if (m0.y != kKpNone) {
+                    const int4 m1 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][4]);
+                    const int k0 = g_qnib[m0.y + 3 * cj];
+                    pr = k0 == 0 ? m0.w : k0 == 1 ? m1.x : k0 == 2 ? m1.y : k0 == 3 ? m1.z : k0 == 4 ? m1.w : -1;
+                }
+                okk = pr == ri - 1 && !(t & kTbNM);
+                nd = m0.z;
+            }
+            const unsigned long long bad = ~__ballot(okk);
+            const int f = bad ? __ffsll((long long)bad) - 1 : kWave;
+#ifdef MANDO_BT_STATS
+            if (a.prof && f < kWave) {
+                int why = 0;
+                if (ri >= w.lo && ri > 0 && cj > 0) {
+                    const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[w.hi - ri][0]);
+                    const int t = sh.bt.tb[m0.x + cj];
+                    why = (t & kTbNM) ? 3 : 2;
+                }
+                why = readlane(why, f);
+                if (lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 8 + why] += 1;
+            }
+#endif
+            if (f > 0) {
+                if (lane < f) s.qnode[cj - 1] = nd;
+                i -= f;
+                j -= f;
                 continue;
             }
         }
@@ -1855,41 +1963,71 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
     s.nxt = (gint *)(ws + a.lay.nxt);
     s.order = (gint *)(ws + a.lay.order0);
     s.order2 = (gint *)(ws + a.lay.order1);
-    if (lane == 0) sh.slot = s;
+    if (lane == 0) {
+        sh.slot = s;
+        sh.order0 = s.order;
+        sh.order1 = s.order2;
+    }
     wave_sync();
-    int64_t *prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
 
+    // Nothing of the kernel arguments or the slot stays live across the loop: every phase re-reads
+    // what it needs from LDS (args_of / slot_of), which keeps SGPRs free for the DP row loop.
     for (;;) {
         int gi = 0;
-        if (lane == 0) gi = atomicAdd(a.counter, 1);
-        gi = bcast0(gi);
-        if (gi >= a.n_groups) break;
-        const int g = a.gorder ? a.gorder[gi] : gi;
+        {
+            const PoaKArgs a = args_of(sh);
+            if (lane == 0) gi = atomicAdd(a.counter, 1);
+            gi = bcast0(gi);
+            if (gi >= a.n_groups) break;
+        }
+        int g;
+        int64_t r0, r1;
+        {
+            const PoaKArgs a = args_of(sh);
+            g = a.gorder ? bcast0(a.gorder[gi]) : gi;
+            r0 = uni64(a.grp_off[g]);
+            r1 = uni64(a.grp_off[g + 1]);
+        }
         if (lane == 0) {
-            sh.slot.order = (gint *)(ws + a.lay.order0);
-            sh.slot.order2 = (gint *)(ws + a.lay.order1);
+            sh.slot.order = sh.order0;
+            sh.slot.order2 = sh.order1;
         }
         wave_sync();
-        const int64_t r0 = a.grp_off[g], r1 = a.grp_off[g + 1];
         int st = kStOk;
         int n = 0, ng = 0;
         int64_t cells = 0;
         int64_t first = r0;
-        while (first < r1 && a.seq_off[first + 1] - a.seq_off[first] <= 0) ++first;
+        {
+            const PoaKArgs a = args_of(sh);
+            while (first < r1 && a.seq_off[first + 1] - a.seq_off[first] <= 0) ++first;
+            first = uni64(first);
+        }
         int clen = 0;
         if (first < r1) {
-            const uint8_t *q0 = a.seq + a.seq_off[first];
-            const int L0 = (int)(a.seq_off[first + 1] - a.seq_off[first]);
-            st = init_chain(sh, q0, L0, lane, n);
+            {
+                const PoaKArgs a = args_of(sh);
+                const int64_t o0 = uni64(a.seq_off[first]);
+                const uint8_t *q0 = a.seq + o0;
+                const int L0 = (int)(uni64(a.seq_off[first + 1]) - o0);
+                st = init_chain(sh, q0, L0, lane, n);
+            }
             wave_sync();
             for (int64_t rd = first + 1; rd < r1 && st == kStOk; ++rd) {
-                const int qlen = (int)(a.seq_off[rd + 1] - a.seq_off[rd]);
-                if (qlen <= 0) continue;
-                if (qlen > a.caps.QC) {
-                    st = kStCap;
-                    break;
+                int qlen;
+                const uint8_t *q;
+                int64_t *prof;
+                {
+                    const PoaKArgs a = args_of(sh);
+                    const int64_t o0 = uni64(a.seq_off[rd]);
+                    qlen = (int)(uni64(a.seq_off[rd + 1]) - o0);
+                    if (qlen <= 0) continue;
+                    if (qlen > a.caps.QC) {
+                        st = kStCap;
+                        break;
+                    }
+                    q = a.seq + o0;
+                    prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
                 }
-                const uint8_t *q = a.seq + a.seq_off[rd];
                 uint64_t t0 = prof ? clock64() : 0;
                 build_desc(sh, n, lane);
                 uint64_t t1 = prof ? clock64() : 0;
@@ -1901,9 +2039,10 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
                 }
                 // 16-bit mode when the read's score range allows it; a read that leaves the safe
                 // range is re-aligned in 32-bit mode (the graph is untouched until update_graph)
-                st = (r16_eligible(sc, qlen) && !(args_of(sh).dbg & 1)) ? run_dp<SC, true>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
+                st = (r16_eligible(sc, qlen) && !(args_of(sh).dbg & 1)) ? run_dp<SC, true>(sh, sc, q, qlen, n, lane, cells, bi)
+                                                                        : kStRetry32;
                 if (st == kStRetry32) {
-                    if (prof && !(args_of(sh).dbg & 16) && lane == 0) prof[15] += 1;
+                    if (prof && lane == 0) prof[15] += 1;
                     st = run_dp<SC, false>(sh, sc, q, qlen, n, lane, cells, bi);
                 }
                 uint64_t t2 = prof ? clock64() : 0;
@@ -1933,6 +2072,8 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
                 }
             }
             if (st == kStOk) {
+                const PoaKArgs a = args_of(sh);
+                int64_t *prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
                 uint64_t t6 = prof ? clock64() : 0;
                 int cst = kStOk, len = 0;
                 if (lane == 0) {
@@ -1945,6 +2086,7 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
             }
         }
         if (lane == 0) {
+            const PoaKArgs a = args_of(sh);
             a.status[g] = st;
             a.cons_len[g] = clen;
             a.cells[g] = cells;
