@@ -194,6 +194,41 @@ int mando_sam_to_psl(const char *sam_path, const char *psl_path, int32_t mando_m
  * their blocks; primary != 0 keeps only the first line per read name. */
 int mando_clean_psl(const char *in_path, const char *out_path, int32_t primary, int64_t *n_records);
 
+/* Module F, filterIsoforms.py arguments (:19-47) */
+typedef struct {
+    double minimum_ratio;          /* -r */
+    double minimum_reads;          /* -R */
+    double internal_ratio;         /* -n */
+    double Acutoff;                /* -A */
+    int32_t overhangs[4];          /* -O "a,b,c,d" */
+    int32_t splice_window;         /* -s */
+    int32_t downstream_buffer;     /* -d */
+    int32_t minimum_isoform_length; /* -I */
+    int32_t multi_exon_only;       /* -M */
+    int32_t threads;               /* -t (chromosomes in parallel; <= 0: all cores) */
+} mando_filter_params;
+
+void mando_filter_default_params(mando_filter_params *p);
+
+/* filter_sam (filterIsoforms.py:280-296): drops secondary (256) and supplementary (2048) records. */
+int mando_filter_sam(const char *sam_path, const char *out_path, int64_t *n_kept);
+
+/* Per-chromosome isoform filters of module F (filterIsoforms.py:81-278, :310-410, :456-510) on the
+ * clean PSL of the consensi's alignments: absolute filters, relative expression, polyA extension and
+ * containment.  Writes the kept consensi (FASTA), their PSL lines and, if reasons_path, the filter
+ * reasons (what the reference writes to stderr).  whitelist_bed: polyAWhiteList.bed (or NULL). */
+int mando_filter_isoforms(const mando_filter_params *p, const char *isoform_fasta, const char *genome_fasta,
+                          const char *clean_psl, const char *whitelist_bed, const char *out_fasta,
+                          const char *out_psl, const char *reasons_path, int64_t *n_kept);
+
+/* psl_to_gtf (filterIsoforms.py:413-433). */
+int mando_psl_to_gtf(const char *psl_path, const char *gtf_path);
+
+/* Module Q, assignReadsToIsoforms.py:27-105: per-sample read counts and TPM of
+ * every isoform of the filtered PSL, from reads2isoforms.txt and the read files (FASTA/FASTQ, gz). */
+int mando_quantify(const char *const *fasta_paths, int32_t n_fasta, const char *r2i_path,
+                   const char *filtered_psl, const char *out_quant, const char *out_tpm);
+
 #ifdef __cplusplus
 }
 #endif

@@ -38,6 +38,11 @@ EXPORTED = (
     "mando_split_loci",
     "mando_sam_to_psl",
     "mando_clean_psl",
+    "mando_filter_default_params",
+    "mando_filter_sam",
+    "mando_filter_isoforms",
+    "mando_psl_to_gtf",
+    "mando_quantify",
 )
 
 STATUS = {
@@ -175,6 +180,12 @@ def load(path: str | None = None):
         lib.mando_split_loci.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _P, _P]
         lib.mando_sam_to_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, _P]
         lib.mando_clean_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, _P]
+        lib.mando_filter_default_params.argtypes = [_P]
+        lib.mando_filter_default_params.restype = None
+        lib.mando_filter_sam.argtypes = [ctypes.c_char_p, ctypes.c_char_p, _P]
+        lib.mando_filter_isoforms.argtypes = [_P] + [ctypes.c_char_p] * 7 + [_P]
+        lib.mando_psl_to_gtf.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        lib.mando_quantify.argtypes = [_P, ctypes.c_int32] + [ctypes.c_char_p] * 4
         lib.mando_pack_segments.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, ctypes.c_int32]
         if hasattr(lib, "mando_selftest"):
             lib.mando_selftest.argtypes = [_P, _P]

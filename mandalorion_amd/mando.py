@@ -4,9 +4,11 @@ Keeps the reference's command-line surface (/root/reference/Mando.py:22-205) so 
 `Mando.py -M D ...` can switch over unchanged.  Only the D module (defining isoforms) is built here:
 it runs mandalorion_amd.define (clustering on host C++ threads, orientation and POA consensus on the
 GPU) with exactly the arguments Mando.py passes to defineIsoforms.py (Mando.py:382-399).  Module P
-(SAM -> PSL, clean_psl, sort + locus split: the D module's input) runs natively (mandalorion_amd.psl).
-The other modules (A alignment, F filtering, Q quantification) are outside this build's scope
- and are reported and skipped.  Without a SAM, P starts from an existing clean PSL.
+(SAM -> PSL, clean_psl, sort + locus split: the D module's input) runs natively (mandalorion_amd.psl);
+so do modules F (isoform filters, with minimap2 as the external aligner of the consensi or an existing
+tmp/Isoforms.aligned.out.sam) and Q (quantification) (mandalorion_amd.modules).  Module A (read
+alignment) and F's gene grouping (groupIsoforms.py) are outside this build's scope and are
+reported and skipped.  Without a SAM, P starts from an existing clean PSL.
 """
 from __future__ import annotations
 
@@ -88,6 +90,57 @@ def main(argv: list[str] | None = None) -> int:
             nrec, nloc = psl.split_loci(clean, temp_path + "/tmp_SS", sort_lines=True,
                                         sorted_out=temp_path + "/mm2Alignments.clean.sorted.psl")
             print(f"\t\tsplit {nrec} psl entries into {nloc} loci")
+            continue
+        if mod == "F":
+            # module F (Mando.py:404-470): filterIsoforms natively; the consensi's alignment is minimap2's
+            # (--mm2_path) or an existing tmp/Isoforms.aligned.out.sam
+            import shutil
+
+            from . import modules, psl
+
+            iso = temp_path + "/Isoform_Consensi.fasta"
+            ok = os.path.exists(iso) and os.path.getsize(iso) > 0
+            if not ok:
+                print("\tisoforms fasta missing or empty")
+            if not a.genome_sequence or not os.path.exists(a.genome_sequence) or os.path.getsize(a.genome_sequence) == 0:
+                print("\tgenome sequence fasta missing or empty")
+                ok = False
+            if not ok:
+                print("\tone or more input files missing or empty. Isoforms not filtered")
+                continue
+            p = modules.FilterParams.default()
+            p.minimum_ratio = float(a.minimum_ratio)
+            p.minimum_reads = float(a.minimum_reads)
+            p.internal_ratio = float(a.minimum_internal_ratio)
+            p.Acutoff = float(a.Acutoff)
+            for i, v in enumerate(a.overhangs.split(",")):
+                p.overhangs[i] = int(v)
+            p.splice_window = int(a.splice_site_window)
+            p.downstream_buffer = int(a.downstream_buffer)
+            p.minimum_isoform_length = int(a.minimum_isoform_length)
+            p.multi_exon_only = int(a.multi_exon_only)
+            p.threads = int(a.minimap2_threads)
+            n = modules.module_f(temp_path, iso, a.genome_sequence, p, minimap2=a.mm2_path,
+                                 threads=int(a.minimap2_threads))
+            print(f"\t{n} isoforms kept")
+            srt = temp_path + "/Isoforms.sorted.psl"
+            psl.split_loci(temp_path + "/Isoforms.filtered.clean.psl", temp_path + "/tmp_iso_split", sort_lines=True,
+                           sorted_out=srt)
+            shutil.rmtree(temp_path + "/tmp_iso_split", ignore_errors=True)
+            print("\tgene grouping (groupIsoforms.py) is not part of this build")
+            for f in os.listdir(temp_path):
+                if f.startswith("Isoforms.filtered."):
+                    shutil.copy(os.path.join(temp_path, f), path)
+            continue
+        if mod == "Q":
+            # module Q (Mando.py:474-491): assignReadsToIsoforms natively
+            import shutil
+
+            from . import modules
+
+            modules.quantify(temp_path, fasta_list)
+            for f in ("Isoforms.filtered.clean.quant", "Isoforms.filtered.clean.tpm"):
+                shutil.copy(temp_path + "/" + f, path)
             continue
         if mod != "D":
             print(f"\tmodule {mod}: not part of this build (D module only), skipped")

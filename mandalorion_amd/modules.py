@@ -1,0 +1,87 @@
+"""Modules F and Q natively (libmando, csrc/module_f.cpp): the consumers of the D module's consensi
+(SURVEY.md §8(f) rows 3-4).
+
+- Module F: filterIsoforms.py (/root/reference/filterIsoforms.py:456-510). The consensi are aligned by
+  an external aligner (minimap2, as in the reference), then filter_sam -> SAM->PSL (emtrey, plain
+  mode) -> clean_psl(primary=False) -> per-chromosome filters -> Isoforms.filtered.fasta,
+  Isoforms.filtered.clean.psl, Isoforms.filtered.clean.gtf, filter_reasons.txt.
+- Module Q: assignReadsToIsoforms.py:27-105 -> Isoforms.filtered.clean.quant / .tpm.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+from . import _lib, psl
+
+
+class FilterParams(ctypes.Structure):
+    """include/mando.h mando_filter_params (filterIsoforms.py arguments)."""
+    _fields_ = [("minimum_ratio", ctypes.c_double), ("minimum_reads", ctypes.c_double),
+                ("internal_ratio", ctypes.c_double), ("Acutoff", ctypes.c_double),
+                ("overhangs", ctypes.c_int32 * 4), ("splice_window", ctypes.c_int32),
+                ("downstream_buffer", ctypes.c_int32), ("minimum_isoform_length", ctypes.c_int32),
+                ("multi_exon_only", ctypes.c_int32), ("threads", ctypes.c_int32)]
+
+    @classmethod
+    def default(cls) -> "FilterParams":
+        p = cls()
+        _lib.load().mando_filter_default_params(ctypes.byref(p))
+        return p
+
+
+def filter_sam(sam: str, out: str) -> int:
+    n = ctypes.c_int64()
+    _lib.check(_lib.load().mando_filter_sam(sam.encode(), out.encode(), ctypes.byref(n)))
+    return n.value
+
+
+def psl_to_gtf(psl_file: str, gtf_file: str) -> None:
+    _lib.check(_lib.load().mando_psl_to_gtf(psl_file.encode(), gtf_file.encode()))
+
+
+def filter_isoforms(params: FilterParams, isoform_fasta: str, genome_fasta: str, clean_psl: str,
+                    whitelist_bed: str | None, out_fasta: str, out_psl: str, reasons: str | None = None) -> int:
+    n = ctypes.c_int64()
+    enc = lambda x: x.encode() if x else None  # noqa: E731
+    _lib.check(_lib.load().mando_filter_isoforms(ctypes.byref(params), enc(isoform_fasta), enc(genome_fasta),
+                                                 enc(clean_psl), enc(whitelist_bed), enc(out_fasta), enc(out_psl),
+                                                 enc(reasons), ctypes.byref(n)))
+    return n.value
+
+
+def module_f(path: str, isoform_fasta: str, genome_fasta: str, params: FilterParams,
+             minimap2: str | None = None, threads: int = 8) -> int:
+    """filterIsoforms.main (filterIsoforms.py:456-510) in `path`.  The alignment of the consensi is the
+    reference's minimap2 command when `minimap2` is given; otherwise `path`/Isoforms.aligned.out.sam
+    must already exist."""
+    sam = os.path.join(path, "Isoforms.aligned.out.sam")
+    fsam = os.path.join(path, "Isoforms.aligned.out.filtered.sam")
+    pslf = os.path.join(path, "Isoforms.aligned.out.psl")
+    clean = os.path.join(path, "Isoforms.aligned.out.clean.psl")
+    if minimap2:
+        with open(sam, "w") as out:
+            subprocess.run([minimap2, "-G", "400k", "-uf", "--secondary=no", "-ax", "splice:hq", "-t", str(threads),
+                            genome_fasta, isoform_fasta], stdout=out, check=True)
+    if not os.path.exists(sam):
+        raise FileNotFoundError(f"{sam} (consensus alignments; pass an aligner or provide the SAM)")
+    filter_sam(sam, fsam)
+    psl.sam_to_psl(fsam, pslf, mando=False, threads=threads)
+    psl.clean_psl(pslf, clean, False)
+    out_fa = os.path.join(path, "Isoforms.filtered.fasta")
+    out_psl = os.path.join(path, "Isoforms.filtered.clean.psl")
+    wl = os.path.join(path, "polyAWhiteList.bed")
+    n = filter_isoforms(params, isoform_fasta, genome_fasta, clean, wl, out_fa, out_psl,
+                        os.path.join(path, "filter_reasons.txt"))
+    psl_to_gtf(out_psl, os.path.join(path, "Isoforms.filtered.clean.gtf"))
+    return n
+
+
+def quantify(folder: str, fasta_files: list[str]) -> None:
+    """assignReadsToIsoforms.py -m folder -f files: Isoforms.filtered.clean.quant / .tpm in folder."""
+    arr = (ctypes.c_char_p * len(fasta_files))(*[f.encode() for f in fasta_files])
+    _lib.check(_lib.load().mando_quantify(arr, len(fasta_files), os.path.join(folder, "reads2isoforms.txt").encode(),
+                                          os.path.join(folder, "Isoforms.filtered.clean.psl").encode(),
+                                          os.path.join(folder, "Isoforms.filtered.clean.quant").encode(),
+                                          os.path.join(folder, "Isoforms.filtered.clean.tpm").encode()))
