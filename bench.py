@@ -274,7 +274,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int32",
+        "dtype": "int16",
         "data": "synthetic R2C2-shaped read groups (seed 20250117+rank), oriented, inputs resident in HBM",
         "config": {
             "workload": f"config3: {n_groups} isoform groups x {args.depth} reads x {args.len_lo}-{args.len_hi} nt "
