@@ -1625,24 +1625,35 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
             // predecessor (the only one, or the one its predecessor byte names) is the row right
             // above.  Every step before the first lane that fails is taken at once (runs end at
             // indels and at graph rows out of order, typically tens of cells apart).
+            // The first failing lane's cell, when it is still an M step (its predecessor merely
+            // not the row right above: a branch of the graph), is taken too, so runs continue
+            // through the graph's branches instead of falling back to the serial walk.
             const int ri = i - lane, cj = j - lane;
-            bool okk = false;
-            int nd = 0;
+            bool okk = false, okm = false;
+            int nd = 0, pr = -1;
             if (ri >= w.lo && ri > 0 && cj > 0) {
                 const int idx = w.hi - ri;
                 const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][0]);
                 const int t = sh.bt.tb[m0.x + cj];
-                int pr = m0.w;
+                pr = m0.w;
                 if (m0.y != kKpNone) {
                     const int4 m1 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][4]);
                     const int k0 = g_qnib[m0.y + 3 * cj];
                     pr = k0 == 0 ? m0.w : k0 == 1 ? m1.x : k0 == 2 ? m1.y : k0 == 3 ? m1.z : k0 == 4 ? m1.w : -1;
                 }
-                okk = pr == ri - 1 && !(t & kTbNM);
+                okm = pr >= 0 && !(t & kTbNM);
+                okk = okm && pr == ri - 1;
                 nd = m0.z;
             }
             const unsigned long long bad = ~__ballot(okk);
             const int f = bad ? __ffsll((long long)bad) - 1 : kWave;
+            if (f < kWave && ((__ballot(okm) >> f) & 1ull)) {
+                // lanes [0, f] are all M steps; lane f's leads to predecessor row pr (not f's i-1)
+                if (lane <= f) s.qnode[cj - 1] = nd;
+                i = readlane(pr, f);
+                j -= f + 1;
+                continue;
+            }
 #ifdef MANDO_BT_STATS
             if (a.prof && f < kWave) {
                 int why = 0;
