@@ -1212,10 +1212,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         kp_lim = (int)a.caps.KPC - 6 * (kChunk + 4);
         sv_lim = (int)a.caps.SVC - 3 * kChunk;
     }
-    __builtin_amdgcn_s_dcache_inv();  // descriptors were just written by build_desc (vector stores)
     int prv_r = -1, prv_beg = 0, prv_end = 0, prv_am = 0;
-    cint *dq = (cint *)(desc + kDescInts);
-    int nd_node = dq[0], nd_d1 = dq[1], nd_rem = dq[2], nd_p0 = dq[3], nd_p1 = dq[4];
     for (int r = 0; r < n - 1; ++r) {
         if ((r & (kDescBatch - 1)) == 0) {
             // descriptors -> LDS for the generic row (one global round trip per batch)
@@ -1230,15 +1227,11 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         int bad = -1;
         Row16 R;
         if (r > 0) {
-            const int node = nd_node, d1 = nd_d1, rem = nd_rem, p0 = nd_p0, p1 = nd_p1;
-            if (r + 1 < n - 1) {  // next row's descriptor, in flight during this row
-                cint *dn = (cint *)(desc + (r + 1) * kDescInts);
-                nd_node = dn[0];
-                nd_d1 = dn[1];
-                nd_rem = dn[2];
-                nd_p0 = dn[3];
-                nd_p1 = dn[4];
-            }
+            // this row's descriptor from the LDS batch (an HBM scalar load per row would put a full
+            // memory latency on every row: build_desc's stores are long out of L2 by now)
+            const int4 dA = *reinterpret_cast<const int4 *>(&sh.desc[r & (kDescBatch - 1)][0]);
+            const int node = bcast0(dA.x), d1 = bcast0(dA.y), rem = bcast0(dA.z), p0 = bcast0(dA.w);
+            const int p1 = bcast0(sh.desc[r & (kDescBatch - 1)][4]);
             if (d1 & 0x8000) {  // 1-2 predecessors, all in the LDS ring (build_desc)
                 int am0, am1;
                 if (p0 == prv_r) {
