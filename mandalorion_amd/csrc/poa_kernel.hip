@@ -1213,15 +1213,21 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         sv_lim = (int)a.caps.SVC - 3 * kChunk;
     }
     int prv_r = -1, prv_beg = 0, prv_end = 0, prv_am = 0;
+    // Descriptor batches reach LDS one batch ahead: lane l holds ints [4l, 4l+4) of the next 32 rows
+    // (loaded while the current batch's rows run), so the batch refill waits on no HBM round trip.
+    static_assert(kDescBatch * kDescInts == 4 * kWave, "one int4 per lane per descriptor batch");
+    int4 pf = make_int4(0, 0, 0, 0);
+    if ((lane >> 1) < n) {
+        const GLB int4 *g = reinterpret_cast<const GLB int4 *>(desc + 4 * lane);
+        pf = make_int4(g->x, g->y, g->z, g->w);
+    }
     for (int r = 0; r < n - 1; ++r) {
         if ((r & (kDescBatch - 1)) == 0) {
-            // descriptors -> LDS for the generic row (one global round trip per batch)
-            const int rr0 = r + lane;
-            if (lane < kDescBatch && rr0 < n) {
-                const gint *dg = desc + (int64_t)rr0 * kDescInts;
-                int *dl = &sh.desc[lane][0];
-#pragma unroll
-                for (int k = 0; k < kDescInts; ++k) dl[k] = dg[k];
+            if (r + (lane >> 1) < n) *reinterpret_cast<int4 *>(&sh.desc[0][0] + 4 * lane) = pf;
+            const int rn = r + kDescBatch;
+            if (rn < n && rn + (lane >> 1) < n) {
+                const GLB int4 *g = reinterpret_cast<const GLB int4 *>(desc + (int64_t)rn * kDescInts + 4 * lane);
+                pf = make_int4(g->x, g->y, g->z, g->w);
             }
         }
         int bad = -1;
