@@ -218,7 +218,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
             fprintf(stderr, "[mando prof] run stops per read: window %.1f multi %.1f non-adjacent %.1f not-M %.1f\n",
                     tot[8] / reads, tot[9] / reads, tot[10] / reads, tot[11] / reads);
         if (tot[8] + tot[9] + tot[10] + tot[11] > 0)
-            fprintf(stderr, "[mando prof] per DP row: band %.0f  pre-loop %.0f  compute %.0f  store+argmax %.0f\n",
+            fprintf(stderr, "[mando prof] per DP row: seg0 %.3f  seg1 %.4f  seg2 %.4f  seg3 %.4f\n",
                     tot[8] / rows, tot[9] / rows, tot[10] / rows, tot[11] / rows);
     }
     return MANDO_OK;

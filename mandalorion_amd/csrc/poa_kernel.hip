@@ -393,7 +393,12 @@ __device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane) {
             // bit 15: the row's predecessor structure allows the fast row (1-2 predecessors, all
             // within the LDS ring); the band-dependent tests are made per read
             const int sfast = (pn == 1 || pn == 2) && r - pre[0] < kRing && (pn == 1 || r - pre[1] < kRing);
-            d[1] = vb | (far << 8) | (sfast << 15) | (pn << 16);
+            // bit 14: 3..kPreInline predecessors, all within the LDS ring (the 16-bit row loop's
+            // multi-predecessor fast row)
+            bool near = pn >= 3 && pn <= kPreInline;
+#pragma unroll
+            for (int k = 0; k < kPreInline; ++k) near = near && (k >= pn || r - pre[k] < kRing);
+            d[1] = vb | (far << 8) | (near ? (1 << 14) : 0) | (sfast << 15) | (pn << 16);
             d[2] = val;
 #pragma unroll
             for (int k = 0; k < kPreInline; ++k) d[3 + k] = pre[k];
@@ -1068,6 +1073,7 @@ struct Row16 {
     int p0slot, p1slot;        // ring rows of the predecessors (p % kRing)
     int b0, e0, b1, e1;        // their bands
     int two, far, multi, nomask;  // 0/1 (ints: LLVM keeps uniform bools as 64-bit lane masks)
+    int pn3;                      // predecessor count when >= 3 (predecessors 2.. are read in row16_vec)
 };
 
 template <class SC>
@@ -1123,6 +1129,33 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         Hd = pk_max(Hd, Hd1);
         X1 = pk_max(X1, X11);
         X2 = pk_max(X2, X21);
+    }
+    // predecessors 2.. of a multi-predecessor row (records re-read from the LDS row ring; the first
+    // strictly larger value names the predecessor, as in dp_row)
+    for (int k = 2; k < R.pn3; ++k) {
+        const int p = bcast0(sh.desc[R.r & (kDescBatch - 1)][3 + k]);
+        const int4 x = sh.rrow[p & (kRowRing - 1)];
+        const int bk = bcast0(x.x), ek = bcast0(x.y);
+        const uint32_t *wk = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[p & (kRing - 1)][0][0]);
+        uint32_t Hdk = __builtin_amdgcn_alignbit(wk[iw], wk[iwp], 16);
+        uint32_t X1k = wk[kChunk / 2 + iw], X2k = wk[kChunk + iw];
+        const int pck = bk & ~1;
+        if (((beg - 1 - pck) | (pck + kChunk - 1 - end)) < 0) {
+            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(bk))) |
+                                            as_u32(as_s16x2(pk2(ek)) - as_s16x2(JD)));
+            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(bk))) |
+                                            as_u32(as_s16x2(pk2(ek)) - as_s16x2(J)));
+            Hdk = bfi(md, kNeg2, Hdk);
+            X1k = bfi(me, kNeg2, X1k);
+            X2k = bfi(me, kNeg2, X2k);
+        }
+        const uint32_t kk = pk2(k);
+        MK = bfi(pk_neg_mask(pk_subs(Hd, Hdk)), kk, MK);
+        K1 = bfi(pk_neg_mask(pk_subs(X1, X1k)), kk, K1);
+        K2 = bfi(pk_neg_mask(pk_subs(X2, X2k)), kk, K2);
+        Hd = pk_max(Hd, Hdk);
+        X1 = pk_max(X1, X1k);
+        X2 = pk_max(X2, X2k);
     }
     const uint32_t M = pk_subs(pk_adds(Hd, S), pk2(sc.mismatch));
     const uint32_t H0 = bfi(inv, kNeg2, pk_max(M, pk_max(X1, X2)));
@@ -1238,7 +1271,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
             const int4 dA = *reinterpret_cast<const int4 *>(&sh.desc[r & (kDescBatch - 1)][0]);
             const int node = bcast0(dA.x), d1 = bcast0(dA.y), rem = bcast0(dA.z), p0 = bcast0(dA.w);
             const int p1 = bcast0(sh.desc[r & (kDescBatch - 1)][4]);
-            if (d1 & 0x8000) {  // 1-2 predecessors, all in the LDS ring (build_desc)
+            if (d1 & 0xC000) {  // 1-kPreInline predecessors, all in the LDS ring (build_desc)
                 int am0, am1;
                 if (p0 == prv_r) {
                     R.b0 = prv_beg;
@@ -1250,7 +1283,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
                     R.e0 = bcast0(x.y);
                     am0 = bcast0(x.z);
                 }
-                R.two = (d1 >> 16) == 2;
+                R.two = (d1 >> 16) >= 2;
                 if (R.two) {
                     if (p1 == prv_r) {
                         R.b1 = prv_beg;
@@ -1267,15 +1300,24 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
                     R.e1 = R.e0;
                     am1 = am0;
                 }
+                int amL = min(am0, am1), amR = max(am0, am1), narrowk = 0;
+                R.pn3 = (d1 & 0x4000) ? (d1 >> 16) : 0;
+                for (int k = 2; k < R.pn3; ++k) {
+                    const int4 x = sh.rrow[bcast0(sh.desc[r & (kDescBatch - 1)][3 + k]) & (kRowRing - 1)];
+                    const int amk = bcast0(x.z);
+                    amL = min(amL, amk);
+                    amR = max(amR, amk);
+                    narrowk |= kChunk - 1 - (bcast0(x.y) - (bcast0(x.x) & ~1));
+                }
                 const int xr = qlen - rem;
-                R.beg = max(0, min(min(am0, am1) + 1, xr) - w);
-                R.end = min(qlen, max(max(am0, am1) + 1, xr) + w);
+                R.beg = max(0, min(amL + 1, xr) - w);
+                R.end = min(qlen, max(amR + 1, xr) + w);
                 R.cb0 = R.beg & ~1;
                 const int span = R.end - R.cb0 + 1;
                 R.tbw = (span + 3) & ~3;
                 const int pc0 = R.b0 & ~1, pc1 = R.b1 & ~1;
                 // each term is negative exactly when its test fails
-                bad = (kChunk - span) | (kChunk - 1 - (R.e0 - pc0)) | (kChunk - 1 - (R.e1 - pc1)) |
+                bad = (kChunk - span) | (kChunk - 1 - (R.e0 - pc0)) | (kChunk - 1 - (R.e1 - pc1)) | narrowk |
                       (tb_lim - ds.tb_used) | (kp_lim - ds.kp_used) | (sv_lim - ds.sv_used);
                 R.nomask = ((R.beg - 1 - pc0) | (pc0 + kChunk - 1 - R.end) | (R.beg - 1 - pc1) |
                             (pc1 + kChunk - 1 - R.end)) >= 0;
@@ -1299,7 +1341,22 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         } else {
             Slot s = slot_of(sh);
             const PoaKArgs a = args_of(sh);
+#ifdef MANDO_GENPROF
+            const uint64_t g0 = clock64();
+#endif
             const int st = dp_row<SC, true>(a, sc, s, sh, qlen, w, r, lane, ds);
+#ifdef MANDO_GENPROF
+            ds.seg[0] += clock64() - g0;
+            {
+                const int *dl = &sh.desc[r & (kDescBatch - 1)][0];
+                const int pnn = bcast0(dl[1]) >> 16;
+                int md = 0;
+                for (int k = 0; k < min(pnn, kPreInline); ++k) md = max(md, r - bcast0(dl[3 + k]));
+                if (pnn > 2) ds.seg[1] += 1;
+                else if (md < 8) ds.seg[2] += 1;
+                else ds.seg[3] += 1;
+            }
+#endif
             if (st != kStOk) return st;
             const int4 x = sh.rrow[r & (kRowRing - 1)];
             prv_r = r;
@@ -1376,7 +1433,7 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
     }
     cells += ds.cells;
     if (a.prof && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 7] += nfast;
-#ifdef MANDO_STAMPS
+#if defined(MANDO_STAMPS) || defined(MANDO_GENPROF)
     if (a.prof && lane == 0) {
         int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
         for (int k = 0; k < 4; ++k) pf[8 + k] += (int64_t)ds.seg[k];
