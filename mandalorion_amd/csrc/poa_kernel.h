@@ -9,7 +9,8 @@ namespace mando {
 constexpr int kWave = 64;
 constexpr int kCPL = 2;                  // DP cells per lane per chunk
 constexpr int kChunk = kWave * kCPL;     // 128 band columns per chunk
-constexpr int kRing = 4;                 // rows of H/E1/E2 kept in LDS
+constexpr int kRing = 4;                 // rows of H/E1/E2 kept in LDS (32-bit mode)
+constexpr int kRing16 = 8;               // the same in 16-bit mode (same bytes)
 constexpr int kRowRing = 32;             // rows of band info kept in LDS
 constexpr int kPreInline = 5;            // predecessor rows stored inline in a row descriptor
 constexpr int kDescInts = 8;             // ints per row descriptor

@@ -166,7 +166,7 @@ constexpr int kKpWinMax = 2048;       // backtrack: predecessor-byte window (in 
 struct DpLds {
     union {
         int ring[kRing][3][kChunk];      // H, E1out, E2out of the last kRing narrow rows, col & 127
-        short ring16[kRing][3][kChunk];  // the same in 16-bit mode (run_dp<SC, true>)
+        short ring16[kRing16][3][kChunk];  // the same in 16-bit mode (run_dp<SC, true>): twice the rows
     };
 };
 // backtrack phase (the DP state is dead by then); the predecessor-byte window uses the read's
@@ -325,7 +325,7 @@ __device__ __forceinline__ int init_chain(SharedState &sh, const uint8_t *q, int
 // row descriptors + remain (heaviest out-edge path length to the sink), 64-row chunks from the end
 // desc[r] = {node, base | far<<8 | pre_n<<16, remain, pre_row[0..4]}
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane) {
+__device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane, int ring) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
     const int nch = (n + kWave - 1) / kWave;
@@ -358,7 +358,7 @@ __device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane) {
                 }
                 maxd = max(maxd, po - r);
             }
-            far = maxd >= kRing ? 1 : 0;
+            far = maxd >= ring ? 1 : 0;
         }
         const int lo_next = (c + 1) * kWave, lo_next2 = (c + 2) * kWave;
         const int idx_prev = (bh >= lo_next && bh < lo_next2) ? bh - lo_next : lane;
@@ -392,12 +392,12 @@ __device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane) {
             d[0] = v;
             // bit 15: the row's predecessor structure allows the fast row (1-2 predecessors, all
             // within the LDS ring); the band-dependent tests are made per read
-            const int sfast = (pn == 1 || pn == 2) && r - pre[0] < kRing && (pn == 1 || r - pre[1] < kRing);
+            const int sfast = (pn == 1 || pn == 2) && r - pre[0] < ring && (pn == 1 || r - pre[1] < ring);
             // bit 14: 3..kPreInline predecessors, all within the LDS ring (the 16-bit row loop's
             // multi-predecessor fast row)
             bool near = pn >= 3 && pn <= kPreInline;
 #pragma unroll
-            for (int k = 0; k < kPreInline; ++k) near = near && (k >= pn || r - pre[k] < kRing);
+            for (int k = 0; k < kPreInline; ++k) near = near && (k >= pn || r - pre[k] < ring);
             d[1] = vb | (far << 8) | (near ? (1 << 14) : 0) | (sfast << 15) | (pn << 16);
             d[2] = val;
 #pragma unroll
@@ -438,11 +438,15 @@ __device__ __forceinline__ RowRec load_rowrec(const SharedState &sh, const Slot 
 // planes of nchunk*128 ints starting at column cb0; a (rare) predecessor outside the ring is read
 // from those planes.
 __device__ __forceinline__ bool row_narrow(int beg, int end) { return end - (beg & ~1) < kChunk; }
+// rows of H/E1/E2 the LDS ring holds: the 16-bit ring fits twice as many in the same bytes
+template <bool R16>
+__device__ __forceinline__ constexpr int ring_rows() { return R16 ? kRing16 : kRing; }
 __device__ __forceinline__ int row_spill_width(int beg, int end) {
     return ((end - (beg & ~1)) / kChunk + 1) * kChunk;
 }
+template <bool R16>
 __device__ __forceinline__ bool pre_in_ring(int r, int p, const RowRec &pr) {
-    return (r - p < kRing) && row_narrow(pr.beg, pr.end);
+    return (r - p < ring_rows<R16>()) && row_narrow(pr.beg, pr.end);
 }
 
 // predecessor row k of the current row (descriptor `dl` in the LDS batch)
@@ -614,7 +618,8 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
         beg = max(0, min(posL, x) - w);
         end = min(qlen, max(posR, x) + w);
     }
-    const bool pring = (r - pP < kRing) && row_narrow(pB, pE);
+    constexpr int kR = ring_rows<R16>();
+    const bool pring = (r - pP < kR) && row_narrow(pB, pE);
     const bool all_ring = __ballot(lane < pn && !pring) == 0;
     const int cb0 = beg & ~1;
     const int span = end - cb0 + 1;
@@ -664,7 +669,7 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
             if (all_ring && pn == 1) {
                 // the common row: one predecessor, in the ring
                 const int p0 = readlane(pP, 0), b0 = readlane(pB, 0), e0 = readlane(pE, 0);
-                const int pr = p0 % kRing;
+                const int pr = p0 % kR;
                 const int hA = ring_get<R16>(sh, pr, 0, ia), hB = ring_get<R16>(sh, pr, 0, ib);
                 const int2 x1 = ring_get2<R16>(sh, pr, 1, ib);
                 const int2 x2 = ring_get2<R16>(sh, pr, 2, ib);
@@ -683,8 +688,8 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
                     const int pk = readlane(pP, k), bk = readlane(pB, k), ek = readlane(pE, k);
                     int hA, hB;
                     int2 x1, x2;
-                    if (all_ring || (r - pk < kRing && row_narrow(bk, ek))) {
-                        const int pr = pk % kRing;
+                    if (all_ring || (r - pk < kR && row_narrow(bk, ek))) {
+                        const int pr = pk % kR;
                         const int iA = (j0 - 1) & (kChunk - 1), iB = j0 & (kChunk - 1);
                         hA = ring_get<R16>(sh, pr, 0, iA);
                         hB = ring_get<R16>(sh, pr, 0, iB);
@@ -764,7 +769,7 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
         }
         if (va || vbb) *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)tpair;
         if (narrow) {  // out-of-band columns hold -inf (see dp_row_fast)
-            const int ibk = j0 & (kChunk - 1), rr = r % kRing;
+            const int ibk = j0 & (kChunk - 1), rr = r % kR;
             ring_put2<R16>(sh, rr, 0, ibk, Ha, va, Hb, vbb);
             ring_put2<R16>(sh, rr, 1, ibk, E1a, va, E1b, vbb);
             ring_put2<R16>(sh, rr, 2, ibk, E2a, va, E2b, vbb);
@@ -1070,7 +1075,7 @@ typedef __attribute__((address_space(4))) const int cint;
 
 struct Row16 {
     int r, node, vb, pn, beg, end, cb0, tbw;
-    int p0slot, p1slot;        // ring rows of the predecessors (p % kRing)
+    int p0slot, p1slot;        // ring rows of the predecessors (p % kRing16)
     int b0, e0, b1, e1;        // their bands
     int two, far, multi, nomask;  // 0/1 (ints: LLVM keeps uniform bools as 64-bit lane masks)
     int pn3;                      // predecessor count when >= 3 (predecessors 2.. are read in row16_vec)
@@ -1136,7 +1141,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         const int p = bcast0(sh.desc[R.r & (kDescBatch - 1)][3 + k]);
         const int4 x = sh.rrow[p & (kRowRing - 1)];
         const int bk = bcast0(x.x), ek = bcast0(x.y);
-        const uint32_t *wk = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[p & (kRing - 1)][0][0]);
+        const uint32_t *wk = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[p & (kRing16 - 1)][0][0]);
         uint32_t Hdk = __builtin_amdgcn_alignbit(wk[iw], wk[iwp], 16);
         uint32_t X1k = wk[kChunk / 2 + iw], X2k = wk[kChunk + iw];
         const int pck = bk & ~1;
@@ -1185,7 +1190,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         kq[2] = (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u);
     }
     const uint32_t Hs = bfi(inv, kNeg2, H);
-    uint32_t *wr = reinterpret_cast<uint32_t *>(&sh.dp.ring16[R.r & (kRing - 1)][0][0]);
+    uint32_t *wr = reinterpret_cast<uint32_t *>(&sh.dp.ring16[R.r & (kRing16 - 1)][0][0]);
     wr[iw] = Hs;
     wr[kChunk / 2 + iw] = bfi(inv, kNeg2, E1);
     wr[kChunk + iw] = bfi(inv, kNeg2, E2);
@@ -1327,8 +1332,8 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
                 R.pn = d1 >> 16;
                 R.far = (d1 >> 8) & 1;
                 R.multi = R.two;
-                R.p0slot = p0 & (kRing - 1);
-                R.p1slot = (R.two ? p1 : p0) & (kRing - 1);
+                R.p0slot = p0 & (kRing16 - 1);
+                R.p1slot = (R.two ? p1 : p0) & (kRing16 - 1);
             }
         }
         if (bad >= 0) {
@@ -1450,8 +1455,8 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
         const RowRec pr = load_rowrec(sh, s, sr, p);
         if (qlen < pr.beg || qlen > pr.end) continue;
         int hv;
-        if (pre_in_ring(sr, p, pr)) {
-            hv = ring_get<R16>(sh, p % kRing, 0, qlen & (kChunk - 1));
+        if (pre_in_ring<R16>(sr, p, pr)) {
+            hv = ring_get<R16>(sh, p % ring_rows<R16>(), 0, qlen & (kChunk - 1));
         } else {
             hv = s.sv[pr.soff + (qlen - (pr.beg & ~1))];
         }
@@ -2095,21 +2100,25 @@ __global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
                     q = a.seq + o0;
                     prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
                 }
-                uint64_t t0 = prof ? clock64() : 0;
-                build_desc(sh, n, lane);
-                uint64_t t1 = prof ? clock64() : 0;
-                int bi = -1;
                 SC sc;
                 if constexpr (!std::is_same<SC, DefaultScores>::value) {
                     const PoaKArgs aa = args_of(sh);
                     sc = SC{aa.match, aa.mismatch, aa.o1, aa.e1, aa.o2, aa.e2};
                 }
+                uint64_t t0 = prof ? clock64() : 0;
+                const bool try16 = r16_eligible(sc, qlen) && !(args_of(sh).dbg & 1);
+                build_desc(sh, n, lane, try16 ? kRing16 : kRing);
+                uint64_t t1 = prof ? clock64() : 0;
+                int bi = -1;
                 // 16-bit mode when the read's score range allows it; a read that leaves the safe
                 // range is re-aligned in 32-bit mode (the graph is untouched until update_graph)
-                st = (r16_eligible(sc, qlen) && !(args_of(sh).dbg & 1)) ? run_dp<SC, true>(sh, sc, q, qlen, n, lane, cells, bi)
-                                                                        : kStRetry32;
+                st = try16 ? run_dp<SC, true>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
                 if (st == kStRetry32) {
                     if (prof && lane == 0) prof[15] += 1;
+                    if (try16) {  // descriptors of the 32-bit ring (far / fast flags depend on its depth)
+                        wave_sync();
+                        build_desc(sh, n, lane, kRing);
+                    }
                     st = run_dp<SC, false>(sh, sc, q, qlen, n, lane, cells, bi);
                 }
                 uint64_t t2 = prof ? clock64() : 0;

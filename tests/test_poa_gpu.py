@@ -91,3 +91,16 @@ def test_config3_full_size_properties():
     assert ratio.min() > 0.9 and ratio.max() < 1.1
     pick = list(range(0, 2000, 40))
     assert [got[i] for i in pick] == opoa.consensus_batch([groups[i] for i in pick])
+
+
+def test_32bit_rows_everywhere(monkeypatch):
+    """MANDO_POA_DBG=1 forces the 32-bit row loop (4-row LDS ring) for every read: same bytes."""
+    monkeypatch.setenv("MANDO_POA_DBG", "1")
+    _check(poa_cases.noisy_groups(24, (300, 3500), (3, 20), seed=91)[1])
+
+
+def test_dense_branching_graphs():
+    """Very noisy reads: many rows with 3-5+ predecessors and predecessors several rows back
+    (the 16-bit loop's multi-predecessor rows, its 8-row ring and the generic row)."""
+    _, g = synth.read_groups(16, (400, 1500), (20, 40), seed=17, model=dict(sub=0.06, ins=0.05, dele=0.05))
+    _check(g)
