@@ -325,86 +325,141 @@ __device__ __forceinline__ int init_chain(SharedState &sh, const uint8_t *q, int
 // row descriptors + remain (heaviest out-edge path length to the sink), 64-row chunks from the end
 // desc[r] = {node, base | far<<8 | pre_n<<16, remain, pre_row[0..4]}
 // ---------------------------------------------------------------------------------------------
+// Per-row graph facts of one 64-row chunk.  The loads form three dependent levels (order ->
+// node arrays / adjacency rows -> pos), each issued for all edges at once, so a chunk costs three
+// memory round trips; build_desc gathers two chunks before using either.
+struct DescRow {
+    int v, vb, pn, bh, far;
+    int pre[kPreInline];
+};
+constexpr int kOutInline = 4;  // out-edges gathered in the batched levels (more: a serial tail)
+
+__device__ __forceinline__ DescRow desc_gather(const PoaKArgs &a, const Slot &s, int r, bool valid, int ring) {
+    DescRow d;
+    d.v = 0;
+    d.vb = 4;
+    d.pn = 0;
+    d.bh = -1;
+    d.far = 0;
+#pragma unroll
+    for (int k = 0; k < kPreInline; ++k) d.pre[k] = -1;
+    if (!valid) return d;
+    const int v = s.order[r];
+    d.v = v;
+    // level 2: node arrays and the leading adjacency entries (capacity >= 16, so reading past the
+    // list's length stays inside the node's row)
+    const int pn = s.in_n[v], on = s.out_n[v];
+    d.vb = s.base[v];
+    const gint *il = in_list(s, a, v);
+    const gint *ol = out_list(s, a, v);
+    const gint *ow = out_wlist(s, a, v);
+    int iid[kPreInline], oid[kOutInline], owt[kOutInline];
+#pragma unroll
+    for (int k = 0; k < kPreInline; ++k) iid[k] = il[k];
+#pragma unroll
+    for (int k = 0; k < kOutInline; ++k) {
+        oid[k] = ol[k];
+        owt[k] = ow[k];
+    }
+    d.pn = pn;
+    // level 3: topological positions
+#pragma unroll
+    for (int k = 0; k < kPreInline; ++k)
+        if (k < pn) d.pre[k] = s.pos[iid[k]];
+    int opos[kOutInline];
+#pragma unroll
+    for (int k = 0; k < kOutInline; ++k) opos[k] = (k < on) ? s.pos[oid[k]] : 0;
+    int bw = -2147483647 - 1, maxd = 0, bh = -1;
+#pragma unroll
+    for (int k = 0; k < kOutInline; ++k) {
+        if (k < on) {
+            if (owt[k] > bw) {
+                bw = owt[k];
+                bh = opos[k];
+            }
+            maxd = max(maxd, opos[k] - r);
+        }
+    }
+    for (int k = kOutInline; k < on; ++k) {
+        const int po = s.pos[ol[k]];
+        const int wg = ow[k];
+        if (wg > bw) {
+            bw = wg;
+            bh = po;
+        }
+        maxd = max(maxd, po - r);
+    }
+    d.bh = bh;
+    d.far = maxd >= ring ? 1 : 0;
+    return d;
+}
+
+// remain (pointer jumping within the chunk, the chunk above's values via prev_val) and the
+// descriptor store of one chunk
+__device__ __forceinline__ void desc_finish(const Slot &s, const DescRow &d, int c, int n, int lane, int ring,
+                                            int &prev_val) {
+    const int r = c * kWave + lane;
+    const bool valid = r < n;
+    const int bh = d.bh;
+    const int lo_next = (c + 1) * kWave, lo_next2 = (c + 2) * kWave;
+    const int idx_prev = (bh >= lo_next && bh < lo_next2) ? bh - lo_next : lane;
+    const int from_prev = __shfl(prev_val, idx_prev, kWave);
+    int val = 0, ptr = -1;
+    if (valid) {
+        if (d.v == kSink) {
+            val = -1;
+        } else if (bh >= lo_next2) {
+            val = s.remrow[bh] + 1;
+        } else if (bh >= lo_next) {
+            val = from_prev + 1;
+        } else {
+            val = 1;
+            ptr = bh - c * kWave;
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+        const int src = ptr >= 0 ? ptr : lane;
+        const int pv = __shfl(val, src, kWave);
+        const int pp = __shfl(ptr, src, kWave);
+        if (ptr >= 0) {
+            val += pv;
+            ptr = pp;
+        }
+    }
+    if (valid) {
+        const int pn = d.pn;
+        s.remrow[r] = val;
+        gint *dd = s.desc + (int64_t)r * kDescInts;
+        dd[0] = d.v;
+        // bit 15: the row's predecessor structure allows the fast row (1-2 predecessors, all
+        // within the LDS ring); the band-dependent tests are made per read
+        const int sfast = (pn == 1 || pn == 2) && r - d.pre[0] < ring && (pn == 1 || r - d.pre[1] < ring);
+        // bit 14: 3..kPreInline predecessors, all within the LDS ring (the 16-bit row loop's
+        // multi-predecessor fast row)
+        bool near = pn >= 3 && pn <= kPreInline;
+#pragma unroll
+        for (int k = 0; k < kPreInline; ++k) near = near && (k >= pn || r - d.pre[k] < ring);
+        dd[1] = d.vb | (d.far << 8) | (near ? (1 << 14) : 0) | (sfast << 15) | (pn << 16);
+        dd[2] = val;
+#pragma unroll
+        for (int k = 0; k < kPreInline; ++k) dd[3 + k] = d.pre[k];
+    }
+    prev_val = val;
+    wave_sync();
+}
+
 __device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane, int ring) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
     const int nch = (n + kWave - 1) / kWave;
     int prev_val = 0;
-    for (int c = nch - 1; c >= 0; --c) {
-        const int r = c * kWave + lane;
-        const bool valid = r < n;
-        int v = 0, bh = -1, far = 0, pn = 0, vb = 4;
-        int pre[kPreInline];
-#pragma unroll
-        for (int k = 0; k < kPreInline; ++k) pre[k] = -1;
-        if (valid) {
-            v = s.order[r];
-            vb = s.base[v];
-            pn = s.in_n[v];
-            const gint *il = in_list(s, a, v);
-#pragma unroll
-            for (int k = 0; k < kPreInline; ++k)
-                if (k < pn) pre[k] = s.pos[il[k]];
-            const int on = s.out_n[v];
-            const gint *ol = out_list(s, a, v);
-            const gint *ow = out_wlist(s, a, v);
-            int bw = -2147483647 - 1, maxd = 0;
-            for (int k = 0; k < on; ++k) {
-                int po = s.pos[ol[k]];
-                int wg = ow[k];
-                if (wg > bw) {
-                    bw = wg;
-                    bh = po;
-                }
-                maxd = max(maxd, po - r);
-            }
-            far = maxd >= ring ? 1 : 0;
-        }
-        const int lo_next = (c + 1) * kWave, lo_next2 = (c + 2) * kWave;
-        const int idx_prev = (bh >= lo_next && bh < lo_next2) ? bh - lo_next : lane;
-        const int from_prev = __shfl(prev_val, idx_prev, kWave);
-        int val = 0, ptr = -1;
-        if (valid) {
-            if (v == kSink) {
-                val = -1;
-            } else if (bh >= lo_next2) {
-                val = s.remrow[bh] + 1;
-            } else if (bh >= lo_next) {
-                val = from_prev + 1;
-            } else {
-                val = 1;
-                ptr = bh - c * kWave;
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < 6; ++it) {
-            const int src = ptr >= 0 ? ptr : lane;
-            const int pv = __shfl(val, src, kWave);
-            const int pp = __shfl(ptr, src, kWave);
-            if (ptr >= 0) {
-                val += pv;
-                ptr = pp;
-            }
-        }
-        if (valid) {
-            s.remrow[r] = val;
-            gint *d = s.desc + (int64_t)r * kDescInts;
-            d[0] = v;
-            // bit 15: the row's predecessor structure allows the fast row (1-2 predecessors, all
-            // within the LDS ring); the band-dependent tests are made per read
-            const int sfast = (pn == 1 || pn == 2) && r - pre[0] < ring && (pn == 1 || r - pre[1] < ring);
-            // bit 14: 3..kPreInline predecessors, all within the LDS ring (the 16-bit row loop's
-            // multi-predecessor fast row)
-            bool near = pn >= 3 && pn <= kPreInline;
-#pragma unroll
-            for (int k = 0; k < kPreInline; ++k) near = near && (k >= pn || r - pre[k] < ring);
-            d[1] = vb | (far << 8) | (near ? (1 << 14) : 0) | (sfast << 15) | (pn << 16);
-            d[2] = val;
-#pragma unroll
-            for (int k = 0; k < kPreInline; ++k) d[3 + k] = pre[k];
-        }
-        prev_val = val;
-        wave_sync();
+    for (int c = nch - 1; c >= 0; c -= 2) {
+        const int r = c * kWave + lane, r2 = r - kWave;
+        const DescRow d = desc_gather(a, s, r, r < n, ring);
+        const DescRow d2 = desc_gather(a, s, r2, c >= 1, ring);
+        desc_finish(s, d, c, n, lane, ring, prev_val);
+        if (c >= 1) desc_finish(s, d2, c - 1, n, lane, ring, prev_val);
     }
 }
 
