@@ -1314,6 +1314,11 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         const GLB int4 *g = reinterpret_cast<const GLB int4 *>(desc + 4 * lane);
         pf = make_int4(g->x, g->y, g->z, g->w);
     }
+    // the current row's descriptor fields, read from the LDS batch one row ahead (an HBM scalar
+    // load per row would put a full memory latency on every row: build_desc's stores are long out
+    // of L2 by now)
+    int4 nA = make_int4(0, 0, 0, 0);
+    int np1 = 0;
     for (int r = 0; r < n - 1; ++r) {
         if ((r & (kDescBatch - 1)) == 0) {
             if (r + (lane >> 1) < n) *reinterpret_cast<int4 *>(&sh.desc[0][0] + 4 * lane) = pf;
@@ -1322,15 +1327,20 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
                 const GLB int4 *g = reinterpret_cast<const GLB int4 *>(desc + (int64_t)rn * kDescInts + 4 * lane);
                 pf = make_int4(g->x, g->y, g->z, g->w);
             }
+            nA = *reinterpret_cast<const int4 *>(&sh.desc[0][0]);
+            np1 = sh.desc[0][4];
+        }
+        const int4 dA = nA;
+        const int dp1 = np1;
+        if (((r + 1) & (kDescBatch - 1)) != 0) {  // next row's descriptor, in flight during this row
+            nA = *reinterpret_cast<const int4 *>(&sh.desc[(r + 1) & (kDescBatch - 1)][0]);
+            np1 = sh.desc[(r + 1) & (kDescBatch - 1)][4];
         }
         int bad = -1;
         Row16 R;
         if (r > 0) {
-            // this row's descriptor from the LDS batch (an HBM scalar load per row would put a full
-            // memory latency on every row: build_desc's stores are long out of L2 by now)
-            const int4 dA = *reinterpret_cast<const int4 *>(&sh.desc[r & (kDescBatch - 1)][0]);
             const int node = bcast0(dA.x), d1 = bcast0(dA.y), rem = bcast0(dA.z), p0 = bcast0(dA.w);
-            const int p1 = bcast0(sh.desc[r & (kDescBatch - 1)][4]);
+            const int p1 = bcast0(dp1);
             if (d1 & 0xC000) {  // 1-kPreInline predecessors, all in the LDS ring (build_desc)
                 int am0, am1;
                 if (p0 == prv_r) {
