@@ -1317,28 +1317,43 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
     // the current row's descriptor fields, read from the LDS batch one row ahead (an HBM scalar
     // load per row would put a full memory latency on every row: build_desc's stores are long out
     // of L2 by now)
-    int4 nA = make_int4(0, 0, 0, 0);
-    int np1 = 0;
-    for (int r = 0; r < n - 1; ++r) {
-        if ((r & (kDescBatch - 1)) == 0) {
-            if (r + (lane >> 1) < n) *reinterpret_cast<int4 *>(&sh.desc[0][0] + 4 * lane) = pf;
-            const int rn = r + kDescBatch;
+    // Batches of kDescBatch rows; row 0 (the source row) is peeled off the first batch, so the row
+    // loop carries no batch-boundary or first-row tests.
+    for (int b0 = 0, i0 = 1; b0 < n - 1; b0 += kDescBatch, i0 = 0) {
+        if (b0 + (lane >> 1) < n) *reinterpret_cast<int4 *>(&sh.desc[0][0] + 4 * lane) = pf;
+        {
+            const int rn = b0 + kDescBatch;
             if (rn < n && rn + (lane >> 1) < n) {
                 const GLB int4 *g = reinterpret_cast<const GLB int4 *>(desc + (int64_t)rn * kDescInts + 4 * lane);
                 pf = make_int4(g->x, g->y, g->z, g->w);
             }
-            nA = *reinterpret_cast<const int4 *>(&sh.desc[0][0]);
-            np1 = sh.desc[0][4];
         }
+        if (b0 == 0) {
+            Slot s = slot_of(sh);
+            const PoaKArgs a = args_of(sh);
+            const int st = dp_row<SC, true>(a, sc, s, sh, qlen, w, 0, lane, ds);
+            if (st != kStOk) return st;
+            const int4 x = sh.rrow[0];
+            prv_r = 0;
+            prv_beg = bcast0(x.x);
+            prv_end = bcast0(x.y);
+            prv_am = bcast0(x.z);
+        }
+        const int iend = min(kDescBatch, n - 1 - b0);
+        // the current row's descriptor fields, read from the LDS batch one row ahead (an HBM scalar
+        // load per row would put a full memory latency on every row: build_desc's stores are long
+        // out of L2 by now); past the batch end the read is harmless and unused
+        int4 nA = *reinterpret_cast<const int4 *>(&sh.desc[i0][0]);
+        int np1 = sh.desc[i0][4];
+    for (int i = i0; i < iend; ++i) {
+        const int r = b0 + i;
         const int4 dA = nA;
         const int dp1 = np1;
-        if (((r + 1) & (kDescBatch - 1)) != 0) {  // next row's descriptor, in flight during this row
-            nA = *reinterpret_cast<const int4 *>(&sh.desc[(r + 1) & (kDescBatch - 1)][0]);
-            np1 = sh.desc[(r + 1) & (kDescBatch - 1)][4];
-        }
+        nA = *reinterpret_cast<const int4 *>(&sh.desc[(i + 1) & (kDescBatch - 1)][0]);
+        np1 = sh.desc[(i + 1) & (kDescBatch - 1)][4];
         int bad = -1;
         Row16 R;
-        if (r > 0) {
+        {
             const int node = bcast0(dA.x), d1 = bcast0(dA.y), rem = bcast0(dA.z), p0 = bcast0(dA.w);
             const int p1 = bcast0(dp1);
             if (d1 & 0xC000) {  // 1-kPreInline predecessors, all in the LDS ring (build_desc)
@@ -1434,6 +1449,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
             prv_end = bcast0(x.y);
             prv_am = bcast0(x.z);
         }
+    }
     }
     return kStOk;
 }
@@ -2062,7 +2078,7 @@ __device__ __forceinline__ int consensus(SharedState &sh, int n, uint8_t *out, i
 }
 
 template <class SC>
-__global__ __launch_bounds__(kWave) void poa_kernel(PoaKArgs ka) {
+__global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
     __shared__ SharedState sh;
     const int lane = lane_id();
     if (lane == 0) sh.args = ka;
