@@ -1,14 +1,17 @@
+# Round profile on the GPU box: PMC HBM passes (FETCH_SIZE, WRITE_SIZE; separate runs), the default
+# bench line (reads the PMC traffic just measured), and a rocprofv3 kernel-trace summary of the same
+# command.  usage: TAG=r01e bash tools/profile_round.sh   (outputs under gpurun_out/$TAG)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/r01c
+D=gpurun_out/${TAG:-prof}
+mkdir -p $D
 export TMPDIR=/tmp
-timeout -k 10 400 python bench.py --e2e-loci 0 > gpurun_out/r01c/bench.json 2> gpurun_out/r01c/bench.err
-echo "bench rc=$?"
-cat gpurun_out/r01c/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r01c/prof -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --e2e-loci 0 > gpurun_out/r01c/prof.out 2>&1
-echo "prof rc=$?"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r01c/pmcf -o f --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --e2e-loci 0 > gpurun_out/r01c/pmcf.out 2>&1
-echo "pmcf rc=$?"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/r01c/pmcw -o w --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --e2e-loci 0 > gpurun_out/r01c/pmcw.out 2>&1
-echo "pmcw rc=$?"
-find gpurun_out/r01c -name "*.csv" | head -20
+B="python3 bench.py --no-cpu-baseline --e2e-loci 0"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $D/pmcf -o f --output-format csv -- $B --steps 1 --warmup 0 > $D/pmcf.out 2>&1 || { echo "pmcf failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $D/pmcw -o w --output-format csv -- $B --steps 1 --warmup 0 > $D/pmcw.out 2>&1 || { echo "pmcw failed"; exit 1; }
+F=$(find $D/pmcf -name "*counter_collection.csv" | head -1); W=$(find $D/pmcw -name "*counter_collection.csv" | head -1)
+python3 tools/pmc_traffic.py $F $W 20000x50x2700-3300 $D/pmc_latest.json || exit 1
+timeout -k 10 500 python3 bench.py --pmc-json $D/pmc_latest.json > $D/bench.json 2> $D/bench.err || { echo "bench failed"; tail -5 $D/bench.err; exit 1; }
+cat $D/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-format csv -- $B --steps 3 --warmup 1 --pmc-json $D/pmc_latest.json > $D/prof.out 2>&1 || { echo "prof failed"; exit 1; }
+find $D/prof -name "*kernel_stats.csv" | head -1 | xargs head -3
