@@ -79,12 +79,12 @@ struct mando_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_launches = 0;
     bool timed = false;
-    DevBuf ws, counter, prof;
+    DevBuf ws, counter, prof, o_gidx;
     DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
     DevBuf o_hits, o_strand, o_status;
     ~mando_ctx() {
         for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
-                          &cons_len, &cells, &status, &o_hits, &o_strand, &o_status})
+                          &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx})
             b->release();
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -493,6 +493,12 @@ int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_o
                            ctx->stream));
     HIP_TRY(hipMemsetAsync(ctx->o_hits.p, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(n_reads, 1), ctx->stream));
     HIP_TRY(hipMemsetAsync(ctx->counter.p, 0, sizeof(int32_t), ctx->stream));
+    // per-read capacity from the longest read (~2 minimizers per W+1 positions, with margin); groups
+    // that overflow it are re-run at kOrientCap
+    int64_t maxlen = 0;
+    for (int64_t r = 0; r < n_reads; ++r) maxlen = std::max<int64_t>(maxlen, seq_off[r + 1] - seq_off[r]);
+    int cap = 1024;
+    while (cap < mando::kOrientCap && maxlen * 26 / 110 > cap) cap *= 2;
     mando::OrientArgs a;
     a.seq = ctx->seq.as<uint8_t>();
     a.seq_off = ctx->seq_off.as<int64_t>();
@@ -503,15 +509,44 @@ int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_o
     a.max_hits = max_hits;
     a.status = ctx->o_status.as<int32_t>();
     a.counter = ctx->counter.as<int32_t>();
-    const int slots = (int)std::min<int64_t>(n_groups, (int64_t)ctx->n_cu * 2);
+    a.gidx = nullptr;
+    a.cap = cap;
+    std::vector<int32_t> st((size_t)n_groups);
+    std::vector<int32_t> redo;
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-    HIP_TRY(mando::launch_orient(a, slots, ctx->stream));
+    ctx->last_launches = 0;
+    for (;;) {
+        const int64_t ng = a.gidx ? (int64_t)redo.size() : n_groups;
+        a.n_groups = (int32_t)ng;
+        const int slots = (int)std::min<int64_t>(ng, (int64_t)ctx->n_cu * mando::orient_blocks_per_cu(a.cap));
+        HIP_TRY(hipMemsetAsync(ctx->counter.p, 0, sizeof(int32_t), ctx->stream));
+        HIP_TRY(mando::launch_orient(a, slots, ctx->stream));
+        ++ctx->last_launches;
+        HIP_TRY(hipMemcpyAsync(st.data(), ctx->o_status.p, sizeof(int32_t) * (size_t)n_groups, hipMemcpyDeviceToHost,
+                               ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        const std::vector<int32_t> prev = redo;
+        redo.clear();
+        if (a.gidx) {
+            for (int32_t g : prev)
+                if (st[(size_t)g] != 0) redo.push_back(g);
+        } else {
+            for (int64_t g = 0; g < n_groups; ++g)
+                if (st[(size_t)g] != 0) redo.push_back((int32_t)g);
+        }
+        if (redo.empty()) break;
+        if (a.cap >= mando::kOrientCap)
+            return fail(MANDO_E_UNSUPPORTED, "orientation: group " + std::to_string(redo[0]) + " has a read with more than " +
+                                                 std::to_string(mando::kOrientCap) + " minimizers or anchors");
+        // overflowed groups again, at the next capacity (their outputs are rewritten in full)
+        if ((rc = ctx->o_gidx.ensure(sizeof(int32_t) * redo.size())) != MANDO_OK) return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->o_gidx.p, redo.data(), sizeof(int32_t) * redo.size(), hipMemcpyHostToDevice,
+                               ctx->stream));
+        a.gidx = ctx->o_gidx.as<int32_t>();
+        a.cap = std::min(mando::kOrientCap, a.cap * 2);
+    }
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->timed = true;
-    ctx->last_launches = 1;
-    std::vector<int32_t> st((size_t)n_groups);
-    HIP_TRY(hipMemcpyAsync(st.data(), ctx->o_status.p, sizeof(int32_t) * (size_t)n_groups, hipMemcpyDeviceToHost,
-                           ctx->stream));
     if (n_reads > 0) {
         HIP_TRY(hipMemcpyAsync(hit_strands, ctx->o_strand.p, (size_t)n_reads * (size_t)max_hits, hipMemcpyDeviceToHost,
                                ctx->stream));
@@ -519,10 +554,6 @@ int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_o
                                ctx->stream));
     }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    for (int64_t g = 0; g < n_groups; ++g)
-        if (st[(size_t)g] != 0)
-            return fail(MANDO_E_UNSUPPORTED, "orientation: group " + std::to_string(g) + " has a read with more than " +
-                                                 std::to_string(mando::kOrientCap) + " minimizers or anchors");
     return MANDO_OK;
 }
 

@@ -5,7 +5,7 @@
 
 namespace mando {
 
-constexpr int kOrientCap = 2048;  // minimizers per sequence and anchors per read held in LDS
+constexpr int kOrientCap = 2048;  // largest per-read capacity (minimizers / anchors held in LDS)
 
 struct OrientArgs {
     const uint8_t *seq;       // ASCII reads
@@ -15,10 +15,14 @@ struct OrientArgs {
     int8_t *hits;             // n_reads * max_hits
     int32_t *n_hits;          // n_reads
     int32_t max_hits;
-    int32_t *status;          // per group: 0 ok, -1 over kOrientCap
+    int32_t *status;          // per group: 0 ok, -1 over this launch's cap
     int32_t *counter;         // work-queue head (zeroed before launch)
+    const int32_t *gidx;      // optional: the group indices to process (a re-run of overflowed groups)
+    int32_t cap;              // per-read capacity of this launch (power of two, <= kOrientCap)
 };
 
+size_t orient_dyn_bytes(int cap);
+int orient_blocks_per_cu(int cap);
 hipError_t launch_orient(const OrientArgs &a, int n_slots, hipStream_t stream);
 
 }  // namespace mando

@@ -198,15 +198,27 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                                  minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
                                  downstream_buffer=downstream_buffer, junctions=junctions, seed=seed,
                                  threads=threads)
-        return r, time.perf_counter() - tc
+        te = time.perf_counter()
+        timeline.append(("cluster", tc - t0, te - t0))
+        return r, te - tc
 
     from concurrent.futures import ThreadPoolExecutor
 
     stats = {"loci": len(roots), "isoforms": 0, "poa_groups": 0, "records": 0, "poa_reads": 0,
              "t_ingest": t1 - t0, "t_cluster": 0.0, "t_orient": 0.0, "t_poa": 0.0, "chunks": len(spans)}
     payloads = []
-    with ThreadPoolExecutor(max_workers=1) as ex:
+    timeline = []
+    stats["timeline"] = timeline
+    def compact_close(pl, res):
+        # copy this chunk's results out of its locus text, then free the text; runs on its own thread
+        # so the main thread starts the next chunk's GPU work at once
+        out = _compact(pl)
+        res.close()
+        return out
+
+    with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as post:
         fut = ex.submit(run_cluster, *spans[0])
+        pending = []
         for k, (lo, hi) in enumerate(spans):
             res, tcl = fut.result()
             if k + 1 < len(spans):
@@ -218,13 +230,15 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                 raise RuntimeError(f"locus {my_roots[lo + i]}: "
                                    f"{cluster.STATUS.get(int(res.locus_status[i]), res.locus_status[i])} "
                                    "(the reference's locus worker raises here)")
+            tg = time.perf_counter()
             pl = _consensus_chunk(res, mine[lo:hi], orient_fn, consensus_fn, stats)
+            timeline.append(("gpu", tg - t0, time.perf_counter() - t0))
             if len(spans) > 1:
-                pl = _compact(pl)
-                res.close()
+                pending.append(post.submit(compact_close, pl, res))
             else:
                 pl["_res"] = res
-            payloads.append(pl)
+                payloads.append(pl)
+        payloads += [f.result() for f in pending]
     payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
     if world > 1:
         payload = _gather(payload, rank, world)

@@ -63,3 +63,21 @@ def test_orient_gpu_long_reads(gpu_ctx):
     groups, truth = _groups(6, 21, lens=(7000, 9000), depth=(5, 12))
     got = orient.orient_batch(groups)
     assert got == oref.orient_batch(groups) == truth
+
+
+@pytest.mark.gpu
+def test_orient_gpu_capacity_rerun(gpu_ctx):
+    """A 3-copy tandem repeat gives ~3 anchors per query minimizer: over the first launch's per-read
+    capacity (1024 for these lengths), so the host re-runs that group at 2048; the other groups of the
+    batch keep their first-launch results.  Same hit lists as the restatement."""
+    from mandalorion_amd import orient
+    from oracle import orient as oref
+
+    rng = np.random.default_rng(31)
+    unit = "".join(rng.choice(list("ACGT"), 1000))
+    rep = [unit * 3, unit * 3, synth.revcomp(unit * 3), unit[:500] + unit * 2]
+    groups, _ = _groups(20, 33)
+    groups = groups[:10] + [rep] + groups[10:]
+    got = orient.orient_batch(groups)
+    assert got == oref.orient_batch(groups)
+    assert got[10][1] == [1] and got[10][2] == [-1]
