@@ -1565,6 +1565,7 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
 // is read from row i itself, so every step reads only the current row's window entry.
 // ---------------------------------------------------------------------------------------------
 constexpr int kKpNone = -2147483647 - 1;
+constexpr int kSerialPrio = 1;  // wave priority of the non-DP phases (see the read loop)
 
 struct BtWin {
     int lo, hi, glob;  // rows [lo, hi] are in the window; glob: single row read from HBM
@@ -2186,11 +2187,16 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                     const PoaKArgs aa = args_of(sh);
                     sc = SC{aa.match, aa.mismatch, aa.o1, aa.e1, aa.o2, aa.e2};
                 }
+                // The serial, latency-bound phases (descriptors, backtrack, graph update, consensus) issue
+                // ahead of the co-resident waves' DP rows (s_setprio 1; the DP runs at 0): those waves
+                // return to their DP sooner, the SIMD's issue slots stay busy (config-3 kernel -3.5 %).
+                __builtin_amdgcn_s_setprio(kSerialPrio);
                 uint64_t t0 = prof ? clock64() : 0;
                 const bool try16 = r16_eligible(sc, qlen) && !(args_of(sh).dbg & 1);
                 build_desc(sh, n, lane, try16 ? kRing16 : kRing);
                 uint64_t t1 = prof ? clock64() : 0;
                 int bi = -1;
+                __builtin_amdgcn_s_setprio(0);
                 // 16-bit mode when the read's score range allows it; a read that leaves the safe
                 // range is re-aligned in 32-bit mode (the graph is untouched until update_graph)
                 st = try16 ? run_dp<SC, true>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
@@ -2216,6 +2222,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 }
                 wave_sync();
                 uint64_t t3 = prof ? clock64() : 0;
+                __builtin_amdgcn_s_setprio(kSerialPrio);
                 st = backtrack(sh, bi, qlen, n, lane);
                 if (st != kStOk) break;
                 wave_sync();
