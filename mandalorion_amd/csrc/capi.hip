@@ -95,6 +95,12 @@ struct mando_ctx {
 namespace {
 
 constexpr int kMaxWavesPerCu = 16;  // upper bound on resident POA waves per CU
+#ifndef MANDO_WS_SHARE
+#define MANDO_WS_SHARE 0.8
+#endif
+// share of the free HBM the POA workspace may take (one slot per resident wave; deep, long groups
+// need ~100 MB per slot, so the share decides how many waves run)
+constexpr double kWsShare = MANDO_WS_SHARE;
 
 struct GroupStat {
     int64_t nreads = 0, first_len = 0, sum = 0, maxlen = 0;
@@ -158,15 +164,23 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    const size_t budget = std::max<size_t>((size_t)1 << 30, (size_t)(0.5 * (double)free_b) + ctx->ws.bytes);
+    const size_t budget = std::max<size_t>((size_t)1 << 30, (size_t)(kWsShare * (double)free_b) + ctx->ws.bytes);
     // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
     const int per_cu = mando::poa_blocks_per_cu(a, cap);
     int64_t slots = std::min<int64_t>(n_groups, (int64_t)ctx->n_cu * per_cu);
     while (slots > 1 && (size_t)(slots * a.slot_bytes) > budget) slots /= 2;
+    if (getenv("MANDO_PROF"))
+        fprintf(stderr, "[mando prof] slot workspace %.1f MB, %lld slots (free %.1f GB, budget %.1f GB)\n",
+                a.slot_bytes / 1e6, (long long)slots, free_b / 1e9, budget / 1e9);
     if (slots < 1) slots = 1;
     int rc = ctx->ws.ensure((size_t)(slots * a.slot_bytes));
+    while (rc == MANDO_E_NOMEM && slots > 1) {  // memory taken by others since hipMemGetInfo: fewer slots
+        (void)hipGetLastError();                // clear the failed allocation's error state
+        slots /= 2;
+        rc = ctx->ws.ensure((size_t)(slots * a.slot_bytes));
+    }
     if (rc) return rc;
     rc = ctx->counter.ensure(256);
     if (rc) return rc;

@@ -4,7 +4,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["MANDO_PROF"] = "1"
 from mandalorion_amd import synth, poa
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 500
-s, so, go = synth.fast_groups(n, (2700, 3300), (50, 50), seed=1)
+lo, hi, dep = (int(os.environ.get(k, d)) for k, d in (("LEN_LO", 2700), ("LEN_HI", 3300), ("DEPTH", 50)))
+s, so, go = synth.fast_groups(n, (lo, hi), (dep, dep), seed=1)
 groups = synth.unpack_groups(s, so, go)
 t = time.time()
 out, cells = poa.poa_consensus_batch(groups, return_cells=True)
