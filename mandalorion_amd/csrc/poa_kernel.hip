@@ -1063,6 +1063,13 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 __host__ __device__ constexpr uint32_t pk2(int v) { return ((uint32_t)v & 0xffffu) * 0x10001u; }
 constexpr uint32_t kNeg2 = 0x80008000u;  // (-32768, -32768): -inf of the 16-bit mode
+// pk2 of a wave-uniform value, built on the scalar unit (left alone, the compiler splats with a VALU
+// multiply per value)
+__device__ __forceinline__ uint32_t pk2s(int v) {
+    uint32_t r;
+    asm("s_pack_ll_b32_b16 %0, %1, %1" : "=s"(r) : "s"(v));
+    return r;
+}
 __device__ __forceinline__ uint32_t pk_adds(uint32_t a, uint32_t b) {
     return as_u32(__builtin_elementwise_add_sat(as_s16x2(a), as_s16x2(b)));
 }
@@ -1148,8 +1155,8 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     const int j0 = cb0 + 2 * lane;
     const uint32_t J = (uint32_t)j0 * 0x10001u + 0x10000u;         // (j0, j0 + 1)
     const uint32_t LJ = (uint32_t)(2 * lane) * 0x10001u + 0x10000u;  // (j0, j0 + 1) - cb0
-    const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(beg))) |
-                                     as_u32(as_s16x2(pk2(end)) - as_s16x2(J)));
+    const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2s(beg))) |
+                                     as_u32(as_s16x2(pk2s(end)) - as_s16x2(J)));
     const int qbyte = g_qnib[j0 >> 1];
     const uint32_t sel = (uint32_t)(qbyte & 0xf) | (((uint32_t)qbyte & 0xf0u) << 12) | 0x0C000C00u;
     const uint32_t tlo =
@@ -1161,10 +1168,10 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     uint32_t X1 = w0[kChunk / 2 + iw], X2 = w0[kChunk + iw];
     const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0)
     if (!R.nomask) {
-        const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(R.b0))) |
-                                        as_u32(as_s16x2(pk2(R.e0)) - as_s16x2(JD)));
-        const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(R.b0))) |
-                                        as_u32(as_s16x2(pk2(R.e0)) - as_s16x2(J)));
+        const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2s(R.b0))) |
+                                        as_u32(as_s16x2(pk2s(R.e0)) - as_s16x2(JD)));
+        const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2s(R.b0))) |
+                                        as_u32(as_s16x2(pk2s(R.e0)) - as_s16x2(J)));
         Hd = bfi(md, kNeg2, Hd);
         X1 = bfi(me, kNeg2, X1);
         X2 = bfi(me, kNeg2, X2);
@@ -1175,10 +1182,10 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         uint32_t Hd1 = __builtin_amdgcn_alignbit(w1[iw], w1[iwp], 16);
         uint32_t X11 = w1[kChunk / 2 + iw], X21 = w1[kChunk + iw];
         if (!R.nomask) {
-            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(R.b1))) |
-                                            as_u32(as_s16x2(pk2(R.e1)) - as_s16x2(JD)));
-            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(R.b1))) |
-                                            as_u32(as_s16x2(pk2(R.e1)) - as_s16x2(J)));
+            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2s(R.b1))) |
+                                            as_u32(as_s16x2(pk2s(R.e1)) - as_s16x2(JD)));
+            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2s(R.b1))) |
+                                            as_u32(as_s16x2(pk2s(R.e1)) - as_s16x2(J)));
             Hd1 = bfi(md, kNeg2, Hd1);
             X11 = bfi(me, kNeg2, X11);
             X21 = bfi(me, kNeg2, X21);
@@ -1201,10 +1208,10 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         uint32_t X1k = wk[kChunk / 2 + iw], X2k = wk[kChunk + iw];
         const int pck = bk & ~1;
         if (((beg - 1 - pck) | (pck + kChunk - 1 - end)) < 0) {
-            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2(bk))) |
-                                            as_u32(as_s16x2(pk2(ek)) - as_s16x2(JD)));
-            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2(bk))) |
-                                            as_u32(as_s16x2(pk2(ek)) - as_s16x2(J)));
+            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2s(bk))) |
+                                            as_u32(as_s16x2(pk2s(ek)) - as_s16x2(JD)));
+            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2s(bk))) |
+                                            as_u32(as_s16x2(pk2s(ek)) - as_s16x2(J)));
             Hdk = bfi(md, kNeg2, Hdk);
             X1k = bfi(me, kNeg2, X1k);
             X2k = bfi(me, kNeg2, X2k);
