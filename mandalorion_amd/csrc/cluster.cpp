@@ -42,6 +42,8 @@
 #include <unordered_set>
 #include <vector>
 
+#include <emmintrin.h>
+
 #include "../../include/mando.h"
 #include "mt19937.h"
 #include "revcomp.h"
@@ -206,19 +208,40 @@ struct OpTable {
 const OpTable kOps;
 inline bool is_op(char c) { return kOps.t[(unsigned char)c]; }
 
+// first cs operator at or after i ('=' runs carry the read bases, so the scan is 16 bytes a step)
+inline size_t next_op(string_view cs, size_t i) {
+    const char *p = cs.data();
+    const size_t n = cs.size();
+    const __m128i c0 = _mm_set1_epi8('='), c1 = _mm_set1_epi8('+'), c2 = _mm_set1_epi8('-'),
+                  c3 = _mm_set1_epi8('*'), c4 = _mm_set1_epi8('~'), c5 = _mm_set1_epi8('\\');
+    for (; i + 16 <= n; i += 16) {
+        const __m128i v = _mm_loadu_si128((const __m128i *)(p + i));
+        const __m128i m = _mm_or_si128(
+            _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, c0), _mm_cmpeq_epi8(v, c1)),
+                         _mm_or_si128(_mm_cmpeq_epi8(v, c2), _mm_cmpeq_epi8(v, c3))),
+            _mm_or_si128(_mm_cmpeq_epi8(v, c4), _mm_cmpeq_epi8(v, c5)));
+        const int bits = _mm_movemask_epi8(m);
+        if (bits) return i + (size_t)__builtin_ctz((unsigned)bits);
+    }
+    while (i < n && !is_op(p[i])) ++i;
+    return i;
+}
+
 void build_cs(string_view cs, int64_t begin, CsIndex &ix) {
     ix.runs.clear();
     ix.adv.clear();
     ix.adv_first.clear();
+    ix.runs.reserve(cs.size() / 8 + 8);
+    ix.adv.reserve(cs.size() / 8 + 8);
+    ix.adv_first.reserve(cs.size() / 8 + 8);
     int64_t g = begin;
     int32_t rec = 0;
     size_t i = 0;
     // re.split keeps text before the first operator as element 0, which the zip drops
-    while (i < cs.size() && !is_op(cs[i])) ++i;
+    i = next_op(cs, i);
     while (i < cs.size()) {
         const char op = cs[i++];
-        size_t j = i;
-        while (j < cs.size() && !is_op(cs[j])) ++j;
+        const size_t j = next_op(cs, i);
         const string_view e = cs.substr(i, j - i);
         i = j;
         CsRun r{rec, 0, g, 0, op, {0, 0, 0, 0}};
@@ -491,11 +514,11 @@ class LocusRunner {
     int64_t bin_lo = INT64_MAX, bin_hi = INT64_MIN, nbins = 0;
     int64_t span_lo = 0, span_hi = -1;  // genome span of the locus' records  // rounded positions (multiples of 10)
     vector<int32_t> hcov;     // histo_cov, dense over [bin_lo, bin_hi] step 10
-    vector<int32_t> ccount;   // scratch: coverage counts of the winning bin's reads
     OrderedMap<vector<HistEntry>> hist_l, hist_r;
     vector<vector<int64_t>> cov_sets;                    // per record (rounded, unique, sorted)
     std::unordered_map<string_view, int32_t> cs_dict;     // name -> last record
     vector<CsIndex> cs_ix;
+    vector<int32_t> cs_of;  // record -> cs_dict[name] once the dict is complete (-1: other chrom)
     // spliceDict
     std::unordered_map<int64_t, int32_t> splice;
     vector<string> labels;
@@ -558,11 +581,13 @@ class LocusRunner {
             for (int64_t b : low) hist_l.at(b).push_back({(int32_t)r});
             for (int64_t b : up) hist_r.at(b).push_back({(int32_t)r});
         }
+        cs_of.assign(n, -1);
+        for (size_t r = 0; r < n; ++r)
+            if (recs[r].chrom == string_view(in.chrom)) cs_of[r] = cs_dict.at(recs[r].name);
         // dense per-locus coverage histogram over 10-nt bins (histo_cov)
         if (bin_lo <= bin_hi) {
             nbins = (bin_hi - bin_lo) / 10 + 1;
             hcov.assign((size_t)nbins, 0);
-            ccount.assign((size_t)nbins, 0);
             for (size_t r = 0; r < n; ++r)
                 for (int64_t b : cov_sets[r]) hcov[(size_t)((b - bin_lo) / 10)] += 1;
         }
@@ -605,8 +630,7 @@ class LocusRunner {
         int64_t lc[6] = {0}, rc[6] = {0};
         CsResult res;
         for (int64_t t : pick) {
-            const string_view nm = recs[(size_t)names[(size_t)t]].name;
-            const int32_t ri = cs_dict.at(nm);
+            const int32_t ri = cs_of[(size_t)names[(size_t)t]];
             CsIndex &ix = cs_ix[(size_t)ri];
             if (!ix.built) build_cs(recs[(size_t)ri].cs, recs[(size_t)ri].tstart, ix);
             cs_around(ix, left, right, res);
@@ -629,6 +653,78 @@ class LocusRunner {
         return la > 0.85 && ra > 0.85;
     }
 
+    // determine_cov (SDC:200-224): over the winners' coverage bins (a multiset: a read listed twice
+    // counts twice), the first 4 bins with count > 1 strictly beyond the centre (downward for the
+    // left side); max of histo_cov over them.  The winners' sorted coverage sets are merged from the
+    // centre outwards, so a candidate touches only the bins up to the fourth hit instead of
+    // scattering every winner's ~300 bins.
+    int64_t determine_cov(const vector<int32_t> &names, int64_t center, bool reverse) {
+        using Ent = std::pair<int64_t, int32_t>;  // (bin position, cursor)
+        int64_t kstart;
+        if (reverse) {
+            const int64_t k = center - 1 - bin_lo;
+            kstart = k < 0 ? -1 : std::min<int64_t>(k / 10, nbins - 1);
+            if (kstart < 0) return 0;
+        } else {
+            const int64_t k = center + 1 - bin_lo;
+            kstart = k <= 0 ? 0 : (k + 9) / 10;
+            if (kstart >= nbins) return 0;
+        }
+        const int64_t bound = bin_lo + 10 * kstart;
+        merge_pos.assign(names.size(), 0);
+        merge_heap.clear();
+        for (size_t c = 0; c < names.size(); ++c) {
+            const vector<int64_t> &cs = cov_sets[(size_t)names[c]];
+            if (reverse) {
+                const size_t i = (size_t)(std::upper_bound(cs.begin(), cs.end(), bound) - cs.begin());
+                if (i == 0) continue;
+                merge_pos[c] = i - 1;
+                merge_heap.push_back({cs[i - 1], (int32_t)c});
+            } else {
+                const size_t i = (size_t)(std::lower_bound(cs.begin(), cs.end(), bound) - cs.begin());
+                if (i == cs.size()) continue;
+                merge_pos[c] = i;
+                merge_heap.push_back({-cs[i], (int32_t)c});  // max-heap on -position: smallest first
+            }
+        }
+        auto cmp = [](const Ent &a, const Ent &b) { return a.first < b.first; };
+        std::make_heap(merge_heap.begin(), merge_heap.end(), cmp);
+        int64_t cov = 0;
+        int counter = 0;
+        while (!merge_heap.empty() && counter < 4) {
+            const int64_t top = merge_heap.front().first;
+            int64_t count = 0;
+            while (!merge_heap.empty() && merge_heap.front().first == top) {
+                std::pop_heap(merge_heap.begin(), merge_heap.end(), cmp);
+                const int32_t c = merge_heap.back().second;
+                merge_heap.pop_back();
+                ++count;
+                const vector<int64_t> &cs = cov_sets[(size_t)names[(size_t)c]];
+                size_t &i = merge_pos[(size_t)c];
+                if (reverse) {
+                    if (i > 0) {
+                        --i;
+                        merge_heap.push_back({cs[i], c});
+                        std::push_heap(merge_heap.begin(), merge_heap.end(), cmp);
+                    }
+                } else if (++i < cs.size()) {
+                    merge_heap.push_back({-cs[i], c});
+                    std::push_heap(merge_heap.begin(), merge_heap.end(), cmp);
+                }
+            }
+            if (count > 1) {
+                ++counter;
+                const int64_t pos = reverse ? top : -top;
+                cov = std::max<int64_t>(cov, hcov[(size_t)((pos - bin_lo) / 10)]);
+            }
+        }
+        return cov;
+    }
+    vector<size_t> merge_pos;
+    vector<std::pair<int64_t, int32_t>> merge_heap;
+    vector<int64_t> win_cnt, win_p, win_m;  // find_peaks: per-position counts over entry +- 2w
+    vector<uint8_t> win_flag;               // bit 0: called area, bit 1: record with a bad strand
+
     void find_peaks(OrderedMap<vector<HistEntry>> &dd, bool reverse, char side,
                     PosSet &areas, vector<Peak> &tw) {
         vector<int64_t> dist{0};
@@ -645,31 +741,44 @@ class LocusRunner {
             const int64_t entry = dd.keys[ci];
             if (areas.has(entry)) continue;
             // scan_for_best_bin: the winning shift by read count (strict >, first wins); the
-            // coverage counts are only needed for the winner
+            // coverage counts are only needed for the winner.  Every window entry+x+y lies in
+            // entry +- 2w, so the per-position read counts and called flags are gathered once and
+            // the 2w+1 windows summed from them (a record with a strand other than +/- raises the
+            // KeyError as soon as an uncalled window covers it, as the per-read loop did).
+            const int64_t w = P.w, span = 4 * w + 1;
+            win_cnt.assign((size_t)span, 0);
+            win_p.assign((size_t)span, 0);
+            win_m.assign((size_t)span, 0);
+            win_flag.assign((size_t)span, 0);
+            for (int64_t d = 0; d < span; ++d) {
+                const int64_t pos = entry - 2 * w + d;
+                if (areas.has(pos)) win_flag[(size_t)d] |= 1;
+                const vector<HistEntry> *lst = dd.find(pos);
+                if (!lst) continue;
+                win_cnt[(size_t)d] = (int64_t)lst->size();
+                for (const HistEntry &h : *lst) {
+                    const string_view dn = recs[(size_t)h.rec].dirn;
+                    if (dn == "+")
+                        win_p[(size_t)d] += 1;
+                    else if (dn == "-")
+                        win_m[(size_t)d] += 1;
+                    else
+                        win_flag[(size_t)d] |= 2;
+                }
+            }
             int64_t best = 0, center = 0, bx = 0;
             int64_t bdir_p = 0, bdir_m = 0;
             for (int64_t x : dist) {
-                bool called = false;
-                for (int64_t y : dist)
-                    if (areas.has(entry + x + y)) {
-                        called = true;
-                        break;
-                    }
-                if (called) continue;
+                const size_t d0 = (size_t)(x + w);  // index of entry+x-w
+                uint8_t fl = 0;
+                for (size_t d = d0; d < d0 + (size_t)(2 * w + 1); ++d) fl |= win_flag[d];
+                if (fl & 1) continue;
+                if (fl & 2) throw LocusError{kLocusKeyError};
                 int64_t cnt = 0, dp = 0, dm = 0;
-                for (int64_t y : dist) {
-                    const vector<HistEntry> *lst = dd.find(entry + x + y);
-                    if (!lst) continue;
-                    for (const HistEntry &h : *lst) {
-                        cnt += 1;
-                        const string_view d = recs[(size_t)h.rec].dirn;
-                        if (d == "+")
-                            dp += 1;
-                        else if (d == "-")
-                            dm += 1;
-                        else
-                            throw LocusError{kLocusKeyError};
-                    }
+                for (size_t d = d0; d < d0 + (size_t)(2 * w + 1); ++d) {
+                    cnt += win_cnt[d];
+                    dp += win_p[d];
+                    dm += win_m[d];
                 }
                 if (cnt > best) {
                     best = cnt;
@@ -685,33 +794,9 @@ class LocusRunner {
                 for (int64_t y : dist) {
                     const vector<HistEntry> *lst = dd.find(entry + bx + y);
                     if (!lst) continue;
-                    for (const HistEntry &h : *lst) {
-                        best_names.push_back(h.rec);
-                        for (int64_t cp : cov_sets[(size_t)h.rec]) ccount[(size_t)((cp - bin_lo) / 10)] += 1;
-                    }
+                    for (const HistEntry &h : *lst) best_names.push_back(h.rec);
                 }
-                // determine_cov: the first 4 bins with count > 1 strictly beyond the centre (downward
-                // for the left side), max of their histo_cov
-                int counter = 0;
-                if (reverse) {
-                    int64_t k = center - 1 - bin_lo;
-                    k = k < 0 ? -1 : std::min<int64_t>(k / 10, nbins - 1);
-                    for (; k >= 0 && counter < 4; --k)
-                        if (ccount[(size_t)k] > 1) {
-                            ++counter;
-                            cov = std::max<int64_t>(cov, hcov[(size_t)k]);
-                        }
-                } else {
-                    int64_t k = center + 1 - bin_lo;
-                    k = k <= 0 ? 0 : (k + 9) / 10;
-                    for (; k < nbins && counter < 4; ++k)
-                        if (ccount[(size_t)k] > 1) {
-                            ++counter;
-                            cov = std::max<int64_t>(cov, hcov[(size_t)k]);
-                        }
-                }
-                for (int32_t rr : best_names)
-                    for (int64_t cp : cov_sets[(size_t)rr]) ccount[(size_t)((cp - bin_lo) / 10)] = 0;
+                cov = determine_cov(best_names, center, reverse);
             }
             if (cov <= 0) continue;
             const double prop = py_round3((double)best / (double)cov);

@@ -271,12 +271,15 @@ def _consensus_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], orient
     t2 = time.perf_counter()
     # orientation: every subsampled read against its isoform's first subsampled read
     o_seqs, o_off = _lib.pack_segments([res.text], res.seq_off[res.sub], res.seq_len[res.sub])
+    t2b = time.perf_counter()
     hits, n_hits = orient_fn(o_seqs, o_off, res.sub_off)
     t3 = time.perf_counter()
     asm = Assembly(res, hits, n_hits)
     p_seqs, p_off, p_grp = asm.poa_input()
+    t3b = time.perf_counter()
     cons, cons_off = consensus_fn(p_seqs, p_off, p_grp, asm.seeding)
     t4 = time.perf_counter()
+    stats["t_pack"] = stats.get("t_pack", 0.0) + (t2b - t2) + (t3b - t3)
     # consensus of every isoform as a byte segment: POA output, else (<=2 sequences, or an empty POA
     # result) the first emission, re-bound (SDC:911-926)
     n_iso = res.n_isoforms

@@ -88,7 +88,7 @@ def poa_consensus_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndar
     grp_off = np.ascontiguousarray(grp_off, dtype=np.int64)
     seed_arr = None if seeding is None else np.ascontiguousarray(np.asarray(seeding, dtype=np.uint8))
     cap = int(seq_off[-1] - seq_off[0]) * 2 + 1024
-    cons = np.zeros(cap, dtype=np.uint8)
+    cons = np.empty(cap, dtype=np.uint8)   # written up to cons_off[-1]; untouched pages stay unmapped
     cons_off = np.zeros(n + 1, dtype=np.int64)
     if n > 0:
         _lib.check(ctx.lib.mando_poa_batch(ctx.handle, _lib.ctypes.byref(p), _lib.ptr(seqs), _lib.ptr(seq_off),
