@@ -72,7 +72,6 @@ class ClusterResult:
         self.peak_type = bytes(_arr(v.peak_type, npk, np.uint8)).decode() if npk else ""
         self.peak_side = bytes(_arr(v.peak_side, npk, np.uint8)).decode() if npk else ""
         self.peak_prop = _arr(v.peak_prop, npk, np.float64)
-        self._raw = self.text.tobytes() if v.text_len else b""
 
     def close(self):
         if self._h is not None:
@@ -92,11 +91,11 @@ class ClusterResult:
 
     def name(self, r: int) -> str:
         a = int(self.name_off[r])
-        return self._raw[a:a + int(self.name_len[r])].decode()
+        return bytes(self.text[a:a + int(self.name_len[r])]).decode()
 
     def seq(self, r: int) -> str:
         a = int(self.seq_off[r])
-        return self._raw[a:a + int(self.seq_len[r])].decode()
+        return bytes(self.text[a:a + int(self.seq_len[r])]).decode()
 
     def members(self, i: int) -> np.ndarray:
         return self.mem[self.mem_off[i]:self.mem_off[i + 1]]

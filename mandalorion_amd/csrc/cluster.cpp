@@ -1064,7 +1064,8 @@ void parse_locus(string_view text, int64_t base, vector<Record> &recs) {
 }  // namespace
 
 struct mando_cluster_result {
-    string text;
+    std::unique_ptr<char[]> text;  // all locus files; left uninitialised, the parallel reads fault it in
+    size_t text_len = 0;
     vector<int64_t> name_off, seq_off, rec_locus;
     vector<int32_t> name_len, seq_len;
     vector<int64_t> iso_locus, mem_off, mem, sub_off, sub;
@@ -1130,7 +1131,8 @@ int mando_cluster_loci(const mando_cluster_params *prm, const char *const *psl_p
         fclose(fh);
     }
     for (int64_t i = 0; i < n_loci; ++i) foff[(size_t)i + 1] = foff[(size_t)i] + std::max<int64_t>(0, fsize[(size_t)i]);
-    res->text.resize((size_t)foff[(size_t)n_loci]);
+    res->text_len = (size_t)foff[(size_t)n_loci];
+    res->text.reset(new char[std::max<size_t>(res->text_len, 1)]);
     int nth = prm->threads > 0 ? prm->threads : (int)std::max(1u, std::thread::hardware_concurrency());
     nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n_loci));
     vector<LocusIn> ins((size_t)n_loci);
@@ -1149,7 +1151,7 @@ int mando_cluster_loci(const mando_cluster_params *prm, const char *const *psl_p
             LocusOut &lo = outs[(size_t)i];
             try {
                 if (fsize[(size_t)i] < 0) throw LocusError{kLocusIO};
-                char *dst = &res->text[(size_t)foff[(size_t)i]];
+                char *dst = res->text.get() + foff[(size_t)i];
                 FILE *fh = fopen(psl_paths[i], "rb");
                 if (!fh) throw LocusError{kLocusIO};
                 const size_t got = fread(dst, 1, (size_t)fsize[(size_t)i], fh);
@@ -1190,7 +1192,7 @@ int mando_cluster_loci(const mando_cluster_params *prm, const char *const *psl_p
         fprintf(stderr, "\n");
     }
     // flatten
-    const char *base = res->text.data();
+    const char *base = res->text.get();
     vector<int64_t> rec_base((size_t)n_loci + 1, 0);
     for (int64_t i = 0; i < n_loci; ++i) rec_base[(size_t)i + 1] = rec_base[(size_t)i] + (int64_t)recs[(size_t)i].size();
     const int64_t nr = rec_base[(size_t)n_loci];
@@ -1239,8 +1241,8 @@ int mando_cluster_view_get(const mando_cluster_result *r, mando_cluster_view *v)
     if (!r || !v) return MANDO_E_ARG;
     v->n_loci = (int64_t)r->locus_status.size();
     v->locus_status = r->locus_status.data();
-    v->text = r->text.data();
-    v->text_len = (int64_t)r->text.size();
+    v->text = r->text.get();
+    v->text_len = (int64_t)r->text_len;
     v->n_records = (int64_t)r->name_off.size();
     v->name_off = r->name_off.data();
     v->name_len = r->name_len.data();
