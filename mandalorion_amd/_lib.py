@@ -277,12 +277,15 @@ class Context:
         return bad.value
 
 
-_ctx_cache: dict[int, Context] = {}
+_ctx_cache: dict[tuple[int, int], Context] = {}
 
 
-def context(device: int = 0) -> Context:
-    c = _ctx_cache.get(device)
+def context(device: int = 0, slot: int = 0) -> Context:
+    """Per-(device, slot) context: each slot owns a HIP stream and its device buffers, so two host threads
+    can drive the same GPU at once (the D pipeline orients chunk k+1 on slot 1 while chunk k's POA runs
+    on slot 0)."""
+    c = _ctx_cache.get((device, slot))
     if c is None or c.handle is None:
         c = Context(device)
-        _ctx_cache[device] = c
+        _ctx_cache[(device, slot)] = c
     return c

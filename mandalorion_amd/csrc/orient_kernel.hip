@@ -31,9 +31,19 @@ constexpr int TILE = 256;
 constexpr int MAXCH = 64;
 constexpr uint64_t INF = ~0ull;
 
+// bases one tile's k-mers touch (k-mer starts h0 .. h0 + TILE + 2W - 2), staged once per tile as
+// 2-bit codes, 16 per word with the first base in the top bits, plus a 1-bit-per-base mask of
+// non-ACGT bases (and of positions outside the read)
+constexpr int TB = TILE + 2 * W - 1 + K - 1;
+constexpr int NPK = ((TB + 15) / 16 + 1 + 3) / 4 * 4;  // + the second word of the last window; x4 lanes
+constexpr int NNM = NPK / 4 + 1;                       // 64-bit words; +1 read (masked) past the end
+static_assert(NPK * 16 >= TB + 16 && (NPK * 16) % 64 == 0, "tile staging size");
+
 // fixed-size part (static LDS); the cap-sized arrays live in dynamic LDS (see OrientDyn)
 struct OrientLds {
     int cap;
+    uint32_t pk[NPK];           // staged 2-bit codes
+    uint64_t nm[NNM];           // staged non-ACGT mask
     uint64_t hb[TILE + 2 * W];  // (hash << 1 | z) of the tile's k-mers, INF when invalid
     uint64_t mb[TILE + W];      // window minima (hash only)
     int32_t ch_score[MAXCH], ch_rev[MAXCH], ch_qs[MAXCH], ch_qe[MAXCH];
@@ -132,22 +142,65 @@ __device__ int minimizers(OrientLds &sh, const uint8_t *s, int64_t L, uint64_t *
     const int64_t nw = np <= W ? 1 : np - W + 1;
     const int ww = np <= W ? (int)np : W;
     int n = 0;
+    const uint32_t mask30 = (1u << (2 * K)) - 1;
     for (int64_t t0 = 0; t0 < np; t0 += TILE) {
         const int64_t h0 = t0 - (W - 1);  // position of hb[0] and of window mb[0]
+        // stage the tile's bases: one coalesced byte load per base, 16 codes OR-reduced per word
+        for (int e0 = 0; e0 < NPK * 16; e0 += 64) {
+            const int e = e0 + lane;
+            const int64_t p = h0 + e;
+            const int c = (p >= 0 && p < L) ? enc(s[p]) : 4;
+            uint32_t v = c > 3 ? 0u : (uint32_t)c << (2 * (15 - (lane & 15)));
+            v |= (uint32_t)__shfl_xor((int)v, 1, 64);
+            v |= (uint32_t)__shfl_xor((int)v, 2, 64);
+            v |= (uint32_t)__shfl_xor((int)v, 4, 64);
+            v |= (uint32_t)__shfl_xor((int)v, 8, 64);
+            const unsigned long long bad = __ballot(c > 3);
+            if ((lane & 15) == 0) sh.pk[e >> 4] = v;
+            if (lane == 0) sh.nm[e0 >> 6] = bad;
+        }
+        if (lane == 0) sh.nm[NNM - 1] = ~0ull;
+        wsync();
+        // (hash << 1 | z) of each k-mer: a 30-bit window of two staged words; the reverse complement
+        // by complementing and reversing the 2-bit groups
         for (int e = lane; e < TILE + 2 * W - 1; e += 64) {
             const int64_t p = h0 + e;
-            sh.hb[e] = (p >= 0 && p < np) ? kmer_hz(s, p) : INF;
+            uint64_t hz = INF;
+            if (p >= 0 && p < np) {
+                uint64_t m = sh.nm[e >> 6] >> (e & 63);
+                if ((e & 63) > 64 - K) m |= sh.nm[(e >> 6) + 1] << (64 - (e & 63));
+                if (!(m & ((1ull << K) - 1))) {
+                    const int q = e >> 4, o = e & 15;
+                    const uint64_t w = ((uint64_t)sh.pk[q] << 32) | sh.pk[q + 1];
+                    const uint32_t f = (uint32_t)(w >> (2 * (32 - o - K))) & mask30;
+                    const uint32_t x = __builtin_bitreverse32(f ^ mask30) >> (32 - 2 * K);
+                    const uint32_t r = ((x >> 1) & 0x15555555u) | ((x & 0x15555555u) << 1);
+                    if (f != r)
+                        hz = (hash64(f < r ? f : r, (1ull << (2 * K)) - 1) << 1) | (f < r ? 0 : 1);
+                }
+            }
+            sh.hb[e] = hz;
         }
         wsync();
         for (int e = lane; e < TILE + W - 1; e += 64) {
             const int64_t w0 = h0 + e;
             uint64_t m = INF;
-            if (w0 >= 0 && w0 < nw)
-                for (int t = 0; t < ww; ++t) {
-                    const uint64_t v = sh.hb[e + t];
-                    const uint64_t hv = v == INF ? INF : v >> 1;
-                    m = hv < m ? hv : m;
+            if (w0 >= 0 && w0 < nw) {
+                if (ww == W) {
+#pragma unroll
+                    for (int t = 0; t < W; ++t) {
+                        const uint64_t v = sh.hb[e + t];
+                        const uint64_t hv = v == INF ? INF : v >> 1;
+                        m = hv < m ? hv : m;
+                    }
+                } else {
+                    for (int t = 0; t < ww; ++t) {
+                        const uint64_t v = sh.hb[e + t];
+                        const uint64_t hv = v == INF ? INF : v >> 1;
+                        m = hv < m ? hv : m;
+                    }
                 }
+            }
             sh.mb[e] = m;
         }
         wsync();
@@ -260,8 +313,10 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
     // strand, f) lives in registers and slides one lane per anchor (DPP wave_shl); the best
     // predecessor is one DPP max-reduction.  Only lane 0 stores f / p (for the chain walk below).
     int wx = 0, wy = 0, wr = -1, wf = 0;  // wr = -1: empty slot (j < 0)
+    uint64_t an_next = na > 0 ? o_an(sh)[0] : 0;  // one anchor ahead: the LDS read leaves the DP chain
     for (int i = 0; i < na; ++i) {
-        const uint64_t ai = o_an(sh)[i];
+        const uint64_t ai = an_next;
+        if (i + 1 < na) an_next = o_an(sh)[i + 1];
         const int ri = (int)(ai >> 62);
         const int xi = (int)((ai >> 31) & 0x7fffffff), yi = (int)(ai & 0x7fffffff);
         const int dr = xi - wx, dq = yi - wy;

@@ -41,7 +41,7 @@ def gpu_orient(seqs, seq_off, grp_off, device: int = 0, max_hits: int = 4):
     """Per read: the strands (+1/-1) of its primary hits against its group's first read (HIP)."""
     from . import orient
 
-    return orient.orient_packed(seqs, seq_off, grp_off, device=device, max_hits=max_hits)
+    return orient.orient_packed(seqs, seq_off, grp_off, device=device, max_hits=max_hits, slot=1)
 
 
 def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0):
@@ -192,6 +192,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     spans = [(cuts[k], cuts[k + 1]) for k in range(len(cuts) - 1) if cuts[k + 1] > cuts[k]] or [(0, 0)]
 
     def run_cluster(lo, hi):
+        # clustering (host C++ threads, GIL released), then the orientation input: the subsampled reads
         tc = time.perf_counter()
         r = cluster.cluster_loci([os.path.join(out_tmp, x + ".psl") for x in my_roots[lo:hi]], chroms[lo:hi],
                                  ann=ann[lo:hi], cutoff=cutoff, splice_site_width=splice_site_width,
@@ -200,44 +201,79 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                                  threads=threads)
         te = time.perf_counter()
         timeline.append(("cluster", tc - t0, te - t0))
-        return r, te - tc
+        bad = np.nonzero(r.locus_status != 0)[0]
+        if len(bad):
+            i = int(bad[0])
+            code = int(r.locus_status[i])
+            r.close()
+            raise RuntimeError(f"locus {my_roots[lo + i]}: {cluster.STATUS.get(code, code)} "
+                               "(the reference's locus worker raises here)")
+        o_in = _lib.pack_segments([r.text], r.seq_off[r.sub], r.seq_len[r.sub])
+        return r, te - tc, o_in, time.perf_counter() - te
 
     from concurrent.futures import ThreadPoolExecutor
 
     stats = {"loci": len(roots), "isoforms": 0, "poa_groups": 0, "records": 0, "poa_reads": 0,
-             "t_ingest": t1 - t0, "t_cluster": 0.0, "t_orient": 0.0, "t_poa": 0.0, "chunks": len(spans)}
+             "t_ingest": t1 - t0, "t_cluster": 0.0, "t_pack": 0.0, "t_orient": 0.0, "t_assemble": 0.0,
+             "t_poa": 0.0, "chunks": len(spans)}
     payloads = []
     timeline = []
     stats["timeline"] = timeline
+
     def compact_close(pl, res):
-        # copy this chunk's results out of its locus text, then free the text; runs on its own thread
-        # so the main thread starts the next chunk's GPU work at once
+        # copy this chunk's results out of its locus text, then free the text
         out = _compact(pl)
         res.close()
         return out
 
-    with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as post:
+    def assemble(res, hits, n_hits):
+        ta = time.perf_counter()
+        asm = Assembly(res, hits, n_hits)
+        prep = (asm,) + tuple(asm.poa_input())
+        stats["t_assemble"] += time.perf_counter() - ta
+        return prep
+
+    # The main thread issues the GPU work in the order orientation(k+1), POA(k): chunk k+1's emission
+    # assembly (host) then overlaps chunk k's POA kernel, and no kernel waits behind the persistent POA
+    # grid.  Clustering + packing of chunk k+2 runs on its own thread meanwhile; compaction of finished
+    # chunks on another.
+    with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
+            ThreadPoolExecutor(max_workers=1) as post:
+        def orient(c):
+            res, tcl, (o_seqs, o_off), tpk = c
+            stats["t_cluster"] += tcl
+            stats["t_pack"] += tpk
+            tg = time.perf_counter()
+            hits, n_hits = orient_fn(o_seqs, o_off, res.sub_off)
+            te = time.perf_counter()
+            timeline.append(("orient", tg - t0, te - t0))
+            stats["t_orient"] += te - tg
+            return res, host.submit(assemble, res, hits, n_hits)
+
         fut = ex.submit(run_cluster, *spans[0])
+        c = fut.result()
+        if len(spans) > 1:
+            fut = ex.submit(run_cluster, *spans[1])
+        cur = orient(c)
         pending = []
         for k, (lo, hi) in enumerate(spans):
-            res, tcl = fut.result()
+            nxt = None
             if k + 1 < len(spans):
-                fut = ex.submit(run_cluster, *spans[k + 1])
-            stats["t_cluster"] += tcl
-            bad = np.nonzero(res.locus_status != 0)[0]
-            if len(bad):
-                i = int(bad[0])
-                raise RuntimeError(f"locus {my_roots[lo + i]}: "
-                                   f"{cluster.STATUS.get(int(res.locus_status[i]), res.locus_status[i])} "
-                                   "(the reference's locus worker raises here)")
-            tg = time.perf_counter()
-            pl = _consensus_chunk(res, mine[lo:hi], orient_fn, consensus_fn, stats)
-            timeline.append(("gpu", tg - t0, time.perf_counter() - t0))
+                c = fut.result()
+                if k + 2 < len(spans):
+                    fut = ex.submit(run_cluster, *spans[k + 2])
+                nxt = orient(c)
+            res, asm_fut = cur
+            prep = asm_fut.result()
+            tp = time.perf_counter()
+            pl = _poa_chunk(res, mine[lo:hi], prep, consensus_fn, stats)
+            timeline.append(("poa", tp - t0, time.perf_counter() - t0))
             if len(spans) > 1:
                 pending.append(post.submit(compact_close, pl, res))
             else:
                 pl["_res"] = res
                 payloads.append(pl)
+            cur = nxt
         payloads += [f.result() for f in pending]
     payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
     if world > 1:
@@ -248,14 +284,16 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         cnt = np.diff(mo)[order]
         new_off = np.zeros(len(order) + 1, dtype=np.int64)
         np.cumsum(cnt, out=new_off[1:])
-        midx = np.concatenate([np.arange(mo[i], mo[i + 1]) for i in order]) if len(order) else np.zeros(0, np.int64)
+        # member rows in output order: for each isoform in `order`, mo[i] .. mo[i+1]-1
+        midx = (np.repeat(mo[:-1][order] - new_off[:-1], cnt) + np.arange(int(new_off[-1]))
+                if len(order) else np.zeros(0, np.int64))
         fasta, r2i = _fasta_and_r2i(payload["names"], payload["n_start"][midx], payload["n_len"][midx], new_off,
                                     payload["cons"], payload["c_sel"][order], payload["c_start"][order],
                                     payload["c_len"][order], payload["c_rc"][order])
         with open(out_path + "/Isoform_Consensi.fasta", "wb") as fh:
-            fh.write(fasta.tobytes())
+            fh.write(memoryview(np.ascontiguousarray(fasta)))
         with open(out_path + "/reads2isoforms.txt", "wb") as fh:
-            fh.write(r2i.tobytes())
+            fh.write(memoryview(np.ascontiguousarray(r2i)))
         stats["written_isoforms"] = int(len(order))
     stats["t_total"] = time.perf_counter() - t0
     for pl in payloads:
@@ -266,20 +304,12 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     return stats
 
 
-def _consensus_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], orient_fn, consensus_fn, stats: dict):
-    """Orientation + assembly + POA for one clustered chunk; returns its writer payload."""
-    t2 = time.perf_counter()
-    # orientation: every subsampled read against its isoform's first subsampled read
-    o_seqs, o_off = _lib.pack_segments([res.text], res.seq_off[res.sub], res.seq_len[res.sub])
-    t2b = time.perf_counter()
-    hits, n_hits = orient_fn(o_seqs, o_off, res.sub_off)
+def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, consensus_fn, stats: dict):
+    """POA of one oriented chunk; returns its writer payload."""
+    asm, p_seqs, p_off, p_grp = prep
     t3 = time.perf_counter()
-    asm = Assembly(res, hits, n_hits)
-    p_seqs, p_off, p_grp = asm.poa_input()
-    t3b = time.perf_counter()
     cons, cons_off = consensus_fn(p_seqs, p_off, p_grp, asm.seeding)
     t4 = time.perf_counter()
-    stats["t_pack"] = stats.get("t_pack", 0.0) + (t2b - t2) + (t3b - t3)
     # consensus of every isoform as a byte segment: POA output, else (<=2 sequences, or an empty POA
     # result) the first emission, re-bound (SDC:911-926)
     n_iso = res.n_isoforms
@@ -299,7 +329,6 @@ def _consensus_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], orient
     stats["poa_groups"] += int(len(asm.poa_iso))
     stats["records"] += int(res.n_records)
     stats["poa_reads"] += int(p_grp[-1])
-    stats["t_orient"] += t3 - t2
     stats["t_poa"] += t4 - t3
     ri = np.asarray(root_idx, dtype=np.int64)
     return dict(iso_root=ri[res.iso_locus] if n_iso else np.zeros(0, np.int64),

@@ -36,9 +36,10 @@ def orient_batch(groups: Sequence[Sequence[str | bytes]], device: int = 0, max_h
     return out
 
 
-def orient_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, device: int = 0, max_hits: int = 4):
+def orient_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, device: int = 0, max_hits: int = 4,
+                  slot: int = 0):
     """Packed form: returns (hits int8 [n_reads, max_hits], n_hits int32 [n_reads])."""
-    ctx = _lib.context(device)
+    ctx = _lib.context(device, slot)
     n = int(len(seq_off)) - 1
     seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
     if seqs.size == 0:

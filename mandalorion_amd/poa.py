@@ -94,4 +94,4 @@ def poa_consensus_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndar
         _lib.check(ctx.lib.mando_poa_batch(ctx.handle, _lib.ctypes.byref(p), _lib.ptr(seqs), _lib.ptr(seq_off),
                                            _lib.ptr(grp_off), n, _lib.ptr(seed_arr), _lib.ptr(cons), cap,
                                            _lib.ptr(cons_off), None))
-    return cons, cons_off
+    return cons[:int(cons_off[-1])], cons_off
