@@ -43,6 +43,7 @@
 #include <vector>
 
 #include <emmintrin.h>
+#include <sys/mman.h>
 
 #include "../../include/mando.h"
 #include "mt19937.h"
@@ -1064,7 +1065,9 @@ void parse_locus(string_view text, int64_t base, vector<Record> &recs) {
 }  // namespace
 
 struct mando_cluster_result {
-    std::unique_ptr<char[]> text;  // all locus files; left uninitialised, the parallel reads fault it in
+    // all locus files; left uninitialised (the parallel reads fault it in), 2 MB-aligned and advised
+    // for transparent huge pages, so a chunk's ~1 GB costs a few hundred faults, not ~300k
+    std::unique_ptr<char, void (*)(void *)> text{nullptr, free};
     size_t text_len = 0;
     vector<int64_t> name_off, seq_off, rec_locus;
     vector<int32_t> name_len, seq_len;
@@ -1132,7 +1135,14 @@ int mando_cluster_loci(const mando_cluster_params *prm, const char *const *psl_p
     }
     for (int64_t i = 0; i < n_loci; ++i) foff[(size_t)i + 1] = foff[(size_t)i] + std::max<int64_t>(0, fsize[(size_t)i]);
     res->text_len = (size_t)foff[(size_t)n_loci];
-    res->text.reset(new char[std::max<size_t>(res->text_len, 1)]);
+    {
+        constexpr size_t kHuge = size_t(2) << 20;
+        const size_t bytes = (std::max<size_t>(res->text_len, 1) + kHuge - 1) / kHuge * kHuge;
+        void *buf = nullptr;
+        if (posix_memalign(&buf, kHuge, bytes) != 0) return MANDO_E_NOMEM;
+        (void)madvise(buf, bytes, MADV_HUGEPAGE);
+        res->text.reset(static_cast<char *>(buf));
+    }
     int nth = prm->threads > 0 ? prm->threads : (int)std::max(1u, std::thread::hardware_concurrency());
     nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n_loci));
     vector<LocusIn> ins((size_t)n_loci);

@@ -191,6 +191,10 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     cuts = sorted(set(min(max(c, 0), len(my_roots)) for c in cuts))
     spans = [(cuts[k], cuts[k + 1]) for k in range(len(cuts) - 1) if cuts[k + 1] > cuts[k]] or [(0, 0)]
 
+    # with several chunks in flight, two cores stay with the GPU driver, assembly and compaction threads
+    n_cpu = threads if threads > 0 else (os.cpu_count() or 1)
+    cl_threads = max(1, n_cpu - 2) if len(spans) > 1 and n_cpu > 4 else threads
+
     def run_cluster(lo, hi):
         # clustering (host C++ threads, GIL released), then the orientation input: the subsampled reads
         tc = time.perf_counter()
@@ -198,7 +202,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                                  ann=ann[lo:hi], cutoff=cutoff, splice_site_width=splice_site_width,
                                  minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
                                  downstream_buffer=downstream_buffer, junctions=junctions, seed=seed,
-                                 threads=threads)
+                                 threads=cl_threads)
         te = time.perf_counter()
         timeline.append(("cluster", tc - t0, te - t0))
         bad = np.nonzero(r.locus_status != 0)[0]
@@ -230,13 +234,17 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         ta = time.perf_counter()
         asm = Assembly(res, hits, n_hits)
         prep = (asm,) + tuple(asm.poa_input())
-        stats["t_assemble"] += time.perf_counter() - ta
+        te = time.perf_counter()
+        stats["t_assemble"] += te - ta
+        timeline.append(("assemble", ta - t0, te - t0))
         return prep
 
-    # The main thread issues the GPU work in the order orientation(k+1), POA(k): chunk k+1's emission
-    # assembly (host) then overlaps chunk k's POA kernel, and no kernel waits behind the persistent POA
-    # grid.  Clustering + packing of chunk k+2 runs on its own thread meanwhile; compaction of finished
-    # chunks on another.
+    # The main thread issues the GPU work in the order orientation(k+1), POA(k) once chunk k+1 is
+    # clustered (waiting for it, except for the first chunk): chunk k+1's emission assembly (host) then
+    # overlaps chunk k's POA kernel, and no kernel waits behind the persistent POA grid.  The first
+    # chunk's POA does not wait for the second chunk's clustering.
+    # Clustering + packing of chunk k+2 runs on its own thread meanwhile; compaction of finished chunks
+    # on another.
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
             ThreadPoolExecutor(max_workers=1) as post:
         def orient(c):
@@ -256,13 +264,18 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             fut = ex.submit(run_cluster, *spans[1])
         cur = orient(c)
         pending = []
+
+        def take_next(k):
+            nonlocal fut
+            c = fut.result()
+            if k + 2 < len(spans):
+                fut = ex.submit(run_cluster, *spans[k + 2])
+            return orient(c)
+
         for k, (lo, hi) in enumerate(spans):
             nxt = None
-            if k + 1 < len(spans):
-                c = fut.result()
-                if k + 2 < len(spans):
-                    fut = ex.submit(run_cluster, *spans[k + 2])
-                nxt = orient(c)
+            if k + 1 < len(spans) and (k > 0 or fut.done()):
+                nxt = take_next(k)
             res, asm_fut = cur
             prep = asm_fut.result()
             tp = time.perf_counter()
@@ -273,6 +286,8 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             else:
                 pl["_res"] = res
                 payloads.append(pl)
+            if k + 1 < len(spans) and nxt is None:
+                nxt = take_next(k)
             cur = nxt
         payloads += [f.result() for f in pending]
     payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
