@@ -180,7 +180,9 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     # POA of chunk k on the GPU.  Chunks are contiguous runs of sorted roots with balanced bytes.
     sizes = np.array([os.path.getsize(os.path.join(out_tmp, r + ".psl")) for r in my_roots], dtype=np.int64)
     if n_chunks <= 0:
-        n_chunks = 1 if sizes.sum() < (64 << 20) else 4
+        # a chunk must keep the persistent POA grid (4,096 waves) busy: the deepest group of a chunk takes
+        # ~0.3 s alone, so chunks of fewer than ~5,000 loci (~10,000 groups) cost more than they overlap
+        n_chunks = 1 if sizes.sum() < (64 << 20) else max(1, min(4, len(my_roots) // 5000))
     n_chunks = max(1, min(n_chunks, len(my_roots)))
     cuts = [0]
     if n_chunks > 1:
