@@ -213,11 +213,24 @@ __device__ int minimizers(OrientLds &sh, const uint8_t *s, int64_t L, uint64_t *
                 if (v != INF) {
                     const int64_t slo = p - ww + 1 > 0 ? p - ww + 1 : 0;
                     const int64_t shi = p < nw - 1 ? p : nw - 1;
-                    for (int64_t w0 = slo; w0 <= shi; ++w0)
-                        if (sh.mb[w0 - h0] == (v >> 1)) {
-                            mark = true;
-                            break;
+                    if (ww == W) {
+                        // every window holding p has minimum <= h(p), so p is some window's minimum
+                        // iff h(p) <= the largest of those minima: W independent LDS reads, no break
+                        uint64_t mx = 0;
+#pragma unroll
+                        for (int t = 0; t < W; ++t) {
+                            const int64_t w0 = p - (W - 1) + t;
+                            const uint64_t mv = sh.mb[i0 + lane + t];  // mb index of window w0
+                            if (w0 >= slo && w0 <= shi) mx = mv > mx ? mv : mx;
                         }
+                        mark = (v >> 1) <= mx;
+                    } else {
+                        for (int64_t w0 = slo; w0 <= shi; ++w0)
+                            if (sh.mb[w0 - h0] == (v >> 1)) {
+                                mark = true;
+                                break;
+                            }
+                    }
                 }
             }
             const unsigned long long m = __ballot(mark);
