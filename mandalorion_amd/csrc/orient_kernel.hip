@@ -143,13 +143,32 @@ __device__ int minimizers(OrientLds &sh, const uint8_t *s, int64_t L, uint64_t *
     const int ww = np <= W ? (int)np : W;
     int n = 0;
     const uint32_t mask30 = (1u << (2 * K)) - 1;
+    // the bases of the next tile are loaded while this one is processed (NPK / 4 bytes per lane)
+    constexpr int NST = NPK * 16 / 64;
+    uint8_t nxt[NST];
+#pragma unroll
+    for (int j = 0; j < NST; ++j) {
+        const int64_t p = -(W - 1) + 64 * j + lane;
+        nxt[j] = (p >= 0 && p < L) ? s[p] : (uint8_t)'N';
+    }
     for (int64_t t0 = 0; t0 < np; t0 += TILE) {
         const int64_t h0 = t0 - (W - 1);  // position of hb[0] and of window mb[0]
-        // stage the tile's bases: one coalesced byte load per base, 16 codes OR-reduced per word
-        for (int e0 = 0; e0 < NPK * 16; e0 += 64) {
+        uint8_t cur[NST];
+#pragma unroll
+        for (int j = 0; j < NST; ++j) cur[j] = nxt[j];
+        if (t0 + TILE < np) {
+#pragma unroll
+            for (int j = 0; j < NST; ++j) {
+                const int64_t p = h0 + TILE + 64 * j + lane;
+                nxt[j] = p < L ? s[p] : (uint8_t)'N';
+            }
+        }
+        // stage the tile's bases: 16 two-bit codes OR-reduced per word
+#pragma unroll
+        for (int j = 0; j < NST; ++j) {
+            const int e0 = 64 * j;
             const int e = e0 + lane;
-            const int64_t p = h0 + e;
-            const int c = (p >= 0 && p < L) ? enc(s[p]) : 4;
+            const int c = enc(cur[j]);
             uint32_t v = c > 3 ? 0u : (uint32_t)c << (2 * (15 - (lane & 15)));
             v |= (uint32_t)__shfl_xor((int)v, 1, 64);
             v |= (uint32_t)__shfl_xor((int)v, 2, 64);
