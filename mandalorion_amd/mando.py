@@ -127,7 +127,10 @@ def main(argv: list[str] | None = None) -> int:
             psl.split_loci(temp_path + "/Isoforms.filtered.clean.psl", temp_path + "/tmp_iso_split", sort_lines=True,
                            sorted_out=srt)
             shutil.rmtree(temp_path + "/tmp_iso_split", ignore_errors=True)
-            print("\tgene grouping (groupIsoforms.py) is not part of this build")
+            from . import genes
+
+            print("\tgrouping isoforms and assigning them to genes (if annotation is provided)")
+            genes.group_isoforms(srt, temp_path + "/Isoforms.filtered.clean.genes", a.genome_annotation)
             for f in os.listdir(temp_path):
                 if f.startswith("Isoforms.filtered."):
                     shutil.copy(os.path.join(temp_path, f), path)
