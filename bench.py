@@ -1,22 +1,33 @@
 #!/usr/bin/env python3
-"""Benchmark of the D-module hot path: batched POA consensus on MI355X (libmando, HIP/gfx950).
+"""Benchmark of the D module (`Mando.py -M D`, i.e. defineIsoforms.py) on MI355X — SURVEY.md §8(d).
 
-Workload (BASELINE.json configs[2], "1M synthetic 3 kb R2C2 reads over 20k loci"): per rank, 20,000
-isoform read groups x 50 reads, templates uniform 2.7-3.3 kb, R2C2 error model (synthetic, seed
-20250117 + rank), already oriented — i.e. exactly what determine_consensus hands abPOA.  One step =
-one mando_poa_batch_device call over all groups with every input resident in HBM, plus (N>1) the
-RCCL all-gather that reassembles the consensus FASTA on rank 0.  Loci shard across ranks (weak
-scaling: every rank gets its own 1M-read shard), no data-path collective besides the reassembly.
+Headline (`value`): PSL records / wall second of the whole D module — locus PSL files on disk ->
+clustering -> orientation (HIP) -> batched POA consensus (HIP) -> Isoform_Consensi.fasta +
+reads2isoforms.txt closed — on BASELINE.json configs[2]: 20,000 synthetic loci x 50 R2C2-shaped reads
+of ~3 kb (1M PSL records; 30 % of the reads on the '-' strand), seed 20250117.  One step = one full
+`define_isoforms` pass over the data set; the clock runs from the start of locus ingest until both
+output files are closed.
 
-Prints ONE JSON line (rank 0).  metric/unit follow BASELINE.json: consensus reads/s (whole node).
+Multi-GPU (`--gpus N`, one process per GPU under the driver's launcher): strong scaling.  The same data
+set is sharded over the ranks by the §8(e) cost estimate (LPT); each rank clusters, orients and runs
+the POA on its loci; one all-gather (RCCL over xGMI, libmando mando_comm_*) brings the results to rank
+0, which writes the files.  value = records / max-over-ranks wall time.
+
+Also reported: the POA kernel's roofline (algorithmic bytes per launch / launch time from HIP events on
+the launch stream), the POA kernel rate (reads through POA / kernel time), and `cpu_baseline`: the same
+driver with the CPU restatements (oracle/) injected for orientation and POA, on a bounded sample of
+the same loci, on the box's host cores (rank 0, N=1 only).  That sample's GPU output must be
+byte-identical to the CPU run's.
+
+Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
-import ctypes
+import hashlib
 import json
-import multiprocessing as mp
 import os
+import shutil
 import sys
 import time
 
@@ -25,7 +36,18 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md "Chip-level parameters"
+HBM_PEAK_GBS = 8000.0  # MI355X, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
+
+WORKLOADS = {
+    # BASELINE.json configs[2]: 1M synthetic ~3 kb R2C2 reads over 20k loci
+    "config3": dict(loci=20000, reads=(50, 50), exon_len=(200, 500), pacbio_frac=0.0, rev_frac=0.3,
+                    text="config3: 20,000 loci x 50 synthetic R2C2 reads (~3 kb, 5-12 exons of 200-500 nt, "
+                         "1-3 isoforms/locus, 30% '-' strand), 1M PSL records, Mando.py -M D"),
+    # BASELINE.json configs[3]: 10M mixed R2C2 + PacBio 2-4 kb reads (~200k gencode-like loci)
+    "config4": dict(loci=200000, reads=(40, 60), exon_len=(130, 570), pacbio_frac=0.2, rev_frac=0.5,
+                    text="config4: 200,000 loci x 40-60 synthetic reads (2-4 kb, 80% R2C2 / 20% PacBio error "
+                         "rates, 50% '-' strand), ~10M PSL records, Mando.py -M D"),
+}
 
 
 def parse():
@@ -33,127 +55,124 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--groups", type=int, default=20000)
-    ap.add_argument("--depth", type=int, default=50)
-    ap.add_argument("--len-lo", type=int, default=2700)
-    ap.add_argument("--len-hi", type=int, default=3300)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config3")
+    ap.add_argument("--loci", type=int, default=0, help="override the workload's locus count")
+    ap.add_argument("--data-dir", default="", help="where the synthetic tmp_SS goes (default $TMPDIR)")
+    ap.add_argument("--threads", type=int, default=0, help="host threads per rank (0: 16 / ranks per node)")
+    ap.add_argument("--cpu-loci", type=int, default=640, help="cpu_baseline sample size (loci)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
-    ap.add_argument("--e2e-loci", type=int, default=2000,
-                    help="also time the whole D module (define_isoforms: PSL files -> FASTA) on this many "
-                         "synthetic 50-read loci; 0 = skip (reported as d_module, never as value)")
     return ap.parse_args()
 
 
-_ENC = np.full(256, 4, dtype=np.uint8)
-for _c, _v in zip(b"ACGTacgt", (0, 1, 2, 3, 0, 1, 2, 3)):
-    _ENC[_c] = _v
-
-
-def lpt_order(seq_off, grp_off):
-    """Groups sorted by estimated DP work (reads x first-read length), largest first."""
-    lens = np.diff(seq_off)
-    first = lens[grp_off[:-1]]
-    tot = np.add.reduceat(lens, grp_off[:-1]) if len(lens) else np.zeros(0)
-    return np.argsort(-(tot - first).astype(np.float64) * first, kind="stable")
-
-
-def reorder(seqs, seq_off, grp_off, order):
-    """Repack groups in `order` (so the device processes the heaviest groups first)."""
-    parts, offs, goff = [], [0], [0]
-    total = 0
-    for g in order:
-        a, b = grp_off[g], grp_off[g + 1]
-        s0, s1 = seq_off[a], seq_off[b]
-        parts.append(seqs[s0:s1])
-        offs.extend((seq_off[a + 1:b + 1] - s0 + total).tolist())
-        total += s1 - s0
-        goff.append(goff[-1] + (b - a))
-    return np.concatenate(parts), np.asarray(offs, dtype=np.int64), np.asarray(goff, dtype=np.int64)
-
-
-def _cpu_worker(args):
-    groups, deadline = args
-    from oracle import poa as opoa
-
-    done_reads = 0
-    done_groups = 0
-    t0 = time.perf_counter()
-    for g in groups:
-        if time.perf_counter() > deadline:
-            break
-        opoa.consensus_batch([g])
-        done_reads += len(g)
-        done_groups += 1
-    return done_reads, done_groups, time.perf_counter() - t0
-
-
-def _cpu_init():
-    from oracle import poa as opoa
-
-    opoa.load()
-
-
-def cpu_baseline(seqs, seq_off, grp_off, seconds, procs):
-    """oracle/poa_ref.c (C restatement of abPOA, 1 thread per process) on a time-bounded sample.
-
-    Runs before the GPU is initialised, in `spawn` workers (no inherited HIP state); each process gets
-    far more groups than it can finish (~0.2 s per 50x3kb group) and stops at the shared deadline."""
+def gen_data(d: str, wl: dict, n_loci: int, threads: int) -> int:
+    """Synthetic tmp_SS (libmando_synth); a marker file caches the record count across runs."""
     from mandalorion_amd import synth
 
-    n_groups = len(grp_off) - 1
-    per = max(8, int(seconds * 12))
-    want = min(n_groups, procs * per)
-    pick = list(range(0, n_groups, max(1, n_groups // want)))[:want]  # evenly strided sample
-    groups = synth.unpack_groups(seqs, seq_off, grp_off, pick)
-    chunks = [groups[i::procs] for i in range(procs)]
-    ctx = mp.get_context("spawn")
-    with ctx.Pool(procs, initializer=_cpu_init) as pool:
-        pool.map(_cpu_init_probe, range(procs))  # workers up and the oracle loaded before the clock
-        t0 = time.perf_counter()
-        deadline = t0 + seconds
-        res = pool.map(_cpu_worker, [(c, deadline) for c in chunks])
-        wall = time.perf_counter() - t0
-    reads = sum(r[0] for r in res)
-    ngr = sum(r[1] for r in res)
-    return {
-        "value": reads / wall if wall > 0 else 0.0,
-        "unit": "reads/s",
-        "cores": procs,
-        "kind": "port",
-        "sample": f"{ngr} groups x {groups[0] and len(groups[0])} reads of this workload through oracle/poa_ref.c "
-                  f"(C restatement of abPOA v1.4.1, scalar), {procs} processes, {wall:.1f} s wall",
-    }
+    marker = os.path.join(d, "records.txt")
+    if os.path.exists(marker):
+        return int(open(marker).read())
+    shutil.rmtree(os.path.join(d, "tmp_SS"), ignore_errors=True)
+    n = synth.write_loci(os.path.join(d, "tmp_SS"), n_loci, reads=wl["reads"], exon_len=wl["exon_len"],
+                         threads=threads, pacbio_frac=wl["pacbio_frac"], rev_frac=wl["rev_frac"])
+    with open(marker + ".tmp", "w") as fh:
+        fh.write(str(n))
+    os.replace(marker + ".tmp", marker)
+    return n
 
 
-def d_module_e2e(n_loci, device):
-    """Whole D module (mandalorion_amd.define.define_isoforms, i.e. `Mando.py -M D`): locus PSL files on
-    disk -> clustering (host C++) -> orientation + POA (GPU) -> Isoform_Consensi.fasta.  Reported as
-    PSL records / wall second, the BASELINE.md end-to-end metric, on a config-3-shaped sample."""
-    import shutil
-    import tempfile
+def cpu_fns(threads: int):
+    """orient_fn / consensus_fn over the CPU restatements (oracle/), groups split over host threads
+    (ctypes drops the GIL inside the C calls)."""
+    from concurrent.futures import ThreadPoolExecutor
 
-    from mandalorion_amd import define, synth
+    from oracle import orient as oref
+    from oracle import poa as opoa
 
-    d = tempfile.mkdtemp(prefix="mando_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+    pool = ThreadPoolExecutor(max_workers=threads)
+
+    def split(seq_off, grp_off, k):
+        lens = np.diff(seq_off)
+        cost = np.add.reduceat(lens, grp_off[:-1]).astype(np.float64) if len(lens) else np.zeros(0)
+        cost *= np.maximum(1, np.diff(grp_off))
+        cs = np.cumsum(cost)
+        cuts = [0] + [int(np.searchsorted(cs, cs[-1] * i / k)) for i in range(1, k)] + [len(grp_off) - 1]
+        cuts = sorted(set(min(max(c, 0), len(grp_off) - 1) for c in cuts))
+        return [(cuts[i], cuts[i + 1]) for i in range(len(cuts) - 1) if cuts[i + 1] > cuts[i]]
+
+    def sub(seqs, seq_off, grp_off, a, b):
+        r0, r1 = grp_off[a], grp_off[b]
+        return seqs, seq_off[r0:r1 + 1], grp_off[a:b + 1] - r0
+
+    def orient_fn(seqs, seq_off, grp_off):
+        parts = split(seq_off, grp_off, 4 * threads)
+        res = list(pool.map(lambda ab: oref.orient_packed(*sub(seqs, seq_off, grp_off, *ab)), parts))
+        if not res:
+            return oref.orient_packed(seqs, seq_off, grp_off)
+        return np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res])
+
+    def consensus_fn(seqs, seq_off, grp_off, seeding):
+        parts = split(seq_off, grp_off, 4 * threads)
+        if not parts:
+            return opoa.consensus_packed(seqs, seq_off, grp_off)
+        res = list(pool.map(lambda ab: opoa.consensus_packed(*sub(seqs, seq_off, grp_off, *ab),
+                                                             seeding=None if seeding is None else seeding[ab[0]:ab[1]]),
+                            parts))
+        cons = np.concatenate([c[:int(o[-1])] for c, o in res])
+        off = [np.zeros(1, dtype=np.int64)]
+        base = 0
+        for _, o in res:
+            off.append(o[1:] + base)
+            base += int(o[-1])
+        return cons, np.concatenate(off)
+
+    return orient_fn, consensus_fn, pool
+
+
+def run_define(d, threads, device, comm=None, **kw):
+    from mandalorion_amd import define
+
+    return define.define_isoforms(d, threads=threads, device=device, comm=comm, **kw)
+
+
+def sample_dir(src: str, dst: str, n: int) -> int:
+    """dst/tmp_SS = symlinks to the first n locus files of src (sorted roots), for the CPU baseline."""
+    from mandalorion_amd import define
+
+    roots = define._roots(os.path.join(src, "tmp_SS"))[:n]
+    shutil.rmtree(dst, ignore_errors=True)
+    os.makedirs(os.path.join(dst, "tmp_SS"))
+    recs = 0
+    for r in roots:
+        f = os.path.join(src, "tmp_SS", r + ".psl")
+        os.symlink(f, os.path.join(dst, "tmp_SS", r + ".psl"))
+        with open(f, "rb") as fh:
+            recs += sum(1 for _ in fh)
+    return recs
+
+
+def sha(path):
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()
+
+
+def cpu_baseline(data: str, n_loci: int, threads: int):
+    """The restated CPU baseline (SURVEY.md §8(d) option 2): host clustering + oracle/ orientation and
+    POA on `threads` host threads, on the first n_loci loci of the same data set."""
+    d = os.path.join(data, "cpu_sample")
+    recs = sample_dir(data, d, n_loci)
+    of, cf, pool = cpu_fns(threads)
     try:
-        n = synth.write_loci(os.path.join(d, "tmp_SS"), n_loci, threads=16)
-        define.define_isoforms(d, threads=16, device=device)  # warm (context, kernels, page cache)
         t0 = time.perf_counter()
-        st = define.define_isoforms(d, threads=16, device=device)
+        st = run_define(d, threads, 0, orient_fn=of, consensus_fn=cf)
         wall = time.perf_counter() - t0
     finally:
-        shutil.rmtree(d, ignore_errors=True)
-    return {"records": n, "loci": st["loci"], "isoforms": st["isoforms"], "poa_groups": st["poa_groups"],
-            "wall_s": wall, "reads_per_s": n / wall, "t_cluster": st["t_cluster"], "t_orient": st["t_orient"],
-            "t_poa": st["t_poa"], "host_threads": 16,
-            "input": f"{n_loci} synthetic loci x 50 R2C2 reads (5-12 exons of 150-400 nt), PSL files on disk"}
-
-
-def _cpu_init_probe(_):
-    return os.getpid()
+        pool.shutdown()
+    out = {"value": recs / wall, "unit": "records/s", "cores": threads, "kind": "port",
+           "sample": f"first {n_loci} loci ({recs} PSL records, {st['poa_reads']} POA reads) of this workload through "
+                     f"the same D driver with oracle/orient_ref.c + oracle/poa_ref.c (C restatements of mappy "
+                     f"map-ont and abPOA v1.4.1) on {threads} host threads, clustering on the host; {wall:.1f} s wall"}
+    hashes = (sha(os.path.join(d, "Isoform_Consensi.fasta")), sha(os.path.join(d, "reads2isoforms.txt")))
+    return out, d, hashes
 
 
 def main():
@@ -161,148 +180,125 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    from mandalorion_amd import synth
-
-    seqs, seq_off, grp_off = synth.fast_groups(args.groups, (args.len_lo, args.len_hi),
-                                               (args.depth, args.depth), seed=synth.DATA_SEED + rank,
-                                               threads=16)
-    # CPU baseline first, on rank 0 of a 1-GPU run, before anything touches the GPU
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(seqs, seq_off, grp_off, args.cpu_seconds, procs)
-    import torch
-
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    wl = WORKLOADS[args.workload]
+    n_loci = args.loci or wl["loci"]
+    threads = args.threads or max(2, 16 // max(1, local_world) if local_world <= 8 else 2)
+    gen_threads = 16 if rank == 0 else threads
+    base = args.data_dir or os.environ.get("TMPDIR", "/tmp")
+    data = os.path.join(base, f"mando_bench_{args.workload}_{n_loci}")
+    os.makedirs(data, exist_ok=True)
 
     from mandalorion_amd import _lib
 
-    ctx = _lib.context(local)
-    order = lpt_order(seq_off, grp_off)
-    seqs, seq_off, grp_off = reorder(seqs, seq_off, grp_off, order)
-    n_groups = len(grp_off) - 1
-    n_reads = len(seq_off) - 1
-    lens = np.diff(seq_off)
-    max_len = int(lens.max())
-    gsum = np.add.reduceat(lens, grp_off[:-1])
-    ccap = np.zeros(n_groups + 1, dtype=np.int64)
-    np.cumsum(2 * np.maximum.reduceat(lens, grp_off[:-1]) + 256, out=ccap[1:])
+    comm = None
+    if world > 1:
+        from mandalorion_amd.comm import Comm
 
-    d_seq = torch.from_numpy(_ENC[seqs]).to(dev)
-    d_seq_off = torch.from_numpy(seq_off).to(dev)
-    d_grp_off = torch.from_numpy(grp_off).to(dev)
-    d_cons_off = torch.from_numpy(ccap).to(dev)
-    d_cons = torch.zeros(int(ccap[-1]), dtype=torch.uint8, device=dev)
-    d_cons_len = torch.zeros(n_groups, dtype=torch.int32, device=dev)
-    d_cells = torch.zeros(n_groups, dtype=torch.int64, device=dev)
-    d_status = torch.full((n_groups,), 99, dtype=torch.int32, device=dev)
-    torch.cuda.synchronize()
-    p = _lib.PoaParams.defaults()
-
-    def step():
-        _lib.check(ctx.lib.mando_poa_batch_device(
-            ctx.handle, ctypes.byref(p), d_seq.data_ptr(), d_seq_off.data_ptr(), d_grp_off.data_ptr(),
-            n_groups, max_len, int(gsum.max()), d_cons.data_ptr(), d_cons_off.data_ptr(),
-            d_cons_len.data_ptr(), d_cells.data_ptr(), d_status.data_ptr()))
-        ctx.sync()
-        if dist is not None:  # reassembly of the consensus FASTA on rank 0 (RCCL over xGMI)
-            lens_all = [torch.empty_like(d_cons_len) for _ in range(world)]
-            dist.all_gather(lens_all, d_cons_len)
-            cons_all = [torch.empty_like(d_cons) for _ in range(world)]
-            dist.all_gather(cons_all, d_cons)
-        return ctx.last_kernel_ms()
-
-    for _ in range(args.warmup):
-        step()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    kms = [step() for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    status = d_status.cpu().numpy()
-    if (status != 0).any():
-        raise SystemExit(f"rank {rank}: {int((status != 0).sum())} groups failed (status {np.unique(status)})")
-    cells = d_cells.cpu().numpy()
-    clen = d_cons_len.cpu().numpy().astype(np.int64)
-    # spot parity check of two groups against the CPU restatement (full parity: tests/test_poa_gpu.py)
+        comm = Comm.from_env(device=local)
     if rank == 0:
-        from oracle import poa as opoa
+        records = gen_data(data, wl, n_loci, gen_threads)
+    if comm is not None:
+        comm.barrier()
+    records = int(open(os.path.join(data, "records.txt")).read())
 
-        pick = [n_groups - 1, n_groups // 2]
-        want = opoa.consensus_batch(synth.unpack_groups(seqs, seq_off, grp_off, pick))
-        raw = d_cons.cpu().numpy()
-        got = [bytes(raw[ccap[g]:ccap[g] + clen[g]]).translate(bytes.maketrans(b"\0\1\2\3\4", b"ACGTN")).decode()
-               for g in pick]
-        if got != want:
-            raise SystemExit("GPU consensus differs from the CPU restatement on the spot check")
+    # CPU baseline first (rank 0 of a 1-GPU run): bounded sample, oracle orientation + POA on host threads
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, cpu_dir, cpu_hashes = cpu_baseline(data, min(args.cpu_loci, n_loci), 16)
 
-    # roofline: algorithmic bytes per launch = 1 B traceback per DP cell + each read once + consensus
-    alg_bytes = float(cells.sum() + lens.sum() + clen.sum())
-    kernel_s = float(np.mean(kms)) / 1e3
-    achieved = alg_bytes / kernel_s / 1e9
+    ctx = _lib.context(local)
+    for _ in range(args.warmup):
+        run_define(data, threads, local, comm)
+    if comm is not None:
+        comm.barrier()
+    t0 = time.perf_counter()
+    stats = [run_define(data, threads, local, comm) for _ in range(args.steps)]
+    if comm is not None:
+        comm.barrier()
+    elapsed = time.perf_counter() - t0
+    if comm is not None:
+        elapsed = comm.max(elapsed)
+    st = stats[-1]
+
+    # roofline of the dominant kernel (POA), from this rank's launches of the last timed step:
+    # algorithmic bytes per launch = 1 B traceback per DP cell + each read once + each consensus once
+    la = st["poa_launches"]
+    n_launch = sum(x["launches"] for x in la)
+    alg = sum(x["cells"] + x["read_bytes"] + x["cons_bytes"] for x in la)
+    k_ms = sum(x["kernel_ms"] for x in la)
+    achieved = (alg / max(1, n_launch)) / (k_ms / max(1, n_launch) / 1e3) / 1e9 if k_ms > 0 else 0.0
     traffic = None
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
-            if pm.get("workload") == f"{args.groups}x{args.depth}x{args.len_lo}-{args.len_hi}":
+            if pm.get("workload") == f"{args.workload}:{n_loci}":
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+
+    # parity of the GPU path on the CPU baseline's sample (byte-identical output files)
+    parity = None
+    if cpu is not None:
+        run_define(cpu_dir, threads, local)
+        got = (sha(os.path.join(cpu_dir, "Isoform_Consensi.fasta")), sha(os.path.join(cpu_dir, "reads2isoforms.txt")))
+        parity = got == cpu_hashes
+        if not parity:
+            raise SystemExit("GPU D-module output differs from the CPU restatement on the baseline sample")
+
     out = {
-        "metric": "consensus reads/s (whole node)",
-        "value": world * n_reads * args.steps / elapsed,
-        "unit": "reads/s",
+        "metric": "consensus reads/s (whole node): PSL records / wall s of Mando.py -M D",
+        "value": records * args.steps / elapsed,
+        "unit": "records/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int16",
-        "data": "synthetic R2C2-shaped read groups (seed 20250117+rank), oriented, inputs resident in HBM",
+        "data": "synthetic PSL loci (libmando_synth, seed 20250117): no real reads in the container",
         "config": {
-            "workload": f"config3: {n_groups} isoform groups x {args.depth} reads x {args.len_lo}-{args.len_hi} nt "
-                        f"per GPU ({n_reads} reads), abPOA -M 5 -r 0 semantics",
-            "groups_per_gpu": n_groups,
-            "reads_per_gpu": n_reads,
-            "parallelism": f"loci sharded over {world} GPU(s), RCCL all-gather reassembly",
-            "dp_cells_per_launch": int(cells.sum()),
-            "kernel_ms": float(np.mean(kms)),
-            "gcups": float(cells.sum()) / kernel_s / 1e9,
+            "workload": wl["text"] + (f" (loci overridden: {n_loci})" if args.loci else ""),
+            "records": records,
+            "loci": st["loci"],
+            "isoforms": st["isoforms"],
+            "poa_groups_rank0": st["poa_groups"],
+            "poa_reads_rank0": st["poa_reads"],
+            "parallelism": f"loci sharded over {world} GPU(s) (LPT on the DP-cost estimate), one all-gather "
+                          f"({comm.backend if comm else 'none'}) to the writer on rank 0",
+            "host_threads_per_rank": threads,
+            "phases_rank0_s": {k: round(st[k], 4) for k in ("t_ingest", "t_cluster", "t_orient", "t_assemble", "t_poa",
+                                                             "t_total") if k in st},
+            "poa_kernel": {
+                "launches": n_launch,
+                "kernel_ms_total": k_ms,
+                "dp_cells": sum(x["cells"] for x in la),
+                "gcups": sum(x["cells"] for x in la) / (k_ms / 1e3) / 1e9 if k_ms > 0 else None,
+                "reads_per_s": sum(x["reads"] for x in la) / (k_ms / 1e3) if k_ms > 0 else None,
+            },
+            "gpu_equals_cpu_on_sample": parity,
         },
         "roofline": {
-            "bound": "hbm",
+            "bound": "issue",
+            "roofline": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "kernel": "poa_kernel",
+            "note": "integer DP, no MFMA; the kernel is issue/latency-bound (SQ counters: DESIGN.md §3.1)",
         },
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu
-    if rank == 0 and world == 1 and args.e2e_loci > 0:
-        out["d_module"] = d_module_e2e(args.e2e_loci, local)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.close()
+    ctx.close()
 
 
 if __name__ == "__main__":

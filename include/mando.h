@@ -97,8 +97,12 @@ float mando_last_kernel_ms(mando_ctx *ctx);
 int mando_last_kernel_launches(mando_ctx *ctx);
 
 /* Read orientation (mappy map-ont strand / primary-hit replacement).  For each group the
- * reference sequence is the group's first read.  For every read r, n_hits[r] in {0,1} is the
- * number of primary hits and hit_strands[r*max_hits] is +1 / -1.  seqs as in mando_poa_batch. */
+ * reference sequence is the group's first read.  For every read r, n_hits[r] is the number of primary
+ * hits (0 = unmapped; the reference then drops the read) and hit_strands[r*max_hits + h] (+1 / -1) the
+ * strand of hit h, in mappy's hit order; the reference writes the read once per primary hit, re-bound
+ * by the hits before it (SpliceDefineConsensus.py:902-907).  Counting stops at max_hits + 1:
+ * n_hits[r] == max_hits + 1 means "more than max_hits primaries" (only max_hits strands written), and
+ * the caller re-runs with a larger max_hits (1..8). */
 int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_off,
                        const int64_t *grp_off, int64_t n_groups, int8_t *hit_strands,
                        int32_t max_hits, int32_t *n_hits);
@@ -170,6 +174,31 @@ int mando_cluster_loci(const mando_cluster_params *params, const char *const *ps
                        const int64_t *ann_off, mando_cluster_result **out);
 int mando_cluster_view_get(const mando_cluster_result *res, mando_cluster_view *view);
 void mando_cluster_free(mando_cluster_result *res);
+
+/* ------------------------------------------------------------------------------------------------
+ * Reassembly of the sharded D module: loci are split over ranks (one process per
+ * GPU); the only exchange is one all-gather of each rank's results to the ordered writer on rank 0
+ * (the reference's Pool writer, /root/reference/defineIsoforms.py:130-166).
+ * Rendezvous is a TCP star (rank 0 listens on addr:port; the others connect, retrying for up to
+ * timeout_s seconds).  With a device ctx the ranks then form an RCCL communicator on that device
+ * (rank 0 draws the ncclUniqueId and ships it over the star) and mando_allgather_bytes runs over RCCL
+ * / xGMI; with ctx == NULL the star carries the bytes (CPU-only runs).  nranks == 1 needs no peers.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct mando_comm mando_comm;
+
+int mando_comm_init(mando_ctx *ctx, int nranks, int rank, const char *addr, int port, double timeout_s,
+                    mando_comm **out);
+/* 1 = RCCL, 0 = host sockets */
+int mando_comm_backend(const mando_comm *comm);
+/* counts[r] = rank r's n (every rank gets all nranks counts) */
+int mando_allgather_counts(mando_comm *comm, int64_t n, int64_t *counts);
+/* recv = every rank's send bytes concatenated in rank order; recv_counts from mando_allgather_counts */
+int mando_allgather_bytes(mando_comm *comm, const uint8_t *send, int64_t n, uint8_t *recv,
+                          const int64_t *recv_counts);
+/* *v = max over ranks of *v (the benchmark's max-over-ranks wall time) */
+int mando_allreduce_max_f64(mando_comm *comm, double *v);
+int mando_comm_barrier(mando_comm *comm);
+void mando_comm_destroy(mando_comm *comm);
 
 /* Host helper of the D driver (FASTA / read-group assembly without per-read interpreter work):
  * segment i = src[sel[i]] + starts[i], lens[i] bytes (sel may be NULL: src[0]), reverse-complemented

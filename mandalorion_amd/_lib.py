@@ -34,6 +34,13 @@ EXPORTED = (
     "mando_cluster_loci",
     "mando_cluster_view_get",
     "mando_cluster_free",
+    "mando_comm_init",
+    "mando_comm_backend",
+    "mando_allgather_counts",
+    "mando_allgather_bytes",
+    "mando_allreduce_max_f64",
+    "mando_comm_barrier",
+    "mando_comm_destroy",
     "mando_pack_segments",
     "mando_split_loci",
     "mando_sam_to_psl",
@@ -187,6 +194,15 @@ def load(path: str | None = None):
         lib.mando_psl_to_gtf.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         lib.mando_quantify.argtypes = [_P, ctypes.c_int32] + [ctypes.c_char_p] * 4
         lib.mando_pack_segments.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, ctypes.c_int32]
+        lib.mando_comm_init.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                        ctypes.c_double, _P]
+        lib.mando_comm_backend.argtypes = [_P]
+        lib.mando_allgather_counts.argtypes = [_P, _I64, _P]
+        lib.mando_allgather_bytes.argtypes = [_P, _P, _I64, _P, _P]
+        lib.mando_allreduce_max_f64.argtypes = [_P, _P]
+        lib.mando_comm_barrier.argtypes = [_P]
+        lib.mando_comm_destroy.argtypes = [_P]
+        lib.mando_comm_destroy.restype = None
         if hasattr(lib, "mando_selftest"):
             lib.mando_selftest.argtypes = [_P, _P]
         if path is None:

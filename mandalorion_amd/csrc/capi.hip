@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/mando.h"
+#include "internal.h"
 #include "orient_kernel.h"
 #include "poa_kernel.h"
 
@@ -239,6 +240,12 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
 }
 
 }  // namespace
+
+namespace mando {
+int set_error(int code, const std::string &msg) { return fail(code, msg); }
+int ctx_device(const mando_ctx *ctx) { return ctx->device; }
+hipStream_t ctx_stream(const mando_ctx *ctx) { return ctx->stream; }
+}  // namespace mando
 
 extern "C" {
 

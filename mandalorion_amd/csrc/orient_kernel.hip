@@ -434,8 +434,10 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
             idx[t] = c;
         }
         int np = 0;
-        int pqs[8], pqe[8];
-        for (int c = 0; c < nch && np < max_hits && np < 8; ++c) {
+        // one primary past max_hits (<= 8) is still counted: n_hits == max_hits + 1 reports the
+        // overflow, and the host re-runs with room for more (the reference writes every primary)
+        int pqs[9], pqe[9];
+        for (int c = 0; c < nch && np <= max_hits && np < 9; ++c) {
             const int id = idx[c];
             const int qs = sh.ch_qs[id], qe = sh.ch_qe[id];
             bool prim = true;
@@ -450,7 +452,7 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
             if (!prim) continue;
             pqs[np] = qs;
             pqe[np] = qe;
-            hits[np] = sh.ch_rev[id] ? -1 : 1;
+            if (np < max_hits) hits[np] = sh.ch_rev[id] ? -1 : 1;
             ++np;
         }
         *n_hits = np;

@@ -149,6 +149,7 @@ void mando_synth_free(void *p) { free(p); }
 int64_t mando_synth_loci(const char *dir, uint64_t seed, int64_t n_loci, int32_t reads_lo, int32_t reads_hi,
                          int32_t ex_lo, int32_t ex_hi, int32_t elen_lo, int32_t elen_hi, int32_t ilen_lo,
                          int32_t ilen_hi, int32_t iso_lo, int32_t iso_hi, double sub, double ins, double dele,
+                         double pb_frac, double pb_sub, double pb_ins, double pb_dele, double rev_frac,
                          int threads) {
     if (n_loci < 0 || reads_lo < 1 || reads_hi < reads_lo || ex_lo < 1 || ex_hi < ex_lo || elen_lo < 20 ||
         elen_hi < elen_lo || ilen_lo < 60 || ilen_hi < ilen_lo || iso_lo < 1 || iso_hi < iso_lo)
@@ -206,6 +207,12 @@ int64_t mando_synth_loci(const char *dir, uint64_t seed, int64_t n_loci, int32_t
         std::vector<std::tuple<int64_t, int64_t, std::string>> lines;
         for (int rd = 0; rd < nreads; ++rd) {
             const auto &iso = isos[(size_t)r.below((int)isos.size())];
+            // per read: PacBio-like rates for a pb_frac share of the reads (config 4's mix), and the
+            // read's own orientation (a '-' strand record carries the reverse-complemented read, as
+            // emtrey writes it); no extra draws when the shares are 0, so those streams are unchanged
+            const bool pb = pb_frac > 0 && r.uni() < pb_frac;
+            const bool rev = rev_frac > 0 && r.uni() < rev_frac;
+            const double sub_r = pb ? pb_sub : sub, ins_r = pb ? pb_ins : ins, dele_r = pb ? pb_dele : dele;
             std::vector<std::pair<int64_t, int64_t>> e;
             for (int k : iso) e.push_back(ex[(size_t)k]);
             e.front().first += r.below(7) - 3;
@@ -222,12 +229,12 @@ int64_t mando_synth_loci(const char *dir, uint64_t seed, int64_t n_loci, int32_t
                     const double f = hp ? 2.0 : 1.0;
                     const bool edge = (k == 0 && i == 0) || (k + 1 == e.size() && i == n - 1);
                     const double u = r.uni();
-                    if (!edge && u < dele * f) {
+                    if (!edge && u < dele_r * f) {
                         if (last != '-') { cs += '-'; ++tins; }
                         cs += (char)(c | 0x20);
                         last = '-';
                         ++tbase;
-                    } else if (!edge && u < dele * f + sub) {
+                    } else if (!edge && u < dele_r * f + sub_r) {
                         const char qb = kB[(idx(c) + 1 + r.below(3)) & 3];
                         cs += '*';
                         cs += (char)(c | 0x20);
@@ -242,7 +249,7 @@ int64_t mando_synth_loci(const char *dir, uint64_t seed, int64_t n_loci, int32_t
                         last = '=';
                         ++match;
                     }
-                    if (!(k + 1 == e.size() && i == n - 1) && r.uni() < ins * f) {
+                    if (!(k + 1 == e.size() && i == n - 1) && r.uni() < ins_r * f) {
                         const char b = r.uni() < 0.5 ? c : kB[r.below(4)];
                         if (last != '+') { cs += '+'; ++qins; }
                         cs += (char)(b | 0x20);
@@ -269,12 +276,16 @@ int64_t mando_synth_loci(const char *dir, uint64_t seed, int64_t n_loci, int32_t
                 qq += e[k].second - e[k].first;
                 if (k + 1 < e.size()) introns += e[k + 1].first - e[k].second;
             }
+            if (rev) {
+                std::reverse(q.begin(), q.end());
+                for (auto &ch : q) ch = ch == 'A' ? 'T' : ch == 'C' ? 'G' : ch == 'G' ? 'C' : ch == 'T' ? 'A' : ch;
+            }
             const int64_t alen = match + mis + qbase + tbase;
             char acc[32];
             snprintf(acc, sizeof acc, "%.4f", alen ? (double)match / (double)alen : 1.0);
             std::string line = std::to_string(match) + "\t" + std::to_string(mis) + "\t0\t" + std::to_string(introns) +
                                "\t" + std::to_string(qins) + "\t" + std::to_string(qbase) + "\t" + std::to_string(tins) +
-                               "\t" + std::to_string(tbase) + "\t+\tS" + std::to_string(li) + "_r" + std::to_string(rd) +
+                               "\t" + std::to_string(tbase) + (rev ? "\t-\tS" : "\t+\tS") + std::to_string(li) + "_r" + std::to_string(rd) +
                                "\t" + std::to_string(q.size()) + "\t0\t" + std::to_string(q.size()) + "\t" + chrom +
                                "\t250000000\t" + std::to_string(e.front().first) + "\t" + std::to_string(e.back().second) +
                                "\t" + std::to_string(e.size()) + "\t" + bs + "\t" + qs + "\t" + ts + "\t" + acc + "\t" +

@@ -13,8 +13,8 @@ Instead of one forked process per locus calling mappy + an `abpoa` subprocess pe
      length -> `-S`) on the host;
   4. one batched POA consensus over all remaining isoforms (`mando_poa_batch`, HIP);
   5. the ordered writer (sorted roots x IsoDict order, `Isoform{k}_{n}`).
-Loci shard across ranks (torch.distributed, one process per GPU); the only exchange is the gather of
-per-locus results to rank 0 for the writer.
+Loci shard across ranks (one process per GPU, mandalorion_amd.comm); the only exchange is one all-gather
+of per-locus results to rank 0 for the writer (RCCL over xGMI).
 """
 from __future__ import annotations
 
@@ -38,16 +38,23 @@ def revcomp(s: str) -> str:
 
 
 def gpu_orient(seqs, seq_off, grp_off, device: int = 0, max_hits: int = 4):
-    """Per read: the strands (+1/-1) of its primary hits against its group's first read (HIP)."""
+    """Per read: the strands (+1/-1) of its primary hits against its group's first read (HIP).  A read
+    with more than max_hits primaries (n_hits == max_hits + 1) re-runs the batch with room for 8; more
+    than 8 is refused rather than silently truncated."""
     from . import orient
 
-    return orient.orient_packed(seqs, seq_off, grp_off, device=device, max_hits=max_hits, slot=1)
+    hits, nh = orient.orient_packed(seqs, seq_off, grp_off, device=device, max_hits=max_hits, slot=1)
+    if len(nh) and int(nh.max()) > max_hits:
+        if max_hits >= 8:
+            raise _lib.MandoError(-5, "a read has more than 8 primary hits against its isoform's first read")
+        return gpu_orient(seqs, seq_off, grp_off, device=device, max_hits=8)
+    return hits, nh
 
 
-def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0):
+def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0, info: dict | None = None):
     from . import poa
 
-    return poa.poa_consensus_packed(seqs, seq_off, grp_off, seeding=seeding, device=device)
+    return poa.poa_consensus_packed(seqs, seq_off, grp_off, seeding=seeding, device=device, info=info)
 
 
 def _roots(out_tmp: str) -> list[str]:
@@ -56,6 +63,28 @@ def _roots(out_tmp: str) -> list[str]:
         if os.path.isfile(os.path.join(out_tmp, f)) and ".psl" in f:
             roots.add(f.split(".psl")[0])  # chrom~start~end (a '~' in a chrom breaks the reference too)
     return sorted(roots, key=lambda x: (x.split("~")[0], int(x.split("~")[1])))
+
+
+def _locus_costs(out_tmp: str, roots: list[str]) -> np.ndarray:
+    """Per-locus POA cost estimate: n reads of length L cost n * L * (2w + 1) * 1.1 L
+    with w = 10 + 0.01 L (rows ~ 1.1 L graph nodes, band 2w+1).  L is the first record's qSize (col 10)
+    and n ~ file size / that record's length: one small read per file, no parse of the locus."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(r):
+        f = os.path.join(out_tmp, r + ".psl")
+        size = os.path.getsize(f)
+        with open(f, "rb") as fh:
+            line = fh.readline()
+        try:
+            L = float(line.split(b"\t", 11)[10])
+        except (IndexError, ValueError):
+            L = 1.0
+        n = size / max(1, len(line))
+        return n * L * (2 * (10 + 0.01 * L) + 1) * 1.1 * L
+
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        return np.fromiter(ex.map(one, roots), dtype=np.float64, count=len(roots))
 
 
 class Assembly:
@@ -145,12 +174,26 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                     junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", upstream_buffer: int = 10,
                     downstream_buffer: int = 50, seed: int = 0, device: int = 0,
                     orient_fn: Callable | None = None, consensus_fn: Callable | None = None,
-                    rank: int = 0, world: int = 1, comm=None, verbose: bool = False, n_chunks: int = 0) -> dict:
+                    comm=None, verbose: bool = False, n_chunks: int = 0) -> dict:
     """Runs the D module on <path>/tmp_SS/*.psl.  orient_fn(seqs, seq_off, grp_off) -> (hits, n_hits) and
-    consensus_fn(seqs, seq_off, grp_off, seeding) -> (cons bytes, cons_off) default to the HIP path."""
+    consensus_fn(seqs, seq_off, grp_off, seeding) -> (cons bytes, cons_off) default to the HIP path.
+    comm (mandalorion_amd.comm.Comm, optional): shard the loci over comm.world ranks; rank 0 writes."""
     t0 = time.perf_counter()
+    rank, world = (comm.rank, comm.world) if comm is not None else (0, 1)
     orient_fn = orient_fn or (lambda s, o, g: gpu_orient(s, o, g, device=device))
-    consensus_fn = consensus_fn or (lambda s, o, g, sd: gpu_consensus(s, o, g, sd, device=device))
+    poa_launches = []  # per POA call: DP cells, kernel ms, read + consensus bytes (the roofline's inputs)
+
+    def _gpu_poa(s, o, g, sd):
+        info = {}
+        out = gpu_consensus(s, o, g, sd, device=device, info=info)
+        if "kernel_ms" in info:
+            info["read_bytes"] = int(o[-1] - o[0])
+            info["cons_bytes"] = int(out[1][-1])
+            info["reads"] = int(g[-1])
+            poa_launches.append(info)
+        return out
+
+    consensus_fn = consensus_fn or _gpu_poa
     out_path = path + "/"
     out_tmp = out_path + "/tmp_SS"
     wl = list(white_list_polyA)
@@ -160,16 +203,16 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     if rank == 0:
         gtf.write_polya_bed(out_path + "/polyAWhiteList.bed", poly, wl)
     roots = _roots(out_tmp)
-    # shard loci over ranks: LPT on file size (cost ~ reads x length), results regathered in root order
+    # shard loci over ranks: LPT on the DP-cost estimate of SURVEY.md §8(e), results regathered in root order
     mine = list(range(len(roots)))
     if world > 1:
-        sizes = [os.path.getsize(os.path.join(out_tmp, r + ".psl")) for r in roots]
-        load = [0] * world
-        owner = [0] * len(roots)
-        for i in sorted(range(len(roots)), key=lambda i: -sizes[i]):
+        cost = _locus_costs(out_tmp, roots)
+        load = np.zeros(world)
+        owner = np.zeros(len(roots), dtype=np.int64)
+        for i in np.argsort(-cost, kind="stable"):
             k = int(np.argmin(load))
             owner[i] = k
-            load[k] += sizes[i]
+            load[k] += cost[i]
         mine = [i for i in range(len(roots)) if owner[i] == rank]
     my_roots = [roots[i] for i in mine]
     chroms = [r.split("~")[0] for r in my_roots]
@@ -221,7 +264,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
 
     stats = {"loci": len(roots), "isoforms": 0, "poa_groups": 0, "records": 0, "poa_reads": 0,
              "t_ingest": t1 - t0, "t_cluster": 0.0, "t_pack": 0.0, "t_orient": 0.0, "t_assemble": 0.0,
-             "t_poa": 0.0, "chunks": len(spans)}
+             "t_poa": 0.0, "chunks": len(spans), "poa_launches": poa_launches}
     payloads = []
     timeline = []
     stats["timeline"] = timeline
@@ -294,7 +337,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         payloads += [f.result() for f in pending]
     payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
     if world > 1:
-        payload = _gather(payload, rank, world)
+        payload = _gather(payload, comm)
     if rank == 0:
         order = np.argsort(payload["iso_root"], kind="stable")   # sorted roots x IsoDict order
         mo = payload["mem_off"]
@@ -317,7 +360,8 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         if "_res" in pl:
             pl["_res"].close()
     if verbose and rank == 0:
-        print("\t" + " ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in stats.items()))
+        print("\t" + " ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in stats.items()
+                               if not isinstance(v, list)))
     return stats
 
 
@@ -373,32 +417,23 @@ def _compact(payload: dict) -> dict:
 _FIELDS = ("iso_root", "c_sel", "c_start", "c_len", "c_rc", "n_start", "n_len", "mem_off")
 
 
-def _gather(payload: dict, rank: int, world: int) -> dict:
-    """Reassembly on rank 0: one all-gather of byte counts, one of padded byte buffers (RCCL over xGMI
-    with the nccl backend, gloo on CPU).  Each rank ships its isoforms' root indices, consensus bytes
-    and member names."""
-    import torch
-    import torch.distributed as dist
-
+def _gather(payload: dict, comm) -> dict:
+    """Reassembly on rank 0: one all-gather of each rank's compacted results (RCCL over
+    xGMI between GPUs, the rendezvous sockets on CPU).  Each rank ships its isoforms' root indices,
+    consensus bytes and member names; only rank 0 unpacks them for the writer."""
     p = _compact(payload)
     arrays = [np.ascontiguousarray(p[f]) for f in _FIELDS] + [p["cons"][0], p["cons"][1], p["names"]]
     hdr = np.array([a.nbytes for a in arrays] + [a.dtype.num for a in arrays], dtype=np.int64)
     blob = np.concatenate([hdr.view(np.uint8)] + [a.view(np.uint8).ravel() for a in arrays])
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
-    n = torch.tensor([blob.size], dtype=torch.int64, device=dev)
-    ns = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(ns, n)
-    mx = int(max(int(x.item()) for x in ns))
-    buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    buf[:blob.size] = torch.from_numpy(blob).to(dev)
-    bufs = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(bufs, buf)
-    if rank != 0:
+    allb, counts = comm.allgather_bytes(blob)
+    if comm.rank != 0:
         return payload
     parts = []
     na = len(arrays)
-    for k in range(world):
-        raw = bufs[k][: int(ns[k].item())].cpu().numpy()
+    base = 0
+    for k in range(comm.world):
+        raw = allb[base:base + int(counts[k])]
+        base += int(counts[k])
         h = raw[: 16 * na].view(np.int64)
         sizes, kinds = h[:na], h[na:]
         pos = 16 * na
@@ -477,26 +512,21 @@ def main(argv: list[str] | None = None) -> int:
         ap.print_help()
         return 0
     a = ap.parse_args(argv)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    if world > 1:
-        import torch
-        import torch.distributed as dist
+    comm = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        from .comm import Comm
 
-        if torch.cuda.is_available():
-            torch.cuda.set_device(a.device)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", a.device))
-        else:
-            dist.init_process_group("gloo")
-    define_isoforms(a.path, cutoff=float(a.cutoff), genome_file=a.genome_file, splice_site_width=int(a.splice_site_width),
-                    minimum_read_count=int(a.minimum_read_count), white_list_polyA=a.white_list_polyA.split(","),
-                    threads=int(a.numThreads), junctions=a.junctions, upstream_buffer=int(a.upstream_buffer),
-                    downstream_buffer=int(a.downstream_buffer), seed=a.seed, device=a.device, rank=rank,
-                    world=world, verbose=True)
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.destroy_process_group()
+        comm = Comm.from_env(device=a.device)
+    try:
+        define_isoforms(a.path, cutoff=float(a.cutoff), genome_file=a.genome_file,
+                        splice_site_width=int(a.splice_site_width), minimum_read_count=int(a.minimum_read_count),
+                        white_list_polyA=a.white_list_polyA.split(","), threads=int(a.numThreads),
+                        junctions=a.junctions, upstream_buffer=int(a.upstream_buffer),
+                        downstream_buffer=int(a.downstream_buffer), seed=a.seed, device=a.device, comm=comm,
+                        verbose=True)
+    finally:
+        if comm is not None:
+            comm.close()
     return 0
 
 

@@ -68,7 +68,32 @@ def main(argv: list[str] | None = None) -> int:
         log.write(f'\nMandalorion "{VERSION}" was run on {strftime("%Y-%m-%d %H:%M:%S", localtime())}\n'
                   f"with the following parameters\n{str(a).replace('Namespace(', '').replace(')', '')}\n")
     os.makedirs(temp_path, exist_ok=True)
-    for mod in a.Modules:
+    # The reference runs its modules in a fixed order whatever the order of the -M string
+    # (Mando.py:270-475).  Under a multi-rank launch (WORLD_SIZE > 1) only the D module is sharded:
+    # P, F and Q run on rank 0 alone, and every rank waits for P before D reads tmp_SS.
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    comm = None
+    if world > 1:
+        from .comm import Comm
+
+        comm = Comm.from_env()
+    try:
+        _run_modules(a, path, temp_path, fasta_list, comm, rank)
+    finally:
+        if comm is not None:
+            comm.close()
+    return 0
+
+
+def _run_modules(a, path: str, temp_path: str, fasta_list: list, comm, rank: int) -> None:
+    for mod in "APDFQ":
+        if mod not in a.Modules:
+            continue
+        if mod == "D" and comm is not None:
+            comm.barrier()  # module P (rank 0) has written tmp_SS
+        if rank != 0 and mod != "D":
+            continue
         if mod == "P":
             # module P (Mando.py:323-358): SAM -> PSL (emtrey -m), clean_psl, sort + locus split, all native
             import shutil
@@ -162,29 +187,19 @@ def main(argv: list[str] | None = None) -> int:
             continue
         from . import define
 
-        world = int(os.environ.get("WORLD_SIZE", "1"))
-        rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        if world > 1:
-            import torch
-            import torch.distributed as dist
-
-            if torch.cuda.is_available():
-                torch.cuda.set_device(local)
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            else:
-                dist.init_process_group("gloo")
         define.define_isoforms(temp_path, cutoff=0.1, genome_file=a.genome_annotation,
                                splice_site_width=int(a.splice_site_window),
                                minimum_read_count=int(a.minimum_feature_count),
                                white_list_polyA=a.white_list_polyA.split(","), threads=int(a.minimap2_threads),
                                junctions=a.junctions, upstream_buffer=int(a.upstream_buffer),
-                               downstream_buffer=int(a.downstream_buffer), seed=a.seed, device=local,
-                               rank=rank, world=world, verbose=True)
-        if world > 1:
-            import torch.distributed as dist
+                               downstream_buffer=int(a.downstream_buffer), seed=a.seed, device=local, comm=comm,
+                               verbose=True)
+        if rank == 0:
+            # Mando.py:400: the read -> isoform table is also kept next to the outputs
+            import shutil
 
-            dist.destroy_process_group()
+            shutil.copy(temp_path + "/reads2isoforms.txt", path + "Mando_isoforms.read_stat.txt")
     return 0
 
 

@@ -26,6 +26,10 @@ def orient_batch(groups: Sequence[Sequence[str | bytes]], device: int = 0, max_h
     sbuf = np.frombuffer(seqs, dtype=np.uint8) if seqs else np.zeros(1, dtype=np.uint8)
     _lib.check(ctx.lib.mando_orient_batch(ctx.handle, _lib.ptr(sbuf), _lib.ptr(seq_off), _lib.ptr(grp_off),
                                           len(groups), _lib.ptr(hits), max_hits, _lib.ptr(nh)))
+    if n and int(nh[:n].max()) > max_hits:  # more primaries than max_hits: re-run with room for 8
+        if max_hits >= 8:
+            raise RuntimeError("a read has more than 8 primary hits")
+        return orient_batch(groups, max_hits=8)
     out, r = [], 0
     for g in groups:
         gl = []

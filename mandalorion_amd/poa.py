@@ -75,9 +75,10 @@ def poa_consensus_batch(
 
 
 def poa_consensus_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, seeding=None,
-                         device: int = 0, params: _lib.PoaParams | None = None):
+                         device: int = 0, params: _lib.PoaParams | None = None, info: dict | None = None):
     """Packed form (no per-read Python objects): uint8 reads + int64 offsets in, consensus bytes
-    (uint8) + int64 offsets (n_groups+1) out."""
+    (uint8) + int64 offsets (n_groups+1) out.  `info`, when given, receives the launch facts the
+    roofline needs: DP cells, kernel milliseconds (HIP events on the ctx stream) and launch count."""
     ctx = _lib.context(device)
     p = params or _lib.PoaParams.defaults()
     n = int(len(grp_off)) - 1
@@ -90,8 +91,13 @@ def poa_consensus_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndar
     cap = int(seq_off[-1] - seq_off[0]) * 2 + 1024
     cons = np.empty(cap, dtype=np.uint8)   # written up to cons_off[-1]; untouched pages stay unmapped
     cons_off = np.zeros(n + 1, dtype=np.int64)
+    cells = np.zeros(max(n, 1), dtype=np.int64) if info is not None else None
     if n > 0:
         _lib.check(ctx.lib.mando_poa_batch(ctx.handle, _lib.ctypes.byref(p), _lib.ptr(seqs), _lib.ptr(seq_off),
                                            _lib.ptr(grp_off), n, _lib.ptr(seed_arr), _lib.ptr(cons), cap,
-                                           _lib.ptr(cons_off), None))
+                                           _lib.ptr(cons_off), _lib.ptr(cells)))
+        if info is not None:
+            info["cells"] = int(cells[:n].sum())
+            info["kernel_ms"] = ctx.last_kernel_ms()
+            info["launches"] = ctx.last_kernel_launches()
     return cons[:int(cons_off[-1])], cons_off

@@ -149,20 +149,22 @@ def unpack_groups(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, gr
 def write_loci(tmp_ss: str, n_loci: int, reads: tuple[int, int] = (50, 50), exons: tuple[int, int] = (5, 12),
                exon_len: tuple[int, int] = (150, 400), intron_len: tuple[int, int] = (300, 3000),
                isoforms: tuple[int, int] = (1, 3), seed: int = DATA_SEED, model: dict = R2C2,
-               threads: int = 0) -> int:
+               threads: int = 0, pacbio_frac: float = 0.0, rev_frac: float = 0.0) -> int:
     """Benchmark-scale locus PSL files (libmando_synth mando_synth_loci, same format as simdata.py) into
-    tmp_ss; returns the number of PSL records written."""
+    tmp_ss; returns the number of PSL records written.  pacbio_frac of the reads use the PacBio error
+    rates (config 4's mix); rev_frac of them are '-' strand records (reverse-complemented read)."""
     import ctypes
     import os
 
     lib = _synth_lib()
     lib.mando_synth_loci.restype = ctypes.c_int64
     lib.mando_synth_loci.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int64] + [ctypes.c_int32] * 10 + \
-        [ctypes.c_double] * 3 + [ctypes.c_int]
+        [ctypes.c_double] * 8 + [ctypes.c_int]
     os.makedirs(tmp_ss, exist_ok=True)
     n = lib.mando_synth_loci(tmp_ss.encode(), seed, n_loci, reads[0], reads[1], exons[0], exons[1], exon_len[0],
                              exon_len[1], intron_len[0], intron_len[1], isoforms[0], isoforms[1], model["sub"],
-                             model["ins"], model["dele"], threads)
+                             model["ins"], model["dele"], pacbio_frac, PACBIO["sub"], PACBIO["ins"],
+                             PACBIO["dele"], rev_frac, threads)
     if n < 0:
         raise RuntimeError(f"mando_synth_loci failed: {n}")
     return int(n)

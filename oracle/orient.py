@@ -50,11 +50,15 @@ def orient_batch(groups: Sequence[Sequence[str]], max_hits: int = 4) -> list[lis
                               max_hits, nh.ctypes.data)
     if rc != 0:
         raise RuntimeError(f"orient_ref_batch failed: {rc}")
+    if n and int(nh[:n].max()) > max_hits:  # more primaries than max_hits: re-run with room for 8
+        if max_hits >= 8:
+            raise RuntimeError("a read has more than 8 primary hits")
+        return orient_batch(groups, max_hits=8)
     out, r = [], 0
     for g in groups:
         gl = []
         for _ in g:
-            gl.append([int(x) for x in hits[r * max_hits:r * max_hits + nh[r]]])
+            gl.append([int(x) for x in hits[r * max_hits:r * max_hits + int(nh[r])]])
             r += 1
         out.append(gl)
     return out

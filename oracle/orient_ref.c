@@ -207,7 +207,8 @@ static int orient_one(const uint64_t *ref, int64_t nref, const uint8_t *q, int64
     qsort(ch, (size_t)nch, sizeof(chain_t), cmp_chain);
     int32_t np_ = 0;
     int32_t pqs[64], pqe[64];
-    for (int32_t c = 0; c < nch && np_ < max_hits && np_ < 64; ++c) {
+    /* one primary past max_hits is still counted: *n_hits == max_hits + 1 reports the overflow */
+    for (int32_t c = 0; c < nch && np_ <= max_hits && np_ < 64; ++c) {
         const int32_t qs = ch[c].rev ? (int32_t)qlen - ch[c].ye : ch[c].ys;
         const int32_t qe = ch[c].rev ? (int32_t)qlen - ch[c].ys : ch[c].ye;
         int prim = 1;
@@ -219,7 +220,7 @@ static int orient_one(const uint64_t *ref, int64_t nref, const uint8_t *q, int64
         if (!prim) continue;
         pqs[np_] = qs;
         pqe[np_] = qe;
-        hits[np_] = ch[c].rev ? -1 : 1;
+        if (np_ < max_hits) hits[np_] = ch[c].rev ? -1 : 1;
         ++np_;
     }
     *n_hits = np_;

@@ -79,7 +79,7 @@ def consensus_batch(groups: Sequence[Sequence[str]], params: Params | None = Non
     return (cons, cells[:n].copy()) if return_cells else cons
 
 
-def consensus_packed(seqs, seq_off, grp_off, params: Params | None = None):
+def consensus_packed(seqs, seq_off, grp_off, params: Params | None = None, seeding=None):
     """Packed form of consensus_batch (mirrors mandalorion_amd.poa.poa_consensus_packed)."""
     lib = load()
     p = params or Params.defaults()
@@ -92,9 +92,11 @@ def consensus_packed(seqs, seq_off, grp_off, params: Params | None = None):
     cap = int(seq_off[-1] - seq_off[0]) * 2 + 1024
     out = np.zeros(cap, dtype=np.uint8)
     cons_off = np.zeros(n + 1, dtype=np.int64)
+    sd = None if seeding is None else np.ascontiguousarray(np.asarray(seeding, dtype=np.uint8))
     if n > 0:
         rc = lib.poa_ref_batch(ctypes.addressof(p), seqs.ctypes.data, seq_off.ctypes.data, grp_off.ctypes.data, n,
-                               None, out.ctypes.data, cap, cons_off.ctypes.data, None)
+                               None if sd is None else sd.ctypes.data, out.ctypes.data, cap, cons_off.ctypes.data,
+                               None)
         if rc != 0:
             raise RuntimeError(f"poa_ref_batch failed: {rc}")
     return out, cons_off

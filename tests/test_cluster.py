@@ -148,24 +148,22 @@ def _free_port():
 
 
 def _rank_main(rank, world, port, d, gtf_path, seed, q):
-    import torch.distributed as dist
+    from mandalorion_amd.comm import Comm
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm(world, rank, "127.0.0.1", port)  # host transport (no device context)
     try:
         st = define.define_isoforms(d, cutoff=P["cutoff"], genome_file=gtf_path, splice_site_width=P["splice_site_width"],
                                     minimum_read_count=P["minimum_read_count"],
                                     white_list_polyA=P["white_list_polyA"].split(","), threads=2,
                                     junctions=P["junctions"], upstream_buffer=P["upstream_buffer"],
                                     downstream_buffer=P["downstream_buffer"], seed=seed, orient_fn=_stub_orient,
-                                    consensus_fn=lambda s, o, g, sd: _first_of_groups(s, o, g), rank=rank,
-                                    world=world)
-        q.put((rank, st["loci"], st["isoforms"]))
+                                    consensus_fn=lambda s, o, g, sd: _first_of_groups(s, o, g), comm=comm)
+        q.put((rank, st["loci"], st["isoforms"], comm.backend))
     finally:
-        dist.destroy_process_group()
+        comm.close()
 
 
-def test_sharded_two_ranks_gloo(dataset, tmp_path):
+def test_sharded_two_ranks_host_comm(dataset, tmp_path):
     """Loci sharded over 2 ranks (LPT on file size), gathered on rank 0: output identical to 1 rank."""
     import multiprocessing as mp
 
@@ -185,6 +183,7 @@ def test_sharded_two_ranks_gloo(dataset, tmp_path):
         p.join(120)
         assert p.exitcode == 0
     got = sorted(q.get() for _ in range(2))
+    assert got[0][3] == got[1][3] == "host"
     assert got[0][2] + got[1][2] == len(exp["isoform_headers"])  # isoforms split across ranks
     assert got[0][2] > 0 and got[1][2] > 0
     sha = lambda f: hashlib.sha256(open(os.path.join(d, f), "rb").read()).hexdigest()

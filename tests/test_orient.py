@@ -42,6 +42,43 @@ def test_oracle_edge_cases():
     assert res[1] == [[], [], []]
 
 
+def _chimera_group():
+    """A query made of the reference's two halves, the second one reverse-complemented: two primary
+    hits (one per strand), which the reference writes twice (SpliceDefineConsensus.py:902-907)."""
+    rng = np.random.default_rng(41)
+    a = "".join(rng.choice(list("ACGT"), 1500))
+    b = "".join(rng.choice(list("ACGT"), 1500))
+    return [a + b, a + synth.revcomp(b), a + b]
+
+
+def test_oracle_counts_primaries_past_max_hits():
+    from oracle import orient as oref
+
+    g = [_chimera_group()]
+    lib = oref.load()
+    raw = "".join(g[0]).encode()
+    so = np.cumsum([0] + [len(s) for s in g[0]]).astype(np.int64)
+    go = np.array([0, 3], dtype=np.int64)
+    hits = np.zeros(3, dtype=np.int8)
+    nh = np.zeros(3, dtype=np.int32)
+    buf = np.frombuffer(raw, dtype=np.uint8)
+    assert lib.orient_ref_batch(buf.ctypes.data, so.ctypes.data, go.ctypes.data, 1, hits.ctypes.data, 1,
+                                nh.ctypes.data) == 0
+    assert nh.tolist() == [1, 2, 1]  # 2 = max_hits + 1: overflow reported, not truncated
+    res = oref.orient_batch(g, max_hits=1)  # re-run with room for 8
+    assert sorted(res[0][1]) == [-1, 1] and res[0][0] == [1] and res[0][2] == [1]
+
+
+@pytest.mark.gpu
+def test_orient_gpu_reports_extra_primaries(gpu_ctx):
+    from mandalorion_amd import orient
+    from oracle import orient as oref
+
+    g = [_chimera_group()] + _groups(5, 3)[0]
+    assert orient.orient_batch(g, max_hits=1) == oref.orient_batch(g, max_hits=1)
+    assert sorted(orient.orient_batch(g, max_hits=1)[0][1]) == [-1, 1]
+
+
 @pytest.mark.gpu
 def test_orient_gpu_matches_oracle(gpu_ctx):
     from mandalorion_amd import orient
