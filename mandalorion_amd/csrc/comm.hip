@@ -6,8 +6,8 @@
 //   * rendezvous: a TCP star — rank 0 listens on addr:port, the other ranks connect and announce
 //     their rank.  This is how the ncclUniqueId travels (rank 0 draws it, the star ships it).
 //   * data: RCCL over xGMI when the communicator is bound to a device context (one process per GPU);
-//     RCCL has no allgatherv, so the byte all-gather is one ncclGroup of per-root ncclBroadcast calls
-//     straight into each rank's slice of the receive buffer (no padding to the largest rank).
+//     RCCL has no allgatherv, so the byte all-gather is one ncclAllGather of every rank's bytes padded
+//     to the largest rank's count (the byte counts travel first), compacted on the way to the host.
 //   * host mode (ctx == NULL): the star itself carries the bytes (CPU-only runs and tests).
 // Byte counts, barriers and the max-over-ranks timing reduction always use the star (tiny messages).
 #include <arpa/inet.h>
@@ -297,23 +297,24 @@ int mando_allgather_bytes(mando_comm *c, const uint8_t *send, int64_t n, uint8_t
         if (tot > 0) memcpy(recv, all.data(), (size_t)tot);
         return MANDO_OK;
     }
+    // RCCL has no allgatherv: one ncclAllGather of every rank's bytes padded to the largest count
+    // (SURVEY.md §8(e)), then each rank's slice is compacted on the way back to the host
     if (hipSetDevice(c->device) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: hipSetDevice failed");
-    int rc = ensure_dev(&c->dsend, &c->dsend_cap, (size_t)std::max<int64_t>(n, 1));
-    if (!rc) rc = ensure_dev(&c->drecv, &c->drecv_cap, (size_t)std::max<int64_t>(tot, 1));
+    int64_t maxc = 1;
+    for (int r = 0; r < R; ++r) maxc = std::max(maxc, recv_counts[r]);
+    int rc = ensure_dev(&c->dsend, &c->dsend_cap, (size_t)maxc);
+    if (!rc) rc = ensure_dev(&c->drecv, &c->drecv_cap, (size_t)maxc * (size_t)R);
     if (rc) return rc;
     if (n > 0 && hipMemcpyAsync(c->dsend, send, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return mando::set_error(MANDO_E_HIP, "comm: H2D copy failed");
-    ncclResult_t r = ncclGroupStart();
-    for (int root = 0; root < R && r == ncclSuccess; ++root) {
+    const ncclResult_t r = ncclAllGather(c->dsend, c->drecv, (size_t)maxc, ncclUint8, c->nccl, c->stream);
+    if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
+    for (int root = 0; root < R; ++root) {
         if (recv_counts[root] == 0) continue;
-        r = ncclBroadcast(c->dsend, static_cast<uint8_t *>(c->drecv) + off[(size_t)root], (size_t)recv_counts[root],
-                          ncclUint8, root, c->nccl, c->stream);
+        if (hipMemcpyAsync(recv + off[(size_t)root], static_cast<uint8_t *>(c->drecv) + (size_t)root * (size_t)maxc,
+                           (size_t)recv_counts[root], hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+            return mando::set_error(MANDO_E_HIP, "comm: D2H copy failed");
     }
-    const ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return nccl_fail(r, "ncclBroadcast");
-    if (r2 != ncclSuccess) return nccl_fail(r2, "ncclGroupEnd");
-    if (tot > 0 && hipMemcpyAsync(recv, c->drecv, (size_t)tot, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-        return mando::set_error(MANDO_E_HIP, "comm: D2H copy failed");
     if (hipStreamSynchronize(c->stream) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: stream sync failed");
     return MANDO_OK;
 }

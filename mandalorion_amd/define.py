@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import os
 import sys
+import threading
 import time
 from typing import Callable, Sequence
 
@@ -51,10 +52,10 @@ def gpu_orient(seqs, seq_off, grp_off, device: int = 0, max_hits: int = 4):
     return hits, nh
 
 
-def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0, info: dict | None = None):
+def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0, info: dict | None = None, slot: int = 0):
     from . import poa
 
-    return poa.poa_consensus_packed(seqs, seq_off, grp_off, seeding=seeding, device=device, info=info)
+    return poa.poa_consensus_packed(seqs, seq_off, grp_off, seeding=seeding, device=device, info=info, slot=slot)
 
 
 def _roots(out_tmp: str) -> list[str]:
@@ -183,9 +184,16 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     orient_fn = orient_fn or (lambda s, o, g: gpu_orient(s, o, g, device=device))
     poa_launches = []  # per POA call: DP cells, kernel ms, read + consensus bytes (the roofline's inputs)
 
+    poa_slots: dict = {}
+    slot_lock = threading.Lock()
+
     def _gpu_poa(s, o, g, sd):
+        # one device context (stream + buffers) per POA host thread: slots 0 and 3 (1: orientation)
+        tid = threading.get_ident()
+        with slot_lock:
+            slot = poa_slots.setdefault(tid, 3 * len(poa_slots))
         info = {}
-        out = gpu_consensus(s, o, g, sd, device=device, info=info)
+        out = gpu_consensus(s, o, g, sd, device=device, info=info, slot=slot)
         if "kernel_ms" in info:
             info["read_bytes"] = int(o[-1] - o[0])
             info["cons_bytes"] = int(out[1][-1])
@@ -280,60 +288,51 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         asm = Assembly(res, hits, n_hits)
         prep = (asm,) + tuple(asm.poa_input())
         te = time.perf_counter()
-        stats["t_assemble"] += te - ta
+        add("t_assemble", te - ta)
         timeline.append(("assemble", ta - t0, te - t0))
         return prep
 
-    # The main thread issues the GPU work in the order orientation(k+1), POA(k) once chunk k+1 is
-    # clustered (waiting for it, except for the first chunk): chunk k+1's emission assembly (host) then
-    # overlaps chunk k's POA kernel, and no kernel waits behind the persistent POA grid.  The first
-    # chunk's POA does not wait for the second chunk's clustering.
-    # Clustering + packing of chunk k+2 runs on its own thread meanwhile; compaction of finished chunks
-    # on another.
+    # Staged pipeline over chunks: clustering (one host thread driving the C++ pool, chunks in order) ->
+    # orientation (main thread, GPU slot 1) -> emission assembly (host thread) -> POA (two host threads,
+    # GPU slots 0 and 3: chunk k+1's POA kernel is queued while chunk k's persistent grid drains, so
+    # its waves fill the CUs chunk k's tail leaves idle) -> compaction (host thread).
+    lock = threading.Lock()
+
+    def add(key, v):
+        with lock:
+            stats[key] += v
+
+    def poa_job(res, asm_fut, lo, hi):
+        prep = asm_fut.result()
+        tp = time.perf_counter()
+        pl = _poa_chunk(res, mine[lo:hi], prep, consensus_fn, stats, lock)
+        timeline.append(("poa", tp - t0, time.perf_counter() - t0))
+        return pl, res
+
+    n_poa = 2 if len(spans) > 1 else 1
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
-            ThreadPoolExecutor(max_workers=1) as post:
-        def orient(c):
-            res, tcl, (o_seqs, o_off), tpk = c
-            stats["t_cluster"] += tcl
-            stats["t_pack"] += tpk
+            ThreadPoolExecutor(max_workers=n_poa) as gpu_poa, ThreadPoolExecutor(max_workers=1) as post:
+        cl = [ex.submit(run_cluster, lo, hi) for lo, hi in spans]
+        poa_futs = []
+        for k, (lo, hi) in enumerate(spans):
+            res, tcl, (o_seqs, o_off), tpk = cl[k].result()
+            add("t_cluster", tcl)
+            add("t_pack", tpk)
             tg = time.perf_counter()
             hits, n_hits = orient_fn(o_seqs, o_off, res.sub_off)
             te = time.perf_counter()
             timeline.append(("orient", tg - t0, te - t0))
-            stats["t_orient"] += te - tg
-            return res, host.submit(assemble, res, hits, n_hits)
-
-        fut = ex.submit(run_cluster, *spans[0])
-        c = fut.result()
-        if len(spans) > 1:
-            fut = ex.submit(run_cluster, *spans[1])
-        cur = orient(c)
+            add("t_orient", te - tg)
+            asm_fut = host.submit(assemble, res, hits, n_hits)
+            poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
         pending = []
-
-        def take_next(k):
-            nonlocal fut
-            c = fut.result()
-            if k + 2 < len(spans):
-                fut = ex.submit(run_cluster, *spans[k + 2])
-            return orient(c)
-
-        for k, (lo, hi) in enumerate(spans):
-            nxt = None
-            if k + 1 < len(spans) and (k > 0 or fut.done()):
-                nxt = take_next(k)
-            res, asm_fut = cur
-            prep = asm_fut.result()
-            tp = time.perf_counter()
-            pl = _poa_chunk(res, mine[lo:hi], prep, consensus_fn, stats)
-            timeline.append(("poa", tp - t0, time.perf_counter() - t0))
+        for f in poa_futs:
+            pl, res = f.result()
             if len(spans) > 1:
                 pending.append(post.submit(compact_close, pl, res))
             else:
                 pl["_res"] = res
                 payloads.append(pl)
-            if k + 1 < len(spans) and nxt is None:
-                nxt = take_next(k)
-            cur = nxt
         payloads += [f.result() for f in pending]
     payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
     if world > 1:
@@ -365,7 +364,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     return stats
 
 
-def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, consensus_fn, stats: dict):
+def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, consensus_fn, stats: dict, lock):
     """POA of one oriented chunk; returns its writer payload."""
     asm, p_seqs, p_off, p_grp = prep
     t3 = time.perf_counter()
@@ -386,11 +385,12 @@ def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, consen
     c_start[pi] = cons_off[:-1][use]
     c_len[pi] = plen[use]
     c_rc[pi] = 0
-    stats["isoforms"] += n_iso
-    stats["poa_groups"] += int(len(asm.poa_iso))
-    stats["records"] += int(res.n_records)
-    stats["poa_reads"] += int(p_grp[-1])
-    stats["t_poa"] += t4 - t3
+    with lock:
+        stats["isoforms"] += n_iso
+        stats["poa_groups"] += int(len(asm.poa_iso))
+        stats["records"] += int(res.n_records)
+        stats["poa_reads"] += int(p_grp[-1])
+        stats["t_poa"] += t4 - t3
     ri = np.asarray(root_idx, dtype=np.int64)
     return dict(iso_root=ri[res.iso_locus] if n_iso else np.zeros(0, np.int64),
                 cons=[res.text, cons], c_sel=c_sel, c_start=c_start, c_len=c_len, c_rc=c_rc,

@@ -75,11 +75,14 @@ def poa_consensus_batch(
 
 
 def poa_consensus_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, seeding=None,
-                         device: int = 0, params: _lib.PoaParams | None = None, info: dict | None = None):
+                         device: int = 0, params: _lib.PoaParams | None = None, info: dict | None = None,
+                         slot: int = 0):
     """Packed form (no per-read Python objects): uint8 reads + int64 offsets in, consensus bytes
     (uint8) + int64 offsets (n_groups+1) out.  `info`, when given, receives the launch facts the
-    roofline needs: DP cells, kernel milliseconds (HIP events on the ctx stream) and launch count."""
-    ctx = _lib.context(device)
+    roofline needs: DP cells, kernel milliseconds (HIP events on the ctx stream) and launch count.
+    `slot` selects the device context (its own stream), so two host threads can keep two launches in
+    flight."""
+    ctx = _lib.context(device, slot)
     p = params or _lib.PoaParams.defaults()
     n = int(len(grp_off)) - 1
     seqs = np.ascontiguousarray(seqs, dtype=np.uint8)

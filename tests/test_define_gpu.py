@@ -41,3 +41,18 @@ def test_define_gpu_equals_cpu_restatement(gpu_ctx, tmp_path):
          consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g))
     assert read("Isoform_Consensi.fasta") == gpu_fa
     assert read("reads2isoforms.txt") == gpu_r2i
+
+
+@pytest.mark.gpu
+def test_define_gpu_chunked_pipeline(gpu_ctx, tmp_path):
+    """Three chunks: two POA launches in flight on two device contexts (slots 0 and 3) while the next
+    chunk is oriented (slot 1); the files must equal the one-chunk run's."""
+    d = str(tmp_path)
+    loci = simdata.make_dataset(simdata.fixture_specs())
+    info = simdata.write_dataset(loci, d)
+    read = lambda f: open(os.path.join(d, f), "rb").read()
+    _run(d, info["gtf"])
+    one = read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")
+    st = _run(d, info["gtf"], n_chunks=3)
+    assert st["chunks"] == 3 and len(st["poa_launches"]) == 3
+    assert (read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")) == one
