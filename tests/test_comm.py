@@ -75,6 +75,6 @@ def test_rccl_backend_single_rank(gpu_ctx):
 
     with Comm(1, 0, device_ctx=gpu_ctx) as c:
         assert c.backend == "rccl"
-        b, cnt = c.allgather_bytes(np.arange(1000, dtype=np.uint8) % 251)
+        b, cnt = c.allgather_bytes((np.arange(1000) % 251).astype(np.uint8))
         assert cnt.tolist() == [1000] and b.tolist() == [i % 251 for i in range(1000)]
         c.barrier()

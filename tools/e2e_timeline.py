@@ -1,17 +1,18 @@
-"""Dev helper: whole D module on N synthetic config-3 loci with the stage timeline (cluster chunks on
-the host worker thread vs orientation+POA chunks on the GPU)."""
-import os, sys, shutil, tempfile, time
+"""Dev helper: whole D module on the bench's config-3 loci with the stage timeline (cluster chunks on
+the host worker thread vs orientation / POA chunks on the GPU).  CHUNKS=<n> fixes the chunk count."""
+import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from mandalorion_amd import define, synth
+import bench
+from mandalorion_amd import define
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
-d = tempfile.mkdtemp(prefix="mando_tl_", dir=os.environ.get("TMPDIR", "/tmp"))
-try:
-    t = time.time(); synth.write_loci(os.path.join(d, "tmp_SS"), n, threads=16); print(f"write {time.time()-t:.1f}s")
-    nc = int(os.environ.get("CHUNKS", "0"))
+d = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mando_bench_config3_{n}")
+os.makedirs(d, exist_ok=True)
+t = time.time(); bench.gen_data(d, bench.WORKLOADS["config3"], n, 16); print(f"data {time.time()-t:.1f}s")
+for nc in [int(x) for x in os.environ.get("CHUNKS", "0").split(",")]:
     define.define_isoforms(d, threads=16, n_chunks=nc)
     st = define.define_isoforms(d, threads=16, n_chunks=nc)
+    print(f"== chunks {st['chunks']}: total {st['t_total']:.3f}")
     for k, v in st.items():
-        if k != "timeline": print(k, v)
+        if not isinstance(v, list): print("  ", k, v)
+    for x in st["poa_launches"]: print("   poa launch", {k: round(v, 3) if isinstance(v, float) else v for k, v in x.items()})
     for name, a, b in sorted(st["timeline"], key=lambda x: x[1]): print(f"  {name:8s} {a:7.3f} -> {b:7.3f} ({b-a:.3f})")
-finally:
-    shutil.rmtree(d, ignore_errors=True)
