@@ -44,12 +44,34 @@ def load():
         P = ctypes.c_void_p
         lib.poa_ref_batch.argtypes = [P, P, P, P, ctypes.c_int64, P, P, ctypes.c_int64, P, P]
         lib.poa_ref_batch.restype = ctypes.c_int
+        lib.poa_ref_seed_partition.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, P, P, ctypes.c_int]
+        lib.poa_ref_seed_partition.restype = ctypes.c_int
         _lib = lib
     return _lib
 
 
+_ENC = np.full(256, 4, dtype=np.uint8)
+for _c, _v in zip(b"ACGTacgt", (0, 1, 2, 3, 0, 1, 2, 3)):
+    _ENC[_c] = _v
+
+
+def seed_partition(t: str, q: str, params: Params | None = None) -> list[tuple[int, int]]:
+    """-S partition anchors (k-mer starts in t, in q) of read q against the previous read t."""
+    lib = load()
+    p = params or Params.defaults()
+    te = _ENC[np.frombuffer(t.encode() or b"N", dtype=np.uint8)]
+    qe = _ENC[np.frombuffer(q.encode() or b"N", dtype=np.uint8)]
+    cap = len(q) // max(1, p.min_w) + 2
+    pt = np.zeros(cap, dtype=np.int32)
+    pq = np.zeros(cap, dtype=np.int32)
+    n = lib.poa_ref_seed_partition(te.ctypes.data, len(t), qe.ctypes.data, len(q), p.k, p.w, p.min_w,
+                                   pt.ctypes.data, pq.ctypes.data, cap)
+    return list(zip(pt[:n].tolist(), pq[:n].tolist()))
+
+
 def consensus_batch(groups: Sequence[Sequence[str]], params: Params | None = None,
-                    return_cells: bool = False):
+                    return_cells: bool = False, seeding: Sequence[bool] | None = None):
     lib = load()
     p = params or Params.defaults()
     parts, lens, grp = [], [], [0]
@@ -69,8 +91,9 @@ def consensus_batch(groups: Sequence[Sequence[str]], params: Params | None = Non
     out = np.zeros(cap, dtype=np.uint8)
     cons_off = np.zeros(n + 1, dtype=np.int64)
     cells = np.zeros(max(n, 1), dtype=np.int64)
+    sd = None if seeding is None else np.asarray([1 if x else 0 for x in seeding], dtype=np.uint8)
     rc = lib.poa_ref_batch(ctypes.addressof(p), seqs.ctypes.data, seq_off.ctypes.data,
-                           grp_off.ctypes.data, n, None, out.ctypes.data, cap,
+                           grp_off.ctypes.data, n, None if sd is None else sd.ctypes.data, out.ctypes.data, cap,
                            cons_off.ctypes.data, cells.ctypes.data)
     if rc != 0:
         raise RuntimeError(f"poa_ref_batch failed: {rc}")

@@ -33,8 +33,8 @@
  * aligned-group tables instead of lists, flag-based traceback instead of score re-comparison), so
  * agreement also checks those design claims.
  *
- * The -S (minimizer seeding) window partition is not restated: seeded groups run the same full
- * adaptive-band DP, exactly like the HIP kernel (DESIGN.md "Known gaps").
+ * -S (minimizer-seeded window partition) is restated below ("-S: ..."), with its reconstructed choices
+ * listed there; also PARITY UNPINNED.
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -235,27 +235,52 @@ static int band_w(const mando_poa_params *p, int qlen) {
     return p->band_b + (int)f;
 }
 
-/* Align one encoded read to the graph and add it (abPOA align + add_graph_alignment).
+/* Banded DP of q[0..qlen) against the subgraph between node B and node E (both included): the rows
+ * are the nodes v with B ~> v ~> E in topological order, B is the source row (row 0) and E the sink
+ * (not a DP row).  remain relative to E: rem(v) = remain[v] - remain[E] - 1 (= remain[v] for E = SINK).
+ * Predecessors outside the subgraph are ignored.  Fills qnode[0..qlen) with the aligned node of every
+ * query position (-1 = inserted).  B = SRC, E = SINK is the whole-graph alignment of the default mode.
  * Returns the number of DP cells evaluated, or -1 on an internal inconsistency. */
-static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const scorer *sc) {
-    int n = g->n;
-    int *order = (int *)malloc(sizeof(int) * (size_t)n);
-    int *pos = (int *)malloc(sizeof(int) * (size_t)n);
-    int *remain = (int *)malloc(sizeof(int) * (size_t)n);
-    if (topo_bfs(g, order, pos) != 0) {
-        free(order);
-        free(pos);
-        free(remain);
-        return -1;
+static int64_t align_window(const graph_t *g, const int *order, const int *pos, const int *remain, int B, int E,
+                            const uint8_t *q, int qlen, const scorer *sc, int *qnode) {
+    const int pB = pos[B], pE = pos[E];
+    if (pE <= pB) return -1;
+    const int span = pE - pB + 1;
+    /* rows: forward reachability from B, backward from E, inside the topological range [pB, pE] */
+    uint8_t *fl = (uint8_t *)calloc((size_t)span, 1);
+    for (int r = pB; r <= pE; ++r) {
+        const int v = order[r];
+        if (v == B) { fl[r - pB] |= 1; continue; }
+        for (int k = 0; k < g->in[v].n; ++k) {
+            const int pu = pos[g->in[v].a[k]];
+            if (pu >= pB && (fl[pu - pB] & 1)) { fl[r - pB] |= 1; break; }
+        }
     }
-    set_remain(g, order, remain);
+    for (int r = pE; r >= pB; --r) {
+        const int v = order[r];
+        if (v == E) { fl[r - pB] |= 2; continue; }
+        for (int k = 0; k < g->out[v].n; ++k) {
+            const int pu = pos[g->out[v].a[k]];
+            if (pu <= pE && pu > r && (fl[pu - pB] & 2)) { fl[r - pB] |= 2; break; }
+        }
+    }
+    int m = 0;
+    int *wrow = (int *)malloc(sizeof(int) * (size_t)span); /* window row of topological row pB + x, -1 if not in */
+    int *rowv = (int *)malloc(sizeof(int) * (size_t)span); /* node of window row */
+    for (int x = 0; x < span; ++x) {
+        wrow[x] = (fl[x] == 3) ? m : -1;
+        if (fl[x] == 3) rowv[m++] = order[pB + x];
+    }
+    free(fl);
+#define WROW(node_) ((pos[node_] >= pB && pos[node_] <= pE) ? wrow[pos[node_] - pB] : -1)
+    const int remE = remain[E];
     int w = band_w(sc->p, qlen);
     const int e1 = sc->p->gap_ext1, e2 = sc->p->gap_ext2, o1 = sc->p->gap_open1,
               o2 = sc->p->gap_open2;
     const int oe1 = sc->oe1, oe2 = sc->oe2;
 
-    rowinfo *ri = (rowinfo *)malloc(sizeof(rowinfo) * (size_t)n);
-    int64_t cap = (int64_t)(n) * (2 * w + 64) + 1024, used = 0;
+    rowinfo *ri = (rowinfo *)malloc(sizeof(rowinfo) * (size_t)m);
+    int64_t cap = (int64_t)(m) * (2 * w + 64) + 1024, used = 0;
     int *H = (int *)malloc(sizeof(int) * (size_t)cap), *H0 = (int *)malloc(sizeof(int) * (size_t)cap);
     int *E1 = (int *)malloc(sizeof(int) * (size_t)cap), *E2 = (int *)malloc(sizeof(int) * (size_t)cap);
     int *F1 = (int *)malloc(sizeof(int) * (size_t)cap), *F2 = (int *)malloc(sizeof(int) * (size_t)cap);
@@ -273,9 +298,10 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
     } while (0)
 
     int64_t cells = 0;
-    /* source row */
+    /* source row (B) */
     {
-        int end = imin(qlen, imax(0, qlen - remain[SRC]) + w);
+        const int remB = remain[B] - remE - 1;
+        int end = imin(qlen, imax(0, qlen - remB) + w);
         ri[0].beg = 0;
         ri[0].end = end;
         ri[0].off = 0;
@@ -302,16 +328,17 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
         cells += end + 1;
     }
 
-    for (int i = 1; i < n - 1; ++i) {
-        int v = order[i];
+    for (int i = 1; i < m - 1; ++i) {
+        int v = rowv[i];
         const ivec *in = &g->in[v];
         int posL = 2147483647, posR = -2147483647 - 1;
         for (int k = 0; k < in->n; ++k) {
-            int pr = pos[in->a[k]];
+            int pr = WROW(in->a[k]);
+            if (pr < 0) continue;
             posL = imin(posL, ri[pr].argmax + 1);
             posR = imax(posR, ri[pr].argmax + 1);
         }
-        int x = qlen - remain[v];
+        int x = qlen - (remain[v] - remE - 1);
         int beg = imax(0, imin(posL, x) - w);
         int end = imin(qlen, imax(posR, x) + w);
         int width = end - beg + 1;
@@ -328,7 +355,8 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
             int64_t c = o + (j - beg);
             int mv = NEG_INF, e1in = NEG_INF, e2in = NEG_INF;
             for (int k = 0; k < in->n; ++k) {
-                int pr = pos[in->a[k]];
+                int pr = WROW(in->a[k]);
+                if (pr < 0) continue;
                 const rowinfo *pi = &ri[pr];
                 if (j - 1 >= pi->beg && j - 1 <= pi->end) mv = imax(mv, H[pi->off + (j - 1 - pi->beg)]);
                 if (j >= pi->beg && j <= pi->end) {
@@ -337,8 +365,8 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
                 }
             }
             int s = (j >= 1) ? sc->mat[vb][q[j - 1]] : 0;
-            int m = mv + s;
-            int h0 = imax(m, imax(e1in, e2in));
+            int mm = mv + s;
+            int h0 = imax(mm, imax(e1in, e2in));
             int f1, f2;
             if (j == beg) {
                 f1 = NEG_INF;
@@ -362,10 +390,11 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
         ri[i].argmax = besti;
     }
 
-    /* global end: best predecessor of the sink at column qlen */
+    /* end: best predecessor of E at column qlen (first in in-edge order on ties) */
     int bi = -1, bs = -2147483647 - 1;
-    for (int k = 0; k < g->in[SINK].n; ++k) {
-        int pr = pos[g->in[SINK].a[k]];
+    for (int k = 0; k < g->in[E].n; ++k) {
+        int pr = WROW(g->in[E].a[k]);
+        if (pr < 0) continue;
         if (qlen < ri[pr].beg || qlen > ri[pr].end) continue;
         int h = H[ri[pr].off + (qlen - ri[pr].beg)];
         if (h > bs) {
@@ -373,40 +402,26 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
             bi = pr;
         }
     }
-    if (bi < 0) {
-        free(order); free(pos); free(remain); free(ri);
-        free(H); free(H0); free(E1); free(E2); free(F1); free(F2);
-        return -1;
-    }
+    int fail = 0;
+    if (bi < 0) fail = 1;
 
-    /* backtrack by score comparison (abPOA style); ops recorded in reverse */
-    int opcap = qlen + n + 16, nops = 0;
-    int *opk = (int *)malloc(sizeof(int) * (size_t)opcap);
-    int *opn = (int *)malloc(sizeof(int) * (size_t)opcap);
-    int *opq = (int *)malloc(sizeof(int) * (size_t)opcap);
-#define PUSHOP(k_, n_, q_)   \
-    do {                     \
-        opk[nops] = (k_);    \
-        opn[nops] = (n_);    \
-        opq[nops] = (q_);    \
-        ++nops;              \
-    } while (0)
+    /* backtrack by score comparison (abPOA style) */
 #define CELL(r_, col_) (ri[r_].off + ((col_)-ri[r_].beg))
     int i = bi, j = qlen;
     enum { ST_H = 0, ST_E1, ST_E2, ST_F1, ST_F2 } st = ST_H;
-    int fail = 0;
-    while (i > 0 && j > 0) {
-        int v = order[i];
+    while (!fail && i > 0 && j > 0) {
+        int v = rowv[i];
         const ivec *in = &g->in[v];
         if (st == ST_H) {
             int hcur = H[CELL(i, j)];
             int s = sc->mat[g->base[v]][q[j - 1]];
             int hit = 0;
             for (int k = 0; k < in->n && !hit; ++k) {
-                int pr = pos[in->a[k]];
+                int pr = WROW(in->a[k]);
+                if (pr < 0) continue;
                 if (j - 1 < ri[pr].beg || j - 1 > ri[pr].end) continue;
                 if (H[CELL(pr, j - 1)] + s == hcur) {
-                    PUSHOP(OP_M, v, j - 1);
+                    qnode[j - 1] = v;
                     i = pr;
                     --j;
                     hit = 1;
@@ -414,16 +429,15 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
             }
             if (hit) continue;
             for (int k = 0; k < in->n && !hit; ++k) {
-                int pr = pos[in->a[k]];
+                int pr = WROW(in->a[k]);
+                if (pr < 0) continue;
                 if (j < ri[pr].beg || j > ri[pr].end) continue;
                 int64_t pc = CELL(pr, j);
                 if (E1[pc] == hcur) {
-                    PUSHOP(OP_D, v, -1);
                     st = (H[pc] - oe1 == E1[pc]) ? ST_H : ST_E1;
                     i = pr;
                     hit = 1;
                 } else if (E2[pc] == hcur) {
-                    PUSHOP(OP_D, v, -1);
                     st = (H[pc] - oe2 == E2[pc]) ? ST_H : ST_E2;
                     i = pr;
                     hit = 1;
@@ -443,9 +457,9 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
             int64_t cc = CELL(i, j);
             int want = (st == ST_E1) ? E1[cc] + e1 : E2[cc] + e2;
             int hit = 0;
-            PUSHOP(OP_D, v, -1);
             for (int k = 0; k < in->n && !hit; ++k) {
-                int pr = pos[in->a[k]];
+                int pr = WROW(in->a[k]);
+                if (pr < 0) continue;
                 if (j < ri[pr].beg || j > ri[pr].end) continue;
                 int64_t pc = CELL(pr, j);
                 if (st == ST_E1 && E1[pc] == want) {
@@ -466,7 +480,7 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
         }
         if (st == ST_F1 || st == ST_F2) {
             int64_t cc = CELL(i, j);
-            PUSHOP(OP_I, -1, j - 1);
+            qnode[j - 1] = -1;
             if (st == ST_F1) {
                 if (H0[cc - 1] - oe1 == F1[cc])
                     st = ST_H;
@@ -489,35 +503,32 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
             --j;
         }
     }
-    int lead_ins = j;
+    for (int t = 0; t < j && !fail; ++t) qnode[t] = -1; /* leading insertions (right after B) */
     free(H); free(H0); free(E1); free(E2); free(F1); free(F2);
     free(ri);
-    free(order); free(pos); free(remain);
-    if (fail) {
-        free(opk); free(opn); free(opq);
-        return -1;
-    }
+    free(wrow);
+    free(rowv);
+    return fail ? -1 : cells;
+#undef GROW
+#undef CELL
+#undef WROW
+}
 
-    /* graph update, forward order: leading insertions then the reversed op list */
+/* Graph update from the per-position path (abPOA add_graph_alignment): query position t joins node
+ * qnode[t] (match: that node; mismatch: the aligned node of the same base, else a new aligned node) or
+ * becomes a new node (qnode[t] = -1); consecutive positions are linked from SRC to SINK, edge weight +1.
+ * tnode (optional) receives the node each position ended up on. */
+static void apply_path(graph_t *g, const uint8_t *q, int qlen, const int *qnode, int *tnode) {
     int last = SRC, last_new = 0;
-    for (int t = 0; t < lead_ins; ++t) {
-        int nw = g_add_node(g, q[t]);
-        g_add_edge(g, last, nw, 0);
-        last = nw;
-        last_new = 1;
-    }
-    for (int t = nops - 1; t >= 0; --t) {
-        if (opk[t] == OP_D) continue;
-        if (opk[t] == OP_I) {
-            int nw = g_add_node(g, q[opq[t]]);
+    for (int t = 0; t < qlen; ++t) {
+        const int node = qnode[t];
+        const uint8_t b = q[t];
+        if (node < 0) {
+            int nw = g_add_node(g, b);
             g_add_edge(g, last, nw, 0);
             last = nw;
             last_new = 1;
-            continue;
-        }
-        int node = opn[t];
-        uint8_t b = q[opq[t]];
-        if (g->base[node] == b) {
+        } else if (g->base[node] == b) {
             g_add_edge(g, last, node, !last_new);
             last = node;
             last_new = 0;
@@ -535,13 +546,176 @@ static int64_t align_and_add(graph_t *g, const uint8_t *q, int qlen, const score
                 last_new = 1;
             }
         }
+        if (tnode) tnode[t] = last;
     }
     g_add_edge(g, last, SINK, !last_new);
-    free(opk); free(opn); free(opq);
-    return cells;
-#undef GROW
-#undef PUSHOP
-#undef CELL
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * -S: minimizer-seeded window partition (abPOA v1.4.1 `-S`, SpliceDefineConsensus.py:915-919 when the
+ * median subsample length is >= 8000).  Restated from abPOA's published description (seeding with
+ * (k, w) minimizers, anchors chained by a longest increasing subsequence, the read split at anchors at
+ * least min_w apart, each window aligned to the subgraph between its bounding anchor nodes, the whole
+ * read's path added to the graph at once).  PARITY UNPINNED; the choices below are this restatement's
+ * and the HIP kernel follows them exactly:
+ *   - anchors pair read r with the previous non-empty read r' of the group: minimizers (minimap2's
+ *     canonical k-mer hash, ambiguous and strand-symmetric k-mers skipped, every window minimum kept)
+ *     with equal hash and strand; hashes occurring more than SEED_MAX_OCC times in r' are skipped;
+ *   - anchors sorted by (start in r' ascending, start in r descending); the chain is the longest
+ *     strictly increasing subsequence in both (patience sorting, leftmost pile, traced back from the
+ *     last pile);
+ *   - partition: walking the chain, an anchor (t, q) (k-mer starts) is kept when t - T >= min_w,
+ *     q - Q >= min_w, len(r') - (t + k) >= min_w and len(r) - (q + k) >= min_w, with (T, Q) the end of
+ *     the last kept anchor's k-mer (initially 0, 0);
+ *   - the kept k-mers are pinned: q + i joins node(r', t + i) (the node position t + i of r' was
+ *     assigned to), i < k; the stretch between two kept k-mers (or the read ends) is aligned to the
+ *     subgraph between node(r', last base of the left k-mer) (SRC at the start) and node(r', first base
+ *     of the right k-mer) (SINK at the end), with that stretch's length as qlen of the adaptive band.
+ * --------------------------------------------------------------------------------------------- */
+#define SEED_MAX_OCC 8
+
+typedef struct {
+    uint64_t h;
+    int32_t pos; /* k-mer start */
+    int32_t z;
+} seed_mm;
+
+/* minimizers of encoded s[0..L) (codes 0..4), in position order */
+static int seed_minimizers(const uint8_t *s, int L, int k, int w, seed_mm **out) {
+    *out = NULL;
+    if (L < k || k <= 0 || k > 28 || w <= 0) return 0;
+    const uint64_t mask = (1ull << (2 * k)) - 1;
+    const int np = L - k + 1;
+    uint64_t *H = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)np);
+    uint8_t *z = (uint8_t *)malloc((size_t)np);
+    uint8_t *mark = (uint8_t *)calloc((size_t)np, 1);
+    for (int p = 0; p < np; ++p) {
+        uint64_t f = 0, r = 0;
+        int bad = 0;
+        for (int t = 0; t < k; ++t) {
+            const int c = s[p + t];
+            if (c > 3) { bad = 1; break; }
+            f = (f << 2) | (uint64_t)c;
+            r |= (uint64_t)(3 - c) << (2 * t);
+        }
+        if (bad || f == r) {
+            H[p] = UINT64_MAX;
+            z[p] = 0;
+        } else {
+            uint64_t key = f < r ? f : r;
+            key = (~key + (key << 21)) & mask;
+            key = key ^ key >> 24;
+            key = ((key + (key << 3)) + (key << 8)) & mask;
+            key = key ^ key >> 14;
+            key = ((key + (key << 2)) + (key << 4)) & mask;
+            key = key ^ key >> 28;
+            key = (key + (key << 31)) & mask;
+            H[p] = key;
+            z[p] = f < r ? 0 : 1;
+        }
+    }
+    const int nw = np <= w ? 1 : np - w + 1;
+    const int ww = np <= w ? np : w;
+    for (int w0 = 0; w0 < nw; ++w0) {
+        uint64_t mn = UINT64_MAX;
+        for (int t = 0; t < ww; ++t) if (H[w0 + t] < mn) mn = H[w0 + t];
+        if (mn == UINT64_MAX) continue;
+        for (int t = 0; t < ww; ++t) if (H[w0 + t] == mn) mark[w0 + t] = 1;
+    }
+    int n = 0;
+    for (int p = 0; p < np; ++p) n += mark[p];
+    seed_mm *o = (seed_mm *)malloc(sizeof(seed_mm) * (size_t)(n ? n : 1));
+    n = 0;
+    for (int p = 0; p < np; ++p)
+        if (mark[p]) {
+            o[n].h = H[p];
+            o[n].pos = p;
+            o[n].z = z[p];
+            ++n;
+        }
+    free(H); free(z); free(mark);
+    *out = o;
+    return n;
+}
+
+static int cmp_mm_key(const void *a, const void *b) {
+    const seed_mm *x = (const seed_mm *)a, *y = (const seed_mm *)b;
+    if (x->h != y->h) return x->h < y->h ? -1 : 1;
+    if (x->z != y->z) return x->z - y->z;
+    return x->pos - y->pos;
+}
+
+typedef struct { int32_t t, q; } seed_anchor;
+
+static int cmp_anchor(const void *a, const void *b) {
+    const seed_anchor *x = (const seed_anchor *)a, *y = (const seed_anchor *)b;
+    if (x->t != y->t) return x->t < y->t ? -1 : 1;
+    return x->q > y->q ? -1 : (x->q < y->q);
+}
+
+/* the kept partition anchors (k-mer starts in t and q) of read q against the previous read t */
+int poa_ref_seed_partition(const uint8_t *t, int tlen, const uint8_t *q, int qlen, int k, int w, int min_w,
+                           int32_t *par_t, int32_t *par_q, int cap) {
+    seed_mm *mt = NULL, *mq = NULL;
+    const int nt = seed_minimizers(t, tlen, k, w, &mt);
+    const int nq = seed_minimizers(q, qlen, k, w, &mq);
+    int np = 0;
+    if (nt > 0 && nq > 0) {
+        qsort(mt, (size_t)nt, sizeof(seed_mm), cmp_mm_key);
+        seed_anchor *an = (seed_anchor *)malloc(sizeof(seed_anchor) * (size_t)nq * SEED_MAX_OCC + 1);
+        int na = 0;
+        for (int i = 0; i < nq; ++i) {
+            int lo = 0, hi = nt; /* first entry >= (h, z) */
+            while (lo < hi) {
+                const int mid = (lo + hi) / 2;
+                if (mt[mid].h < mq[i].h || (mt[mid].h == mq[i].h && mt[mid].z < mq[i].z)) lo = mid + 1;
+                else hi = mid;
+            }
+            int e = lo;
+            while (e < nt && mt[e].h == mq[i].h && mt[e].z == mq[i].z) ++e;
+            if (e - lo == 0 || e - lo > SEED_MAX_OCC) continue;
+            for (int x = lo; x < e; ++x) {
+                an[na].t = mt[x].pos;
+                an[na].q = mq[i].pos;
+                ++na;
+            }
+        }
+        qsort(an, (size_t)na, sizeof(seed_anchor), cmp_anchor);
+        /* longest strictly increasing subsequence of q (t is strictly increasing along it by the order) */
+        int *tail = (int *)malloc(sizeof(int) * (size_t)(na + 1));
+        int *prev = (int *)malloc(sizeof(int) * (size_t)(na + 1));
+        int L = 0;
+        for (int i = 0; i < na; ++i) {
+            int lo = 0, hi = L; /* leftmost pile whose tail q >= an[i].q */
+            while (lo < hi) {
+                const int mid = (lo + hi) / 2;
+                if (an[tail[mid]].q < an[i].q) lo = mid + 1;
+                else hi = mid;
+            }
+            prev[i] = lo > 0 ? tail[lo - 1] : -1;
+            tail[lo] = i;
+            if (lo == L) ++L;
+        }
+        int *chain = (int *)malloc(sizeof(int) * (size_t)(L + 1));
+        for (int x = L - 1, c = L ? tail[L - 1] : -1; x >= 0; --x, c = prev[c]) chain[x] = c;
+        int T = 0, Q = 0;
+        for (int x = 0; x < L; ++x) {
+            const seed_anchor *a = &an[chain[x]];
+            if (a->t - T >= min_w && a->q - Q >= min_w && tlen - (a->t + k) >= min_w && qlen - (a->q + k) >= min_w) {
+                if (np < cap) {
+                    par_t[np] = a->t;
+                    par_q[np] = a->q;
+                }
+                ++np;
+                T = a->t + k;
+                Q = a->q + k;
+            }
+        }
+        free(chain); free(tail); free(prev); free(an);
+    }
+    free(mt);
+    free(mq);
+    return np;
 }
 
 static void add_chain(graph_t *g, const uint8_t *q, int qlen) {
@@ -611,12 +785,51 @@ static int hb_consensus(const graph_t *g, uint8_t *out, int cap) {
     return len;
 }
 
+static int64_t align_read(graph_t *g, const uint8_t *q, int qlen, const scorer *sc, int seeding, const uint8_t *t,
+                          int tlen, const int *tnode, int *qnode) {
+    int n = g->n;
+    int *order = (int *)malloc(sizeof(int) * (size_t)n);
+    int *pos = (int *)malloc(sizeof(int) * (size_t)n);
+    int *remain = (int *)malloc(sizeof(int) * (size_t)n);
+    int64_t cells = 0;
+    if (topo_bfs(g, order, pos) != 0) {
+        cells = -1;
+    } else {
+        set_remain(g, order, remain);
+        const mando_poa_params *p = sc->p;
+        int np = 0, cap = qlen / (p->min_w > 0 ? p->min_w : 1) + 2;
+        int32_t *pt = (int32_t *)malloc(sizeof(int32_t) * (size_t)cap), *pq = (int32_t *)malloc(sizeof(int32_t) * (size_t)cap);
+        if (seeding && t) np = poa_ref_seed_partition(t, tlen, q, qlen, p->k, p->w, p->min_w, pt, pq, cap);
+        if (np > cap) np = -1;
+        if (np < 0) cells = -1;
+        int B = SRC, q0 = 0;
+        for (int x = 0; x <= np && cells >= 0; ++x) {
+            const int E = x < np ? tnode[pt[x]] : SINK;
+            const int q1 = x < np ? pq[x] : qlen;
+            if (q1 > q0) {
+                const int64_t c = align_window(g, order, pos, remain, B, E, q + q0, q1 - q0, sc, qnode + q0);
+                cells = c < 0 ? -1 : cells + c;
+            }
+            if (x < np) {
+                for (int i = 0; i < p->k; ++i) qnode[pq[x] + i] = tnode[pt[x] + i];
+                B = tnode[pt[x] + p->k - 1];
+                q0 = pq[x] + p->k;
+            }
+        }
+        free(pt);
+        free(pq);
+    }
+    free(order);
+    free(pos);
+    free(remain);
+    return cells;
+}
+
 /* One group: encoded reads (0..4).  Writes the encoded consensus; returns its length, -1 on an
- * internal error.  `seeding` (-S) is accepted and ignored (see header).  *cells_out gets the DP cell count. */
+ * internal error.  seeding != 0 runs the -S path (see above).  *cells_out gets the DP cell count. */
 int poa_ref_group_encoded(const uint8_t *const *reads, const int *lens, int n_reads,
                           const mando_poa_params *p, int seeding, uint8_t *cons, int cap,
                           int64_t *cells_out) {
-    (void)seeding;
     scorer sc;
     make_scorer(&sc, p);
     graph_t g;
@@ -625,22 +838,34 @@ int poa_ref_group_encoded(const uint8_t *const *reads, const int *lens, int n_re
     g_add_node(&g, 4); /* SINK */
     int64_t cells = 0;
     int have_graph = 0;
+    int maxlen = 1;
+    for (int r = 0; r < n_reads; ++r) maxlen = imax(maxlen, lens[r]);
+    int *tnode = (int *)malloc(sizeof(int) * (size_t)maxlen), *qnode = (int *)malloc(sizeof(int) * (size_t)maxlen);
+    const uint8_t *t = NULL;
+    int tlen = 0;
     for (int r = 0; r < n_reads; ++r) {
         if (lens[r] <= 0) continue;
         if (!have_graph) {
             add_chain(&g, reads[r], lens[r]);
+            for (int i = 0; i < lens[r]; ++i) tnode[i] = 2 + i;
             have_graph = 1;
-            continue;
+        } else {
+            int64_t c = align_read(&g, reads[r], lens[r], &sc, seeding, t, tlen, tnode, qnode);
+            if (c < 0) {
+                g_free(&g);
+                free(tnode); free(qnode);
+                return -1;
+            }
+            cells += c;
+            apply_path(&g, reads[r], lens[r], qnode, tnode);
         }
-        int64_t c = align_and_add(&g, reads[r], lens[r], &sc);
-        if (c < 0) {
-            g_free(&g);
-            return -1;
-        }
-        cells += c;
+        t = reads[r];
+        tlen = lens[r];
     }
     int len = have_graph ? hb_consensus(&g, cons, cap) : 0;
     g_free(&g);
+    free(tnode);
+    free(qnode);
     if (cells_out) *cells_out = cells;
     return len;
 }
