@@ -13,6 +13,7 @@
 #include "internal.h"
 #include "orient_kernel.h"
 #include "poa_kernel.h"
+#include "seed_kernel.h"
 
 namespace {
 
@@ -83,9 +84,11 @@ struct mando_ctx {
     DevBuf ws, counter, prof, o_gidx;
     DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
     DevBuf o_hits, o_strand, o_status;
+    DevBuf s_items, s_item_of, s_n, s_t, s_q, s_scratch, s_redo, gorder2;  // -S partition
     ~mando_ctx() {
         for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
-                          &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx})
+                          &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx, &s_items,
+                          &s_item_of, &s_n, &s_t, &s_q, &s_scratch, &s_redo, &gorder2})
             b->release();
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -132,12 +135,30 @@ mando::PoaCaps plan_caps(const mando_poa_params &p, int64_t max_first, int64_t m
     return c;
 }
 
+// device-side -S partition of a batch (mando_poa_batch; see seed_kernel.hip)
+struct SeedPlan {
+    const int32_t *par_item = nullptr, *par_n = nullptr, *par_t = nullptr, *par_q = nullptr;
+    int32_t pc = 0, k = 0;
+};
+
+// One POA launch over n_groups groups (d_gorder: their indices).  sp != null: the groups are -S
+// groups (the seeded kernel instantiation).  ev_start / ev_end: record the ctx's timing events around
+// this launch (a batch of several launches times from the first start to the last end).
 int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps &caps,
                  const uint8_t *d_seq, const int64_t *d_seq_off, const int64_t *d_grp_off,
                  const int32_t *d_gorder, int64_t n_groups, uint8_t *d_cons,
                  const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
-                 int32_t *d_status, int max_per_cu) {
+                 int32_t *d_status, int max_per_cu, const SeedPlan *sp = nullptr, bool ev_start = true,
+                 bool ev_end = true) {
     mando::PoaKArgs a{};
+    if (sp) {
+        a.par_item = sp->par_item;
+        a.par_n = sp->par_n;
+        a.par_t = sp->par_t;
+        a.par_q = sp->par_q;
+        a.pc = sp->pc;
+        a.seed_k = sp->k;
+    }
     a.seq = d_seq;
     a.seq_off = d_seq_off;
     a.grp_off = d_grp_off;
@@ -196,9 +217,9 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         HIP_TRY(hipMemsetAsync(ctx->prof.p, 0, (size_t)slots * mando::kProfPhases * 8, ctx->stream));
         a.prof = ctx->prof.as<int64_t>();
     }
-    HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    if (ev_start) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
     HIP_TRY(mando::launch_poa(a, (int)slots, ctx->stream));
-    HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    if (ev_end) HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->timed = true;
     if (prof) {
         std::vector<int64_t> h((size_t)slots * mando::kProfPhases);
@@ -235,6 +256,103 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         if (tot[8] + tot[9] + tot[10] + tot[11] > 0)
             fprintf(stderr, "[mando prof] per DP row: seg0 %.3f  seg1 %.4f  seg2 %.4f  seg3 %.4f\n",
                     tot[8] / rows, tot[9] / rows, tot[10] / rows, tot[11] / rows);
+    }
+    return MANDO_OK;
+}
+
+// -S partitions of every seeded group (seed_kernel.hip): items pair each non-empty read after a group's
+// first with the previous non-empty read; the reads are already encoded on the device (ctx->seq).
+// Items over the launch's LDS capacity are re-run at twice the capacity.
+template <class IsSeeded>
+int plan_seeds(mando_ctx *ctx, const mando_poa_params &p, const std::vector<int64_t> &soff, const int64_t *grp_off,
+               int64_t n_groups, IsSeeded seeded_group, SeedPlan &sp) {
+    if (p.k < 1 || p.k > 19 || p.w < 1 || p.min_w < p.k)
+        return fail(MANDO_E_UNSUPPORTED, "-S needs 1 <= k <= 19, w >= 1, min_w >= k on this build");
+    const int64_t n_reads = (int64_t)soff.size() - 1;
+    std::vector<int32_t> items, item_of((size_t)std::max<int64_t>(n_reads, 1), -1);
+    int64_t max_len = 1, pc = 1;
+    for (int64_t g = 0; g < n_groups; ++g) {
+        if (!seeded_group(g)) continue;
+        int64_t prev = -1;
+        for (int64_t r = grp_off[g]; r < grp_off[g + 1]; ++r) {
+            const int64_t L = soff[(size_t)r + 1] - soff[(size_t)r];
+            if (L <= 0) continue;
+            max_len = std::max(max_len, L);
+            if (prev >= 0) {
+                item_of[(size_t)r] = (int32_t)(items.size() / 2);
+                items.push_back((int32_t)prev);
+                items.push_back((int32_t)r);
+                pc = std::max<int64_t>(pc, L / p.min_w + 2);
+            }
+            prev = r;
+        }
+    }
+    if (max_len >= (1 << 25)) return fail(MANDO_E_UNSUPPORTED, "-S: read longer than 2^25 bases");
+    const int64_t n_items = (int64_t)items.size() / 2;
+    int rc;
+    if ((rc = ctx->s_items.ensure(std::max<size_t>(items.size(), 1) * 4)) ||
+        (rc = ctx->s_item_of.ensure(item_of.size() * 4)) ||
+        (rc = ctx->s_n.ensure((size_t)std::max<int64_t>(n_items, 1) * 4)) ||
+        (rc = ctx->s_t.ensure((size_t)std::max<int64_t>(n_items, 1) * (size_t)pc * 4)) ||
+        (rc = ctx->s_q.ensure((size_t)std::max<int64_t>(n_items, 1) * (size_t)pc * 4)) ||
+        (rc = ctx->counter.ensure(256)))
+        return rc;
+    if (!items.empty())
+        HIP_TRY(hipMemcpyAsync(ctx->s_items.p, items.data(), items.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->s_item_of.p, item_of.data(), item_of.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    sp.par_item = ctx->s_item_of.as<int32_t>();
+    sp.par_n = ctx->s_n.as<int32_t>();
+    sp.par_t = ctx->s_t.as<int32_t>();
+    sp.par_q = ctx->s_q.as<int32_t>();
+    sp.pc = (int32_t)pc;
+    sp.k = p.k;
+    if (n_items == 0) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        return MANDO_OK;
+    }
+    // minimizer capacity: ~2 per w+1 positions, with room for ties
+    int cap = 1024;
+    while (cap < mando::kSeedCapMax && cap < 3 * max_len / (p.w + 1)) cap *= 2;
+    mando::SeedArgs a{};
+    a.seq = ctx->seq.as<uint8_t>();
+    a.seq_off = ctx->seq_off.as<int64_t>();
+    a.items = ctx->s_items.as<int32_t>();
+    a.k = p.k;
+    a.w = p.w;
+    a.min_w = p.min_w;
+    a.max_occ = mando::kSeedMaxOcc;
+    a.pc = (int32_t)pc;
+    a.par_n = ctx->s_n.as<int32_t>();
+    a.par_t = ctx->s_t.as<int32_t>();
+    a.par_q = ctx->s_q.as<int32_t>();
+    a.max_len = (int32_t)max_len;
+    a.counter = ctx->counter.as<int32_t>();
+    std::vector<int32_t> redo, nres((size_t)n_items);
+    for (;;) {
+        a.cap = cap;
+        a.redo = redo.empty() ? nullptr : ctx->s_redo.as<int32_t>();
+        a.n_items = (int32_t)(redo.empty() ? n_items : (int64_t)redo.size());
+        const int blocks = (int)std::min<int64_t>(a.n_items, (int64_t)ctx->n_cu * 4);
+        a.scratch_words = mando::seed_scratch_words((int)max_len, cap);
+        if ((rc = ctx->s_scratch.ensure((size_t)blocks * (size_t)a.scratch_words * 8))) return rc;
+        a.scratch = ctx->s_scratch.as<uint64_t>();
+        HIP_TRY(hipMemsetAsync(a.counter, 0, 4, ctx->stream));
+        HIP_TRY(mando::launch_seed(a, blocks, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(nres.data(), ctx->s_n.p, nres.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        std::vector<int32_t> again;
+        for (int64_t i = 0; i < n_items; ++i) {
+            if (nres[(size_t)i] == -2) return fail(MANDO_E_INTERNAL, "-S: more kept anchors than the read allows");
+            if (nres[(size_t)i] == -1) again.push_back((int32_t)i);
+        }
+        if (again.empty()) break;
+        if (cap >= mando::kSeedCapMax)
+            return fail(MANDO_E_UNSUPPORTED, "-S: a read has more than " + std::to_string(mando::kSeedCapMax) +
+                                                 " minimizers or anchors");
+        cap *= 2;
+        redo.swap(again);
+        if ((rc = ctx->s_redo.ensure(redo.size() * 4))) return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->s_redo.p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     }
     return MANDO_OK;
 }
@@ -352,9 +470,10 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
         cons_off[0] = 0;
         return MANDO_OK;
     }
-    // -S (params->seeding / seeding_per_group): abPOA's minimizer-window partition is not restated;
-    // seeded groups run the same full adaptive-band DP (DESIGN.md "Known gaps").
-    (void)seeding_per_group;
+    // -S for a group: seeding_per_group[g], or params->seeding for every group
+    auto seeded_group = [&](int64_t g) {
+        return seeding_per_group ? seeding_per_group[g] != 0 : params->seeding != 0;
+    };
     const int64_t n_reads = grp_off[n_groups] - grp_off[0];
     if (grp_off[0] != 0 || n_reads < 0) return fail(MANDO_E_ARG, "grp_off must start at 0");
     for (int64_t g = 0; g < n_groups; ++g)
@@ -415,28 +534,53 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
     HIP_TRY(hipMemcpyAsync(ctx->grp_off.p, goff.data(), goff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->cons_off.p, ccap.data(), ccap.size() * 8, hipMemcpyHostToDevice, ctx->stream));
 
+    // -S groups: their window partitions first (seed kernel over every read of a seeded group paired
+    // with the group's previous non-empty read)
+    SeedPlan sp;
+    bool any_seeded = false;
+    for (int64_t g = 0; g < n_groups && !any_seeded; ++g) any_seeded = seeded_group(g);
+    if (any_seeded) {
+        rc = plan_seeds(ctx, *params, soff, grp_off, n_groups, seeded_group, sp);
+        if (rc) return rc;
+    }
+
     std::vector<int32_t> st((size_t)n_groups), clen((size_t)n_groups);
     std::vector<int64_t> cells((size_t)n_groups);
     std::vector<int32_t> todo = order;
     std::vector<uint8_t> cons_enc((size_t)ccap[(size_t)n_groups]);
     ctx->last_launches = 0;
     for (int attempt = 0; attempt < 4 && !todo.empty(); ++attempt) {
-        int64_t mf = 0, ms = 0, ml = 0, mr = 0;
-        for (int32_t g : todo) {
-            mf = std::max(mf, gs[(size_t)g].first_len);
-            ms = std::max(ms, gs[(size_t)g].sum);
-            ml = std::max(ml, gs[(size_t)g].maxlen);
-            mr = std::max(mr, gs[(size_t)g].nreads);
+        // unseeded and seeded groups run as two launches of the two kernel instantiations
+        std::vector<int32_t> lists[2];
+        for (int32_t g : todo) lists[seeded_group(g) ? 1 : 0].push_back(g);
+        bool first = true;
+        for (int kind = 0; kind < 2; ++kind) {
+            const std::vector<int32_t> &L = lists[kind];
+            if (L.empty()) continue;
+            int64_t mf = 0, ms = 0, ml = 0, mr = 0;
+            for (int32_t g : L) {
+                mf = std::max(mf, gs[(size_t)g].first_len);
+                ms = std::max(ms, gs[(size_t)g].sum);
+                ml = std::max(ml, gs[(size_t)g].maxlen);
+                mr = std::max(mr, gs[(size_t)g].nreads);
+            }
+            mando::PoaCaps caps = plan_caps(*params, mf, ms, ml, mr, attempt);
+            caps.seeded = kind;
+            // the second launch may need a larger workspace: the first must be done with it
+            if (!first) HIP_TRY(hipStreamSynchronize(ctx->stream));
+            DevBuf &gb = kind ? ctx->gorder2 : ctx->gorder;
+            if ((rc = gb.ensure(L.size() * 4))) return rc;
+            HIP_TRY(hipMemcpyAsync(gb.p, L.data(), L.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+            const bool last = kind == 1 || lists[1].empty();
+            rc = launch_batch(ctx, *params, caps, ctx->seq.as<uint8_t>(), ctx->seq_off.as<int64_t>(),
+                              ctx->grp_off.as<int64_t>(), gb.as<int32_t>(), (int64_t)L.size(),
+                              ctx->cons.as<uint8_t>(), ctx->cons_off.as<int64_t>(),
+                              ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
+                              ctx->status.as<int32_t>(), kMaxWavesPerCu, kind ? &sp : nullptr, first, last);
+            if (rc) return rc;
+            ctx->last_launches += 1;
+            first = false;
         }
-        mando::PoaCaps caps = plan_caps(*params, mf, ms, ml, mr, attempt);
-        HIP_TRY(hipMemcpyAsync(ctx->gorder.p, todo.data(), todo.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-        rc = launch_batch(ctx, *params, caps, ctx->seq.as<uint8_t>(), ctx->seq_off.as<int64_t>(),
-                          ctx->grp_off.as<int64_t>(), ctx->gorder.as<int32_t>(), (int64_t)todo.size(),
-                          ctx->cons.as<uint8_t>(), ctx->cons_off.as<int64_t>(),
-                          ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
-                          ctx->status.as<int32_t>(), kMaxWavesPerCu);
-        if (rc) return rc;
-        ctx->last_launches += 1;
         HIP_TRY(hipMemcpyAsync(st.data(), ctx->status.p, st.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipMemcpyAsync(clen.data(), ctx->cons_len.p, clen.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipMemcpyAsync(cells.data(), ctx->cells.p, cells.size() * 8, hipMemcpyDeviceToHost, ctx->stream));

@@ -50,12 +50,13 @@ struct PoaCaps {
     int64_t TBC;     // traceback bytes per read
     int64_t KPC;     // predecessor-index bytes per read (multi-predecessor rows)
     int64_t SVC;     // spilled H/E1/E2 ints per read
+    int32_t seeded;  // the launch has -S groups: window descriptors and maps, per-position read nodes
 };
 
 struct SlotLayout {
     int64_t base, gid, gtab, in_n, out_n, in_id, out_id, out_w, sink_in, src_out, src_out_w;
     int64_t order0, order1, pos, remrow, desc, rinfo, tb, kp, sv, qnode, qtgt, qflag, qnb, qoff, qmslot,
-        ins, insmm, score, nxt;
+        ins, insmm, score, nxt, xpre, wdesc, wxpre, wmap, wlist, wf, wb, tnode;
     int64_t total;
 };
 
@@ -96,6 +97,19 @@ __host__ __device__ inline SlotLayout make_layout(const PoaCaps &c) {
     L.insmm = o; o = align256(o + 4 * nc);
     L.score = o; o = align256(o + 4 * nc);
     L.nxt = o; o = align256(o + 4 * nc);
+    // predecessor rows past the kPreInline a descriptor holds (rows with more predecessors only)
+    L.xpre = o; o = align256(o + 4 * nc * dc);
+    // -S windows: window descriptors + their extra predecessors, topological row -> window row map,
+    // window row -> topological row list, reachability flags, and the node each position of the
+    // previous read was assigned to
+    const int64_t sn = c.seeded ? nc : 0;
+    L.wdesc = o; o = align256(o + 4 * kDescInts * (c.seeded ? nc + kWave : 0));
+    L.wxpre = o; o = align256(o + 4 * sn * dc);
+    L.wmap = o; o = align256(o + 4 * sn);
+    L.wlist = o; o = align256(o + 4 * sn);
+    L.wf = o; o = align256(o + 4 * sn);
+    L.wb = o; o = align256(o + 4 * sn);
+    L.tnode = o; o = align256(o + 4 * (c.seeded ? qc : 0));
     L.total = o;
     return L;
 }
@@ -120,6 +134,11 @@ struct PoaKArgs {
     int32_t match, mismatch, o1, e1, o2, e2, band_b;
     float band_f;
     int32_t qlds;            // dynamic LDS bytes for the read stream (see poa_qlds_bytes)
+    // -S (a launch of seeded groups, caps.seeded): per read its seed item (-1: none), per item the
+    // kept partition anchors from the seed kernel (k-mer starts in the previous read and in this read)
+    const int32_t *par_item;
+    const int32_t *par_n, *par_t, *par_q;
+    int32_t pc, seed_k;
     int32_t dbg;             // MANDO_POA_DBG: bit 0 no 16-bit mode, bit 1 no 16-bit fast rows
 };
 

@@ -40,6 +40,9 @@ struct Slot {
     gint *order, *order2, *pos, *remrow, *desc, *rinfo;
     gu8 *tb, *kp;
     gint *sv, *qnode, *qtgt, *qflag, *qnb, *qoff, *qmslot, *ins, *insmm, *score, *nxt;
+    gint *xpre;                                    // extra predecessor rows (> kPreInline), row * DCAP + k
+    gint *wdesc, *wxpre, *wmap, *wlist, *wf, *wb;  // -S window rows (see build_window)
+    gint *tnode;                                   // -S: node of each position of the previous read
 };
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
@@ -188,6 +191,10 @@ struct alignas(16) SharedState {
     Slot slot;                      // this wave's workspace arrays (read per phase, see slot_of)
     gint *order0, *order1;          // the two topological-order buffers (slot.order swaps them)
     PoaKArgs args;                  // kernel arguments (read per phase, see args_of)
+    // -S window DP: slot.desc / slot.xpre / slot.qnode point at the window's arrays while it runs;
+    // the sink of the DP is node win_sink, and a node's row is wmap[pos - win_pb] inside [pb, pe]
+    int win_on, win_sink, win_pb, win_pe;
+    gint *desc_full, *xpre_full, *qnode_full;
 };
 static_assert(sizeof(BtLds) <= sizeof(DpLds), "backtrack window must fit the DP scratch");
 
@@ -241,6 +248,14 @@ __device__ __forceinline__ Slot slot_of(SharedState &sh) {
     s.insmm = uniptr(s.insmm);
     s.score = uniptr(s.score);
     s.nxt = uniptr(s.nxt);
+    s.xpre = uniptr(s.xpre);
+    s.wdesc = uniptr(s.wdesc);
+    s.wxpre = uniptr(s.wxpre);
+    s.wmap = uniptr(s.wmap);
+    s.wlist = uniptr(s.wlist);
+    s.wf = uniptr(s.wf);
+    s.wb = uniptr(s.wb);
+    s.tnode = uniptr(s.tnode);
     return s;
 }
 __device__ __forceinline__ PoaKArgs args_of(SharedState &sh) {
@@ -274,6 +289,12 @@ __device__ __forceinline__ PoaKArgs args_of(SharedState &sh) {
     a.cells = uniptr(a.cells);
     a.status = uniptr(a.status);
     a.n_groups = bcast0(a.n_groups);
+    a.par_item = uniptr(a.par_item);
+    a.par_n = uniptr(a.par_n);
+    a.par_t = uniptr(a.par_t);
+    a.par_q = uniptr(a.par_q);
+    a.pc = bcast0(a.pc);
+    a.seed_k = bcast0(a.seed_k);
     return a;
 }
 
@@ -366,6 +387,9 @@ __device__ __forceinline__ DescRow desc_gather(const PoaKArgs &a, const Slot &s,
 #pragma unroll
     for (int k = 0; k < kPreInline; ++k)
         if (k < pn) d.pre[k] = s.pos[iid[k]];
+    // rare rows with more predecessors: the rest go to the row's xpre list (read by the generic row
+    // and the backtrack, which never look predecessors up through the graph)
+    for (int k = kPreInline; k < pn; ++k) s.xpre[(int64_t)r * a.caps.DCAP + k] = s.pos[il[k]];
     int opos[kOutInline];
 #pragma unroll
     for (int k = 0; k < kOutInline; ++k) opos[k] = (k < on) ? s.pos[oid[k]] : 0;
@@ -463,9 +487,153 @@ __device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane, int
     }
 }
 
-// predecessor row k of row r (node v); the first kPreInline come from the descriptor
-__device__ __forceinline__ int pre_row_slow(const PoaKArgs &a, const Slot &s, int v, int k) {
-    return s.pos[in_list(s, a, v)[k]];
+// ---------------------------------------------------------------------------------------------
+// -S window rows (oracle/poa_ref.c align_window): the topological rows r in [pos B, pos E] that are
+// reachable from B and reach E, in order, become window rows 0..m-1 (B the source row, E the sink).
+// Built from the whole-graph descriptors of this read (build_desc at the 32-bit ring depth, so their
+// `far` bits are safe for both ring depths: a window only shortens row distances).
+//   1. forward reachability, 64 rows at a time: a row is reached when a predecessor is; predecessors
+//      in earlier chunks are read from wf[], the chunk's own chain is resolved by a scalar walk over
+//      the lanes (bit masks of in-chunk predecessors);
+//   2. backward reachability from E the same way, descending: reached rows mark their earlier-chunk
+//      predecessors in wb[] (idempotent stores), the chunk's own rows by a descending scalar walk;
+//   3. compaction (ballot prefix) into wmap (topological -> window row) and wlist (window -> topological);
+//   4. window descriptors: predecessors outside the window dropped (in in-edge order), remain taken
+//      relative to E (remain[v] - remain[E] - 1), fast-row bits recomputed on window distances.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ int build_window(SharedState &sh, int B, int E, int lane, int ring, int &m_out) {
+    const PoaKArgs a = args_of(sh);
+    Slot s = slot_of(sh);
+    const int DC = a.caps.DCAP;
+    const int pB = bcast0(s.pos[B]), pE = bcast0(s.pos[E]);
+    if (pE <= pB) return kStInternal;
+    const int span = pE - pB + 1;
+    for (int x = lane; x < span; x += kWave) s.wb[x] = 0;
+    hbm_fence();
+    wave_sync();
+    // 1. forward
+    for (int c0 = 0; c0 < span; c0 += kWave) {
+        const int x = c0 + lane;
+        bool ext = false;
+        uint64_t pm = 0;
+        if (x < span) {
+            if (x == 0) {
+                ext = true;
+            } else {
+                const gint *dd = s.desc + (int64_t)(pB + x) * kDescInts;
+                const int pn = dd[1] >> 16;
+                for (int k = 0; k < pn; ++k) {
+                    const int p = (k < kPreInline ? dd[3 + k] : s.xpre[(int64_t)(pB + x) * DC + k]) - pB;
+                    if (p < 0) continue;
+                    if (p < c0) ext |= s.wf[p] != 0;
+                    else pm |= 1ull << (p - c0);
+                }
+            }
+        }
+        const uint64_t eb = __ballot(ext);
+        uint64_t m = 0;
+        const int lim = min(kWave, span - c0);
+        for (int l = 0; l < lim; ++l)
+            if (((eb >> l) & 1) || (readlane64(pm, l) & m)) m |= 1ull << l;
+        if (x < span) s.wf[x] = (int)((m >> lane) & 1);
+        hbm_fence();
+        wave_sync();
+    }
+    // 2. backward
+    for (int c0 = ((span - 1) / kWave) * kWave; c0 >= 0; c0 -= kWave) {
+        const int x = c0 + lane;
+        uint64_t pm = 0;
+        bool ext = false;
+        if (x < span) {
+            ext = x == span - 1 || s.wb[x] != 0;
+            if (x > 0) {
+                const gint *dd = s.desc + (int64_t)(pB + x) * kDescInts;
+                const int pn = dd[1] >> 16;
+                for (int k = 0; k < pn; ++k) {
+                    const int p = (k < kPreInline ? dd[3 + k] : s.xpre[(int64_t)(pB + x) * DC + k]) - pB;
+                    if (p >= c0) pm |= 1ull << (p - c0);
+                }
+            }
+        }
+        const uint64_t eb = __ballot(ext);
+        uint64_t m = 0;
+        const int lim = min(kWave, span - c0);
+        for (int l = lim - 1; l >= 0; --l)
+            if (((eb | m) >> l) & 1) m |= (1ull << l) | readlane64(pm, l);
+        const bool on = x < span && ((m >> lane) & 1);
+        if (x < span) s.wb[x] = on ? 1 : 0;
+        if (on && x > 0) {  // reached: so are its predecessors in earlier chunks
+            const gint *dd = s.desc + (int64_t)(pB + x) * kDescInts;
+            const int pn = dd[1] >> 16;
+            for (int k = 0; k < pn; ++k) {
+                const int p = (k < kPreInline ? dd[3 + k] : s.xpre[(int64_t)(pB + x) * DC + k]) - pB;
+                if (p >= 0 && p < c0) s.wb[p] = 1;
+            }
+        }
+        hbm_fence();
+        wave_sync();
+    }
+    // 3. compaction
+    int m = 0;
+    for (int c0 = 0; c0 < span; c0 += kWave) {
+        const int x = c0 + lane;
+        const bool in = x < span && s.wf[x] != 0 && s.wb[x] != 0;
+        const uint64_t b = __ballot(in);
+        const int idx = m + __popcll(b & lanemask_lt(lane));
+        if (x < span) s.wmap[x] = in ? idx : -1;
+        if (in) s.wlist[idx] = pB + x;
+        m += __popcll(b);
+    }
+    hbm_fence();
+    wave_sync();
+    // 4. window descriptors
+    const int remE = bcast0(s.remrow[pE]);
+    for (int i0 = 0; i0 < m; i0 += kWave) {
+        const int i = i0 + lane;
+        if (i < m) {
+            const int r = s.wlist[i];
+            const gint *dd = s.desc + (int64_t)r * kDescInts;
+            const int d1 = dd[1], pn = d1 >> 16;
+            int pre[kPreInline];
+#pragma unroll
+            for (int k = 0; k < kPreInline; ++k) pre[k] = -1;
+            int np = 0;
+            for (int k = 0; k < pn; ++k) {
+                const int p = k < kPreInline ? dd[3 + k] : s.xpre[(int64_t)r * DC + k];
+                if (p < pB || p > pE) continue;
+                const int wp = s.wmap[p - pB];
+                if (wp < 0) continue;
+                if (np < kPreInline) {
+#pragma unroll
+                    for (int t = 0; t < kPreInline; ++t)
+                        if (t == np) pre[t] = wp;
+                } else {
+                    s.wxpre[(int64_t)i * DC + np] = wp;
+                }
+                ++np;
+            }
+            const int sfast = (np == 1 || np == 2) && i - pre[0] < ring && (np == 1 || i - pre[1] < ring);
+            bool near = np >= 3 && np <= kPreInline;
+#pragma unroll
+            for (int k = 0; k < kPreInline; ++k) near = near && (k >= np || i - pre[k] < ring);
+            gint *wd = s.wdesc + (int64_t)i * kDescInts;
+            wd[0] = dd[0];
+            wd[1] = (d1 & 0x1ff) | (near ? (1 << 14) : 0) | (sfast << 15) | (np << 16);
+            wd[2] = s.remrow[r] - remE - 1;
+#pragma unroll
+            for (int k = 0; k < kPreInline; ++k) wd[3 + k] = pre[k];
+        }
+    }
+    hbm_fence();
+    wave_sync();
+    m_out = m;
+    return kStOk;
 }
 
 __device__ __forceinline__ RowRec load_rowrec(const SharedState &sh, const Slot &s, int r, int p) {
@@ -502,15 +670,6 @@ __device__ __forceinline__ int row_spill_width(int beg, int end) {
 template <bool R16>
 __device__ __forceinline__ bool pre_in_ring(int r, int p, const RowRec &pr) {
     return (r - p < ring_rows<R16>()) && row_narrow(pr.beg, pr.end);
-}
-
-// predecessor row k of the current row (descriptor `dl` in the LDS batch)
-__device__ __forceinline__ int pre_row_k(const PoaKArgs &a, const Slot &s, const int *dl, int node, int k) {
-    if (k >= kPreInline) {
-        hbm_fence();
-        return bcast0(s.pos[in_list(s, a, node)[k]]);
-    }
-    return dl[3 + k];
 }
 
 // Scoring: the reference always runs `abpoa -M 5` with default gaps, so that case is compiled with
@@ -551,7 +710,7 @@ __device__ __forceinline__ void pre_records_slow(const PoaKArgs &a, const Slot &
                                                  int &pE, int &pA, int &pS) {
     hbm_fence();
     if (lane < pn) {
-        const int p = (lane < kPreInline) ? dl[3 + lane] : s.pos[in_list(s, a, node)[lane]];
+        const int p = (lane < kPreInline) ? dl[3 + lane] : s.xpre[(int64_t)r * a.caps.DCAP + lane];
         int4 x;
         if (r - p < kRowRing) {
             x = sh.rrow[p % kRowRing];
@@ -1533,13 +1692,23 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
     }
 #endif
 
-    // best predecessor of the sink at column qlen (first in in-edge order on ties)
+    // best predecessor of the sink at column qlen (first in in-edge order on ties); in a -S window
+    // the sink is the window's end node and only its predecessors inside the window count
     hbm_fence();
     const int sr = n - 1;
-    const int nin = s.in_n[kSink];
+    const bool win = bcast0(sh.win_on) != 0;
+    const int snode = win ? bcast0(sh.win_sink) : kSink;
+    const int wpb = bcast0(sh.win_pb), wpe = bcast0(sh.win_pe);
+    const int nin = s.in_n[snode];
+    const gint *sin = in_list(s, a, snode);
     int bs = -2147483647 - 1, bi = -1;
     for (int k = 0; k < nin; ++k) {
-        const int p = bcast0(s.pos[s.sink_in[k]]);
+        int p = bcast0(s.pos[sin[k]]);
+        if (win) {
+            if (p < wpb || p > wpe) continue;
+            p = bcast0(s.wmap[p - wpb]);
+            if (p < 0) continue;
+        }
         const RowRec pr = load_rowrec(sh, s, sr, p);
         if (qlen < pr.beg || qlen > pr.end) continue;
         int hv;
@@ -1686,7 +1855,7 @@ __device__ __forceinline__ void bt_step_global(const PoaKArgs &a, const Slot &s,
                            : st;
     if (ty <= 2) {
         const int k = multi ? s.kp[kpbase + 3 * j + ty] : 0;
-        const int p = (k < kPreInline) ? s.desc[(int64_t)i * kDescInts + 3 + k] : s.pos[in_list(s, a, node)[k]];
+        const int p = (k < kPreInline) ? s.desc[(int64_t)i * kDescInts + 3 + k] : s.xpre[(int64_t)i * a.caps.DCAP + k];
         if (ty == 0) {
             s.qnode[j - 1] = node;
             --j;
@@ -1840,6 +2009,109 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
         }
     }
     for (int t = lane; t < j; t += kWave) s.qnode[t] = -1;
+    return kStOk;
+}
+
+// ---------------------------------------------------------------------------------------------
+// -S: one read aligned window by window (oracle/poa_ref.c align_read).  The seed kernel's kept
+// anchors (k-mer starts t_x in the previous read, q_x in this one) pin q_x + i to the node position
+// t_x + i of the previous read joined (tnode); the stretches between pinned k-mers are banded DPs over
+// the window rows between their bounding nodes, each writing its slice of qnode.  The whole read's
+// path then goes through update_graph at once, exactly like an unseeded read.
+// ---------------------------------------------------------------------------------------------
+template <class SC>
+__device__ __forceinline__ int align_seeded(SharedState &sh, const SC &sc, const uint8_t *q, int qlen, int n, int lane,
+                                            int64_t &cells, int64_t rd) {
+    int np = 0, item = -1, k = 0, pc = 0;
+    const int32_t *par_t = nullptr, *par_q = nullptr;
+    {
+        const PoaKArgs a = args_of(sh);
+        item = bcast0(a.par_item[rd]);
+        if (item >= 0) np = bcast0(a.par_n[item]);
+        if (np < 0) return kStInternal;
+        k = a.seed_k;
+        pc = a.pc;
+        par_t = a.par_t;
+        par_q = a.par_q;
+    }
+    build_desc(sh, n, lane, kRing);
+    wave_sync();
+    int B = kSrc, q0 = 0;
+    for (int x = 0; x <= np; ++x) {
+        int E = kSink, q1 = qlen, tx = 0;
+        {
+            const Slot s = slot_of(sh);
+            if (x < np) {
+                tx = bcast0(par_t[(int64_t)item * pc + x]);
+                q1 = bcast0(par_q[(int64_t)item * pc + x]);
+                E = bcast0(s.tnode[tx]);
+            }
+        }
+        if (q1 > q0) {
+            const int qw = q1 - q0;
+            const bool try16 = r16_eligible(sc, qw) && !(args_of(sh).dbg & 1);
+            int m = 0;
+            int st = build_window(sh, B, E, lane, try16 ? kRing16 : kRing, m);
+            if (st != kStOk) return st;
+            {
+                const Slot s = slot_of(sh);
+                const int pB = bcast0(s.pos[B]), pE = bcast0(s.pos[E]);
+                if (lane == 0) {
+                    sh.slot.desc = s.wdesc;
+                    sh.slot.xpre = s.wxpre;
+                    sh.slot.qnode = sh.qnode_full + q0;
+                    sh.win_on = 1;
+                    sh.win_sink = E;
+                    sh.win_pb = pB;
+                    sh.win_pe = pE;
+                }
+            }
+            wave_sync();
+            int bi = -1;
+            st = try16 ? run_dp<SC, true>(sh, sc, q + q0, qw, m, lane, cells, bi) : kStRetry32;
+            if (st == kStRetry32) {
+                if (try16) {  // window descriptors at the 32-bit ring depth
+                    if (lane == 0) {
+                        sh.slot.desc = sh.desc_full;
+                        sh.slot.xpre = sh.xpre_full;
+                    }
+                    wave_sync();
+                    st = build_window(sh, B, E, lane, kRing, m);
+                    if (st != kStOk) return st;
+                    if (lane == 0) {
+                        const Slot s = sh.slot;
+                        sh.slot.desc = s.wdesc;
+                        sh.slot.xpre = s.wxpre;
+                    }
+                    wave_sync();
+                }
+                st = run_dp<SC, false>(sh, sc, q + q0, qw, m, lane, cells, bi);
+            }
+            if (st == kStOk && bi < 0) st = kStInternal;
+            if (st == kStOk) {
+                wave_sync();
+                __builtin_amdgcn_s_setprio(kSerialPrio);
+                st = backtrack(sh, bi, qw, m, lane);
+                __builtin_amdgcn_s_setprio(0);
+            }
+            if (lane == 0) {
+                sh.slot.desc = sh.desc_full;
+                sh.slot.xpre = sh.xpre_full;
+                sh.slot.qnode = sh.qnode_full;
+                sh.win_on = 0;
+            }
+            wave_sync();
+            if (st != kStOk) return st;
+        }
+        if (x < np) {  // the pinned k-mer
+            const Slot s = slot_of(sh);
+            hbm_fence();
+            for (int i = lane; i < k; i += kWave) s.qnode[q1 + i] = s.tnode[tx + i];
+            B = bcast0(s.tnode[tx + k - 1]);
+            q0 = q1 + k;
+            wave_sync();
+        }
+    }
     return kStOk;
 }
 
@@ -2085,7 +2357,9 @@ __device__ __forceinline__ int consensus(SharedState &sh, int n, uint8_t *out, i
     return l <= cap ? kStOk : kStCap;
 }
 
-template <class SC>
+// SEEDED: the launch holds only -S groups (align_seeded); the unseeded instantiation carries none of
+// that code, so the hot DP keeps its register allocation.
+template <class SC, bool SEEDED>
 __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
     __shared__ SharedState sh;
     const int lane = lane_id();
@@ -2124,10 +2398,25 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
     s.nxt = (gint *)(ws + a.lay.nxt);
     s.order = (gint *)(ws + a.lay.order0);
     s.order2 = (gint *)(ws + a.lay.order1);
+    s.xpre = (gint *)(ws + a.lay.xpre);
+    s.wdesc = (gint *)(ws + a.lay.wdesc);
+    s.wxpre = (gint *)(ws + a.lay.wxpre);
+    s.wmap = (gint *)(ws + a.lay.wmap);
+    s.wlist = (gint *)(ws + a.lay.wlist);
+    s.wf = (gint *)(ws + a.lay.wf);
+    s.wb = (gint *)(ws + a.lay.wb);
+    s.tnode = (gint *)(ws + a.lay.tnode);
     if (lane == 0) {
         sh.slot = s;
         sh.order0 = s.order;
         sh.order1 = s.order2;
+        sh.win_on = 0;
+        sh.win_sink = kSink;
+        sh.win_pb = 0;
+        sh.win_pe = 0;
+        sh.desc_full = s.desc;
+        sh.xpre_full = s.xpre;
+        sh.qnode_full = s.qnode;
     }
     wave_sync();
 
@@ -2164,6 +2453,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
             first = uni64(first);
         }
         int clen = 0;
+        constexpr bool seeded = SEEDED;
         if (first < r1) {
             {
                 const PoaKArgs a = args_of(sh);
@@ -2171,6 +2461,10 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 const uint8_t *q0 = a.seq + o0;
                 const int L0 = (int)(uni64(a.seq_off[first + 1]) - o0);
                 st = init_chain(sh, q0, L0, lane, n);
+                if (seeded && st == kStOk) {  // the chain's node of every position (init_chain: 2 + t)
+                    const Slot s = slot_of(sh);
+                    for (int t = lane; t < L0; t += kWave) s.tnode[t] = 2 + t;
+                }
             }
             wave_sync();
             for (int64_t rd = first + 1; rd < r1 && st == kStOk; ++rd) {
@@ -2197,6 +2491,24 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 // The serial, latency-bound phases (descriptors, backtrack, graph update, consensus) issue
                 // ahead of the co-resident waves' DP rows (s_setprio 1; the DP runs at 0): those waves
                 // return to their DP sooner, the SIMD's issue slots stay busy (config-3 kernel -3.5 %).
+                if constexpr (SEEDED) {
+                    // -S: windows between the seed kernel's anchors, then the whole read's update
+                    __builtin_amdgcn_s_setprio(kSerialPrio);
+                    st = align_seeded(sh, sc, q, qlen, n, lane, cells, rd);
+                    if (st != kStOk) break;
+                    wave_sync();
+                    __builtin_amdgcn_s_setprio(kSerialPrio);
+                    st = update_graph(sh, q, qlen, n, ng, lane);
+                    wave_sync();
+                    if (st != kStOk) break;
+                    {  // this read's node per position: the next read's anchors resolve through it
+                        const Slot s = slot_of(sh);
+                        hbm_fence();
+                        for (int t = lane; t < qlen; t += kWave) s.tnode[t] = s.qtgt[t];
+                    }
+                    wave_sync();
+                    continue;
+                }
                 __builtin_amdgcn_s_setprio(kSerialPrio);
                 uint64_t t0 = prof ? clock64() : 0;
                 const bool try16 = r16_eligible(sc, qlen) && !(args_of(sh).dbg & 1);
@@ -2296,25 +2608,39 @@ hipError_t launch_encode(uint8_t *buf, int64_t n, hipStream_t stream) {
     return hipGetLastError();
 }
 
-int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
+template <bool SEEDED>
+static int blocks_per_cu_t(const PoaKArgs &a, bool dflt) {
     int nb = 0;
-    const bool dflt = a.match == DefaultScores::match && a.mismatch == DefaultScores::mismatch &&
-                      a.o1 == DefaultScores::o1 && a.e1 == DefaultScores::e1 && a.o2 == DefaultScores::o2 &&
-                      a.e2 == DefaultScores::e2;
-    hipError_t e = dflt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, poa_kernel<DefaultScores>, kWave, a.qlds)
-                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, poa_kernel<RuntimeScores>, kWave, a.qlds);
-    if (e != hipSuccess || nb < 1) nb = 8;
+    hipError_t e = dflt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, poa_kernel<DefaultScores, SEEDED>, kWave, a.qlds)
+                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, poa_kernel<RuntimeScores, SEEDED>, kWave, a.qlds);
+    return e == hipSuccess ? nb : 0;
+}
+
+static bool default_scores(const PoaKArgs &a) {
+    return a.match == DefaultScores::match && a.mismatch == DefaultScores::mismatch && a.o1 == DefaultScores::o1 &&
+           a.e1 == DefaultScores::e1 && a.o2 == DefaultScores::o2 && a.e2 == DefaultScores::e2;
+}
+
+int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
+    const bool dflt = default_scores(a);
+    int nb = a.caps.seeded ? blocks_per_cu_t<true>(a, dflt) : blocks_per_cu_t<false>(a, dflt);
+    if (nb < 1) nb = 8;
     return nb < cap ? nb : cap;
 }
 
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream) {
-    const bool dflt = a.match == DefaultScores::match && a.mismatch == DefaultScores::mismatch &&
-                      a.o1 == DefaultScores::o1 && a.e1 == DefaultScores::e1 && a.o2 == DefaultScores::o2 &&
-                      a.e2 == DefaultScores::e2;
-    if (dflt)
-        hipLaunchKernelGGL(poa_kernel<DefaultScores>, dim3(n_slots), dim3(kWave), a.qlds, stream, a);
-    else
-        hipLaunchKernelGGL(poa_kernel<RuntimeScores>, dim3(n_slots), dim3(kWave), a.qlds, stream, a);
+    const bool dflt = default_scores(a);
+    if (a.caps.seeded) {
+        if (dflt)
+            hipLaunchKernelGGL((poa_kernel<DefaultScores, true>), dim3(n_slots), dim3(kWave), a.qlds, stream, a);
+        else
+            hipLaunchKernelGGL((poa_kernel<RuntimeScores, true>), dim3(n_slots), dim3(kWave), a.qlds, stream, a);
+    } else {
+        if (dflt)
+            hipLaunchKernelGGL((poa_kernel<DefaultScores, false>), dim3(n_slots), dim3(kWave), a.qlds, stream, a);
+        else
+            hipLaunchKernelGGL((poa_kernel<RuntimeScores, false>), dim3(n_slots), dim3(kWave), a.qlds, stream, a);
+    }
     return hipGetLastError();
 }
 

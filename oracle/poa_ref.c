@@ -561,9 +561,10 @@ static void apply_path(graph_t *g, const uint8_t *q, int qlen, const int *qnode,
  *   - anchors pair read r with the previous non-empty read r' of the group: minimizers (minimap2's
  *     canonical k-mer hash, ambiguous and strand-symmetric k-mers skipped, every window minimum kept)
  *     with equal hash and strand; hashes occurring more than SEED_MAX_OCC times in r' are skipped;
- *   - anchors sorted by (start in r' ascending, start in r descending); the chain is the longest
- *     strictly increasing subsequence in both (patience sorting, leftmost pile, traced back from the
- *     last pile);
+ *   - anchors in (start in r ascending, start in r' descending) order -- the order in which r's
+ *     minimizers meet r''s sorted index; the chain is the longest strictly increasing subsequence of
+ *     the r' starts (hence strictly increasing in both reads; patience sorting, leftmost pile, traced
+ *     back from the last pile);
  *   - partition: walking the chain, an anchor (t, q) (k-mer starts) is kept when t - T >= min_w,
  *     q - Q >= min_w, len(r') - (t + k) >= min_w and len(r) - (q + k) >= min_w, with (T, Q) the end of
  *     the last kept anchor's k-mer (initially 0, 0);
@@ -647,12 +648,6 @@ static int cmp_mm_key(const void *a, const void *b) {
 
 typedef struct { int32_t t, q; } seed_anchor;
 
-static int cmp_anchor(const void *a, const void *b) {
-    const seed_anchor *x = (const seed_anchor *)a, *y = (const seed_anchor *)b;
-    if (x->t != y->t) return x->t < y->t ? -1 : 1;
-    return x->q > y->q ? -1 : (x->q < y->q);
-}
-
 /* the kept partition anchors (k-mer starts in t and q) of read q against the previous read t */
 int poa_ref_seed_partition(const uint8_t *t, int tlen, const uint8_t *q, int qlen, int k, int w, int min_w,
                            int32_t *par_t, int32_t *par_q, int cap) {
@@ -674,22 +669,21 @@ int poa_ref_seed_partition(const uint8_t *t, int tlen, const uint8_t *q, int qle
             int e = lo;
             while (e < nt && mt[e].h == mq[i].h && mt[e].z == mq[i].z) ++e;
             if (e - lo == 0 || e - lo > SEED_MAX_OCC) continue;
-            for (int x = lo; x < e; ++x) {
+            for (int x = e - 1; x >= lo; --x) { /* anchors in (q ascending, t descending) order */
                 an[na].t = mt[x].pos;
                 an[na].q = mq[i].pos;
                 ++na;
             }
         }
-        qsort(an, (size_t)na, sizeof(seed_anchor), cmp_anchor);
-        /* longest strictly increasing subsequence of q (t is strictly increasing along it by the order) */
+        /* longest strictly increasing subsequence of t (q is strictly increasing along it by the order) */
         int *tail = (int *)malloc(sizeof(int) * (size_t)(na + 1));
         int *prev = (int *)malloc(sizeof(int) * (size_t)(na + 1));
         int L = 0;
         for (int i = 0; i < na; ++i) {
-            int lo = 0, hi = L; /* leftmost pile whose tail q >= an[i].q */
+            int lo = 0, hi = L; /* leftmost pile whose tail t >= an[i].t */
             while (lo < hi) {
                 const int mid = (lo + hi) / 2;
-                if (an[tail[mid]].q < an[i].q) lo = mid + 1;
+                if (an[tail[mid]].t < an[i].t) lo = mid + 1;
                 else hi = mid;
             }
             prev[i] = lo > 0 ? tail[lo - 1] : -1;

@@ -38,7 +38,7 @@ def test_define_gpu_equals_cpu_restatement(gpu_ctx, tmp_path):
     assert hashlib.sha256(gpu_r2i).hexdigest() == GOLD["seeds"]["0"]["reads2isoforms_sha256"]
     assert st["poa_groups"] > 20
     _run(d, info["gtf"], orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
-         consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g))
+         consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd))
     assert read("Isoform_Consensi.fasta") == gpu_fa
     assert read("reads2isoforms.txt") == gpu_r2i
 

@@ -12,9 +12,9 @@ from tests import poa_cases
 pytestmark = pytest.mark.gpu
 
 
-def _check(groups):
-    got, gcells = poa.poa_consensus_batch(groups, return_cells=True)
-    want, wcells = opoa.consensus_batch(groups, return_cells=True)
+def _check(groups, seeding=None):
+    got, gcells = poa.poa_consensus_batch(groups, return_cells=True, seeding=seeding)
+    want, wcells = opoa.consensus_batch(groups, return_cells=True, seeding=seeding)
     bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
     assert not bad, f"{len(bad)} groups differ, first {bad[:5]}"
     assert np.array_equal(gcells, wcells)
@@ -74,8 +74,35 @@ def test_mixed_lengths_one_batch():
 
 
 def test_config5_deep_long_group():
-    """Config-5 shape: one isoform of 100 reads x ~8.5 kb (what the reference hands `abpoa -S`)."""
-    _check(poa_cases.noisy_groups(1, (8300, 8700), (100, 100), seed=55)[1])
+    """Config-5 shape: one isoform of 100 reads x ~8.5 kb, run through the -S path the reference takes
+    for it (median length >= 8000 -> `abpoa -S`, SpliceDefineConsensus.py:915-919): seed kernel
+    partition + window DPs, byte-equal to the oracle's -S restatement, with far fewer DP cells than
+    the unseeded alignment of the same group."""
+    g = poa_cases.noisy_groups(1, (8300, 8700), (100, 100), seed=55)[1]
+    _, seeded_cells = opoa.consensus_batch(g, return_cells=True, seeding=[1])
+    _, full_cells = opoa.consensus_batch(g, return_cells=True)
+    assert seeded_cells[0] < full_cells[0] / 3  # the seeded path ran (windows, not one 8.5 kb band)
+    _check(g, seeding=[1])
+
+
+def test_seeded_groups_mixed_with_unseeded():
+    """-S and plain groups in one call (two launches: the seeded and unseeded kernel instantiations),
+    short seeded groups (no anchors: plain DP), N runs, and a read sharing no k-mer with its
+    predecessor (one window)."""
+    _, long_g = poa_cases.noisy_groups(6, (5000, 9000), (4, 12), seed=61)
+    _, short_g = poa_cases.noisy_groups(6, (200, 900), (3, 8), seed=62)
+    rng = np.random.default_rng(63)
+    t = synth.random_template(rng, 4000).tobytes().decode()
+    u = synth.random_template(rng, 3000).tobytes().decode()
+    odd = [[t, t[:1500] + "N" * 40 + t[1540:], u, t, t[:2000] + t[2100:]]]
+    groups = long_g + short_g + odd + long_g[:2]
+    seeding = [1] * 6 + [1, 0, 1, 0, 1, 0] + [1] + [0, 0]
+    _check(groups, seeding=seeding)
+
+
+def test_seeded_32bit_rows(monkeypatch):
+    monkeypatch.setenv("MANDO_POA_DBG", "1")
+    _check(poa_cases.noisy_groups(3, (6000, 8000), (5, 10), seed=64)[1], seeding=[1, 1, 1])
 
 
 def test_config3_full_size_properties():
