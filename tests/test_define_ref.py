@@ -1,0 +1,79 @@
+"""The D module against the UNMODIFIED reference run end to end with real consensi and orientation
+(tests/golden/define_vectors.json, made by tests/golden/make_define_vectors.py): 35-40 % '-' strand
+records, >100-read isoforms (subsample cap), 8-11 kb loci that take abPOA's `-S` branch.
+
+* CPU (not gpu): the driver with the oracle's orientation and POA injected must write the reference's
+  exact Isoform_Consensi.fasta / reads2isoforms.txt — pins rebinding, revcomp, fallbacks, `-S`
+  selection and the writer against the reference's own code.
+* GPU: the product path (HIP orientation + HIP POA) must write the same bytes.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+
+import pytest
+
+from mandalorion_amd import define, synth
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "define_vectors.json")))
+P = GOLD["params"]
+
+
+def sha(path):
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()
+
+
+def _dataset(tmp_path, name):
+    spec = dict(GOLD["datasets"][name]["synth"])
+    n = spec.pop("n_loci")
+    d = str(tmp_path / name)
+    recs = synth.write_loci(os.path.join(d, "tmp_SS"), n, threads=4, **spec)
+    inp = GOLD["datasets"][name]["inputs"]
+    assert recs == inp["records"]
+    got = {f: sha(os.path.join(d, "tmp_SS", f)) for f in sorted(os.listdir(os.path.join(d, "tmp_SS")))}
+    assert got == inp["psl_sha256"], "synthetic input differs from the one the reference ran on"
+    return d
+
+
+def _run(d, **kw):
+    return define.define_isoforms(d, cutoff=P["cutoff"], genome_file="None", splice_site_width=P["splice_site_width"],
+                                  minimum_read_count=P["minimum_read_count"],
+                                  white_list_polyA=P["white_list_polyA"].split(","), threads=8,
+                                  junctions=P["junctions"], upstream_buffer=P["upstream_buffer"],
+                                  downstream_buffer=P["downstream_buffer"], seed=GOLD["seed"], **kw)
+
+
+def _check(d, name, st):
+    ref = GOLD["datasets"][name]["reference"]
+    headers = [l[1:].rstrip("\n") for l in open(os.path.join(d, "Isoform_Consensi.fasta")) if l.startswith(">")]
+    assert headers == ref["isoform_headers"]
+    assert sha(os.path.join(d, "reads2isoforms.txt")) == ref["reads2isoforms_sha256"]
+    assert sha(os.path.join(d, "Isoform_Consensi.fasta")) == ref["isoform_consensi_sha256"]
+    assert st["poa_groups"] == ref["n_abpoa_calls"]
+
+
+@pytest.mark.parametrize("name", sorted(GOLD["datasets"]))
+def test_driver_with_oracle_equals_reference(tmp_path, name):
+    from oracle import orient as oref
+    from oracle import poa as opoa
+
+    d = _dataset(tmp_path, name)
+    seeded = []
+
+    def cons(s, o, g, sd):
+        seeded.append(int(sd.sum()) if sd is not None else 0)
+        return opoa.consensus_packed(s, o, g, seeding=sd)
+
+    st = _run(d, orient_fn=lambda s, o, g: oref.orient_packed(s, o, g), consensus_fn=cons)
+    _check(d, name, st)
+    assert sum(seeded) == GOLD["datasets"][name]["reference"]["n_seeded_calls"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(GOLD["datasets"]))
+def test_gpu_driver_equals_reference(gpu_ctx, tmp_path, name):
+    d = _dataset(tmp_path, name)
+    st = _run(d)
+    _check(d, name, st)
