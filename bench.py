@@ -39,10 +39,20 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
 
 WORKLOADS = {
+    # BASELINE.json configs[1]: SIRV-like spike-in set, 7 genes x ~10 isoforms, ~50k R2C2 reads
+    "config2": dict(loci=7, reads=(6500, 7500), exons=(10, 14), exon_len=(60, 200), isoforms=(9, 11), pacbio_frac=0.0,
+                    rev_frac=0.3,
+                    text="config2: SIRV-like, 7 loci x ~7,000 synthetic R2C2 reads (10-14 exons of 60-200 nt, 9-11 "
+                         "isoforms/locus, 30% '-' strand), ~50k PSL records, Mando.py -M D"),
     # BASELINE.json configs[2]: 1M synthetic ~3 kb R2C2 reads over 20k loci
     "config3": dict(loci=20000, reads=(50, 50), exon_len=(200, 500), pacbio_frac=0.0, rev_frac=0.3,
                     text="config3: 20,000 loci x 50 synthetic R2C2 reads (~3 kb, 5-12 exons of 200-500 nt, "
                          "1-3 isoforms/locus, 30% '-' strand), 1M PSL records, Mando.py -M D"),
+    # BASELINE.json configs[4]: stress, 200-read-deep loci at ~8 kb (POA sees 100 per isoform, abPOA -S)
+    "config5": dict(loci=100, reads=(200, 200), exons=(8, 10), exon_len=(850, 1000), isoforms=(1, 1), pacbio_frac=0.0,
+                    rev_frac=0.3,
+                    text="config5: 100 loci x 200 synthetic R2C2 reads of ~8.5 kb (1 isoform/locus, subsampled to "
+                         "100, median >= 8000 nt -> -S), 20k PSL records, Mando.py -M D"),
     # BASELINE.json configs[3]: 10M mixed R2C2 + PacBio 2-4 kb reads (~200k gencode-like loci)
     "config4": dict(loci=200000, reads=(40, 60), exon_len=(130, 570), pacbio_frac=0.2, rev_frac=0.5,
                     text="config4: 200,000 loci x 40-60 synthetic reads (2-4 kb, 80% R2C2 / 20% PacBio error "
@@ -73,8 +83,9 @@ def gen_data(d: str, wl: dict, n_loci: int, threads: int) -> int:
     if os.path.exists(marker):
         return int(open(marker).read())
     shutil.rmtree(os.path.join(d, "tmp_SS"), ignore_errors=True)
+    extra = {k: wl[k] for k in ("exons", "isoforms") if k in wl}
     n = synth.write_loci(os.path.join(d, "tmp_SS"), n_loci, reads=wl["reads"], exon_len=wl["exon_len"],
-                         threads=threads, pacbio_frac=wl["pacbio_frac"], rev_frac=wl["rev_frac"])
+                         threads=threads, pacbio_frac=wl["pacbio_frac"], rev_frac=wl["rev_frac"], **extra)
     with open(marker + ".tmp", "w") as fh:
         fh.write(str(n))
     os.replace(marker + ".tmp", marker)

@@ -33,6 +33,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 REF = "/root/reference"
+DST = os.path.join(os.path.dirname(os.path.abspath(__file__)), "define_vectors.json")
 SEED = 0
 PARAMS = dict(cutoff=0.1, splice_site_width=1, minimum_read_count=2, junctions="gtag,gcag,atac,ctac,ctgc,gtat",
               upstream_buffer=10, downstream_buffer=50, white_list_polyA="0")
@@ -40,6 +41,9 @@ PARAMS = dict(cutoff=0.1, splice_site_width=1, minimum_read_count=2, junctions="
 DATASETS = {
     "r2c2_rev": dict(n_loci=48, reads=(6, 40), exons=(4, 10), exon_len=(150, 400), rev_frac=0.35, seed=4242),
     "deep": dict(n_loci=6, reads=(110, 170), exons=(3, 6), exon_len=(120, 300), rev_frac=0.4, seed=99),
+    # BASELINE configs[1] shape: SIRV-like, 7 genes x ~10 isoforms, ~50k reads (~7,000 per locus)
+    "sirv_like": dict(n_loci=7, reads=(6500, 7500), exons=(10, 14), exon_len=(60, 200), isoforms=(9, 11),
+                      rev_frac=0.3, seed=20250117),
     "long_seeded": dict(n_loci=3, reads=(5, 9), exons=(8, 10), exon_len=(950, 1150), rev_frac=0.3, seed=777),
 }
 
@@ -154,7 +158,12 @@ def main():
         open(ab, "w").write(ORACLE_ABPOA.format(py=sys.executable, root=ROOT))
         os.chmod(ab, 0o755)
         open(os.path.join(tools, "runner.py"), "w").write(RUNNER)
+        only = sys.argv[1:] or list(DATASETS)
+        if os.path.exists(DST):  # keep datasets not regenerated in this run
+            out["datasets"] = {k: v for k, v in json.load(open(DST))["datasets"].items() if k not in only}
         for name, kw in DATASETS.items():
+            if name not in only:
+                continue
             d = os.path.join(tmp, name)
             os.makedirs(d)
             inputs = write_dataset(d, kw)
@@ -162,9 +171,9 @@ def main():
             out["datasets"][name] = {"synth": kw, "inputs": inputs, "reference": res}
             print(name, inputs["records"], "records;", res["n_abpoa_calls"], "abpoa calls,",
                   res["n_seeded_calls"], "with -S")
-    dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "define_vectors.json")
-    json.dump(out, open(dst, "w"), indent=1)
-    print("wrote", dst)
+    out["datasets"] = {k: out["datasets"][k] for k in DATASETS if k in out["datasets"]}
+    json.dump(out, open(DST, "w"), indent=1)
+    print("wrote", DST)
 
 
 if __name__ == "__main__":

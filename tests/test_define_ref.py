@@ -77,3 +77,84 @@ def test_gpu_driver_equals_reference(gpu_ctx, tmp_path, name):
     d = _dataset(tmp_path, name)
     st = _run(d)
     _check(d, name, st)
+
+
+# ---------------------------------------------------------------------------------------------
+# sharded runs: loci LPT-sharded over 2 ranks, one all-gather to rank 0's writer
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard_rank(rank, world, port, d, use_oracle, q):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from mandalorion_amd.comm import Comm
+
+    kw = {}
+    if use_oracle:
+        from oracle import orient as oref
+        from oracle import poa as opoa
+
+        kw = dict(orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
+                  consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd))
+    with Comm(world, rank, "127.0.0.1", port, timeout_s=120) as c:  # host transport (one GPU or none)
+        st = _run(d, comm=c, **kw)
+        q.put((rank, st["isoforms"], c.backend))
+
+
+def _sharded(d, use_oracle, world=2):
+    import multiprocessing as mp
+
+    for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt"):
+        if os.path.exists(os.path.join(d, f)):
+            os.remove(os.path.join(d, f))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_shard_rank, args=(r, world, port, d, use_oracle, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    assert all(g[1] > 0 for g in got)  # every rank got loci
+    return got
+
+
+def test_sharded_two_ranks_equals_reference(tmp_path):
+    d = _dataset(tmp_path, "r2c2_rev")
+    _sharded(d, use_oracle=True)
+    ref = GOLD["datasets"]["r2c2_rev"]["reference"]
+    assert sha(os.path.join(d, "reads2isoforms.txt")) == ref["reads2isoforms_sha256"]
+    assert sha(os.path.join(d, "Isoform_Consensi.fasta")) == ref["isoform_consensi_sha256"]
+
+
+# BASELINE configs[3] shape (10M mixed R2C2 + PacBio 2-4 kb, sharded): a small slice of it
+CONFIG4_SLICE = dict(reads=(40, 60), exons=(5, 12), exon_len=(130, 570), pacbio_frac=0.2, rev_frac=0.5, seed=4)
+
+
+@pytest.mark.gpu
+def test_gpu_config4_slice_sharded_equals_one_rank(gpu_ctx, tmp_path):
+    d = str(tmp_path / "c4")
+    synth.write_loci(os.path.join(d, "tmp_SS"), 96, threads=8, **CONFIG4_SLICE)
+    _run(d)
+    one = [open(os.path.join(d, f), "rb").read() for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt")]
+    _sharded(d, use_oracle=False)
+    two = [open(os.path.join(d, f), "rb").read() for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt")]
+    assert one == two
+    # and the one-rank GPU files equal the CPU restatements' on the same slice
+    from oracle import orient as oref
+    from oracle import poa as opoa
+
+    _run(d, orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
+         consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd))
+    assert [open(os.path.join(d, f), "rb").read() for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt")] == one
