@@ -174,14 +174,17 @@ def cpu_baseline(data: str, n_loci: int, threads: int):
     of, cf, pool = cpu_fns(threads)
     try:
         t0 = time.perf_counter()
-        st = run_define(d, threads, 0, orient_fn=of, consensus_fn=cf)
+        from oracle import cluster as ocl
+
+        st = run_define(d, threads, 0, orient_fn=of, consensus_fn=cf, cluster_fn=ocl.cluster_loci)
         wall = time.perf_counter() - t0
     finally:
         pool.shutdown()
     out = {"value": recs / wall, "unit": "records/s", "cores": threads, "kind": "port",
            "sample": f"first {n_loci} loci ({recs} PSL records, {st['poa_reads']} POA reads) of this workload through "
                      f"the same D driver with oracle/orient_ref.c + oracle/poa_ref.c (C restatements of mappy "
-                     f"map-ont and abPOA v1.4.1) on {threads} host threads, clustering on the host; {wall:.1f} s wall"}
+                     f"map-ont and abPOA v1.4.1) and oracle/cluster_ref.cpp (clustering) on {threads} host threads; "
+                     f"{wall:.1f} s wall"}
     hashes = (sha(os.path.join(d, "Isoform_Consensi.fasta")), sha(os.path.join(d, "reads2isoforms.txt")))
     return out, d, hashes
 

@@ -117,9 +117,12 @@ int mando_mt_permutation(uint32_t seed, const int64_t *ns, const int64_t *ks, in
                          int64_t *out, int64_t out_cap);
 
 /* ------------------------------------------------------------------------------------------------
- * Per-locus read clustering (host C++, one locus per worker thread).  Replaces the clustering half of
- * process_locus (/root/reference/defineIsoforms.py:55-91 -> SpliceDefineConsensus.py:278-868) and the
- * subsample draw of determine_consensus (SpliceDefineConsensus.py:884-888).  Every locus replays the
+ * Per-locus read clustering on the GPU: host threads read the locus files, then two HIP kernels run one
+ * locus per 64-lane wave (parse + cs tokenisation; peaks, identities, isoform groups).  Replaces the
+ * clustering half of process_locus (/root/reference/defineIsoforms.py:55-91 -> SpliceDefineConsensus.py
+ * :107-868) and the subsample draw of determine_consensus (SpliceDefineConsensus.py:884-888), i.e. the
+ * reference's per-locus Pool worker minus mappy/abPOA.  ctx: the device (its stream runs the kernels;
+ * the call blocks until the results are on the host).  Every locus replays the
  * numpy legacy RNG stream of RandomState(seed), which is what each forked locus worker of the
  * reference sees when its parent seeded numpy (defineIsoforms.py:130).
  * ---------------------------------------------------------------------------------------------- */
@@ -131,7 +134,7 @@ typedef struct {
     int32_t downstream_buffer;  /* -d (50) */
     const char *junctions;      /* -j, comma separated ("gtag,gcag,atac,ctac,ctgc,gtat") */
     uint32_t seed;              /* numpy global RNG seed every locus starts from */
-    int32_t threads;            /* host worker threads (0 = all hardware threads) */
+    int32_t threads;            /* host threads reading the locus files (0 = all hardware threads) */
     int32_t poa_subsample;      /* determine_consensus subsample size (100) */
 } mando_cluster_params;
 
@@ -169,7 +172,7 @@ void mando_cluster_default_params(mando_cluster_params *p);
 /* psl_paths[i]: locus file tmp_SS/<chrom~start~end>.psl; chroms[i]: its chrom.  Annotated splice
  * bounds inside the locus (defineIsoforms.py:140-150) as 4 lists per locus (left '5', left '3',
  * right '5', right '3'): ann_pos[ann_off[4i+s] .. ann_off[4i+s+1]); both may be NULL. */
-int mando_cluster_loci(const mando_cluster_params *params, const char *const *psl_paths,
+int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *params, const char *const *psl_paths,
                        const char *const *chroms, int64_t n_loci, const int64_t *ann_pos,
                        const int64_t *ann_off, mando_cluster_result **out);
 int mando_cluster_view_get(const mando_cluster_result *res, mando_cluster_view *view);

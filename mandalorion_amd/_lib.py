@@ -180,7 +180,7 @@ def load(path: str | None = None):
         lib.mando_mt_permutation.argtypes = [ctypes.c_uint32, _P, _P, _I64, _P, _I64]
         lib.mando_cluster_default_params.argtypes = [_P]
         lib.mando_cluster_default_params.restype = None
-        lib.mando_cluster_loci.argtypes = [_P, _P, _P, _I64, _P, _P, _P]
+        lib.mando_cluster_loci.argtypes = [_P, _P, _P, _P, _I64, _P, _P, _P]
         lib.mando_cluster_view_get.argtypes = [_P, _P]
         lib.mando_cluster_free.argtypes = [_P]
         lib.mando_cluster_free.restype = None

@@ -1,4 +1,5 @@
-"""Per-locus read clustering (libmando `mando_cluster_loci`, host C++ threads).
+"""Per-locus read clustering on the GPU (libmando `mando_cluster_loci`: host threads read the locus
+files, two HIP kernels cluster one locus per wave, csrc/cluster_kernel.hip).
 
 Replaces the clustering half of the reference's `process_locus`
 (/root/reference/defineIsoforms.py:55-91: collect_reads, make_genome_bins, find_peaks,
@@ -41,13 +42,15 @@ def _arr(p, n, dtype):
 
 
 class ClusterResult:
-    """Owns a mando_cluster_result; arrays are copied out, the text buffer is viewed in place."""
+    """Owns a mando_cluster_result; arrays are copied out, the text buffer is viewed in place.
+    view_get / free default to libmando's (the oracle passes its own)."""
 
-    def __init__(self, handle: ctypes.c_void_p):
+    def __init__(self, handle: ctypes.c_void_p, view_get=None, free=None):
         self._lib = _lib.load()
         self._h = handle
+        self._free = free or self._lib.mando_cluster_free
         v = _lib.ClusterView()
-        _lib.check(self._lib.mando_cluster_view_get(handle, ctypes.byref(v)))
+        _lib.check((view_get or self._lib.mando_cluster_view_get)(handle, ctypes.byref(v)))
         self.n_loci = v.n_loci
         self.n_records = v.n_records
         self.locus_status = _arr(v.locus_status, v.n_loci, np.int32)
@@ -75,7 +78,7 @@ class ClusterResult:
 
     def close(self):
         if self._h is not None:
-            self._lib.mando_cluster_free(self._h)
+            self._free(self._h)
             self._h = None
             self.text = np.zeros(0, dtype=np.uint8)
 
@@ -109,25 +112,26 @@ class ClusterResult:
                      float(self.peak_prop[k])) for k in idx]
 
 
-def cluster_loci(paths: list[str], chroms: list[str], ann: list[list[list[int]]] | None = None,
-                 cutoff: float = 0.1, splice_site_width: int = 1, minimum_read_count: int = 2,
-                 upstream_buffer: int = 10, downstream_buffer: int = 50,
-                 junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", seed: int = 0, threads: int = 0,
-                 poa_subsample: int = 100) -> ClusterResult:
-    """Cluster every locus file.  ann[i] = [left '5', left '3', right '5', right '3'] position lists."""
-    lib = _lib.load()
+def cluster_params(cutoff: float = 0.1, splice_site_width: int = 1, minimum_read_count: int = 2,
+                   upstream_buffer: int = 10, downstream_buffer: int = 50,
+                   junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", seed: int = 0, threads: int = 0,
+                   poa_subsample: int = 100):
     p = _lib.ClusterParams()
-    lib.mando_cluster_default_params(ctypes.byref(p))
+    _lib.load().mando_cluster_default_params(ctypes.byref(p))
     p.cutoff = cutoff
     p.splice_site_width = splice_site_width
     p.minimum_read_count = minimum_read_count
     p.upstream_buffer = upstream_buffer
     p.downstream_buffer = downstream_buffer
-    jb = junctions.encode()
-    p.junctions = jb
+    p.junctions = junctions.encode()  # ctypes keeps the bytes alive with the struct
     p.seed = seed & 0xFFFFFFFF
     p.threads = threads
     p.poa_subsample = poa_subsample
+    return p
+
+
+def c_inputs(paths: list[str], chroms: list[str], ann):
+    """ctypes arrays of the locus paths / chroms and the flattened annotated bounds."""
     n = len(paths)
     cpaths = (ctypes.c_char_p * max(n, 1))(*[x.encode() for x in paths])
     cchroms = (ctypes.c_char_p * max(n, 1))(*[x.encode() for x in chroms])
@@ -140,7 +144,18 @@ def cluster_loci(paths: list[str], chroms: list[str], ann: list[list[list[int]]]
                 off.append(len(flat))
         ann_pos = np.asarray(flat if flat else [0], dtype=np.int64)
         ann_off = np.asarray(off, dtype=np.int64)
+    return n, cpaths, cchroms, ann_pos, ann_off
+
+
+def cluster_loci(paths: list[str], chroms: list[str], ann: list[list[list[int]]] | None = None,
+                 device: int = 0, slot: int = 4, **params) -> ClusterResult:
+    """Cluster every locus file on the GPU.  ann[i] = [left '5', left '3', right '5', right '3'] position
+    lists; params as cluster_params (threads: host threads reading the files)."""
+    lib = _lib.load()
+    p = cluster_params(**params)
+    n, cpaths, cchroms, ann_pos, ann_off = c_inputs(paths, chroms, ann)
+    ctx = _lib.context(device, slot=slot)
     h = ctypes.c_void_p()
-    _lib.check(lib.mando_cluster_loci(ctypes.byref(p), cpaths, cchroms, n, _lib.ptr(ann_pos), _lib.ptr(ann_off),
-                                      ctypes.byref(h)))
+    _lib.check(lib.mando_cluster_loci(ctx.handle, ctypes.byref(p), cpaths, cchroms, n, _lib.ptr(ann_pos),
+                                      _lib.ptr(ann_off), ctypes.byref(h)))
     return ClusterResult(h)

@@ -1,0 +1,2413 @@
+// cluster_kernel.hip — per-locus read clustering of the D module on the GPU (gfx950).
+//
+// Restates the clustering half of the reference's process_locus (/root/reference/defineIsoforms.py:55-91)
+// as two kernels, one 64-lane wave per locus (the workgroup is that one wave, so __syncthreads() is a
+// wave-local barrier + fence):
+//   cluster_parse  PSL text -> records (SDC:278-331 field use), blocks, and every cs string tokenised
+//                  into run-length records (getCSaroundSS, SDC:107-161)
+//   cluster_locus  collect_reads (SDC:278-331), make_genome_bins (:392-438), find_peaks /
+//                  scan_for_best_bin / determine_cov (:232-275, :163-224), characterize_splicing_event
+//                  (:499-550), spliceDict (defineIsoforms.py:71-83), sort_reads_into_splice_junctions
+//                  (:714-769), group_mono_exon_transcripts (:772-794), define_start_end_sites / find_ends
+//                  (:797-868, :554-711) and determine_consensus's subsample draw (:884-888)
+// Control that the reference runs in RNG order (candidate peaks, identities, isoforms) stays in that
+// order and is executed wave-uniformly; the data-parallel parts (text scans, per-read work, window
+// sums, the coverage merge, the sampled junction queries, sorts) are spread over the lanes.  The
+// numpy RandomState stream (MT19937) lives in LDS and is refilled by the wave.
+// Semantics follow oracle/cluster_ref.cpp (the host restatement pinned byte-for-byte against the
+// reference by tests/golden/*_vectors.json), which the GPU tests compare against locus by locus.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cluster_gpu.h"
+#include "internal.h"
+#include "mt19937.h"
+
+namespace mando {
+namespace cl {
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// wave helpers (one workgroup == one wave of 64 lanes)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int ln() { return (int)threadIdx.x; }
+
+template <class T>
+__device__ __forceinline__ T wsum(T v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+template <class T>
+__device__ __forceinline__ T wmax(T v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const T t = __shfl_xor(v, o);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+template <class T>
+__device__ __forceinline__ T wmin(T v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const T t = __shfl_xor(v, o);
+        v = t < v ? t : v;
+    }
+    return v;
+}
+// inclusive prefix sum over the lanes
+template <class T>
+__device__ __forceinline__ T wincl(T v) {
+    for (int o = 1; o < 64; o <<= 1) {
+        const T t = __shfl_up(v, o);
+        if (ln() >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+__host__ __device__ __forceinline__ int64_t al256(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+__device__ __forceinline__ bool is_space6(uint8_t c) { return c == ' ' || (c >= 9 && c <= 13); }  // C isspace
+__device__ __forceinline__ bool is_trim4(uint8_t c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
+__device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
+__device__ __forceinline__ bool is_op(uint8_t c) {
+    return c == '=' || c == '+' || c == '-' || c == '*' || c == '~' || c == '\\';
+}
+
+// Python int() as the host restatement parses it: surrounding ' ' '\t' '\r' '\n', a sign, digits, '_'
+__device__ int64_t to_i64(const uint8_t *s, int a, int b, bool &ok) {
+    while (a < b && is_trim4(s[a])) ++a;
+    while (b > a && is_trim4(s[b - 1])) --b;
+    if (a == b) {
+        ok = false;
+        return 0;
+    }
+    bool neg = false;
+    if (s[a] == '+' || s[a] == '-') {
+        neg = s[a] == '-';
+        ++a;
+    }
+    if (a == b) {
+        ok = false;
+        return 0;
+    }
+    int64_t v = 0;
+    for (int i = a; i < b; ++i) {
+        const uint8_t c = s[i];
+        if (c == '_') continue;
+        if (!is_digit(c)) {
+            ok = false;
+            return 0;
+        }
+        v = v * 10 + (c - '0');
+    }
+    return neg ? -v : v;
+}
+
+// float(accuracy) < 0.9 (SDC:321), decided exactly on the decimal text: the double nearest the text
+// is below 0.9 iff the text is <= the midpoint between 0.9 and its predecessor (ties go to the even
+// predecessor).  Accepts what float() accepts in a PSL column: sign, digits with an optional point,
+// an exponent, inf / nan; anything else is a parse error.
+__device__ bool acc_below_09(const uint8_t *s, int a, int b, bool &ok) {
+    const char *kMid = "899999999999999966693309261245303787291049957275390625";  // digits of 0.8999...625
+    constexpr int kMidN = 54;
+    int i = a;
+    while (i < b && is_space6(s[i])) ++i;
+    int e_ = b;
+    while (e_ > i && is_space6(s[e_ - 1])) --e_;
+    b = e_;
+    bool neg = false;
+    if (i < b && (s[i] == '+' || s[i] == '-')) {
+        neg = s[i] == '-';
+        ++i;
+    }
+    auto low = [&](int k) -> uint8_t {
+        const uint8_t c = s[k];
+        return (c >= 'A' && c <= 'Z') ? (uint8_t)(c + 32) : c;
+    };
+    if (i + 3 <= b && low(i) == 'i' && low(i + 1) == 'n' && low(i + 2) == 'f') {
+        if (!((b == i + 3) || (b == i + 8 && low(i + 3) == 'i' && low(i + 4) == 'n' && low(i + 5) == 'i' &&
+                               low(i + 6) == 't' && low(i + 7) == 'y')))
+            ok = false;
+        return neg;
+    }
+    if (i + 3 == b && low(i) == 'n' && low(i + 1) == 'a' && low(i + 2) == 'n') return false;
+    const int is0 = i;
+    while (i < b && (is_digit(s[i]) || (s[i] == '_' && i > is0 && i + 1 < b && is_digit(s[i - 1]) && is_digit(s[i + 1])))) ++i;
+    const int ie = i;
+    int fs = -1, fe = -1;
+    if (i < b && s[i] == '.') {
+        ++i;
+        fs = i;
+        while (i < b && (is_digit(s[i]) || (s[i] == '_' && i > fs && i + 1 < b && is_digit(s[i - 1]) && is_digit(s[i + 1])))) ++i;
+        fe = i;
+    }
+    // digits only (underscores skipped)
+    auto ndig = [&](int x, int y) {
+        int c = 0;
+        for (int k = x; k < y; ++k) c += is_digit(s[k]);
+        return c;
+    };
+    const int ni = ndig(is0, ie), nf = fs >= 0 ? ndig(fs, fe) : 0;
+    if (ni + nf == 0) {
+        ok = false;
+        return false;
+    }
+    int64_t ex = 0;
+    if (i < b && (s[i] == 'e' || s[i] == 'E')) {
+        int j = i + 1;
+        bool en = false;
+        if (j < b && (s[j] == '+' || s[j] == '-')) {
+            en = s[j] == '-';
+            ++j;
+        }
+        if (j < b && is_digit(s[j])) {
+            while (j < b && (is_digit(s[j]) || (s[j] == '_' && j + 1 < b && is_digit(s[j + 1])))) {
+                if (is_digit(s[j]) && ex < 100000000) ex = ex * 10 + (s[j] - '0');
+                ++j;
+            }
+            if (en) ex = -ex;
+            i = j;
+        } else {
+            ok = false;
+            return false;
+        }
+    }
+    if (i != b) {  // trailing characters: ValueError in float()
+        ok = false;
+        return false;
+    }
+    // k-th digit of the concatenated integer and fraction digits
+    auto dig = [&](int k) -> int {
+        int x = is0, y = ie;
+        if (k >= ni) {
+            k -= ni;
+            x = fs;
+            y = fe;
+        }
+        for (int p = x; p < y; ++p)
+            if (is_digit(s[p])) {
+                if (k == 0) return s[p] - '0';
+                --k;
+            }
+        return 0;
+    };
+    const int nd = ni + nf;
+    int z = 0;
+    while (z < nd && dig(z) == 0) ++z;
+    if (z == nd || neg) return true;  // zero, or negative
+    const int64_t P = (int64_t)ni - z + ex;  // value = 0.d_z d_z+1 ... x 10^P
+    if (P > 0) return false;
+    if (P < 0) return true;
+    for (int k = 0;; ++k) {
+        if (k >= kMidN) {
+            for (int q = z + k; q < nd; ++q)
+                if (dig(q) != 0) return false;
+            return true;
+        }
+        if (z + k >= nd) return true;
+        const int vd = dig(z + k), md = kMid[k] - '0';
+        if (vd != md) return vd < md;
+    }
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t *x, const uint8_t *y, int n) {
+    for (int i = 0; i < n; ++i)
+        if (x[i] != y[i]) return false;
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1: parse
+// ---------------------------------------------------------------------------------------------
+struct ALayout {
+    int32_t *line_end;
+    Rec *recs;
+    int64_t *blk;  // (size, start) pairs
+    int32_t *ops;
+    Run *runs;
+    int32_t *adv_run;
+    int64_t *adv_first;
+};
+
+__device__ __forceinline__ ALayout a_layout(uint8_t *base, const Locus &L) {
+    ALayout A;
+    uint8_t *p = base;
+    A.line_end = (int32_t *)p;
+    p += al256((int64_t)L.line_cap * 4);
+    A.recs = (Rec *)p;
+    p += al256((int64_t)L.line_cap * (int64_t)sizeof(Rec));
+    A.blk = (int64_t *)p;
+    p += al256((int64_t)L.blk_cap * 16);
+    A.ops = (int32_t *)p;
+    p += al256((int64_t)L.op_cap * 4);
+    A.runs = (Run *)p;
+    p += al256((int64_t)L.op_cap * (int64_t)sizeof(Run));
+    A.adv_run = (int32_t *)p;
+    p += al256((int64_t)L.op_cap * 4);
+    A.adv_first = (int64_t *)p;
+    return A;
+}
+
+__global__ __launch_bounds__(64) void cluster_parse(Args G) {
+    const int li = G.order[blockIdx.x];
+    const Locus L = G.loci[li];
+    Stats *st = G.stats + li;
+    const uint8_t *T = G.text + L.text_off;
+    const int64_t n = L.text_len;
+    ALayout A = a_layout(G.scratch_a + L.a_off, L);
+    const uint8_t *lchrom = G.chroms + L.chrom_off;
+
+    // 1. line ends: coalesced 16-byte chunks, newline masks compacted in text order
+    const uintptr_t base = (uintptr_t)T & ~(uintptr_t)15;
+    const int pad0 = (int)((uintptr_t)T - base);
+    const int64_t nch = (pad0 + n + 15) >> 4;
+    int32_t nl = 0;
+    for (int64_t c0 = 0; c0 < nch; c0 += 64) {
+        const int64_t c = c0 + ln();
+        uint32_t m = 0;
+        if (c < nch) {
+            const uint4 v = ((const uint4 *)base)[c];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int64_t pos = c * 16 + k - pad0;
+                if (((w[k >> 2] >> ((k & 3) * 8)) & 0xffu) == '\n' && pos >= 0 && pos < n) m |= 1u << k;
+            }
+        }
+        const int cnt = __popc(m);
+        const int incl = wincl(cnt);
+        int idx = nl + incl - cnt;
+        while (m) {
+            const int k = __ffs(m) - 1;
+            m &= m - 1;
+            if (idx < L.line_cap) A.line_end[idx] = (int32_t)(c * 16 + k - pad0);
+            ++idx;
+        }
+        nl += __shfl(incl, 63);
+    }
+    const bool tail = n > 0 && T[n - 1] != '\n';
+    const int32_t nrec = nl + (tail ? 1 : 0);
+    if (tail && nl < L.line_cap && ln() == 0) A.line_end[nl] = (int32_t)n;
+    if (nrec > L.line_cap) {
+        if (ln() == 0) {
+            st->status = kCapacity;
+            st->n_rec = nrec;
+            st->n_ops = 0;
+            st->n_blk = 0;
+        }
+        return;
+    }
+    wsync();
+
+    // 2. fields 0-21 and the blocks, one record per lane
+    int err = 0;
+    int64_t blk_carry = 0, cov_cap = 0, ident_cap = 0;
+    int64_t span_lo = INT64_MAX, span_hi = INT64_MIN;
+    int32_t hist_l = 0, hist_r = 0, max_nblk = 0;
+    for (int r0 = 0; r0 < nrec; r0 += 64) {
+        const int r = r0 + ln();
+        const bool act = r < nrec;
+        Rec R = {};
+        int nb = 0;
+        int f18a = 0, f18b = 0, f20a = 0, f20b = 0;
+        if (act) {
+            int a = r == 0 ? 0 : A.line_end[r - 1] + 1, b = A.line_end[r];
+            while (a < b && is_space6(T[a])) ++a;
+            while (b > a && is_space6(T[b - 1])) --b;
+            R.line_lo = a;
+            R.line_hi = b;
+            // field k = [fs, fe); we need 8-13, 15, 16, 18, 20, 21 and the start of 22
+            int k = 0, fs = a;
+            // starts / ends of the columns the clustering reads (8-13, 15, 16, 18, 20, 21)
+            int f8a = 0, f8b = 0, f9a = 0, f9b = 0, f10a = 0, f10b = 0, f11a = 0, f11b = 0, f12a = 0, f12b = 0;
+            int f13a = 0, f13b = 0, f15a = 0, f15b = 0, f16a = 0, f16b = 0, f21a = 0, f21b = 0;
+            bool done = false;
+            for (int i = a; i < b && !done; ++i) {
+                if (T[i] == '\t') {
+                    switch (k) {
+                        case 8: f8a = fs; f8b = i; break;
+                        case 9: f9a = fs; f9b = i; break;
+                        case 10: f10a = fs; f10b = i; break;
+                        case 11: f11a = fs; f11b = i; break;
+                        case 12: f12a = fs; f12b = i; break;
+                        case 13: f13a = fs; f13b = i; break;
+                        case 15: f15a = fs; f15b = i; break;
+                        case 16: f16a = fs; f16b = i; break;
+                        case 18: f18a = fs; f18b = i; break;
+                        case 20: f20a = fs; f20b = i; break;
+                        case 21: f21a = fs; f21b = i; break;
+                        default: break;
+                    }
+                    ++k;
+                    fs = i + 1;
+                    if (k == 22) {
+                        R.cs_off = fs;
+                        done = true;
+                    }
+                }
+            }
+            if (!done) {
+                err = 1;
+            } else {
+                bool ok = true;
+                R.dirn = (f8b - f8a == 1 && T[f8a] == '+') ? 0 : (f8b - f8a == 1 && T[f8a] == '-') ? 1 : 2;
+                R.name_off = f9a;
+                R.name_len = f9b - f9a;
+                R.qsize = to_i64(T, f10a, f10b, ok);
+                R.qstart = to_i64(T, f11a, f11b, ok);
+                R.qend = to_i64(T, f12a, f12b, ok);
+                R.chrom_off = f13a;
+                R.chrom_len = f13b - f13a;
+                R.same_chrom = R.chrom_len == L.chrom_len && bytes_eq(T + R.chrom_off, lchrom, L.chrom_len);
+                R.tstart = to_i64(T, f15a, f15b, ok);
+                R.tend = to_i64(T, f16a, f16b, ok);
+                int c18 = 0, c20 = 0;
+                for (int i = f18a; i < f18b; ++i) c18 += T[i] == ',';
+                for (int i = f20a; i < f20b; ++i) c20 += T[i] == ',';
+                if (c18 != c20) ok = false;
+                nb = c18;
+                R.acc_lt = acc_below_09(T, f21a, f21b, ok);
+                if (!ok) err = 1;
+            }
+        }
+        // block offsets: prefix over the lanes
+        const int nbi = act && !err ? nb : 0;
+        const int incl = wincl(nbi);
+        const int64_t boff = blk_carry + incl - nbi;
+        blk_carry += __shfl(incl, 63);
+        R.blk_off = (int32_t)boff;
+        R.nblk = nbi;
+        if (act && !err) {
+            // blocks: str.split(',')[:-1] of columns 18 (sizes) and 20 (starts)
+            const bool room = boff + nb <= L.blk_cap;
+            int64_t cc = 0, lo_cnt = 0, up_cnt = 0;
+            bool ok = true;
+            int pa = f18a, qa = f20a;
+            for (int x = 0; x < nb; ++x) {
+                int pe = pa;
+                while (T[pe] != ',') ++pe;
+                int qe = qa;
+                while (T[qe] != ',') ++qe;
+                const int64_t sz = to_i64(T, pa, pe, ok), bs = to_i64(T, qa, qe, ok);
+                pa = pe + 1;
+                qa = qe + 1;
+                if (room) {
+                    A.blk[2 * (boff + x)] = sz;
+                    A.blk[2 * (boff + x) + 1] = bs;
+                }
+                cc += (sz > 0 ? (sz + 9) / 10 : 0) + 11;
+                lo_cnt += (bs + sz) != R.tend;
+                up_cnt += bs != R.tstart;
+            }
+            if (!ok) err = 1;
+            if (R.same_chrom) {
+                cov_cap += cc;
+                span_lo = R.tstart < span_lo ? R.tstart : span_lo;
+                span_hi = R.tend > span_hi ? R.tend : span_hi;
+                if (!R.acc_lt) {
+                    hist_l += (int32_t)lo_cnt;
+                    hist_r += (int32_t)up_cnt;
+                }
+            }
+            ident_cap += (R.chrom_len + 2 + (int64_t)(nb > 0 ? nb - 1 : 0) * 28 + 7) & ~int64_t(7);
+            max_nblk = nb > max_nblk ? nb : max_nblk;
+            A.recs[r] = R;
+        }
+    }
+    if (wany(err != 0)) {
+        if (ln() == 0) st->status = kParse;
+        return;
+    }
+    const int64_t n_blk = blk_carry;
+    if (n_blk > L.blk_cap) {
+        if (ln() == 0) {
+            st->status = kCapacity;
+            st->n_rec = nrec;
+            st->n_blk = (int32_t)n_blk;
+            st->n_ops = 0;
+        }
+        return;
+    }
+    wsync();
+
+    // 3. per record: the cs column (field 22) up to its tab, the seq column (23) up to the next tab or
+    //    the line end; cs operators compacted in text order (a wave scans 1 KB a step)
+    int64_t op_carry = 0;
+    for (int r = 0; r < nrec; ++r) {
+        const int a = A.recs[r].cs_off, b = A.recs[r].line_hi;
+        const uintptr_t b0 = (uintptr_t)(T + a) & ~(uintptr_t)15;
+        const int64_t first = (int64_t)(b0 - (uintptr_t)T);  // text offset of chunk 0 (<= a)
+        int t1 = -1, t2 = -1;
+        const int64_t op0 = op_carry;
+        for (int64_t c0 = first; c0 < b && t2 < 0; c0 += 1024) {
+            const int64_t c = c0 + 16 * ln();
+            uint32_t tm = 0, om = 0;
+            if (c < b) {
+                const uint4 v = *(const uint4 *)(T + c);
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const uint8_t ch = (uint8_t)((w[k >> 2] >> ((k & 3) * 8)) & 0xffu);
+                    const int64_t pos = c + k;
+                    if (pos < a || pos >= b) continue;
+                    if (ch == '\t') tm |= 1u << k;
+                    if (is_op(ch)) om |= 1u << k;
+                }
+            }
+            // tabs of this step in text order (lanes ascending, bits ascending)
+            const uint64_t has = __ballot(tm != 0);
+            if (has) {
+                if (t1 < 0) {
+                    const int l1 = __ffsll((unsigned long long)has) - 1;
+                    const uint32_t m1 = __shfl(tm, l1);
+                    t1 = (int)(c0 + 16 * l1 + (__ffs(m1) - 1));
+                    // a second tab in the same step
+                    const uint32_t m1r = m1 & (m1 - 1);
+                    if (m1r) {
+                        t2 = (int)(c0 + 16 * l1 + (__ffs(m1r) - 1));
+                    } else {
+                        const uint64_t rest = has & ~((2ull << l1) - 1);
+                        if (rest) {
+                            const int l2 = __ffsll((unsigned long long)rest) - 1;
+                            t2 = (int)(c0 + 16 * l2 + (__ffs(__shfl(tm, l2)) - 1));
+                        }
+                    }
+                } else {
+                    const int l2 = __ffsll((unsigned long long)has) - 1;
+                    t2 = (int)(c0 + 16 * l2 + (__ffs(__shfl(tm, l2)) - 1));
+                }
+            }
+            // operators before the cs column's end
+            if (t1 >= 0) {
+                for (int k = 0; k < 16; ++k)
+                    if ((om >> k) & 1u)
+                        if (c + k >= t1) om &= ~(1u << k);
+            }
+            const int cnt = __popc(om);
+            const int incl = wincl(cnt);
+            int64_t idx = op_carry + incl - cnt;
+            while (om) {
+                const int k = __ffs(om) - 1;
+                om &= om - 1;
+                if (idx < L.op_cap) A.ops[idx] = (int32_t)(c + k);
+                ++idx;
+            }
+            op_carry += __shfl(incl, 63);
+        }
+        if (t1 < 0) {
+            err = 1;  // fewer than 24 columns
+            break;
+        }
+        if (ln() == 0) {
+            Rec &R = A.recs[r];
+            R.cs_len = t1 - a;
+            R.seq_off = t1 + 1;
+            R.seq_len = (t2 >= 0 ? t2 : b) - (t1 + 1);
+            R.op_off = (int32_t)op0;
+            R.nop = (int32_t)(op_carry - op0);
+        }
+    }
+    if (err) {
+        if (ln() == 0) st->status = kParse;
+        return;
+    }
+    if (op_carry > L.op_cap) {
+        if (ln() == 0) {
+            st->status = kCapacity;
+            st->n_rec = nrec;
+            st->n_blk = (int32_t)n_blk;
+            st->n_ops = (int32_t)op_carry;
+        }
+        return;
+    }
+    wsync();
+
+    // 4. runs (cluster.cpp build_cs): one operator per lane, record by record; prefix sums give each
+    //    run's first record index and genome position, advancing runs are compacted with the genome
+    //    position of their first record
+    int64_t run_carry = 0, adv_carry = 0;
+    for (int r = 0; r < nrec; ++r) {
+        const Rec R = A.recs[r];
+        const int cs_end = R.cs_off + R.cs_len;
+        int64_t rec_c = 0, g_c = 0;
+        const int64_t r0 = run_carry, a0 = adv_carry;
+        int bad = 0;
+        for (int j0 = 0; j0 < R.nop; j0 += 64) {
+            const int j = j0 + ln();
+            bool valid = false;
+            Run u = {};
+            if (j < R.nop) {
+                const int p = A.ops[R.op_off + j];
+                const int q = j + 1 < R.nop ? A.ops[R.op_off + j + 1] : cs_end;
+                const int len = q - p - 1;
+                const uint8_t op = T[p];
+                u.st = (char)op;
+                switch (op) {
+                    case '=':
+                    case '-':
+                        u.n = len;
+                        u.step = 1;
+                        break;
+                    case '+':
+                        u.n = len;
+                        u.step = 0;
+                        break;
+                    case '*':
+                        u.n = (len + 1) / 2;
+                        u.step = 1;
+                        break;
+                    case '~': {
+                        u.n = 1;
+                        u.st = '|';
+                        if (len < 4) {
+                            bad = 1;
+                            u.n = 0;
+                            break;
+                        }
+                        bool ok = true;
+                        const int64_t il = to_i64(T, p + 3, q - 2, ok);
+                        if (!ok) {
+                            bad = 1;
+                            u.n = 0;
+                            break;
+                        }
+                        u.step = (int32_t)il;
+                        u.motif[0] = (char)T[p + 1];
+                        u.motif[1] = (char)T[p + 2];
+                        u.motif[2] = (char)T[q - 2];
+                        u.motif[3] = (char)T[q - 1];
+                        break;
+                    }
+                    default:  // '\\'
+                        u.n = 0;
+                }
+                valid = u.n != 0;
+            }
+            const int vi = valid ? 1 : 0;
+            const int v_incl = wincl(vi);
+            const int64_t nn = valid ? u.n : 0, gs = valid ? (int64_t)u.step * u.n : 0;
+            const int64_t n_incl = wincl(nn), g_incl = wincl(gs);
+            const bool adv = valid && (u.step > 0 || u.st == '|');
+            const int ai = adv ? 1 : 0;
+            const int a_incl = wincl(ai);
+            if (valid) {
+                u.rec0 = (int32_t)(rec_c + n_incl - nn);
+                u.g0 = R.tstart + g_c + g_incl - gs;
+                const int64_t ri = run_carry + v_incl - vi;
+                A.runs[ri] = u;
+                if (adv) {
+                    const int64_t ai_ = adv_carry + a_incl - ai;
+                    A.adv_run[ai_] = (int32_t)(ri - r0);
+                    A.adv_first[ai_] = u.g0 + u.step;
+                }
+            }
+            run_carry += __shfl(v_incl, 63);
+            rec_c += __shfl(n_incl, 63);
+            g_c += __shfl(g_incl, 63);
+            adv_carry += __shfl(a_incl, 63);
+        }
+        const bool any_bad = wany(bad != 0);
+        if (ln() == 0) {
+            Rec &W = A.recs[r];
+            W.run_off = (int32_t)r0;
+            W.nrun = (int32_t)(run_carry - r0);
+            W.adv_off = (int32_t)a0;
+            W.nadv = (int32_t)(adv_carry - a0);
+            W.nrec_cs = (int32_t)rec_c;
+            W.cs_bad = any_bad ? 1 : 0;
+        }
+    }
+
+    // 5. statistics for the host (scratch B sizing) and K2
+    cov_cap = wsum(cov_cap);
+    ident_cap = wsum(ident_cap);
+    hist_l = wsum(hist_l);
+    hist_r = wsum(hist_r);
+    span_lo = wmin(span_lo);
+    span_hi = wmax(span_hi);
+    max_nblk = wmax(max_nblk);
+    if (ln() == 0) {
+        st->status = kOk;
+        st->n_rec = nrec;
+        st->n_ops = (int32_t)op_carry;
+        st->n_blk = (int32_t)n_blk;
+        st->n_hist_l = hist_l;
+        st->n_hist_r = hist_r;
+        st->max_nblk = max_nblk;
+        st->span_lo = span_lo;
+        st->span_hi = span_hi;
+        st->cov_cap = cov_cap;
+        st->ident_cap = ident_cap;
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// K2 scratch layout; the host sizes it with the same carve (base == nullptr)
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ int64_t pow2ge(int64_t x) {
+    int64_t p = 64;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+struct Side {          // one side's splice-bound histogram (histo_left_bases / histo_right_bases)
+    uint64_t *sk;      // entry sort keys: (position + bias) << 24 | insertion rank
+    int32_t *erec;     // record of each entry, in sorted (position, insertion) order
+    int32_t *etmp;     // insertion rank -> record; later: first insertion rank -> key index
+    int64_t *ukey;     // distinct positions, ascending
+    int32_t *ulo, *ucnt, *ufirst;
+    int32_t *upmb;     // per key: reads on '+', on '-', on anything else
+    uint64_t *cand;    // candidate order: count descending, then insertion order
+    int32_t H, P, nkeys, ncand;
+};
+
+struct BPtr {
+    int64_t *cov;
+    Side s[2];
+    int32_t *names, *cur, *perm;
+    int64_t *win;
+    uint8_t *areas[2];
+    int32_t *splice, *sc, *ec, *sp, *ep;
+    int64_t *ann;
+    int32_t *lab;
+    uint8_t *ibuf;
+    int32_t *ioff, *ilen;
+    uint64_t *ihash;
+    int8_t *ikind;
+    int32_t *grp;
+    uint64_t *isort;
+    int32_t *msuf, *id_lo, *id_hi, *id_rep, *id_m, *idsort, *msort;
+    uint64_t *ss;
+    int32_t *pa, *pb;
+    int8_t *asg;
+    int32_t *mem_tmp;
+    int64_t total;
+};
+
+struct OPtr {
+    Peak *peaks;
+    int32_t *iso_nmem, *mem, *iso_nsub, *sub;
+    int32_t peak_cap;
+    int64_t total;
+};
+
+__host__ __device__ inline int32_t n_ann_of(const Locus &L) { return L.ann_off[4] - L.ann_off[0]; }
+__host__ __device__ inline int32_t peak_cap_of(const Stats &S, const Locus &L) {
+    return S.n_hist_l + S.n_hist_r + n_ann_of(L) + 8;
+}
+
+__host__ __device__ inline void carve_b(uint8_t *base, const Stats &S, const Locus &L, int w, BPtr &B) {
+    int64_t off = 0;
+    auto take = [&](int64_t bytes) -> uint8_t * {
+        uint8_t *p = base ? base + off : nullptr;
+        off += al256(bytes > 0 ? bytes : 1);
+        return p;
+    };
+    const int64_t n = S.n_rec > 0 ? S.n_rec : 1;
+    const int64_t pn = pow2ge(n);
+    B.cov = (int64_t *)take(S.cov_cap * 8);
+    int64_t hmax = 1;
+    for (int k = 0; k < 2; ++k) {
+        Side &d = B.s[k];
+        d.H = k == 0 ? S.n_hist_l : S.n_hist_r;
+        d.P = (int32_t)pow2ge(d.H);
+        d.nkeys = d.ncand = 0;
+        hmax = d.H > hmax ? d.H : hmax;
+        d.sk = (uint64_t *)take((int64_t)d.P * 8);
+        d.erec = (int32_t *)take((int64_t)d.H * 4);
+        d.etmp = (int32_t *)take((int64_t)d.H * 4);
+        d.ukey = (int64_t *)take((int64_t)d.H * 8);
+        d.ulo = (int32_t *)take((int64_t)d.H * 4);
+        d.ucnt = (int32_t *)take((int64_t)d.H * 4);
+        d.ufirst = (int32_t *)take((int64_t)d.H * 4);
+        d.upmb = (int32_t *)take((int64_t)d.H * 12);
+        d.cand = (uint64_t *)take((int64_t)d.P * 8);
+    }
+    B.names = (int32_t *)take(hmax * 4);
+    B.cur = (int32_t *)take(hmax * 4);
+    B.perm = (int32_t *)take((n > hmax ? n : hmax) * 4);
+    B.win = (int64_t *)take(4 * (4 * (int64_t)w + 1) * 8);
+    B.areas[0] = take(L.map_n);
+    B.areas[1] = take(L.map_n);
+    B.splice = (int32_t *)take(L.map_n * 4);
+    B.sc = (int32_t *)take(L.map_n * 4);
+    B.ec = (int32_t *)take(L.map_n * 4);
+    B.sp = (int32_t *)take(L.map_n * 4);
+    B.ep = (int32_t *)take(L.map_n * 4);
+    B.ann = (int64_t *)take((int64_t)n_ann_of(L) * 8);
+    B.lab = (int32_t *)take((int64_t)peak_cap_of(S, L) * 4);
+    B.ibuf = take(S.ident_cap);
+    B.ioff = (int32_t *)take(n * 4);
+    B.ilen = (int32_t *)take(n * 4);
+    B.ihash = (uint64_t *)take(n * 8);
+    B.ikind = (int8_t *)take(n);
+    B.grp = (int32_t *)take(n * 4);
+    B.isort = (uint64_t *)take(pn * 8);
+    B.msuf = (int32_t *)take(n * 4);
+    B.id_lo = (int32_t *)take(n * 4);
+    B.id_hi = (int32_t *)take(n * 4);
+    B.id_rep = (int32_t *)take(n * 4);
+    B.id_m = (int32_t *)take(n * 4);
+    B.idsort = (int32_t *)take(pn * 4);
+    B.msort = (int32_t *)take(pn * 4);
+    B.ss = (uint64_t *)take(pn * 8);
+    B.pa = (int32_t *)take(n * 4);
+    B.pb = (int32_t *)take(n * 4);
+    B.asg = (int8_t *)take(n);
+    B.mem_tmp = (int32_t *)take(n * 4);
+    B.total = off;
+}
+
+__host__ __device__ inline void carve_o(uint8_t *base, const Stats &S, const Locus &L, OPtr &O) {
+    int64_t off = 0;
+    auto take = [&](int64_t bytes) -> uint8_t * {
+        uint8_t *p = base ? base + off : nullptr;
+        off += al256(bytes > 0 ? bytes : 1);
+        return p;
+    };
+    const int64_t n = S.n_rec > 0 ? S.n_rec : 1;
+    O.peak_cap = peak_cap_of(S, L);
+    O.peaks = (Peak *)take((int64_t)O.peak_cap * (int64_t)sizeof(Peak));
+    O.iso_nmem = (int32_t *)take(n * 4);
+    O.mem = (int32_t *)take(n * 4);
+    O.iso_nsub = (int32_t *)take(n * 4);
+    O.sub = (int32_t *)take(n * 4);
+    O.total = off;
+}
+
+// ---------------------------------------------------------------------------------------------
+// wave sorts (bitonic, in global scratch; P a power of two >= 64)
+// ---------------------------------------------------------------------------------------------
+__device__ void sort_u64(uint64_t *a, int64_t P) {
+    for (int64_t k = 2; k <= P; k <<= 1)
+        for (int64_t j = k >> 1; j > 0; j >>= 1) {
+            for (int64_t i = ln(); i < P; i += 64) {
+                const int64_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t x = a[i], y = a[l];
+                    if ((x > y) == ((i & k) == 0)) {
+                        a[i] = y;
+                        a[l] = x;
+                    }
+                }
+            }
+            wsync();
+        }
+}
+
+// indices with a strict-weak "less"; padding entries are -1 and sort last
+template <class Less>
+__device__ void sort_idx(int32_t *a, int64_t P, Less less) {
+    for (int64_t k = 2; k <= P; k <<= 1)
+        for (int64_t j = k >> 1; j > 0; j >>= 1) {
+            for (int64_t i = ln(); i < P; i += 64) {
+                const int64_t l = i ^ j;
+                if (l > i) {
+                    const int32_t x = a[i], y = a[l];
+                    const bool gt = (x < 0) ? (y >= 0) : (y >= 0 && less(y, x));  // x > y
+                    if (gt == ((i & k) == 0)) {
+                        a[i] = y;
+                        a[l] = x;
+                    }
+                }
+            }
+            wsync();
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
+// numpy RandomState (MT19937) in LDS; the refill is spread over the wave
+// ---------------------------------------------------------------------------------------------
+__device__ void mt_refill(uint32_t *key) {
+    auto twist = [&](int lo, int hi, int src_off) {  // key[kk] = key[kk + src_off] ^ f(key[kk], key[kk + 1])
+        for (int k0 = lo; k0 < hi; k0 += 64) {
+            const int kk = k0 + ln();
+            uint32_t v = 0;
+            if (kk < hi) {
+                const uint32_t y = (key[kk] & 0x80000000u) | (key[kk + 1] & 0x7fffffffu);
+                v = key[kk + src_off] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+            }
+            wsync();
+            if (kk < hi) key[kk] = v;
+            wsync();
+        }
+    };
+    twist(0, 227, 397);
+    twist(227, 454, -227);
+    twist(454, 623, -227);
+    uint32_t v = 0;
+    if (ln() == 0) {
+        const uint32_t y = (key[623] & 0x80000000u) | (key[0] & 0x7fffffffu);
+        v = key[396] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    wsync();
+    if (ln() == 0) key[623] = v;
+    wsync();
+}
+
+struct MT {
+    uint32_t *key;
+    int pos;
+    __device__ uint32_t next32() {
+        if (pos == 624) {
+            mt_refill(key);
+            pos = 0;
+        }
+        uint32_t y = key[pos++];
+        y ^= (y >> 11);
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= (y >> 18);
+        return y;
+    }
+    // random_interval(max) for max < 2^32 (every draw here)
+    __device__ uint32_t interval(uint32_t max) {
+        if (max == 0) return 0;
+        uint32_t mask = max;
+        mask |= mask >> 1;
+        mask |= mask >> 2;
+        mask |= mask >> 4;
+        mask |= mask >> 8;
+        mask |= mask >> 16;
+        uint32_t v;
+        while ((v = (next32() & mask)) > max) {
+        }
+        return v;
+    }
+    // permutation(n): Fisher-Yates from the top (all lanes draw the same j; lane 0 swaps)
+    __device__ void permutation(int32_t n, int32_t *perm) {
+        for (int i = ln(); i < n; i += 64) perm[i] = i;
+        wsync();
+        for (int32_t i = n - 1; i >= 1; --i) {
+            const int32_t j = (int32_t)interval((uint32_t)i);
+            if (ln() == 0) {
+                const int32_t t = perm[i];
+                perm[i] = perm[j];
+                perm[j] = t;
+            }
+        }
+        wsync();
+    }
+};
+
+// Python round(best / cov, 3) for positive integers: q * 1000 rounded half-even on its exact binary
+// value, then k / 1000 correctly rounded (the double Python's round returns)
+__device__ double round3(int64_t best, int64_t cov) {
+    const double q = (double)best / (double)cov;
+    const uint64_t bits = (uint64_t)__double_as_longlong(q);
+    const int ex = (int)((bits >> 52) & 0x7ff);
+    uint64_t mant = bits & ((1ull << 52) - 1);
+    int e2;
+    if (ex == 0) {
+        e2 = -1074;
+    } else {
+        mant |= 1ull << 52;
+        e2 = ex - 1075;
+    }
+    const uint64_t Pm = mant * 1000ull;  // < 2^63
+    uint64_t k;
+    if (e2 >= 0) {
+        if (e2 > 8) return q;  // q >= 2^52 is an integer already
+        k = Pm << e2;
+    } else {
+        const int s = -e2;
+        if (s >= 64) {
+            k = 0;
+        } else {
+            k = Pm >> s;
+            const uint64_t rem = Pm & ((1ull << s) - 1), half = 1ull << (s - 1);
+            if (rem > half || (rem == half && (k & 1ull))) ++k;
+        }
+    }
+    return (double)k / 1000.0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2: one locus
+// ---------------------------------------------------------------------------------------------
+constexpr int kLdsPerm = 2048;
+constexpr int64_t kPosBias = int64_t(1) << 39;  // sort keys hold position + bias in 40 bits
+
+struct LocusRun {
+    const uint8_t *T;
+    Locus L;
+    Stats S;
+    const Params *P;
+    ALayout A;
+    BPtr B;
+    OPtr O;
+    MT mt;
+    int32_t *lperm;
+    int n;
+    int status;
+    int64_t bin_lo, bin_hi, nbins;
+    int32_t n_peaks;
+    int32_t ctr[2];  // spliceDict per-side counters
+    int32_t n_iso, n_mem, n_sub;
+
+    __device__ bool in_map(int64_t p) const { return p >= L.map_lo && p < L.map_lo + L.map_n; }
+    __device__ int64_t mi(int64_t p) const { return p - L.map_lo; }
+
+    __device__ void fail(int code) {
+        if (status == kOk) status = code;
+    }
+
+    // --- collect_reads (SDC:278-331) -----------------------------------------------------------
+    __device__ void collect() {
+        // cs_of: the last record with this name on the locus chromosome (csDict[name] = cs)
+        for (int r0 = 0; r0 < n; r0 += 64) {
+            const int r = r0 + ln();
+            if (r < n) {
+                const Rec &R = A.recs[r];
+                uint64_t h = 1469598103934665603ull;
+                for (int i = 0; i < R.name_len; ++i) h = (h ^ T[R.name_off + i]) * 1099511628211ull;
+                B.ihash[r] = h;
+            }
+        }
+        wsync();
+        for (int r0 = 0; r0 < n; r0 += 64) {
+            const int r = r0 + ln();
+            int32_t of = -1;
+            if (r < n && A.recs[r].same_chrom) {
+                const Rec &R = A.recs[r];
+                const uint64_t h = B.ihash[r];
+                of = r;
+                for (int k = n - 1; k > r; --k) {
+                    if (B.ihash[k] != h) continue;
+                    const Rec &K = A.recs[k];
+                    if (!K.same_chrom || K.name_len != R.name_len) continue;
+                    if (bytes_eq(T + K.name_off, T + R.name_off, R.name_len)) {
+                        of = k;
+                        break;
+                    }
+                }
+            }
+            if (r < n) A.recs[r].cs_of = of;
+        }
+        // coverage bins per record: myround over each block at stride 10 plus the block's tail, sorted
+        // and made unique (cov_set)
+        int64_t carry = 0, lo = INT64_MAX, hi = INT64_MIN;
+        int bad = 0;
+        int32_t hl_carry = 0, hr_carry = 0;
+        for (int r0 = 0; r0 < n; r0 += 64) {
+            const int r = r0 + ln();
+            const bool act = r < n && A.recs[r].same_chrom;
+            const Rec R = act ? A.recs[r] : Rec{};
+            int64_t capr = 0;
+            int32_t nl = 0, nr = 0;
+            if (act) {
+                for (int x = 0; x < R.nblk; ++x) {
+                    const int64_t sz = A.blk[2 * (R.blk_off + x)], bs = A.blk[2 * (R.blk_off + x) + 1];
+                    capr += (sz > 0 ? (sz + 9) / 10 : 0) + 11;
+                    if (!R.acc_lt) {
+                        nl += (bs + sz) != R.tend;
+                        nr += bs != R.tstart;
+                    }
+                }
+            }
+            const int64_t ci = wincl(capr);
+            const int64_t coff = carry + ci - capr;
+            carry += __shfl(ci, 63);
+            const int32_t li_ = wincl(nl), ri_ = wincl(nr);
+            int32_t el = hl_carry + li_ - nl, er = hr_carry + ri_ - nr;
+            hl_carry += __shfl(li_, 63);
+            hr_carry += __shfl(ri_, 63);
+            if (act) {
+                int64_t *v = B.cov + coff;
+                int64_t m = 0;
+                int64_t y = 0;
+                bool y_set = false, sorted = true;
+                for (int x = 0; x < R.nblk && !bad; ++x) {
+                    const int64_t sz = A.blk[2 * (R.blk_off + x)], bs = A.blk[2 * (R.blk_off + x) + 1];
+                    for (int64_t t = 0; t < sz; t += 10) {
+                        const int64_t val = myround(bs + t);
+                        if (m > 0 && val < v[m - 1]) sorted = false;
+                        v[m++] = val;
+                        y = t;
+                        y_set = true;
+                    }
+                    if (!y_set) {
+                        bad = 1;  // NameError in the reference
+                        break;
+                    }
+                    int64_t last = INT64_MIN;
+                    for (int64_t t = y; t < sz; ++t) {
+                        const int64_t val = myround(bs + t);
+                        if (val != last) {
+                            if (m > 0 && val < v[m - 1]) sorted = false;
+                            v[m++] = val;
+                        }
+                        last = val;
+                    }
+                    // histogram entries in block order (acc >= 0.9 only)
+                    if (!R.acc_lt) {
+                        const int64_t be = bs + sz;
+                        if (be != R.tend) {
+                            B.s[0].sk[el] = ((uint64_t)(be + kPosBias) << 24) | (uint64_t)el;
+                            B.s[0].etmp[el] = r;
+                            if (be + kPosBias < 0 || be + kPosBias >= (int64_t(1) << 40) || el >= (1 << 24)) bad = 2;
+                            ++el;
+                        }
+                        if (bs != R.tstart) {
+                            B.s[1].sk[er] = ((uint64_t)(bs + kPosBias) << 24) | (uint64_t)er;
+                            B.s[1].etmp[er] = r;
+                            if (bs + kPosBias < 0 || bs + kPosBias >= (int64_t(1) << 40) || er >= (1 << 24)) bad = 2;
+                            ++er;
+                        }
+                    }
+                }
+                if (!bad) {
+                    if (!sorted) heap_sort(v, m);
+                    int64_t u = 0;
+                    for (int64_t i = 0; i < m; ++i)
+                        if (u == 0 || v[i] != v[u - 1]) v[u++] = v[i];
+                    A.recs[r].cov_off = (int32_t)coff;
+                    A.recs[r].cov_n = (int32_t)u;
+                    if (u > 0) {
+                        lo = v[0] < lo ? v[0] : lo;
+                        hi = v[u - 1] > hi ? v[u - 1] : hi;
+                    }
+                }
+            } else if (r < n) {
+                A.recs[r].cov_off = 0;
+                A.recs[r].cov_n = 0;
+            }
+        }
+        const int b = wmax(bad);
+        if (b) {
+            fail(b == 1 ? kParse : kRange);
+            return;
+        }
+        bin_lo = wmin(lo);
+        bin_hi = wmax(hi);
+        nbins = bin_lo <= bin_hi ? (bin_hi - bin_lo) / 10 + 1 : 0;
+        wsync();
+        for (int k = 0; k < 2; ++k) build_side(B.s[k]);
+    }
+
+    __device__ static int64_t myround(int64_t x) {
+        int64_t q = x >= 0 ? x / 10 : -((-x + 9) / 10);
+        const int64_t r = x - 10 * q;
+        if (r > 5 || (r == 5 && (q & 1))) ++q;
+        return 10 * q;
+    }
+
+    __device__ static void heap_sort(int64_t *v, int64_t m) {
+        auto sift = [&](int64_t i, int64_t len) {
+            while (true) {
+                int64_t c = 2 * i + 1;
+                if (c >= len) break;
+                if (c + 1 < len && v[c + 1] > v[c]) ++c;
+                if (v[i] >= v[c]) break;
+                const int64_t t = v[i];
+                v[i] = v[c];
+                v[c] = t;
+                i = c;
+            }
+        };
+        for (int64_t i = m / 2 - 1; i >= 0; --i) sift(i, m);
+        for (int64_t e = m - 1; e > 0; --e) {
+            const int64_t t = v[0];
+            v[0] = v[e];
+            v[e] = t;
+            sift(0, e);
+        }
+    }
+
+    // histogram of one side: entries sorted by (position, insertion), distinct keys with their
+    // first insertion rank, strand counts, and the candidate order of find_peaks
+    __device__ void build_side(Side &d) {
+        const int H = d.H;
+        for (int64_t i = H + ln(); i < d.P; i += 64) d.sk[i] = ~0ull;
+        wsync();
+        sort_u64(d.sk, d.P);
+        // records in sorted order; distinct-key flags
+        int32_t kc = 0;
+        for (int i0 = 0; i0 < H; i0 += 64) {
+            const int i = i0 + ln();
+            int first = 0;
+            int64_t pos = 0;
+            int32_t seq = 0;
+            if (i < H) {
+                const uint64_t k = d.sk[i];
+                pos = (int64_t)(k >> 24) - kPosBias;
+                seq = (int32_t)(k & 0xffffffu);
+                d.erec[i] = d.etmp[seq];
+                first = (i == 0 || (int64_t)(d.sk[i - 1] >> 24) - kPosBias != pos) ? 1 : 0;
+            }
+            const int32_t fi = wincl(first);
+            if (first) {
+                const int32_t u = kc + fi - 1;
+                d.ukey[u] = pos;
+                d.ulo[u] = i;
+                d.ufirst[u] = seq;
+                d.upmb[3 * u] = d.upmb[3 * u + 1] = d.upmb[3 * u + 2] = 0;
+            }
+            kc += __shfl(fi, 63);
+        }
+        d.nkeys = kc;
+        wsync();
+        for (int u0 = 0; u0 < kc; u0 += 64) {
+            const int u = u0 + ln();
+            if (u < kc) d.ucnt[u] = (u + 1 < kc ? d.ulo[u + 1] : H) - d.ulo[u];
+        }
+        wsync();
+        // strand counts per key (lane per entry)
+        for (int i0 = 0; i0 < H; i0 += 64) {
+            const int i = i0 + ln();
+            if (i < H) {
+                const int64_t pos = (int64_t)(d.sk[i] >> 24) - kPosBias;
+                const int u = find_key(d, pos);
+                const int8_t dn = A.recs[d.erec[i]].dirn;
+                atomicAdd(&d.upmb[3 * u + (dn == 0 ? 0 : dn == 1 ? 1 : 2)], 1);
+            }
+        }
+        wsync();
+        // candidates: count >= min_count, count descending, insertion order on ties
+        int32_t cc = 0;
+        for (int u0 = 0; u0 < kc; u0 += 64) {
+            const int u = u0 + ln();
+            const int take = (u < kc && d.ucnt[u] >= P->min_count) ? 1 : 0;
+            const int32_t ti = wincl(take);
+            if (take) {
+                d.cand[cc + ti - 1] = ((uint64_t)(0x7fffffff - d.ucnt[u]) << 32) | (uint64_t)d.ufirst[u];
+                d.etmp[d.ufirst[u]] = u;
+            }
+            cc += __shfl(ti, 63);
+        }
+        d.ncand = cc;
+        for (int64_t i = cc + ln(); i < d.P; i += 64) d.cand[i] = ~0ull;
+        wsync();
+        sort_u64(d.cand, pow2ge(cc));
+    }
+
+    __device__ int find_key(const Side &d, int64_t pos) const {
+        int lo = 0, hi = d.nkeys;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (d.ukey[mid] < pos)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        return (lo < d.nkeys && d.ukey[lo] == pos) ? lo : -1;
+    }
+
+    // --- make_genome_bins (SDC:392-438) -------------------------------------------------------
+    __device__ void push_peak(int64_t s, int64_t e, char type, char side, double prop, int side_i) {
+        if (n_peaks >= O.peak_cap) {
+            fail(kCapacity);
+            return;
+        }
+        if (!in_map(s) || !in_map(e)) {
+            fail(kRange);
+            return;
+        }
+        if (ln() == 0) {
+            Peak pk;
+            pk.start = s;
+            pk.end = e;
+            pk.prop = prop;
+            pk.type = type;
+            pk.side = side;
+            O.peaks[n_peaks] = pk;
+        }
+        for (int64_t b = s + ln(); b <= e; b += 64) B.areas[side_i][mi(b)] = 1;
+        wsync();
+        ++n_peaks;
+    }
+
+    __device__ void genome_bins(int side_i) {
+        const int w = P->w;
+        for (int ti = 0; ti < 2; ++ti) {
+            const int s = side_i * 2 + ti;
+            const int a = L.ann_off[s] - L.ann_off[0], len = L.ann_off[s + 1] - L.ann_off[s];
+            if (len <= 0) continue;
+            int64_t *pl = B.ann + a;
+            // the host passes each list as is; sort ascending (insertion sort on lane 0: short lists)
+            if (ln() == 0) {
+                for (int i = 1; i < len; ++i) {
+                    const int64_t x = pl[i];
+                    int j = i - 1;
+                    while (j >= 0 && pl[j] > x) {
+                        pl[j + 1] = pl[j];
+                        --j;
+                    }
+                    pl[j + 1] = x;
+                }
+            }
+            wsync();
+            int i1 = 0;
+            while (i1 < len) {
+                int64_t mx = pl[i1], mn = pl[i1];
+                int i2 = i1;
+                while (i2 < len && pl[i2] - mx <= w) {
+                    mx = pl[i2] > mx ? pl[i2] : mx;
+                    mn = pl[i2] < mn ? pl[i2] : mn;
+                    ++i2;
+                }
+                push_peak(mn - w, mx + w, ti == 0 ? '5' : '3', side_i == 0 ? 'l' : 'r', -1.0, side_i);
+                if (status != kOk) return;
+                i1 = i2;
+            }
+        }
+    }
+
+    // --- determine_cov (SDC:200-224) ------------------------------------------------------------
+    __device__ int32_t hcov(int64_t pos) {
+        int32_t c = 0;
+        for (int r0 = 0; r0 < n; r0 += 64) {
+            const int r = r0 + ln();
+            if (r < n && A.recs[r].cov_n > 0) {
+                const Rec &R = A.recs[r];
+                const int64_t *v = B.cov + R.cov_off;
+                int lo = 0, hi = R.cov_n;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (v[mid] < pos)
+                        lo = mid + 1;
+                    else
+                        hi = mid;
+                }
+                c += (lo < R.cov_n && v[lo] == pos) ? 1 : 0;
+            }
+        }
+        return wsum(c);
+    }
+
+    __device__ int64_t determine_cov(int32_t nn, int64_t center, bool reverse) {
+        int64_t kstart;
+        if (reverse) {
+            const int64_t k = center - 1 - bin_lo;
+            kstart = k < 0 ? -1 : (k / 10 < nbins - 1 ? k / 10 : nbins - 1);
+            if (kstart < 0) return 0;
+        } else {
+            const int64_t k = center + 1 - bin_lo;
+            kstart = k <= 0 ? 0 : (k + 9) / 10;
+            if (kstart >= nbins) return 0;
+        }
+        const int64_t bound = bin_lo + 10 * kstart;
+        for (int c0 = 0; c0 < nn; c0 += 64) {
+            const int c = c0 + ln();
+            if (c < nn) {
+                const Rec &R = A.recs[B.names[c]];
+                const int64_t *v = B.cov + R.cov_off;
+                int lo = 0, hi = R.cov_n;
+                if (reverse) {  // last element <= bound
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (v[mid] <= bound)
+                            lo = mid + 1;
+                        else
+                            hi = mid;
+                    }
+                    B.cur[c] = lo - 1;
+                } else {  // first element >= bound
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (v[mid] < bound)
+                            lo = mid + 1;
+                        else
+                            hi = mid;
+                    }
+                    B.cur[c] = lo < R.cov_n ? lo : -1;
+                }
+            }
+        }
+        wsync();
+        int64_t cov = 0;
+        int counter = 0;
+        while (counter < 4) {
+            // next position over the winners' heads (largest for the left side, smallest for the right)
+            int64_t best = reverse ? INT64_MIN : INT64_MAX;
+            for (int c0 = 0; c0 < nn; c0 += 64) {
+                const int c = c0 + ln();
+                if (c < nn && B.cur[c] >= 0) {
+                    const int64_t h = B.cov[A.recs[B.names[c]].cov_off + B.cur[c]];
+                    best = reverse ? (h > best ? h : best) : (h < best ? h : best);
+                }
+            }
+            const int64_t top = reverse ? wmax(best) : wmin(best);
+            if (top == (reverse ? INT64_MIN : INT64_MAX)) break;
+            int32_t count = 0;
+            for (int c0 = 0; c0 < nn; c0 += 64) {
+                const int c = c0 + ln();
+                if (c < nn && B.cur[c] >= 0) {
+                    const Rec &R = A.recs[B.names[c]];
+                    if (B.cov[R.cov_off + B.cur[c]] == top) {
+                        ++count;
+                        const int nx = reverse ? B.cur[c] - 1 : B.cur[c] + 1;
+                        B.cur[c] = (nx >= 0 && nx < R.cov_n) ? nx : -1;
+                    }
+                }
+            }
+            count = wsum(count);
+            wsync();
+            if (count > 1) {
+                ++counter;
+                const int64_t hc = hcov(top);
+                cov = hc > cov ? hc : cov;
+            }
+        }
+        return cov;
+    }
+
+    // --- getCSaroundSS on the tokenised cs (cluster.cpp cs_around) --------------------------------
+    __device__ int run_of(const Rec &R, int32_t t) const {
+        int lo = 0, hi = R.nrun - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (A.runs[R.run_off + mid].rec0 <= t)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        return lo;
+    }
+    __device__ static int st_slot(char c) {
+        return c == '*' ? 0 : c == '+' ? 1 : c == '-' ? 2 : c == '=' ? 3 : 4;
+    }
+    __device__ void count_range(const Rec &R, int32_t a, int32_t b, int32_t *cnt) const {
+        if (a >= b) return;
+        int k = run_of(R, a);
+        while (a < b) {
+            const Run &U = A.runs[R.run_off + k];
+            const int32_t e = b < U.rec0 + U.n ? b : U.rec0 + U.n;
+            cnt[st_slot(U.st)] += e - a;
+            cnt[5] += e - a;
+            a = e;
+            ++k;
+        }
+    }
+    // returns the junction motif (4 chars packed, 0 for "nnnn"), counts into cl / cr
+    __device__ bool cs_around(const Rec &R, int64_t start, int64_t end, char mot[4], int32_t *cl, int32_t *cr,
+                              bool &has_l, bool &has_r) const {
+        mot[0] = mot[1] = mot[2] = mot[3] = 'n';
+        has_l = has_r = false;
+        const int32_t nrec = R.nrec_cs;
+        int lo = 0, hi = R.nadv;  // upper_bound(adv_first, end) - 1
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (A.adv_first[R.adv_off + mid] <= end)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        const int ka = lo - 1;
+        if (ka < 0) return false;
+        const Run U = A.runs[R.run_off + A.adv_run[R.adv_off + ka]];
+        int64_t i_in = 0;
+        if (U.n != 1) {
+            const int64_t q = (end - U.g0) / U.step - 1;
+            i_in = q < U.n - 1 ? q : U.n - 1;
+        }
+        const int64_t pos = U.g0 + (int64_t)U.step * (i_in + 1);
+        if (pos < start) return false;
+        const int64_t si = U.rec0 + i_in + 1;
+        const int64_t wlo = si - 10 > 0 ? si - 10 : 0, whi = si + 10 < nrec ? si + 10 : nrec;
+        int64_t idx = -1;
+        Run IR = {};
+        if (wlo < whi) {
+            for (int k = run_of(R, (int32_t)(whi - 1)); k >= 0; --k) {
+                const Run &V = A.runs[R.run_off + k];
+                if (V.rec0 + V.n <= wlo) break;
+                if (V.st == '|') {
+                    idx = V.rec0;
+                    IR = V;
+                    break;
+                }
+            }
+        }
+        if (idx < 0) return false;
+        mot[0] = IR.motif[0];
+        mot[1] = IR.motif[1];
+        mot[2] = IR.motif[2];
+        mot[3] = IR.motif[3];
+        int64_t a = idx - 5, b = idx;
+        if (a < 0) a += nrec;
+        if (a < 0) a = 0;
+        if (a < b) {
+            count_range(R, (int32_t)a, (int32_t)(b < nrec ? b : nrec), cl);
+            has_l = true;
+        }
+        const int64_t ra = idx + 1, rb = idx + 6 < nrec ? idx + 6 : nrec;
+        if (ra < rb) {
+            count_range(R, (int32_t)ra, (int32_t)rb, cr);
+            has_r = true;
+        }
+        return true;
+    }
+
+    // --- characterize_splicing_event (SDC:499-550) ----------------------------------------------
+    __device__ bool characterize(int64_t left, int64_t right, int32_t nn) {
+        const int32_t k = nn < 500 ? nn : 500;
+        int32_t *perm = nn <= kLdsPerm ? lperm : B.perm;
+        mt.permutation(nn, perm);
+        int32_t allowed = 0, bad = 0;
+        int32_t lc[6] = {0, 0, 0, 0, 0, 0}, rc[6] = {0, 0, 0, 0, 0, 0};
+        for (int t0 = 0; t0 < k; t0 += 64) {
+            const int t = t0 + ln();
+            if (t < k) {
+                const int32_t ri = A.recs[B.names[perm[t]]].cs_of;
+                const Rec R = A.recs[ri];
+                if (R.cs_bad) {
+                    bad = 1;
+                } else {
+                    char mot[4];
+                    int32_t cl[6] = {0, 0, 0, 0, 0, 0}, cr[6] = {0, 0, 0, 0, 0, 0};
+                    bool hl, hr;
+                    cs_around(R, left, right, mot, cl, cr, hl, hr);
+                    for (int j = 0; j < P->n_junc; ++j)
+                        if (P->junc_len4[j] && P->junc[j][0] == mot[0] && P->junc[j][1] == mot[1] &&
+                            P->junc[j][2] == mot[2] && P->junc[j][3] == mot[3]) {
+                            ++allowed;
+                            break;
+                        }
+                    if (hl)
+                        for (int s = 0; s < 6; ++s) lc[s] += cl[s];
+                    if (hr)
+                        for (int s = 0; s < 6; ++s) rc[s] += cr[s];
+                }
+            }
+        }
+        wsync();
+        if (wany(bad != 0)) {
+            fail(kParse);
+            return false;
+        }
+        allowed = wsum(allowed);
+        for (int s = 0; s < 6; ++s) {
+            lc[s] = wsum(lc[s]);
+            rc[s] = wsum(rc[s]);
+        }
+        if (k == 0) {
+            fail(kZeroDivision);
+            return false;
+        }
+        if (!((double)allowed / (double)k > 0.85)) return false;
+        if (lc[5] == 0 || rc[5] == 0) {
+            fail(kZeroDivision);
+            return false;
+        }
+        return (double)lc[3] / (double)lc[5] > 0.85 && (double)rc[3] / (double)rc[5] > 0.85;
+    }
+
+    // --- find_peaks / scan_for_best_bin (SDC:232-275, :163-197) --------------------------------
+    __device__ void find_peaks(int side_i) {
+        Side &d = B.s[side_i];
+        const bool reverse = side_i == 0;
+        const int64_t w = P->w, span = 4 * w + 1;
+        int64_t *wc = B.win, *wp = B.win + span, *wm = B.win + 2 * span, *wf = B.win + 3 * span;
+        uint8_t *areas = B.areas[side_i];
+        for (int ci = 0; ci < d.ncand; ++ci) {
+            const int u = d.etmp[(int)(d.cand[ci] & 0xffffffffu)];
+            const int64_t entry = d.ukey[u];
+            if (!in_map(entry - 2 * w) || !in_map(entry + 2 * w)) {
+                fail(kRange);
+                return;
+            }
+            if (areas[mi(entry)]) continue;
+            for (int64_t dd = ln(); dd < span; dd += 64) {
+                const int64_t pos = entry - 2 * w + dd;
+                int64_t f = areas[mi(pos)] ? 1 : 0, c = 0, p = 0, m = 0;
+                const int k = find_key(d, pos);
+                if (k >= 0) {
+                    c = d.ucnt[k];
+                    p = d.upmb[3 * k];
+                    m = d.upmb[3 * k + 1];
+                    if (d.upmb[3 * k + 2] > 0) f |= 2;
+                }
+                wc[dd] = c;
+                wp[dd] = p;
+                wm[dd] = m;
+                wf[dd] = f;
+            }
+            wsync();
+            int64_t best = 0, center = 0, bx = 0, bdp = 0, bdm = 0;
+            bool key_err = false;
+            for (int64_t xi = 0; xi < 2 * w + 1 && !key_err; ++xi) {
+                const int64_t x = xi == 0 ? 0 : ((xi & 1) ? (xi + 1) / 2 : -(xi / 2));
+                const int64_t d0 = x + w;
+                int64_t fl = 0, cnt = 0, dp = 0, dm = 0;
+                for (int64_t q = d0; q < d0 + 2 * w + 1; ++q) fl |= wf[q];
+                if (fl & 1) continue;
+                if (fl & 2) {
+                    key_err = true;
+                    break;
+                }
+                for (int64_t q = d0; q < d0 + 2 * w + 1; ++q) {
+                    cnt += wc[q];
+                    dp += wp[q];
+                    dm += wm[q];
+                }
+                if (cnt > best) {
+                    best = cnt;
+                    center = entry + x;
+                    bx = x;
+                    bdp = dp;
+                    bdm = dm;
+                }
+            }
+            if (key_err) {
+                fail(kKeyError);
+                return;
+            }
+            int32_t nn = 0;
+            int64_t cov = 0;
+            if (best > 0) {
+                for (int64_t yi = 0; yi < 2 * w + 1; ++yi) {
+                    const int64_t y = yi == 0 ? 0 : ((yi & 1) ? (yi + 1) / 2 : -(yi / 2));
+                    const int k = find_key(d, entry + bx + y);
+                    if (k < 0) continue;
+                    const int c = d.ucnt[k], lo = d.ulo[k];
+                    for (int i = ln(); i < c; i += 64) B.names[nn + i] = d.erec[lo + i];
+                    nn += c;
+                }
+                wsync();
+                cov = determine_cov(nn, center, reverse);
+            }
+            if (cov <= 0) continue;
+            const double prop = round3(best, cov);
+            if (!(prop > P->cutoff)) continue;
+            char type = 0;
+            if (bdp < bdm)
+                type = reverse ? '3' : '5';
+            else if (bdp > bdm)
+                type = reverse ? '5' : '3';
+            if (!type) continue;
+            const bool ok = characterize(center - w, center + w, nn);
+            if (status != kOk) return;
+            if (ok) {
+                push_peak(center - w, center + w, type, side_i == 0 ? 'l' : 'r', prop, side_i);
+                if (status != kOk) return;
+            }
+        }
+    }
+
+    // --- spliceDict (defineIsoforms.py:71-83): per-side counters, later rows overwrite -------------
+    __device__ void splice_dict() {
+        ctr[0] = ctr[1] = 0;
+        for (int pi = 0; pi < n_peaks; ++pi) {
+            const Peak pk = O.peaks[pi];
+            const int s = pk.side == 'l' ? 0 : 1;
+            ctr[s] += 1;
+            if (ln() == 0) B.lab[pi] = ctr[s] | (pk.type == '3' ? (1 << 30) : 0) | (s ? (1 << 29) : 0);
+            for (int64_t b = pk.start + ln(); b <= pk.end; b += 64) B.splice[mi(b)] = pi;
+            wsync();
+        }
+    }
+
+    __device__ int put_label(uint8_t *o, int32_t lab) const {
+        int len = 0;
+        o[len++] = (lab & (1 << 30)) ? '3' : '5';
+        o[len++] = (lab & (1 << 29)) ? 'r' : 'l';
+        const int32_t c = lab & ((1 << 29) - 1);
+        char d[12];
+        int nd = 0;
+        int32_t v = c;
+        do {
+            d[nd++] = (char)('0' + v % 10);
+            v /= 10;
+        } while (v);
+        while (nd) o[len++] = (uint8_t)d[--nd];
+        return len;
+    }
+
+    // --- sort_reads_into_splice_junctions (SDC:714-769): identity text per record -----------------
+    __device__ void sort_reads() {
+        int64_t carry = 0;
+        for (int r0 = 0; r0 < n; r0 += 64) {
+            const int r = r0 + ln();
+            int64_t cap = 0;
+            Rec R = {};
+            if (r < n) {
+                R = A.recs[r];
+                cap = (R.chrom_len + 2 + (int64_t)(R.nblk > 0 ? R.nblk - 1 : 0) * 28 + 7) & ~int64_t(7);
+            }
+            const int64_t ci = wincl(cap);
+            const int64_t off = carry + ci - cap;
+            carry += __shfl(ci, 63);
+            if (r < n) {
+                uint8_t *o = B.ibuf + off;
+                int len = 0;
+                for (int i = 0; i < R.chrom_len; ++i) o[len++] = T[R.chrom_off + i];
+                o[len++] = '_';
+                bool failed = false;
+                for (int x = 0; x + 1 < R.nblk; ++x) {
+                    const int64_t ls = A.blk[2 * (R.blk_off + x) + 1] + A.blk[2 * (R.blk_off + x)];
+                    const int64_t rs = A.blk[2 * (R.blk_off + x + 1) + 1];
+                    if (rs - ls > 50) {
+                        if (!R.same_chrom) {
+                            failed = true;
+                            break;
+                        }
+                        const int32_t a = in_map(ls) ? B.splice[mi(ls)] : -1;
+                        const int32_t b = in_map(rs) ? B.splice[mi(rs)] : -1;
+                        if (a < 0 || b < 0) {
+                            failed = true;
+                            break;
+                        }
+                        len += put_label(o + len, B.lab[a]);
+                        o[len++] = '-';
+                        len += put_label(o + len, B.lab[b]);
+                        o[len++] = '~';
+                    }
+                }
+                int8_t kind = 0;
+                if (!failed) {
+                    // identity.split('_')[1] != ''
+                    int u1 = -1;
+                    for (int i = 0; i < R.chrom_len; ++i)
+                        if (o[i] == '_') {
+                            u1 = i;
+                            break;
+                        }
+                    bool spliced;
+                    if (u1 < 0) {
+                        spliced = len > R.chrom_len + 1;
+                    } else {
+                        int u2 = R.chrom_len;
+                        for (int i = u1 + 1; i < R.chrom_len; ++i)
+                            if (o[i] == '_') {
+                                u2 = i;
+                                break;
+                            }
+                        spliced = u2 > u1 + 1;
+                    }
+                    kind = spliced ? 1 : 2;
+                }
+                uint64_t h = 1469598103934665603ull;
+                for (int i = 0; i < len; ++i) h = (h ^ o[i]) * 1099511628211ull;
+                B.ioff[r] = (int32_t)off;
+                B.ilen[r] = len;
+                B.ikind[r] = kind;
+                B.ihash[r] = h;
+            }
+        }
+        wsync();
+    }
+
+    __device__ bool ident_eq(int32_t a, int32_t b) const {
+        return B.ilen[a] == B.ilen[b] && bytes_eq(B.ibuf + B.ioff[a], B.ibuf + B.ioff[b], B.ilen[a]);
+    }
+
+    // byte p of identity `id`: the rep record's identity text, then "M<k>" for a mono-exon group
+    __device__ int id_char(int32_t id, int p) const {
+        const int32_t rep = B.id_rep[id];
+        const int L0 = B.ilen[rep];
+        if (p < L0) return B.ibuf[B.ioff[rep] + p];
+        const int32_t m = B.id_m[id];
+        if (m < 0) return -1;
+        if (p == L0) return 'M';
+        int nd = 1;
+        for (int32_t v = m; v >= 10; v /= 10) ++nd;
+        const int k = p - L0 - 1;
+        if (k >= nd) return -1;
+        int32_t v = m;
+        for (int i = 0; i < nd - 1 - k; ++i) v /= 10;
+        return '0' + v % 10;
+    }
+    __device__ bool id_less(int32_t a, int32_t b) const {
+        for (int p = 0;; ++p) {
+            const int x = id_char(a, p), y = id_char(b, p);
+            if (x != y) return x < y;  // -1 (end) sorts first
+            if (x < 0) return false;
+        }
+    }
+
+    // the position tuple of group_mono's sort: (start, end, (name, seq), left_extra, right_extra)
+    __device__ int bytes_cmp(const uint8_t *x, int nx, const uint8_t *y, int ny) const {
+        const int m = nx < ny ? nx : ny;
+        for (int i = 0; i < m; ++i)
+            if (x[i] != y[i]) return x[i] < y[i] ? -1 : 1;
+        return nx < ny ? -1 : nx > ny ? 1 : 0;
+    }
+    __device__ bool pos_less(int32_t a, int32_t b) const {
+        const Rec &X = A.recs[a], &Y = A.recs[b];
+        if (X.tstart != Y.tstart) return X.tstart < Y.tstart;
+        if (X.tend != Y.tend) return X.tend < Y.tend;
+        int c = bytes_cmp(T + X.name_off, X.name_len, T + Y.name_off, Y.name_len);
+        if (c) return c < 0;
+        c = bytes_cmp(T + X.seq_off, X.seq_len, T + Y.seq_off, Y.seq_len);
+        if (c) return c < 0;
+        if (X.qstart != Y.qstart) return X.qstart < Y.qstart;
+        const int64_t rx = X.qsize - X.qend, ry = Y.qsize - Y.qend;
+        if (rx != ry) return rx < ry;
+        return a < b;  // stable
+    }
+
+    // --- identities: group records by identity text; mono-exon groups split into "M<k>" groups
+    //     (group_mono_exon_transcripts, SDC:772-794); all identities sorted by text --------------------
+    int32_t n_ids, n_members;
+    __device__ void identities() {
+        const int64_t pn = pow2ge(n);
+        for (int64_t i = ln(); i < pn; i += 64) {
+            uint64_t k = ~0ull;
+            if (i < n && B.ikind[i] != 0) k = (B.ihash[i] & ~0xffffffull) | (uint64_t)i;
+            B.isort[i] = k;
+        }
+        wsync();
+        sort_u64(B.isort, pn);
+        // valid entries and hash-run starts (max-scan of run-start flags)
+        int32_t nv = 0, carry = 0;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + ln();
+            const uint64_t k = i < n ? B.isort[i] : ~0ull;
+            const bool valid = k != ~0ull;
+            int32_t st_ = -1;
+            if (valid) st_ = (i == 0 || (B.isort[i - 1] >> 24) != (k >> 24)) ? i : -1;
+            int32_t m = st_;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int32_t t = __shfl_up(m, o);
+                if (ln() >= o && t > m) m = t;
+            }
+            m = m > carry ? m : carry;
+            if (valid) B.msort[i] = m;
+            carry = __shfl(m, 63);
+            nv += (int32_t)__popcll(__ballot(valid));
+        }
+        wsync();
+        // group representative: the first record of the run with the same identity text
+        for (int i0 = 0; i0 < nv; i0 += 64) {
+            const int i = i0 + ln();
+            if (i < nv) {
+                const int32_t r = (int32_t)(B.isort[i] & 0xffffffu);
+                int32_t rep = r;
+                for (int j = B.msort[i]; j < i; ++j) {
+                    const int32_t q = (int32_t)(B.isort[j] & 0xffffffu);
+                    if (ident_eq(q, r)) {
+                        rep = q;
+                        break;
+                    }
+                }
+                B.grp[r] = rep;
+            }
+        }
+        wsync();
+        // members grouped by representative (first occurrence), record order inside
+        for (int64_t i = ln(); i < pn; i += 64) {
+            uint64_t k = ~0ull;
+            if (i < n && B.ikind[i] != 0) k = ((uint64_t)B.grp[i] << 24) | (uint64_t)i;
+            B.isort[i] = k;
+        }
+        wsync();
+        sort_u64(B.isort, pn);
+        for (int i = ln(); i < nv; i += 64) B.msort[i] = (int32_t)(B.isort[i] & 0xffffffu);
+        wsync();
+        n_members = nv;
+        // walk the groups (uniform): spliced groups are one identity; mono groups are sorted by the
+        // position tuple and split by the overlap counter
+        n_ids = 0;
+        int g0 = 0;
+        while (g0 < nv) {
+            const int32_t rep = (int32_t)(B.isort[g0] >> 24);
+            // group end: first index with another representative (binary search: keys ascend)
+            int lo = g0 + 1, hi = nv;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((int32_t)(B.isort[mid] >> 24) == rep)
+                    lo = mid + 1;
+                else
+                    hi = mid;
+            }
+            const int g1 = lo;
+            if (B.ikind[rep] == 1) {
+                if (ln() == 0) {
+                    B.id_lo[n_ids] = g0;
+                    B.id_hi[n_ids] = g1;
+                    B.id_rep[n_ids] = rep;
+                    B.id_m[n_ids] = -1;
+                }
+                ++n_ids;
+            } else {
+                const int m = g1 - g0;
+                const int64_t pm = pow2ge(m);
+                for (int64_t i = ln(); i < pm; i += 64) B.idsort[i] = i < m ? B.msort[g0 + i] : -1;
+                wsync();
+                sort_idx(B.idsort, pm, [&](int32_t a, int32_t b) { return pos_less(a, b); });
+                for (int i = ln(); i < m; i += 64) B.msort[g0 + i] = B.idsort[i];
+                wsync();
+                // overlap counter (lane 0, in order), then one identity per counter run
+                if (ln() == 0) {
+                    int64_t prev_end = 0;
+                    int32_t counter = 0;
+                    for (int i = 0; i < m; ++i) {
+                        const Rec &R = A.recs[B.msort[g0 + i]];
+                        if (R.tstart > prev_end) {
+                            counter += 1;
+                            prev_end = R.tend > prev_end ? R.tend : prev_end;
+                        } else {
+                            prev_end = R.tend;
+                        }
+                        B.msuf[g0 + i] = counter;
+                    }
+                }
+                wsync();
+                int i = 0;
+                while (i < m) {
+                    const int32_t c = B.msuf[g0 + i];
+                    int j = i + 1;
+                    while (j < m && B.msuf[g0 + j] == c) ++j;
+                    if (ln() == 0) {
+                        B.id_lo[n_ids] = g0 + i;
+                        B.id_hi[n_ids] = g0 + j;
+                        B.id_rep[n_ids] = rep;
+                        B.id_m[n_ids] = c;
+                    }
+                    ++n_ids;
+                    i = j;
+                }
+            }
+            wsync();
+            g0 = g1;
+        }
+        const int64_t pi = pow2ge(n_ids);
+        for (int64_t i = ln(); i < pi; i += 64) B.idsort[i] = i < n_ids ? (int32_t)i : -1;
+        wsync();
+        sort_idx(B.idsort, pi, [&](int32_t a, int32_t b) { return id_less(a, b); });
+    }
+
+    // --- find_ends (SDC:554-711) with dense position maps ----------------------------------------
+    __device__ void extend(int32_t *peaks, const int32_t *cnt, int64_t position, int64_t adjacent, int dir,
+                           int64_t best_bin) {
+        const int64_t mc = P->min_count;
+        bool extended = true;
+        while (extended) {
+            const int64_t a = adjacent + dir * (int64_t)(ln() + 1);
+            const bool mine = ln() < 10;
+            const bool rng = wany(mine && !in_map(a));
+            if (rng) {
+                fail(kRange);
+                return;
+            }
+            const int32_t c = mine ? cnt[mi(a)] : 0;
+            const int64_t wc = wsum((int64_t)c);
+            if (best_bin > wc && wc >= mc) {
+                const bool present = mine && peaks[mi(a)] >= 0;
+                wsync();
+                if (mine && !present) peaks[mi(a)] = (int32_t)mi(position);
+                if (wany(present)) extended = false;
+            } else {
+                extended = false;
+            }
+            adjacent += dir * 10;
+            wsync();
+        }
+    }
+
+    // one side of find_ends: sorted positions pos_at(i), i < k, walked in `order` (+1 ascending
+    // starts, -1 descending ends)
+    __device__ void ends_side(int32_t *pk, const int32_t *cnt, const uint64_t *sorted, int32_t k, bool starts) {
+        const int64_t up = P->up, down = P->down, mc = P->min_count;
+        int64_t prev = INT64_MIN;
+        for (int32_t ii = 0; ii < k; ++ii) {
+            const int32_t i = starts ? ii : k - 1 - ii;
+            const int64_t position = (int64_t)sorted[i] - kPosBias;
+            if (position == prev) continue;  // same answer as the previous visit
+            prev = position;
+            const int64_t probe = starts ? position - up : position + up - 1;
+            if (!in_map(probe)) {
+                fail(kRange);
+                return;
+            }
+            if (pk[mi(probe)] >= 0) continue;
+            int64_t wc = 0;
+            {
+                const int64_t q = starts ? position + ln() : position - ln();
+                int32_t c = 0;
+                if (ln() < 10 && in_map(q)) c = cnt[mi(q)];
+                wc = wsum((int64_t)c);
+            }
+            if (wc < mc) continue;
+            const int64_t s_lo = starts ? -up : -down, s_hi = starts ? down : up;
+            if (s_lo >= s_hi) {
+                fail(kValueError);
+                return;
+            }
+            if (!in_map(position + s_lo) || !in_map(position + s_hi)) {
+                fail(kRange);
+                return;
+            }
+            for (int64_t s = s_lo + ln(); s < s_hi; s += 64) pk[mi(position + s)] = (int32_t)mi(position);
+            const int64_t ob_min = position + s_lo, ob_max = position + s_hi - 1;
+            if (ob_min >= ob_max) {
+                fail(kValueError);
+                return;
+            }
+            int64_t bb = INT64_MIN;
+            for (int64_t x = ob_min + ln(); x < ob_max; x += 64) {
+                int64_t b = 0;
+                for (int q = 0; q < 10; ++q)
+                    if (in_map(x + q)) b += cnt[mi(x + q)];
+                bb = b > bb ? b : bb;
+            }
+            const int64_t best_bin = wmax(bb);
+            wsync();
+            extend(pk, cnt, position, position + s_lo, -1, best_bin);
+            if (status != kOk) return;
+            extend(pk, cnt, position, position + s_hi - 1, +1, best_bin);
+            if (status != kOk) return;
+        }
+    }
+
+    // --- define_start_end_sites (SDC:797-868) + the subsample draw (SDC:884-888) -----------------
+    __device__ void start_end_sites() {
+        n_iso = n_mem = n_sub = 0;
+        for (int t = 0; t < n_ids; ++t) {
+            const int32_t id = B.idsort[t];
+            const int lo = B.id_lo[id], m = B.id_hi[id] - lo;
+            const int32_t k = m < 10000 ? m : 10000;
+            int32_t *perm = m <= kLdsPerm ? lperm : B.perm;
+            mt.permutation(m, perm);
+            const int64_t pk = pow2ge(k);
+            int64_t tlo = INT64_MAX, thi = INT64_MIN;
+            for (int64_t i = ln(); i < pk; i += 64) {
+                uint64_t s = ~0ull, e = ~0ull;
+                if (i < k) {
+                    const Rec &R = A.recs[B.msort[lo + perm[i]]];
+                    s = (uint64_t)(R.tstart + kPosBias);
+                    e = (uint64_t)(R.tend + kPosBias);
+                    tlo = R.tstart < tlo ? R.tstart : tlo;
+                    tlo = R.tend < tlo ? R.tend : tlo;
+                    thi = R.tstart > thi ? R.tstart : thi;
+                    thi = R.tend > thi ? R.tend : thi;
+                }
+                B.ss[i] = s;
+                B.isort[i] = e;
+            }
+            tlo = wmin(tlo);
+            thi = wmax(thi);
+            if (k > 0 && (!in_map(tlo) || !in_map(thi))) {
+                fail(kRange);
+                return;
+            }
+            for (int i = ln(); i < k; i += 64) {
+                atomicAdd(&B.sc[mi((int64_t)B.ss[i] - kPosBias)], 1);
+                atomicAdd(&B.ec[mi((int64_t)B.isort[i] - kPosBias)], 1);
+            }
+            wsync();
+            sort_u64(B.ss, pk);
+            sort_u64(B.isort, pk);
+            ends_side(B.sp, B.sc, B.ss, k, true);
+            if (status != kOk) return;
+            ends_side(B.ep, B.ec, B.isort, k, false);
+            if (status != kOk) return;
+            wsync();
+            // isoforms: (start window, end window) pairs in Pos order, first seen first
+            for (int i = ln(); i < m; i += 64) {
+                const Rec &R = A.recs[B.msort[lo + i]];
+                const int32_t a = in_map(R.tstart) ? B.sp[mi(R.tstart)] : -1;
+                const int32_t b = in_map(R.tend) ? B.ep[mi(R.tend)] : -1;
+                B.pa[i] = a;
+                B.pb[i] = b;
+                B.asg[i] = (a >= 0 && b >= 0) ? 0 : 1;
+            }
+            wsync();
+            while (true) {
+                int32_t f = INT32_MAX;
+                for (int i = ln(); i < m; i += 64)
+                    if (!B.asg[i] && i < f) f = i;
+                f = wmin(f);
+                if (f == INT32_MAX) break;
+                const int32_t a0 = B.pa[f], b0 = B.pb[f];
+                int32_t cnt = 0;
+                for (int i0 = f; i0 < m; i0 += 64) {
+                    const int i = i0 + ln();
+                    const bool mt_ = i < m && !B.asg[i] && B.pa[i] == a0 && B.pb[i] == b0;
+                    const int32_t inc = wincl(mt_ ? 1 : 0);
+                    if (mt_) {
+                        O.mem[n_mem + cnt + inc - 1] = B.msort[lo + i];
+                        B.asg[i] = 1;
+                    }
+                    cnt += __shfl(inc, 63);
+                }
+                if (ln() == 0) O.iso_nmem[n_iso] = cnt;
+                ++n_iso;
+                n_mem += cnt;
+                wsync();
+            }
+            // clear the maps this identity touched
+            const int64_t c_lo0 = tlo - P->up - P->down - 32, c_hi0 = thi + P->up + P->down + 32;
+            const int64_t c_lo = c_lo0 > L.map_lo ? c_lo0 : L.map_lo;
+            const int64_t c_hi = c_hi0 < L.map_lo + L.map_n - 1 ? c_hi0 : L.map_lo + L.map_n - 1;
+            for (int64_t p = c_lo + ln(); p <= c_hi; p += 64) {
+                B.sc[mi(p)] = 0;
+                B.ec[mi(p)] = 0;
+                B.sp[mi(p)] = -1;
+                B.ep[mi(p)] = -1;
+            }
+            wsync();
+        }
+        // determine_consensus subsample per isoform, IsoDict order
+        int32_t moff = 0;
+        for (int iso = 0; iso < n_iso; ++iso) {
+            const int32_t m = O.iso_nmem[iso];
+            const int32_t k = m < P->sub_k ? m : P->sub_k;
+            int32_t *perm = m <= kLdsPerm ? lperm : B.perm;
+            mt.permutation(m, perm);
+            for (int i = ln(); i < k; i += 64) O.sub[n_sub + i] = O.mem[moff + perm[i]];
+            if (ln() == 0) O.iso_nsub[iso] = k;
+            n_sub += k;
+            moff += m;
+            wsync();
+        }
+    }
+
+    __device__ void run(const Args &G) {
+        // per-record text offsets for the host (names for reads2isoforms, sequences for the POA)
+        for (int r = ln(); r < n; r += 64) {
+            const Rec &R = A.recs[r];
+            int64_t *o = G.rec_text + 4 * (L.rec_base + r);
+            o[0] = L.text_off + R.name_off;
+            o[1] = R.name_len;
+            o[2] = L.text_off + R.seq_off;
+            o[3] = R.seq_len;
+        }
+        for (int64_t p = ln(); p < L.map_n; p += 64) {
+            B.areas[0][p] = 0;
+            B.areas[1][p] = 0;
+            B.splice[p] = -1;
+            B.sc[p] = 0;
+            B.ec[p] = 0;
+            B.sp[p] = -1;
+            B.ep[p] = -1;
+        }
+        for (int i = ln(); i < n_ann_of(L); i += 64) B.ann[i] = G.ann_pos[L.ann_off[0] + i];
+        wsync();
+        collect();
+        if (status != kOk) return;
+        genome_bins(0);
+        if (status != kOk) return;
+        genome_bins(1);
+        if (status != kOk) return;
+        find_peaks(0);
+        if (status != kOk) return;
+        find_peaks(1);
+        if (status != kOk) return;
+        splice_dict();
+        sort_reads();
+        identities();
+        start_end_sites();
+    }
+};
+
+__global__ __launch_bounds__(64) void cluster_locus(Args G) {
+    __shared__ uint32_t mtk[624];
+    __shared__ int32_t lperm[kLdsPerm];
+    const int li = G.order[blockIdx.x];
+    Stats *st = G.stats + li;
+    LocusRun R;
+    R.S = *st;
+    if (R.S.status != kOk) return;
+    R.L = G.loci[li];
+    R.T = G.text + R.L.text_off;
+    R.P = G.prm;
+    R.A = a_layout(G.scratch_a + R.L.a_off, R.L);
+    carve_b(G.scratch_b + R.L.b_off, R.S, R.L, R.P->w, R.B);
+    carve_o(G.out + R.L.o_off, R.S, R.L, R.O);
+    R.n = R.S.n_rec;
+    R.status = kOk;
+    R.n_peaks = 0;
+    R.n_iso = R.n_mem = R.n_sub = 0;
+    R.n_ids = R.n_members = 0;
+    for (int i = ln(); i < 624; i += 64) mtk[i] = R.P->mt_init[i];
+    R.mt.key = mtk;
+    R.mt.pos = 624;
+    R.lperm = lperm;
+    wsync();
+    R.run(G);
+    wsync();
+    if (ln() == 0) {
+        st->status = R.status;
+        st->n_peaks = R.n_peaks;
+        st->n_iso = R.n_iso;
+        st->n_mem = R.n_mem;
+        st->n_sub = R.n_sub;
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+hipError_t launch_parse(const Args &a, int n_blocks, hipStream_t s) {
+    if (n_blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cluster_parse, dim3(n_blocks), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_locus(const Args &a, int n_blocks, hipStream_t s) {
+    if (n_blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cluster_locus, dim3(n_blocks), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+int64_t b_bytes(const Stats &S, const Locus &L, int w) {
+    BPtr B;
+    carve_b(nullptr, S, L, w, B);
+    return B.total;
+}
+int64_t o_bytes(const Stats &S, const Locus &L) {
+    OPtr O;
+    carve_o(nullptr, S, L, O);
+    return O.total;
+}
+// host view of a locus' output region (offsets relative to the region)
+void o_offsets(const Stats &S, const Locus &L, int64_t *peaks, int64_t *nmem, int64_t *mem, int64_t *nsub,
+               int64_t *sub) {
+    OPtr O;
+    uint8_t *z = reinterpret_cast<uint8_t *>(uintptr_t(1) << 20);  // any non-null base: offsets only
+    carve_o(z, S, L, O);
+    *peaks = (uint8_t *)O.peaks - z;
+    *nmem = (uint8_t *)O.iso_nmem - z;
+    *mem = (uint8_t *)O.mem - z;
+    *nsub = (uint8_t *)O.iso_nsub - z;
+    *sub = (uint8_t *)O.sub - z;
+}
+
+
+namespace {
+
+struct DevMem {
+    void *p = nullptr;
+    ~DevMem() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t n) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        return hipMalloc(&p, n > 0 ? n : 1);
+    }
+    template <class T>
+    T *as() const {
+        return (T *)p;
+    }
+};
+
+#define CL_TRY(expr)                                                                             \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess)                                                                    \
+            return mando::set_error(MANDO_E_HIP, std::string("cluster: ") + #expr + ": " +       \
+                                                     hipGetErrorString(_e));                     \
+    } while (0)
+
+}  // namespace
+
+// Runs both kernels over every locus of `in` (see cluster_gpu.h); fills `out`.
+int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
+    const int64_t nl = in.n_loci;
+    out.status.assign((size_t)nl, kOk);
+    out.n_rec.assign((size_t)nl, 0);
+    out.rec_base.assign((size_t)nl + 1, 0);
+    out.peaks.assign((size_t)nl, {});
+    out.iso_nmem.assign((size_t)nl, {});
+    out.mem.assign((size_t)nl, {});
+    out.iso_nsub.assign((size_t)nl, {});
+    out.sub.assign((size_t)nl, {});
+    out.rec_text.clear();
+    if (nl == 0) return MANDO_OK;
+    CL_TRY(hipSetDevice(mando::ctx_device(ctx)));
+    hipStream_t s = mando::ctx_stream(ctx);
+
+    // parameters + the RNG state every locus starts from
+    Params prm;
+    memset(&prm, 0, sizeof prm);
+    prm.cutoff = in.cutoff;
+    prm.w = in.w;
+    prm.min_count = in.min_count;
+    prm.up = in.up;
+    prm.down = in.down;
+    prm.sub_k = in.sub_k;
+    prm.n_junc = 0;
+    for (const std::string &j : in.junctions) {
+        if (prm.n_junc >= 16) break;
+        prm.junc_len4[prm.n_junc] = j.size() == 4;
+        for (size_t c = 0; c < 4 && c < j.size(); ++c) prm.junc[prm.n_junc][c] = j[c];
+        ++prm.n_junc;
+    }
+    {
+        mando::MT19937 mt(in.seed);
+        for (int i = 0; i < 624; ++i) prm.mt_init[i] = mt.key[i];
+    }
+    // locus descriptors; loci whose file could not be read keep their I/O status
+    std::vector<Locus> L((size_t)nl);
+    std::string chroms;
+    std::vector<int32_t> run_order;
+    std::vector<int32_t> ann_off_all;
+    std::vector<int64_t> ann;
+    for (int64_t i = 0; i < nl; ++i) {
+        Locus &x = L[(size_t)i];
+        memset(&x, 0, sizeof x);
+        x.text_off = in.foff[i];
+        x.text_len = in.foff[i + 1] - in.foff[i];
+        x.chrom_off = (int32_t)chroms.size();
+        x.chrom_len = (int32_t)strlen(in.chroms[i]);
+        chroms += in.chroms[i];
+        x.ann_off[0] = (int32_t)ann.size();
+        for (int k = 0; k < 4; ++k) {
+            if (in.ann_pos && in.ann_off)
+                for (int64_t q = in.ann_off[4 * i + k]; q < in.ann_off[4 * i + k + 1]; ++q) ann.push_back(in.ann_pos[q]);
+            x.ann_off[k + 1] = (int32_t)ann.size();
+        }
+        if (in.fstatus[i] != kOk) {
+            out.status[(size_t)i] = in.fstatus[i];
+            continue;
+        }
+        if (x.text_len >= (int64_t(1) << 31) - 64) {
+            out.status[(size_t)i] = kRange;
+            continue;
+        }
+        x.line_cap = (int32_t)(x.text_len / 160 + 8);
+        x.op_cap = (int32_t)(x.text_len / 32 + 64);
+        x.blk_cap = (int32_t)(x.text_len / 96 + 64);
+        run_order.push_back((int32_t)i);
+    }
+    std::stable_sort(run_order.begin(), run_order.end(),
+                     [&](int32_t a, int32_t b) { return L[(size_t)a].text_len > L[(size_t)b].text_len; });
+    const int nrun = (int)run_order.size();
+
+    DevMem d_text, d_chroms, d_ann, d_loci, d_order, d_stats, d_a, d_b, d_o, d_rec, d_prm;
+    CL_TRY(d_text.alloc((size_t)in.text_len + 64));
+    CL_TRY(hipMemcpyAsync(d_text.p, in.text, (size_t)in.text_len, hipMemcpyHostToDevice, s));
+    CL_TRY(d_chroms.alloc(chroms.size() + 1));
+    CL_TRY(hipMemcpyAsync(d_chroms.p, chroms.data(), chroms.size() + 1, hipMemcpyHostToDevice, s));
+    CL_TRY(d_ann.alloc((ann.size() + 1) * 8));
+    if (!ann.empty()) CL_TRY(hipMemcpyAsync(d_ann.p, ann.data(), ann.size() * 8, hipMemcpyHostToDevice, s));
+    CL_TRY(d_order.alloc((size_t)(nrun + 1) * 4));
+    if (nrun) CL_TRY(hipMemcpyAsync(d_order.p, run_order.data(), (size_t)nrun * 4, hipMemcpyHostToDevice, s));
+    CL_TRY(d_prm.alloc(sizeof(Params)));
+    CL_TRY(hipMemcpyAsync(d_prm.p, &prm, sizeof(Params), hipMemcpyHostToDevice, s));
+    CL_TRY(d_loci.alloc((size_t)nl * sizeof(Locus)));
+    CL_TRY(d_stats.alloc((size_t)nl * sizeof(Stats)));
+    std::vector<Stats> st((size_t)nl);
+
+    Args G;
+    G.text = d_text.as<uint8_t>();
+    G.chroms = d_chroms.as<uint8_t>();
+    G.ann_pos = d_ann.as<int64_t>();
+    G.loci = d_loci.as<Locus>();
+    G.order = d_order.as<int32_t>();
+    G.stats = d_stats.as<Stats>();
+    G.prm = d_prm.as<Params>();
+
+    // K1, re-run with the reported sizes while a locus outgrows its scratch
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        int64_t a_tot = 0;
+        for (int32_t i : run_order) {
+            Locus &x = L[(size_t)i];
+            x.a_off = a_tot;
+            a_tot += al256(scratch_a_bytes(x.line_cap, x.op_cap, x.blk_cap));
+        }
+        CL_TRY(d_a.alloc((size_t)a_tot + 256));
+        CL_TRY(hipMemcpyAsync(d_loci.p, L.data(), (size_t)nl * sizeof(Locus), hipMemcpyHostToDevice, s));
+        CL_TRY(hipMemsetAsync(d_stats.p, 0, (size_t)nl * sizeof(Stats), s));
+        G.scratch_a = d_a.as<uint8_t>();
+        CL_TRY(launch_parse(G, nrun, s));
+        CL_TRY(hipMemcpyAsync(st.data(), d_stats.p, (size_t)nl * sizeof(Stats), hipMemcpyDeviceToHost, s));
+        CL_TRY(hipStreamSynchronize(s));
+        bool again = false;
+        for (int32_t i : run_order) {
+            const Stats &x = st[(size_t)i];
+            if (x.status != kCapacity) continue;
+            Locus &y = L[(size_t)i];
+            y.line_cap = std::max<int32_t>(y.line_cap, x.n_rec + 8);
+            y.op_cap = std::max<int32_t>(y.op_cap, x.n_ops + 64);
+            y.blk_cap = std::max<int32_t>(y.blk_cap, x.n_blk + 64);
+            // the kernel stops at the first exceeded capacity; later ones are bounded by the text
+            if (x.n_rec > 0 && x.n_blk == 0) y.blk_cap = std::max<int64_t>(y.blk_cap, y.text_len / 2 + 64);
+            if (x.n_rec > 0 && x.n_ops == 0) y.op_cap = std::max<int64_t>(y.op_cap, y.text_len / 2 + 64);
+            again = true;
+        }
+        if (!again) break;
+    }
+
+    // K2 sizes from K1's statistics: dense position maps over the locus span and its annotation
+    const int64_t M = 4 * (int64_t)in.w + in.up + in.down + 256;
+    int64_t b_tot = 0, o_tot = 0, recs = 0;
+    std::vector<int32_t> k2_order;
+    for (int64_t i = 0; i < nl; ++i) {
+        out.rec_base[(size_t)i] = recs;
+        if (out.status[(size_t)i] != kOk) continue;
+        Stats &x = st[(size_t)i];
+        if (x.status == kCapacity) x.status = kParse;  // still too big after the re-runs
+        out.status[(size_t)i] = x.status;
+        if (x.status != kOk) continue;
+        out.n_rec[(size_t)i] = x.n_rec;
+        recs += x.n_rec;
+    }
+    out.rec_base[(size_t)nl] = recs;
+    for (int32_t i : run_order) {
+        if (out.status[(size_t)i] != kOk) continue;
+        Locus &x = L[(size_t)i];
+        const Stats &y = st[(size_t)i];
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        if (y.span_lo <= y.span_hi) {
+            lo = y.span_lo;
+            hi = y.span_hi;
+        }
+        for (int32_t q = x.ann_off[0]; q < x.ann_off[4]; ++q) {
+            lo = std::min(lo, ann[(size_t)q]);
+            hi = std::max(hi, ann[(size_t)q]);
+        }
+        if (lo > hi) lo = hi = 0;
+        x.map_lo = lo - M;
+        x.map_n = hi - lo + 2 * M + 1;
+        if (x.map_n > (int64_t(1) << 30)) {
+            out.status[(size_t)i] = kRange;
+            continue;
+        }
+        x.rec_base = out.rec_base[(size_t)i];
+        x.b_off = b_tot;
+        x.b_len = b_bytes(y, x, in.w);
+        b_tot += al256(x.b_len);
+        x.o_off = o_tot;
+        o_tot += al256(o_bytes(y, x));
+        k2_order.push_back(i);
+    }
+    if (!k2_order.empty()) {
+        CL_TRY(d_b.alloc((size_t)b_tot + 256));
+        CL_TRY(d_o.alloc((size_t)o_tot + 256));
+        CL_TRY(d_rec.alloc((size_t)(recs + 1) * 32));
+        // loci not run by K2 must not be: mark them in the stats copy the kernel reads
+        for (int64_t i = 0; i < nl; ++i)
+            if (out.status[(size_t)i] != kOk && st[(size_t)i].status == kOk) st[(size_t)i].status = out.status[(size_t)i];
+        CL_TRY(hipMemcpyAsync(d_stats.p, st.data(), (size_t)nl * sizeof(Stats), hipMemcpyHostToDevice, s));
+        CL_TRY(hipMemcpyAsync(d_loci.p, L.data(), (size_t)nl * sizeof(Locus), hipMemcpyHostToDevice, s));
+        CL_TRY(hipMemcpyAsync(d_order.p, k2_order.data(), k2_order.size() * 4, hipMemcpyHostToDevice, s));
+        G.scratch_b = d_b.as<uint8_t>();
+        G.out = d_o.as<uint8_t>();
+        G.rec_text = d_rec.as<int64_t>();
+        CL_TRY(launch_locus(G, (int)k2_order.size(), s));
+        std::vector<uint8_t> ho((size_t)o_tot + 256);
+        out.rec_text.resize((size_t)recs * 4);
+        CL_TRY(hipMemcpyAsync(st.data(), d_stats.p, (size_t)nl * sizeof(Stats), hipMemcpyDeviceToHost, s));
+        CL_TRY(hipMemcpyAsync(ho.data(), d_o.p, (size_t)o_tot, hipMemcpyDeviceToHost, s));
+        if (recs) CL_TRY(hipMemcpyAsync(out.rec_text.data(), d_rec.p, (size_t)recs * 32, hipMemcpyDeviceToHost, s));
+        CL_TRY(hipStreamSynchronize(s));
+        for (int32_t i : k2_order) {
+            const Stats &y = st[(size_t)i];
+            out.status[(size_t)i] = y.status;
+            if (y.status != kOk) continue;
+            const Locus &x = L[(size_t)i];
+            int64_t op, onm, om, ons, os;
+            o_offsets(y, x, &op, &onm, &om, &ons, &os);
+            const uint8_t *base = ho.data() + x.o_off;
+            out.peaks[(size_t)i].assign((const Peak *)(base + op), (const Peak *)(base + op) + y.n_peaks);
+            out.iso_nmem[(size_t)i].assign((const int32_t *)(base + onm), (const int32_t *)(base + onm) + y.n_iso);
+            out.mem[(size_t)i].assign((const int32_t *)(base + om), (const int32_t *)(base + om) + y.n_mem);
+            out.iso_nsub[(size_t)i].assign((const int32_t *)(base + ons), (const int32_t *)(base + ons) + y.n_iso);
+            out.sub[(size_t)i].assign((const int32_t *)(base + os), (const int32_t *)(base + os) + y.n_sub);
+        }
+    }
+    return MANDO_OK;
+}
+
+}  // namespace cl
+}  // namespace mando

@@ -5,8 +5,9 @@ writes <p>/Isoform_Consensi.fasta, <p>/reads2isoforms.txt and <p>/polyAWhiteList
 
 Instead of one forked process per locus calling mappy + an `abpoa` subprocess per isoform
 (defineIsoforms.py:130-153, SpliceDefineConsensus.py:876-931), the whole locus set goes through:
-  1. clustering (libmando `mando_cluster_loci`, host C++ threads): peaks, isoform groups, RNG replay of
-     every locus' draws and the determine_consensus subsample;
+  1. clustering (libmando `mando_cluster_loci`: host threads read the files, HIP kernels cluster one
+     locus per wave): peaks, isoform groups, RNG replay of every locus' draws and the
+     determine_consensus subsample;
   2. orientation of every subsampled read against its isoform's first subsampled read
      (`mando_orient_batch`, HIP);
   3. the reference's per-isoform assembly logic (duplicate-primary rebinding, <=2 fallback, median
@@ -175,9 +176,10 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                     junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", upstream_buffer: int = 10,
                     downstream_buffer: int = 50, seed: int = 0, device: int = 0,
                     orient_fn: Callable | None = None, consensus_fn: Callable | None = None,
-                    comm=None, verbose: bool = False, n_chunks: int = 0) -> dict:
-    """Runs the D module on <path>/tmp_SS/*.psl.  orient_fn(seqs, seq_off, grp_off) -> (hits, n_hits) and
-    consensus_fn(seqs, seq_off, grp_off, seeding) -> (cons bytes, cons_off) default to the HIP path.
+                    cluster_fn: Callable | None = None, comm=None, verbose: bool = False, n_chunks: int = 0) -> dict:
+    """Runs the D module on <path>/tmp_SS/*.psl.  orient_fn(seqs, seq_off, grp_off) -> (hits, n_hits),
+    consensus_fn(seqs, seq_off, grp_off, seeding) -> (cons bytes, cons_off) and cluster_fn (the signature
+    of cluster.cluster_loci) default to the HIP path.
     comm (mandalorion_amd.comm.Comm, optional): shard the loci over comm.world ranks; rank 0 writes."""
     t0 = time.perf_counter()
     rank, world = (comm.rank, comm.world) if comm is not None else (0, 1)
@@ -257,11 +259,11 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     def run_cluster(lo, hi):
         # clustering (host C++ threads, GIL released), then the orientation input: the subsampled reads
         tc = time.perf_counter()
-        r = cluster.cluster_loci([os.path.join(out_tmp, x + ".psl") for x in my_roots[lo:hi]], chroms[lo:hi],
-                                 ann=ann[lo:hi], cutoff=cutoff, splice_site_width=splice_site_width,
-                                 minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
-                                 downstream_buffer=downstream_buffer, junctions=junctions, seed=seed,
-                                 threads=cl_threads)
+        r = (cluster_fn or cluster.cluster_loci)(
+            [os.path.join(out_tmp, x + ".psl") for x in my_roots[lo:hi]], chroms[lo:hi], ann=ann[lo:hi],
+            device=device, cutoff=cutoff, splice_site_width=splice_site_width,
+            minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
+            downstream_buffer=downstream_buffer, junctions=junctions, seed=seed, threads=cl_threads)
         te = time.perf_counter()
         timeline.append(("cluster", tc - t0, te - t0))
         bad = np.nonzero(r.locus_status != 0)[0]

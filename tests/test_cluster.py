@@ -3,10 +3,11 @@
 The fixtures were produced by the unmodified reference defineIsoforms.py (seeded parent, stub mappy,
 capture-only abpoa that answers with the first input sequence) on the synthetic loci of
 mandalorion_amd.simdata.fixture_specs(); see tests/golden/make_cluster_vectors.py.  Here the same loci
-are regenerated (hash-checked), clustered by libmando (host C++), and run through the D driver with
-the same two stand-ins injected (every read one forward primary hit; consensus = first input
-sequence), so the written files must be byte-identical to the reference's.
-CPU only: clustering is host code; the HIP orientation / POA paths are covered by the gpu tests.
+are regenerated (hash-checked), clustered, and run through the D driver with the same two stand-ins
+injected (every read one forward primary hit; consensus = first input sequence), so the written files
+must be byte-identical to the reference's.
+CPU: the clustering restatement (oracle/cluster_ref.cpp) against the fixtures — this pins the oracle.
+GPU: the HIP clustering kernels (libmando mando_cluster_loci) against the same fixtures.
 """
 from __future__ import annotations
 
@@ -20,6 +21,14 @@ import pytest
 import numpy as np
 
 from mandalorion_amd import _lib, cluster, define, gtf, simdata
+from oracle import cluster as ocl
+
+# (clustering function, pytest marks): the oracle on CPU, the HIP kernels on the GPU
+CLUSTERERS = [pytest.param("oracle", id="oracle"), pytest.param("gpu", id="gpu", marks=pytest.mark.gpu)]
+
+
+def _cl(kind):
+    return ocl.cluster_loci if kind == "oracle" else cluster.cluster_loci
 
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "cluster_vectors.json")))
 P = GOLD["params"]
@@ -59,11 +68,12 @@ def _ann(info, roots):
     return [gtf.locus_bounds(lb, rb, r.split("~")[0], int(r.split("~")[1]), int(r.split("~")[2])) for r in roots]
 
 
+@pytest.mark.parametrize("kind", CLUSTERERS)
 @pytest.mark.parametrize("seed", [0, 7])
-def test_peaks_and_isoforms_match_reference(dataset, seed):
+def test_peaks_and_isoforms_match_reference(dataset, seed, kind):
     d, roots, info = dataset
     exp = GOLD["seeds"][str(seed)]
-    res = cluster.cluster_loci([os.path.join(d, "tmp_SS", r + ".psl") for r in roots], [r.split("~")[0] for r in roots],
+    res = _cl(kind)([os.path.join(d, "tmp_SS", r + ".psl") for r in roots], [r.split("~")[0] for r in roots],
                                ann=_ann(info, roots), seed=seed, threads=4)
     assert (res.locus_status == 0).all()
     for li, r in enumerate(roots):
@@ -82,15 +92,17 @@ def test_peaks_and_isoforms_match_reference(dataset, seed):
     assert calls == [c["names"] for c in exp["abpoa_calls"]]
 
 
+@pytest.mark.parametrize("kind", CLUSTERERS)
 @pytest.mark.parametrize("seed,chunks", [(0, 1), (7, 1), (0, 3)])
-def test_define_driver_files_byte_identical(dataset, seed, chunks, tmp_path):
+def test_define_driver_files_byte_identical(dataset, seed, chunks, kind, tmp_path):
     d, roots, info = dataset
     exp = GOLD["seeds"][str(seed)]
     stats = define.define_isoforms(d, cutoff=P["cutoff"], genome_file=info["gtf"], splice_site_width=P["splice_site_width"],
                                    minimum_read_count=P["minimum_read_count"], white_list_polyA=P["white_list_polyA"].split(","),
                                    threads=2, junctions=P["junctions"], upstream_buffer=P["upstream_buffer"],
                                    downstream_buffer=P["downstream_buffer"], seed=seed, orient_fn=_stub_orient,
-                                   consensus_fn=_stub_consensus, n_chunks=chunks)
+                                   consensus_fn=_stub_consensus, n_chunks=chunks,
+                                   cluster_fn=ocl.cluster_loci if kind == "oracle" else None)
     assert stats["chunks"] == chunks
     sha = lambda f: hashlib.sha256(open(os.path.join(d, f), "rb").read()).hexdigest()
     assert sha("Isoform_Consensi.fasta") == exp["isoform_consensi_sha256"]
@@ -106,7 +118,7 @@ def test_rebinding_and_fallbacks(dataset):
     second hit's orientation applies to the already re-bound sequence); <=2 oriented reads -> the first;
     zero -> IndexError."""
     d, roots, _ = dataset
-    res = cluster.cluster_loci([os.path.join(d, "tmp_SS", roots[0] + ".psl")], [roots[0].split("~")[0]], seed=0)
+    res = ocl.cluster_loci([os.path.join(d, "tmp_SS", roots[0] + ".psl")], [roots[0].split("~")[0]], seed=0)
     sub = res.subsample(0)
     n = len(sub)
     assert n >= 3 and res.n_isoforms >= 1
@@ -157,7 +169,8 @@ def _rank_main(rank, world, port, d, gtf_path, seed, q):
                                     white_list_polyA=P["white_list_polyA"].split(","), threads=2,
                                     junctions=P["junctions"], upstream_buffer=P["upstream_buffer"],
                                     downstream_buffer=P["downstream_buffer"], seed=seed, orient_fn=_stub_orient,
-                                    consensus_fn=lambda s, o, g, sd: _first_of_groups(s, o, g), comm=comm)
+                                    consensus_fn=lambda s, o, g, sd: _first_of_groups(s, o, g), comm=comm,
+                                    cluster_fn=ocl.cluster_loci)
         q.put((rank, st["loci"], st["isoforms"], comm.backend))
     finally:
         comm.close()

@@ -1,4 +1,4 @@
-"""End-to-end D module on the GPU: clustering (host C++) -> orientation (HIP) -> batched POA (HIP) ->
+"""End-to-end D module on the GPU: clustering (HIP) -> orientation (HIP) -> batched POA (HIP) ->
 writer, against the same driver with the CPU restatements (oracle/) injected for orientation and POA.
 The written Isoform_Consensi.fasta / reads2isoforms.txt must be byte-identical; reads2isoforms.txt must
 also equal the reference's own (tests/golden/cluster_vectors.json, independent of consensus)."""
@@ -37,8 +37,10 @@ def test_define_gpu_equals_cpu_restatement(gpu_ctx, tmp_path):
     gpu_fa, gpu_r2i = read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")
     assert hashlib.sha256(gpu_r2i).hexdigest() == GOLD["seeds"]["0"]["reads2isoforms_sha256"]
     assert st["poa_groups"] > 20
+    from oracle import cluster as ocl
+
     _run(d, info["gtf"], orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
-         consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd))
+         consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci)
     assert read("Isoform_Consensi.fasta") == gpu_fa
     assert read("reads2isoforms.txt") == gpu_r2i
 

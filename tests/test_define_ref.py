@@ -2,10 +2,10 @@
 (tests/golden/define_vectors.json, made by tests/golden/make_define_vectors.py): 35-40 % '-' strand
 records, >100-read isoforms (subsample cap), 8-11 kb loci that take abPOA's `-S` branch.
 
-* CPU (not gpu): the driver with the oracle's orientation and POA injected must write the reference's
+* CPU (not gpu): the driver with the oracle's clustering, orientation and POA injected must write the reference's
   exact Isoform_Consensi.fasta / reads2isoforms.txt — pins rebinding, revcomp, fallbacks, `-S`
   selection and the writer against the reference's own code.
-* GPU: the product path (HIP orientation + HIP POA) must write the same bytes.
+* GPU: the product path (HIP clustering + HIP orientation + HIP POA) must write the same bytes.
 """
 from __future__ import annotations
 
@@ -16,6 +16,7 @@ import os
 import pytest
 
 from mandalorion_amd import define, synth
+from oracle import cluster as ocl
 
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "define_vectors.json")))
 P = GOLD["params"]
@@ -66,7 +67,7 @@ def test_driver_with_oracle_equals_reference(tmp_path, name):
         seeded.append(int(sd.sum()) if sd is not None else 0)
         return opoa.consensus_packed(s, o, g, seeding=sd)
 
-    st = _run(d, orient_fn=lambda s, o, g: oref.orient_packed(s, o, g), consensus_fn=cons)
+    st = _run(d, orient_fn=lambda s, o, g: oref.orient_packed(s, o, g), consensus_fn=cons, cluster_fn=ocl.cluster_loci)
     _check(d, name, st)
     assert sum(seeded) == GOLD["datasets"][name]["reference"]["n_seeded_calls"]
 
@@ -104,7 +105,8 @@ def _shard_rank(rank, world, port, d, use_oracle, q):
         from oracle import poa as opoa
 
         kw = dict(orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
-                  consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd))
+                  consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd),
+                  cluster_fn=ocl.cluster_loci)
     with Comm(world, rank, "127.0.0.1", port, timeout_s=120) as c:  # host transport (one GPU or none)
         st = _run(d, comm=c, **kw)
         q.put((rank, st["isoforms"], c.backend))
@@ -156,5 +158,5 @@ def test_gpu_config4_slice_sharded_equals_one_rank(gpu_ctx, tmp_path):
     from oracle import poa as opoa
 
     _run(d, orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
-         consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd))
+         consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci)
     assert [open(os.path.join(d, f), "rb").read() for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt")] == one
