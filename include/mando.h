@@ -177,6 +177,23 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *params, const
                        const int64_t *ann_off, mando_cluster_result **out);
 int mando_cluster_view_get(const mando_cluster_result *res, mando_cluster_view *view);
 void mando_cluster_free(mando_cluster_result *res);
+/* The same locus text on the device the clustering ran on (valid until mando_cluster_free): the
+ * orientation and POA inputs are gathered from it (mando_orient_segments / mando_poa_segments) instead
+ * of being packed on the host and copied again. */
+int mando_cluster_device_text(const mando_cluster_result *res, const uint8_t **d_text, int64_t *len);
+
+/* Device-resident inputs: read r of a batch is d_text[off[r] .. off[r] + len[r]) (a device pointer of
+ * ctx's device, text_len bytes; off / len / rc are host arrays), reverse-complemented like
+ * mappy.revcomp when rc && rc[r].  Otherwise identical to mando_orient_batch / mando_poa_batch: the
+ * reads are gathered on the device into the batch layout, so only the (off, len, rc) arrays cross
+ * PCIe. */
+int mando_orient_segments(mando_ctx *ctx, const uint8_t *d_text, int64_t text_len, const int64_t *off,
+                          const int32_t *len, const int64_t *grp_off, int64_t n_groups, int8_t *hit_strands,
+                          int32_t max_hits, int32_t *n_hits);
+int mando_poa_segments(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *d_text, int64_t text_len,
+                       const int64_t *off, const int32_t *len, const int8_t *rc, const int64_t *grp_off,
+                       int64_t n_groups, const uint8_t *seeding_per_group, uint8_t *cons_out, int64_t cons_cap,
+                       int64_t *cons_off, int64_t *cells_out);
 
 /* ------------------------------------------------------------------------------------------------
  * Reassembly of the sharded D module: loci are split over ranks (one process per

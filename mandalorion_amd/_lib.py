@@ -34,6 +34,9 @@ EXPORTED = (
     "mando_cluster_loci",
     "mando_cluster_view_get",
     "mando_cluster_free",
+    "mando_cluster_device_text",
+    "mando_orient_segments",
+    "mando_poa_segments",
     "mando_comm_init",
     "mando_comm_backend",
     "mando_allgather_counts",
@@ -184,6 +187,9 @@ def load(path: str | None = None):
         lib.mando_cluster_view_get.argtypes = [_P, _P]
         lib.mando_cluster_free.argtypes = [_P]
         lib.mando_cluster_free.restype = None
+        lib.mando_cluster_device_text.argtypes = [_P, _P, _P]
+        lib.mando_orient_segments.argtypes = [_P, _P, _I64, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
+        lib.mando_poa_segments.argtypes = [_P, _P, _P, _I64, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]
         lib.mando_split_loci.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _P, _P]
         lib.mando_sam_to_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, _P]
         lib.mando_clean_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, _P]

@@ -76,6 +76,16 @@ class ClusterResult:
         self.peak_side = bytes(_arr(v.peak_side, npk, np.uint8)).decode() if npk else ""
         self.peak_prop = _arr(v.peak_prop, npk, np.float64)
 
+    def device_text(self) -> tuple[int, int]:
+        """(device pointer, length) of the locus text on the GPU the clustering ran on (0 for the
+        restatement's results, which have none)."""
+        if not hasattr(self._lib, "mando_cluster_device_text") or self._free != self._lib.mando_cluster_free:
+            return 0, 0
+        d = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        _lib.check(self._lib.mando_cluster_device_text(self._h, ctypes.byref(d), ctypes.byref(n)))
+        return int(d.value or 0), int(n.value)
+
     def close(self):
         if self._h is not None:
             self._free(self._h)

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -60,6 +61,44 @@ struct DevBuf {
     }
 };
 
+// Segment gather for the device-resident inputs (mando_orient_segments / mando_poa_segments): read r is
+// text[off[r] .. off[r] + len[r]), reverse-complemented like mappy.revcomp (revcomp.h) when rc[r];
+// written ASCII at dst + dst_off[r].  One 256-thread block walks segments (grid-stride).
+__device__ __forceinline__ uint8_t comp_base(uint8_t c) {
+    switch (c | 0x20) {
+        case 'a': return (uint8_t)(c ^ ('A' ^ 'T'));
+        case 't': return (uint8_t)(c ^ ('A' ^ 'T'));
+        case 'u': return (uint8_t)(c == 'U' ? 'A' : 'a');
+        case 'c': return (uint8_t)(c ^ ('C' ^ 'G'));
+        case 'g': return (uint8_t)(c ^ ('C' ^ 'G'));
+        case 'r': return (uint8_t)(c ^ ('R' ^ 'Y'));
+        case 'y': return (uint8_t)(c ^ ('R' ^ 'Y'));
+        case 'k': return (uint8_t)(c ^ ('K' ^ 'M'));
+        case 'm': return (uint8_t)(c ^ ('K' ^ 'M'));
+        case 'b': return (uint8_t)(c ^ ('B' ^ 'V'));
+        case 'v': return (uint8_t)(c ^ ('B' ^ 'V'));
+        case 'd': return (uint8_t)(c ^ ('D' ^ 'H'));
+        case 'h': return (uint8_t)(c ^ ('D' ^ 'H'));
+        default: return c;  // S, W, N and anything else
+    }
+}
+
+__global__ __launch_bounds__(256) void gather_kernel(const uint8_t *__restrict__ text, const int64_t *__restrict__ off,
+                                                     const int32_t *__restrict__ len, const int8_t *__restrict__ rc,
+                                                     const int64_t *__restrict__ dst_off, int64_t n,
+                                                     uint8_t *__restrict__ dst) {
+    for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const uint8_t *src = text + off[r];
+        uint8_t *d = dst + dst_off[r];
+        const int L = len[r];
+        if (rc && rc[r]) {
+            for (int k = threadIdx.x; k < L; k += 256) d[k] = comp_base(src[L - 1 - k]);
+        } else {
+            for (int k = threadIdx.x; k < L; k += 256) d[k] = src[k];
+        }
+    }
+}
+
 uint8_t g_enc[256];
 struct EncInit {
     EncInit() {
@@ -85,10 +124,12 @@ struct mando_ctx {
     DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
     DevBuf o_hits, o_strand, o_status;
     DevBuf s_items, s_item_of, s_n, s_t, s_q, s_scratch, s_redo, gorder2;  // -S partition
+    DevBuf g_off, g_len, g_rc, g_dst;                                      // segment gather
     ~mando_ctx() {
         for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
                           &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx, &s_items,
-                          &s_item_of, &s_n, &s_t, &s_q, &s_scratch, &s_redo, &gorder2})
+                          &s_item_of, &s_n, &s_t, &s_q, &s_scratch, &s_redo, &gorder2, &g_off, &g_len, &g_rc,
+                          &g_dst})
             b->release();
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -460,33 +501,26 @@ int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const
                         d_cons, d_cons_off, d_cons_len, d_cells, d_status, kMaxWavesPerCu);
 }
 
-int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *seqs,
-                    const int64_t *seq_off, const int64_t *grp_off, int64_t n_groups,
-                    const uint8_t *seeding_per_group, uint8_t *cons_out, int64_t cons_cap,
-                    int64_t *cons_off, int64_t *cells_out) {
-    if (!ctx || !params || !seq_off || !grp_off || !cons_off || n_groups < 0 || cons_cap < 0)
-        return fail(MANDO_E_ARG, "mando_poa_batch: bad argument");
-    if (n_groups == 0) {
-        cons_off[0] = 0;
-        return MANDO_OK;
-    }
+}  // extern "C"
+
+namespace {
+
+// Stages the reads of a batch as ASCII into ctx->seq (soff: their offsets there); returns a status.
+using StageFn = std::function<int(mando_ctx *)>;
+
+// The POA batch once its reads' layout (soff) is known: stage + encode, plan, launch, collect.
+int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::vector<int64_t> &soff,
+                   const int64_t *grp_off, int64_t n_groups, const uint8_t *seeding_per_group, uint8_t *cons_out,
+                   int64_t cons_cap, int64_t *cons_off, int64_t *cells_out, const StageFn &stage) {
     // -S for a group: seeding_per_group[g], or params->seeding for every group
     auto seeded_group = [&](int64_t g) {
         return seeding_per_group ? seeding_per_group[g] != 0 : params->seeding != 0;
     };
-    const int64_t n_reads = grp_off[n_groups] - grp_off[0];
-    if (grp_off[0] != 0 || n_reads < 0) return fail(MANDO_E_ARG, "grp_off must start at 0");
-    for (int64_t g = 0; g < n_groups; ++g)
-        if (grp_off[g + 1] < grp_off[g]) return fail(MANDO_E_ARG, "grp_off not monotone");
-    for (int64_t r = 0; r < n_reads; ++r)
-        if (seq_off[r + 1] < seq_off[r]) return fail(MANDO_E_ARG, "seq_off not monotone");
-    const int64_t total = seq_off[n_reads] - seq_off[0];
-    if (total > 0 && !seqs) return fail(MANDO_E_ARG, "null seqs");
+    const int64_t n_reads = grp_off[n_groups];
+    const int64_t total = soff[(size_t)n_reads];
     HIP_TRY(hipSetDevice(ctx->device));
 
-    // per-group statistics (the bases are uploaded as ASCII and encoded on the device)
-    std::vector<int64_t> soff((size_t)n_reads + 1);
-    for (int64_t r = 0; r <= n_reads; ++r) soff[(size_t)r] = seq_off[r] - seq_off[0];
+    // per-group statistics (the bases are staged as ASCII and encoded on the device)
     std::vector<GroupStat> gs((size_t)n_groups);
     int64_t max_first = 0, max_sum = 0, max_len = 0, max_nreads = 0;
     std::vector<int64_t> ccap((size_t)n_groups + 1, 0);
@@ -527,7 +561,7 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
     std::vector<int64_t> goff((size_t)n_groups + 1);
     for (int64_t g = 0; g <= n_groups; ++g) goff[(size_t)g] = grp_off[g];
     if (total > 0) {
-        HIP_TRY(hipMemcpyAsync(ctx->seq.p, seqs + seq_off[0], (size_t)total, hipMemcpyHostToDevice, ctx->stream));
+        if ((rc = stage(ctx))) return rc;
         HIP_TRY(mando::launch_encode(ctx->seq.as<uint8_t>(), total, ctx->stream));
     }
     HIP_TRY(hipMemcpyAsync(ctx->seq_off.p, soff.data(), soff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -614,6 +648,95 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
     return MANDO_OK;
 }
 
+int check_groups(const int64_t *grp_off, int64_t n_groups) {
+    if (grp_off[0] != 0) return fail(MANDO_E_ARG, "grp_off must start at 0");
+    for (int64_t g = 0; g < n_groups; ++g)
+        if (grp_off[g + 1] < grp_off[g]) return fail(MANDO_E_ARG, "grp_off not monotone");
+    return MANDO_OK;
+}
+
+// segments of a device-resident text: layout (exclusive prefix of len) and the gather stage
+int segment_layout(const int64_t *off, const int32_t *len, int64_t n, int64_t text_len, std::vector<int64_t> &soff) {
+    soff.assign((size_t)n + 1, 0);
+    for (int64_t r = 0; r < n; ++r) {
+        if (len[r] < 0 || off[r] < 0 || off[r] + len[r] > text_len)
+            return fail(MANDO_E_ARG, "segment " + std::to_string(r) + " outside the device text");
+        soff[(size_t)r + 1] = soff[(size_t)r] + len[r];
+    }
+    return MANDO_OK;
+}
+
+int gather_stage(mando_ctx *ctx, const uint8_t *d_text, const int64_t *off, const int32_t *len, const int8_t *rc,
+                 const std::vector<int64_t> &soff) {
+    const int64_t n = (int64_t)soff.size() - 1;
+    if (n <= 0) return MANDO_OK;
+    int e;
+    if ((e = ctx->g_off.ensure((size_t)n * 8)) || (e = ctx->g_len.ensure((size_t)n * 4)) ||
+        (e = ctx->g_dst.ensure((size_t)n * 8)) || (rc && (e = ctx->g_rc.ensure((size_t)n))))
+        return e;
+    HIP_TRY(hipMemcpyAsync(ctx->g_off.p, off, (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->g_len.p, len, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->g_dst.p, soff.data(), (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (rc) HIP_TRY(hipMemcpyAsync(ctx->g_rc.p, rc, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    const int blocks = (int)std::min<int64_t>(n, (int64_t)ctx->n_cu * 32);
+    hipLaunchKernelGGL(gather_kernel, dim3(blocks), dim3(256), 0, ctx->stream, d_text, ctx->g_off.as<int64_t>(),
+                       ctx->g_len.as<int32_t>(), rc ? ctx->g_rc.as<int8_t>() : nullptr, ctx->g_dst.as<int64_t>(), n,
+                       ctx->seq.as<uint8_t>());
+    HIP_TRY(hipGetLastError());
+    return MANDO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *seqs,
+                    const int64_t *seq_off, const int64_t *grp_off, int64_t n_groups,
+                    const uint8_t *seeding_per_group, uint8_t *cons_out, int64_t cons_cap,
+                    int64_t *cons_off, int64_t *cells_out) {
+    if (!ctx || !params || !seq_off || !grp_off || !cons_off || n_groups < 0 || cons_cap < 0)
+        return fail(MANDO_E_ARG, "mando_poa_batch: bad argument");
+    if (n_groups == 0) {
+        cons_off[0] = 0;
+        return MANDO_OK;
+    }
+    int rc = check_groups(grp_off, n_groups);
+    if (rc) return rc;
+    const int64_t n_reads = grp_off[n_groups];
+    for (int64_t r = 0; r < n_reads; ++r)
+        if (seq_off[r + 1] < seq_off[r]) return fail(MANDO_E_ARG, "seq_off not monotone");
+    const int64_t total = seq_off[n_reads] - seq_off[0];
+    if (total > 0 && !seqs) return fail(MANDO_E_ARG, "null seqs");
+    std::vector<int64_t> soff((size_t)n_reads + 1);
+    for (int64_t r = 0; r <= n_reads; ++r) soff[(size_t)r] = seq_off[r] - seq_off[0];
+    return poa_batch_impl(ctx, params, soff, grp_off, n_groups, seeding_per_group, cons_out, cons_cap, cons_off,
+                          cells_out, [&](mando_ctx *c) -> int {
+                              HIP_TRY(hipMemcpyAsync(c->seq.p, seqs + seq_off[0], (size_t)total, hipMemcpyHostToDevice,
+                                                     c->stream));
+                              return MANDO_OK;
+                          });
+}
+
+int mando_poa_segments(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *d_text, int64_t text_len,
+                       const int64_t *off, const int32_t *len, const int8_t *rc, const int64_t *grp_off,
+                       int64_t n_groups, const uint8_t *seeding_per_group, uint8_t *cons_out, int64_t cons_cap,
+                       int64_t *cons_off, int64_t *cells_out) {
+    if (!ctx || !params || !grp_off || !cons_off || n_groups < 0 || cons_cap < 0)
+        return fail(MANDO_E_ARG, "mando_poa_segments: bad argument");
+    if (n_groups == 0) {
+        cons_off[0] = 0;
+        return MANDO_OK;
+    }
+    int e = check_groups(grp_off, n_groups);
+    if (e) return e;
+    const int64_t n_reads = grp_off[n_groups];
+    if (n_reads > 0 && (!d_text || !off || !len)) return fail(MANDO_E_ARG, "mando_poa_segments: null segments");
+    std::vector<int64_t> soff;
+    if ((e = segment_layout(off, len, n_reads, text_len, soff))) return e;
+    return poa_batch_impl(ctx, params, soff, grp_off, n_groups, seeding_per_group, cons_out, cons_cap, cons_off,
+                          cells_out, [&](mando_ctx *c) { return gather_stage(c, d_text, off, len, rc, soff); });
+}
+
 int mando_selftest(mando_ctx *ctx, int *bad) {
     if (!ctx || !bad) return fail(MANDO_E_ARG, "bad argument");
     HIP_TRY(hipSetDevice(ctx->device));
@@ -626,19 +749,14 @@ int mando_selftest(mando_ctx *ctx, int *bad) {
     return MANDO_OK;
 }
 
-int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_off, const int64_t *grp_off,
-                       int64_t n_groups, int8_t *hit_strands, int32_t max_hits, int32_t *n_hits) {
-    if (!ctx || n_groups < 0 || max_hits < 1 || max_hits > 8 || (n_groups > 0 && (!seq_off || !grp_off)))
-        return fail(MANDO_E_ARG, "mando_orient_batch: bad argument (max_hits must be 1..8)");
-    if (n_groups == 0) return MANDO_OK;
-    if (grp_off[0] != 0) return fail(MANDO_E_ARG, "grp_off must start at 0");
-    for (int64_t g = 0; g < n_groups; ++g)
-        if (grp_off[g + 1] < grp_off[g]) return fail(MANDO_E_ARG, "grp_off not monotone");
+}  // extern "C"
+
+namespace {
+
+int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t *grp_off, int64_t n_groups,
+                int8_t *hit_strands, int32_t max_hits, int32_t *n_hits, const StageFn &stage) {
     const int64_t n_reads = grp_off[n_groups];
-    for (int64_t r = 0; r < n_reads; ++r)
-        if (seq_off[r + 1] < seq_off[r]) return fail(MANDO_E_ARG, "seq_off not monotone");
-    const int64_t total = seq_off[n_reads] - seq_off[0];
-    if (total > 0 && !seqs) return fail(MANDO_E_ARG, "null seqs");
+    const int64_t total = soff[(size_t)n_reads];
     if (n_reads > 0 && (!hit_strands || !n_hits)) return fail(MANDO_E_ARG, "null outputs");
     if (n_groups > INT32_MAX) return fail(MANDO_E_ARG, "too many groups");
     HIP_TRY(hipSetDevice(ctx->device));
@@ -650,18 +768,24 @@ int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_o
     if ((rc = ctx->o_hits.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(n_reads, 1))) != MANDO_OK) return rc;
     if ((rc = ctx->o_status.ensure(sizeof(int32_t) * (size_t)n_groups)) != MANDO_OK) return rc;
     if ((rc = ctx->counter.ensure(sizeof(int32_t))) != MANDO_OK) return rc;
-    std::vector<int64_t> so((size_t)n_reads + 1);
-    for (int64_t r = 0; r <= n_reads; ++r) so[(size_t)r] = seq_off[r] - seq_off[0];
-    if (total > 0) HIP_TRY(hipMemcpyAsync(ctx->seq.p, seqs + seq_off[0], (size_t)total, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(ctx->seq_off.p, so.data(), so.size() * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
+    if (total > 0 && (rc = stage(ctx))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->seq_off.p, soff.data(), soff.size() * sizeof(int64_t), hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->grp_off.p, grp_off, sizeof(int64_t) * (size_t)(n_groups + 1), hipMemcpyHostToDevice,
                            ctx->stream));
     HIP_TRY(hipMemsetAsync(ctx->o_hits.p, 0, sizeof(int32_t) * (size_t)std::max<int64_t>(n_reads, 1), ctx->stream));
     HIP_TRY(hipMemsetAsync(ctx->counter.p, 0, sizeof(int32_t), ctx->stream));
-    // per-read capacity from the longest read (~2 minimizers per W+1 positions, with margin); groups
-    // that overflow it are re-run at kOrientCap
-    int64_t maxlen = 0;
-    for (int64_t r = 0; r < n_reads; ++r) maxlen = std::max<int64_t>(maxlen, seq_off[r + 1] - seq_off[r]);
+    const int64_t *seq_off = soff.data();
+    // per-read capacity (~2 minimizers per W+1 positions, with margin) sized for the 95th percentile of
+    // the groups' longest reads, not the batch maximum: the capacity sets the LDS per wave and so the
+    // waves per CU (1024: 5, 2048: 2), and one 6 kb read must not halve the occupancy of 40k groups of
+    // 3 kb reads; groups that overflow are re-run at the next capacity
+    std::vector<int64_t> gmax((size_t)n_groups, 0);
+    for (int64_t g = 0; g < n_groups; ++g)
+        for (int64_t r = grp_off[g]; r < grp_off[g + 1]; ++r)
+            gmax[(size_t)g] = std::max<int64_t>(gmax[(size_t)g], seq_off[r + 1] - seq_off[r]);
+    const size_t q95 = (size_t)((double)(n_groups - 1) * 0.95);
+    std::nth_element(gmax.begin(), gmax.begin() + (ptrdiff_t)q95, gmax.end());
+    const int64_t maxlen = gmax[q95];
     int cap = 1024;
     while (cap < mando::kOrientCap && maxlen * 26 / 110 > cap) cap *= 2;
     mando::OrientArgs a;
@@ -720,6 +844,46 @@ int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_o
     }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return MANDO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mando_orient_batch(mando_ctx *ctx, const uint8_t *seqs, const int64_t *seq_off, const int64_t *grp_off,
+                       int64_t n_groups, int8_t *hit_strands, int32_t max_hits, int32_t *n_hits) {
+    if (!ctx || n_groups < 0 || max_hits < 1 || max_hits > 8 || (n_groups > 0 && (!seq_off || !grp_off)))
+        return fail(MANDO_E_ARG, "mando_orient_batch: bad argument (max_hits must be 1..8)");
+    if (n_groups == 0) return MANDO_OK;
+    int rc = check_groups(grp_off, n_groups);
+    if (rc) return rc;
+    const int64_t n_reads = grp_off[n_groups];
+    for (int64_t r = 0; r < n_reads; ++r)
+        if (seq_off[r + 1] < seq_off[r]) return fail(MANDO_E_ARG, "seq_off not monotone");
+    const int64_t total = seq_off[n_reads] - seq_off[0];
+    if (total > 0 && !seqs) return fail(MANDO_E_ARG, "null seqs");
+    std::vector<int64_t> so((size_t)n_reads + 1);
+    for (int64_t r = 0; r <= n_reads; ++r) so[(size_t)r] = seq_off[r] - seq_off[0];
+    return orient_impl(ctx, so, grp_off, n_groups, hit_strands, max_hits, n_hits, [&](mando_ctx *c) -> int {
+        HIP_TRY(hipMemcpyAsync(c->seq.p, seqs + seq_off[0], (size_t)total, hipMemcpyHostToDevice, c->stream));
+        return MANDO_OK;
+    });
+}
+
+int mando_orient_segments(mando_ctx *ctx, const uint8_t *d_text, int64_t text_len, const int64_t *off,
+                          const int32_t *len, const int64_t *grp_off, int64_t n_groups, int8_t *hit_strands,
+                          int32_t max_hits, int32_t *n_hits) {
+    if (!ctx || n_groups < 0 || max_hits < 1 || max_hits > 8 || (n_groups > 0 && !grp_off))
+        return fail(MANDO_E_ARG, "mando_orient_segments: bad argument (max_hits must be 1..8)");
+    if (n_groups == 0) return MANDO_OK;
+    int e = check_groups(grp_off, n_groups);
+    if (e) return e;
+    const int64_t n_reads = grp_off[n_groups];
+    if (n_reads > 0 && (!d_text || !off || !len)) return fail(MANDO_E_ARG, "mando_orient_segments: null segments");
+    std::vector<int64_t> soff;
+    if ((e = segment_layout(off, len, n_reads, text_len, soff))) return e;
+    return orient_impl(ctx, soff, grp_off, n_groups, hit_strands, max_hits, n_hits,
+                       [&](mando_ctx *c) { return gather_stage(c, d_text, off, len, nullptr, soff); });
 }
 
 }  // extern "C"

@@ -39,6 +39,10 @@ struct mando_cluster_result {
     vector<char> peak_type, peak_side;
     vector<double> peak_prop;
     vector<int32_t> locus_status;
+    // the same text on the device (freed stream-ordered on the clustering context's stream)
+    mando_ctx *ctx = nullptr;
+    void *d_text = nullptr;
+    ~mando_cluster_result() { mando::cl::release_text(ctx, d_text); }
 };
 
 extern "C" {
@@ -143,6 +147,8 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     in.ann_off = ann_off;
     cl::ClusterOut o;
     const int rc = cl::cluster_gpu(ctx, in, o);
+    res->ctx = ctx;
+    res->d_text = o.d_text;
     if (rc != MANDO_OK) return rc;
     // flatten: records in locus order, isoforms in locus then IsoDict order
     const int64_t nr = o.rec_base[(size_t)n_loci];
@@ -218,6 +224,13 @@ int mando_cluster_view_get(const mando_cluster_result *r, mando_cluster_view *v)
 }
 
 void mando_cluster_free(mando_cluster_result *r) { delete r; }
+
+int mando_cluster_device_text(const mando_cluster_result *r, const uint8_t **d_text, int64_t *len) {
+    if (!r || !d_text || !len) return MANDO_E_ARG;
+    *d_text = static_cast<const uint8_t *>(r->d_text);
+    *len = (int64_t)r->text_len;
+    return MANDO_OK;
+}
 
 // Host helper of the D driver: concatenates n byte segments into out (at out_off[i], caller-computed
 // exclusive prefix sums of lens).  Segment i is src[sel[i]] + starts[i], lens[i] bytes, reverse-

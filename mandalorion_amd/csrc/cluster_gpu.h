@@ -142,6 +142,7 @@ struct ClusterOut {
     std::vector<int64_t> rec_text;  // per record: name_off, name_len, seq_off, seq_len (text-absolute)
     std::vector<std::vector<Peak>> peaks;
     std::vector<std::vector<int32_t>> iso_nmem, mem, iso_nsub, sub;  // locus-local record indices
+    void *d_text = nullptr;  // the locus text on the device (owned by the caller: release_text)
 };
 
 // sizes of the K1 scratch for caps (bytes), 256-aligned pieces
@@ -153,6 +154,7 @@ CL_HD inline int64_t scratch_a_bytes(int64_t line_cap, int64_t op_cap, int64_t b
 }
 
 int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out);
+void release_text(mando_ctx *ctx, void *d_text);
 
 }  // namespace cl
 }  // namespace mando

@@ -2174,15 +2174,24 @@ void o_offsets(const Stats &S, const Locus &L, int64_t *peaks, int64_t *nmem, in
 
 namespace {
 
+// stream-ordered allocations: a hipFree would wait for the whole device, i.e. for the previous
+// chunk's POA kernel running on another stream
 struct DevMem {
     void *p = nullptr;
+    hipStream_t s = nullptr;
+    explicit DevMem(hipStream_t st) : s(st) {}
     ~DevMem() {
-        if (p) (void)hipFree(p);
+        if (p) (void)hipFreeAsync(p, s);
     }
     hipError_t alloc(size_t n) {
-        if (p) (void)hipFree(p);
+        if (p) (void)hipFreeAsync(p, s);
         p = nullptr;
-        return hipMalloc(&p, n > 0 ? n : 1);
+        return hipMallocAsync(&p, n > 0 ? n : 1, s);
+    }
+    void *release() {
+        void *q = p;
+        p = nullptr;
+        return q;
     }
     template <class T>
     T *as() const {
@@ -2212,6 +2221,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     out.iso_nsub.assign((size_t)nl, {});
     out.sub.assign((size_t)nl, {});
     out.rec_text.clear();
+    out.d_text = nullptr;
     if (nl == 0) return MANDO_OK;
     CL_TRY(hipSetDevice(mando::ctx_device(ctx)));
     hipStream_t s = mando::ctx_stream(ctx);
@@ -2273,7 +2283,8 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
                      [&](int32_t a, int32_t b) { return L[(size_t)a].text_len > L[(size_t)b].text_len; });
     const int nrun = (int)run_order.size();
 
-    DevMem d_text, d_chroms, d_ann, d_loci, d_order, d_stats, d_a, d_b, d_o, d_rec, d_prm;
+    DevMem d_text(s), d_chroms(s), d_ann(s), d_loci(s), d_order(s), d_stats(s), d_a(s), d_b(s), d_o(s), d_rec(s),
+        d_prm(s);
     CL_TRY(d_text.alloc((size_t)in.text_len + 64));
     CL_TRY(hipMemcpyAsync(d_text.p, in.text, (size_t)in.text_len, hipMemcpyHostToDevice, s));
     CL_TRY(d_chroms.alloc(chroms.size() + 1));
@@ -2406,7 +2417,12 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
             out.sub[(size_t)i].assign((const int32_t *)(base + os), (const int32_t *)(base + os) + y.n_sub);
         }
     }
+    out.d_text = d_text.release();  // the orientation / POA inputs are gathered from it
     return MANDO_OK;
+}
+
+void release_text(mando_ctx *ctx, void *d_text) {
+    if (d_text) (void)hipFreeAsync(d_text, mando::ctx_stream(ctx));
 }
 
 }  // namespace cl

@@ -53,6 +53,19 @@ def gpu_orient(seqs, seq_off, grp_off, device: int = 0, max_hits: int = 4):
     return hits, nh
 
 
+def gpu_orient_segments(res, off, length, grp_off, device: int = 0, max_hits: int = 4):
+    """gpu_orient over reads that stay in the clustering result's device text (no host packing)."""
+    from . import orient
+
+    d, n = res.device_text()
+    hits, nh = orient.orient_segments(d, n, off, length, grp_off, device=device, max_hits=max_hits, slot=1)
+    if len(nh) and int(nh.max()) > max_hits:
+        if max_hits >= 8:
+            raise _lib.MandoError(-5, "a read has more than 8 primary hits against its isoform's first read")
+        return gpu_orient_segments(res, off, length, grp_off, device=device, max_hits=8)
+    return hits, nh
+
+
 def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0, info: dict | None = None, slot: int = 0):
     from . import poa
 
@@ -122,14 +135,19 @@ class Assembly:
                                 dtype=np.uint8)
         self.res = res
 
-    def poa_input(self):
+    def poa_segments(self):
+        """The POA input as (text offset, length, reverse-complement flag) per emission + group offsets."""
         sel = ~self.direct[self.e_iso]
         rec = self.e_rec[sel]
-        seqs, off = _lib.pack_segments([self.res.text], self.res.seq_off[rec], self.res.seq_len[rec],
-                                       rc=(self.e_sign[sel] == -1).astype(np.int8))
         grp = np.zeros(len(self.poa_iso) + 1, dtype=np.int64)
         np.cumsum(self.n_emit[self.poa_iso], out=grp[1:])
-        return seqs, off, grp
+        return self.res.seq_off[rec], self.res.seq_len[rec], (self.e_sign[sel] == -1).astype(np.int8), grp
+
+    def poa_input(self):
+        """The POA input packed on the host (for an injected consensus_fn)."""
+        off, length, rc, grp = self.poa_segments()
+        seqs, so = _lib.pack_segments([self.res.text], off, length, rc=rc)
+        return seqs, so, grp
 
 
 def _fasta_and_r2i(names_src, name_start, name_len, mem_off, cons_src, cons_sel, cons_start, cons_len, cons_rc,
@@ -183,27 +201,37 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     comm (mandalorion_amd.comm.Comm, optional): shard the loci over comm.world ranks; rank 0 writes."""
     t0 = time.perf_counter()
     rank, world = (comm.rank, comm.world) if comm is not None else (0, 1)
-    orient_fn = orient_fn or (lambda s, o, g: gpu_orient(s, o, g, device=device))
+    # the HIP path keeps the reads on the device (gathered from the clustering's device text); injected
+    # host functions get them packed
+    dev_orient = orient_fn is None
+    dev_poa = consensus_fn is None
     poa_launches = []  # per POA call: DP cells, kernel ms, read + consensus bytes (the roofline's inputs)
 
     poa_slots: dict = {}
     slot_lock = threading.Lock()
 
-    def _gpu_poa(s, o, g, sd):
+    def _gpu_poa(res, off, length, rc, g, sd):
         # one device context (stream + buffers) per POA host thread: slots 0 and 3 (1: orientation)
+        from . import poa
+
         tid = threading.get_ident()
         with slot_lock:
             slot = poa_slots.setdefault(tid, 3 * len(poa_slots))
         info = {}
-        out = gpu_consensus(s, o, g, sd, device=device, info=info, slot=slot)
+        d, n = res.device_text()
+        out = poa.poa_consensus_segments(d, n, off, length, rc, g, seeding=sd, device=device, info=info, slot=slot)
         if "kernel_ms" in info:
-            info["read_bytes"] = int(o[-1] - o[0])
+            info["read_bytes"] = int(np.asarray(length, dtype=np.int64).sum())
             info["cons_bytes"] = int(out[1][-1])
             info["reads"] = int(g[-1])
             poa_launches.append(info)
         return out
 
-    consensus_fn = consensus_fn or _gpu_poa
+    def run_poa(res, prep):
+        asm = prep[0]
+        if dev_poa:
+            return _gpu_poa(res, *prep[1:], asm.seeding)
+        return consensus_fn(*prep[1:], asm.seeding)
     out_path = path + "/"
     out_tmp = out_path + "/tmp_SS"
     wl = list(white_list_polyA)
@@ -273,7 +301,10 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             r.close()
             raise RuntimeError(f"locus {my_roots[lo + i]}: {cluster.STATUS.get(code, code)} "
                                "(the reference's locus worker raises here)")
-        o_in = _lib.pack_segments([r.text], r.seq_off[r.sub], r.seq_len[r.sub])
+        if dev_orient:
+            o_in = (r.seq_off[r.sub], r.seq_len[r.sub])
+        else:
+            o_in = _lib.pack_segments([r.text], r.seq_off[r.sub], r.seq_len[r.sub])
         return r, te - tc, o_in, time.perf_counter() - te
 
     from concurrent.futures import ThreadPoolExecutor
@@ -294,7 +325,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     def assemble(res, hits, n_hits):
         ta = time.perf_counter()
         asm = Assembly(res, hits, n_hits)
-        prep = (asm,) + tuple(asm.poa_input())
+        prep = (asm,) + tuple(asm.poa_segments() if dev_poa else asm.poa_input())
         te = time.perf_counter()
         add("t_assemble", te - ta)
         timeline.append(("assemble", ta - t0, te - t0))
@@ -313,7 +344,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     def poa_job(res, asm_fut, lo, hi):
         prep = asm_fut.result()
         tp = time.perf_counter()
-        pl = _poa_chunk(res, mine[lo:hi], prep, consensus_fn, stats, lock)
+        pl = _poa_chunk(res, mine[lo:hi], prep, run_poa, stats, lock)
         timeline.append(("poa", tp - t0, time.perf_counter() - t0))
         return pl, res
 
@@ -323,11 +354,14 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         cl = [ex.submit(run_cluster, lo, hi) for lo, hi in spans]
         poa_futs = []
         for k, (lo, hi) in enumerate(spans):
-            res, tcl, (o_seqs, o_off), tpk = cl[k].result()
+            res, tcl, (o_a, o_b), tpk = cl[k].result()
             add("t_cluster", tcl)
             add("t_pack", tpk)
             tg = time.perf_counter()
-            hits, n_hits = orient_fn(o_seqs, o_off, res.sub_off)
+            if dev_orient:
+                hits, n_hits = gpu_orient_segments(res, o_a, o_b, res.sub_off, device=device)
+            else:
+                hits, n_hits = orient_fn(o_a, o_b, res.sub_off)
             te = time.perf_counter()
             timeline.append(("orient", tg - t0, te - t0))
             add("t_orient", te - tg)
@@ -372,11 +406,11 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     return stats
 
 
-def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, consensus_fn, stats: dict, lock):
+def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, run_poa, stats: dict, lock):
     """POA of one oriented chunk; returns its writer payload."""
-    asm, p_seqs, p_off, p_grp = prep
+    asm, p_grp = prep[0], prep[-1]
     t3 = time.perf_counter()
-    cons, cons_off = consensus_fn(p_seqs, p_off, p_grp, asm.seeding)
+    cons, cons_off = run_poa(res, prep)
     t4 = time.perf_counter()
     # consensus of every isoform as a byte segment: POA output, else (<=2 sequences, or an empty POA
     # result) the first emission, re-bound (SDC:911-926)

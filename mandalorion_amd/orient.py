@@ -55,3 +55,20 @@ def orient_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndarray, de
                                               _lib.ptr(np.ascontiguousarray(grp_off, np.int64)), len(grp_off) - 1,
                                               _lib.ptr(hits), max_hits, _lib.ptr(nh)))
     return hits[:n], nh[:n]
+
+
+def orient_segments(d_text: int, text_len: int, off: np.ndarray, length: np.ndarray, grp_off: np.ndarray,
+                    device: int = 0, max_hits: int = 4, slot: int = 0):
+    """orient_packed over reads that stay on the device: read r = d_text[off[r] .. off[r] + length[r])
+    (mando_orient_segments; d_text from ClusterResult.device_text())."""
+    ctx = _lib.context(device, slot)
+    n = int(len(off))
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    length = np.ascontiguousarray(length, dtype=np.int32)
+    hits = np.zeros((max(n, 1), max_hits), dtype=np.int8)
+    nh = np.zeros(max(n, 1), dtype=np.int32)
+    if len(grp_off) > 1:
+        _lib.check(ctx.lib.mando_orient_segments(ctx.handle, _lib.ctypes.c_void_p(d_text), int(text_len), _lib.ptr(off),
+                                                 _lib.ptr(length), _lib.ptr(np.ascontiguousarray(grp_off, np.int64)),
+                                                 len(grp_off) - 1, _lib.ptr(hits), max_hits, _lib.ptr(nh)))
+    return hits[:n], nh[:n]

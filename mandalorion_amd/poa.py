@@ -104,3 +104,32 @@ def poa_consensus_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndar
             info["kernel_ms"] = ctx.last_kernel_ms()
             info["launches"] = ctx.last_kernel_launches()
     return cons[:int(cons_off[-1])], cons_off
+
+
+def poa_consensus_segments(d_text: int, text_len: int, off: np.ndarray, length: np.ndarray, rc: np.ndarray | None,
+                           grp_off: np.ndarray, seeding=None, device: int = 0, params: _lib.PoaParams | None = None,
+                           info: dict | None = None, slot: int = 0):
+    """poa_consensus_packed over reads that stay on the device (mando_poa_segments): read r =
+    d_text[off[r] .. off[r] + length[r]), reverse-complemented when rc[r]."""
+    ctx = _lib.context(device, slot)
+    p = params or _lib.PoaParams.defaults()
+    n = int(len(grp_off)) - 1
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    length = np.ascontiguousarray(length, dtype=np.int32)
+    rc = None if rc is None else np.ascontiguousarray(rc, dtype=np.int8)
+    grp_off = np.ascontiguousarray(grp_off, dtype=np.int64)
+    seed_arr = None if seeding is None else np.ascontiguousarray(np.asarray(seeding, dtype=np.uint8))
+    cap = int(length.sum()) * 2 + 1024
+    cons = np.empty(cap, dtype=np.uint8)
+    cons_off = np.zeros(n + 1, dtype=np.int64)
+    cells = np.zeros(max(n, 1), dtype=np.int64) if info is not None else None
+    if n > 0:
+        _lib.check(ctx.lib.mando_poa_segments(ctx.handle, _lib.ctypes.byref(p), _lib.ctypes.c_void_p(d_text),
+                                              int(text_len), _lib.ptr(off), _lib.ptr(length), _lib.ptr(rc),
+                                              _lib.ptr(grp_off), n, _lib.ptr(seed_arr), _lib.ptr(cons), cap,
+                                              _lib.ptr(cons_off), _lib.ptr(cells)))
+        if info is not None:
+            info["cells"] = int(cells[:n].sum())
+            info["kernel_ms"] = ctx.last_kernel_ms()
+            info["launches"] = ctx.last_kernel_launches()
+    return cons[:int(cons_off[-1])], cons_off
