@@ -248,6 +248,8 @@ def pack_segments(srcs: list[np.ndarray], starts: np.ndarray, lens: np.ndarray, 
     out = np.empty(max(int(off[-1]), 1), dtype=np.uint8)
     if n == 0:
         return out[:0], off
+    if len(srcs) > 127:
+        raise ValueError("pack_segments: at most 127 sources (int8 selectors)")
     keep = [np.ascontiguousarray(s, dtype=np.uint8) for s in srcs]
     ptrs = (ctypes.c_void_p * len(keep))(*[k.ctypes.data for k in keep])
     starts = np.ascontiguousarray(starts, dtype=np.int64)

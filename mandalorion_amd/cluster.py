@@ -147,13 +147,11 @@ def c_inputs(paths: list[str], chroms: list[str], ann):
     cchroms = (ctypes.c_char_p * max(n, 1))(*[x.encode() for x in chroms])
     ann_pos = ann_off = None
     if ann is not None:
-        flat, off = [], [0]
-        for i in range(n):
-            for s in range(4):
-                flat.extend(int(v) for v in ann[i][s])
-                off.append(len(flat))
-        ann_pos = np.asarray(flat if flat else [0], dtype=np.int64)
-        ann_off = np.asarray(off, dtype=np.int64)
+        parts = [np.asarray(ann[i][s], dtype=np.int64).ravel() for i in range(n) for s in range(4)]
+        off = np.zeros(4 * n + 1, dtype=np.int64)
+        np.cumsum([len(x) for x in parts], out=off[1:])
+        ann_pos = np.concatenate(parts) if parts and off[-1] else np.zeros(1, dtype=np.int64)
+        ann_off = off
     return n, cpaths, cchroms, ann_pos, ann_off
 
 

@@ -99,6 +99,22 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint8_t *__restrict__
     }
 }
 
+// consensus codes (0-4) of group g at cons[src_off[g] ..] -> ASCII at dst[dst_off[g] ..]
+__global__ __launch_bounds__(256) void decode_cons_kernel(const uint8_t *__restrict__ cons,
+                                                          const int64_t *__restrict__ src_off,
+                                                          const int32_t *__restrict__ len,
+                                                          const int64_t *__restrict__ dst_off, int64_t n,
+                                                          uint8_t *__restrict__ dst) {
+    for (int64_t g = blockIdx.x; g < n; g += gridDim.x) {
+        const uint8_t *s = cons + src_off[g];
+        uint8_t *d = dst + dst_off[g];
+        for (int k = threadIdx.x; k < len[g]; k += 256) {
+            const uint8_t c = s[k];
+            d[k] = c == 0 ? 'A' : c == 1 ? 'C' : c == 2 ? 'G' : c == 3 ? 'T' : 'N';
+        }
+    }
+}
+
 uint8_t g_enc[256];
 struct EncInit {
     EncInit() {
@@ -109,7 +125,6 @@ struct EncInit {
         g_enc['T'] = g_enc['t'] = 3;
     }
 } g_enc_init;
-const char g_dec[5] = {'A', 'C', 'G', 'T', 'N'};
 
 }  // namespace
 
@@ -125,11 +140,12 @@ struct mando_ctx {
     DevBuf o_hits, o_strand, o_status;
     DevBuf s_items, s_item_of, s_n, s_t, s_q, s_scratch, s_redo, gorder2;  // -S partition
     DevBuf g_off, g_len, g_rc, g_dst;                                      // segment gather
+    DevBuf cons_txt;                                                       // decoded consensi
     ~mando_ctx() {
         for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
                           &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx, &s_items,
                           &s_item_of, &s_n, &s_t, &s_q, &s_scratch, &s_redo, &gorder2, &g_off, &g_len, &g_rc,
-                          &g_dst})
+                          &g_dst, &cons_txt})
             b->release();
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -581,7 +597,6 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
     std::vector<int32_t> st((size_t)n_groups), clen((size_t)n_groups);
     std::vector<int64_t> cells((size_t)n_groups);
     std::vector<int32_t> todo = order;
-    std::vector<uint8_t> cons_enc((size_t)ccap[(size_t)n_groups]);
     ctx->last_launches = 0;
     for (int attempt = 0; attempt < 4 && !todo.empty(); ++attempt) {
         // unseeded and seeded groups run as two launches of the two kernel instantiations
@@ -618,7 +633,6 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
         HIP_TRY(hipMemcpyAsync(st.data(), ctx->status.p, st.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipMemcpyAsync(clen.data(), ctx->cons_len.p, clen.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipMemcpyAsync(cells.data(), ctx->cells.p, cells.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(cons_enc.data(), ctx->cons.p, cons_enc.size(), hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         std::vector<int32_t> again;
         for (int32_t g : todo) {
@@ -632,17 +646,28 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
     if (!todo.empty())
         return fail(MANDO_E_INTERNAL, "POA workspace capacity still exceeded after retries");
 
+    // consensi: decoded to ASCII and packed back to back on the device, then one copy of the used bytes
     int64_t used = 0;
     cons_off[0] = 0;
     for (int64_t g = 0; g < n_groups; ++g) {
-        const int64_t L = clen[(size_t)g];
-        if (cons_out && used + L <= cons_cap) {
-            const uint8_t *src = cons_enc.data() + ccap[(size_t)g];
-            for (int64_t t = 0; t < L; ++t) cons_out[used + t] = (uint8_t)g_dec[src[t] > 4 ? 4 : src[t]];
-        }
-        used += L;
+        used += clen[(size_t)g];
         cons_off[g + 1] = used;
         if (cells_out) cells_out[g] = cells[(size_t)g];
+    }
+    if (cons_out && used > 0 && used <= cons_cap) {
+        if ((rc = ctx->g_dst.ensure(((size_t)n_groups + 1) * 8)) || (rc = ctx->g_len.ensure((size_t)n_groups * 4)) ||
+            (rc = ctx->g_off.ensure((size_t)(n_groups + 1) * 8)) || (rc = ctx->cons_txt.ensure((size_t)used + 16)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->g_dst.p, cons_off, ((size_t)n_groups + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->g_len.p, clen.data(), (size_t)n_groups * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->g_off.p, ccap.data(), ((size_t)n_groups + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        const int blocks = (int)std::min<int64_t>(n_groups, (int64_t)ctx->n_cu * 32);
+        hipLaunchKernelGGL(decode_cons_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ctx->cons.as<uint8_t>(),
+                           ctx->g_off.as<int64_t>(), ctx->g_len.as<int32_t>(), ctx->g_dst.as<int64_t>(), n_groups,
+                           ctx->cons_txt.as<uint8_t>());
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(cons_out, ctx->cons_txt.p, (size_t)used, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
     if (used > cons_cap || (!cons_out && used > 0)) return fail(MANDO_E_CAP, "cons_out too small");
     return MANDO_OK;

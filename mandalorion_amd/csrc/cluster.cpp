@@ -9,15 +9,18 @@
 // and the output files.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
-#include <thread>
-#include <vector>
 
 #include <sys/mman.h>
+#include <thread>
+#include <vector>
 
 #include "../../include/mando.h"
 #include "cluster_gpu.h"
@@ -27,10 +30,62 @@
 using std::string;
 using std::vector;
 
+namespace {
+
+// Host buffers for the locus text, kept for reuse (2 MB-aligned, transparent huge pages: a chunk's
+// few GB then costs no first-touch page faults and no munmap on the next call).  They are pageable:
+// the copies to the device are staged by the runtime.  Reusing page-locked buffers instead was
+// measured to hand the kernels stale bytes on MI355X (a rewritten pinned buffer copied again, 12 of 15
+// runs; never with fresh or pageable buffers), and pinning fresh buffers each call costs more than
+// the staging (14k loci: 1.2-1.4 s vs 0.57-0.64 s).
+struct PinnedPool {
+    std::mutex mu;
+    std::vector<std::pair<char *, size_t>> free_list;
+    char *acquire(size_t need, size_t &cap) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            size_t best = (size_t)-1;
+            for (size_t i = 0; i < free_list.size(); ++i)
+                if (free_list[i].second >= need && (best == (size_t)-1 || free_list[i].second < free_list[best].second))
+                    best = i;
+            if (best != (size_t)-1) {
+                auto e = free_list[best];
+                free_list.erase(free_list.begin() + (ptrdiff_t)best);
+                cap = e.second;
+                return e.first;
+            }
+        }
+        constexpr size_t kStep = size_t(256) << 20;
+        cap = (std::max<size_t>(need, 1) + kStep - 1) / kStep * kStep;
+        void *p = nullptr;
+        if (posix_memalign(&p, size_t(2) << 20, cap) != 0) return nullptr;
+        (void)madvise(p, cap, MADV_HUGEPAGE);
+        return static_cast<char *>(p);
+    }
+    void release(char *p, size_t cap) {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(mu);
+        free_list.push_back({p, cap});
+        // keep at most the two largest buffers (two chunks in flight)
+        while (free_list.size() > 2) {
+            auto it = std::min_element(free_list.begin(), free_list.end(),
+                                       [](const auto &a, const auto &b) { return a.second < b.second; });
+            free(it->first);
+            free_list.erase(it);
+        }
+    }
+};
+PinnedPool &pool() {
+    static PinnedPool *p = new PinnedPool();  // never destroyed: buffers live until process exit
+    return *p;
+}
+
+}  // namespace
+
 struct mando_cluster_result {
-    // all locus files; left uninitialised (the parallel reads fault it in), 2 MB-aligned and advised
-    // for transparent huge pages, so a chunk's ~1 GB costs a few hundred faults, not ~300k
-    std::unique_ptr<char, void (*)(void *)> text{nullptr, free};
+    // all locus files, in a buffer from the pool (returned to it on destruction)
+    char *text_p = nullptr;
+    size_t text_cap = 0;
     size_t text_len = 0;
     vector<int64_t> name_off, seq_off, rec_locus;
     vector<int32_t> name_len, seq_len;
@@ -42,7 +97,11 @@ struct mando_cluster_result {
     // the same text on the device (freed stream-ordered on the clustering context's stream)
     mando_ctx *ctx = nullptr;
     void *d_text = nullptr;
-    ~mando_cluster_result() { mando::cl::release_text(ctx, d_text); }
+    size_t d_cap = 0;
+    ~mando_cluster_result() {
+        mando::cl::release_text(ctx, d_text, d_cap);
+        pool().release(text_p, text_cap);
+    }
 };
 
 extern "C" {
@@ -104,41 +163,68 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     }
     for (int64_t i = 0; i < n_loci; ++i) foff[(size_t)i + 1] = foff[(size_t)i] + std::max<int64_t>(0, fsize[(size_t)i]);
     res->text_len = (size_t)foff[(size_t)n_loci];
-    {
-        constexpr size_t kHuge = size_t(2) << 20;
-        const size_t bytes = (std::max<size_t>(res->text_len, 1) + kHuge - 1) / kHuge * kHuge;
-        void *buf = nullptr;
-        if (posix_memalign(&buf, kHuge, bytes) != 0) return MANDO_E_NOMEM;
-        (void)madvise(buf, bytes, MADV_HUGEPAGE);
-        res->text.reset(static_cast<char *>(buf));
-    }
+    res->text_p = pool().acquire(res->text_len + 64, res->text_cap);
+    if (!res->text_p) return mando::set_error(MANDO_E_NOMEM, "cluster: pinned host buffer");
+    // device copy of the text, filled piecewise while later files are still being read
+    hipStream_t stream = mando::ctx_stream(ctx);
+    size_t d_cap = 0;
+    void *d_text = hipSetDevice(mando::ctx_device(ctx)) == hipSuccess
+                       ? mando::cl::acquire_text(ctx, res->text_len + 64, d_cap) : nullptr;
+    if (!d_text) return mando::set_error(MANDO_E_NOMEM, "cluster: device text buffer");
+    res->ctx = ctx;
+    res->d_text = d_text;
+    res->d_cap = d_cap;
     int nth = prm->threads > 0 ? prm->threads : (int)std::max(1u, std::thread::hardware_concurrency());
     nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n_loci));
     std::atomic<int64_t> next{0};
+    vector<std::atomic<uint8_t>> done((size_t)n_loci);
+    for (auto &d : done) d.store(0);
+    std::mutex mu;
+    std::condition_variable cv;
     auto reader = [&]() {
         while (true) {
             const int64_t i = next.fetch_add(1);
             if (i >= n_loci) break;
             if (fsize[(size_t)i] < 0) {
                 fstatus[(size_t)i] = cl::kIO;
-                continue;
-            }
-            FILE *fh = fopen(psl_paths[i], "rb");
-            if (!fh) {
+            } else if (FILE *fh = fopen(psl_paths[i], "rb")) {
+                const size_t got = fread(res->text_p + foff[(size_t)i], 1, (size_t)fsize[(size_t)i], fh);
+                fclose(fh);
+                if ((int64_t)got != fsize[(size_t)i]) fstatus[(size_t)i] = cl::kIO;
+            } else {
                 fstatus[(size_t)i] = cl::kIO;
-                continue;
             }
-            const size_t got = fread(res->text.get() + foff[(size_t)i], 1, (size_t)fsize[(size_t)i], fh);
-            fclose(fh);
-            if ((int64_t)got != fsize[(size_t)i]) fstatus[(size_t)i] = cl::kIO;
+            done[(size_t)i].store(1, std::memory_order_release);
+            cv.notify_one();
         }
     };
     {
         vector<std::thread> th;
         for (int t = 0; t < nth; ++t) th.emplace_back(reader);
+        // copy the completed prefix in >= 64 MB pieces as the readers advance
+        constexpr int64_t kPiece = int64_t(64) << 20;
+        int64_t upto = 0, sent = 0;
+        while (upto < n_loci) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait_for(lk, std::chrono::microseconds(200),
+                            [&] { return done[(size_t)upto].load(std::memory_order_acquire) != 0; });
+            }
+            while (upto < n_loci && done[(size_t)upto].load(std::memory_order_acquire)) ++upto;
+            const int64_t avail = foff[(size_t)upto];
+            if (avail - sent >= kPiece || (upto == n_loci && avail > sent)) {
+                if (hipMemcpyAsync((char *)d_text + sent, res->text_p + sent, (size_t)(avail - sent),
+                                   hipMemcpyHostToDevice, stream) != hipSuccess) {
+                    for (auto &t : th) t.join();
+                    return mando::set_error(MANDO_E_HIP, "cluster: text copy to the device");
+                }
+                sent = avail;
+            }
+        }
         for (auto &t : th) t.join();
     }
-    in.text = res->text.get();
+    in.text = res->text_p;
+    in.d_text = d_text;
     in.text_len = (int64_t)res->text_len;
     in.foff = foff.data();
     in.fstatus = fstatus.data();
@@ -147,8 +233,6 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     in.ann_off = ann_off;
     cl::ClusterOut o;
     const int rc = cl::cluster_gpu(ctx, in, o);
-    res->ctx = ctx;
-    res->d_text = o.d_text;
     if (rc != MANDO_OK) return rc;
     // flatten: records in locus order, isoforms in locus then IsoDict order
     const int64_t nr = o.rec_base[(size_t)n_loci];
@@ -199,7 +283,7 @@ int mando_cluster_view_get(const mando_cluster_result *r, mando_cluster_view *v)
     if (!r || !v) return MANDO_E_ARG;
     v->n_loci = (int64_t)r->locus_status.size();
     v->locus_status = r->locus_status.data();
-    v->text = r->text.get();
+    v->text = r->text_p;
     v->text_len = (int64_t)r->text_len;
     v->n_records = (int64_t)r->name_off.size();
     v->name_off = r->name_off.data();

@@ -127,6 +127,7 @@ struct ClusterIn {
     int64_t n_loci;
     const char *text;
     int64_t text_len;
+    void *d_text;             // the same text already on (or being copied to) the device, stream-ordered
     const int64_t *foff;      // n_loci + 1 offsets of each locus file in text
     const int32_t *fstatus;   // kOk, or kIO for a file that could not be read
     const char *const *chroms;
@@ -142,7 +143,6 @@ struct ClusterOut {
     std::vector<int64_t> rec_text;  // per record: name_off, name_len, seq_off, seq_len (text-absolute)
     std::vector<std::vector<Peak>> peaks;
     std::vector<std::vector<int32_t>> iso_nmem, mem, iso_nsub, sub;  // locus-local record indices
-    void *d_text = nullptr;  // the locus text on the device (owned by the caller: release_text)
 };
 
 // sizes of the K1 scratch for caps (bytes), 256-aligned pieces
@@ -154,7 +154,9 @@ CL_HD inline int64_t scratch_a_bytes(int64_t line_cap, int64_t op_cap, int64_t b
 }
 
 int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out);
-void release_text(mando_ctx *ctx, void *d_text);
+// the device copy of the locus text (cached whole buffers; the result keeps one until it is freed)
+void *acquire_text(mando_ctx *ctx, size_t need, size_t &cap);
+void release_text(mando_ctx *ctx, void *d_text, size_t cap);
 
 }  // namespace cl
 }  // namespace mando

@@ -19,6 +19,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -2174,30 +2178,45 @@ void o_offsets(const Stats &S, const Locus &L, int64_t *peaks, int64_t *nmem, in
 
 namespace {
 
-// stream-ordered allocations: a hipFree would wait for the whole device, i.e. for the previous
-// chunk's POA kernel running on another stream
+// Device buffers are hipMalloc'd and kept per context for reuse (grown, never shrunk).  Not the
+// stream-ordered pool: memory it recycles and then refills with a host-to-device copy was measured to
+// give the kernels stale bytes on MI355X / ROCm 7.2 (a recycled text buffer, 11 of 15 repeated calls;
+// none with hipMalloc'd buffers), and a hipFree per call would wait for the whole device.
+std::mutex g_buf_mu;
+std::map<std::pair<const mando_ctx *, int>, std::pair<void *, size_t>> g_bufs;
+
 struct DevMem {
+    const mando_ctx *ctx;
+    int id;
     void *p = nullptr;
-    hipStream_t s = nullptr;
-    explicit DevMem(hipStream_t st) : s(st) {}
-    ~DevMem() {
-        if (p) (void)hipFreeAsync(p, s);
-    }
+    DevMem(const mando_ctx *c, int i) : ctx(c), id(i) {}
     hipError_t alloc(size_t n) {
-        if (p) (void)hipFreeAsync(p, s);
-        p = nullptr;
-        return hipMallocAsync(&p, n > 0 ? n : 1, s);
-    }
-    void *release() {
-        void *q = p;
-        p = nullptr;
-        return q;
+        n = std::max<size_t>(n, 256);
+        std::lock_guard<std::mutex> g(g_buf_mu);
+        auto &e = g_bufs[{ctx, id}];
+        if (e.first && e.second >= n) {
+            p = e.first;
+            return hipSuccess;
+        }
+        if (e.first) (void)hipFree(e.first);
+        e = {nullptr, 0};
+        const size_t cap = n + n / 4;  // headroom: chunk sizes vary from call to call
+        hipError_t r = hipMalloc(&p, cap);
+        if (r != hipSuccess) {
+            p = nullptr;
+            return r;
+        }
+        e = {p, cap};
+        return hipSuccess;
     }
     template <class T>
     T *as() const {
         return (T *)p;
     }
 };
+
+// the device copy of a result's locus text outlives the call: a small cache of whole buffers
+std::vector<std::pair<void *, size_t>> g_text_free;
 
 #define CL_TRY(expr)                                                                             \
     do {                                                                                         \
@@ -2221,7 +2240,6 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     out.iso_nsub.assign((size_t)nl, {});
     out.sub.assign((size_t)nl, {});
     out.rec_text.clear();
-    out.d_text = nullptr;
     if (nl == 0) return MANDO_OK;
     CL_TRY(hipSetDevice(mando::ctx_device(ctx)));
     hipStream_t s = mando::ctx_stream(ctx);
@@ -2283,10 +2301,8 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
                      [&](int32_t a, int32_t b) { return L[(size_t)a].text_len > L[(size_t)b].text_len; });
     const int nrun = (int)run_order.size();
 
-    DevMem d_text(s), d_chroms(s), d_ann(s), d_loci(s), d_order(s), d_stats(s), d_a(s), d_b(s), d_o(s), d_rec(s),
-        d_prm(s);
-    CL_TRY(d_text.alloc((size_t)in.text_len + 64));
-    CL_TRY(hipMemcpyAsync(d_text.p, in.text, (size_t)in.text_len, hipMemcpyHostToDevice, s));
+    DevMem d_chroms(ctx, 0), d_ann(ctx, 1), d_loci(ctx, 2), d_order(ctx, 3), d_stats(ctx, 4), d_a(ctx, 5),
+        d_b(ctx, 6), d_o(ctx, 7), d_rec(ctx, 8), d_prm(ctx, 9);
     CL_TRY(d_chroms.alloc(chroms.size() + 1));
     CL_TRY(hipMemcpyAsync(d_chroms.p, chroms.data(), chroms.size() + 1, hipMemcpyHostToDevice, s));
     CL_TRY(d_ann.alloc((ann.size() + 1) * 8));
@@ -2300,7 +2316,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     std::vector<Stats> st((size_t)nl);
 
     Args G;
-    G.text = d_text.as<uint8_t>();
+    G.text = static_cast<const uint8_t *>(in.d_text);
     G.chroms = d_chroms.as<uint8_t>();
     G.ann_pos = d_ann.as<int64_t>();
     G.loci = d_loci.as<Locus>();
@@ -2339,6 +2355,13 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         if (!again) break;
     }
 
+    if (getenv("MANDO_CL_DEBUG"))
+        for (int64_t i = 0; i < nl; ++i) {
+            const Stats &x = st[(size_t)i];
+            fprintf(stderr, "[K1] %lld st %d rec %d ops %d blk %d hl %d hr %d span %lld %lld cov %lld id %lld\n",
+                    (long long)i, x.status, x.n_rec, x.n_ops, x.n_blk, x.n_hist_l, x.n_hist_r, (long long)x.span_lo,
+                    (long long)x.span_hi, (long long)x.cov_cap, (long long)x.ident_cap);
+        }
     // K2 sizes from K1's statistics: dense position maps over the locus span and its annotation
     const int64_t M = 4 * (int64_t)in.w + in.up + in.down + 256;
     int64_t b_tot = 0, o_tot = 0, recs = 0;
@@ -2402,6 +2425,12 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         CL_TRY(hipMemcpyAsync(ho.data(), d_o.p, (size_t)o_tot, hipMemcpyDeviceToHost, s));
         if (recs) CL_TRY(hipMemcpyAsync(out.rec_text.data(), d_rec.p, (size_t)recs * 32, hipMemcpyDeviceToHost, s));
         CL_TRY(hipStreamSynchronize(s));
+        if (getenv("MANDO_CL_DEBUG"))
+            for (int32_t i : k2_order) {
+                const Stats &x = st[(size_t)i];
+                fprintf(stderr, "[K2] %d st %d peaks %d iso %d mem %d sub %d\n", i, x.status, x.n_peaks, x.n_iso,
+                        x.n_mem, x.n_sub);
+            }
         for (int32_t i : k2_order) {
             const Stats &y = st[(size_t)i];
             out.status[(size_t)i] = y.status;
@@ -2417,12 +2446,42 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
             out.sub[(size_t)i].assign((const int32_t *)(base + os), (const int32_t *)(base + os) + y.n_sub);
         }
     }
-    out.d_text = d_text.release();  // the orientation / POA inputs are gathered from it
     return MANDO_OK;
 }
 
-void release_text(mando_ctx *ctx, void *d_text) {
-    if (d_text) (void)hipFreeAsync(d_text, mando::ctx_stream(ctx));
+void *acquire_text(mando_ctx *ctx, size_t need, size_t &cap) {
+    (void)ctx;
+    {
+        std::lock_guard<std::mutex> g(g_buf_mu);
+        size_t best = (size_t)-1;
+        for (size_t i = 0; i < g_text_free.size(); ++i)
+            if (g_text_free[i].second >= need && (best == (size_t)-1 || g_text_free[i].second < g_text_free[best].second))
+                best = i;
+        if (best != (size_t)-1) {
+            auto e = g_text_free[best];
+            g_text_free.erase(g_text_free.begin() + (ptrdiff_t)best);
+            cap = e.second;
+            return e.first;
+        }
+    }
+    constexpr size_t kStep = size_t(256) << 20;
+    cap = (std::max<size_t>(need, 1) + kStep - 1) / kStep * kStep;
+    void *p = nullptr;
+    if (hipMalloc(&p, cap) != hipSuccess) return nullptr;
+    return p;
+}
+
+void release_text(mando_ctx *ctx, void *d_text, size_t cap) {
+    (void)ctx;
+    if (!d_text) return;
+    std::lock_guard<std::mutex> g(g_buf_mu);
+    g_text_free.push_back({d_text, cap});
+    while (g_text_free.size() > 2) {  // two chunks in flight
+        auto it = std::min_element(g_text_free.begin(), g_text_free.end(),
+                                   [](const auto &a, const auto &b) { return a.second < b.second; });
+        (void)hipFree(it->first);
+        g_text_free.erase(it);
+    }
 }
 
 }  // namespace cl

@@ -130,9 +130,16 @@ class Assembly:
         self.poa_iso = np.nonzero(~self.direct)[0]
         self.e_rec = res.sub[self.e_read] if n_sub else np.zeros(0, np.int64)
         # -S when the median subsample length (all subsampled reads, mapped or not) is >= 8000
-        lens = res.seq_len[res.sub].astype(np.int64) if n_sub else np.zeros(0, np.int64)
-        self.seeding = np.array([np.median(lens[sub_off[i]:sub_off[i + 1]]) >= 8000 for i in self.poa_iso],
-                                dtype=np.uint8)
+        # (np.median of a group = mean of its two middle values: sort inside groups, pick them)
+        self.seeding = np.zeros(len(self.poa_iso), dtype=np.uint8)
+        if len(self.poa_iso):
+            lens = res.seq_len[res.sub].astype(np.int64)
+            gid = np.repeat(np.arange(n_iso), np.diff(sub_off))
+            srt = lens[np.lexsort((lens, gid))]
+            lo = sub_off[:-1] + (np.diff(sub_off) - 1) // 2
+            hi = sub_off[:-1] + np.diff(sub_off) // 2
+            med2 = srt[np.minimum(lo, max(n_sub - 1, 0))] + srt[np.minimum(hi, max(n_sub - 1, 0))]
+            self.seeding = (med2[self.poa_iso] >= 16000).astype(np.uint8)
         self.res = res
 
     def poa_segments(self):
@@ -150,10 +157,11 @@ class Assembly:
         return seqs, so, grp
 
 
-def _fasta_and_r2i(names_src, name_start, name_len, mem_off, cons_src, cons_sel, cons_start, cons_len, cons_rc,
-                   counter0: int = 0):
+def _fasta_and_r2i(name_src, name_sel, name_start, name_len, mem_off, cons_src, cons_sel, cons_start, cons_len,
+                   cons_rc, counter0: int = 0):
     """Isoform_Consensi.fasta and reads2isoforms.txt bytes for isoforms in output order
-    (defineIsoforms.py:155-166): '>Isoform{k}_{n}\n{consensus}\n' and '{name}\tIsoform{k}_{n}\n'."""
+    (defineIsoforms.py:155-166): '>Isoform{k}_{n}\n{consensus}\n' and '{name}\tIsoform{k}_{n}\n'.
+    Consensi and names are byte segments of several sources (locus texts, POA outputs), gathered once."""
     n_iso = len(mem_off) - 1
     n_mem = np.diff(mem_off)
     labels = [f"Isoform{counter0 + i + 1}_{int(n_mem[i])}" for i in range(n_iso)]
@@ -169,7 +177,7 @@ def _fasta_and_r2i(names_src, name_start, name_len, mem_off, cons_src, cons_sel,
     ss = nl_pos + 1 + hs
     # FASTA: [header (aux)] [consensus (its source)] ["\n" (aux)] per isoform; sources: 0 aux, 1.. cons
     srcs = [aux] + list(cons_src)
-    sel = np.empty(3 * n_iso, dtype=np.int8)
+    sel = np.empty(3 * n_iso, dtype=np.int16)
     st = np.empty(3 * n_iso, dtype=np.int64)
     ln = np.empty(3 * n_iso, dtype=np.int64)
     rc = np.zeros(3 * n_iso, dtype=np.int8)
@@ -177,15 +185,15 @@ def _fasta_and_r2i(names_src, name_start, name_len, mem_off, cons_src, cons_sel,
     sel[1::3], st[1::3], ln[1::3], rc[1::3] = 1 + np.asarray(cons_sel), cons_start, cons_len, cons_rc
     sel[2::3], st[2::3], ln[2::3] = 0, nl_pos, 1
     fasta, _ = _lib.pack_segments(srcs, st, ln, sel=sel, rc=rc)
-    # reads2isoforms: [name (names_src)] [suffix (aux)] per member
+    # reads2isoforms: [name (its source)] [suffix (aux)] per member
     m = int(mem_off[-1])
     iso_of_mem = np.repeat(np.arange(n_iso), n_mem)
-    sel = np.empty(2 * m, dtype=np.int8)
+    sel = np.empty(2 * m, dtype=np.int16)
     st = np.empty(2 * m, dtype=np.int64)
     ln = np.empty(2 * m, dtype=np.int64)
-    sel[0::2], st[0::2], ln[0::2] = 1, name_start, name_len
+    sel[0::2], st[0::2], ln[0::2] = 1 + np.asarray(name_sel), name_start, name_len
     sel[1::2], st[1::2], ln[1::2] = 0, ss[iso_of_mem], sl[iso_of_mem]
-    r2i, _ = _lib.pack_segments([aux, names_src], st, ln, sel=sel)
+    r2i, _ = _lib.pack_segments([aux] + list(name_src), st, ln, sel=sel)
     return fasta, r2i
 
 
@@ -254,9 +262,11 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         mine = [i for i in range(len(roots)) if owner[i] == rank]
     my_roots = [roots[i] for i in mine]
     chroms = [r.split("~")[0] for r in my_roots]
-    ann = [gtf.locus_bounds(left, right, r.split("~")[0], int(r.split("~")[1]), int(r.split("~")[2]))
-           for r in my_roots]
+    bidx = gtf.BoundsIndex(left, right)
+    ann = ([bidx.bounds(r.split("~")[0], int(r.split("~")[1]), int(r.split("~")[2])) for r in my_roots]
+           if bidx else None)
     t1 = time.perf_counter()
+    timeline = [("ingest", 0.0, t1 - t0)]
     # Chunked pipeline: clustering of chunk k+1 (host C++ threads, GIL released) overlaps orientation +
     # POA of chunk k on the GPU.  Chunks are contiguous runs of sorted roots.  The POA kernel is
     # persistent (one grid, LPT over the launch's groups), so every launch ends in a tail that only its
@@ -288,7 +298,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         # clustering (host C++ threads, GIL released), then the orientation input: the subsampled reads
         tc = time.perf_counter()
         r = (cluster_fn or cluster.cluster_loci)(
-            [os.path.join(out_tmp, x + ".psl") for x in my_roots[lo:hi]], chroms[lo:hi], ann=ann[lo:hi],
+            [os.path.join(out_tmp, x + ".psl") for x in my_roots[lo:hi]], chroms[lo:hi], ann=ann[lo:hi] if ann else None,
             device=device, cutoff=cutoff, splice_site_width=splice_site_width,
             minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
             downstream_buffer=downstream_buffer, junctions=junctions, seed=seed, threads=cl_threads)
@@ -313,14 +323,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
              "t_ingest": t1 - t0, "t_cluster": 0.0, "t_pack": 0.0, "t_orient": 0.0, "t_assemble": 0.0,
              "t_poa": 0.0, "chunks": len(spans), "poa_launches": poa_launches}
     payloads = []
-    timeline = []
     stats["timeline"] = timeline
-
-    def compact_close(pl, res):
-        # copy this chunk's results out of its locus text, then free the text
-        out = _compact(pl)
-        res.close()
-        return out
 
     def assemble(res, hits, n_hits):
         ta = time.perf_counter()
@@ -350,7 +353,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
 
     n_poa = int(os.environ.get("MANDO_POA_STREAMS", "2")) if len(spans) > 1 else 1
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
-            ThreadPoolExecutor(max_workers=n_poa) as gpu_poa, ThreadPoolExecutor(max_workers=1) as post:
+            ThreadPoolExecutor(max_workers=n_poa) as gpu_poa:
         cl = [ex.submit(run_cluster, lo, hi) for lo, hi in spans]
         poa_futs = []
         for k, (lo, hi) in enumerate(spans):
@@ -367,19 +370,18 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             add("t_orient", te - tg)
             asm_fut = host.submit(assemble, res, hits, n_hits)
             poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
-        pending = []
+        results = []
         for f in poa_futs:
             pl, res = f.result()
-            if len(spans) > 1:
-                pending.append(post.submit(compact_close, pl, res))
-            else:
-                pl["_res"] = res
-                payloads.append(pl)
-        payloads += [f.result() for f in pending]
+            results.append(res)
+            payloads.append(pl)
+    tm = time.perf_counter()
     payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
     if world > 1:
         payload = _gather(payload, comm)
+    timeline.append(("merge", tm - t0, time.perf_counter() - t0))
     if rank == 0:
+        tw = time.perf_counter()
         order = np.argsort(payload["iso_root"], kind="stable")   # sorted roots x IsoDict order
         mo = payload["mem_off"]
         cnt = np.diff(mo)[order]
@@ -388,18 +390,19 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         # member rows in output order: for each isoform in `order`, mo[i] .. mo[i+1]-1
         midx = (np.repeat(mo[:-1][order] - new_off[:-1], cnt) + np.arange(int(new_off[-1]))
                 if len(order) else np.zeros(0, np.int64))
-        fasta, r2i = _fasta_and_r2i(payload["names"], payload["n_start"][midx], payload["n_len"][midx], new_off,
-                                    payload["cons"], payload["c_sel"][order], payload["c_start"][order],
-                                    payload["c_len"][order], payload["c_rc"][order])
+        fasta, r2i = _fasta_and_r2i(payload["name_src"], payload["n_sel"][midx], payload["n_start"][midx],
+                                    payload["n_len"][midx], new_off, payload["cons_src"], payload["c_sel"][order],
+                                    payload["c_start"][order], payload["c_len"][order], payload["c_rc"][order])
         with open(out_path + "/Isoform_Consensi.fasta", "wb") as fh:
             fh.write(memoryview(np.ascontiguousarray(fasta)))
         with open(out_path + "/reads2isoforms.txt", "wb") as fh:
             fh.write(memoryview(np.ascontiguousarray(r2i)))
         stats["written_isoforms"] = int(len(order))
+        timeline.append(("write", tw - t0, time.perf_counter() - t0))
     stats["t_total"] = time.perf_counter() - t0
-    for pl in payloads:
-        if "_res" in pl:
-            pl["_res"].close()
+    # the chunks' text buffers go back to the pinned pool off the caller's path
+    del payload, payloads
+    threading.Thread(target=lambda rs: [r.close() for r in rs], args=(results,), daemon=True).start()
     if verbose and rank == 0:
         print("\t" + " ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in stats.items()
                                if not isinstance(v, list)))
@@ -434,29 +437,26 @@ def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, run_po
         stats["poa_reads"] += int(p_grp[-1])
         stats["t_poa"] += t4 - t3
     ri = np.asarray(root_idx, dtype=np.int64)
+    n_mem = int(res.mem_off[-1])
     return dict(iso_root=ri[res.iso_locus] if n_iso else np.zeros(0, np.int64),
-                cons=[res.text, cons], c_sel=c_sel, c_start=c_start, c_len=c_len, c_rc=c_rc,
-                names=res.text, n_start=res.name_off[res.mem], n_len=res.name_len[res.mem].astype(np.int64),
-                mem_off=res.mem_off)
+                cons_src=[res.text, cons], c_sel=c_sel.astype(np.int16), c_start=c_start, c_len=c_len, c_rc=c_rc,
+                name_src=[res.text], n_sel=np.zeros(n_mem, np.int16), n_start=res.name_off[res.mem],
+                n_len=res.name_len[res.mem].astype(np.int64), mem_off=res.mem_off)
 
 
 def _compact(payload: dict) -> dict:
-    """Copy the referenced bytes out of the (large) locus text, so a rank ships only its results."""
-    cons_text = payload["cons"][0]
-    tsel = payload["c_sel"] == 0
-    ct, co = _lib.pack_segments([cons_text], payload["c_start"][tsel], payload["c_len"][tsel],
-                                rc=payload["c_rc"][tsel])
-    c_start = payload["c_start"].copy()
-    c_rc = payload["c_rc"].copy()
-    c_start[tsel] = co[:-1]
-    c_rc[tsel] = 0
-    names, noff = _lib.pack_segments([payload["names"]], payload["n_start"], payload["n_len"])
-    return dict(iso_root=payload["iso_root"], cons=[ct, payload["cons"][1]], c_sel=payload["c_sel"], c_start=c_start,
-                c_len=payload["c_len"], c_rc=c_rc, names=names, n_start=noff[:-1], n_len=payload["n_len"],
-                mem_off=payload["mem_off"])
+    """One consensus buffer and one name buffer (the referenced bytes gathered out of every source), so a
+    rank ships only its results."""
+    ct, co = _lib.pack_segments(payload["cons_src"], payload["c_start"], payload["c_len"], sel=payload["c_sel"],
+                                rc=payload["c_rc"])
+    names, noff = _lib.pack_segments(payload["name_src"], payload["n_start"], payload["n_len"], sel=payload["n_sel"])
+    n_iso, n_mem = len(payload["c_len"]), len(payload["n_len"])
+    return dict(iso_root=payload["iso_root"], cons_src=[ct], c_sel=np.zeros(n_iso, np.int16), c_start=co[:-1],
+                c_len=payload["c_len"], c_rc=np.zeros(n_iso, np.int8), name_src=[names],
+                n_sel=np.zeros(n_mem, np.int16), n_start=noff[:-1], n_len=payload["n_len"], mem_off=payload["mem_off"])
 
 
-_FIELDS = ("iso_root", "c_sel", "c_start", "c_len", "c_rc", "n_start", "n_len", "mem_off")
+_FIELDS = ("iso_root", "c_start", "c_len", "n_start", "n_len", "mem_off")
 
 
 def _gather(payload: dict, comm) -> dict:
@@ -464,7 +464,7 @@ def _gather(payload: dict, comm) -> dict:
     xGMI between GPUs, the rendezvous sockets on CPU).  Each rank ships its isoforms' root indices,
     consensus bytes and member names; only rank 0 unpacks them for the writer."""
     p = _compact(payload)
-    arrays = [np.ascontiguousarray(p[f]) for f in _FIELDS] + [p["cons"][0], p["cons"][1], p["names"]]
+    arrays = [np.ascontiguousarray(p[f]) for f in _FIELDS] + [p["cons_src"][0], p["name_src"][0]]
     hdr = np.array([a.nbytes for a in arrays] + [a.dtype.num for a in arrays], dtype=np.int64)
     blob = np.concatenate([hdr.view(np.uint8)] + [a.view(np.uint8).ravel() for a in arrays])
     allb, counts = comm.allgather_bytes(blob)
@@ -483,40 +483,38 @@ def _gather(payload: dict, comm) -> dict:
         for sz, kd in zip(sizes, kinds):
             arrs.append(raw[pos:pos + sz].view(_dtype_of(int(kd))))
             pos += int(sz)
-        parts.append(arrs)
-    return _merge([dict(zip(_FIELDS, arrs[:len(_FIELDS)]), cons=[arrs[len(_FIELDS)], arrs[len(_FIELDS) + 1]],
-                        names=arrs[len(_FIELDS) + 2]) for arrs in parts])
+        d = dict(zip(_FIELDS, arrs[:len(_FIELDS)]))
+        n_iso, n_mem = len(d["c_len"]), len(d["n_len"])
+        d.update(cons_src=[arrs[len(_FIELDS)]], c_sel=np.zeros(n_iso, np.int16), c_rc=np.zeros(n_iso, np.int8),
+                 name_src=[arrs[len(_FIELDS) + 1]], n_sel=np.zeros(n_mem, np.int16))
+        parts.append(d)
+    return _merge(parts)
 
 
 def _merge(payloads: list) -> dict:
-    """Concatenate compacted payloads, rebasing offsets into the concatenated byte buffers."""
-    out = {f: [] for f in _FIELDS}
-    cons_t, cons_p, names = [], [], []
-    bt = bp = bn = bm = 0
+    """Concatenate payloads: index arrays appended, byte sources listed (selectors rebased), offsets of
+    members rebased; no bytes are copied."""
+    if len(payloads) == 1:
+        return payloads[0]
+    out = {f: [] for f in ("iso_root", "c_sel", "c_start", "c_len", "c_rc", "n_sel", "n_start", "n_len", "mem_off")}
+    cons_src, name_src = [], []
+    bm = 0
     for d in payloads:
-        ct, cp = d["cons"]
-        nm = d["names"]
-        cs = d["c_start"].copy()
-        cs[d["c_sel"] == 0] += bt
-        cs[d["c_sel"] == 1] += bp
         out["iso_root"].append(d["iso_root"])
-        out["c_sel"].append(d["c_sel"])
-        out["c_start"].append(cs)
+        out["c_sel"].append(d["c_sel"].astype(np.int16) + len(cons_src))
+        out["c_start"].append(d["c_start"])
         out["c_len"].append(d["c_len"])
         out["c_rc"].append(d["c_rc"])
-        out["n_start"].append(d["n_start"] + bn)
+        out["n_sel"].append(d["n_sel"].astype(np.int16) + len(name_src))
+        out["n_start"].append(d["n_start"])
         out["n_len"].append(d["n_len"])
         out["mem_off"].append(d["mem_off"][1:] + bm if len(out["mem_off"]) else d["mem_off"] + bm)
         bm += int(d["mem_off"][-1])
-        bt += ct.size
-        bp += cp.size
-        bn += nm.size
-        cons_t.append(ct)
-        cons_p.append(cp)
-        names.append(nm)
+        cons_src += list(d["cons_src"])
+        name_src += list(d["name_src"])
     merged = {f: np.concatenate(v) for f, v in out.items()}
-    merged["cons"] = [np.concatenate(cons_t), np.concatenate(cons_p)]
-    merged["names"] = np.concatenate(names)
+    merged["cons_src"] = cons_src
+    merged["name_src"] = name_src
     return merged
 
 

@@ -62,6 +62,32 @@ def locus_bounds(left: dict, right: dict, chrom: str, start: int, end: int) -> l
             [p for p in rb["5"] if start < p < end], [p for p in rb["3"] if start < p < end]]
 
 
+class BoundsIndex:
+    """locus_bounds for many loci: each chromosome's four position lists sorted once, every locus a
+    pair of binary searches (the lists' order does not matter downstream: make_genome_bins sorts them,
+    SDC:396-399).  Equal to [sorted(x) for x in locus_bounds(...)]."""
+
+    def __init__(self, left: dict, right: dict):
+        import numpy as np
+
+        self.np = np
+        self.idx = {}
+        for chrom in set(left) | set(right):
+            lb = left.get(chrom, {"5": [], "3": []})
+            rb = right.get(chrom, {"5": [], "3": []})
+            self.idx[chrom] = [np.sort(np.asarray(x, dtype=np.int64)) for x in (lb["5"], lb["3"], rb["5"], rb["3"])]
+
+    def __bool__(self):
+        return bool(self.idx)
+
+    def bounds(self, chrom: str, start: int, end: int):
+        np = self.np
+        lists = self.idx.get(chrom)
+        if lists is None:
+            return [np.zeros(0, np.int64)] * 4
+        return [a[np.searchsorted(a, start, "right"):np.searchsorted(a, end, "left")] for a in lists]
+
+
 def write_polya_bed(path: str, poly: list, white_list_polyA: list[str]) -> None:
     """polyAWhiteList.bed exactly as defineIsoforms.main writes it (:111-120)."""
     with open(path, "w") as out:

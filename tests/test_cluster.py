@@ -202,3 +202,18 @@ def test_sharded_two_ranks_host_comm(dataset, tmp_path):
     sha = lambda f: hashlib.sha256(open(os.path.join(d, f), "rb").read()).hexdigest()
     assert sha("Isoform_Consensi.fasta") == exp["isoform_consensi_sha256"]
     assert sha("reads2isoforms.txt") == exp["reads2isoforms_sha256"]
+
+
+def test_bounds_index_equals_locus_bounds(dataset):
+    """gtf.BoundsIndex (sorted lists + binary search) == the per-locus scan of the reference's bounds
+    (defineIsoforms.py:140-150), up to list order, which make_genome_bins sorts away."""
+    d, roots, info = dataset
+    _, lb, rb, _ = gtf.parse_genome(info["gtf"], P["white_list_polyA"].split(","))
+    bi = gtf.BoundsIndex(lb, rb)
+    assert bi
+    for r in roots + ["chrNone~1~100"]:
+        c, a, b = r.split("~")
+        want = gtf.locus_bounds(lb, rb, c, int(a), int(b))
+        got = bi.bounds(c, int(a), int(b))
+        assert [sorted(x) for x in want] == [x.tolist() for x in got]
+    assert not gtf.BoundsIndex({}, {})
