@@ -163,3 +163,20 @@ def test_edge_cases(tmp_path):
         chroms.append(first[13] if len(first) > 13 else "chrA")
     _compare(paths, chroms, seed=2)
     _compare(paths + ["/nonexistent/x.psl"], chroms + ["chrA"], seed=2)
+
+
+def test_repeated_calls_reuse_buffers(tmp_path):
+    """Back-to-back calls reuse the host and device text buffers and the per-context scratch; every call
+    must equal the restatement (a refilled, recycled buffer once handed the kernels stale bytes)."""
+    spec = dict(GOLD["datasets"]["sirv_like"]["synth"])
+    n = spec.pop("n_loci")
+    d = str(tmp_path)
+    synth.write_loci(os.path.join(d, "tmp_SS"), n, threads=8, **spec)
+    _, paths, chroms, _ = _inputs(d)
+    want = ocl.cluster_loci(paths, chroms, threads=8)
+    ref = (want.locus_status.tolist(), want.mem.tolist(), want.sub.tolist())
+    want.close()
+    for _ in range(6):
+        got = cluster.cluster_loci(paths, chroms, threads=8)
+        assert (got.locus_status.tolist(), got.mem.tolist(), got.sub.tolist()) == ref
+        got.close()
