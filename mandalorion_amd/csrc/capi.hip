@@ -141,11 +141,12 @@ struct mando_ctx {
     DevBuf s_items, s_item_of, s_n, s_t, s_q, s_scratch, s_redo, gorder2;  // -S partition
     DevBuf g_off, g_len, g_rc, g_dst;                                      // segment gather
     DevBuf cons_txt;                                                       // decoded consensi
+    DevBuf o_scratch;                                                      // long-read orientation slabs
     ~mando_ctx() {
         for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
                           &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx, &s_items,
                           &s_item_of, &s_n, &s_t, &s_q, &s_scratch, &s_redo, &gorder2, &g_off, &g_len, &g_rc,
-                          &g_dst, &cons_txt})
+                          &g_dst, &cons_txt, &o_scratch})
             b->release();
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -825,6 +826,7 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
     a.counter = ctx->counter.as<int32_t>();
     a.gidx = nullptr;
     a.cap = cap;
+    a.gscratch = nullptr;
     std::vector<int32_t> st((size_t)n_groups);
     std::vector<int32_t> redo;
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
@@ -849,15 +851,29 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
                 if (st[(size_t)g] != 0) redo.push_back((int32_t)g);
         }
         if (redo.empty()) break;
-        if (a.cap >= mando::kOrientCap)
+        if (a.cap >= mando::kOrientCapMax)
             return fail(MANDO_E_UNSUPPORTED, "orientation: group " + std::to_string(redo[0]) + " has a read with more than " +
-                                                 std::to_string(mando::kOrientCap) + " minimizers or anchors");
-        // overflowed groups again, at the next capacity (their outputs are rewritten in full)
+                                                 std::to_string(mando::kOrientCapMax) + " minimizers or anchors");
+        // overflowed groups again, at the next capacity (their outputs are rewritten in full); past the
+        // LDS capacity the arrays move to per-wave HBM slabs, sized for the longest read of those groups
         if ((rc = ctx->o_gidx.ensure(sizeof(int32_t) * redo.size())) != MANDO_OK) return rc;
         HIP_TRY(hipMemcpyAsync(ctx->o_gidx.p, redo.data(), sizeof(int32_t) * redo.size(), hipMemcpyHostToDevice,
                                ctx->stream));
         a.gidx = ctx->o_gidx.as<int32_t>();
-        a.cap = std::min(mando::kOrientCap, a.cap * 2);
+        if (a.cap < mando::kOrientCap) {
+            a.cap *= 2;
+        } else {
+            int64_t ml = 0;
+            for (int32_t g : redo)
+                for (int64_t r = grp_off[g]; r < grp_off[g + 1]; ++r) ml = std::max<int64_t>(ml, seq_off[r + 1] - seq_off[r]);
+            int cap2 = a.cap * 2;
+            while (cap2 < mando::kOrientCapMax && ml * 26 / 110 > cap2) cap2 *= 2;
+            a.cap = cap2;
+            const int64_t slots = std::min<int64_t>((int64_t)redo.size(), (int64_t)ctx->n_cu * mando::orient_blocks_per_cu(a.cap));
+            if ((rc = ctx->o_scratch.ensure((size_t)slots * (size_t)(3 * (int64_t)a.cap + a.cap / 64) * 8)) != MANDO_OK)
+                return rc;
+            a.gscratch = ctx->o_scratch.as<uint64_t>();
+        }
     }
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->timed = true;

@@ -5,7 +5,8 @@
 
 namespace mando {
 
-constexpr int kOrientCap = 2048;  // largest per-read capacity (minimizers / anchors held in LDS)
+constexpr int kOrientCap = 2048;     // largest per-read capacity held in LDS
+constexpr int kOrientCapMax = 1 << 22;  // HBM-slab variant beyond it (a read of ~40 Mb)
 
 struct OrientArgs {
     const uint8_t *seq;       // ASCII reads
@@ -18,7 +19,8 @@ struct OrientArgs {
     int32_t *status;          // per group: 0 ok, -1 over this launch's cap
     int32_t *counter;         // work-queue head (zeroed before launch)
     const int32_t *gidx;      // optional: the group indices to process (a re-run of overflowed groups)
-    int32_t cap;              // per-read capacity of this launch (power of two, <= kOrientCap)
+    int32_t cap;              // per-read capacity of this launch (power of two; > kOrientCap: HBM slabs)
+    uint64_t *gscratch;       // HBM slabs, (3 * cap + cap / 64) words per launched block (cap > kOrientCap)
 };
 
 size_t orient_dyn_bytes(int cap);

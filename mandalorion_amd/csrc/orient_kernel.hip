@@ -9,9 +9,10 @@
 // the known differences from minimap2; parity with mappy itself is unpinned).
 //
 // Layout: one 64-lane wave per isoform group (persistent over groups); everything stays in LDS.
-// The three per-read arrays hold `cap` entries (a power of two chosen per launch from the batch's
-// longest read, 1024 for R2C2-length reads: 24 KB, so 5 waves fit per CU; groups that overflow are
-// re-run by the host at the next capacity):
+// The three per-read arrays hold `cap` entries (a power of two chosen per launch, 1024 for R2C2-length
+// reads: 24 KB, so 5 waves fit per CU; groups that overflow are re-run by the host at the next
+// capacity).  Beyond kOrientCap (2048, ~10 kb reads) the same code runs with the arrays in a per-wave
+// HBM slab (orient_kernel<true>), so long reads are oriented instead of refused:
 //   refk  sorted reference minimizer keys  (h << 33 | pos << 1 | strand)          8 B x cap
 //   qm    query minimizer keys, then reused as f[] / p[] of the chaining DP       8 B x cap
 //   an    anchor keys (rev << 62 | x << 31 | y), bitonic-sorted in LDS              8 B x cap
@@ -42,6 +43,7 @@ static_assert(NPK * 16 >= TB + 16 && (NPK * 16) % 64 == 0, "tile staging size");
 // fixed-size part (static LDS); the cap-sized arrays live in dynamic LDS (see OrientDyn)
 struct OrientLds {
     int cap;
+    uint64_t *gdyn;  // the cap-sized arrays in HBM (the long-read variant), else null
     uint32_t pk[NPK];           // staged 2-bit codes
     uint64_t nm[NNM];           // staged non-ACGT mask
     uint64_t hb[TILE + 2 * W];  // (hash << 1 | z) of the tile's k-mers, INF when invalid
@@ -51,13 +53,30 @@ struct OrientLds {
 };
 extern __shared__ __attribute__((aligned(16))) uint64_t g_orient_dyn[];  // 3 * cap + cap / 64 words
 // views into the dynamic buffer (LDS address space kept: the base is the LDS symbol itself)
+// G: the arrays live in a per-wave HBM slab (reads beyond the LDS capacity) instead of dynamic LDS
 __device__ __forceinline__ int o_cap(const OrientLds &sh) { return __builtin_amdgcn_readfirstlane(sh.cap); }
-__device__ __forceinline__ uint64_t *o_refk(const OrientLds &) { return g_orient_dyn; }
-__device__ __forceinline__ uint64_t *o_qm(const OrientLds &sh) { return g_orient_dyn + o_cap(sh); }
-__device__ __forceinline__ uint64_t *o_an(const OrientLds &sh) { return g_orient_dyn + 2 * o_cap(sh); }
-__device__ __forceinline__ uint64_t *o_used(const OrientLds &sh) { return g_orient_dyn + 3 * o_cap(sh); }
-__device__ __forceinline__ int32_t *o_f(const OrientLds &sh) { return reinterpret_cast<int32_t *>(o_qm(sh)); }
-__device__ __forceinline__ int32_t *o_p(const OrientLds &sh) { return reinterpret_cast<int32_t *>(o_qm(sh)) + o_cap(sh); }
+template <bool G>
+__device__ __forceinline__ uint64_t *o_base(const OrientLds &sh) {
+    if constexpr (G) {
+        return sh.gdyn;
+    } else {
+        return g_orient_dyn;
+    }
+}
+template <bool G>
+__device__ __forceinline__ uint64_t *o_refk(const OrientLds &sh) { return o_base<G>(sh); }
+template <bool G>
+__device__ __forceinline__ uint64_t *o_qm(const OrientLds &sh) { return o_base<G>(sh) + o_cap(sh); }
+template <bool G>
+__device__ __forceinline__ uint64_t *o_an(const OrientLds &sh) { return o_base<G>(sh) + 2 * o_cap(sh); }
+template <bool G>
+__device__ __forceinline__ uint64_t *o_used(const OrientLds &sh) { return o_base<G>(sh) + 3 * o_cap(sh); }
+template <bool G>
+__device__ __forceinline__ int32_t *o_f(const OrientLds &sh) { return reinterpret_cast<int32_t *>(o_qm<G>(sh)); }
+template <bool G>
+__device__ __forceinline__ int32_t *o_p(const OrientLds &sh) {
+    return reinterpret_cast<int32_t *>(o_qm<G>(sh)) + o_cap(sh);
+}
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 __device__ __forceinline__ void wsync() { __syncthreads(); }
@@ -303,9 +322,10 @@ __device__ __forceinline__ int lower_bound_h(const uint64_t *a, int n, uint64_t 
 __device__ __forceinline__ int ilog2_u32(uint32_t v) { return 31 - __clz((int)v); }
 
 // one query read; returns 0 or -1 (over CAP)
+template <bool G>
 __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t qlen, int8_t *hits, int max_hits,
                            int32_t *n_hits, int lane) {
-    const int nq = minimizers(sh, q, qlen, o_qm(sh), lane);
+    const int nq = minimizers(sh, q, qlen, o_qm<G>(sh), lane);
     if (nq < 0) return -1;
     // anchors: count per query minimizer, exclusive scan, scatter
     int na = 0;
@@ -314,10 +334,10 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         int lo = 0, cnt = 0;
         uint64_t key = 0;
         if (i < nq) {
-            key = o_qm(sh)[i];
+            key = o_qm<G>(sh)[i];
             const uint64_t h = key >> 33;
-            lo = lower_bound_h(o_refk(sh), nref, h);
-            while (lo + cnt < nref && (o_refk(sh)[lo + cnt] >> 33) == h && cnt <= MAX_OCC) ++cnt;
+            lo = lower_bound_h(o_refk<G>(sh), nref, h);
+            while (lo + cnt < nref && (o_refk<G>(sh)[lo + cnt] >> 33) == h && cnt <= MAX_OCC) ++cnt;
             if (cnt > MAX_OCC) cnt = 0;
         }
         int incl = cnt;
@@ -331,24 +351,24 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         const int64_t qpos = (int64_t)((key >> 1) & 0xffffffffull);
         const int qz = (int)(key & 1);
         for (int t = 0; t < cnt; ++t) {
-            const uint64_t r = o_refk(sh)[lo + t];
+            const uint64_t r = o_refk<G>(sh)[lo + t];
             const int64_t rpos = (int64_t)((r >> 1) & 0xffffffffull);
             const int rev = qz ^ (int)(r & 1);
             const int64_t y = rev ? qlen - 1 - (qpos - K + 1) : qpos;
-            o_an(sh)[base + t] = ((uint64_t)rev << 62) | ((uint64_t)rpos << 31) | (uint64_t)y;
+            o_an<G>(sh)[base + t] = ((uint64_t)rev << 62) | ((uint64_t)rpos << 31) | (uint64_t)y;
         }
         na += tot;
     }
     wsync();
-    bitonic_sort(o_an(sh), na, lane);
+    bitonic_sort(o_an<G>(sh), na, lane);
     // chaining DP: lane l looks at predecessor j = i - 64 + l.  The 64-anchor look-back window (x, y,
     // strand, f) lives in registers and slides one lane per anchor (DPP wave_shl); the best
     // predecessor is one DPP max-reduction.  Only lane 0 stores f / p (for the chain walk below).
     int wx = 0, wy = 0, wr = -1, wf = 0;  // wr = -1: empty slot (j < 0)
-    uint64_t an_next = na > 0 ? o_an(sh)[0] : 0;  // one anchor ahead: the LDS read leaves the DP chain
+    uint64_t an_next = na > 0 ? o_an<G>(sh)[0] : 0;  // one anchor ahead: the LDS read leaves the DP chain
     for (int i = 0; i < na; ++i) {
         const uint64_t ai = an_next;
-        if (i + 1 < na) an_next = o_an(sh)[i + 1];
+        if (i + 1 < na) an_next = o_an<G>(sh)[i + 1];
         const int ri = (int)(ai >> 62);
         const int xi = (int)((ai >> 31) & 0x7fffffff), yi = (int)(ai & 0x7fffffff);
         const int dr = xi - wx, dq = yi - wy;
@@ -365,8 +385,8 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         const bool take = best != 0 && cand > K;
         const int fi = take ? cand : K;
         if (lane == 0) {
-            o_f(sh)[i] = fi;
-            o_p(sh)[i] = take ? i - 64 + (best & 63) : -1;
+            o_f<G>(sh)[i] = fi;
+            o_p<G>(sh)[i] = take ? i - 64 + (best & 63) : -1;
         }
         wx = wave_shl1(wx, xi);
         wy = wave_shl1(wy, yi);
@@ -375,15 +395,15 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
     }
     wsync();
     // greedy chain extraction: highest f first (ties: lowest index), walk back to a used anchor
-    for (int t = lane; t < o_cap(sh) / 64; t += 64) o_used(sh)[t] = 0;
+    for (int t = lane; t < o_cap(sh) / 64; t += 64) o_used<G>(sh)[t] = 0;
     wsync();
     int nch = 0;
     for (;;) {
         uint64_t bk = 0;  // (f + 2^20) << 32 | (2^31 - 1 - i): max picks highest f, then lowest i
         for (int c0 = 0; c0 < na; c0 += 64) {
             const int i = c0 + lane;
-            if (i < na && !((o_used(sh)[i >> 6] >> (i & 63)) & 1)) {
-                const uint64_t k = ((uint64_t)(uint32_t)(o_f(sh)[i] + (1 << 20)) << 32) | (uint64_t)(0x7fffffff - i);
+            if (i < na && !((o_used<G>(sh)[i >> 6] >> (i & 63)) & 1)) {
+                const uint64_t k = ((uint64_t)(uint32_t)(o_f<G>(sh)[i] + (1 << 20)) << 32) | (uint64_t)(0x7fffffff - i);
                 bk = k > bk ? k : bk;
             }
         }
@@ -394,21 +414,21 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         if (fbest < MIN_SCORE) break;
         if (lane == 0) {
             int k = bi, first = bi, cnt = 0;
-            while (k >= 0 && !((o_used(sh)[k >> 6] >> (k & 63)) & 1)) {
-                o_used(sh)[k >> 6] |= 1ull << (k & 63);
+            while (k >= 0 && !((o_used<G>(sh)[k >> 6] >> (k & 63)) & 1)) {
+                o_used<G>(sh)[k >> 6] |= 1ull << (k & 63);
                 ++cnt;
                 first = k;
-                k = o_p(sh)[k];
+                k = o_p<G>(sh)[k];
             }
-            const int score = fbest - (k >= 0 ? o_f(sh)[k] : 0);
+            const int score = fbest - (k >= 0 ? o_f<G>(sh)[k] : 0);
             int ok = 0;
             if (cnt >= MIN_CNT && score >= MIN_SCORE) {
                 if (nch >= MAXCH) {
                     ok = -1;
                 } else {
                     sh.ch_score[nch] = score;
-                    sh.ch_rev[nch] = (int)(o_an(sh)[bi] >> 62);
-                    const int ys = (int)(o_an(sh)[first] & 0x7fffffff) - K + 1, ye = (int)(o_an(sh)[bi] & 0x7fffffff) + 1;
+                    sh.ch_rev[nch] = (int)(o_an<G>(sh)[bi] >> 62);
+                    const int ys = (int)(o_an<G>(sh)[first] & 0x7fffffff) - K + 1, ye = (int)(o_an<G>(sh)[bi] & 0x7fffffff) + 1;
                     sh.ch_qs[nch] = sh.ch_rev[nch] ? (int)qlen - ye : ys;
                     sh.ch_qe[nch] = sh.ch_rev[nch] ? (int)qlen - ys : ye;
                     ok = 1;
@@ -461,10 +481,14 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
     return 0;
 }
 
+template <bool G>
 __global__ __launch_bounds__(64) void orient_kernel(OrientArgs a) {
     __shared__ OrientLds sh;
     const int lane = lane_id();
-    if (lane == 0) sh.cap = a.cap;
+    if (lane == 0) {
+        sh.cap = a.cap;
+        sh.gdyn = G ? a.gscratch + (int64_t)blockIdx.x * (3 * (int64_t)a.cap + a.cap / 64) : nullptr;
+    }
     wsync();
     for (;;) {
         int gi = 0;
@@ -475,14 +499,14 @@ __global__ __launch_bounds__(64) void orient_kernel(OrientArgs a) {
         const int64_t r0 = a.grp_off[g], r1 = a.grp_off[g + 1];
         int st = 0;
         if (r1 > r0) {
-            const int nref = minimizers(sh, a.seq + a.seq_off[r0], a.seq_off[r0 + 1] - a.seq_off[r0], o_refk(sh), lane);
+            const int nref = minimizers(sh, a.seq + a.seq_off[r0], a.seq_off[r0 + 1] - a.seq_off[r0], o_refk<G>(sh), lane);
             wsync();
             if (nref < 0) {
                 st = -1;
             } else {
-                bitonic_sort(o_refk(sh), nref, lane);
+                bitonic_sort(o_refk<G>(sh), nref, lane);
                 for (int64_t r = r0; r < r1; ++r) {
-                    const int rc = orient_read(sh, nref, a.seq + a.seq_off[r], a.seq_off[r + 1] - a.seq_off[r],
+                    const int rc = orient_read<G>(sh, nref, a.seq + a.seq_off[r], a.seq_off[r + 1] - a.seq_off[r],
                                                a.hits + r * a.max_hits, a.max_hits, a.n_hits + r, lane);
                     if (rc < 0) {
                         st = -1;
@@ -502,13 +526,22 @@ size_t orient_dyn_bytes(int cap) { return (size_t)(3 * cap + cap / 64) * sizeof(
 
 int orient_blocks_per_cu(int cap) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, orient_kernel, 64, orient_dyn_bytes(cap)) != hipSuccess || nb < 1)
+    if (cap > kOrientCap) {  // HBM variant: no dynamic LDS
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, orient_kernel<true>, 64, 0) != hipSuccess || nb < 1) nb = 1;
+        return nb;
+    }
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, orient_kernel<false>, 64, orient_dyn_bytes(cap)) != hipSuccess ||
+        nb < 1)
         nb = 1;
     return nb;
 }
 
 hipError_t launch_orient(const OrientArgs &a, int n_slots, hipStream_t stream) {
-    hipLaunchKernelGGL(orient_kernel, dim3(n_slots), dim3(64), orient_dyn_bytes(a.cap), stream, a);
+    if (a.cap > kOrientCap) {
+        hipLaunchKernelGGL(orient_kernel<true>, dim3(n_slots), dim3(64), 0, stream, a);
+    } else {
+        hipLaunchKernelGGL(orient_kernel<false>, dim3(n_slots), dim3(64), orient_dyn_bytes(a.cap), stream, a);
+    }
     return hipGetLastError();
 }
 

@@ -35,8 +35,7 @@
 #define E_NOMEM -3
 #define E_UNSUP -5
 
-enum { K = 15, W = 10, MAX_OCC = 10, MAX_GAP = 5000, BW = 500, LOOKBACK = 64, MIN_CNT = 3, MIN_SCORE = 40,
-       CAP = 2048 };
+enum { K = 15, W = 10, MAX_OCC = 10, MAX_GAP = 5000, BW = 500, LOOKBACK = 64, MIN_CNT = 3, MIN_SCORE = 40 };
 
 static inline int enc(uint8_t c) {
     switch (c) {
@@ -128,16 +127,18 @@ static int cmp_chain(const void *a, const void *b) {
 /* one query against the sorted reference keys; writes up to max_hits strands */
 static int orient_one(const uint64_t *ref, int64_t nref, const uint8_t *q, int64_t qlen, int8_t *hits,
                       int32_t max_hits, int32_t *n_hits) {
-    uint64_t *qm = (uint64_t *)malloc(sizeof(uint64_t) * CAP);
-    uint64_t *an = (uint64_t *)malloc(sizeof(uint64_t) * CAP);
-    int32_t *f = (int32_t *)malloc(sizeof(int32_t) * CAP);
-    int32_t *p = (int32_t *)malloc(sizeof(int32_t) * CAP);
-    uint8_t *used = (uint8_t *)malloc(CAP);
-    chain_t *ch = (chain_t *)malloc(sizeof(chain_t) * CAP);
+    /* no capacity limit (mappy has none): at most one minimizer per position, MAX_OCC anchors each */
+    const size_t qcap = (size_t)(qlen > 0 ? qlen : 1), acap = qcap * MAX_OCC + 1;
+    uint64_t *qm = (uint64_t *)malloc(sizeof(uint64_t) * qcap);
+    uint64_t *an = (uint64_t *)malloc(sizeof(uint64_t) * acap);
+    int32_t *f = (int32_t *)malloc(sizeof(int32_t) * acap);
+    int32_t *p = (int32_t *)malloc(sizeof(int32_t) * acap);
+    uint8_t *used = (uint8_t *)malloc(acap);
+    chain_t *ch = (chain_t *)malloc(sizeof(chain_t) * acap);
     int rc = OK_;
     *n_hits = 0;
     if (!qm || !an || !f || !p || !used || !ch) { rc = E_NOMEM; goto done; }
-    const int64_t nq = minimizers(q, qlen, qm, CAP);
+    const int64_t nq = minimizers(q, qlen, qm, (int64_t)qcap);
     if (nq == -1) { rc = E_NOMEM; goto done; }
     if (nq == -2) { rc = E_UNSUP; goto done; }
     int64_t na = 0;
@@ -158,7 +159,7 @@ static int orient_one(const uint64_t *ref, int64_t nref, const uint8_t *q, int64
             const int64_t rpos = (int64_t)((ref[t] >> 1) & 0xffffffffull);
             const int rev = qz ^ (int)(ref[t] & 1);
             const int64_t y = rev ? qlen - 1 - (qpos - K + 1) : qpos;
-            if (na >= CAP) { rc = E_UNSUP; goto done; }
+            if ((size_t)na >= acap) { rc = E_UNSUP; goto done; }
             an[na++] = ((uint64_t)rev << 62) | ((uint64_t)rpos << 31) | (uint64_t)y;
         }
     }
@@ -233,13 +234,16 @@ done:
 int orient_ref_batch(const uint8_t *seqs, const int64_t *seq_off, const int64_t *grp_off, int64_t n_groups,
                      int8_t *hit_strands, int32_t max_hits, int32_t *n_hits) {
     if (n_groups < 0 || max_hits < 1) return E_ARG;
-    uint64_t *ref = (uint64_t *)malloc(sizeof(uint64_t) * CAP);
-    if (!ref) return E_NOMEM;
     int rc = OK_;
+    uint64_t *ref = NULL;
     for (int64_t g = 0; g < n_groups && rc == OK_; ++g) {
         const int64_t r0 = grp_off[g], r1 = grp_off[g + 1];
         if (r1 <= r0) continue;
-        const int64_t nref = minimizers(seqs + seq_off[r0], seq_off[r0 + 1] - seq_off[r0], ref, CAP);
+        const int64_t L0 = seq_off[r0 + 1] - seq_off[r0];
+        free(ref);
+        ref = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(L0 > 0 ? L0 : 1));
+        if (!ref) return E_NOMEM;
+        const int64_t nref = minimizers(seqs + seq_off[r0], L0, ref, L0 > 0 ? L0 : 1);
         if (nref == -1) { rc = E_NOMEM; break; }
         if (nref == -2) { rc = E_UNSUP; break; }
         qsort(ref, (size_t)nref, sizeof(uint64_t), cmp_u64);

@@ -118,3 +118,19 @@ def test_orient_gpu_capacity_rerun(gpu_ctx):
     got = orient.orient_batch(groups)
     assert got == oref.orient_batch(groups)
     assert got[10][1] == [1] and got[10][2] == [-1]
+
+
+@pytest.mark.gpu
+def test_orient_gpu_reads_beyond_lds_capacity(gpu_ctx):
+    """Reads of 20-40 kb hold more minimizers than the LDS capacity (2048): those groups re-run with
+    the arrays in per-wave HBM slabs instead of being refused (mappy has no such limit).  Same hit
+    lists as the restatement, and the true strands; short groups in the same batch are unaffected."""
+    from mandalorion_amd import orient
+    from oracle import orient as oref
+
+    long_groups, long_truth = _groups(3, 41, lens=(20000, 40000), depth=(3, 5))
+    short_groups, short_truth = _groups(8, 42)
+    groups = short_groups[:4] + long_groups + short_groups[4:]
+    truth = short_truth[:4] + long_truth + short_truth[4:]
+    got = orient.orient_batch(groups)
+    assert got == oref.orient_batch(groups) == truth
