@@ -139,15 +139,27 @@ struct mando_ctx {
     DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
     DevBuf o_hits, o_strand, o_status;
     DevBuf s_items, s_item_of, s_n, s_t, s_q, s_scratch, s_redo, gorder2;  // -S partition
+    DevBuf gorder_w;                                                       // wide-launch groups
     DevBuf g_off, g_len, g_rc, g_dst;                                      // segment gather
     DevBuf cons_txt;                                                       // decoded consensi
     DevBuf o_scratch;                                                      // long-read orientation slabs
+    // extra POA lanes: a batch's launches of different kinds (narrow, wide, seeded) run side by side,
+    // each with its own stream and workspace
+    hipStream_t lane_stream[2] = {nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_lane[2] = {nullptr, nullptr};
+    DevBuf lane_ws[2], lane_counter[2], lane_prof[2];
     ~mando_ctx() {
         for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
                           &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx, &s_items,
                           &s_item_of, &s_n, &s_t, &s_q, &s_scratch, &s_redo, &gorder2, &g_off, &g_len, &g_rc,
-                          &g_dst, &cons_txt, &o_scratch})
+                          &g_dst, &cons_txt, &o_scratch, &lane_ws[0], &lane_ws[1], &lane_counter[0],
+                          &lane_counter[1], &lane_prof[0], &lane_prof[1], &gorder_w})
             b->release();
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        for (int k = 0; k < 2; ++k) {
+            if (ev_lane[k]) (void)hipEventDestroy(ev_lane[k]);
+            if (lane_stream[k]) (void)hipStreamDestroy(lane_stream[k]);
+        }
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (stream) (void)hipStreamDestroy(stream);
@@ -157,6 +169,9 @@ struct mando_ctx {
 namespace {
 
 constexpr int kMaxWavesPerCu = 16;  // upper bound on resident POA waves per CU
+// groups whose band 2w + 1 (at their longest read) is wider than this run in the wide-ring launch:
+// their rows mostly exceed one 128-column chunk (the band also drifts with the argmax)
+constexpr int64_t kWideBand = 112;
 #ifndef MANDO_WS_SHARE
 #define MANDO_WS_SHARE 0.8
 #endif
@@ -170,7 +185,7 @@ struct GroupStat {
 
 mando::PoaCaps plan_caps(const mando_poa_params &p, int64_t max_first, int64_t max_sum,
                          int64_t max_len, int64_t max_reads, int attempt) {
-    mando::PoaCaps c;
+    mando::PoaCaps c{};
     const double grow = (double)(1 << attempt);
     int64_t rest = std::max<int64_t>(0, max_sum - max_first);
     int64_t nc = max_first + 2 + (int64_t)(0.06 * grow * (double)rest) + 256;
@@ -207,7 +222,12 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
                  const int32_t *d_gorder, int64_t n_groups, uint8_t *d_cons,
                  const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
                  int32_t *d_status, int max_per_cu, const SeedPlan *sp = nullptr, bool ev_start = true,
-                 bool ev_end = true) {
+                 bool ev_end = true, int lane = 0) {
+    // lane k > 0: the context's extra stream and workspace k - 1 (launches of other kinds alongside)
+    hipStream_t stream = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
+    DevBuf &ws = lane ? ctx->lane_ws[lane - 1] : ctx->ws;
+    DevBuf &counter = lane ? ctx->lane_counter[lane - 1] : ctx->counter;
+    DevBuf &profb = lane ? ctx->lane_prof[lane - 1] : ctx->prof;
     mando::PoaKArgs a{};
     if (sp) {
         a.par_item = sp->par_item;
@@ -244,7 +264,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    const size_t budget = std::max<size_t>((size_t)1 << 30, (size_t)(kWsShare * (double)free_b) + ctx->ws.bytes);
+    const size_t budget = std::max<size_t>((size_t)1 << 30, (size_t)(kWsShare * (double)free_b) + ws.bytes);
     // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
@@ -255,34 +275,34 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         fprintf(stderr, "[mando prof] slot workspace %.1f MB, %lld slots (free %.1f GB, budget %.1f GB)\n",
                 a.slot_bytes / 1e6, (long long)slots, free_b / 1e9, budget / 1e9);
     if (slots < 1) slots = 1;
-    int rc = ctx->ws.ensure((size_t)(slots * a.slot_bytes));
+    int rc = ws.ensure((size_t)(slots * a.slot_bytes));
     while (rc == MANDO_E_NOMEM && slots > 1) {  // memory taken by others since hipMemGetInfo: fewer slots
         (void)hipGetLastError();                // clear the failed allocation's error state
         slots /= 2;
-        rc = ctx->ws.ensure((size_t)(slots * a.slot_bytes));
+        rc = ws.ensure((size_t)(slots * a.slot_bytes));
     }
     if (rc) return rc;
-    rc = ctx->counter.ensure(256);
+    rc = counter.ensure(256);
     if (rc) return rc;
-    a.ws = ctx->ws.as<char>();
-    a.counter = ctx->counter.as<int32_t>();
-    HIP_TRY(hipMemsetAsync(a.counter, 0, sizeof(int32_t), ctx->stream));
+    a.ws = ws.as<char>();
+    a.counter = counter.as<int32_t>();
+    HIP_TRY(hipMemsetAsync(a.counter, 0, sizeof(int32_t), stream));
     const char *pe = getenv("MANDO_PROF");
     const bool prof = pe && pe[0] == '1';
     if (prof) {
-        rc = ctx->prof.ensure((size_t)slots * mando::kProfPhases * 8);
+        rc = profb.ensure((size_t)slots * mando::kProfPhases * 8);
         if (rc) return rc;
-        HIP_TRY(hipMemsetAsync(ctx->prof.p, 0, (size_t)slots * mando::kProfPhases * 8, ctx->stream));
-        a.prof = ctx->prof.as<int64_t>();
+        HIP_TRY(hipMemsetAsync(profb.p, 0, (size_t)slots * mando::kProfPhases * 8, stream));
+        a.prof = profb.as<int64_t>();
     }
-    if (ev_start) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-    HIP_TRY(mando::launch_poa(a, (int)slots, ctx->stream));
-    if (ev_end) HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    if (ev_start) HIP_TRY(hipEventRecord(ctx->ev0, stream));
+    HIP_TRY(mando::launch_poa(a, (int)slots, stream));
+    if (ev_end) HIP_TRY(hipEventRecord(ctx->ev1, stream));
     ctx->timed = true;
     if (prof) {
         std::vector<int64_t> h((size_t)slots * mando::kProfPhases);
-        HIP_TRY(hipMemcpyAsync(h.data(), ctx->prof.p, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipMemcpyAsync(h.data(), profb.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
         double tot[mando::kProfPhases] = {0};
         for (int64_t s = 0; s < slots; ++s)
             for (int k = 0; k < mando::kProfPhases; ++k) tot[k] += (double)h[(size_t)(s * mando::kProfPhases + k)];
@@ -292,6 +312,8 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         fprintf(stderr, "[mando prof] slots=%lld reads=%.0f rows/read=%.0f | cycles per read: desc %.0f dp %.0f (%.1f/row) backtrack %.0f update %.0f | consensus/slot %.0f\n",
                 (long long)slots, reads, rows / reads, tot[0] / reads, tot[1] / reads, tot[1] / rows,
                 tot[2] / reads, tot[3] / reads, tot[4] / (double)slots);
+        fprintf(stderr, "[mando prof] total Gcycles: desc %.3f dp %.3f backtrack %.3f update %.3f consensus %.3f\n",
+                tot[0] * 1e-9, tot[1] * 1e-9, tot[2] * 1e-9, tot[3] * 1e-9, tot[4] * 1e-9);
         if (a.dbg & 16) {
             for (int64_t s = 0; s < slots; ++s) {
                 const int64_t *f = &h[(size_t)(s * mando::kProfPhases)];
@@ -513,6 +535,8 @@ int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const
     HIP_TRY(hipSetDevice(ctx->device));
     mando::PoaCaps caps = plan_caps(*params, max_read_len, max_group_bases, max_read_len,
                                     std::max<int64_t>(1, max_group_bases / std::max<int64_t>(1, max_read_len / 4)), 0);
+    const int64_t w = params->band_b + (int64_t)(params->band_f * (float)max_read_len);
+    caps.wide = 2 * w + 1 > kWideBand;
     ctx->last_launches = 1;
     return launch_batch(ctx, *params, caps, d_seqs, d_seq_off, d_grp_off, nullptr, n_groups,
                         d_cons, d_cons_off, d_cons_len, d_cells, d_status, kMaxWavesPerCu);
@@ -601,12 +625,33 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
     ctx->last_launches = 0;
     for (int attempt = 0; attempt < 4 && !todo.empty(); ++attempt) {
         // unseeded and seeded groups run as two launches of the two kernel instantiations
-        std::vector<int32_t> lists[2];
-        for (int32_t g : todo) lists[seeded_group(g) ? 1 : 0].push_back(g);
-        bool first = true;
-        for (int kind = 0; kind < 2; ++kind) {
+        // three kinds of launch: unseeded groups with bands of one chunk, unseeded groups whose band
+        // (2w + 1 at their longest read) exceeds one chunk (the wide-ring instantiation), -S groups
+        std::vector<int32_t> lists[3];
+        for (int32_t g : todo) {
+            const int64_t w = params->band_b + (int64_t)(params->band_f * (float)gs[(size_t)g].maxlen);
+            lists[seeded_group(g) ? 2 : (2 * w + 1 > kWideBand ? 1 : 0)].push_back(g);
+        }
+        // several kinds: each runs on its own lane (stream + workspace), concurrently, after everything
+        // staged so far on the first stream
+        int nk = 0;
+        for (int kind = 0; kind < 3; ++kind) nk += !lists[kind].empty();
+        if (nk > 1) {
+            if (!ctx->ev_fork) {
+                HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+                for (int k = 0; k < 2; ++k) {
+                    HIP_TRY(hipStreamCreateWithFlags(&ctx->lane_stream[k], hipStreamNonBlocking));
+                    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_lane[k], hipEventDisableTiming));
+                }
+            }
+            HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+            for (int k = 0; k < nk - 1; ++k) HIP_TRY(hipStreamWaitEvent(ctx->lane_stream[k], ctx->ev_fork, 0));
+        }
+        int lane = 0;
+        for (int kind = 0; kind < 3; ++kind) {
             const std::vector<int32_t> &L = lists[kind];
             if (L.empty()) continue;
+            hipStream_t lst = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
             int64_t mf = 0, ms = 0, ml = 0, mr = 0;
             for (int32_t g : L) {
                 mf = std::max(mf, gs[(size_t)g].first_len);
@@ -615,21 +660,27 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                 mr = std::max(mr, gs[(size_t)g].nreads);
             }
             mando::PoaCaps caps = plan_caps(*params, mf, ms, ml, mr, attempt);
-            caps.seeded = kind;
-            // the second launch may need a larger workspace: the first must be done with it
-            if (!first) HIP_TRY(hipStreamSynchronize(ctx->stream));
-            DevBuf &gb = kind ? ctx->gorder2 : ctx->gorder;
+            caps.seeded = kind == 2;
+            caps.wide = kind == 1;
+            DevBuf &gb = kind == 0 ? ctx->gorder : (kind == 1 ? ctx->gorder_w : ctx->gorder2);
             if ((rc = gb.ensure(L.size() * 4))) return rc;
-            HIP_TRY(hipMemcpyAsync(gb.p, L.data(), L.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-            const bool last = kind == 1 || lists[1].empty();
+            HIP_TRY(hipMemcpyAsync(gb.p, L.data(), L.size() * 4, hipMemcpyHostToDevice, lst));
             rc = launch_batch(ctx, *params, caps, ctx->seq.as<uint8_t>(), ctx->seq_off.as<int64_t>(),
                               ctx->grp_off.as<int64_t>(), gb.as<int32_t>(), (int64_t)L.size(),
                               ctx->cons.as<uint8_t>(), ctx->cons_off.as<int64_t>(),
                               ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
-                              ctx->status.as<int32_t>(), kMaxWavesPerCu, kind ? &sp : nullptr, first, last);
+                              ctx->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &sp : nullptr, lane == 0,
+                              nk == 1, lane);
             if (rc) return rc;
             ctx->last_launches += 1;
-            first = false;
+            ++lane;
+        }
+        if (nk > 1) {  // join the extra lanes; the batch's timing ends when every launch has
+            for (int k = 0; k < nk - 1; ++k) {
+                HIP_TRY(hipEventRecord(ctx->ev_lane[k], ctx->lane_stream[k]));
+                HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_lane[k], 0));
+            }
+            HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
         }
         HIP_TRY(hipMemcpyAsync(st.data(), ctx->status.p, st.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipMemcpyAsync(clen.data(), ctx->cons_len.p, clen.size() * 4, hipMemcpyDeviceToHost, ctx->stream));

@@ -12,6 +12,11 @@ constexpr int kChunk = kWave * kCPL;     // 128 band columns per chunk
 constexpr int kRing = 4;                 // rows of H/E1/E2 kept in LDS (32-bit mode)
 constexpr int kRing16 = 8;               // the same in 16-bit mode (same bytes)
 constexpr int kRowRing = 32;             // rows of band info kept in LDS
+// wide launches (groups whose band exceeds one chunk): the H/E1/E2 ring holds 2 chunks per row and
+// lives at the start of the dynamic LDS, ahead of the read's nibbles
+constexpr int kWideRing = 2 * kChunk;
+constexpr int kWideRingBytes = kRing16 * 3 * kWideRing * 2;
+static_assert(kWideRingBytes == kRing * 3 * kWideRing * 4, "the 16- and 32-bit rings share the bytes");
 constexpr int kPreInline = 5;            // predecessor rows stored inline in a row descriptor
 constexpr int kDescInts = 8;             // ints per row descriptor
 constexpr int kRowInfoInts = 8;          // ints per row record in HBM
@@ -51,6 +56,7 @@ struct PoaCaps {
     int64_t KPC;     // predecessor-index bytes per read (multi-predecessor rows)
     int64_t SVC;     // spilled H/E1/E2 ints per read
     int32_t seeded;  // the launch has -S groups: window descriptors and maps, per-position read nodes
+    int32_t wide;    // the launch keeps 256-column ring rows (kWideRing): bands up to 2 chunks take fast rows
 };
 
 struct SlotLayout {
@@ -139,7 +145,7 @@ struct PoaKArgs {
     const int32_t *par_item;
     const int32_t *par_n, *par_t, *par_q;
     int32_t pc, seed_k;
-    int32_t dbg;             // MANDO_POA_DBG: bit 0 no 16-bit mode, bit 1 no 16-bit fast rows
+    int32_t dbg;             // MANDO_POA_DBG: bit 0 no 16-bit mode, bit 1 no 16-bit fast rows, bit 2 no 32-bit fast rows
 };
 
 // Columns a row can touch past the read: one 128-column chunk beyond `end` (<= qlen) plus slack.
@@ -154,6 +160,9 @@ inline int poa_qlds_bytes(int64_t max_len) {
 
 // Resident workgroups per CU for these arguments (LDS / register limited), at most cap.
 int poa_blocks_per_cu(const PoaKArgs &a, int cap);
+
+// dynamic LDS of a launch: the read's nibbles, plus the wide ring in a wide launch
+inline int poa_dyn_lds(const PoaKArgs &a) { return a.qlds + (a.caps.wide ? kWideRingBytes : 0); }
 
 // Launch the persistent POA kernel on `stream` with `n_slots` one-wave workgroups.
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream);

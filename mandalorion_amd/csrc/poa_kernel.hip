@@ -195,10 +195,29 @@ struct alignas(16) SharedState {
     // the sink of the DP is node win_sink, and a node's row is wmap[pos - win_pb] inside [pb, pe]
     int win_on, win_sink, win_pb, win_pe;
     gint *desc_full, *xpre_full, *qnode_full;
+    uint64_t tmark;                 // MANDO_PROF: the last phase boundary of the -S path (prof_mark)
 };
 static_assert(sizeof(BtLds) <= sizeof(DpLds), "backtrack window must fit the DP scratch");
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_qnib[];  // dynamic: the read, 4-bit codes
+
+// Ring geometry by launch kind: RW = kChunk keeps the ring in the static LDS (col & 127); a wide launch
+// (RW = kWideRing) keeps 256-column rows at the start of the dynamic LDS and the read's nibbles after it.
+template <int RW>
+__device__ __forceinline__ uint8_t *qnib() {
+    if constexpr (RW == kChunk) return g_qnib;
+    else return g_qnib + kWideRingBytes;
+}
+template <int RW>
+__device__ __forceinline__ short *ring16_row(const SharedState &sh, int row) {
+    if constexpr (RW == kChunk) return const_cast<short *>(&sh.dp.ring16[row][0][0]);
+    else return reinterpret_cast<short *>(g_qnib) + row * 3 * RW;
+}
+template <int RW>
+__device__ __forceinline__ int *ring32_row(const SharedState &sh, int row) {
+    if constexpr (RW == kChunk) return const_cast<int *>(&sh.dp.ring[row][0][0]);
+    else return reinterpret_cast<int *>(g_qnib) + row * 3 * RW;
+}
 
 // Each phase re-reads the few workspace pointers it needs from LDS behind a compiler barrier, so
 // the ~30 loop-invariant 64-bit pointers are not kept live (and spilled) across the whole
@@ -660,16 +679,17 @@ __device__ __forceinline__ RowRec load_rowrec(const SharedState &sh, const Slot 
 // that are wider, or that have a successor >= kRing rows later, are (also) spilled to HBM as three
 // planes of nchunk*128 ints starting at column cb0; a (rare) predecessor outside the ring is read
 // from those planes.
-__device__ __forceinline__ bool row_narrow(int beg, int end) { return end - (beg & ~1) < kChunk; }
+template <int RW = kChunk>
+__device__ __forceinline__ bool row_narrow(int beg, int end) { return end - (beg & ~1) < RW; }
 // rows of H/E1/E2 the LDS ring holds: the 16-bit ring fits twice as many in the same bytes
 template <bool R16>
 __device__ __forceinline__ constexpr int ring_rows() { return R16 ? kRing16 : kRing; }
 __device__ __forceinline__ int row_spill_width(int beg, int end) {
     return ((end - (beg & ~1)) / kChunk + 1) * kChunk;
 }
-template <bool R16>
+template <bool R16, int RW>
 __device__ __forceinline__ bool pre_in_ring(int r, int p, const RowRec &pr) {
-    return (r - p < ring_rows<R16>()) && row_narrow(pr.beg, pr.end);
+    return (r - p < ring_rows<R16>()) && row_narrow<RW>(pr.beg, pr.end);
 }
 
 // Scoring: the reference always runs `abpoa -M 5` with default gaps, so that case is compiled with
@@ -698,8 +718,9 @@ struct DpState {
 
 // code of the query base consumed by column j (base j-1): nibble j of the shifted stream, 4 for
 // column 0 and every column past the read
-__device__ __forceinline__ int qcol(const SharedState &sh, int j) {
-    return (g_qnib[j >> 1] >> ((j & 1) << 2)) & 0xf;
+template <int RW>
+__device__ __forceinline__ int qcol(int j) {
+    return (qnib<RW>()[j >> 1] >> ((j & 1) << 2)) & 0xf;
 }
 
 // Rare-case predecessor records (more than kPreInline predecessors, or a predecessor whose record
@@ -751,33 +772,55 @@ __device__ __forceinline__ bool in_band(int col, int b, int e) {
 }
 
 // Ring access for the generic row in both modes.  16-bit mode stores values clamped to int16
-// (-inf = -32768); the 32-bit mode stores kNegInf.  Columns are absolute & 127.
+// (-inf = -32768); the 32-bit mode stores kNegInf.  Columns are absolute & (RW - 1).
 __device__ __forceinline__ int clamp16(int v) { return min(max(v, -32768), 32767); }
-template <bool R16>
+template <bool R16, int RW>
 __device__ __forceinline__ int ring_get(const SharedState &sh, int row, int plane, int col) {
-    if constexpr (R16) return sh.dp.ring16[row][plane][col];
-    else return sh.dp.ring[row][plane][col];
+    if constexpr (R16) return ring16_row<RW>(sh, row)[plane * RW + col];
+    else return ring32_row<RW>(sh, row)[plane * RW + col];
 }
 // (col, col+1) of one plane; col even
-template <bool R16>
+template <bool R16, int RW>
 __device__ __forceinline__ int2 ring_get2(const SharedState &sh, int row, int plane, int col) {
     if constexpr (R16) {
-        const uint32_t w = *reinterpret_cast<const uint32_t *>(&sh.dp.ring16[row][plane][col]);
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, row) + plane * RW + col);
         return make_int2((int)(short)(w & 0xffff), (int)w >> 16);
     } else {
-        return *reinterpret_cast<const int2 *>(&sh.dp.ring[row][plane][col]);
+        return *reinterpret_cast<const int2 *>(ring32_row<RW>(sh, row) + plane * RW + col);
     }
 }
-template <bool R16>
+template <bool R16, int RW>
 __device__ __forceinline__ void ring_put2(SharedState &sh, int row, int plane, int col, int a, bool va, int b,
                                           bool vb) {
     if constexpr (R16) {
         const uint32_t lo = (uint32_t)(va ? clamp16(a) : -32768) & 0xffff;
         const uint32_t hi = (uint32_t)(vb ? clamp16(b) : -32768) << 16;
-        *reinterpret_cast<uint32_t *>(&sh.dp.ring16[row][plane][col]) = lo | hi;
+        *reinterpret_cast<uint32_t *>(ring16_row<RW>(sh, row) + plane * RW + col) = lo | hi;
     } else {
-        *reinterpret_cast<int2 *>(&sh.dp.ring[row][plane][col]) = make_int2(va ? a : kNegInf, vb ? b : kNegInf);
+        *reinterpret_cast<int2 *>(ring32_row<RW>(sh, row) + plane * RW + col) =
+            make_int2(va ? a : kNegInf, vb ? b : kNegInf);
     }
+}
+
+// 16-bit mode is exact when every finite value fits with room to spare (see kR16Low) and the
+// biased score table fits in bytes.  No score exceeds match * qlen, and the gap terms of a row add
+// at most (e1 + e2) * RW + o1 + o2 on top; a read whose scores would not fit is shifted down by a
+// constant (every value of every row, the source row included: the DP is translation-invariant), as
+// long as the shift leaves room above the -inf band for the low scores (8000 or more; a read that
+// still leaves the safe range is re-aligned in 32-bit mode).  Reads up to ~6.4 kb (default scores)
+// are not shifted.
+constexpr int kR16NoBias = 1 << 30;
+template <class SC, int RW>
+__device__ __forceinline__ int r16_bias(const SC &sc, int qlen) {
+    const bool ok = sc.match >= 0 && sc.mismatch >= 0 && sc.match + sc.mismatch <= 255 && sc.e1 >= 0 && sc.e2 >= 0 &&
+                    sc.o1 >= 0 && sc.o2 >= 0 && (sc.e1 + sc.e2) * kChunk + sc.o1 + sc.o2 <= 2000;
+    const int64_t top = (int64_t)sc.match * qlen + (int64_t)(sc.e1 + sc.e2) * RW + sc.o1 + sc.o2 + 64;
+    const int64_t b = top > 32767 ? 32767 - top : 0;
+    return ok && b >= -20000 ? (int)b : kR16NoBias;
+}
+template <class SC, int RW>
+__device__ __forceinline__ bool r16_eligible(const SC &sc, int qlen) {
+    return r16_bias<SC, RW>(sc, qlen) != kR16NoBias;
 }
 
 // 16-bit mode: a finite H must never be confused with a -inf-derived one (those stay below
@@ -787,8 +830,10 @@ constexpr int kR16Low = -31000, kR16High = -28000;
 
 // One DP row r.  Predecessor k's record lives in lane k (pP row, pB/pE band, pA argmax, pS spill
 // offset); the common case (every predecessor in the LDS ring) reads values with 4 LDS ops per
-// predecessor and no global memory traffic except the traceback stores.
-template <class SC, bool R16>
+// predecessor and no global memory traffic except the traceback stores.  RW: ring columns per row
+// (a wide launch keeps rows of up to two chunks in the ring; those rows hold only the columns they
+// wrote, which the band masks below cover).
+template <class SC, bool R16, int RW = kChunk>
 __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
                                       int w, int r, int lane, DpState &ds) {
     const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
@@ -833,12 +878,12 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
         end = min(qlen, max(posR, x) + w);
     }
     constexpr int kR = ring_rows<R16>();
-    const bool pring = (r - pP < kR) && row_narrow(pB, pE);
+    const bool pring = (r - pP < kR) && row_narrow<RW>(pB, pE);
     const bool all_ring = __ballot(lane < pn && !pring) == 0;
     const int cb0 = beg & ~1;
     const int span = end - cb0 + 1;
     const int nchunk = (span + kChunk - 1) / kChunk;
-    const bool narrow = nchunk == 1;
+    const bool narrow = nchunk <= RW / kChunk;  // kept in the ring
     const bool spill = far || !narrow;
     const int wa = nchunk * kChunk;
     const int tbw = (span + 3) & ~3;
@@ -868,25 +913,27 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
         int Ha, Hb, E1a, E1b, E2a, E2b;
         int tpair = 0;
         if (r == 0) {
-            // source row: H[0][0] = 0, H[0][j] = max(-(o1+e1 j), -(o2+e2 j))
-            Ha = (j0 == 0) ? 0 : max(-(sc.o1 + e1 * j0), -(sc.o2 + e2 * j0));
-            Hb = max(-(sc.o1 + e1 * j1), -(sc.o2 + e2 * j1));
+            // source row: H[0][0] = 0, H[0][j] = max(-(o1+e1 j), -(o2+e2 j)) (+ the 16-bit bias)
+            int B = 0;
+            if constexpr (R16) B = r16_bias<SC, RW>(sc, qlen);  // eligible: the caller checked
+            Ha = B + ((j0 == 0) ? 0 : max(-(sc.o1 + e1 * j0), -(sc.o2 + e2 * j0)));
+            Hb = B + max(-(sc.o1 + e1 * j1), -(sc.o2 + e2 * j1));
             E1a = Ha - oe1;
             E1b = Hb - oe1;
             E2a = Ha - oe2;
             E2b = Hb - oe2;
         } else {
-            const int qa = qcol(sh, j0), qb = qcol(sh, j1);
+            const int qa = qcol<RW>(j0), qb = qcol<RW>(j1);
             int Mva, Mvb, X1a, X1b, X2a, X2b;
             int mka = 0, mkb = 0, k1a = 0, k1b = 0, k2a = 0, k2b = 0;
-            const int ia = (j0 - 1) & (kChunk - 1), ib = j0 & (kChunk - 1);
+            const int ia = (j0 - 1) & (RW - 1), ib = j0 & (RW - 1);
             if (all_ring && pn == 1) {
                 // the common row: one predecessor, in the ring
                 const int p0 = readlane(pP, 0), b0 = readlane(pB, 0), e0 = readlane(pE, 0);
                 const int pr = p0 % kR;
-                const int hA = ring_get<R16>(sh, pr, 0, ia), hB = ring_get<R16>(sh, pr, 0, ib);
-                const int2 x1 = ring_get2<R16>(sh, pr, 1, ib);
-                const int2 x2 = ring_get2<R16>(sh, pr, 2, ib);
+                const int hA = ring_get<R16, RW>(sh, pr, 0, ia), hB = ring_get<R16, RW>(sh, pr, 0, ib);
+                const int2 x1 = ring_get2<R16, RW>(sh, pr, 1, ib);
+                const int2 x2 = ring_get2<R16, RW>(sh, pr, 2, ib);
                 const bool inA = in_band(j0 - 1, b0, e0), inB = in_band(j0, b0, e0),
                            inC = in_band(j1, b0, e0);
                 Mva = inA ? hA : kNegInf;
@@ -902,13 +949,13 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
                     const int pk = readlane(pP, k), bk = readlane(pB, k), ek = readlane(pE, k);
                     int hA, hB;
                     int2 x1, x2;
-                    if (all_ring || (r - pk < kR && row_narrow(bk, ek))) {
+                    if (all_ring || (r - pk < kR && row_narrow<RW>(bk, ek))) {
                         const int pr = pk % kR;
-                        const int iA = (j0 - 1) & (kChunk - 1), iB = j0 & (kChunk - 1);
-                        hA = ring_get<R16>(sh, pr, 0, iA);
-                        hB = ring_get<R16>(sh, pr, 0, iB);
-                        x1 = ring_get2<R16>(sh, pr, 1, iB);
-                        x2 = ring_get2<R16>(sh, pr, 2, iB);
+                        const int iA = (j0 - 1) & (RW - 1), iB = j0 & (RW - 1);
+                        hA = ring_get<R16, RW>(sh, pr, 0, iA);
+                        hB = ring_get<R16, RW>(sh, pr, 0, iB);
+                        x1 = ring_get2<R16, RW>(sh, pr, 1, iB);
+                        x2 = ring_get2<R16, RW>(sh, pr, 2, iB);
                     } else {
                         // predecessor outside the ring: its spill planes in HBM (columns clamped to
                         // the spilled width; out-of-band values are masked below)
@@ -983,10 +1030,10 @@ __device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, 
         }
         if (va || vbb) *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)tpair;
         if (narrow) {  // out-of-band columns hold -inf (see dp_row_fast)
-            const int ibk = j0 & (kChunk - 1), rr = r % kR;
-            ring_put2<R16>(sh, rr, 0, ibk, Ha, va, Hb, vbb);
-            ring_put2<R16>(sh, rr, 1, ibk, E1a, va, E1b, vbb);
-            ring_put2<R16>(sh, rr, 2, ibk, E2a, va, E2b, vbb);
+            const int ibk = j0 & (RW - 1), rr = r % kR;
+            ring_put2<R16, RW>(sh, rr, 0, ibk, Ha, va, Hb, vbb);
+            ring_put2<R16, RW>(sh, rr, 1, ibk, E1a, va, E1b, vbb);
+            ring_put2<R16, RW>(sh, rr, 2, ibk, E2a, va, E2b, vbb);
         }
         if constexpr (R16) {
             // finite values must stay clear of the -inf band (see kR16Low)
@@ -1277,14 +1324,6 @@ __device__ __forceinline__ uint32_t pk_scan_umax(uint32_t u) {
     return u;
 }
 
-// 16-bit mode is exact when every finite value fits with room to spare (see kR16Low) and the
-// biased score table fits in bytes.
-template <class SC>
-__device__ __forceinline__ bool r16_eligible(const SC &sc, int qlen) {
-    return sc.match >= 0 && sc.mismatch >= 0 && sc.match + sc.mismatch <= 255 && sc.e1 >= 0 && sc.e2 >= 0 &&
-           sc.o1 >= 0 && sc.o2 >= 0 && (sc.e1 + sc.e2) * kChunk + sc.o1 + sc.o2 <= 2000 &&
-           (int64_t)sc.match * qlen <= 30000;
-}
 
 // ---- 16-bit mode with scalar row control -------------------------------------------------------
 // Everything that is uniform per row (descriptor, predecessor band records, band, fast-path
@@ -1302,9 +1341,10 @@ struct Row16 {
     int pn3;                      // predecessor count when >= 3 (predecessors 2.. are read in row16_vec)
 };
 
-template <class SC>
+template <class SC, int RW>
 __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *sv, gint *rinfo, SharedState &sh,
                                          int lane, const Row16 &R, DpState &ds) {
+    constexpr int HW = RW / 2;  // ring words per plane
     const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
     const int beg = R.beg, end = R.end, cb0 = R.cb0;
     const int tbbase = ds.tb_used - cb0;
@@ -1316,15 +1356,15 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     const uint32_t LJ = (uint32_t)(2 * lane) * 0x10001u + 0x10000u;  // (j0, j0 + 1) - cb0
     const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2s(beg))) |
                                      as_u32(as_s16x2(pk2s(end)) - as_s16x2(J)));
-    const int qbyte = g_qnib[j0 >> 1];
+    const int qbyte = qnib<RW>()[j0 >> 1];
     const uint32_t sel = (uint32_t)(qbyte & 0xf) | (((uint32_t)qbyte & 0xf0u) << 12) | 0x0C000C00u;
     const uint32_t tlo =
         R.vb < 4 ? (uint32_t)(sc.match + sc.mismatch) << (8 * R.vb) : (uint32_t)sc.mismatch * 0x01010101u;
     const uint32_t S = __builtin_amdgcn_perm((uint32_t)sc.mismatch, tlo, sel);
-    const int iw = (j0 >> 1) & (kChunk / 2 - 1), iwp = (iw - 1) & (kChunk / 2 - 1);
-    const uint32_t *w0 = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[R.p0slot][0][0]);
+    const int iw = (j0 >> 1) & (HW - 1), iwp = (iw - 1) & (HW - 1);
+    const uint32_t *w0 = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, R.p0slot));
     uint32_t Hd = __builtin_amdgcn_alignbit(w0[iw], w0[iwp], 16);
-    uint32_t X1 = w0[kChunk / 2 + iw], X2 = w0[kChunk + iw];
+    uint32_t X1 = w0[HW + iw], X2 = w0[2 * HW + iw];
     const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0)
     if (!R.nomask) {
         const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2s(R.b0))) |
@@ -1337,9 +1377,9 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     }
     uint32_t MK = 0, K1 = 0, K2 = 0;
     if (R.two) {
-        const uint32_t *w1 = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[R.p1slot][0][0]);
+        const uint32_t *w1 = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, R.p1slot));
         uint32_t Hd1 = __builtin_amdgcn_alignbit(w1[iw], w1[iwp], 16);
-        uint32_t X11 = w1[kChunk / 2 + iw], X21 = w1[kChunk + iw];
+        uint32_t X11 = w1[HW + iw], X21 = w1[2 * HW + iw];
         if (!R.nomask) {
             const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2s(R.b1))) |
                                             as_u32(as_s16x2(pk2s(R.e1)) - as_s16x2(JD)));
@@ -1362,11 +1402,11 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         const int p = bcast0(sh.desc[R.r & (kDescBatch - 1)][3 + k]);
         const int4 x = sh.rrow[p & (kRowRing - 1)];
         const int bk = bcast0(x.x), ek = bcast0(x.y);
-        const uint32_t *wk = reinterpret_cast<const uint32_t *>(&sh.dp.ring16[p & (kRing16 - 1)][0][0]);
+        const uint32_t *wk = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, p & (kRing16 - 1)));
         uint32_t Hdk = __builtin_amdgcn_alignbit(wk[iw], wk[iwp], 16);
-        uint32_t X1k = wk[kChunk / 2 + iw], X2k = wk[kChunk + iw];
+        uint32_t X1k = wk[HW + iw], X2k = wk[2 * HW + iw];
         const int pck = bk & ~1;
-        if (((beg - 1 - pck) | (pck + kChunk - 1 - end)) < 0) {
+        if (RW != kChunk || ((beg - 1 - pck) | (pck + kChunk - 1 - end)) < 0) {
             const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(pk2s(bk))) |
                                             as_u32(as_s16x2(pk2s(ek)) - as_s16x2(JD)));
             const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2s(bk))) |
@@ -1411,10 +1451,10 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         kq[2] = (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u);
     }
     const uint32_t Hs = bfi(inv, kNeg2, H);
-    uint32_t *wr = reinterpret_cast<uint32_t *>(&sh.dp.ring16[R.r & (kRing16 - 1)][0][0]);
+    uint32_t *wr = reinterpret_cast<uint32_t *>(ring16_row<RW>(sh, R.r & (kRing16 - 1)));
     wr[iw] = Hs;
-    wr[kChunk / 2 + iw] = bfi(inv, kNeg2, E1);
-    wr[kChunk + iw] = bfi(inv, kNeg2, E2);
+    wr[HW + iw] = bfi(inv, kNeg2, E1);
+    wr[2 * HW + iw] = bfi(inv, kNeg2, E2);
     if (R.far) {
         gint *svp = sv + svbase;
         svp[j0] = (int)(short)(H & 0xffff);
@@ -1448,11 +1488,164 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     return besti;
 }
 
+// Wide fast row (wide launches only): a band of 129..256 columns as two 128-column halves, lane l
+// holding columns cb0 + 128h + 2l and +1 of half h.  The halves are computed side by side; their F
+// prefix scans are independent, and the upper half takes the lower half's total as its carry-in.
+// Ring rows of a wide launch hold only the columns their row wrote, so the predecessors' values are
+// always band-masked.  One or two predecessors (more: the generic row).
+template <class SC>
+__device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *sv, gint *rinfo, SharedState &sh,
+                                          int lane, const Row16 &R, DpState &ds) {
+    constexpr int RW = kWideRing, HW = RW / 2;
+    const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
+    const int beg = R.beg, end = R.end, cb0 = R.cb0;
+    const int tbbase = ds.tb_used - cb0;
+    const int kpbase = ds.kp_used - 3 * cb0;
+    const int soff = R.far ? ds.sv_used : -1;
+    const int svbase = ds.sv_used - cb0;
+    const uint32_t *w0 = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, R.p0slot));
+    const uint32_t *w1 = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, R.p1slot));
+    const uint32_t tlo =
+        R.vb < 4 ? (uint32_t)(sc.match + sc.mismatch) << (8 * R.vb) : (uint32_t)sc.mismatch * 0x01010101u;
+    const uint32_t B0 = pk2s(R.b0), E0 = pk2s(R.e0), B1 = pk2s(R.b1), E1b = pk2s(R.e1);
+    const uint32_t BEG = pk2s(beg), END = pk2s(end);
+    uint32_t H0v[2], Mv[2], X1v[2], X2v[2], MKv[2], K1v[2], K2v[2], G1v[2], G2v[2], Gav[2], incv[2], invv[2];
+    uint32_t LJ1v[2], LJ2v[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j0 = cb0 + kChunk * h + 2 * lane;
+        const uint32_t J = (uint32_t)j0 * 0x10001u + 0x10000u;                            // (j0, j0 + 1)
+        const uint32_t LJ = (uint32_t)(kChunk * h + 2 * lane) * 0x10001u + 0x10000u;      // the same - cb0
+        const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(BEG)) | as_u32(as_s16x2(END) - as_s16x2(J)));
+        const int qbyte = qnib<RW>()[j0 >> 1];
+        const uint32_t sel = (uint32_t)(qbyte & 0xf) | (((uint32_t)qbyte & 0xf0u) << 12) | 0x0C000C00u;
+        const uint32_t S = __builtin_amdgcn_perm((uint32_t)sc.mismatch, tlo, sel);
+        const int iw = (j0 >> 1) & (HW - 1), iwp = (iw - 1) & (HW - 1);
+        const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0)
+        uint32_t Hd = __builtin_amdgcn_alignbit(w0[iw], w0[iwp], 16);
+        uint32_t X1 = w0[HW + iw], X2 = w0[2 * HW + iw];
+        {
+            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(B0)) | as_u32(as_s16x2(E0) - as_s16x2(JD)));
+            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(B0)) | as_u32(as_s16x2(E0) - as_s16x2(J)));
+            Hd = bfi(md, kNeg2, Hd);
+            X1 = bfi(me, kNeg2, X1);
+            X2 = bfi(me, kNeg2, X2);
+        }
+        uint32_t MK = 0, K1 = 0, K2 = 0;
+        if (R.two) {
+            uint32_t Hd1 = __builtin_amdgcn_alignbit(w1[iw], w1[iwp], 16);
+            uint32_t X11 = w1[HW + iw], X21 = w1[2 * HW + iw];
+            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(B1)) | as_u32(as_s16x2(E1b) - as_s16x2(JD)));
+            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(B1)) | as_u32(as_s16x2(E1b) - as_s16x2(J)));
+            Hd1 = bfi(md, kNeg2, Hd1);
+            X11 = bfi(me, kNeg2, X11);
+            X21 = bfi(me, kNeg2, X21);
+            MK = pk_lt_bit<0>(Hd, Hd1);
+            K1 = pk_lt_bit<0>(X1, X11);
+            K2 = pk_lt_bit<0>(X2, X21);
+            Hd = pk_max(Hd, Hd1);
+            X1 = pk_max(X1, X11);
+            X2 = pk_max(X2, X21);
+        }
+        const uint32_t M = pk_subs(pk_adds(Hd, S), pk2(sc.mismatch));
+        const uint32_t H0 = bfi(inv, kNeg2, pk_max(M, pk_max(X1, X2)));
+        const uint32_t LJ1 = as_u32(as_u16x2(LJ) * (u16x2){(unsigned short)e1, (unsigned short)e1});
+        const uint32_t LJ2 = as_u32(as_u16x2(LJ) * (u16x2){(unsigned short)e2, (unsigned short)e2});
+        const uint32_t G1 = pk_adds(H0, LJ1), G2 = pk_adds(H0, LJ2);
+        const uint32_t Ga = __builtin_amdgcn_perm(G2, G1, 0x05040100u);
+        const uint32_t Gb = __builtin_amdgcn_perm(G2, G1, 0x07060302u);
+        incv[h] = pk_scan_umax(pk_max(Ga, Gb) ^ kNeg2);
+        H0v[h] = H0;
+        Mv[h] = M;
+        X1v[h] = X1;
+        X2v[h] = X2;
+        MKv[h] = MK;
+        K1v[h] = K1;
+        K2v[h] = K2;
+        G1v[h] = G1;
+        G2v[h] = G2;
+        Gav[h] = Ga;
+        invv[h] = inv;
+        LJ1v[h] = LJ1;
+        LJ2v[h] = LJ2;
+    }
+    // the lower half's total (both F planes, biased) is the carry into the upper half
+    const uint32_t carry = (uint32_t)__builtin_amdgcn_readlane((int)incv[0], kWave - 1);
+    uint32_t *wr = reinterpret_cast<uint32_t *>(ring16_row<RW>(sh, R.r & (kRing16 - 1)));
+    gint *svp = sv + svbase;
+    int amv = -2147483647 - 1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j0 = cb0 + kChunk * h + 2 * lane;
+        const int iw = (j0 >> 1) & (HW - 1);
+        uint32_t Pa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incv[h], 0x138, 0xf, 0xf, true);
+        if (h == 1) Pa = pk_umax(Pa, carry);
+        Pa ^= kNeg2;
+        const uint32_t Pb = pk_max(Pa, Gav[h]);
+        const uint32_t P1 = __builtin_amdgcn_perm(Pb, Pa, 0x05040100u);
+        const uint32_t P2 = __builtin_amdgcn_perm(Pb, Pa, 0x07060302u);
+        const uint32_t F1 = pk_subs(P1, LJ1v[h] + pk2(oe1 - e1)), F2 = pk_subs(P2, LJ2v[h] + pk2(oe2 - e2));
+        const uint32_t X1 = X1v[h], X2 = X2v[h], H0 = H0v[h];
+        const uint32_t H = pk_max(H0, pk_max(F1, F2));
+        const uint32_t X1e = pk_subs(X1, pk2(e1)), Ho1 = pk_subs(H, pk2(oe1));
+        const uint32_t X2e = pk_subs(X2, pk2(e2)), Ho2 = pk_subs(H, pk2(oe2));
+        const uint32_t E1 = pk_max(X1e, Ho1), E2 = pk_max(X2e, Ho2);
+        const uint32_t tbv = pk_ne_bit<0>(H, Mv[h]) | pk_ne_bit<1>(H, X1) | pk_ne_bit<2>(H, X2) | pk_ne_bit<3>(H, F1) |
+                             pk_lt_bit<4>(Ho1, X1e) | pk_lt_bit<5>(Ho2, X2e) | pk_lt_bit<6>(G1v[h], P1) |
+                             pk_lt_bit<7>(G2v[h], P2);
+        *reinterpret_cast<GLB uint16_t *>(tb + (tbbase + j0)) = (uint16_t)__builtin_amdgcn_perm(0u, tbv, 0x0C0C0200u);
+        if (R.multi) {
+            GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(kp + (kpbase + 3 * j0));
+            kq[0] = (uint16_t)__builtin_amdgcn_perm(K1v[h], MKv[h], 0x0C0C0400u);
+            kq[1] = (uint16_t)__builtin_amdgcn_perm(MKv[h], K2v[h], 0x0C0C0600u);
+            kq[2] = (uint16_t)__builtin_amdgcn_perm(K2v[h], K1v[h], 0x0C0C0602u);
+        }
+        const uint32_t inv = invv[h];
+        const uint32_t Hs = bfi(inv, kNeg2, H);
+        wr[iw] = Hs;
+        wr[HW + iw] = bfi(inv, kNeg2, E1);
+        wr[2 * HW + iw] = bfi(inv, kNeg2, E2);
+        if (R.far) {  // spill planes of a two-chunk row: stride RW (row_spill_width)
+            svp[j0] = (int)(short)(H & 0xffff);
+            svp[j0 + 1] = (int)H >> 16;
+            svp[RW + j0] = (int)(short)(E1 & 0xffff);
+            svp[RW + j0 + 1] = (int)E1 >> 16;
+            svp[2 * RW + j0] = (int)(short)(E2 & 0xffff);
+            svp[2 * RW + j0 + 1] = (int)E2 >> 16;
+        }
+        ds.r16acc = pk_umin(ds.r16acc, as_u32(as_u16x2(Hs) - as_u16x2(pk2(kR16Low))));
+        // leftmost argmax: value above 8 bits of (255 - column offset)
+        const int c0 = kChunk * h + 2 * lane;
+        const int ca = ((int)(short)(Hs & 0xffff) << 8) | (255 - c0);
+        const int cbk = (((int)Hs >> 16) << 8) | (254 - c0);
+        amv = max(amv, max(ca, cbk));
+    }
+    const int mp = readlane(dpp_incl_max(amv, -2147483647 - 1), kWave - 1);
+    const int besti = cb0 + 255 - (mp & 255);
+    ds.tb_used += R.tbw;
+    if (R.multi) ds.kp_used += 3 * R.tbw;
+    if (R.far) ds.sv_used += 3 * RW;
+    ds.cells += end - beg + 1;
+    if (lane == 0) {
+        sh.rrow[R.r & (kRowRing - 1)] = make_int4(beg, end, besti, soff);
+        gint *ri = rinfo + (int64_t)R.r * kRowInfoInts;
+        ri[0] = beg;
+        ri[1] = end;
+        ri[2] = besti;
+        ri[3] = soff;
+        ri[4] = tbbase;
+        ri[5] = kpbase;
+        ri[6] = R.node;
+        ri[7] = R.pn;
+    }
+    return besti;
+}
+
 // The row loop of 16-bit mode (same rows, same results as run_dp<SC, true>).  The per-row
 // control is written for the scalar unit: tests accumulate as sign bits into one word
 // (`bad < 0` = take the generic row) rather than as bools, which the compiler would keep as
 // 64-bit lane masks.
-template <class SC>
+template <class SC, int RW>
 __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen, int n, int lane, int w,
                                         DpState &ds, int &nfast) {
     gu8 *tb, *kp;
@@ -1467,9 +1660,9 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         rinfo = s.rinfo;
         desc = s.desc;
         // a fast row allocates at most tbw + one chunk of slack
-        tb_lim = (int)a.caps.TBC - 2 * (kChunk + 4);
-        kp_lim = (int)a.caps.KPC - 6 * (kChunk + 4);
-        sv_lim = (int)a.caps.SVC - 3 * kChunk;
+        tb_lim = (int)a.caps.TBC - 2 * (RW + 4);
+        kp_lim = (int)a.caps.KPC - 6 * (RW + 4);
+        sv_lim = (int)a.caps.SVC - 3 * RW;
     }
     int prv_r = -1, prv_beg = 0, prv_end = 0, prv_am = 0;
     // Descriptor batches reach LDS one batch ahead: lane l holds ints [4l, 4l+4) of the next 32 rows
@@ -1497,7 +1690,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         if (b0 == 0) {
             Slot s = slot_of(sh);
             const PoaKArgs a = args_of(sh);
-            const int st = dp_row<SC, true>(a, sc, s, sh, qlen, w, 0, lane, ds);
+            const int st = dp_row<SC, true, RW>(a, sc, s, sh, qlen, w, 0, lane, ds);
             if (st != kStOk) return st;
             const int4 x = sh.rrow[0];
             prv_r = 0;
@@ -1558,7 +1751,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
                     const int amk = bcast0(x.z);
                     amL = min(amL, amk);
                     amR = max(amR, amk);
-                    narrowk |= kChunk - 1 - (bcast0(x.y) - (bcast0(x.x) & ~1));
+                    narrowk |= RW - 1 - (bcast0(x.y) - (bcast0(x.x) & ~1));
                 }
                 const int xr = qlen - rem;
                 R.beg = max(0, min(amL + 1, xr) - w);
@@ -1567,11 +1760,13 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
                 const int span = R.end - R.cb0 + 1;
                 R.tbw = (span + 3) & ~3;
                 const int pc0 = R.b0 & ~1, pc1 = R.b1 & ~1;
-                // each term is negative exactly when its test fails
-                bad = (kChunk - span) | (kChunk - 1 - (R.e0 - pc0)) | (kChunk - 1 - (R.e1 - pc1)) | narrowk |
+                // each term is negative exactly when its test fails (a two-chunk row: at most two
+                // predecessors)
+                bad = (RW - span) | (RW - 1 - (R.e0 - pc0)) | (RW - 1 - (R.e1 - pc1)) | narrowk |
                       (tb_lim - ds.tb_used) | (kp_lim - ds.kp_used) | (sv_lim - ds.sv_used);
-                R.nomask = ((R.beg - 1 - pc0) | (pc0 + kChunk - 1 - R.end) | (R.beg - 1 - pc1) |
-                            (pc1 + kChunk - 1 - R.end)) >= 0;
+                if (RW != kChunk && span > kChunk) bad |= -R.pn3;
+                R.nomask = RW == kChunk && ((R.beg - 1 - pc0) | (pc0 + kChunk - 1 - R.end) | (R.beg - 1 - pc1) |
+                                            (pc1 + kChunk - 1 - R.end)) >= 0;
                 R.r = r;
                 R.node = node;
                 R.vb = d1 & 0xff;
@@ -1583,7 +1778,9 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
             }
         }
         if (bad >= 0) {
-            const int besti = row16_vec(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
+            int besti;
+            if (RW == kChunk || R.end - R.cb0 < kChunk) besti = row16_vec<SC, RW>(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
+            else besti = row16w_vec(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
             prv_r = r;
             prv_beg = R.beg;
             prv_end = R.end;
@@ -1595,7 +1792,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
 #ifdef MANDO_GENPROF
             const uint64_t g0 = clock64();
 #endif
-            const int st = dp_row<SC, true>(a, sc, s, sh, qlen, w, r, lane, ds);
+            const int st = dp_row<SC, true, RW>(a, sc, s, sh, qlen, w, r, lane, ds);
 #ifdef MANDO_GENPROF
             ds.seg[0] += clock64() - g0;
             {
@@ -1624,7 +1821,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
 // banded DP over all rows of the current graph for read q (qlen): writes the traceback bytes and
 // returns the start row of the backtrack in bi_out (or -1)
 // ---------------------------------------------------------------------------------------------
-template <class SC, bool R16>
+template <class SC, bool R16, int RW = kChunk>
 __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8_t *q, int qlen,
                       int n, int lane, int64_t &cells, int &bi_out) {
     const PoaKArgs a = args_of(sh);
@@ -1639,11 +1836,11 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
     // (shifted by one column: nibble j = base j-1; nibble 0 and the kQPad columns past the read = 4)
     for (int t = 2 * lane; t < qlen + kQPad; t += 2 * kWave) {
         const int lo = (t >= 1 && t <= qlen) ? q[t - 1] : 4, hi = (t < qlen) ? q[t] : 4;
-        g_qnib[t >> 1] = (uint8_t)(lo | (hi << 4));
+        qnib<RW>()[t >> 1] = (uint8_t)(lo | (hi << 4));
     }
     int nfast = 0;
     if constexpr (R16) {
-        const int st = run_dp16(sh, sc, qlen, n, lane, w, ds, nfast);
+        const int st = run_dp16<SC, RW>(sh, sc, qlen, n, lane, w, ds, nfast);
         if (st != kStOk) return st;
     } else {
     RowPipe pp;
@@ -1663,11 +1860,12 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
         }
         bool fastok;
         {
-            fastok = r > 0 && dp_row_fast(a, sc, s, sh, qlen, w, r, lane, ds, pp);
+            if constexpr (RW == kChunk) fastok = r > 0 && !(a.dbg & 4) && dp_row_fast(a, sc, s, sh, qlen, w, r, lane, ds, pp);
+            else fastok = false;
         }
         nfast += fastok;
         if (!fastok) {
-            const int st = dp_row<SC, R16>(a, sc, s, sh, qlen, w, r, lane, ds);
+            const int st = dp_row<SC, R16, RW>(a, sc, s, sh, qlen, w, r, lane, ds);
             if (st != kStOk) return st;
             const int4 x = sh.rrow[r % kRowRing];
             pp.prv_r = r;
@@ -1712,8 +1910,8 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
         const RowRec pr = load_rowrec(sh, s, sr, p);
         if (qlen < pr.beg || qlen > pr.end) continue;
         int hv;
-        if (pre_in_ring<R16>(sr, p, pr)) {
-            hv = ring_get<R16>(sh, p % ring_rows<R16>(), 0, qlen & (kChunk - 1));
+        if (pre_in_ring<R16, RW>(sr, p, pr)) {
+            hv = ring_get<R16, RW>(sh, p % ring_rows<R16>(), 0, qlen & (RW - 1));
         } else {
             hv = s.sv[pr.soff + (qlen - (pr.beg & ~1))];
         }
@@ -2019,6 +2217,22 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
 // the window rows between their bounding nodes, each writing its slice of qnode.  The whole read's
 // path then goes through update_graph at once, exactly like an unseeded read.
 // ---------------------------------------------------------------------------------------------
+// MANDO_PROF: adds the cycles since the last mark to phase k (k < 0: only sets the mark); a window's
+// row count goes to phase 5 and the window to phase 6.  State lives in LDS, not in registers.
+__device__ __forceinline__ void prof_mark(SharedState &sh, int lane, int k, int rows = -1) {
+    int64_t *prof = sh.args.prof;
+    if (prof && lane == 0) {
+        prof += (int64_t)blockIdx.x * kProfPhases;
+        const uint64_t t = clock64();
+        if (k >= 0) prof[k] += (int64_t)(t - sh.tmark);
+        if (rows >= 0) {
+            prof[5] += rows;
+            prof[6] += 1;
+        }
+        sh.tmark = t;
+    }
+}
+
 template <class SC>
 __device__ __forceinline__ int align_seeded(SharedState &sh, const SC &sc, const uint8_t *q, int qlen, int n, int lane,
                                             int64_t &cells, int64_t rd) {
@@ -2034,8 +2248,11 @@ __device__ __forceinline__ int align_seeded(SharedState &sh, const SC &sc, const
         par_t = a.par_t;
         par_q = a.par_q;
     }
+    // MANDO_PROF phases of -S: 0 descriptors + windows, 1 dp, 2 backtrack, 5 window rows, 6 windows
+    prof_mark(sh, lane, -1);
     build_desc(sh, n, lane, kRing);
     wave_sync();
+    prof_mark(sh, lane, 0);
     int B = kSrc, q0 = 0;
     for (int x = 0; x <= np; ++x) {
         int E = kSink, q1 = qlen, tx = 0;
@@ -2049,7 +2266,7 @@ __device__ __forceinline__ int align_seeded(SharedState &sh, const SC &sc, const
         }
         if (q1 > q0) {
             const int qw = q1 - q0;
-            const bool try16 = r16_eligible(sc, qw) && !(args_of(sh).dbg & 1);
+            const bool try16 = r16_eligible<SC, kChunk>(sc, qw) && !(args_of(sh).dbg & 1);
             int m = 0;
             int st = build_window(sh, B, E, lane, try16 ? kRing16 : kRing, m);
             if (st != kStOk) return st;
@@ -2067,6 +2284,7 @@ __device__ __forceinline__ int align_seeded(SharedState &sh, const SC &sc, const
                 }
             }
             wave_sync();
+            prof_mark(sh, lane, 0, m);
             int bi = -1;
             st = try16 ? run_dp<SC, true>(sh, sc, q + q0, qw, m, lane, cells, bi) : kStRetry32;
             if (st == kStRetry32) {
@@ -2088,12 +2306,14 @@ __device__ __forceinline__ int align_seeded(SharedState &sh, const SC &sc, const
                 st = run_dp<SC, false>(sh, sc, q + q0, qw, m, lane, cells, bi);
             }
             if (st == kStOk && bi < 0) st = kStInternal;
+            prof_mark(sh, lane, 1);
             if (st == kStOk) {
                 wave_sync();
                 __builtin_amdgcn_s_setprio(kSerialPrio);
                 st = backtrack(sh, bi, qw, m, lane);
                 __builtin_amdgcn_s_setprio(0);
             }
+            prof_mark(sh, lane, 2);
             if (lane == 0) {
                 sh.slot.desc = sh.desc_full;
                 sh.slot.xpre = sh.xpre_full;
@@ -2102,6 +2322,7 @@ __device__ __forceinline__ int align_seeded(SharedState &sh, const SC &sc, const
             }
             wave_sync();
             if (st != kStOk) return st;
+            prof_mark(sh, lane, -1);
         }
         if (x < np) {  // the pinned k-mer
             const Slot s = slot_of(sh);
@@ -2359,8 +2580,9 @@ __device__ __forceinline__ int consensus(SharedState &sh, int n, uint8_t *out, i
 
 // SEEDED: the launch holds only -S groups (align_seeded); the unseeded instantiation carries none of
 // that code, so the hot DP keeps its register allocation.
-template <class SC, bool SEEDED>
+template <class SC, bool SEEDED, int RW>
 __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
+    static_assert(RW == kChunk || (RW == kWideRing && !SEEDED), "wide rings: unseeded launches");
     __shared__ SharedState sh;
     const int lane = lane_id();
     if (lane == 0) sh.args = ka;
@@ -2498,8 +2720,10 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                     if (st != kStOk) break;
                     wave_sync();
                     __builtin_amdgcn_s_setprio(kSerialPrio);
+                    prof_mark(sh, lane, -1);
                     st = update_graph(sh, q, qlen, n, ng, lane);
                     wave_sync();
+                    prof_mark(sh, lane, 3);
                     if (st != kStOk) break;
                     {  // this read's node per position: the next read's anchors resolve through it
                         const Slot s = slot_of(sh);
@@ -2511,21 +2735,21 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 }
                 __builtin_amdgcn_s_setprio(kSerialPrio);
                 uint64_t t0 = prof ? clock64() : 0;
-                const bool try16 = r16_eligible(sc, qlen) && !(args_of(sh).dbg & 1);
+                const bool try16 = r16_eligible<SC, RW>(sc, qlen) && !(args_of(sh).dbg & 1);
                 build_desc(sh, n, lane, try16 ? kRing16 : kRing);
                 uint64_t t1 = prof ? clock64() : 0;
                 int bi = -1;
                 __builtin_amdgcn_s_setprio(0);
                 // 16-bit mode when the read's score range allows it; a read that leaves the safe
                 // range is re-aligned in 32-bit mode (the graph is untouched until update_graph)
-                st = try16 ? run_dp<SC, true>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
+                st = try16 ? run_dp<SC, true, RW>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
                 if (st == kStRetry32) {
                     if (prof && lane == 0) prof[15] += 1;
                     if (try16) {  // descriptors of the 32-bit ring (far / fast flags depend on its depth)
                         wave_sync();
                         build_desc(sh, n, lane, kRing);
                     }
-                    st = run_dp<SC, false>(sh, sc, q, qlen, n, lane, cells, bi);
+                    st = run_dp<SC, false, RW>(sh, sc, q, qlen, n, lane, cells, bi);
                 }
                 uint64_t t2 = prof ? clock64() : 0;
                 if (prof && lane == 0) {
@@ -2608,39 +2832,35 @@ hipError_t launch_encode(uint8_t *buf, int64_t n, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <bool SEEDED>
-static int blocks_per_cu_t(const PoaKArgs &a, bool dflt) {
-    int nb = 0;
-    hipError_t e = dflt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, poa_kernel<DefaultScores, SEEDED>, kWave, a.qlds)
-                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, poa_kernel<RuntimeScores, SEEDED>, kWave, a.qlds);
-    return e == hipSuccess ? nb : 0;
-}
-
 static bool default_scores(const PoaKArgs &a) {
     return a.match == DefaultScores::match && a.mismatch == DefaultScores::mismatch && a.o1 == DefaultScores::o1 &&
            a.e1 == DefaultScores::e1 && a.o2 == DefaultScores::o2 && a.e2 == DefaultScores::e2;
 }
 
-int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
+// the six instantiations: scores (default / runtime) x kind (narrow, wide, seeded)
+template <class F>
+static auto by_kind(const PoaKArgs &a, F &&f) {
     const bool dflt = default_scores(a);
-    int nb = a.caps.seeded ? blocks_per_cu_t<true>(a, dflt) : blocks_per_cu_t<false>(a, dflt);
+    if (a.caps.seeded) return dflt ? f(poa_kernel<DefaultScores, true, kChunk>) : f(poa_kernel<RuntimeScores, true, kChunk>);
+    if (a.caps.wide)
+        return dflt ? f(poa_kernel<DefaultScores, false, kWideRing>) : f(poa_kernel<RuntimeScores, false, kWideRing>);
+    return dflt ? f(poa_kernel<DefaultScores, false, kChunk>) : f(poa_kernel<RuntimeScores, false, kChunk>);
+}
+
+int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
+    int nb = by_kind(a, [&](auto kern) {
+        int v = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kern, kWave, poa_dyn_lds(a)) == hipSuccess ? v : 0;
+    });
     if (nb < 1) nb = 8;
     return nb < cap ? nb : cap;
 }
 
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream) {
-    const bool dflt = default_scores(a);
-    if (a.caps.seeded) {
-        if (dflt)
-            hipLaunchKernelGGL((poa_kernel<DefaultScores, true>), dim3(n_slots), dim3(kWave), a.qlds, stream, a);
-        else
-            hipLaunchKernelGGL((poa_kernel<RuntimeScores, true>), dim3(n_slots), dim3(kWave), a.qlds, stream, a);
-    } else {
-        if (dflt)
-            hipLaunchKernelGGL((poa_kernel<DefaultScores, false>), dim3(n_slots), dim3(kWave), a.qlds, stream, a);
-        else
-            hipLaunchKernelGGL((poa_kernel<RuntimeScores, false>), dim3(n_slots), dim3(kWave), a.qlds, stream, a);
-    }
+    by_kind(a, [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(n_slots), dim3(kWave), poa_dyn_lds(a), stream, a);
+        return 0;
+    });
     return hipGetLastError();
 }
 
