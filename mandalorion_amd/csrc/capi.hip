@@ -169,8 +169,8 @@ struct mando_ctx {
 namespace {
 
 constexpr int kMaxWavesPerCu = 16;  // upper bound on resident POA waves per CU
-// groups whose band 2w + 1 (at their longest read) is wider than this run in the wide-ring launch:
-// their rows mostly exceed one 128-column chunk (the band also drifts with the argmax)
+// groups whose band 2w + 1 (at their mean read length) is wider than this run in the wide-ring
+// launch: their rows mostly exceed one 128-column chunk (the band also drifts with the argmax)
 constexpr int64_t kWideBand = 112;
 #ifndef MANDO_WS_SHARE
 #define MANDO_WS_SHARE 0.8
@@ -626,10 +626,12 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
     for (int attempt = 0; attempt < 4 && !todo.empty(); ++attempt) {
         // unseeded and seeded groups run as two launches of the two kernel instantiations
         // three kinds of launch: unseeded groups with bands of one chunk, unseeded groups whose band
-        // (2w + 1 at their longest read) exceeds one chunk (the wide-ring instantiation), -S groups
+        // (2w + 1 at their mean read length) exceeds one chunk (the wide-ring instantiation), -S groups
         std::vector<int32_t> lists[3];
         for (int32_t g : todo) {
-            const int64_t w = params->band_b + (int64_t)(params->band_f * (float)gs[(size_t)g].maxlen);
+            const GroupStat &q = gs[(size_t)g];
+            const int64_t mean = q.sum / std::max<int64_t>(1, q.nreads);
+            const int64_t w = params->band_b + (int64_t)(params->band_f * (float)mean);
             lists[seeded_group(g) ? 2 : (2 * w + 1 > kWideBand ? 1 : 0)].push_back(g);
         }
         // several kinds: each runs on its own lane (stream + workspace), concurrently, after everything
@@ -647,8 +649,19 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
             HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
             for (int k = 0; k < nk - 1; ++k) HIP_TRY(hipStreamWaitEvent(ctx->lane_stream[k], ctx->ev_fork, 0));
         }
+        // the kind holding the heaviest group is enqueued first (its slots take the CUs first: a
+        // persistent launch holds them until its queue drains)
+        int korder[3] = {0, 1, 2};
+        double kcost[3] = {0, 0, 0};
+        for (int kind = 0; kind < 3; ++kind)
+            for (int32_t g : lists[kind]) {
+                const GroupStat &q = gs[(size_t)g];
+                kcost[kind] = std::max(kcost[kind], (double)(q.sum - q.first_len) * (double)q.first_len);
+            }
+        std::stable_sort(korder, korder + 3, [&](int x, int y) { return kcost[x] > kcost[y]; });
         int lane = 0;
-        for (int kind = 0; kind < 3; ++kind) {
+        for (int ki = 0; ki < 3; ++ki) {
+            const int kind = korder[ki];
             const std::vector<int32_t> &L = lists[kind];
             if (L.empty()) continue;
             hipStream_t lst = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
