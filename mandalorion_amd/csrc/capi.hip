@@ -148,12 +148,14 @@ struct mando_ctx {
     hipStream_t lane_stream[2] = {nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_lane[2] = {nullptr, nullptr};
     DevBuf lane_ws[2], lane_counter[2], lane_prof[2];
+    DevBuf boxes, lane_boxes[2];  // -S team mailboxes
     ~mando_ctx() {
         for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
                           &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx, &s_items,
                           &s_item_of, &s_n, &s_t, &s_q, &s_scratch, &s_redo, &gorder2, &g_off, &g_len, &g_rc,
                           &g_dst, &cons_txt, &o_scratch, &lane_ws[0], &lane_ws[1], &lane_counter[0],
-                          &lane_counter[1], &lane_prof[0], &lane_prof[1], &gorder_w})
+                          &lane_counter[1], &lane_prof[0], &lane_prof[1], &gorder_w, &boxes, &lane_boxes[0],
+                          &lane_boxes[1]})
             b->release();
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (int k = 0; k < 2; ++k) {
@@ -228,6 +230,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     DevBuf &ws = lane ? ctx->lane_ws[lane - 1] : ctx->ws;
     DevBuf &counter = lane ? ctx->lane_counter[lane - 1] : ctx->counter;
     DevBuf &profb = lane ? ctx->lane_prof[lane - 1] : ctx->prof;
+    DevBuf &boxb = lane ? ctx->lane_boxes[lane - 1] : ctx->boxes;
     mando::PoaKArgs a{};
     if (sp) {
         a.par_item = sp->par_item;
@@ -269,19 +272,35 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
     const int per_cu = mando::poa_blocks_per_cu(a, cap);
-    int64_t slots = std::min<int64_t>(n_groups, (int64_t)ctx->n_cu * per_cu);
-    while (slots > 1 && (size_t)(slots * a.slot_bytes) > budget) slots /= 2;
+    // -S teams: when the seeded groups are too few to fill the resident waves, each gets a team of
+    // up to kMaxTeam one-wave workgroups that align a read's windows side by side
+    int team = 1;
+    if (sp) {
+        const int64_t resident = (int64_t)ctx->n_cu * per_cu;
+        team = (int)std::max<int64_t>(1, std::min<int64_t>(mando::kMaxTeam, resident / std::max<int64_t>(1, n_groups)));
+        if (const char *ev = getenv("MANDO_TEAM")) team = std::max(1, std::min(mando::kMaxTeam, atoi(ev)));
+    }
+    int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, (int64_t)ctx->n_cu * per_cu / team));
+    while (teams > 1 && (size_t)(teams * team * a.slot_bytes) > budget) teams /= 2;
     if (getenv("MANDO_PROF"))
-        fprintf(stderr, "[mando prof] slot workspace %.1f MB, %lld slots (free %.1f GB, budget %.1f GB)\n",
-                a.slot_bytes / 1e6, (long long)slots, free_b / 1e9, budget / 1e9);
-    if (slots < 1) slots = 1;
-    int rc = ws.ensure((size_t)(slots * a.slot_bytes));
-    while (rc == MANDO_E_NOMEM && slots > 1) {  // memory taken by others since hipMemGetInfo: fewer slots
-        (void)hipGetLastError();                // clear the failed allocation's error state
-        slots /= 2;
-        rc = ws.ensure((size_t)(slots * a.slot_bytes));
+        fprintf(stderr, "[mando prof] slot workspace %.1f MB, %lld slots, team %d (free %.1f GB, budget %.1f GB)\n",
+                a.slot_bytes / 1e6, (long long)(teams * team), team, free_b / 1e9, budget / 1e9);
+    if (teams < 1) teams = 1;
+    int rc = ws.ensure((size_t)(teams * team * a.slot_bytes));
+    while (rc == MANDO_E_NOMEM && teams > 1) {  // memory taken by others since hipMemGetInfo: fewer slots
+        (void)hipGetLastError();                 // clear the failed allocation's error state
+        teams /= 2;
+        rc = ws.ensure((size_t)(teams * team * a.slot_bytes));
     }
     if (rc) return rc;
+    const int64_t slots = teams * team;
+    a.team = team;
+    a.boxes = nullptr;
+    if (sp) {  // seeded launches run as teams (of one, when the groups fill the chip)
+        if ((rc = boxb.ensure((size_t)teams * sizeof(mando::TeamBox)))) return rc;
+        HIP_TRY(hipMemsetAsync(boxb.p, 0, (size_t)teams * sizeof(mando::TeamBox), stream));
+        a.boxes = boxb.as<mando::TeamBox>();
+    }
     rc = counter.ensure(256);
     if (rc) return rc;
     a.ws = ws.as<char>();

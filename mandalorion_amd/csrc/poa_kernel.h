@@ -146,7 +146,22 @@ struct PoaKArgs {
     const int32_t *par_n, *par_t, *par_q;
     int32_t pc, seed_k;
     int32_t dbg;             // MANDO_POA_DBG: bit 0 no 16-bit mode, bit 1 no 16-bit fast rows, bit 2 no 32-bit fast rows
+    // -S teams (seeded launches): a.team consecutive one-wave workgroups share a group, member 0
+    // leading; one TeamBox per team (zeroed before the launch; team 1: a leader without helpers)
+    int32_t team;
+    struct TeamBox *boxes;
 };
+
+// A team's mailbox (see poa_kernel.hip, "-S teams").  claim = job << 40 | np << 20 | next window.
+struct alignas(64) TeamBox {
+    uint64_t claim;
+    uint32_t done;     // windows of the current job completed (relaxed agent-scope adds)
+    int32_t status;    // first failing window status of the job (0: none)
+    int64_t cells;     // DP cells of the job's windows
+    int64_t rd;        // the job's read
+    int32_t qlen, item;
+};
+constexpr int kMaxTeam = 8;
 
 // Columns a row can touch past the read: one 128-column chunk beyond `end` (<= qlen) plus slack.
 constexpr int kQPad = 132;

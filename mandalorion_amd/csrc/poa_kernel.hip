@@ -196,6 +196,12 @@ struct alignas(16) SharedState {
     int win_on, win_sink, win_pb, win_pe;
     gint *desc_full, *xpre_full, *qnode_full;
     uint64_t tmark;                 // MANDO_PROF: the last phase boundary of the -S path (prof_mark)
+    // -S team leader (seeded launches): the group / read in progress between jobs (seeded_main)
+    struct {
+        int64_t r1, rd, cells;
+        uint64_t job;
+        int g, n, ng, st, pending, active, np, item, qlen;
+    } lead;
 };
 static_assert(sizeof(BtLds) <= sizeof(DpLds), "backtrack window must fit the DP scratch");
 
@@ -651,6 +657,19 @@ __device__ __forceinline__ int build_window(SharedState &sh, int B, int E, int l
     }
     hbm_fence();
     wave_sync();
+#ifdef MANDO_TEAM_DEBUG
+    if (m == 0) {
+        int nf = 0, nb = 0;
+        for (int x = lane; x < span; x += kWave) {
+            nf += s.wf[x] != 0;
+            nb += s.wb[x] != 0;
+        }
+        nf = wave_incl_sum(nf, lane);
+        nb = wave_incl_sum(nb, lane);
+        if (lane == kWave - 1)
+            printf("[bw] block %d B %d E %d pB %d pE %d span %d wf %d wb %d ring %d\n", (int)blockIdx.x, B, E, pB, pE, span, nf, nb, ring);
+    }
+#endif
     m_out = m;
     return kStOk;
 }
@@ -2233,107 +2252,219 @@ __device__ __forceinline__ void prof_mark(SharedState &sh, int lane, int k, int 
     }
 }
 
+// One -S window x of read q (0 <= x <= np): the rows between the previous pinned k-mer's last node
+// (the source for x = 0) and anchor x's first node (the sink for x = np), aligned to the read's
+// positions between them; then anchor x's k-mer is pinned to its nodes.  Writes the read's qnode
+// entries of those positions only, so windows are independent of each other.
 template <class SC>
-__device__ __forceinline__ int align_seeded(SharedState &sh, const SC &sc, const uint8_t *q, int qlen, int n, int lane,
-                                            int64_t &cells, int64_t rd) {
-    int np = 0, item = -1, k = 0, pc = 0;
+__device__ __forceinline__ int seeded_window(SharedState &sh, const SC &sc, const uint8_t *q, int qlen, int lane,
+                                             int64_t &cells, int item, int np, int x) {
+    int k = 0, pc = 0;
     const int32_t *par_t = nullptr, *par_q = nullptr;
     {
         const PoaKArgs a = args_of(sh);
-        item = bcast0(a.par_item[rd]);
-        if (item >= 0) np = bcast0(a.par_n[item]);
-        if (np < 0) return kStInternal;
         k = a.seed_k;
         pc = a.pc;
         par_t = a.par_t;
         par_q = a.par_q;
     }
-    // MANDO_PROF phases of -S: 0 descriptors + windows, 1 dp, 2 backtrack, 5 window rows, 6 windows
-    prof_mark(sh, lane, -1);
-    build_desc(sh, n, lane, kRing);
-    wave_sync();
-    prof_mark(sh, lane, 0);
-    int B = kSrc, q0 = 0;
-    for (int x = 0; x <= np; ++x) {
-        int E = kSink, q1 = qlen, tx = 0;
-        {
-            const Slot s = slot_of(sh);
-            if (x < np) {
-                tx = bcast0(par_t[(int64_t)item * pc + x]);
-                q1 = bcast0(par_q[(int64_t)item * pc + x]);
-                E = bcast0(s.tnode[tx]);
-            }
+    int B = kSrc, q0 = 0, E = kSink, q1 = qlen, tx = 0;
+    {
+        const Slot s = slot_of(sh);
+        if (x > 0) {
+            const int tp = bcast0(par_t[(int64_t)item * pc + x - 1]);
+            B = bcast0(s.tnode[tp + k - 1]);
+            q0 = bcast0(par_q[(int64_t)item * pc + x - 1]) + k;
         }
-        if (q1 > q0) {
-            const int qw = q1 - q0;
-            const bool try16 = r16_eligible<SC, kChunk>(sc, qw) && !(args_of(sh).dbg & 1);
-            int m = 0;
-            int st = build_window(sh, B, E, lane, try16 ? kRing16 : kRing, m);
-            if (st != kStOk) return st;
-            {
-                const Slot s = slot_of(sh);
-                const int pB = bcast0(s.pos[B]), pE = bcast0(s.pos[E]);
-                if (lane == 0) {
-                    sh.slot.desc = s.wdesc;
-                    sh.slot.xpre = s.wxpre;
-                    sh.slot.qnode = sh.qnode_full + q0;
-                    sh.win_on = 1;
-                    sh.win_sink = E;
-                    sh.win_pb = pB;
-                    sh.win_pe = pE;
-                }
-            }
-            wave_sync();
-            prof_mark(sh, lane, 0, m);
-            int bi = -1;
-            st = try16 ? run_dp<SC, true>(sh, sc, q + q0, qw, m, lane, cells, bi) : kStRetry32;
-            if (st == kStRetry32) {
-                if (try16) {  // window descriptors at the 32-bit ring depth
-                    if (lane == 0) {
-                        sh.slot.desc = sh.desc_full;
-                        sh.slot.xpre = sh.xpre_full;
-                    }
-                    wave_sync();
-                    st = build_window(sh, B, E, lane, kRing, m);
-                    if (st != kStOk) return st;
-                    if (lane == 0) {
-                        const Slot s = sh.slot;
-                        sh.slot.desc = s.wdesc;
-                        sh.slot.xpre = s.wxpre;
-                    }
-                    wave_sync();
-                }
-                st = run_dp<SC, false>(sh, sc, q + q0, qw, m, lane, cells, bi);
-            }
-            if (st == kStOk && bi < 0) st = kStInternal;
-            prof_mark(sh, lane, 1);
-            if (st == kStOk) {
-                wave_sync();
-                __builtin_amdgcn_s_setprio(kSerialPrio);
-                st = backtrack(sh, bi, qw, m, lane);
-                __builtin_amdgcn_s_setprio(0);
-            }
-            prof_mark(sh, lane, 2);
-            if (lane == 0) {
-                sh.slot.desc = sh.desc_full;
-                sh.slot.xpre = sh.xpre_full;
-                sh.slot.qnode = sh.qnode_full;
-                sh.win_on = 0;
-            }
-            wave_sync();
-            if (st != kStOk) return st;
-            prof_mark(sh, lane, -1);
-        }
-        if (x < np) {  // the pinned k-mer
-            const Slot s = slot_of(sh);
-            hbm_fence();
-            for (int i = lane; i < k; i += kWave) s.qnode[q1 + i] = s.tnode[tx + i];
-            B = bcast0(s.tnode[tx + k - 1]);
-            q0 = q1 + k;
-            wave_sync();
+        if (x < np) {
+            tx = bcast0(par_t[(int64_t)item * pc + x]);
+            q1 = bcast0(par_q[(int64_t)item * pc + x]);
+            E = bcast0(s.tnode[tx]);
         }
     }
+    if (q1 > q0) {
+        const int qw = q1 - q0;
+        const bool try16 = r16_eligible<SC, kChunk>(sc, qw) && !(args_of(sh).dbg & 1);
+        int m = 0;
+        int st = build_window(sh, B, E, lane, try16 ? kRing16 : kRing, m);
+#ifdef MANDO_TEAM_DEBUG
+        {
+            const Slot s = slot_of(sh);
+            const int pB = bcast0(s.pos[B]), pE = bcast0(s.pos[E]);
+            if (lane == 0 && st != kStOk)
+                printf("[win] block %d x %d B %d E %d pB %d pE %d q0 %d q1 %d st %d\n", (int)blockIdx.x, x, B, E, pB, pE, q0, q1, st);
+        }
+#endif
+        if (st != kStOk) return st;
+        {
+            const Slot s = slot_of(sh);
+            const int pB = bcast0(s.pos[B]), pE = bcast0(s.pos[E]);
+            if (lane == 0) {
+                sh.slot.desc = s.wdesc;
+                sh.slot.xpre = s.wxpre;
+                sh.slot.qnode = sh.qnode_full + q0;
+                sh.win_on = 1;
+                sh.win_sink = E;
+                sh.win_pb = pB;
+                sh.win_pe = pE;
+            }
+        }
+        wave_sync();
+        prof_mark(sh, lane, 0, m);
+        int bi = -1;
+        st = try16 ? run_dp<SC, true>(sh, sc, q + q0, qw, m, lane, cells, bi) : kStRetry32;
+        if (st == kStRetry32) {
+            if (try16) {  // window descriptors at the 32-bit ring depth
+                if (lane == 0) {
+                    sh.slot.desc = sh.desc_full;
+                    sh.slot.xpre = sh.xpre_full;
+                }
+                wave_sync();
+                st = build_window(sh, B, E, lane, kRing, m);
+                if (st != kStOk) return st;
+                if (lane == 0) {
+                    const Slot s = sh.slot;
+                    sh.slot.desc = s.wdesc;
+                    sh.slot.xpre = s.wxpre;
+                }
+                wave_sync();
+            }
+            st = run_dp<SC, false>(sh, sc, q + q0, qw, m, lane, cells, bi);
+        }
+        if (st == kStOk && bi < 0) st = kStInternal;
+#ifdef MANDO_TEAM_DEBUG
+        if (lane == 0 && st != kStOk) printf("[win] block %d x %d dp st %d bi %d m %d qw %d\n", (int)blockIdx.x, x, st, bi, m, qw);
+#endif
+        prof_mark(sh, lane, 1);
+        if (st == kStOk) {
+            wave_sync();
+            __builtin_amdgcn_s_setprio(kSerialPrio);
+            st = backtrack(sh, bi, qw, m, lane);
+            __builtin_amdgcn_s_setprio(0);
+#ifdef MANDO_TEAM_DEBUG
+            if (lane == 0 && st != kStOk) printf("[win] block %d x %d backtrack st %d\n", (int)blockIdx.x, x, st);
+#endif
+        }
+        prof_mark(sh, lane, 2);
+        if (lane == 0) {
+            sh.slot.desc = sh.desc_full;
+            sh.slot.xpre = sh.xpre_full;
+            sh.slot.qnode = sh.qnode_full;
+            sh.win_on = 0;
+        }
+        wave_sync();
+        if (st != kStOk) return st;
+        prof_mark(sh, lane, -1);
+    }
+    if (x < np) {  // the pinned k-mer
+        const Slot s = slot_of(sh);
+        hbm_fence();
+        for (int i = lane; i < k; i += kWave) s.qnode[q1 + i] = s.tnode[tx + i];
+        wave_sync();
+    }
     return kStOk;
+}
+
+// the read's partition item and anchor count (par_n)
+__device__ __forceinline__ int seeded_item(SharedState &sh, int64_t rd, int &np) {
+    const PoaKArgs a = args_of(sh);
+    const int item = bcast0(a.par_item[rd]);
+    np = item >= 0 ? bcast0(a.par_n[item]) : 0;
+    return item;
+}
+
+// ---- -S teams -----------------------------------------------------------------------------------
+// A seeded launch can give each group a team of a.team one-wave workgroups (consecutive blockIdx,
+// member 0 leading).  The leader owns the graph (its slot), builds the read's descriptors and
+// publishes the read as a job in the team's box; every member, the leader included, then claims the
+// job's windows one at a time (CAS on the box's claim word) and aligns each with its own slot as DP
+// scratch (graph and qnode: the leader's).  The leader waits only for windows that were claimed,
+// so a team whose helpers are not resident (yet) finishes its read alone.  Hand-offs follow the
+// agent-scope release / acquire forms of cdna_hip_programming.md Guideline 16: plain stores, each
+// storing wave's s_waitcnt vmcnt(0), a release fence, s_waitcnt again, a relaxed agent-scope flag
+// (the claim word, the done counter); the other side polls relaxed, then ONE acquire, then plain
+// loads.  The box's own words are read and written only by agent-scope atomics.
+constexpr uint64_t kJobExit = 0xffffffull;
+// every wait is bounded (s_memrealtime ticks at 100 MHz): a team that stops making progress ends
+// with an internal-error status instead of holding the GPU
+constexpr uint64_t kTeamWaitTicks = 60ull * 100000000ull;
+#define MANDO_RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+__device__ __forceinline__ void team_release() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void team_acquire() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// next unclaimed window of job `job` (np anchors), or -1 when the job is exhausted or replaced.
+// Control stays wave-uniform (every lane loads the word; only the CAS itself is lane 0's): a loop
+// inside a lane-0 branch would let the compiler spill other lanes' live values under a one-lane exec.
+__device__ __forceinline__ uint64_t box_load64(uint64_t *p) {
+    return readlane64(__hip_atomic_load(p, MANDO_RLX_AGENT), 0);
+}
+__device__ __forceinline__ int box_load32(uint32_t *p) { return bcast0((int)__hip_atomic_load(p, MANDO_RLX_AGENT)); }
+__device__ __forceinline__ int team_claim(TeamBox *box, uint64_t job, int lane) {
+    for (;;) {
+        const uint64_t c = box_load64(&box->claim);
+        if ((c >> 40) != job) return -1;
+        const int np = (int)((c >> 20) & 0xfffff), nx = (int)(c & 0xfffff);
+        if (nx > np) return -1;
+        int won = 0;
+        if (lane == 0) {
+            uint64_t e = c;
+            won = __hip_atomic_compare_exchange_strong(&box->claim, &e, c + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (bcast0(won)) return nx;
+    }
+}
+
+// a claimed window is done: its qnode entries are published, then counted
+__device__ __forceinline__ void team_report(TeamBox *box, int st, int64_t cells, int lane, bool fence = true) {
+    if (lane == 0) {
+        if (cells) __hip_atomic_fetch_add(&box->cells, cells, MANDO_RLX_AGENT);
+        if (st != kStOk) {
+            int z = 0;
+            __hip_atomic_compare_exchange_strong(&box->status, &z, st, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (fence) team_release();
+    if (lane == 0) __hip_atomic_fetch_add(&box->done, 1u, MANDO_RLX_AGENT);
+}
+
+// claims and aligns windows of `job` until none is left
+template <class SC>
+__device__ __forceinline__ void team_windows(SharedState &sh, const SC &sc, TeamBox *box, uint64_t job,
+                                             const uint8_t *q, int qlen, int item, int np, int lane) {
+#ifdef MANDO_TEAM_DEBUG
+    const int dbg = args_of(sh).dbg;
+    int xs = 0;
+#endif
+    for (;;) {
+#ifdef MANDO_TEAM_DEBUG
+        int x;
+        if (dbg & 32) x = xs <= np ? xs++ : -1;
+        else x = team_claim(box, job, lane);
+#else
+        const int x = team_claim(box, job, lane);
+#endif
+        if (x < 0) break;
+        int64_t wc = 0;
+        const int st = seeded_window(sh, sc, q, qlen, lane, wc, item, np, x);
+#ifdef MANDO_TEAM_DEBUG
+        if (lane == 0 && st != kStOk) printf("[team] block %d window %d/%d status %d\n", (int)blockIdx.x, x, np, st);
+#endif
+#ifdef MANDO_TEAM_DEBUG
+        team_report(box, st, wc, lane, !(dbg & 16));
+#else
+        team_report(box, st, wc, lane);
+#endif
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2578,8 +2709,270 @@ __device__ __forceinline__ int consensus(SharedState &sh, int n, uint8_t *out, i
     return l <= cap ? kStOk : kStCap;
 }
 
-// SEEDED: the launch holds only -S groups (align_seeded); the unseeded instantiation carries none of
-// that code, so the hot DP keeps its register allocation.
+// SEEDED: the launch holds only -S groups (seeded_main: teams of workgroups over a read's windows);
+// the unseeded instantiations carry none of that code, so the hot DP keeps its register allocation.
+// ---- the seeded launch's main loop ---------------------------------------------------------------
+// Every member of a team runs the same loop, so a window is aligned at one place in the code:
+// member 0 first advances the team's group (leader_advance: the serial work between two reads, then
+// the next read's descriptors and its job), then every member claims the job's windows
+// (team_windows).  The leader's state between jobs lives in LDS (sh.lead).
+__device__ __forceinline__ int64_t read_len(SharedState &sh, int64_t rd, const uint8_t *&q) {
+    const PoaKArgs a = args_of(sh);
+    const int64_t o0 = uni64(a.seq_off[rd]);
+    q = a.seq + o0;
+    return uni64(a.seq_off[rd + 1]) - o0;
+}
+
+// leader: finishes the job in flight (wait, graph update), moves to the next read or group and
+// publishes its job; returns 0 when the queue is empty (the helpers have been told to stop)
+template <class SC>
+__device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int lane) {
+    __builtin_amdgcn_s_setprio(kSerialPrio);
+    for (;;) {
+        if (bcast0(sh.lead.pending)) {  // every window of the job has been claimed: wait for the rest
+            const int np = bcast0(sh.lead.np);
+            int late = 0;
+            {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                while (box_load32(&box->done) != np + 1) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > kTeamWaitTicks) {
+                        late = 1;
+                        break;
+                    }
+                }
+            }
+            team_acquire();
+            wave_sync();
+            int st = 0;
+            int64_t c = 0;
+            if (lane == 0) {
+                st = late ? kStInternal : __hip_atomic_load(&box->status, MANDO_RLX_AGENT);
+                c = __hip_atomic_load(&box->cells, MANDO_RLX_AGENT);
+            }
+            st = bcast0(st);
+            const int64_t cells = uni64(readlane64(c, 0));
+            const int64_t rd = uni64(sh.lead.rd);
+            int n = bcast0(sh.lead.n), ng = bcast0(sh.lead.ng);
+            if (st == kStOk) {
+                const uint8_t *q;
+                const int qlen = (int)read_len(sh, rd, q);
+                prof_mark(sh, lane, -1);
+                st = update_graph(sh, q, qlen, n, ng, lane);
+                wave_sync();
+                prof_mark(sh, lane, 3);
+                if (st == kStOk) {  // this read's node per position: the next read's anchors resolve through it
+                    const Slot s = slot_of(sh);
+                    hbm_fence();
+                    for (int t = lane; t < qlen; t += kWave) s.tnode[t] = s.qtgt[t];
+                }
+            }
+            if (lane == 0) {
+                sh.lead.pending = 0;
+                sh.lead.st = st;
+                sh.lead.n = n;
+                sh.lead.ng = ng;
+                sh.lead.cells += cells;
+                sh.lead.rd = rd + 1;
+            }
+            wave_sync();
+        }
+        if (bcast0(sh.lead.active)) {  // the group's next read, or its end
+            int st = bcast0(sh.lead.st);
+            int64_t rd = uni64(sh.lead.rd);
+            const int64_t r1 = uni64(sh.lead.r1);
+            if (st == kStOk) {
+                const uint8_t *q = nullptr;
+                int64_t L = 0;
+                while (rd < r1 && (L = read_len(sh, rd, q)) <= 0) ++rd;
+                if (rd < r1) {
+                    int np = 0, item = -1;
+                    if (L > args_of(sh).caps.QC) {
+                        st = kStCap;
+                    } else {
+                        item = seeded_item(sh, rd, np);
+                        if (np < 0 || np >= (1 << 20) - 1) st = kStInternal;
+                    }
+                    if (st == kStOk) {  // publish the read as the team's next job
+                        const int n = bcast0(sh.lead.n);
+                        prof_mark(sh, lane, -1);
+                        build_desc(sh, n, lane, kRing);
+                        wave_sync();
+                        prof_mark(sh, lane, 0);
+                        const uint64_t job = sh.lead.job % 0xfffffeull + 1;
+                        if (lane == 0) {  // every earlier job is done: nobody else writes the box now
+                            __hip_atomic_store(&box->rd, rd, MANDO_RLX_AGENT);
+                            __hip_atomic_store(&box->qlen, (int)L, MANDO_RLX_AGENT);
+                            __hip_atomic_store(&box->item, item, MANDO_RLX_AGENT);
+                            __hip_atomic_store(&box->cells, (int64_t)0, MANDO_RLX_AGENT);
+                            __hip_atomic_store(&box->status, 0, MANDO_RLX_AGENT);
+                            __hip_atomic_store(&box->done, 0u, MANDO_RLX_AGENT);
+                        }
+                        team_release();  // the descriptors, tnode and the job's words, then the claim word
+                        if (lane == 0) {
+                            __hip_atomic_store(&box->claim, (job << 40) | ((uint64_t)np << 20), MANDO_RLX_AGENT);
+                            sh.lead.job = job;
+                            sh.lead.pending = 1;
+                            sh.lead.np = np;
+                            sh.lead.item = item;
+                            sh.lead.qlen = (int)L;
+                            sh.lead.rd = rd;
+                        }
+                        wave_sync();
+                        return 1;
+                    }
+                }
+            }
+            // the group is done (every read aligned, or a failure)
+            int clen = 0;
+            const int g = bcast0(sh.lead.g);
+            if (st == kStOk) {
+                const PoaKArgs a = args_of(sh);
+                int64_t *prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
+                const uint64_t t6 = prof ? clock64() : 0;
+                const int n = bcast0(sh.lead.n);
+                int cst = kStOk, len = 0;
+                if (lane == 0) {
+                    const int64_t cap = a.cons_off[g + 1] - a.cons_off[g];
+                    cst = consensus(sh, n, a.cons + a.cons_off[g], cap, len);
+                }
+                st = bcast0(cst);
+                clen = bcast0(len);
+                if (prof && lane == 0) prof[4] += (int64_t)(clock64() - t6);
+            }
+            if (lane == 0) {
+                const PoaKArgs a = args_of(sh);
+                a.status[g] = st;
+                a.cons_len[g] = clen;
+                a.cells[g] = sh.lead.cells;
+                sh.lead.active = 0;
+            }
+            wave_sync();
+            continue;
+        }
+        // the next group from the launch's queue
+        int gi = 0;
+        {
+            const PoaKArgs a = args_of(sh);
+            if (lane == 0) gi = atomicAdd(a.counter, 1);
+            gi = bcast0(gi);
+            if (gi >= a.n_groups) {
+                if (lane == 0) __hip_atomic_store(&box->claim, kJobExit << 40, MANDO_RLX_AGENT);
+                return 0;
+            }
+        }
+        int g;
+        int64_t r0, r1;
+        {
+            const PoaKArgs a = args_of(sh);
+            g = a.gorder ? bcast0(a.gorder[gi]) : gi;
+            r0 = uni64(a.grp_off[g]);
+            r1 = uni64(a.grp_off[g + 1]);
+        }
+        if (lane == 0) {
+            sh.slot.order = sh.order0;
+            sh.slot.order2 = sh.order1;
+        }
+        wave_sync();
+        int64_t first = r0;
+        const uint8_t *q0 = nullptr;
+        int64_t L0 = 0;
+        while (first < r1 && (L0 = read_len(sh, first, q0)) <= 0) ++first;
+        int st = kStOk, n = 0;
+        if (first < r1) {
+            st = init_chain(sh, q0, (int)L0, lane, n);
+            if (st == kStOk) {  // the chain's node of every position (init_chain: 2 + t)
+                const Slot s = slot_of(sh);
+                for (int t = lane; t < (int)L0; t += kWave) s.tnode[t] = 2 + t;
+            }
+            wave_sync();
+        }
+        if (lane == 0) {
+            if (first < r1) {
+                sh.lead.r1 = r1;
+                sh.lead.rd = first + 1;
+                sh.lead.cells = 0;
+                sh.lead.g = g;
+                sh.lead.n = n;
+                sh.lead.ng = 0;
+                sh.lead.st = st;
+                sh.lead.pending = 0;
+                sh.lead.active = 1;
+            } else {  // no read: an empty consensus
+                const PoaKArgs a = args_of(sh);
+                a.status[g] = kStOk;
+                a.cons_len[g] = 0;
+                a.cells[g] = 0;
+            }
+        }
+        wave_sync();
+    }
+}
+
+template <class SC>
+__device__ __forceinline__ void seeded_main(SharedState &sh, TeamBox *box, int member, int lane) {
+    SC sc;
+    if constexpr (!std::is_same<SC, DefaultScores>::value) {
+        const PoaKArgs a = args_of(sh);
+        sc = SC{a.match, a.mismatch, a.o1, a.e1, a.o2, a.e2};
+    }
+    if (lane == 0) {
+        sh.lead.job = 0;
+        sh.lead.pending = 0;
+        sh.lead.active = 0;
+    }
+    wave_sync();
+    uint64_t last = 0;
+    for (;;) {
+        uint64_t job = 0;
+        int64_t rd = 0;
+        int qlen = 0, item = 0, np = 0;
+        if (member == 0) {
+            if (!leader_advance<SC>(sh, box, lane)) return;
+            job = (uint64_t)uni64((int64_t)sh.lead.job);
+            rd = uni64(sh.lead.rd);
+            qlen = bcast0(sh.lead.qlen);
+            item = bcast0(sh.lead.item);
+            np = bcast0(sh.lead.np);
+        } else {
+            uint64_t c = 0;
+            {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    c = box_load64(&box->claim);
+                    const uint64_t j = c >> 40;
+                    if (j == kJobExit || (j != 0 && j != last && (c & 0xfffff) <= ((c >> 20) & 0xfffff))) break;
+                    __builtin_amdgcn_s_sleep(4);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > kTeamWaitTicks) {
+                        c = kJobExit << 40;  // the leader is gone: stop
+                        break;
+                    }
+                }
+            }
+            job = c >> 40;
+            if (job == kJobExit) return;
+            np = (int)((c >> 20) & 0xfffff);
+            team_acquire();
+            if (lane == 0) {
+                rd = __hip_atomic_load(&box->rd, MANDO_RLX_AGENT);
+                qlen = __hip_atomic_load(&box->qlen, MANDO_RLX_AGENT);
+                item = __hip_atomic_load(&box->item, MANDO_RLX_AGENT);
+            }
+            rd = uni64((int64_t)readlane64((uint64_t)rd, 0));
+            qlen = bcast0(qlen);
+            item = bcast0(item);
+        }
+        const uint8_t *q;
+        {
+            const PoaKArgs a = args_of(sh);
+            q = a.seq + uni64(a.seq_off[rd]);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        team_windows(sh, sc, box, job, q, qlen, item, np, lane);
+        last = job;
+    }
+}
+
 template <class SC, bool SEEDED, int RW>
 __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
     static_assert(RW == kChunk || (RW == kWideRing && !SEEDED), "wide rings: unseeded launches");
@@ -2588,27 +2981,35 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
     if (lane == 0) sh.args = ka;
     wave_sync();
     const PoaKArgs &a = ka;
+    // -S teams: helpers (member > 0) read the graph from the team leader's slot and keep their own DP
+    // scratch (window descriptors, row records, traceback, spills)
+    int member = 0, team = 1;
+    if constexpr (SEEDED) {
+        team = a.team > 1 ? a.team : 1;
+        member = (int)(blockIdx.x % (unsigned)team);
+    }
     char *ws = a.ws + (int64_t)blockIdx.x * a.slot_bytes;
+    char *gw = ws - (int64_t)member * a.slot_bytes;
     Slot s;
-    s.base = (gu8 *)(ws + a.lay.base);
-    s.gid = (gint *)(ws + a.lay.gid);
-    s.gtab = (gint *)(ws + a.lay.gtab);
-    s.in_n = (gint *)(ws + a.lay.in_n);
-    s.out_n = (gint *)(ws + a.lay.out_n);
-    s.in_id = (gint *)(ws + a.lay.in_id);
-    s.out_id = (gint *)(ws + a.lay.out_id);
-    s.out_w = (gint *)(ws + a.lay.out_w);
-    s.sink_in = (gint *)(ws + a.lay.sink_in);
-    s.src_out = (gint *)(ws + a.lay.src_out);
-    s.src_out_w = (gint *)(ws + a.lay.src_out_w);
-    s.pos = (gint *)(ws + a.lay.pos);
-    s.remrow = (gint *)(ws + a.lay.remrow);
-    s.desc = (gint *)(ws + a.lay.desc);
+    s.base = (gu8 *)(gw + a.lay.base);
+    s.gid = (gint *)(gw + a.lay.gid);
+    s.gtab = (gint *)(gw + a.lay.gtab);
+    s.in_n = (gint *)(gw + a.lay.in_n);
+    s.out_n = (gint *)(gw + a.lay.out_n);
+    s.in_id = (gint *)(gw + a.lay.in_id);
+    s.out_id = (gint *)(gw + a.lay.out_id);
+    s.out_w = (gint *)(gw + a.lay.out_w);
+    s.sink_in = (gint *)(gw + a.lay.sink_in);
+    s.src_out = (gint *)(gw + a.lay.src_out);
+    s.src_out_w = (gint *)(gw + a.lay.src_out_w);
+    s.pos = (gint *)(gw + a.lay.pos);
+    s.remrow = (gint *)(gw + a.lay.remrow);
+    s.desc = (gint *)(gw + a.lay.desc);
     s.rinfo = (gint *)(ws + a.lay.rinfo);
     s.tb = (gu8 *)(ws + a.lay.tb);
     s.kp = (gu8 *)(ws + a.lay.kp);
     s.sv = (gint *)(ws + a.lay.sv);
-    s.qnode = (gint *)(ws + a.lay.qnode);
+    s.qnode = (gint *)(gw + a.lay.qnode);
     s.qtgt = (gint *)(ws + a.lay.qtgt);
     s.qflag = (gint *)(ws + a.lay.qflag);
     s.qnb = (gint *)(ws + a.lay.qnb);
@@ -2620,14 +3021,14 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
     s.nxt = (gint *)(ws + a.lay.nxt);
     s.order = (gint *)(ws + a.lay.order0);
     s.order2 = (gint *)(ws + a.lay.order1);
-    s.xpre = (gint *)(ws + a.lay.xpre);
+    s.xpre = (gint *)(gw + a.lay.xpre);
     s.wdesc = (gint *)(ws + a.lay.wdesc);
     s.wxpre = (gint *)(ws + a.lay.wxpre);
     s.wmap = (gint *)(ws + a.lay.wmap);
     s.wlist = (gint *)(ws + a.lay.wlist);
     s.wf = (gint *)(ws + a.lay.wf);
     s.wb = (gint *)(ws + a.lay.wb);
-    s.tnode = (gint *)(ws + a.lay.tnode);
+    s.tnode = (gint *)(gw + a.lay.tnode);
     if (lane == 0) {
         sh.slot = s;
         sh.order0 = s.order;
@@ -2639,8 +3040,15 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
         sh.desc_full = s.desc;
         sh.xpre_full = s.xpre;
         sh.qnode_full = s.qnode;
+        sh.tmark = clock64();
     }
     wave_sync();
+
+    if constexpr (SEEDED) {
+        if (member > 0 && (a.dbg & 8)) return;  // MANDO_POA_DBG bit 3: helpers absent (leaders align alone)
+        seeded_main<SC>(sh, a.boxes + blockIdx.x / (unsigned)team, member, lane);
+        return;
+    } else {
 
     // Nothing of the kernel arguments or the slot stays live across the loop: every phase re-reads
     // what it needs from LDS (args_of / slot_of), which keeps SGPRs free for the DP row loop.
@@ -2675,7 +3083,6 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
             first = uni64(first);
         }
         int clen = 0;
-        constexpr bool seeded = SEEDED;
         if (first < r1) {
             {
                 const PoaKArgs a = args_of(sh);
@@ -2683,10 +3090,6 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 const uint8_t *q0 = a.seq + o0;
                 const int L0 = (int)(uni64(a.seq_off[first + 1]) - o0);
                 st = init_chain(sh, q0, L0, lane, n);
-                if (seeded && st == kStOk) {  // the chain's node of every position (init_chain: 2 + t)
-                    const Slot s = slot_of(sh);
-                    for (int t = lane; t < L0; t += kWave) s.tnode[t] = 2 + t;
-                }
             }
             wave_sync();
             for (int64_t rd = first + 1; rd < r1 && st == kStOk; ++rd) {
@@ -2713,26 +3116,6 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 // The serial, latency-bound phases (descriptors, backtrack, graph update, consensus) issue
                 // ahead of the co-resident waves' DP rows (s_setprio 1; the DP runs at 0): those waves
                 // return to their DP sooner, the SIMD's issue slots stay busy (config-3 kernel -3.5 %).
-                if constexpr (SEEDED) {
-                    // -S: windows between the seed kernel's anchors, then the whole read's update
-                    __builtin_amdgcn_s_setprio(kSerialPrio);
-                    st = align_seeded(sh, sc, q, qlen, n, lane, cells, rd);
-                    if (st != kStOk) break;
-                    wave_sync();
-                    __builtin_amdgcn_s_setprio(kSerialPrio);
-                    prof_mark(sh, lane, -1);
-                    st = update_graph(sh, q, qlen, n, ng, lane);
-                    wave_sync();
-                    prof_mark(sh, lane, 3);
-                    if (st != kStOk) break;
-                    {  // this read's node per position: the next read's anchors resolve through it
-                        const Slot s = slot_of(sh);
-                        hbm_fence();
-                        for (int t = lane; t < qlen; t += kWave) s.tnode[t] = s.qtgt[t];
-                    }
-                    wave_sync();
-                    continue;
-                }
                 __builtin_amdgcn_s_setprio(kSerialPrio);
                 uint64_t t0 = prof ? clock64() : 0;
                 const bool try16 = r16_eligible<SC, RW>(sc, qlen) && !(args_of(sh).dbg & 1);
@@ -2800,6 +3183,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
         }
         wave_sync();
     }
+    }  // unseeded launches
 }
 
 // ASCII -> 0..4, 16 bytes per thread (HBM-bound streaming map)

@@ -100,6 +100,16 @@ def test_seeded_groups_mixed_with_unseeded():
     _check(groups, seeding=seeding)
 
 
+@pytest.mark.parametrize("team", ["1", "3", "8"])
+def test_seeded_team_sizes(monkeypatch, team):
+    """-S teams (poa_kernel.hip "-S teams"): a read's windows aligned by 1 (solo), 3 or 8 workgroups
+    give the same consensi; 10 seeded groups share the launch with two unseeded ones."""
+    monkeypatch.setenv("MANDO_TEAM", team)
+    _, long_g = poa_cases.noisy_groups(10, (7000, 9000), (6, 14), seed=71)
+    _, short_g = poa_cases.noisy_groups(2, (500, 900), (3, 6), seed=72)
+    _check(long_g + short_g, seeding=[1] * 10 + [0, 0])
+
+
 def test_seeded_32bit_rows(monkeypatch):
     monkeypatch.setenv("MANDO_POA_DBG", "1")
     _check(poa_cases.noisy_groups(3, (6000, 8000), (5, 10), seed=64)[1], seeding=[1, 1, 1])

@@ -5,12 +5,6 @@ set -e
 name=$1; flags=$2
 root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/build/$name
-mkdir -p $out/obj
-cd $root/mandalorion_amd/csrc
-H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -munsafe-fp-atomics $flags"
-objs=""
-for f in capi.hip poa_kernel.hip orient_kernel.hip; do $H -c $f -o $out/obj/$f.o & objs="$objs $out/obj/$f.o"; done
-for f in rng.cpp cluster.cpp psl.cpp sam.cpp module_f.cpp; do $H -x c++ -c $f -o $out/obj/$f.o & objs="$objs $out/obj/$f.o"; done
-wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/libmando.so $objs -lpthread -lz
+mkdir -p $out
+make -s -j8 -C $root/mandalorion_amd/csrc OUT=$out "HIPFLAGS=--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -munsafe-fp-atomics $flags" $out/libmando.so
 echo "built $out/libmando.so"
