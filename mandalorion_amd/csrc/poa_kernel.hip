@@ -1292,7 +1292,7 @@ constexpr uint32_t kNeg2 = 0x80008000u;  // (-32768, -32768): -inf of the 16-bit
 // multiply per value)
 __device__ __forceinline__ uint32_t pk2s(int v) {
     uint32_t r;
-    asm("s_pack_ll_b32_b16 %0, %1, %1" : "=s"(r) : "s"(v));
+    asm("s_pack_ll_b32_b16 %0, %1, %1" : "=s"(r) : "s"(__builtin_amdgcn_readfirstlane(v)));
     return r;
 }
 __device__ __forceinline__ uint32_t pk_adds(uint32_t a, uint32_t b) {
@@ -1511,7 +1511,8 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
 // holding columns cb0 + 128h + 2l and +1 of half h.  The halves are computed side by side; their F
 // prefix scans are independent, and the upper half takes the lower half's total as its carry-in.
 // Ring rows of a wide launch hold only the columns their row wrote, so the predecessors' values are
-// always band-masked.  One or two predecessors (more: the generic row).
+// always band-masked.  Predecessors 2.. of a row with up to kPreInline are re-read from the LDS row
+// ring, as in row16_vec.
 template <class SC>
 __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *sv, gint *rinfo, SharedState &sh,
                                           int lane, const Row16 &R, DpState &ds) {
@@ -1565,6 +1566,26 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
             Hd = pk_max(Hd, Hd1);
             X1 = pk_max(X1, X11);
             X2 = pk_max(X2, X21);
+        }
+        for (int k = 2; k < R.pn3; ++k) {  // the first strictly larger value names the predecessor
+            const int p = bcast0(sh.desc[R.r & (kDescBatch - 1)][3 + k]);
+            const int4 xr = sh.rrow[p & (kRowRing - 1)];
+            const uint32_t Bk = pk2s(xr.x), Ek = pk2s(xr.y);
+            const uint32_t *wk = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, p & (kRing16 - 1)));
+            uint32_t Hdk = __builtin_amdgcn_alignbit(wk[iw], wk[iwp], 16);
+            uint32_t X1k = wk[HW + iw], X2k = wk[2 * HW + iw];
+            const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(Bk)) | as_u32(as_s16x2(Ek) - as_s16x2(JD)));
+            const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(Bk)) | as_u32(as_s16x2(Ek) - as_s16x2(J)));
+            Hdk = bfi(md, kNeg2, Hdk);
+            X1k = bfi(me, kNeg2, X1k);
+            X2k = bfi(me, kNeg2, X2k);
+            const uint32_t kk = pk2(k);
+            MK = bfi(pk_neg_mask(pk_subs(Hd, Hdk)), kk, MK);
+            K1 = bfi(pk_neg_mask(pk_subs(X1, X1k)), kk, K1);
+            K2 = bfi(pk_neg_mask(pk_subs(X2, X2k)), kk, K2);
+            Hd = pk_max(Hd, Hdk);
+            X1 = pk_max(X1, X1k);
+            X2 = pk_max(X2, X2k);
         }
         const uint32_t M = pk_subs(pk_adds(Hd, S), pk2(sc.mismatch));
         const uint32_t H0 = bfi(inv, kNeg2, pk_max(M, pk_max(X1, X2)));
@@ -1783,7 +1804,6 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
                 // predecessors)
                 bad = (RW - span) | (RW - 1 - (R.e0 - pc0)) | (RW - 1 - (R.e1 - pc1)) | narrowk |
                       (tb_lim - ds.tb_used) | (kp_lim - ds.kp_used) | (sv_lim - ds.sv_used);
-                if (RW != kChunk && span > kChunk) bad |= -R.pn3;
                 R.nomask = RW == kChunk && ((R.beg - 1 - pc0) | (pc0 + kChunk - 1 - R.end) | (R.beg - 1 - pc1) |
                                             (pc1 + kChunk - 1 - R.end)) >= 0;
                 R.r = r;
