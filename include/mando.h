@@ -90,6 +90,11 @@ int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const
                            int32_t *d_status);
 int mando_ctx_sync(mando_ctx *ctx);
 
+/* Gives the ctx's stream the device's highest (high != 0) or default scheduling priority: work queued
+ * on it is dispatched ahead of other streams' pending workgroups (the D pipeline's clustering and
+ * orientation streams, whose kernels would otherwise queue behind a POA grid).  Waits for the stream. */
+int mando_ctx_set_priority(mando_ctx *ctx, int high);
+
 /* Device-time of the most recent POA / orientation launch on the ctx stream, from HIP events
  * recorded around the kernel on that stream (milliseconds). */
 float mando_last_kernel_ms(mando_ctx *ctx);

@@ -25,6 +25,7 @@ EXPORTED = (
     "mando_poa_batch",
     "mando_poa_batch_device",
     "mando_ctx_sync",
+    "mando_ctx_set_priority",
     "mando_last_kernel_ms",
     "mando_last_kernel_launches",
     "mando_orient_batch",
@@ -174,6 +175,7 @@ def load(path: str | None = None):
         lib.mando_ctx_destroy.argtypes = [_P]
         lib.mando_ctx_destroy.restype = None
         lib.mando_ctx_sync.argtypes = [_P]
+        lib.mando_ctx_set_priority.argtypes = [_P, ctypes.c_int]
         lib.mando_poa_batch.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]
         lib.mando_poa_batch_device.argtypes = [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]
         lib.mando_last_kernel_ms.argtypes = [_P]
@@ -304,6 +306,13 @@ class Context:
 _ctx_cache: dict[tuple[int, int], Context] = {}
 
 
+# slots whose streams can get the high scheduling priority (MANDO_STREAM_PRIO=1): orientation (1) and
+# clustering (4), whose short kernels sit on the D pipeline's critical path between two POA grids.  Off
+# by default: measured on config 3, the clustering kernels then ran during the first POA grid (0.53 ->
+# 0.13 s) but the POA grids slowed down 2-3x while high-priority work was pending (2.40 -> 3.90 s).
+HIGH_PRIORITY_SLOTS = (1, 4)
+
+
 def context(device: int = 0, slot: int = 0) -> Context:
     """Per-(device, slot) context: each slot owns a HIP stream and its device buffers, so two host threads
     can drive the same GPU at once (the D pipeline orients chunk k+1 on slot 1 while chunk k's POA runs
@@ -311,5 +320,7 @@ def context(device: int = 0, slot: int = 0) -> Context:
     c = _ctx_cache.get((device, slot))
     if c is None or c.handle is None:
         c = Context(device)
+        if slot in HIGH_PRIORITY_SLOTS and os.environ.get("MANDO_STREAM_PRIO", "0") == "1":
+            check(c.lib.mando_ctx_set_priority(c.handle, 1))
         _ctx_cache[(device, slot)] = c
     return c

@@ -149,13 +149,14 @@ struct mando_ctx {
     hipEvent_t ev_fork = nullptr, ev_lane[2] = {nullptr, nullptr};
     DevBuf lane_ws[2], lane_counter[2], lane_prof[2];
     DevBuf boxes, lane_boxes[2];  // -S team mailboxes
+    DevBuf busy, lane_busy[2];    // one-group launches: workspace slot flags
     ~mando_ctx() {
         for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
                           &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx, &s_items,
                           &s_item_of, &s_n, &s_t, &s_q, &s_scratch, &s_redo, &gorder2, &g_off, &g_len, &g_rc,
                           &g_dst, &cons_txt, &o_scratch, &lane_ws[0], &lane_ws[1], &lane_counter[0],
                           &lane_counter[1], &lane_prof[0], &lane_prof[1], &gorder_w, &boxes, &lane_boxes[0],
-                          &lane_boxes[1]})
+                          &lane_boxes[1], &busy, &lane_busy[0], &lane_busy[1]})
             b->release();
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (int k = 0; k < 2; ++k) {
@@ -231,6 +232,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     DevBuf &counter = lane ? ctx->lane_counter[lane - 1] : ctx->counter;
     DevBuf &profb = lane ? ctx->lane_prof[lane - 1] : ctx->prof;
     DevBuf &boxb = lane ? ctx->lane_boxes[lane - 1] : ctx->boxes;
+    DevBuf &busyb = lane ? ctx->lane_busy[lane - 1] : ctx->busy;
     mando::PoaKArgs a{};
     if (sp) {
         a.par_item = sp->par_item;
@@ -301,6 +303,25 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         HIP_TRY(hipMemsetAsync(boxb.p, 0, (size_t)teams * sizeof(mando::TeamBox), stream));
         a.boxes = boxb.as<mando::TeamBox>();
     }
+    // unseeded launches run one workgroup per group by default (MANDO_POA_PERSISTENT=1: persistent
+    // slots): as groups finish, the CUs are shared with the other kernels in flight (clustering and
+    // orientation of later chunks, other POA launches) instead of being held to the launch's end
+    int64_t grid = slots;
+    a.one_group = 0;
+    if (!sp) {
+        // every resident workgroup must find a slot (a waiting one would hold its CU): one-group grids
+        // only when the workspace covers the resident waves, or the groups
+        const char *pe0 = getenv("MANDO_POA_PERSISTENT");
+        const bool enough = slots >= std::min<int64_t>(n_groups, (int64_t)ctx->n_cu * per_cu);
+        if (!(pe0 && pe0[0] == '1') && enough) {
+            a.one_group = 1;
+            a.n_slots = (int32_t)slots;
+            grid = n_groups;
+            if ((rc = busyb.ensure((size_t)slots * 4))) return rc;
+            HIP_TRY(hipMemsetAsync(busyb.p, 0, (size_t)slots * 4, stream));
+            a.slot_busy = busyb.as<int32_t>();
+        }
+    }
     rc = counter.ensure(256);
     if (rc) return rc;
     a.ws = ws.as<char>();
@@ -309,21 +330,21 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     const char *pe = getenv("MANDO_PROF");
     const bool prof = pe && pe[0] == '1';
     if (prof) {
-        rc = profb.ensure((size_t)slots * mando::kProfPhases * 8);
+        rc = profb.ensure((size_t)grid * mando::kProfPhases * 8);
         if (rc) return rc;
-        HIP_TRY(hipMemsetAsync(profb.p, 0, (size_t)slots * mando::kProfPhases * 8, stream));
+        HIP_TRY(hipMemsetAsync(profb.p, 0, (size_t)grid * mando::kProfPhases * 8, stream));
         a.prof = profb.as<int64_t>();
     }
     if (ev_start) HIP_TRY(hipEventRecord(ctx->ev0, stream));
-    HIP_TRY(mando::launch_poa(a, (int)slots, stream));
+    HIP_TRY(mando::launch_poa(a, (int)grid, stream));
     if (ev_end) HIP_TRY(hipEventRecord(ctx->ev1, stream));
     ctx->timed = true;
     if (prof) {
-        std::vector<int64_t> h((size_t)slots * mando::kProfPhases);
+        std::vector<int64_t> h((size_t)grid * mando::kProfPhases);
         HIP_TRY(hipMemcpyAsync(h.data(), profb.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         double tot[mando::kProfPhases] = {0};
-        for (int64_t s = 0; s < slots; ++s)
+        for (int64_t s = 0; s < grid; ++s)
             for (int k = 0; k < mando::kProfPhases; ++k) tot[k] += (double)h[(size_t)(s * mando::kProfPhases + k)];
         const double reads = std::max(1.0, tot[6]), rows = std::max(1.0, tot[5]);
         fprintf(stderr, "[mando prof] fast rows %.1f%%, reads re-aligned in 32-bit mode %.0f\n", 100.0 * tot[7] / rows,
@@ -529,6 +550,19 @@ void mando_ctx_destroy(mando_ctx *ctx) {
 int mando_ctx_sync(mando_ctx *ctx) {
     if (!ctx) return fail(MANDO_E_ARG, "null ctx");
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return MANDO_OK;
+}
+
+int mando_ctx_set_priority(mando_ctx *ctx, int high) {
+    if (!ctx) return fail(MANDO_E_ARG, "null ctx");
+    HIP_TRY(hipSetDevice(ctx->device));
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    (void)hipStreamDestroy(ctx->stream);
+    ctx->stream = s;
     return MANDO_OK;
 }
 

@@ -17,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <sys/stat.h>
 
 #include <sys/mman.h>
 #include <thread>
@@ -148,19 +149,29 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     }
     if (in.junctions.size() > 16) return mando::set_error(MANDO_E_ARG, "cluster: more than 16 junction motifs");
     auto res = std::make_unique<mando_cluster_result>();
-    // read every locus file into one buffer (sizes first, then parallel reads)
+    const bool timing = getenv("MANDO_CL_TIME") != nullptr;
+    const auto t_0 = std::chrono::steady_clock::now();
+    auto secs = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_0).count(); };
+    int nth = prm->threads > 0 ? prm->threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n_loci));
+    // read every locus file into one buffer: sizes first (stat, on the reader threads), then reads
     vector<int64_t> fsize((size_t)n_loci, 0), foff((size_t)n_loci + 1, 0);
     vector<int32_t> fstatus((size_t)n_loci, cl::kOk);
-    for (int64_t i = 0; i < n_loci; ++i) {
-        FILE *fh = fopen(psl_paths[i], "rb");
-        if (!fh) {
-            fsize[(size_t)i] = -1;
-            continue;
-        }
-        fseek(fh, 0, SEEK_END);
-        fsize[(size_t)i] = ftell(fh);
-        fclose(fh);
+    {
+        std::atomic<int64_t> nx{0};
+        auto sizer = [&]() {
+            for (int64_t i; (i = nx.fetch_add(256)) < n_loci;)
+                for (int64_t k = i; k < std::min<int64_t>(n_loci, i + 256); ++k) {
+                    struct stat sb;
+                    fsize[(size_t)k] = (stat(psl_paths[k], &sb) == 0 && S_ISREG(sb.st_mode)) ? (int64_t)sb.st_size : -1;
+                }
+        };
+        vector<std::thread> th;
+        for (int t = 1; t < nth; ++t) th.emplace_back(sizer);
+        sizer();
+        for (auto &t : th) t.join();
     }
+    const double t_size = secs();
     for (int64_t i = 0; i < n_loci; ++i) foff[(size_t)i + 1] = foff[(size_t)i] + std::max<int64_t>(0, fsize[(size_t)i]);
     res->text_len = (size_t)foff[(size_t)n_loci];
     res->text_p = pool().acquire(res->text_len + 64, res->text_cap);
@@ -174,8 +185,6 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     res->ctx = ctx;
     res->d_text = d_text;
     res->d_cap = d_cap;
-    int nth = prm->threads > 0 ? prm->threads : (int)std::max(1u, std::thread::hardware_concurrency());
-    nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n_loci));
     std::atomic<int64_t> next{0};
     vector<std::atomic<uint8_t>> done((size_t)n_loci);
     for (auto &d : done) d.store(0);
@@ -223,6 +232,7 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
         }
         for (auto &t : th) t.join();
     }
+    const double t_read = secs();
     in.text = res->text_p;
     in.d_text = d_text;
     in.text_len = (int64_t)res->text_len;
@@ -234,6 +244,7 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     cl::ClusterOut o;
     const int rc = cl::cluster_gpu(ctx, in, o);
     if (rc != MANDO_OK) return rc;
+    const double t_gpu = secs();
     // flatten: records in locus order, isoforms in locus then IsoDict order
     const int64_t nr = o.rec_base[(size_t)n_loci];
     res->name_off.resize((size_t)nr);
@@ -275,6 +286,9 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
             res->peak_prop.push_back(pk.prop);
         }
     }
+    if (timing)
+        fprintf(stderr, "[cluster] %lld loci, %.1f MB: sizes %.3f s, read + copy %.3f s, kernels %.3f s, flatten %.3f s\n",
+                (long long)n_loci, res->text_len / 1e6, t_size, t_read - t_size, t_gpu - t_read, secs() - t_gpu);
     *out = res.release();
     return MANDO_OK;
 }

@@ -150,6 +150,11 @@ struct PoaKArgs {
     // leading; one TeamBox per team (zeroed before the launch; team 1: a leader without helpers)
     int32_t team;
     struct TeamBox *boxes;
+    // unseeded launches, one_group: a grid of one workgroup per group (blockIdx -> gorder), each taking
+    // a free workspace slot of n_slots (slot_busy, zeroed before the launch) for its group; workgroups
+    // of other kernels get CUs as groups finish.  0: persistent slots pulling groups from `counter`.
+    int32_t one_group, n_slots;
+    int32_t *slot_busy;
 };
 
 // A team's mailbox (see poa_kernel.hip, "-S teams").  claim = job << 40 | np << 20 | next window.

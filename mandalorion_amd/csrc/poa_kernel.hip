@@ -196,6 +196,7 @@ struct alignas(16) SharedState {
     int win_on, win_sink, win_pb, win_pe;
     gint *desc_full, *xpre_full, *qnode_full;
     uint64_t tmark;                 // MANDO_PROF: the last phase boundary of the -S path (prof_mark)
+    int slot_idx;                   // this workgroup's workspace slot (one_group launches claim one)
     // -S team leader (seeded launches): the group / read in progress between jobs (seeded_main)
     struct {
         int64_t r1, rd, cells;
@@ -3008,7 +3009,29 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
         team = a.team > 1 ? a.team : 1;
         member = (int)(blockIdx.x % (unsigned)team);
     }
-    char *ws = a.ws + (int64_t)blockIdx.x * a.slot_bytes;
+    int sidx = (int)blockIdx.x;  // workspace slot
+    if constexpr (!SEEDED) {
+        if (a.one_group) {  // a free slot (at most n_slots workgroups hold one; wave-uniform loop)
+            for (int k = 0;; ++k) {
+                const int c = (int)((blockIdx.x + (unsigned)k) % (unsigned)a.n_slots);
+                int got = 0;
+                if (lane == 0) {
+                    int z = 0;
+                    got = __hip_atomic_compare_exchange_strong(a.slot_busy + c, &z, 1, __ATOMIC_RELAXED,
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (bcast0(got)) {
+                    sidx = c;
+                    break;
+                }
+                if ((k + 1) % a.n_slots == 0) __builtin_amdgcn_s_sleep(8);
+            }
+            // the slot's last user may have run on another CU: drop this CU's L1 copies of it
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    char *ws = a.ws + (int64_t)sidx * a.slot_bytes;
     char *gw = ws - (int64_t)member * a.slot_bytes;
     Slot s;
     s.base = (gu8 *)(gw + a.lay.base);
@@ -3061,6 +3084,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
         sh.xpre_full = s.xpre;
         sh.qnode_full = s.qnode;
         sh.tmark = clock64();
+        sh.slot_idx = sidx;
     }
     wave_sync();
 
@@ -3072,12 +3096,17 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
 
     // Nothing of the kernel arguments or the slot stays live across the loop: every phase re-reads
     // what it needs from LDS (args_of / slot_of), which keeps SGPRs free for the DP row loop.
-    for (;;) {
+    for (int it = 0;; ++it) {
         int gi = 0;
         {
             const PoaKArgs a = args_of(sh);
-            if (lane == 0) gi = atomicAdd(a.counter, 1);
-            gi = bcast0(gi);
+            if (a.one_group) {
+                if (it > 0) break;
+                gi = (int)blockIdx.x;
+            } else {
+                if (lane == 0) gi = atomicAdd(a.counter, 1);
+                gi = bcast0(gi);
+            }
             if (gi >= a.n_groups) break;
         }
         int g;
@@ -3202,6 +3231,12 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
             a.cells[g] = cells;
         }
         wave_sync();
+    }
+    if (ka.one_group) {  // the slot is free again (this group's stores are done first)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(ka.slot_busy + sh.slot_idx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     }  // unseeded launches
 }

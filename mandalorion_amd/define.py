@@ -72,11 +72,17 @@ def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0, info: dict |
     return poa.poa_consensus_packed(seqs, seq_off, grp_off, seeding=seeding, device=device, info=info, slot=slot)
 
 
-def _roots(out_tmp: str) -> list[str]:
+def _roots(out_tmp: str, sizes: dict | None = None) -> list[str]:
+    """Locus roots of tmp_SS (defineIsoforms.py:130-139); sizes (optional) receives each root's
+    <root>.psl size from the same directory scan."""
     roots = set()
-    for f in os.listdir(out_tmp):
-        if os.path.isfile(os.path.join(out_tmp, f)) and ".psl" in f:
-            roots.add(f.split(".psl")[0])  # chrom~start~end (a '~' in a chrom breaks the reference too)
+    with os.scandir(out_tmp) as it:
+        for e in it:
+            if ".psl" in e.name and e.is_file():
+                r = e.name.split(".psl")[0]  # chrom~start~end (a '~' in a chrom breaks the reference too)
+                roots.add(r)
+                if sizes is not None and e.name == r + ".psl":
+                    sizes[r] = e.stat().st_size
     return sorted(roots, key=lambda x: (x.split("~")[0], int(x.split("~")[1])))
 
 
@@ -248,7 +254,8 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         _, left, right, poly = gtf.parse_genome(genome_file, wl)
     if rank == 0:
         gtf.write_polya_bed(out_path + "/polyAWhiteList.bed", poly, wl)
-    roots = _roots(out_tmp)
+    root_size: dict = {}
+    roots = _roots(out_tmp, root_size)
     # shard loci over ranks: LPT on the DP-cost estimate of SURVEY.md §8(e), results regathered in root order
     mine = list(range(len(roots)))
     if world > 1:
@@ -274,11 +281,14 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     # ~30 % of the bytes: its POA starts while the rest is still being clustered, and that POA plus the
     # rest's clustering end at about the same time (measured: 1 chunk 3.70 s, 2 equal 3.97 s, 4 equal
     # 3.83 s on config 3).
-    sizes = np.array([os.path.getsize(os.path.join(out_tmp, r + ".psl")) for r in my_roots], dtype=np.int64)
+    sizes = np.array([root_size.get(r, 0) for r in my_roots], dtype=np.int64)
     fracs = None
     if n_chunks <= 0:
         n_chunks = 1 if sizes.sum() < (64 << 20) else 2
         fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.3"))] if n_chunks == 2 else None
+        if n_chunks == 2 and os.environ.get("MANDO_CHUNK_FRACS"):  # cumulative byte fractions of the cuts
+            fracs = [float(x) for x in os.environ["MANDO_CHUNK_FRACS"].split(",")]
+            n_chunks = len(fracs) + 1
     n_chunks = max(1, min(n_chunks, len(my_roots)))
     cuts = [0]
     if n_chunks > 1:
