@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <cstdio>
@@ -2325,7 +2326,11 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     G.prm = d_prm.as<Params>();
 
     // K1, re-run with the reported sizes while a locus outgrows its scratch
+    const bool timing = getenv("MANDO_CL_TIME") != nullptr;
+    const auto tk0 = std::chrono::steady_clock::now();
+    int k1_runs = 0;
     for (int attempt = 0; attempt < 3; ++attempt) {
+        ++k1_runs;
         int64_t a_tot = 0;
         for (int32_t i : run_order) {
             Locus &x = L[(size_t)i];
@@ -2355,6 +2360,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         if (!again) break;
     }
 
+    const auto tk1 = std::chrono::steady_clock::now();
     if (getenv("MANDO_CL_DEBUG"))
         for (int64_t i = 0; i < nl; ++i) {
             const Stats &x = st[(size_t)i];
@@ -2425,6 +2431,10 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         CL_TRY(hipMemcpyAsync(ho.data(), d_o.p, (size_t)o_tot, hipMemcpyDeviceToHost, s));
         if (recs) CL_TRY(hipMemcpyAsync(out.rec_text.data(), d_rec.p, (size_t)recs * 32, hipMemcpyDeviceToHost, s));
         CL_TRY(hipStreamSynchronize(s));
+        if (timing)
+            fprintf(stderr, "[cluster] K1 %.3f s (%d runs), K2 %.3f s (%zu loci)\n",
+                    std::chrono::duration<double>(tk1 - tk0).count(), k1_runs,
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - tk1).count(), k2_order.size());
         if (getenv("MANDO_CL_DEBUG"))
             for (int32_t i : k2_order) {
                 const Stats &x = st[(size_t)i];

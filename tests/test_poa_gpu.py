@@ -100,6 +100,18 @@ def test_seeded_groups_mixed_with_unseeded():
     _check(groups, seeding=seeding)
 
 
+@pytest.mark.parametrize("persistent", ["0", "1"])
+def test_grid_modes_and_launch_kinds(monkeypatch, persistent):
+    """One-group grids (a workgroup per group, workspace slots claimed from a flag array) and the
+    persistent grid give the same consensi; the batch spans the narrow (3 kb), wide (6-9 kb: 256-column
+    ring rows, 16-bit mode shifted past 6.4 kb) and 32-bit wide (> 10.1 kb) launch kinds at once."""
+    monkeypatch.setenv("MANDO_POA_PERSISTENT", persistent)
+    _, narrow = poa_cases.noisy_groups(40, (2700, 3300), (4, 12), seed=81)
+    _, wide = poa_cases.noisy_groups(4, (6000, 9000), (4, 10), seed=82)
+    _, longer = poa_cases.noisy_groups(2, (10500, 11500), (3, 5), seed=83)
+    _check(narrow + wide + longer)
+
+
 @pytest.mark.parametrize("team", ["1", "3", "8"])
 def test_seeded_team_sizes(monkeypatch, team):
     """-S teams (poa_kernel.hip "-S teams"): a read's windows aligned by 1 (solo), 3 or 8 workgroups
