@@ -310,6 +310,9 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
     }
     wsync();
 
+#ifdef MANDO_CL_PHASES
+    const uint64_t k1t1 = clock64();
+#endif
     // 2. fields 0-21 and the blocks, one record per lane
     int err = 0;
     int64_t blk_carry = 0, cov_cap = 0, ident_cap = 0;
@@ -441,6 +444,9 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
     }
     wsync();
 
+#ifdef MANDO_CL_PHASES
+    const uint64_t k1t2 = clock64();
+#endif
     // 3. per record: the cs column (field 22) up to its tab, the seq column (23) up to the next tab or
     //    the line end; cs operators compacted in text order (a wave scans 1 KB a step)
     int64_t op_carry = 0;
@@ -533,6 +539,9 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
     }
     wsync();
 
+#ifdef MANDO_CL_PHASES
+    const uint64_t k1t3 = clock64();
+#endif
     // 4. runs (cluster.cpp build_cs): one operator per lane, record by record; prefix sums give each
     //    run's first record index and genome position, advancing runs are compacted with the genome
     //    position of their first record
@@ -629,6 +638,11 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
         }
     }
 
+#ifdef MANDO_CL_PHASES
+    if (ln() == 0)
+        printf("[K1 phases] n %d ops %lld: fields %.2f cs scan %.2f runs %.2f Mcyc\n", nrec, (long long)op_carry,
+               (k1t2 - k1t1) * 1e-6, (k1t3 - k1t2) * 1e-6, (clock64() - k1t3) * 1e-6);
+#endif
     // 5. statistics for the host (scratch B sizing) and K2
     cov_cap = wsum(cov_cap);
     ident_cap = wsum(ident_cap);
@@ -790,9 +804,59 @@ __host__ __device__ inline void carve_o(uint8_t *base, const Stats &S, const Loc
 // ---------------------------------------------------------------------------------------------
 // wave sorts (bitonic, in global scratch; P a power of two >= 64)
 // ---------------------------------------------------------------------------------------------
+// The bitonic network's exchanges with partner distance j < kSortTile stay inside aligned tiles of
+// kSortTile keys, so they run in LDS (cluster_locus's dynamic LDS): a tile is loaded once, takes every
+// such pass of the current stage, and is written back; only the passes with j >= kSortTile go through
+// global memory (for 2^17 keys: 10 global passes instead of 153).
+constexpr int64_t kSortTile = 4096;
+extern __shared__ uint64_t g_sort_lds[];  // kSortTile keys
+
+__device__ void sort_tile_lds(uint64_t *a, int64_t t0, int64_t T, int64_t k, int64_t j_hi) {
+    for (int64_t i = ln(); i < T; i += 64) g_sort_lds[i] = a[t0 + i];
+    wsync();
+    for (int64_t j = j_hi; j > 0; j >>= 1) {
+        for (int64_t i = ln(); i < T; i += 64) {
+            const int64_t l = i ^ j;
+            if (l > i) {
+                const uint64_t x = g_sort_lds[i], y = g_sort_lds[l];
+                if ((x > y) == (((t0 + i) & k) == 0)) {
+                    g_sort_lds[i] = y;
+                    g_sort_lds[l] = x;
+                }
+            }
+        }
+        wsync();
+    }
+    for (int64_t i = ln(); i < T; i += 64) a[t0 + i] = g_sort_lds[i];
+    wsync();
+}
+
 __device__ void sort_u64(uint64_t *a, int64_t P) {
-    for (int64_t k = 2; k <= P; k <<= 1)
-        for (int64_t j = k >> 1; j > 0; j >>= 1) {
+    const int64_t T = P < kSortTile ? P : kSortTile;
+    // stages k <= T: every pass inside the tile
+    for (int64_t t0 = 0; t0 < P; t0 += T) {
+        for (int64_t i = ln(); i < T; i += 64) g_sort_lds[i] = a[t0 + i];
+        wsync();
+        for (int64_t k = 2; k <= T; k <<= 1)
+            for (int64_t j = k >> 1; j > 0; j >>= 1) {
+                for (int64_t i = ln(); i < T; i += 64) {
+                    const int64_t l = i ^ j;
+                    if (l > i) {
+                        const uint64_t x = g_sort_lds[i], y = g_sort_lds[l];
+                        if ((x > y) == (((t0 + i) & k) == 0)) {
+                            g_sort_lds[i] = y;
+                            g_sort_lds[l] = x;
+                        }
+                    }
+                }
+                wsync();
+            }
+        for (int64_t i = ln(); i < T; i += 64) a[t0 + i] = g_sort_lds[i];
+        wsync();
+    }
+    // stages k > T: passes j >= T in global memory, then the rest of the stage per tile in LDS
+    for (int64_t k = 2 * T; k <= P; k <<= 1) {
+        for (int64_t j = k >> 1; j >= T; j >>= 1) {
             for (int64_t i = ln(); i < P; i += 64) {
                 const int64_t l = i ^ j;
                 if (l > i) {
@@ -805,6 +869,8 @@ __device__ void sort_u64(uint64_t *a, int64_t P) {
             }
             wsync();
         }
+        for (int64_t t0 = 0; t0 < P; t0 += T) sort_tile_lds(a, t0, T, k, T >> 1);
+    }
 }
 
 // indices with a strict-weak "less"; padding entries are -1 and sort last
@@ -976,26 +1042,36 @@ struct LocusRun {
                 B.ihash[r] = h;
             }
         }
+        // records of the locus chromosome sorted by (40 hash bits, index): a name's records are
+        // adjacent and ascending, so each record's cs_of is the last same-name record after it in its
+        // run (runs of other names that share the 40 bits are skipped by the name compare)
+        const int64_t pn = pow2ge(n);
+        for (int64_t r = ln(); r < pn; r += 64)
+            B.isort[r] = (r < n && A.recs[r].same_chrom) ? ((B.ihash[r] & ~0xffffffull) | (uint64_t)r) : ~0ull;
         wsync();
+        sort_u64(B.isort, pn);
+        for (int64_t i0 = 0; i0 < n; i0 += 64) {
+            const int64_t i = i0 + ln();
+            const uint64_t k = i < n ? B.isort[i] : ~0ull;
+            if (k != ~0ull) {
+                const int r = (int)(k & 0xffffffu);
+                const Rec &R = A.recs[r];
+                int32_t of = r;
+                for (int64_t j = i + 1; j < n; ++j) {
+                    const uint64_t kj = B.isort[j];
+                    if (kj == ~0ull || (kj >> 24) != (k >> 24)) break;
+                    const int q = (int)(kj & 0xffffffu);
+                    const Rec &K = A.recs[q];
+                    if (K.name_len == R.name_len && bytes_eq(T + K.name_off, T + R.name_off, R.name_len)) of = q;
+                }
+                A.recs[r].cs_of = of;
+            }
+        }
         for (int r0 = 0; r0 < n; r0 += 64) {
             const int r = r0 + ln();
-            int32_t of = -1;
-            if (r < n && A.recs[r].same_chrom) {
-                const Rec &R = A.recs[r];
-                const uint64_t h = B.ihash[r];
-                of = r;
-                for (int k = n - 1; k > r; --k) {
-                    if (B.ihash[k] != h) continue;
-                    const Rec &K = A.recs[k];
-                    if (!K.same_chrom || K.name_len != R.name_len) continue;
-                    if (bytes_eq(T + K.name_off, T + R.name_off, R.name_len)) {
-                        of = k;
-                        break;
-                    }
-                }
-            }
-            if (r < n) A.recs[r].cs_of = of;
+            if (r < n && !A.recs[r].same_chrom) A.recs[r].cs_of = -1;
         }
+        wsync();
         // coverage bins per record: myround over each block at stride 10 plus the block's tail, sorted
         // and made unique (cov_set)
         int64_t carry = 0, lo = INT64_MAX, hi = INT64_MIN;
@@ -2086,20 +2162,40 @@ struct LocusRun {
         }
         for (int i = ln(); i < n_ann_of(L); i += 64) B.ann[i] = G.ann_pos[L.ann_off[0] + i];
         wsync();
+#ifdef MANDO_CL_PHASES  // dev build: cycles per K2 phase of each locus
+        uint64_t ph[8];
+#define MANDO_PH(i) ph[i] = clock64()
+#else
+#define MANDO_PH(i)
+#endif
+        MANDO_PH(0);
         collect();
         if (status != kOk) return;
+        MANDO_PH(1);
         genome_bins(0);
         if (status != kOk) return;
         genome_bins(1);
         if (status != kOk) return;
+        MANDO_PH(2);
         find_peaks(0);
         if (status != kOk) return;
         find_peaks(1);
         if (status != kOk) return;
+        MANDO_PH(3);
         splice_dict();
         sort_reads();
+        MANDO_PH(4);
         identities();
+        MANDO_PH(5);
         start_end_sites();
+        MANDO_PH(6);
+#ifdef MANDO_CL_PHASES
+        if (ln() == 0)
+            printf("[K2 phases] n %d: collect %.2f bins %.2f peaks %.2f dict+sort %.2f identities %.2f ends %.2f Mcyc\n", n,
+                   (ph[1] - ph[0]) * 1e-6, (ph[2] - ph[1]) * 1e-6, (ph[3] - ph[2]) * 1e-6, (ph[4] - ph[3]) * 1e-6,
+                   (ph[5] - ph[4]) * 1e-6, (ph[6] - ph[5]) * 1e-6);
+#endif
+#undef MANDO_PH
     }
 };
 
@@ -2150,7 +2246,7 @@ hipError_t launch_parse(const Args &a, int n_blocks, hipStream_t s) {
 }
 hipError_t launch_locus(const Args &a, int n_blocks, hipStream_t s) {
     if (n_blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(cluster_locus, dim3(n_blocks), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(cluster_locus, dim3(n_blocks), dim3(64), kSortTile * 8, s, a);
     return hipGetLastError();
 }
 int64_t b_bytes(const Stats &S, const Locus &L, int w) {
