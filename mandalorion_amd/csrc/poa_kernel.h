@@ -182,7 +182,10 @@ inline int poa_qlds_bytes(int64_t max_len) {
 int poa_blocks_per_cu(const PoaKArgs &a, int cap);
 
 // dynamic LDS of a launch: the read's nibbles, plus the wide ring in a wide launch
-inline int poa_dyn_lds(const PoaKArgs &a) { return a.qlds + (a.caps.wide ? kWideRingBytes : 0); }
+inline int poa_dyn_lds(const PoaKArgs &a) {
+    // a wide launch's backtrack windows use 16 KB of it (poa_kernel.hip bt_tb_win / bt_kp_win)
+    return a.caps.wide ? (a.qlds + kWideRingBytes > 16384 ? a.qlds + kWideRingBytes : 16384) : a.qlds;
+}
 
 // Launch the persistent POA kernel on `stream` with `n_slots` one-wave workgroups.
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream);

@@ -220,6 +220,19 @@ __device__ __forceinline__ short *ring16_row(const SharedState &sh, int row) {
     if constexpr (RW == kChunk) return const_cast<short *>(&sh.dp.ring16[row][0][0]);
     else return reinterpret_cast<short *>(g_qnib) + row * 3 * RW;
 }
+// backtrack windows: the traceback bytes in the static BtLds and the predecessor bytes in the read's
+// buffer; a wide launch's ring is dead during the backtrack, so its windows are twice / four times as
+// large there (predecessor bytes [0, 8 KB), traceback bytes [8 KB, 16 KB) of the dynamic LDS)
+template <int RW>
+__device__ __forceinline__ constexpr int bt_tb_win() { return RW == kChunk ? 4096 : 8192; }
+template <int RW>
+__device__ __forceinline__ constexpr int bt_kp_win() { return RW == kChunk ? 2048 : 8192; }
+template <int RW>
+__device__ __forceinline__ uint8_t *bt_tb(const SharedState &sh) {
+    if constexpr (RW == kChunk) return const_cast<uint8_t *>(sh.bt.tb);
+    else return g_qnib + bt_kp_win<RW>();
+}
+
 template <int RW>
 __device__ __forceinline__ int *ring32_row(const SharedState &sh, int row) {
     if constexpr (RW == kChunk) return const_cast<int *>(&sh.dp.ring[row][0][0]);
@@ -1985,7 +1998,9 @@ struct BtWin {
     int lo, hi, glob;  // rows [lo, hi] are in the window; glob: single row read from HBM
 };
 
+template <int RW>
 __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i, int lane, BtWin &w, int kpwin) {
+    constexpr int kTbWinR = bt_tb_win<RW>(), kKpWinR = bt_kp_win<RW>();
     const int rr = i - lane;
     const bool valid = rr >= 0;
     int4 ra = make_int4(0, -1, 0, 0), rb = make_int4(0, 0, 0, 0), da = make_int4(0, 0, 0, 0),
@@ -2008,7 +2023,7 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
     const unsigned long long mm = __ballot(multi);
     const int fm = mm ? __ffsll((long long)mm) - 1 : 0;
     const int KE = readlane(kend, fm);
-    const bool fit = valid && TE - (tstart & ~15) <= kTbWin && (!multi || KE - (kstart & ~15) <= kpwin);
+    const bool fit = valid && TE - (tstart & ~15) <= kTbWinR && (!multi || KE - (kstart & ~15) <= kpwin);
     const unsigned long long nf = ~__ballot(fit);
     const int cnt = nf ? __ffsll((long long)nf) - 1 : kWave;
     int *md = &sh.bt.md[lane][0];
@@ -2035,7 +2050,7 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
     const int ks16 = readlane(kstart, lm) & ~15;
     const int tsz = TE - rs16, ksz = mw ? KE - ks16 : 0;
     // wide copies: all loads first, then the LDS stores (one HBM round trip)
-    constexpr int kTU = kTbWin / (16 * kWave), kKU = kKpWinMax / (16 * kWave);
+    constexpr int kTU = kTbWinR / (16 * kWave), kKU = kKpWinR / (16 * kWave);
     const GLB int4 *tg = reinterpret_cast<const GLB int4 *>(s.tb + rs16);
     const GLB int4 *kg = reinterpret_cast<const GLB int4 *>(s.kp + ks16);
     int4 tv[kTU], kv[kKU];
@@ -2049,7 +2064,7 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
         const int x = u * kWave + lane;
         if (x * 16 < ksz) kv[u] = make_int4(kg[x].x, kg[x].y, kg[x].z, kg[x].w);
     }
-    int4 *tl = reinterpret_cast<int4 *>(sh.bt.tb);
+    int4 *tl = reinterpret_cast<int4 *>(bt_tb<RW>(sh));
     int4 *kl = reinterpret_cast<int4 *>(g_qnib);
 #pragma unroll
     for (int u = 0; u < kTU; ++u) {
@@ -2110,8 +2125,10 @@ __device__ __forceinline__ void bt_step_global(const PoaKArgs &a, const Slot &s,
 
 // One walk step from the LDS window, branch-free (every lane computes the same step).  A step that
 // cannot be served from the window sets `stall` and changes nothing; finished walks are no-ops.
+template <int RW>
 __device__ __forceinline__ void bt_step_lds(const SharedState &sh, const Slot &s, int wlo, int whi, int &i,
                                             int &j, int &st, int &stall) {
+    const uint8_t *tbw = bt_tb<RW>(sh);
     const bool live = i > 0 && j > 0 && !stall;
     const bool inwin = i >= wlo;
     const int idx = min(max(whi - i, 0), kWave - 1);
@@ -2119,7 +2136,7 @@ __device__ __forceinline__ void bt_step_lds(const SharedState &sh, const Slot &s
     const int4 m1 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][4]);
     const int woff = m0.x, kof = m0.y, node = m0.z;
     const int tix = max(woff + j, 1);
-    const int t = sh.bt.tb[tix], tprev = sh.bt.tb[tix - 1];
+    const int t = tbw[tix], tprev = tbw[tix - 1];
     const bool multi = kof != kKpNone;
     const int kix = multi ? kof + 3 * j : 0;
     const int k0 = g_qnib[kix], k1 = g_qnib[kix + 1], k2 = g_qnib[kix + 2];
@@ -2144,6 +2161,7 @@ __device__ __forceinline__ void bt_step_lds(const SharedState &sh, const Slot &s
     st = go ? nst : st;
 }
 
+template <int RW>
 __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int n, int lane) {
     const PoaKArgs a = args_of(sh);
     Slot s = slot_of(sh);
@@ -2152,7 +2170,8 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
     int guard = (2 * (n + qlen) + 8) / kUnroll + 2 * (n + qlen) + 8;
     BtWin w{1, 0, 0};
     int glob_row = -1;
-    const int kpwin = min(kKpWinMax, a.qlds & ~15);  // predecessor bytes reuse the read's buffer
+    // predecessor bytes reuse the read's buffer (a wide launch: the dead ring, at least 16 KB in all)
+    const int kpwin = RW == kChunk ? min(kKpWinMax, a.qlds & ~15) : bt_kp_win<RW>();
     while (i > 0 && j > 0) {
         if (--guard < 0) return kStInternal;
         if (i == glob_row) {
@@ -2164,7 +2183,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
         }
         if (i < w.lo || i > w.hi) {
             const uint64_t c0 = a.prof ? clock64() : 0;
-            bt_refill(sh, s, i, lane, w, kpwin);
+            bt_refill<RW>(sh, s, i, lane, w, kpwin);
             if (a.prof && !(a.dbg & 16) && lane == 0) {
                 int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
                 pf[12] += (int64_t)(clock64() - c0);
@@ -2191,7 +2210,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
             if (ri >= w.lo && ri > 0 && cj > 0) {
                 const int idx = w.hi - ri;
                 const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][0]);
-                const int t = sh.bt.tb[m0.x + cj];
+                const int t = bt_tb<RW>(sh)[m0.x + cj];
                 pr = m0.w;
                 if (m0.y != kKpNone) {
                     const int4 m1 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][4]);
@@ -2216,7 +2235,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
                 int why = 0;
                 if (ri >= w.lo && ri > 0 && cj > 0) {
                     const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[w.hi - ri][0]);
-                    const int t = sh.bt.tb[m0.x + cj];
+                    const int t = bt_tb<RW>(sh)[m0.x + cj];
                     why = (t & kTbNM) ? 3 : 2;
                 }
                 why = readlane(why, f);
@@ -2233,7 +2252,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
         int stall = 0;
         int vi = i, vj = j, vst = st;
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) bt_step_lds(sh, s, w.lo, w.hi, vi, vj, vst, stall);
+        for (int u = 0; u < kUnroll; ++u) bt_step_lds<RW>(sh, s, w.lo, w.hi, vi, vj, vst, stall);
         if (a.prof && !(a.dbg & 16) && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 14] += 1;
         i = bcast0(vi);
         j = bcast0(vj);
@@ -2360,7 +2379,7 @@ __device__ __forceinline__ int seeded_window(SharedState &sh, const SC &sc, cons
         if (st == kStOk) {
             wave_sync();
             __builtin_amdgcn_s_setprio(kSerialPrio);
-            st = backtrack(sh, bi, qw, m, lane);
+            st = backtrack<kChunk>(sh, bi, qw, m, lane);
             __builtin_amdgcn_s_setprio(0);
 #ifdef MANDO_TEAM_DEBUG
             if (lane == 0 && st != kStOk) printf("[win] block %d x %d backtrack st %d\n", (int)blockIdx.x, x, st);
@@ -3198,7 +3217,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 wave_sync();
                 uint64_t t3 = prof ? clock64() : 0;
                 __builtin_amdgcn_s_setprio(kSerialPrio);
-                st = backtrack(sh, bi, qlen, n, lane);
+                st = backtrack<RW>(sh, bi, qlen, n, lane);
                 if (st != kStOk) break;
                 wave_sync();
                 uint64_t t4 = prof ? clock64() : 0;
