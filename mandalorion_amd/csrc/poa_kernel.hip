@@ -1758,6 +1758,13 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         // out of L2 by now); past the batch end the read is harmless and unused
         int4 nA = *reinterpret_cast<const int4 *>(&sh.desc[i0][0]);
         int np1 = sh.desc[i0][4];
+        // capacity: when the batch's rows cannot outgrow the traceback / predecessor / spill arrays
+        // (the common case), the rows skip the per-row capacity tests (a second copy of the loop)
+        const int cap_ok = ((tb_lim - ds.tb_used - kDescBatch * (RW + 4)) |
+                            (kp_lim - ds.kp_used - 3 * kDescBatch * (RW + 4)) |
+                            (sv_lim - ds.sv_used - 3 * kDescBatch * RW)) >= 0;
+        auto rows = [&](auto capchk) -> int {
+        constexpr bool CAP = decltype(capchk)::value;
     for (int i = i0; i < iend; ++i) {
         const int r = b0 + i;
         const int4 dA = nA;
@@ -1816,8 +1823,8 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
                 const int pc0 = R.b0 & ~1, pc1 = R.b1 & ~1;
                 // each term is negative exactly when its test fails (a two-chunk row: at most two
                 // predecessors)
-                bad = (RW - span) | (RW - 1 - (R.e0 - pc0)) | (RW - 1 - (R.e1 - pc1)) | narrowk |
-                      (tb_lim - ds.tb_used) | (kp_lim - ds.kp_used) | (sv_lim - ds.sv_used);
+                bad = (RW - span) | (RW - 1 - (R.e0 - pc0)) | (RW - 1 - (R.e1 - pc1)) | narrowk;
+                if constexpr (CAP) bad |= (tb_lim - ds.tb_used) | (kp_lim - ds.kp_used) | (sv_lim - ds.sv_used);
                 R.nomask = RW == kChunk && ((R.beg - 1 - pc0) | (pc0 + kChunk - 1 - R.end) | (R.beg - 1 - pc1) |
                                             (pc1 + kChunk - 1 - R.end)) >= 0;
                 R.r = r;
@@ -1866,6 +1873,10 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
             prv_am = bcast0(x.z);
         }
     }
+        return kStOk;
+        };
+        const int rst = cap_ok ? rows(std::false_type{}) : rows(std::true_type{});
+        if (rst != kStOk) return rst;
     }
     return kStOk;
 }
