@@ -381,42 +381,65 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             asm_fut = host.submit(assemble, res, hits, n_hits)
             poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
         results = []
-        for f in poa_futs:
-            pl, res = f.result()
-            results.append(res)
-            payloads.append(pl)
-    tm = time.perf_counter()
-    payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
+        if world == 1:
+            # one rank: chunks are contiguous runs of the sorted roots and finish in order, so each
+            # chunk's part of both files is written as soon as its POA is done (while the next runs)
+            written = 0
+            with open(out_path + "/Isoform_Consensi.fasta", "wb") as fa, \
+                    open(out_path + "/reads2isoforms.txt", "wb") as r2:
+                for f in poa_futs:
+                    pl, res = f.result()
+                    results.append(res)
+                    tw = time.perf_counter()
+                    written += _write_payload(pl, fa, r2, written)
+                    timeline.append(("write", tw - t0, time.perf_counter() - t0))
+                    del pl
+            stats["written_isoforms"] = written
+        else:
+            for f in poa_futs:
+                pl, res = f.result()
+                results.append(res)
+                payloads.append(pl)
     if world > 1:
+        tm = time.perf_counter()
+        payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
         payload = _gather(payload, comm)
-    timeline.append(("merge", tm - t0, time.perf_counter() - t0))
-    if rank == 0:
-        tw = time.perf_counter()
-        order = np.argsort(payload["iso_root"], kind="stable")   # sorted roots x IsoDict order
-        mo = payload["mem_off"]
-        cnt = np.diff(mo)[order]
-        new_off = np.zeros(len(order) + 1, dtype=np.int64)
-        np.cumsum(cnt, out=new_off[1:])
-        # member rows in output order: for each isoform in `order`, mo[i] .. mo[i+1]-1
-        midx = (np.repeat(mo[:-1][order] - new_off[:-1], cnt) + np.arange(int(new_off[-1]))
-                if len(order) else np.zeros(0, np.int64))
-        fasta, r2i = _fasta_and_r2i(payload["name_src"], payload["n_sel"][midx], payload["n_start"][midx],
-                                    payload["n_len"][midx], new_off, payload["cons_src"], payload["c_sel"][order],
-                                    payload["c_start"][order], payload["c_len"][order], payload["c_rc"][order])
-        with open(out_path + "/Isoform_Consensi.fasta", "wb") as fh:
-            fh.write(memoryview(np.ascontiguousarray(fasta)))
-        with open(out_path + "/reads2isoforms.txt", "wb") as fh:
-            fh.write(memoryview(np.ascontiguousarray(r2i)))
-        stats["written_isoforms"] = int(len(order))
-        timeline.append(("write", tw - t0, time.perf_counter() - t0))
+        timeline.append(("merge", tm - t0, time.perf_counter() - t0))
+        if rank == 0:
+            tw = time.perf_counter()
+            with open(out_path + "/Isoform_Consensi.fasta", "wb") as fa, \
+                    open(out_path + "/reads2isoforms.txt", "wb") as r2:
+                stats["written_isoforms"] = _write_payload(payload, fa, r2, 0)
+            timeline.append(("write", tw - t0, time.perf_counter() - t0))
+        del payload
     stats["t_total"] = time.perf_counter() - t0
     # the chunks' text buffers go back to the pinned pool off the caller's path
-    del payload, payloads
+    del payloads
     threading.Thread(target=lambda rs: [r.close() for r in rs], args=(results,), daemon=True).start()
     if verbose and rank == 0:
         print("\t" + " ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in stats.items()
                                if not isinstance(v, list)))
     return stats
+
+
+def _write_payload(payload: dict, fa, r2, counter0: int) -> int:
+    """Appends a payload's isoforms to both files in output order (sorted roots x IsoDict order,
+    defineIsoforms.py:155-166), numbering from counter0 + 1; returns the isoform count."""
+    order = np.argsort(payload["iso_root"], kind="stable")
+    mo = payload["mem_off"]
+    cnt = np.diff(mo)[order]
+    new_off = np.zeros(len(order) + 1, dtype=np.int64)
+    np.cumsum(cnt, out=new_off[1:])
+    # member rows in output order: for each isoform in `order`, mo[i] .. mo[i+1]-1
+    midx = (np.repeat(mo[:-1][order] - new_off[:-1], cnt) + np.arange(int(new_off[-1]))
+            if len(order) else np.zeros(0, np.int64))
+    fasta, r2i = _fasta_and_r2i(payload["name_src"], payload["n_sel"][midx], payload["n_start"][midx],
+                                payload["n_len"][midx], new_off, payload["cons_src"], payload["c_sel"][order],
+                                payload["c_start"][order], payload["c_len"][order], payload["c_rc"][order],
+                                counter0=counter0)
+    fa.write(memoryview(np.ascontiguousarray(fasta)))
+    r2.write(memoryview(np.ascontiguousarray(r2i)))
+    return int(len(order))
 
 
 def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, run_poa, stats: dict, lock):
