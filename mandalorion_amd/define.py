@@ -141,7 +141,7 @@ class Assembly:
         if len(self.poa_iso):
             lens = res.seq_len[res.sub].astype(np.int64)
             gid = np.repeat(np.arange(n_iso), np.diff(sub_off))
-            srt = lens[np.lexsort((lens, gid))]
+            srt = np.sort((gid.astype(np.int64) << 32) | lens) & 0xffffffff  # lens sorted inside groups
             lo = sub_off[:-1] + (np.diff(sub_off) - 1) // 2
             hi = sub_off[:-1] + np.diff(sub_off) // 2
             med2 = srt[np.minimum(lo, max(n_sub - 1, 0))] + srt[np.minimum(hi, max(n_sub - 1, 0))]
