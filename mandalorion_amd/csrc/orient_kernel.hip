@@ -9,16 +9,19 @@
 // the known differences from minimap2; parity with mappy itself is unpinned).
 //
 // Layout: one 64-lane wave per isoform group (persistent over groups); everything stays in LDS.
-// The three per-read arrays hold `cap` entries (a power of two chosen per launch, 1024 for R2C2-length
-// reads: 24 KB, so 5 waves fit per CU; groups that overflow are re-run by the host at the next
-// capacity).  Beyond kOrientCap (2048, ~10 kb reads) the same code runs with the arrays in a per-wave
-// HBM slab (orient_kernel<true>), so long reads are oriented instead of refused:
+// The two per-read arrays hold `cap` entries (a power of two chosen per launch, 1024 for R2C2-length
+// reads: 16 KB of dynamic LDS, so 8 waves fit per CU, the VGPR limit; groups that overflow are re-run
+// by the host at the next capacity):
 //   refk  sorted reference minimizer keys  (h << 33 | pos << 1 | strand)          8 B x cap
-//   qm    query minimizer keys, then reused as f[] / p[] of the chaining DP       8 B x cap
-//   an    anchor keys (rev << 62 | x << 31 | y), bitonic-sorted in LDS              8 B x cap
+//   an    anchor keys (rev << 62 | x << 31 | y), bitonic-sorted in LDS; after the chaining DP each
+//         slot is rewritten as used << 63 | f << 48 | (p + 1) << 32 | rev << 31 | y   8 B x cap
+// The query's minimizers are not stored: each 64-position batch of them is looked up in refk as it is
+// found and its anchors appended.  Beyond kOrientCap (2048, ~10 kb reads) the same code runs with the
+// arrays in a per-wave HBM slab (orient_kernel<true>), with f[] / p[] and a used bitmap of their own,
+// so long reads are oriented instead of refused.
 // Minimizers are computed in 256-position tiles (k-mer hashes -> window minima -> marks -> ballot
 // compaction); the chaining DP is sequential over anchors with the 64-anchor look-back spread over the
-// 64 lanes and a DPP max-reduction per anchor.  Work is tiny next to the POA (~0.2 % of the D module).
+// 64 lanes and a DPP max-reduction per anchor.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -31,6 +34,7 @@ constexpr int K = 15, W = 10, MAX_OCC = 10, MAX_GAP = 5000, BW = 500, MIN_CNT = 
 constexpr int TILE = 256;
 constexpr int MAXCH = 64;
 constexpr uint64_t INF = ~0ull;
+constexpr uint32_t INF32 = ~0u;
 
 // bases one tile's k-mers touch (k-mer starts h0 .. h0 + TILE + 2W - 2), staged once per tile as
 // 2-bit codes, 16 per word with the first base in the top bits, plus a 1-bit-per-base mask of
@@ -46,12 +50,12 @@ struct OrientLds {
     uint64_t *gdyn;  // the cap-sized arrays in HBM (the long-read variant), else null
     uint32_t pk[NPK];           // staged 2-bit codes
     uint64_t nm[NNM];           // staged non-ACGT mask
-    uint64_t hb[TILE + 2 * W];  // (hash << 1 | z) of the tile's k-mers, INF when invalid
-    uint64_t mb[TILE + W];      // window minima (hash only)
+    uint32_t hb[TILE + 2 * W];  // (hash << 1 | z) of the tile's k-mers (30-bit hashes), INF32 when invalid
+    uint32_t mb[TILE + W];      // window minima (hash only)
     int32_t ch_score[MAXCH], ch_rev[MAXCH], ch_qs[MAXCH], ch_qe[MAXCH];
     int32_t misc[8];
 };
-extern __shared__ __attribute__((aligned(16))) uint64_t g_orient_dyn[];  // 3 * cap + cap / 64 words
+extern __shared__ __attribute__((aligned(16))) uint64_t g_orient_dyn[];  // 2 * cap words
 // views into the dynamic buffer (LDS address space kept: the base is the LDS symbol itself)
 // G: the arrays live in a per-wave HBM slab (reads beyond the LDS capacity) instead of dynamic LDS
 __device__ __forceinline__ int o_cap(const OrientLds &sh) { return __builtin_amdgcn_readfirstlane(sh.cap); }
@@ -66,17 +70,16 @@ __device__ __forceinline__ uint64_t *o_base(const OrientLds &sh) {
 template <bool G>
 __device__ __forceinline__ uint64_t *o_refk(const OrientLds &sh) { return o_base<G>(sh); }
 template <bool G>
-__device__ __forceinline__ uint64_t *o_qm(const OrientLds &sh) { return o_base<G>(sh) + o_cap(sh); }
-template <bool G>
-__device__ __forceinline__ uint64_t *o_an(const OrientLds &sh) { return o_base<G>(sh) + 2 * o_cap(sh); }
-template <bool G>
-__device__ __forceinline__ uint64_t *o_used(const OrientLds &sh) { return o_base<G>(sh) + 3 * o_cap(sh); }
-template <bool G>
-__device__ __forceinline__ int32_t *o_f(const OrientLds &sh) { return reinterpret_cast<int32_t *>(o_qm<G>(sh)); }
-template <bool G>
-__device__ __forceinline__ int32_t *o_p(const OrientLds &sh) {
-    return reinterpret_cast<int32_t *>(o_qm<G>(sh)) + o_cap(sh);
-}
+__device__ __forceinline__ uint64_t *o_an(const OrientLds &sh) { return o_base<G>(sh) + (G ? 2 : 1) * o_cap(sh); }
+// HBM variant only: f[] / p[] of the chaining DP and the used bitmap
+__device__ __forceinline__ int32_t *o_f(const OrientLds &sh) { return reinterpret_cast<int32_t *>(sh.gdyn + o_cap(sh)); }
+__device__ __forceinline__ int32_t *o_p(const OrientLds &sh) { return o_f(sh) + o_cap(sh); }
+__device__ __forceinline__ uint64_t *o_used(const OrientLds &sh) { return sh.gdyn + 3 * o_cap(sh); }
+// LDS variant: the DP's results packed into the anchor slot (f < 2^15 and p + 1 < 2^16 for cap <= kOrientCap)
+constexpr uint64_t kUsed = 1ull << 63;
+__device__ __forceinline__ int slot_f(uint64_t s) { return (int)((s >> 48) & 0x7fff); }
+__device__ __forceinline__ int slot_p(uint64_t s) { return (int)((s >> 32) & 0xffff) - 1; }
+static_assert(kOrientCap * K < (1 << 15) && kOrientCap < (1 << 16), "packed f / p fields");
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 __device__ __forceinline__ void wsync() { __syncthreads(); }
@@ -91,31 +94,17 @@ __device__ __forceinline__ int enc(uint8_t c) {
     }
 }
 
-__device__ __forceinline__ uint64_t hash64(uint64_t key, uint64_t mask) {
+// hash64(key, 2^30 - 1) in 32-bit arithmetic: every step is masked to 30 bits (the low bits of a sum
+// depend only on the low bits of its terms) and the last step's key << 31 is masked away entirely
+__device__ __forceinline__ uint32_t hash30(uint32_t key) {
+    constexpr uint32_t mask = (1u << (2 * K)) - 1;
     key = (~key + (key << 21)) & mask;
     key = key ^ key >> 24;
     key = ((key + (key << 3)) + (key << 8)) & mask;
     key = key ^ key >> 14;
     key = ((key + (key << 2)) + (key << 4)) & mask;
     key = key ^ key >> 28;
-    key = (key + (key << 31)) & mask;
     return key;
-}
-
-// (hash << 1 | z) of the k-mer starting at p, INF if it has a non-ACGT base or is its own revcomp
-__device__ __forceinline__ uint64_t kmer_hz(const uint8_t *s, int64_t p) {
-    const uint64_t mask = (1ull << (2 * K)) - 1;
-    uint64_t f = 0, r = 0;
-#pragma unroll
-    for (int t = 0; t < K; ++t) {
-        const int c = enc(s[p + t]);
-        if (c > 3) return INF;
-        f = (f << 2) | (uint64_t)c;
-        r |= (uint64_t)(3 - c) << (2 * t);
-    }
-    if (f == r) return INF;
-    const uint64_t z = f < r ? 0 : 1;
-    return (hash64(f < r ? f : r, mask) << 1) | z;
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -154,13 +143,15 @@ __device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
-// minimizer keys of s[0, L) in position order into out[]; returns count, or -1 when over CAP
-__device__ int minimizers(OrientLds &sh, const uint8_t *s, int64_t L, uint64_t *out, int lane) {
-    if (L < K) return 0;
+// minimizers of s[0, L) in position order, handed to sink(mark, key) one 64-position batch at a time
+// (the whole wave calls it; key = h << 33 | pos << 1 | strand on the marked lanes); a sink returning
+// false (over capacity) ends the scan and minimizers() returns false
+template <class Sink>
+__device__ bool minimizers(OrientLds &sh, const uint8_t *s, int64_t L, int lane, Sink &&sink) {
+    if (L < K) return true;
     const int64_t np = L - K + 1;
     const int64_t nw = np <= W ? 1 : np - W + 1;
     const int ww = np <= W ? (int)np : W;
-    int n = 0;
     const uint32_t mask30 = (1u << (2 * K)) - 1;
     // the bases of the next tile are loaded while this one is processed (NPK / 4 bytes per lane)
     constexpr int NST = NPK * 16 / 64;
@@ -203,7 +194,7 @@ __device__ int minimizers(OrientLds &sh, const uint8_t *s, int64_t L, uint64_t *
         // by complementing and reversing the 2-bit groups
         for (int e = lane; e < TILE + 2 * W - 1; e += 64) {
             const int64_t p = h0 + e;
-            uint64_t hz = INF;
+            uint32_t hz = INF32;
             if (p >= 0 && p < np) {
                 uint64_t m = sh.nm[e >> 6] >> (e & 63);
                 if ((e & 63) > 64 - K) m |= sh.nm[(e >> 6) + 1] << (64 - (e & 63));
@@ -213,8 +204,7 @@ __device__ int minimizers(OrientLds &sh, const uint8_t *s, int64_t L, uint64_t *
                     const uint32_t f = (uint32_t)(w >> (2 * (32 - o - K))) & mask30;
                     const uint32_t x = __builtin_bitreverse32(f ^ mask30) >> (32 - 2 * K);
                     const uint32_t r = ((x >> 1) & 0x15555555u) | ((x & 0x15555555u) << 1);
-                    if (f != r)
-                        hz = (hash64(f < r ? f : r, (1ull << (2 * K)) - 1) << 1) | (f < r ? 0 : 1);
+                    if (f != r) hz = (hash30(f < r ? f : r) << 1) | (f < r ? 0u : 1u);
                 }
             }
             sh.hb[e] = hz;
@@ -222,19 +212,19 @@ __device__ int minimizers(OrientLds &sh, const uint8_t *s, int64_t L, uint64_t *
         wsync();
         for (int e = lane; e < TILE + W - 1; e += 64) {
             const int64_t w0 = h0 + e;
-            uint64_t m = INF;
+            uint32_t m = INF32;
             if (w0 >= 0 && w0 < nw) {
                 if (ww == W) {
 #pragma unroll
                     for (int t = 0; t < W; ++t) {
-                        const uint64_t v = sh.hb[e + t];
-                        const uint64_t hv = v == INF ? INF : v >> 1;
+                        const uint32_t v = sh.hb[e + t];
+                        const uint32_t hv = v == INF32 ? INF32 : v >> 1;
                         m = hv < m ? hv : m;
                     }
                 } else {
                     for (int t = 0; t < ww; ++t) {
-                        const uint64_t v = sh.hb[e + t];
-                        const uint64_t hv = v == INF ? INF : v >> 1;
+                        const uint32_t v = sh.hb[e + t];
+                        const uint32_t hv = v == INF32 ? INF32 : v >> 1;
                         m = hv < m ? hv : m;
                     }
                 }
@@ -245,20 +235,20 @@ __device__ int minimizers(OrientLds &sh, const uint8_t *s, int64_t L, uint64_t *
         for (int i0 = 0; i0 < TILE; i0 += 64) {
             const int64_t p = t0 + i0 + lane;
             bool mark = false;
-            uint64_t v = INF;
+            uint32_t v = INF32;
             if (p < np) {
                 v = sh.hb[i0 + lane + (W - 1)];
-                if (v != INF) {
+                if (v != INF32) {
                     const int64_t slo = p - ww + 1 > 0 ? p - ww + 1 : 0;
                     const int64_t shi = p < nw - 1 ? p : nw - 1;
                     if (ww == W) {
                         // every window holding p has minimum <= h(p), so p is some window's minimum
                         // iff h(p) <= the largest of those minima: W independent LDS reads, no break
-                        uint64_t mx = 0;
+                        uint32_t mx = 0;
 #pragma unroll
                         for (int t = 0; t < W; ++t) {
                             const int64_t w0 = p - (W - 1) + t;
-                            const uint64_t mv = sh.mb[i0 + lane + t];  // mb index of window w0
+                            const uint32_t mv = sh.mb[i0 + lane + t];  // mb index of window w0
                             if (w0 >= slo && w0 <= shi) mx = mv > mx ? mv : mx;
                         }
                         mark = (v >> 1) <= mx;
@@ -271,18 +261,12 @@ __device__ int minimizers(OrientLds &sh, const uint8_t *s, int64_t L, uint64_t *
                     }
                 }
             }
-            const unsigned long long m = __ballot(mark);
-            const int cnt = __popcll(m);
-            if (n + cnt > o_cap(sh)) return -1;
-            if (mark) {
-                const int at = n + __popcll(m & lanemask_lt(lane));
-                out[at] = ((v >> 1) << 33) | ((uint64_t)(p + K - 1) << 1) | (v & 1);
-            }
-            n += cnt;
+            const uint64_t key = ((uint64_t)(v >> 1) << 33) | ((uint64_t)(p + K - 1) << 1) | (uint64_t)(v & 1u);
+            if (!sink(mark, key)) return false;
         }
         wsync();
     }
-    return n;
+    return true;
 }
 
 __device__ void bitonic_sort(uint64_t *a, int n, int lane) {
@@ -325,19 +309,18 @@ __device__ __forceinline__ int ilog2_u32(uint32_t v) { return 31 - __clz((int)v)
 template <bool G>
 __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t qlen, int8_t *hits, int max_hits,
                            int32_t *n_hits, int lane) {
-    const int nq = minimizers(sh, q, qlen, o_qm<G>(sh), lane);
-    if (nq < 0) return -1;
-    // anchors: count per query minimizer, exclusive scan, scatter
+    const uint64_t *refk = o_refk<G>(sh);
+    uint64_t *an = o_an<G>(sh);
+    const int cap = o_cap(sh);
+    // anchors, one batch of query minimizers at a time: count per minimizer, wave scan, scatter
     int na = 0;
-    for (int c0 = 0; c0 < nq; c0 += 64) {
-        const int i = c0 + lane;
+    const bool fits = minimizers(sh, q, qlen, lane, [&](bool mark, uint64_t key) -> bool {
+        if (!__ballot(mark)) return true;
         int lo = 0, cnt = 0;
-        uint64_t key = 0;
-        if (i < nq) {
-            key = o_qm<G>(sh)[i];
+        if (mark) {
             const uint64_t h = key >> 33;
-            lo = lower_bound_h(o_refk<G>(sh), nref, h);
-            while (lo + cnt < nref && (o_refk<G>(sh)[lo + cnt] >> 33) == h && cnt <= MAX_OCC) ++cnt;
+            lo = lower_bound_h(refk, nref, h);
+            while (lo + cnt < nref && (refk[lo + cnt] >> 33) == h && cnt <= MAX_OCC) ++cnt;
             if (cnt > MAX_OCC) cnt = 0;
         }
         int incl = cnt;
@@ -346,29 +329,32 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
             if (lane >= o) incl += u;
         }
         const int tot = __shfl(incl, 63, 64);
-        if (na + tot > o_cap(sh)) return -1;
+        if (na + tot > cap) return false;
         const int base = na + incl - cnt;
         const int64_t qpos = (int64_t)((key >> 1) & 0xffffffffull);
         const int qz = (int)(key & 1);
         for (int t = 0; t < cnt; ++t) {
-            const uint64_t r = o_refk<G>(sh)[lo + t];
+            const uint64_t r = refk[lo + t];
             const int64_t rpos = (int64_t)((r >> 1) & 0xffffffffull);
             const int rev = qz ^ (int)(r & 1);
             const int64_t y = rev ? qlen - 1 - (qpos - K + 1) : qpos;
-            o_an<G>(sh)[base + t] = ((uint64_t)rev << 62) | ((uint64_t)rpos << 31) | (uint64_t)y;
+            an[base + t] = ((uint64_t)rev << 62) | ((uint64_t)rpos << 31) | (uint64_t)y;
         }
         na += tot;
-    }
+        return true;
+    });
+    if (!fits) return -1;
     wsync();
-    bitonic_sort(o_an<G>(sh), na, lane);
+    bitonic_sort(an, na, lane);
     // chaining DP: lane l looks at predecessor j = i - 64 + l.  The 64-anchor look-back window (x, y,
     // strand, f) lives in registers and slides one lane per anchor (DPP wave_shl); the best
-    // predecessor is one DPP max-reduction.  Only lane 0 stores f / p (for the chain walk below).
+    // predecessor is one DPP max-reduction.  Only lane 0 stores f / p (for the chain walk below): in
+    // the LDS variant into anchor i's own slot, which the DP has read by then.
     int wx = 0, wy = 0, wr = -1, wf = 0;  // wr = -1: empty slot (j < 0)
-    uint64_t an_next = na > 0 ? o_an<G>(sh)[0] : 0;  // one anchor ahead: the LDS read leaves the DP chain
+    uint64_t an_next = na > 0 ? an[0] : 0;  // one anchor ahead: the LDS read leaves the DP chain
     for (int i = 0; i < na; ++i) {
         const uint64_t ai = an_next;
-        if (i + 1 < na) an_next = o_an<G>(sh)[i + 1];
+        if (i + 1 < na) an_next = an[i + 1];
         const int ri = (int)(ai >> 62);
         const int xi = (int)((ai >> 31) & 0x7fffffff), yi = (int)(ai & 0x7fffffff);
         const int dr = xi - wx, dq = yi - wy;
@@ -385,8 +371,13 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         const bool take = best != 0 && cand > K;
         const int fi = take ? cand : K;
         if (lane == 0) {
-            o_f<G>(sh)[i] = fi;
-            o_p<G>(sh)[i] = take ? i - 64 + (best & 63) : -1;
+            const int pi = take ? i - 64 + (best & 63) : -1;
+            if constexpr (G) {
+                o_f(sh)[i] = fi;
+                o_p(sh)[i] = pi;
+            } else {
+                an[i] = ((uint64_t)fi << 48) | ((uint64_t)(pi + 1) << 32) | ((uint64_t)ri << 31) | (uint64_t)yi;
+            }
         }
         wx = wave_shl1(wx, xi);
         wy = wave_shl1(wy, yi);
@@ -395,17 +386,27 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
     }
     wsync();
     // greedy chain extraction: highest f first (ties: lowest index), walk back to a used anchor
-    for (int t = lane; t < o_cap(sh) / 64; t += 64) o_used<G>(sh)[t] = 0;
-    wsync();
+    if constexpr (G) {
+        for (int t = lane; t < cap / 64; t += 64) o_used(sh)[t] = 0;
+        wsync();
+    }
     int nch = 0;
     for (;;) {
         uint64_t bk = 0;  // (f + 2^20) << 32 | (2^31 - 1 - i): max picks highest f, then lowest i
         for (int c0 = 0; c0 < na; c0 += 64) {
             const int i = c0 + lane;
-            if (i < na && !((o_used<G>(sh)[i >> 6] >> (i & 63)) & 1)) {
-                const uint64_t k = ((uint64_t)(uint32_t)(o_f<G>(sh)[i] + (1 << 20)) << 32) | (uint64_t)(0x7fffffff - i);
-                bk = k > bk ? k : bk;
+            if (i >= na) continue;
+            int fv;
+            if constexpr (G) {
+                if ((o_used(sh)[i >> 6] >> (i & 63)) & 1) continue;
+                fv = o_f(sh)[i];
+            } else {
+                const uint64_t sl = an[i];
+                if (sl & kUsed) continue;
+                fv = slot_f(sl);
             }
+            const uint64_t k = ((uint64_t)(uint32_t)(fv + (1 << 20)) << 32) | (uint64_t)(0x7fffffff - i);
+            bk = k > bk ? k : bk;
         }
         bk = wave_max_u64(bk);
         if (bk == 0) break;
@@ -413,24 +414,42 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         const int bi = 0x7fffffff - (int)(bk & 0xffffffffull);
         if (fbest < MIN_SCORE) break;
         if (lane == 0) {
-            int k = bi, first = bi, cnt = 0;
-            while (k >= 0 && !((o_used<G>(sh)[k >> 6] >> (k & 63)) & 1)) {
-                o_used<G>(sh)[k >> 6] |= 1ull << (k & 63);
-                ++cnt;
-                first = k;
-                k = o_p<G>(sh)[k];
+            int k = bi, first = bi, cnt = 0, fk = 0;
+            if constexpr (G) {
+                while (k >= 0 && !((o_used(sh)[k >> 6] >> (k & 63)) & 1)) {
+                    o_used(sh)[k >> 6] |= 1ull << (k & 63);
+                    ++cnt;
+                    first = k;
+                    k = o_p(sh)[k];
+                }
+                fk = k >= 0 ? o_f(sh)[k] : 0;
+            } else {
+                // one LDS read per step: the slot holds the used flag, p and f
+                uint64_t sl = an[k];
+                while (!(sl & kUsed)) {
+                    an[k] = sl | kUsed;
+                    ++cnt;
+                    first = k;
+                    k = slot_p(sl);
+                    if (k < 0) break;
+                    sl = an[k];
+                }
+                fk = k >= 0 ? slot_f(sl) : 0;
             }
-            const int score = fbest - (k >= 0 ? o_f<G>(sh)[k] : 0);
+            const int score = fbest - fk;
             int ok = 0;
             if (cnt >= MIN_CNT && score >= MIN_SCORE) {
                 if (nch >= MAXCH) {
                     ok = -1;
                 } else {
+                    // G: anchor keys (rev << 62 | x << 31 | y); LDS: slots (rev << 31 | y)
+                    const uint64_t sb = an[bi], sf = an[first];
+                    const int rev = G ? (int)(sb >> 62) : (int)((sb >> 31) & 1);
                     sh.ch_score[nch] = score;
-                    sh.ch_rev[nch] = (int)(o_an<G>(sh)[bi] >> 62);
-                    const int ys = (int)(o_an<G>(sh)[first] & 0x7fffffff) - K + 1, ye = (int)(o_an<G>(sh)[bi] & 0x7fffffff) + 1;
-                    sh.ch_qs[nch] = sh.ch_rev[nch] ? (int)qlen - ye : ys;
-                    sh.ch_qe[nch] = sh.ch_rev[nch] ? (int)qlen - ys : ye;
+                    sh.ch_rev[nch] = rev;
+                    const int ys = (int)(sf & 0x7fffffff) - K + 1, ye = (int)(sb & 0x7fffffff) + 1;
+                    sh.ch_qs[nch] = rev ? (int)qlen - ye : ys;
+                    sh.ch_qe[nch] = rev ? (int)qlen - ys : ye;
                     ok = 1;
                 }
             }
@@ -499,9 +518,19 @@ __global__ __launch_bounds__(64) void orient_kernel(OrientArgs a) {
         const int64_t r0 = a.grp_off[g], r1 = a.grp_off[g + 1];
         int st = 0;
         if (r1 > r0) {
-            const int nref = minimizers(sh, a.seq + a.seq_off[r0], a.seq_off[r0 + 1] - a.seq_off[r0], o_refk<G>(sh), lane);
+            uint64_t *refk = o_refk<G>(sh);
+            int nref = 0;
+            const bool fits = minimizers(sh, a.seq + a.seq_off[r0], a.seq_off[r0 + 1] - a.seq_off[r0], lane,
+                                         [&](bool mark, uint64_t key) -> bool {
+                                             const unsigned long long m = __ballot(mark);
+                                             const int cnt = __popcll(m);
+                                             if (nref + cnt > o_cap(sh)) return false;
+                                             if (mark) refk[nref + __popcll(m & lanemask_lt(lane))] = key;
+                                             nref += cnt;
+                                             return true;
+                                         });
             wsync();
-            if (nref < 0) {
+            if (!fits) {
                 st = -1;
             } else {
                 bitonic_sort(o_refk<G>(sh), nref, lane);
@@ -522,7 +551,7 @@ __global__ __launch_bounds__(64) void orient_kernel(OrientArgs a) {
 
 }  // namespace
 
-size_t orient_dyn_bytes(int cap) { return (size_t)(3 * cap + cap / 64) * sizeof(uint64_t); }
+size_t orient_dyn_bytes(int cap) { return (size_t)(2 * cap) * sizeof(uint64_t); }
 
 int orient_blocks_per_cu(int cap) {
     int nb = 0;
