@@ -33,6 +33,7 @@ namespace {
 constexpr int K = 15, W = 10, MAX_OCC = 10, MAX_GAP = 5000, BW = 500, MIN_CNT = 3, MIN_SCORE = 40;
 constexpr int TILE = 256;
 constexpr int MAXCH = 64;
+constexpr int kBucketShift = 2 * K - 8, kBuckets = 1 << 8;  // refk index over the top 8 hash bits
 constexpr uint64_t INF = ~0ull;
 constexpr uint32_t INF32 = ~0u;
 
@@ -54,7 +55,24 @@ struct OrientLds {
     uint32_t mb[TILE + W];      // window minima (hash only)
     int32_t ch_score[MAXCH], ch_rev[MAXCH], ch_qs[MAXCH], ch_qe[MAXCH];
     int32_t misc[8];
+    uint16_t bst[kBuckets + 1];  // LDS variant: first refk index of each top-8-bit hash bucket
+#ifdef MANDO_ORIENT_PROF
+    uint64_t prof[8], tlast;
+#endif
 };
+#ifdef MANDO_ORIENT_PROF
+// dev builds: per-phase wall cycles summed over waves, printed by the last wave of each launch
+__device__ unsigned long long g_oprof[8];
+__device__ unsigned int g_odone;
+#define OPROF(i)                                     \
+    if (lane == 0) {                                 \
+        const uint64_t t_ = wall_clock64();          \
+        sh.prof[i] += t_ - sh.tlast;                 \
+        sh.tlast = t_;                               \
+    }
+#else
+#define OPROF(i)
+#endif
 extern __shared__ __attribute__((aligned(16))) uint64_t g_orient_dyn[];  // 2 * cap words
 // views into the dynamic buffer (LDS address space kept: the base is the LDS symbol itself)
 // G: the arrays live in a per-wave HBM slab (reads beyond the LDS capacity) instead of dynamic LDS
@@ -82,16 +100,17 @@ __device__ __forceinline__ int slot_p(uint64_t s) { return (int)((s >> 32) & 0xf
 static_assert(kOrientCap * K < (1 << 15) && kOrientCap < (1 << 16), "packed f / p fields");
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+// the workgroup is one wave, and a wave's LDS accesses complete in order: waiting for its own LDS
+// traffic (with a compiler memory barrier) is the whole sync.  __syncthreads() would also wait for
+// every outstanding global load (its workgroup-scope fence), e.g. the next tile's bases.
+__device__ __forceinline__ void wsync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// A/a 0, C/c 1, G/g 2, T/t 3, anything else 4, without branches: ((c >> 1) ^ (c >> 2)) & 3 maps the
+// eight letters to their codes
 __device__ __forceinline__ int enc(uint8_t c) {
-    switch (c) {
-        case 'A': case 'a': return 0;
-        case 'C': case 'c': return 1;
-        case 'G': case 'g': return 2;
-        case 'T': case 't': return 3;
-        default: return 4;
-    }
+    const uint32_t u = c & 0xdfu;
+    const bool ok = u == 'A' || u == 'C' || u == 'G' || u == 'T';
+    return ok ? (int)(((c >> 1) ^ (c >> 2)) & 3u) : 4;
 }
 
 // hash64(key, 2^30 - 1) in 32-bit arithmetic: every step is masked to 30 bits (the low bits of a sum
@@ -132,6 +151,16 @@ __device__ __forceinline__ int wave_max_dpp(int v) {
                  "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n s_nop 1\n"
                  "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
                  : "+v"(v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+// the same max with DPP builtins, so the compiler may fill the DPP wait states with independent work
+__device__ __forceinline__ int wave_max_dpp_sched(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return __builtin_amdgcn_readlane(v, 63);
 }
 // lane l receives lane l+1's value; lane 63 receives `fill`
@@ -179,13 +208,14 @@ __device__ bool minimizers(OrientLds &sh, const uint8_t *s, int64_t L, int lane,
             const int e0 = 64 * j;
             const int e = e0 + lane;
             const int c = enc(cur[j]);
-            uint32_t v = c > 3 ? 0u : (uint32_t)c << (2 * (15 - (lane & 15)));
-            v |= (uint32_t)__shfl_xor((int)v, 1, 64);
-            v |= (uint32_t)__shfl_xor((int)v, 2, 64);
-            v |= (uint32_t)__shfl_xor((int)v, 4, 64);
-            v |= (uint32_t)__shfl_xor((int)v, 8, 64);
+            int v = c > 3 ? 0 : c << (2 * (15 - (lane & 15)));
+            // OR over each row of 16 lanes (DPP inclusive scan): lane 15 of the row holds the word
+            v |= __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+            v |= __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+            v |= __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+            v |= __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
             const unsigned long long bad = __ballot(c > 3);
-            if ((lane & 15) == 0) sh.pk[e >> 4] = v;
+            if ((lane & 15) == 15) sh.pk[e >> 4] = (uint32_t)v;
             if (lane == 0) sh.nm[e0 >> 6] = bad;
         }
         if (lane == 0) sh.nm[NNM - 1] = ~0ull;
@@ -269,7 +299,64 @@ __device__ bool minimizers(OrientLds &sh, const uint8_t *s, int64_t L, int lane,
     return true;
 }
 
-__device__ void bitonic_sort(uint64_t *a, int n, int lane) {
+// bitonic sort of a[0, n) held in registers: lane l owns elements l * P .. l * P + P - 1 (INF past n),
+// so strides below P are compare-exchanges inside a lane and larger ones one 64-bit lane swap per
+// element; no LDS traffic or barriers between stages (n <= 64 * P)
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+template <int P, int S>
+__device__ __forceinline__ void cx_lane(uint64_t (&v)[P], int lane, int size) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        if (k & S) continue;
+        const bool asc = ((lane * P + k) & size) == 0;
+        const uint64_t x = v[k], y = v[k | S];
+        const bool sw = (x > y) == asc;
+        v[k] = sw ? y : x;
+        v[k | S] = sw ? x : y;
+    }
+}
+template <int P>
+__device__ void sort_regs(uint64_t *a, int n, int lane) {
+    uint64_t v[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int i = lane * P + k;
+        v[k] = i < n ? a[i] : INF;
+    }
+    int n2 = 64 * P;
+    while (n2 / 2 >= n && n2 > P) n2 >>= 1;  // stages past the padded size are no-ops
+    for (int size = 2; size <= n2; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= P) {
+                const int lm = stride / P;
+                const bool keep_min = ((lane & lm) == 0) == (((lane * P) & size) == 0);
+#pragma unroll
+                for (int k = 0; k < P; ++k) {
+                    const uint64_t o = shfl_xor64(v[k], lm);
+                    v[k] = ((v[k] > o) == keep_min) ? o : v[k];
+                }
+            } else if (stride == 1) {
+                cx_lane<P, 1>(v, lane, size);
+            } else if (stride == 2) {
+                if constexpr (P > 2) cx_lane<P, 2>(v, lane, size);
+            } else if (stride == 4) {
+                if constexpr (P > 4) cx_lane<P, 4>(v, lane, size);
+            } else if (stride == 8) {
+                if constexpr (P > 8) cx_lane<P, 8>(v, lane, size);
+            }
+        }
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int i = lane * P + k;
+        if (i < n) a[i] = v[k];
+    }
+    wsync();
+}
+
+__device__ void bitonic_sort_lds(uint64_t *a, int n, int lane) {
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
     for (int i = n + lane; i < n2; i += 64) a[i] = INF;
@@ -290,8 +377,21 @@ __device__ void bitonic_sort(uint64_t *a, int n, int lane) {
         }
 }
 
-__device__ __forceinline__ int lower_bound_h(const uint64_t *a, int n, uint64_t h) {
-    int lo = 0, hi = n;
+// sort a[0, n) ascending: registers up to 1024 elements, the LDS/HBM network beyond
+__device__ void bitonic_sort(uint64_t *a, int n, int lane) {
+    if (n <= 1) return;
+    if (n <= 256) {
+        sort_regs<4>(a, n, lane);
+    } else if (n <= 512) {
+        sort_regs<8>(a, n, lane);
+    } else if (n <= 1024) {
+        sort_regs<16>(a, n, lane);
+    } else {
+        bitonic_sort_lds(a, n, lane);
+    }
+}
+
+__device__ __forceinline__ int lower_bound_h(const uint64_t *a, int lo, int hi, uint64_t h) {
     const uint64_t key = h << 33;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -314,12 +414,18 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
     const int cap = o_cap(sh);
     // anchors, one batch of query minimizers at a time: count per minimizer, wave scan, scatter
     int na = 0;
+    OPROF(7)
     const bool fits = minimizers(sh, q, qlen, lane, [&](bool mark, uint64_t key) -> bool {
         if (!__ballot(mark)) return true;
         int lo = 0, cnt = 0;
         if (mark) {
             const uint64_t h = key >> 33;
-            lo = lower_bound_h(refk, nref, h);
+            if constexpr (G) {
+                lo = lower_bound_h(refk, 0, nref, h);
+            } else {  // within h's bucket (~2 entries for R2C2 reads) instead of all of refk
+                const int b = (int)(h >> kBucketShift);
+                lo = lower_bound_h(refk, sh.bst[b], sh.bst[b + 1], h);
+            }
             while (lo + cnt < nref && (refk[lo + cnt] >> 33) == h && cnt <= MAX_OCC) ++cnt;
             if (cnt > MAX_OCC) cnt = 0;
         }
@@ -345,28 +451,44 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
     });
     if (!fits) return -1;
     wsync();
+    OPROF(1)
     bitonic_sort(an, na, lane);
+    OPROF(2)
     // chaining DP: lane l looks at predecessor j = i - 64 + l.  The 64-anchor look-back window (x, y,
     // strand, f) lives in registers and slides one lane per anchor (DPP wave_shl); the best
-    // predecessor is one DPP max-reduction.  Only lane 0 stores f / p (for the chain walk below): in
-    // the LDS variant into anchor i's own slot, which the DP has read by then.
-    int wx = 0, wy = 0, wr = -1, wf = 0;  // wr = -1: empty slot (j < 0)
-    uint64_t an_next = na > 0 ? an[0] : 0;  // one anchor ahead: the LDS read leaves the DP chain
-    for (int i = 0; i < na; ++i) {
-        const uint64_t ai = an_next;
-        if (i + 1 < na) an_next = an[i + 1];
-        const int ri = (int)(ai >> 62);
-        const int xi = (int)((ai >> 31) & 0x7fffffff), yi = (int)(ai & 0x7fffffff);
-        const int dr = xi - wx, dq = yi - wy;
+    // predecessor is one DPP max-reduction.  Software-pipelined by one anchor: the reduction for
+    // anchor i covers lanes 0..62 (anchors i-64 .. i-2, whose f are known one anchor early) and runs
+    // while anchor i-1's f is being decided; anchor i-1 (lane 63, f = f_prev) joins as one scalar
+    // max, so the loop-carried chain is a few scalar ops.  Only lane 0 stores f / p (for the chain
+    // walk below): in the LDS variant into anchor i's own slot, which the DP has read by then.
+    int wx = 0, wy = 0, wr = -1, wf = 0;  // wr = -1: empty slot (j < 0); wf lane 63 unused
+    // best key of lanes 0..62 for anchor a and lane 63's score term (0: no predecessor there)
+    auto reduce = [&](uint64_t a, int &t63) -> int {
+        const int ra = (int)(a >> 62);
+        const int xa = (int)((a >> 31) & 0x7fffffff), ya = (int)(a & 0x7fffffff);
+        const int dr = xa - wx, dq = ya - wy;
         const int dd = dr > dq ? dr - dq : dq - dr;
-        int key = 0;
-        if (wr == ri && dr > 0 && dq > 0 && dr <= MAX_GAP && dq <= MAX_GAP && dd <= BW) {
+        int kv = 0;
+        if (wr == ra && dr > 0 && dq > 0 && dr <= MAX_GAP && dq <= MAX_GAP && dd <= BW) {
             int sc = dq < dr ? dq : dr;
             if (sc > K) sc = K;
             sc -= dd ? (dd * 15) / 100 + (ilog2_u32((uint32_t)dd) >> 1) : 0;
-            key = ((wf + sc + 65536) << 6) | lane;
+            kv = sc + 65536;
         }
-        const int best = wave_max_dpp(key);
+        t63 = __builtin_amdgcn_readlane(kv, 63);
+        return wave_max_dpp_sched(kv != 0 && lane != 63 ? ((wf + kv) << 6) | lane : 0);
+    };
+    uint64_t ai = na > 0 ? an[0] : 0;
+    uint64_t an_next = na > 1 ? an[1] : 0;  // one anchor ahead: the LDS read leaves the DP chain
+    int t63 = 0;
+    int part = na > 0 ? reduce(ai, t63) : 0;
+    int f_prev = 0;
+    for (int i = 0; i < na; ++i) {
+        const int ri = (int)(ai >> 62);
+        const int xi = (int)((ai >> 31) & 0x7fffffff), yi = (int)(ai & 0x7fffffff);
+        // anchor i: lanes 0..62 (part) and lane 63 = anchor i-1 with f_prev
+        const int k63 = t63 ? ((f_prev + t63) << 6) | 63 : 0;
+        const int best = part > k63 ? part : k63;
         const int cand = (best >> 6) - 65536;
         const bool take = best != 0 && cand > K;
         const int fi = take ? cand : K;
@@ -379,12 +501,23 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
                 an[i] = ((uint64_t)fi << 48) | ((uint64_t)(pi + 1) << 32) | ((uint64_t)ri << 31) | (uint64_t)yi;
             }
         }
+        // the window for anchor i+1: anchor i enters lane 63, f of anchor i-1 lands in lane 62
         wx = wave_shl1(wx, xi);
         wy = wave_shl1(wy, yi);
         wr = wave_shl1(wr, ri);
-        wf = wave_shl1(wf, fi);
+        {
+            const int sh1 = wave_shl1(wf, 0);
+            wf = lane == 62 ? f_prev : sh1;
+        }
+        if (i + 1 < na) {
+            ai = an_next;
+            if (i + 2 < na) an_next = an[i + 2];
+            part = reduce(ai, t63);
+        }
+        f_prev = fi;
     }
     wsync();
+    OPROF(3)
     // greedy chain extraction: highest f first (ties: lowest index), walk back to a used anchor
     if constexpr (G) {
         for (int t = lane; t < cap / 64; t += 64) o_used(sh)[t] = 0;
@@ -461,6 +594,7 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         if (ok < 0) return -1;
         nch += ok;
     }
+    OPROF(4)
     // primary selection (lane 0): decreasing score, extraction order on ties (stable insertion sort)
     if (lane == 0) {
         int idx[MAXCH];
@@ -497,6 +631,7 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         *n_hits = np;
     }
     wsync();
+    OPROF(5)
     return 0;
 }
 
@@ -505,6 +640,10 @@ __global__ __launch_bounds__(64) void orient_kernel(OrientArgs a) {
     __shared__ OrientLds sh;
     const int lane = lane_id();
     if (lane == 0) {
+#ifdef MANDO_ORIENT_PROF
+        for (int k = 0; k < 8; ++k) sh.prof[k] = 0;
+        sh.tlast = wall_clock64();
+#endif
         sh.cap = a.cap;
         sh.gdyn = G ? a.gscratch + (int64_t)blockIdx.x * (3 * (int64_t)a.cap + a.cap / 64) : nullptr;
     }
@@ -534,6 +673,12 @@ __global__ __launch_bounds__(64) void orient_kernel(OrientArgs a) {
                 st = -1;
             } else {
                 bitonic_sort(o_refk<G>(sh), nref, lane);
+                OPROF(6)
+                if constexpr (!G) {
+                    for (int b = lane; b <= kBuckets; b += 64)
+                        sh.bst[b] = (uint16_t)lower_bound_h(refk, 0, nref, (uint64_t)b << kBucketShift);
+                    wsync();
+                }
                 for (int64_t r = r0; r < r1; ++r) {
                     const int rc = orient_read<G>(sh, nref, a.seq + a.seq_off[r], a.seq_off[r + 1] - a.seq_off[r],
                                                a.hits + r * a.max_hits, a.max_hits, a.n_hits + r, lane);
@@ -547,6 +692,16 @@ __global__ __launch_bounds__(64) void orient_kernel(OrientArgs a) {
         if (lane == 0) a.status[g] = st;
         wsync();
     }
+#ifdef MANDO_ORIENT_PROF
+    if (lane == 0) {
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_oprof[k], (unsigned long long)sh.prof[k]);
+        __threadfence();
+        if (atomicAdd(&g_odone, 1u) % gridDim.x == gridDim.x - 1)
+            printf("[orient prof] Mcyc of the 100 MHz clock over all waves: ref %.1f misc %.1f q-min+anchors %.1f sort %.1f dp %.1f extract %.1f primary %.1f\n",
+                   g_oprof[6] * 1e-6, g_oprof[7] * 1e-6, g_oprof[1] * 1e-6, g_oprof[2] * 1e-6, g_oprof[3] * 1e-6,
+                   g_oprof[4] * 1e-6, g_oprof[5] * 1e-6);
+    }
+#endif
 }
 
 }  // namespace

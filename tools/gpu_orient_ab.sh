@@ -13,3 +13,7 @@ for i in 1 2; do
     echo "$v$i $(cat $D/$v$i.log)"
   done
 done
+if [ -f build/oprof/libmando.so ]; then
+  MANDO_LIB=build/oprof/libmando.so timeout -k 10 300 python tools/orient_bench2.py 20000 0.3 > $D/prof.log 2>&1 || { tail -5 $D/prof.log; exit 1; }
+  tail -3 $D/prof.log
+fi
