@@ -163,6 +163,16 @@ __device__ __forceinline__ int wave_max_dpp_sched(int v) {
     v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return __builtin_amdgcn_readlane(v, 63);
 }
+// inclusive prefix sum over the wave (DPP row scans, then the row carries)
+__device__ __forceinline__ int wave_incl_sum(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
 // lane l receives lane l+1's value; lane 63 receives `fill`
 __device__ __forceinline__ int wave_shl1(int v, int fill) {
     return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false);
@@ -429,12 +439,8 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
             while (lo + cnt < nref && (refk[lo + cnt] >> 33) == h && cnt <= MAX_OCC) ++cnt;
             if (cnt > MAX_OCC) cnt = 0;
         }
-        int incl = cnt;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int u = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += u;
-        }
-        const int tot = __shfl(incl, 63, 64);
+        const int incl = wave_incl_sum(cnt);
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
         if (na + tot > cap) return false;
         const int base = na + incl - cnt;
         const int64_t qpos = (int64_t)((key >> 1) & 0xffffffffull);
@@ -461,31 +467,36 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
     // while anchor i-1's f is being decided; anchor i-1 (lane 63, f = f_prev) joins as one scalar
     // max, so the loop-carried chain is a few scalar ops.  Only lane 0 stores f / p (for the chain
     // walk below): in the LDS variant into anchor i's own slot, which the DP has read by then.
-    int wx = 0, wy = 0, wr = -1, wf = 0;  // wr = -1: empty slot (j < 0); wf lane 63 unused
-    // best key of lanes 0..62 for anchor a and lane 63's score term (0: no predecessor there)
-    auto reduce = [&](uint64_t a, int &t63) -> int {
-        const int ra = (int)(a >> 62);
-        const int xa = (int)((a >> 31) & 0x7fffffff), ya = (int)(a & 0x7fffffff);
+    // window x is rev << 30 | x (positions < 2^30), so a strand mismatch puts dr far outside
+    // (0, MAX_GAP]; an empty slot (j < 0) has x = INT_MAX.  wf lane 63 is unused.
+    int wx = 0x7fffffff, wy = 0, wf = 0;
+    // best key of lanes 0..62 for the anchor at (xa, ya) and lane 63's score term (0: no predecessor)
+    auto reduce = [&](int xa, int ya, int &t63) -> int {
         const int dr = xa - wx, dq = ya - wy;
-        const int dd = dr > dq ? dr - dq : dq - dr;
-        int kv = 0;
-        if (wr == ra && dr > 0 && dq > 0 && dr <= MAX_GAP && dq <= MAX_GAP && dd <= BW) {
-            int sc = dq < dr ? dq : dr;
-            if (sc > K) sc = K;
-            sc -= dd ? (dd * 15) / 100 + (ilog2_u32((uint32_t)dd) >> 1) : 0;
-            kv = sc + 65536;
-        }
+        const uint32_t dd = __usad((uint32_t)dr, (uint32_t)dq, 0u);  // |dr - dq| where both are > 0
+        const bool valid = min(dr, dq) > 0 && max(dr, dq) <= MAX_GAP && dd <= (uint32_t)BW;
+        // min(dq, dr, K) - (dd * 15 / 100 + ilog2(dd) / 2): dd * 15 / 100 == dd * 157287 >> 20 for
+        // dd <= BW, and ilog2(dd | 1) == ilog2(dd) with 0 for dd == 0
+        const int sc = min(min(dq, dr), K) - (int)((dd * 157287u) >> 20) - ((31 - __clz((int)(dd | 1u))) >> 1);
+        const int kv = valid ? sc + 65536 : 0;
         t63 = __builtin_amdgcn_readlane(kv, 63);
-        return wave_max_dpp_sched(kv != 0 && lane != 63 ? ((wf + kv) << 6) | lane : 0);
+        return wave_max_dpp_sched(valid && lane != 63 ? ((wf + kv) << 6) | lane : 0);
     };
-    uint64_t ai = na > 0 ? an[0] : 0;
+    // anchor fields, wave-uniform (every lane read the same slot)
+    auto uload = [&](uint64_t v, int &x, int &y, int &r) {
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+        r = (int)(hi >> 30);
+        x = (int)((((hi << 1) | (lo >> 31)) & 0x3fffffffu) | ((hi & 0x40000000u)));
+        y = (int)(lo & 0x7fffffffu);
+    };
+    int xi = 0, yi = 0, ri = 0;
+    if (na > 0) uload(an[0], xi, yi, ri);
     uint64_t an_next = na > 1 ? an[1] : 0;  // one anchor ahead: the LDS read leaves the DP chain
     int t63 = 0;
-    int part = na > 0 ? reduce(ai, t63) : 0;
+    int part = na > 0 ? reduce(xi, yi, t63) : 0;
     int f_prev = 0;
     for (int i = 0; i < na; ++i) {
-        const int ri = (int)(ai >> 62);
-        const int xi = (int)((ai >> 31) & 0x7fffffff), yi = (int)(ai & 0x7fffffff);
         // anchor i: lanes 0..62 (part) and lane 63 = anchor i-1 with f_prev
         const int k63 = t63 ? ((f_prev + t63) << 6) | 63 : 0;
         const int best = part > k63 ? part : k63;
@@ -504,15 +515,14 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         // the window for anchor i+1: anchor i enters lane 63, f of anchor i-1 lands in lane 62
         wx = wave_shl1(wx, xi);
         wy = wave_shl1(wy, yi);
-        wr = wave_shl1(wr, ri);
         {
             const int sh1 = wave_shl1(wf, 0);
             wf = lane == 62 ? f_prev : sh1;
         }
         if (i + 1 < na) {
-            ai = an_next;
+            uload(an_next, xi, yi, ri);
             if (i + 2 < na) an_next = an[i + 2];
-            part = reduce(ai, t63);
+            part = reduce(xi, yi, t63);
         }
         f_prev = fi;
     }
