@@ -534,7 +534,8 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         wsync();
     }
     int nch = 0;
-    for (;;) {
+    for (int it = 0;; ++it) {
+        if (it > na) return -1;  // each pass marks its best anchor used: never reached
         uint64_t bk = 0;  // (f + 2^20) << 32 | (2^31 - 1 - i): max picks highest f, then lowest i
         for (int c0 = 0; c0 < na; c0 += 64) {
             const int i = c0 + lane;

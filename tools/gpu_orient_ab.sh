@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 D=gpurun_out/${RUN:-oab}
 mkdir -p $D
 A=${A:-build/oold/libmando.so}; B=${B:-mandalorion_amd/lib/libmando.so}
-timeout -k 10 400 python -u -m pytest tests/test_orient.py -m gpu -x -v --timeout 200 --timeout-method thread > $D/pytest.log 2>&1
+timeout -k 10 120 python -u -m pytest tests/test_orient.py -m gpu -x -v --timeout 60 --timeout-method thread > $D/pytest.log 2>&1
 rc=$?; grep -E "passed|failed" $D/pytest.log | tail -3; [ $rc -eq 0 ] || { tail -40 $D/pytest.log; exit $rc; }
 for i in 1 2; do
   for v in A B; do
