@@ -285,8 +285,9 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, (int64_t)ctx->n_cu * per_cu / team));
     while (teams > 1 && (size_t)(teams * team * a.slot_bytes) > budget) teams /= 2;
     if (getenv("MANDO_PROF"))
-        fprintf(stderr, "[mando prof] slot workspace %.1f MB, %lld slots, team %d (free %.1f GB, budget %.1f GB)\n",
-                a.slot_bytes / 1e6, (long long)(teams * team), team, free_b / 1e9, budget / 1e9);
+        fprintf(stderr, "[mando prof] slot workspace %.1f MB, %lld slots, team %d, %d waves per CU (longest read %d, %d B of LDS) (free %.1f GB, budget %.1f GB)\n",
+                a.slot_bytes / 1e6, (long long)(teams * team), team, per_cu, (int)a.caps.QC, mando::poa_dyn_lds(a),
+                free_b / 1e9, budget / 1e9);
     if (teams < 1) teams = 1;
     int rc = ws.ensure((size_t)(teams * team * a.slot_bytes));
     while (rc == MANDO_E_NOMEM && teams > 1) {  // memory taken by others since hipMemGetInfo: fewer slots

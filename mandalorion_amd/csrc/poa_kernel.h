@@ -120,7 +120,9 @@ __host__ __device__ inline SlotLayout make_layout(const PoaCaps &c) {
     return L;
 }
 
-struct PoaKArgs {
+// The launch arguments the kernel reads while it runs (its LDS copy, see poa_kernel.hip args_of);
+// PoaKArgs adds the workspace layout, which only the kernel's setup reads (from the argument segment).
+struct PoaRunArgs {
     const uint8_t *seq;      // encoded bases 0..4
     const int64_t *seq_off;  // per read
     const int64_t *grp_off;  // per group, n_groups+1
@@ -136,7 +138,6 @@ struct PoaKArgs {
     char *ws;
     int64_t slot_bytes;
     PoaCaps caps;
-    SlotLayout lay;
     int32_t match, mismatch, o1, e1, o2, e2, band_b;
     float band_f;
     int32_t qlds;            // dynamic LDS bytes for the read stream (see poa_qlds_bytes)
@@ -155,6 +156,9 @@ struct PoaKArgs {
     // of other kernels get CUs as groups finish.  0: persistent slots pulling groups from `counter`.
     int32_t one_group, n_slots;
     int32_t *slot_busy;
+};
+struct PoaKArgs : PoaRunArgs {
+    SlotLayout lay;
 };
 
 // A team's mailbox (see poa_kernel.hip, "-S teams").  claim = job << 40 | np << 20 | next window.

@@ -134,19 +134,19 @@ __device__ __forceinline__ int score_of(int a, int b, int match, int mismatch) {
     return (a == 4 || b == 4) ? 0 : (a == b ? match : -mismatch);
 }
 
-__device__ __forceinline__ gint *in_list(const Slot &s, const PoaKArgs &a, int v) {
+__device__ __forceinline__ gint *in_list(const Slot &s, const PoaRunArgs &a, int v) {
     return v == kSink ? s.sink_in : s.in_id + (int64_t)v * a.caps.DCAP;
 }
-__device__ __forceinline__ int in_cap(const PoaKArgs &a, int v) {
+__device__ __forceinline__ int in_cap(const PoaRunArgs &a, int v) {
     return v == kSink ? a.caps.BIGCAP : a.caps.DCAP;
 }
-__device__ __forceinline__ gint *out_list(const Slot &s, const PoaKArgs &a, int v) {
+__device__ __forceinline__ gint *out_list(const Slot &s, const PoaRunArgs &a, int v) {
     return v == kSrc ? s.src_out : s.out_id + (int64_t)v * a.caps.DCAP;
 }
-__device__ __forceinline__ gint *out_wlist(const Slot &s, const PoaKArgs &a, int v) {
+__device__ __forceinline__ gint *out_wlist(const Slot &s, const PoaRunArgs &a, int v) {
     return v == kSrc ? s.src_out_w : s.out_w + (int64_t)v * a.caps.DCAP;
 }
-__device__ __forceinline__ int out_cap(const PoaKArgs &a, int v) {
+__device__ __forceinline__ int out_cap(const PoaRunArgs &a, int v) {
     return v == kSrc ? a.caps.BIGCAP : a.caps.DCAP;
 }
 
@@ -190,7 +190,7 @@ struct alignas(16) SharedState {
     int desc[kDescBatch][kDescInts];  // descriptors of the current row batch
     Slot slot;                      // this wave's workspace arrays (read per phase, see slot_of)
     gint *order0, *order1;          // the two topological-order buffers (slot.order swaps them)
-    PoaKArgs args;                  // kernel arguments (read per phase, see args_of)
+    PoaRunArgs args;                  // kernel arguments (read per phase, see args_of)
     // -S window DP: slot.desc / slot.xpre / slot.qnode point at the window's arrays while it runs;
     // the sink of the DP is node win_sink, and a node's row is wmap[pos - win_pb] inside [pb, pe]
     int win_on, win_sink, win_pb, win_pe;
@@ -297,9 +297,9 @@ __device__ __forceinline__ Slot slot_of(SharedState &sh) {
     s.tnode = uniptr(s.tnode);
     return s;
 }
-__device__ __forceinline__ PoaKArgs args_of(SharedState &sh) {
+__device__ __forceinline__ PoaRunArgs args_of(SharedState &sh) {
     asm volatile("" ::: "memory");
-    PoaKArgs a = sh.args;
+    PoaRunArgs a = sh.args;
     a.caps.NC = bcast0(a.caps.NC);
     a.caps.DCAP = bcast0(a.caps.DCAP);
     a.caps.BIGCAP = bcast0(a.caps.BIGCAP);
@@ -341,7 +341,7 @@ __device__ __forceinline__ PoaKArgs args_of(SharedState &sh) {
 // first read: a chain SRC -> n0 -> ... -> n(L-1) -> SINK
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int init_chain(SharedState &sh, const uint8_t *q, int L, int lane, int &n) {
-    const PoaKArgs a = args_of(sh);
+    const PoaRunArgs a = args_of(sh);
     Slot s = slot_of(sh);
     if (L + 2 > a.caps.NC) return kStCap;
     for (int t = lane; t < L; t += kWave) {
@@ -394,7 +394,7 @@ struct DescRow {
 };
 constexpr int kOutInline = 4;  // out-edges gathered in the batched levels (more: a serial tail)
 
-__device__ __forceinline__ DescRow desc_gather(const PoaKArgs &a, const Slot &s, int r, bool valid, int ring) {
+__device__ __forceinline__ DescRow desc_gather(const PoaRunArgs &a, const Slot &s, int r, bool valid, int ring) {
     DescRow d;
     d.v = 0;
     d.vb = 4;
@@ -513,7 +513,7 @@ __device__ __forceinline__ void desc_finish(const Slot &s, const DescRow &d, int
 }
 
 __device__ __forceinline__ void build_desc(SharedState &sh, int n, int lane, int ring) {
-    const PoaKArgs a = args_of(sh);
+    const PoaRunArgs a = args_of(sh);
     Slot s = slot_of(sh);
     const int nch = (n + kWave - 1) / kWave;
     int prev_val = 0;
@@ -547,7 +547,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 }
 
 __device__ __forceinline__ int build_window(SharedState &sh, int B, int E, int lane, int ring, int &m_out) {
-    const PoaKArgs a = args_of(sh);
+    const PoaRunArgs a = args_of(sh);
     Slot s = slot_of(sh);
     const int DC = a.caps.DCAP;
     const int pB = bcast0(s.pos[B]), pE = bcast0(s.pos[E]);
@@ -759,7 +759,7 @@ __device__ __forceinline__ int qcol(int j) {
 // Rare-case predecessor records (more than kPreInline predecessors, or a predecessor whose record
 // left the LDS row ring): lane k gathers predecessor k's record from HBM.  The loads are consumed
 // inside this uniform branch, so the common path never carries an outstanding load into an s_waitcnt.
-__device__ __forceinline__ void pre_records_slow(const PoaKArgs &a, const Slot &s, SharedState &sh, int r,
+__device__ __forceinline__ void pre_records_slow(const PoaRunArgs &a, const Slot &s, SharedState &sh, int r,
                                                  int node, int pn, const int *dl, int lane, int &pP, int &pB,
                                                  int &pE, int &pA, int &pS) {
     hbm_fence();
@@ -867,7 +867,7 @@ constexpr int kR16Low = -31000, kR16High = -28000;
 // (a wide launch keeps rows of up to two chunks in the ring; those rows hold only the columns they
 // wrote, which the band masks below cover).
 template <class SC, bool R16, int RW = kChunk>
-__device__ __forceinline__ int dp_row(const PoaKArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
+__device__ __forceinline__ int dp_row(const PoaRunArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
                                       int w, int r, int lane, DpState &ds) {
     const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
     const int IDENT = -(1 << 30);
@@ -1143,7 +1143,7 @@ __device__ __forceinline__ void prefetch_row(const SharedState &sh, int r, RowPi
 // so the row costs a single scalar round trip (the fast-path test) plus the argmax broadcast.
 // Returns false (having changed nothing) when the row must take the general path.
 template <class SC>
-__device__ __forceinline__ bool dp_row_fast(const PoaKArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
+__device__ __forceinline__ bool dp_row_fast(const PoaRunArgs &a, const SC &sc, Slot &s, SharedState &sh, int qlen,
                                            int w, int r, int lane, DpState &ds, RowPipe &pp) {
     const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
     const int IDENT = -(1 << 30);
@@ -1707,7 +1707,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
     int tb_lim, kp_lim, sv_lim;
     {
         const Slot s = slot_of(sh);
-        const PoaKArgs a = args_of(sh);
+        const PoaRunArgs a = args_of(sh);
         tb = s.tb;
         kp = s.kp;
         sv = s.sv;
@@ -1743,7 +1743,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         }
         if (b0 == 0) {
             Slot s = slot_of(sh);
-            const PoaKArgs a = args_of(sh);
+            const PoaRunArgs a = args_of(sh);
             const int st = dp_row<SC, true, RW>(a, sc, s, sh, qlen, w, 0, lane, ds);
             if (st != kStOk) return st;
             const int4 x = sh.rrow[0];
@@ -1848,7 +1848,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
             ++nfast;
         } else {
             Slot s = slot_of(sh);
-            const PoaKArgs a = args_of(sh);
+            const PoaRunArgs a = args_of(sh);
 #ifdef MANDO_GENPROF
             const uint64_t g0 = clock64();
 #endif
@@ -1888,7 +1888,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
 template <class SC, bool R16, int RW = kChunk>
 __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8_t *q, int qlen,
                       int n, int lane, int64_t &cells, int &bi_out) {
-    const PoaKArgs a = args_of(sh);
+    const PoaRunArgs a = args_of(sh);
     Slot s = slot_of(sh);
     if ((qlen + kQPad + 2) / 2 > a.qlds) return kStUnsupported;  // the launch sizes the read buffer
     const int w = a.band_b + (int)(a.band_f * (float)qlen);
@@ -2104,7 +2104,7 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
 }
 
 // One walk step read straight from HBM (rows too wide for the window, > kPreInline predecessors).
-__device__ __forceinline__ void bt_step_global(const PoaKArgs &a, const Slot &s, int &i, int &j, int &st) {
+__device__ __forceinline__ void bt_step_global(const PoaRunArgs &a, const Slot &s, int &i, int &j, int &st) {
     const gint *rb = s.rinfo + (int64_t)i * kRowInfoInts;
     const int tbbase = rb[4], kpbase = rb[5], node = rb[6], pn = rb[7];
     const int t = s.tb[tbbase + j];
@@ -2174,7 +2174,7 @@ __device__ __forceinline__ void bt_step_lds(const SharedState &sh, const Slot &s
 
 template <int RW>
 __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int n, int lane) {
-    const PoaKArgs a = args_of(sh);
+    const PoaRunArgs a = args_of(sh);
     Slot s = slot_of(sh);
     int i = bi, j = qlen, st = 0;  // 0 H, 1 E1 (at E1out[i][j]), 2 E2, 3 F1, 4 F2
     constexpr int kUnroll = 8;
@@ -2313,7 +2313,7 @@ __device__ __forceinline__ int seeded_window(SharedState &sh, const SC &sc, cons
     int k = 0, pc = 0;
     const int32_t *par_t = nullptr, *par_q = nullptr;
     {
-        const PoaKArgs a = args_of(sh);
+        const PoaRunArgs a = args_of(sh);
         k = a.seed_k;
         pc = a.pc;
         par_t = a.par_t;
@@ -2418,7 +2418,7 @@ __device__ __forceinline__ int seeded_window(SharedState &sh, const SC &sc, cons
 
 // the read's partition item and anchor count (par_n)
 __device__ __forceinline__ int seeded_item(SharedState &sh, int64_t rd, int &np) {
-    const PoaKArgs a = args_of(sh);
+    const PoaRunArgs a = args_of(sh);
     const int item = bcast0(a.par_item[rd]);
     np = item >= 0 ? bcast0(a.par_n[item]) : 0;
     return item;
@@ -2521,7 +2521,7 @@ __device__ __forceinline__ void team_windows(SharedState &sh, const SC &sc, Team
 // ---------------------------------------------------------------------------------------------
 // graph update for one aligned read (wave-parallel over query positions)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int add_edge(const PoaKArgs &a, Slot &s, int from, int to, bool check,
+__device__ __forceinline__ int add_edge(const PoaRunArgs &a, Slot &s, int from, int to, bool check,
                                         bool from_new, bool to_new) {
     gint *ol = out_list(s, a, from);
     gint *ow = out_wlist(s, a, from);
@@ -2548,7 +2548,7 @@ __device__ __forceinline__ int add_edge(const PoaKArgs &a, Slot &s, int from, in
 
 __device__ __forceinline__ int update_graph(SharedState &sh, const uint8_t *q, int qlen, int &n,
                             int &ng, int lane) {
-    const PoaKArgs a = args_of(sh);
+    const PoaRunArgs a = args_of(sh);
     Slot s = slot_of(sh);
     // Path kinds per query position: 0 = existing node (matched, or a reused aligned node),
     // 1 = new node aligned to the DP row's node (mismatch), 2 = new inserted node.
@@ -2721,7 +2721,7 @@ __device__ __forceinline__ int update_graph(SharedState &sh, const uint8_t *q, i
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int consensus(SharedState &sh, int n, uint8_t *out, int64_t cap,
                          int &len) {
-    const PoaKArgs a = args_of(sh);
+    const PoaRunArgs a = args_of(sh);
     Slot s = slot_of(sh);
     for (int r = n - 1; r >= 0; --r) {
         const int v = s.order[r];
@@ -2768,7 +2768,7 @@ __device__ __forceinline__ int consensus(SharedState &sh, int n, uint8_t *out, i
 // the next read's descriptors and its job), then every member claims the job's windows
 // (team_windows).  The leader's state between jobs lives in LDS (sh.lead).
 __device__ __forceinline__ int64_t read_len(SharedState &sh, int64_t rd, const uint8_t *&q) {
-    const PoaKArgs a = args_of(sh);
+    const PoaRunArgs a = args_of(sh);
     const int64_t o0 = uni64(a.seq_off[rd]);
     q = a.seq + o0;
     return uni64(a.seq_off[rd + 1]) - o0;
@@ -2878,7 +2878,7 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
             int clen = 0;
             const int g = bcast0(sh.lead.g);
             if (st == kStOk) {
-                const PoaKArgs a = args_of(sh);
+                const PoaRunArgs a = args_of(sh);
                 int64_t *prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
                 const uint64_t t6 = prof ? clock64() : 0;
                 const int n = bcast0(sh.lead.n);
@@ -2892,7 +2892,7 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
                 if (prof && lane == 0) prof[4] += (int64_t)(clock64() - t6);
             }
             if (lane == 0) {
-                const PoaKArgs a = args_of(sh);
+                const PoaRunArgs a = args_of(sh);
                 a.status[g] = st;
                 a.cons_len[g] = clen;
                 a.cells[g] = sh.lead.cells;
@@ -2904,7 +2904,7 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
         // the next group from the launch's queue
         int gi = 0;
         {
-            const PoaKArgs a = args_of(sh);
+            const PoaRunArgs a = args_of(sh);
             if (lane == 0) gi = atomicAdd(a.counter, 1);
             gi = bcast0(gi);
             if (gi >= a.n_groups) {
@@ -2915,7 +2915,7 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
         int g;
         int64_t r0, r1;
         {
-            const PoaKArgs a = args_of(sh);
+            const PoaRunArgs a = args_of(sh);
             g = a.gorder ? bcast0(a.gorder[gi]) : gi;
             r0 = uni64(a.grp_off[g]);
             r1 = uni64(a.grp_off[g + 1]);
@@ -2950,7 +2950,7 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
                 sh.lead.pending = 0;
                 sh.lead.active = 1;
             } else {  // no read: an empty consensus
-                const PoaKArgs a = args_of(sh);
+                const PoaRunArgs a = args_of(sh);
                 a.status[g] = kStOk;
                 a.cons_len[g] = 0;
                 a.cells[g] = 0;
@@ -2964,7 +2964,7 @@ template <class SC>
 __device__ __forceinline__ void seeded_main(SharedState &sh, TeamBox *box, int member, int lane) {
     SC sc;
     if constexpr (!std::is_same<SC, DefaultScores>::value) {
-        const PoaKArgs a = args_of(sh);
+        const PoaRunArgs a = args_of(sh);
         sc = SC{a.match, a.mismatch, a.o1, a.e1, a.o2, a.e2};
     }
     if (lane == 0) {
@@ -3015,7 +3015,7 @@ __device__ __forceinline__ void seeded_main(SharedState &sh, TeamBox *box, int m
         }
         const uint8_t *q;
         {
-            const PoaKArgs a = args_of(sh);
+            const PoaRunArgs a = args_of(sh);
             q = a.seq + uni64(a.seq_off[rd]);
         }
         __builtin_amdgcn_s_setprio(0);
@@ -3129,7 +3129,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
     for (int it = 0;; ++it) {
         int gi = 0;
         {
-            const PoaKArgs a = args_of(sh);
+            const PoaRunArgs a = args_of(sh);
             if (a.one_group) {
                 if (it > 0) break;
                 gi = (int)blockIdx.x;
@@ -3142,7 +3142,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
         int g;
         int64_t r0, r1;
         {
-            const PoaKArgs a = args_of(sh);
+            const PoaRunArgs a = args_of(sh);
             g = a.gorder ? bcast0(a.gorder[gi]) : gi;
             r0 = uni64(a.grp_off[g]);
             r1 = uni64(a.grp_off[g + 1]);
@@ -3157,14 +3157,14 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
         int64_t cells = 0;
         int64_t first = r0;
         {
-            const PoaKArgs a = args_of(sh);
+            const PoaRunArgs a = args_of(sh);
             while (first < r1 && a.seq_off[first + 1] - a.seq_off[first] <= 0) ++first;
             first = uni64(first);
         }
         int clen = 0;
         if (first < r1) {
             {
-                const PoaKArgs a = args_of(sh);
+                const PoaRunArgs a = args_of(sh);
                 const int64_t o0 = uni64(a.seq_off[first]);
                 const uint8_t *q0 = a.seq + o0;
                 const int L0 = (int)(uni64(a.seq_off[first + 1]) - o0);
@@ -3176,7 +3176,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 const uint8_t *q;
                 int64_t *prof;
                 {
-                    const PoaKArgs a = args_of(sh);
+                    const PoaRunArgs a = args_of(sh);
                     const int64_t o0 = uni64(a.seq_off[rd]);
                     qlen = (int)(uni64(a.seq_off[rd + 1]) - o0);
                     if (qlen <= 0) continue;
@@ -3189,7 +3189,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 }
                 SC sc;
                 if constexpr (!std::is_same<SC, DefaultScores>::value) {
-                    const PoaKArgs aa = args_of(sh);
+                    const PoaRunArgs aa = args_of(sh);
                     sc = SC{aa.match, aa.mismatch, aa.o1, aa.e1, aa.o2, aa.e2};
                 }
                 // The serial, latency-bound phases (descriptors, backtrack, graph update, consensus) issue
@@ -3241,7 +3241,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 }
             }
             if (st == kStOk) {
-                const PoaKArgs a = args_of(sh);
+                const PoaRunArgs a = args_of(sh);
                 int64_t *prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
                 uint64_t t6 = prof ? clock64() : 0;
                 int cst = kStOk, len = 0;
@@ -3255,7 +3255,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
             }
         }
         if (lane == 0) {
-            const PoaKArgs a = args_of(sh);
+            const PoaRunArgs a = args_of(sh);
             a.status[g] = st;
             a.cons_len[g] = clen;
             a.cells[g] = cells;
