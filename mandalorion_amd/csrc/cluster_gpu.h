@@ -54,7 +54,7 @@ struct Stats {  // written by K1 (and K2's status)
     int32_t n_ops, n_blk;     // true totals, also when a capacity was exceeded
     int32_t n_hist_l, n_hist_r;
     int32_t max_nblk;
-    int32_t pad;
+    int32_t cs_err;            // a record without the cs / seq columns (set by the cs-count waves)
     int64_t span_lo, span_hi;  // tStart / tEnd range of the records on the locus chromosome
     int64_t cov_cap;           // coverage-bin slots (sum over records of sum over blocks ceil(sz/10) + 11)
     int64_t ident_cap;         // bytes of rendered splice identities
@@ -114,6 +114,7 @@ struct Args {
     const int64_t *ann_pos;
     const Locus *loci;
     const int32_t *order;  // block b runs locus order[b]
+    const int32_t *work;   // cs waves: block b takes locus work[2b], member work[2b+1] & 0xffff of work[2b+1] >> 16
     Stats *stats;
     uint8_t *scratch_a;
     uint8_t *scratch_b;

@@ -227,6 +227,83 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t *x, const uint8_t *y, int
     return true;
 }
 
+// 0x80 in the bytes of x that are zero (exact in every byte, not only the lowest)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+}
+// bits 0..3 <- the 0x80 bits of bytes 0..3 (no two partial products share a bit, so no carries)
+__device__ __forceinline__ uint32_t byte_bits(uint32_t z) { return ((z >> 7) * 0x00204081u) >> 21 & 0xfu; }
+// 16-bit masks of the tabs and the cs operators among the 16 bytes of v
+__device__ __forceinline__ uint32_t tab_mask16(const uint4 v) {
+    const uint32_t K = 0x09090909u;
+    return byte_bits(zero_bytes(v.x ^ K)) | byte_bits(zero_bytes(v.y ^ K)) << 4 |
+           byte_bits(zero_bytes(v.z ^ K)) << 8 | byte_bits(zero_bytes(v.w ^ K)) << 12;
+}
+__device__ __forceinline__ uint32_t op_mask16(const uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t om = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) om |= (uint32_t)is_op((uint8_t)(w[k >> 2] >> ((k & 3) * 8))) << k;
+    return om;
+}
+__device__ __forceinline__ uint8_t byte_of(const uint4 v, int k) {
+    const uint32_t w = k < 8 ? (k < 4 ? v.x : v.y) : (k < 12 ? v.z : v.w);
+    return (uint8_t)(w >> ((k & 3) * 8));
+}
+// bits [lo, hi) of a 16-bit chunk mask, lo in [0, 16), hi clamped to 16
+__device__ __forceinline__ uint32_t span_mask16(int64_t lo, int64_t hi) {
+    const uint32_t h = hi >= 16 ? 0xffffu : hi <= 0 ? 0u : (1u << hi) - 1u;
+    return h & ~((1u << (lo > 0 ? lo : 0)) - 1u);
+}
+// one cs operation of build_cs (cluster.cpp, getCSaroundSS SDC:107-161): operator `op` at p, its text
+// up to q; returns whether it is a run (n != 0); `bad` is set for a malformed intron token
+__device__ __forceinline__ bool cs_run(const uint8_t *T, int p, int q, uint8_t op, Run &u, int &bad) {
+    const int len = q - p - 1;
+    u = Run{};
+    u.st = (char)op;
+    switch (op) {
+        case '=':
+        case '-':
+            u.n = len;
+            u.step = 1;
+            break;
+        case '+':
+            u.n = len;
+            u.step = 0;
+            break;
+        case '*':
+            u.n = (len + 1) / 2;
+            u.step = 1;
+            break;
+        case '~': {
+            u.n = 1;
+            u.st = '|';
+            if (len < 4) {
+                bad = 1;
+                u.n = 0;
+                break;
+            }
+            bool ok = true;
+            const int64_t il = to_i64(T, p + 3, q - 2, ok);
+            if (!ok) {
+                bad = 1;
+                u.n = 0;
+                break;
+            }
+            u.step = (int32_t)il;
+            u.motif[0] = (char)T[p + 1];
+            u.motif[1] = (char)T[p + 2];
+            u.motif[2] = (char)T[q - 2];
+            u.motif[3] = (char)T[q - 1];
+            break;
+        }
+        default:  // '\\'
+            u.n = 0;
+    }
+    return u.n != 0;
+}
+__device__ __forceinline__ bool run_advances(const Run &u) { return u.step > 0 || u.st == '|'; }
+
 // ---------------------------------------------------------------------------------------------
 // K1: parse
 // ---------------------------------------------------------------------------------------------
@@ -268,6 +345,9 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
     ALayout A = a_layout(G.scratch_a + L.a_off, L);
     const uint8_t *lchrom = G.chroms + L.chrom_off;
 
+#ifdef MANDO_CL_PHASES
+    const uint64_t k1t0 = clock64();
+#endif
     // 1. line ends: coalesced 16-byte chunks, newline masks compacted in text order
     const uintptr_t base = (uintptr_t)T & ~(uintptr_t)15;
     const int pad0 = (int)((uintptr_t)T - base);
@@ -447,201 +527,11 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
 #ifdef MANDO_CL_PHASES
     const uint64_t k1t2 = clock64();
 #endif
-    // 3. per record: the cs column (field 22) up to its tab, the seq column (23) up to the next tab or
-    //    the line end; cs operators compacted in text order (a wave scans 1 KB a step)
-    int64_t op_carry = 0;
-    for (int r = 0; r < nrec; ++r) {
-        const int a = A.recs[r].cs_off, b = A.recs[r].line_hi;
-        const uintptr_t b0 = (uintptr_t)(T + a) & ~(uintptr_t)15;
-        const int64_t first = (int64_t)(b0 - (uintptr_t)T);  // text offset of chunk 0 (<= a)
-        int t1 = -1, t2 = -1;
-        const int64_t op0 = op_carry;
-        for (int64_t c0 = first; c0 < b && t2 < 0; c0 += 1024) {
-            const int64_t c = c0 + 16 * ln();
-            uint32_t tm = 0, om = 0;
-            if (c < b) {
-                const uint4 v = *(const uint4 *)(T + c);
-                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const uint8_t ch = (uint8_t)((w[k >> 2] >> ((k & 3) * 8)) & 0xffu);
-                    const int64_t pos = c + k;
-                    if (pos < a || pos >= b) continue;
-                    if (ch == '\t') tm |= 1u << k;
-                    if (is_op(ch)) om |= 1u << k;
-                }
-            }
-            // tabs of this step in text order (lanes ascending, bits ascending)
-            const uint64_t has = __ballot(tm != 0);
-            if (has) {
-                if (t1 < 0) {
-                    const int l1 = __ffsll((unsigned long long)has) - 1;
-                    const uint32_t m1 = __shfl(tm, l1);
-                    t1 = (int)(c0 + 16 * l1 + (__ffs(m1) - 1));
-                    // a second tab in the same step
-                    const uint32_t m1r = m1 & (m1 - 1);
-                    if (m1r) {
-                        t2 = (int)(c0 + 16 * l1 + (__ffs(m1r) - 1));
-                    } else {
-                        const uint64_t rest = has & ~((2ull << l1) - 1);
-                        if (rest) {
-                            const int l2 = __ffsll((unsigned long long)rest) - 1;
-                            t2 = (int)(c0 + 16 * l2 + (__ffs(__shfl(tm, l2)) - 1));
-                        }
-                    }
-                } else {
-                    const int l2 = __ffsll((unsigned long long)has) - 1;
-                    t2 = (int)(c0 + 16 * l2 + (__ffs(__shfl(tm, l2)) - 1));
-                }
-            }
-            // operators before the cs column's end
-            if (t1 >= 0) {
-                for (int k = 0; k < 16; ++k)
-                    if ((om >> k) & 1u)
-                        if (c + k >= t1) om &= ~(1u << k);
-            }
-            const int cnt = __popc(om);
-            const int incl = wincl(cnt);
-            int64_t idx = op_carry + incl - cnt;
-            while (om) {
-                const int k = __ffs(om) - 1;
-                om &= om - 1;
-                if (idx < L.op_cap) A.ops[idx] = (int32_t)(c + k);
-                ++idx;
-            }
-            op_carry += __shfl(incl, 63);
-        }
-        if (t1 < 0) {
-            err = 1;  // fewer than 24 columns
-            break;
-        }
-        if (ln() == 0) {
-            Rec &R = A.recs[r];
-            R.cs_len = t1 - a;
-            R.seq_off = t1 + 1;
-            R.seq_len = (t2 >= 0 ? t2 : b) - (t1 + 1);
-            R.op_off = (int32_t)op0;
-            R.nop = (int32_t)(op_carry - op0);
-        }
-    }
-    if (err) {
-        if (ln() == 0) st->status = kParse;
-        return;
-    }
-    if (op_carry > L.op_cap) {
-        if (ln() == 0) {
-            st->status = kCapacity;
-            st->n_rec = nrec;
-            st->n_blk = (int32_t)n_blk;
-            st->n_ops = (int32_t)op_carry;
-        }
-        return;
-    }
-    wsync();
-
-#ifdef MANDO_CL_PHASES
-    const uint64_t k1t3 = clock64();
-#endif
-    // 4. runs (cluster.cpp build_cs): one operator per lane, record by record; prefix sums give each
-    //    run's first record index and genome position, advancing runs are compacted with the genome
-    //    position of their first record
-    int64_t run_carry = 0, adv_carry = 0;
-    for (int r = 0; r < nrec; ++r) {
-        const Rec R = A.recs[r];
-        const int cs_end = R.cs_off + R.cs_len;
-        int64_t rec_c = 0, g_c = 0;
-        const int64_t r0 = run_carry, a0 = adv_carry;
-        int bad = 0;
-        for (int j0 = 0; j0 < R.nop; j0 += 64) {
-            const int j = j0 + ln();
-            bool valid = false;
-            Run u = {};
-            if (j < R.nop) {
-                const int p = A.ops[R.op_off + j];
-                const int q = j + 1 < R.nop ? A.ops[R.op_off + j + 1] : cs_end;
-                const int len = q - p - 1;
-                const uint8_t op = T[p];
-                u.st = (char)op;
-                switch (op) {
-                    case '=':
-                    case '-':
-                        u.n = len;
-                        u.step = 1;
-                        break;
-                    case '+':
-                        u.n = len;
-                        u.step = 0;
-                        break;
-                    case '*':
-                        u.n = (len + 1) / 2;
-                        u.step = 1;
-                        break;
-                    case '~': {
-                        u.n = 1;
-                        u.st = '|';
-                        if (len < 4) {
-                            bad = 1;
-                            u.n = 0;
-                            break;
-                        }
-                        bool ok = true;
-                        const int64_t il = to_i64(T, p + 3, q - 2, ok);
-                        if (!ok) {
-                            bad = 1;
-                            u.n = 0;
-                            break;
-                        }
-                        u.step = (int32_t)il;
-                        u.motif[0] = (char)T[p + 1];
-                        u.motif[1] = (char)T[p + 2];
-                        u.motif[2] = (char)T[q - 2];
-                        u.motif[3] = (char)T[q - 1];
-                        break;
-                    }
-                    default:  // '\\'
-                        u.n = 0;
-                }
-                valid = u.n != 0;
-            }
-            const int vi = valid ? 1 : 0;
-            const int v_incl = wincl(vi);
-            const int64_t nn = valid ? u.n : 0, gs = valid ? (int64_t)u.step * u.n : 0;
-            const int64_t n_incl = wincl(nn), g_incl = wincl(gs);
-            const bool adv = valid && (u.step > 0 || u.st == '|');
-            const int ai = adv ? 1 : 0;
-            const int a_incl = wincl(ai);
-            if (valid) {
-                u.rec0 = (int32_t)(rec_c + n_incl - nn);
-                u.g0 = R.tstart + g_c + g_incl - gs;
-                const int64_t ri = run_carry + v_incl - vi;
-                A.runs[ri] = u;
-                if (adv) {
-                    const int64_t ai_ = adv_carry + a_incl - ai;
-                    A.adv_run[ai_] = (int32_t)(ri - r0);
-                    A.adv_first[ai_] = u.g0 + u.step;
-                }
-            }
-            run_carry += __shfl(v_incl, 63);
-            rec_c += __shfl(n_incl, 63);
-            g_c += __shfl(g_incl, 63);
-            adv_carry += __shfl(a_incl, 63);
-        }
-        const bool any_bad = wany(bad != 0);
-        if (ln() == 0) {
-            Rec &W = A.recs[r];
-            W.run_off = (int32_t)r0;
-            W.nrun = (int32_t)(run_carry - r0);
-            W.adv_off = (int32_t)a0;
-            W.nadv = (int32_t)(adv_carry - a0);
-            W.nrec_cs = (int32_t)rec_c;
-            W.cs_bad = any_bad ? 1 : 0;
-        }
-    }
-
+    // 3-4 (the cs and seq columns, the runs) follow in cluster_cs_count / _scan / _runs, several waves
+    //    per large locus
 #ifdef MANDO_CL_PHASES
     if (ln() == 0)
-        printf("[K1 phases] n %d ops %lld: fields %.2f cs scan %.2f runs %.2f Mcyc\n", nrec, (long long)op_carry,
-               (k1t2 - k1t1) * 1e-6, (k1t3 - k1t2) * 1e-6, (clock64() - k1t3) * 1e-6);
+        printf("[K1 phases] n %d: lines %.2f fields %.2f Mcyc\n", nrec, (k1t1 - k1t0) * 1e-6, (k1t2 - k1t1) * 1e-6);
 #endif
     // 5. statistics for the host (scratch B sizing) and K2
     cov_cap = wsum(cov_cap);
@@ -654,7 +544,7 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
     if (ln() == 0) {
         st->status = kOk;
         st->n_rec = nrec;
-        st->n_ops = (int32_t)op_carry;
+        st->n_ops = 0;  // cluster_cs_scan
         st->n_blk = (int32_t)n_blk;
         st->n_hist_l = hist_l;
         st->n_hist_r = hist_r;
@@ -666,6 +556,174 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// K1 steps 3-4: the cs column (field 22) up to its tab, the seq column (23) up to the next tab or the
+// line end, and the run-length cs records (cluster.cpp build_cs; getCSaroundSS SDC:107-161).  One record
+// per lane: each lane streams its own record's text in 16-byte chunks.  A large locus (config 2: ~7k
+// records, ~20 MB) is spread over up to kCsMaxWaves one-wave workgroups, each taking every nmem-th batch
+// of 64 records; its offsets come from a per-locus prefix in between.
+//   cluster_cs_count  pass 1: the two tabs; counts of operators, runs (operations of non-zero length)
+//                     and advancing runs per record
+//   cluster_cs_scan   one wave per locus: record offsets by prefix sums, the operator capacity check
+//   cluster_cs_runs   pass 2: every run with its first record index and genome position, and the
+//                     advancing runs with the genome position of their first record
+// ---------------------------------------------------------------------------------------------
+constexpr int64_t kCsTextPerWave = 512 << 10;
+constexpr int kCsMaxWaves = 64;
+
+__global__ __launch_bounds__(64) void cluster_cs_count(Args G) {
+    const int li = G.work[2 * blockIdx.x], mem = G.work[2 * blockIdx.x + 1] & 0xffff,
+              nmem = G.work[2 * blockIdx.x + 1] >> 16;
+    Stats *st = G.stats + li;
+    if (st->status != kOk) return;  // K1 stopped on this locus
+    const Locus L = G.loci[li];
+    const uint8_t *T = G.text + L.text_off;
+    ALayout A = a_layout(G.scratch_a + L.a_off, L);
+    const int nrec = st->n_rec;
+    int err = 0;
+    for (int r0 = 64 * mem; r0 < nrec; r0 += 64 * nmem) {
+        const int r = r0 + ln();
+        if (r >= nrec) break;
+        const int a = A.recs[r].cs_off, b = A.recs[r].line_hi;
+        int t1 = -1, t2 = -1, nop = 0, nrun = 0, nadv = 0, bad = 0;
+        int64_t nrc = 0;
+        const int64_t first = (int64_t)(((uintptr_t)(T + a) & ~(uintptr_t)15) - (uintptr_t)T);
+        int pp = -1;
+        uint8_t pop = 0;
+        auto count = [&](int q) {
+            Run u;
+            if (cs_run(T, pp, q, pop, u, bad)) {
+                ++nrun;
+                nrc += u.n;
+                nadv += run_advances(u) ? 1 : 0;
+            }
+        };
+        for (int64_t c = first; c < b && t2 < 0; c += 16) {
+            const uint4 v = *(const uint4 *)(T + c);
+            const uint32_t in = span_mask16(a - c, b - c);
+            uint32_t tm = tab_mask16(v) & in;
+            if (t1 < 0) {
+                uint32_t om = op_mask16(v) & in;
+                if (tm) om &= (1u << (__ffs(tm) - 1)) - 1u;
+                while (om) {
+                    const int k = __ffs(om) - 1;
+                    om &= om - 1;
+                    if (pp >= 0) count((int)c + k);
+                    pp = (int)c + k;
+                    pop = byte_of(v, k);
+                    ++nop;
+                }
+                if (tm) {
+                    t1 = (int)c + __ffs(tm) - 1;
+                    if (pp >= 0) count(t1);
+                    tm &= tm - 1;
+                }
+            }
+            if (t1 >= 0 && tm) t2 = (int)c + __ffs(tm) - 1;
+        }
+        if (t1 < 0) {
+            err = 1;  // fewer than 24 columns
+            continue;
+        }
+        Rec &W = A.recs[r];
+        W.cs_len = t1 - a;
+        W.seq_off = t1 + 1;
+        W.seq_len = (t2 >= 0 ? t2 : b) - (t1 + 1);
+        W.nop = nop;
+        W.nrun = nrun;
+        W.nadv = nadv;
+        W.nrec_cs = (int32_t)nrc;
+        W.cs_bad = bad ? 1 : 0;
+    }
+    if (wany(err != 0) && ln() == 0) atomicOr(&st->cs_err, 1);
+}
+
+__global__ __launch_bounds__(64) void cluster_cs_scan(Args G) {
+    const int li = G.order[blockIdx.x];
+    Stats *st = G.stats + li;
+    if (st->status != kOk) return;
+    if (st->cs_err) {
+        if (ln() == 0) st->status = kParse;
+        return;
+    }
+    const Locus L = G.loci[li];
+    ALayout A = a_layout(G.scratch_a + L.a_off, L);
+    const int nrec = st->n_rec;
+    int64_t op_carry = 0, run_carry = 0, adv_carry = 0;
+    for (int r0 = 0; r0 < nrec; r0 += 64) {
+        const int r = r0 + ln();
+        int nop = 0, nrun = 0, nadv = 0;
+        if (r < nrec) {
+            nop = A.recs[r].nop;
+            nrun = A.recs[r].nrun;
+            nadv = A.recs[r].nadv;
+        }
+        const int op_in = wincl(nop), run_in = wincl(nrun), adv_in = wincl(nadv);
+        if (r < nrec) {
+            Rec &W = A.recs[r];
+            W.op_off = (int32_t)(op_carry + op_in - nop);
+            W.run_off = (int32_t)(run_carry + run_in - nrun);
+            W.adv_off = (int32_t)(adv_carry + adv_in - nadv);
+        }
+        op_carry += __shfl(op_in, 63);
+        run_carry += __shfl(run_in, 63);
+        adv_carry += __shfl(adv_in, 63);
+    }
+    if (ln() == 0) {
+        st->n_ops = (int32_t)op_carry;
+        if (op_carry > L.op_cap) st->status = kCapacity;
+    }
+}
+
+__global__ __launch_bounds__(64) void cluster_cs_runs(Args G) {
+    const int li = G.work[2 * blockIdx.x], mem = G.work[2 * blockIdx.x + 1] & 0xffff,
+              nmem = G.work[2 * blockIdx.x + 1] >> 16;
+    const Stats *st = G.stats + li;
+    if (st->status != kOk) return;
+    const Locus L = G.loci[li];
+    const uint8_t *T = G.text + L.text_off;
+    ALayout A = a_layout(G.scratch_a + L.a_off, L);
+    const int nrec = st->n_rec;
+    for (int r0 = 64 * mem; r0 < nrec; r0 += 64 * nmem) {
+        const int r = r0 + ln();
+        if (r >= nrec) break;
+        const Rec R = A.recs[r];
+        const int a = R.cs_off, b = R.cs_off + R.cs_len;
+        const int64_t first = (int64_t)(((uintptr_t)(T + a) & ~(uintptr_t)15) - (uintptr_t)T);
+        int pp = -1, bad = 0;
+        uint8_t pop = 0;
+        int64_t ri = R.run_off, ai = R.adv_off, rec_c = 0, g_c = 0;
+        auto emit = [&](int q) {
+            Run u;
+            if (cs_run(T, pp, q, pop, u, bad)) {
+                u.rec0 = (int32_t)rec_c;
+                u.g0 = R.tstart + g_c;
+                A.runs[ri] = u;
+                if (run_advances(u)) {
+                    A.adv_run[ai] = (int32_t)(ri - R.run_off);
+                    A.adv_first[ai] = u.g0 + u.step;
+                    ++ai;
+                }
+                ++ri;
+                rec_c += u.n;
+                g_c += (int64_t)u.step * u.n;
+            }
+        };
+        for (int64_t c = first; c < b; c += 16) {
+            const uint4 v = *(const uint4 *)(T + c);
+            uint32_t om = op_mask16(v) & span_mask16(a - c, b - c);
+            while (om) {
+                const int k = __ffs(om) - 1;
+                om &= om - 1;
+                if (pp >= 0) emit((int)c + k);
+                pp = (int)c + k;
+                pop = byte_of(v, k);
+            }
+        }
+        if (pp >= 0) emit(b);
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // K2 scratch layout; the host sizes it with the same carve (base == nullptr)
@@ -926,17 +984,19 @@ __device__ void mt_refill(uint32_t *key) {
 struct MT {
     uint32_t *key;
     int pos;
-    __device__ uint32_t next32() {
-        if (pos == 624) {
-            mt_refill(key);
-            pos = 0;
-        }
-        uint32_t y = key[pos++];
+    __device__ static uint32_t temper(uint32_t y) {
         y ^= (y >> 11);
         y ^= (y << 7) & 0x9d2c5680u;
         y ^= (y << 15) & 0xefc60000u;
         y ^= (y >> 18);
         return y;
+    }
+    __device__ uint32_t next32() {
+        if (pos == 624) {
+            mt_refill(key);
+            pos = 0;
+        }
+        return temper(key[pos++]);
     }
     // random_interval(max) for max < 2^32 (every draw here)
     __device__ uint32_t interval(uint32_t max) {
@@ -952,17 +1012,34 @@ struct MT {
         }
         return v;
     }
-    // permutation(n): Fisher-Yates from the top (all lanes draw the same j; lane 0 swaps)
+    // permutation(n): Fisher-Yates from the top.  The wave tempers the stream's next outputs one per
+    // lane; random_interval's rejection draws (mask, then accept iff <= i) are resolved in order on the
+    // scalar side (readlane), consuming exactly the outputs interval() would; lane 0 swaps.
     __device__ void permutation(int32_t n, int32_t *perm) {
         for (int i = ln(); i < n; i += 64) perm[i] = i;
         wsync();
-        for (int32_t i = n - 1; i >= 1; --i) {
-            const int32_t j = (int32_t)interval((uint32_t)i);
-            if (ln() == 0) {
-                const int32_t t = perm[i];
-                perm[i] = perm[j];
-                perm[j] = t;
+        int32_t i = n - 1;
+        while (i >= 1) {
+            if (pos == 624) {
+                mt_refill(key);
+                pos = 0;
             }
+            const int m = 624 - pos < 64 ? 624 - pos : 64;
+            const uint32_t y = ln() < m ? temper(key[pos + ln()]) : 0u;
+            int k = 0;
+            for (; k < m && i >= 1; ++k) {
+                const uint32_t mask = 0xffffffffu >> __clz(i);
+                const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)y, k) & mask;
+                if (v <= (uint32_t)i) {
+                    if (ln() == 0) {
+                        const int32_t t = perm[i];
+                        perm[i] = perm[v];
+                        perm[v] = t;
+                    }
+                    --i;
+                }
+            }
+            pos += k;
         }
         wsync();
     }
@@ -1022,7 +1099,16 @@ struct LocusRun {
     int32_t n_peaks;
     int32_t ctr[2];  // spliceDict per-side counters
     int32_t n_iso, n_mem, n_sub;
+#ifdef MANDO_CL_PHASES  // dev build: cycles inside find_peaks (coverage merge, permutation, cs queries)
+    uint64_t pc_cov = 0, pc_perm = 0, pc_cs = 0;
+    int32_t pc_cand = 0, pc_char = 0;
+#endif
 
+    // a permutation's buffer: static LDS, else the sort tile's dynamic LDS (free between sorts; each
+    // permutation is consumed before the next sort), else global scratch
+    __device__ int32_t *perm_buf(int32_t m) const {
+        return m <= kLdsPerm ? lperm : m <= 2 * kSortTile ? reinterpret_cast<int32_t *>(g_sort_lds) : B.perm;
+    }
     __device__ bool in_map(int64_t p) const { return p >= L.map_lo && p < L.map_lo + L.map_n; }
     __device__ int64_t mi(int64_t p) const { return p - L.map_lo; }
 
@@ -1529,8 +1615,16 @@ struct LocusRun {
     // --- characterize_splicing_event (SDC:499-550) ----------------------------------------------
     __device__ bool characterize(int64_t left, int64_t right, int32_t nn) {
         const int32_t k = nn < 500 ? nn : 500;
-        int32_t *perm = nn <= kLdsPerm ? lperm : B.perm;
+        int32_t *perm = perm_buf(nn);
+#ifdef MANDO_CL_PHASES
+        const uint64_t tq0 = clock64();
         mt.permutation(nn, perm);
+        const uint64_t tq1 = clock64();
+        pc_perm += tq1 - tq0;
+        ++pc_char;
+#else
+        mt.permutation(nn, perm);
+#endif
         int32_t allowed = 0, bad = 0;
         int32_t lc[6] = {0, 0, 0, 0, 0, 0}, rc[6] = {0, 0, 0, 0, 0, 0};
         for (int t0 = 0; t0 < k; t0 += 64) {
@@ -1559,6 +1653,9 @@ struct LocusRun {
             }
         }
         wsync();
+#ifdef MANDO_CL_PHASES
+        pc_cs += clock64() - tq1;
+#endif
         if (wany(bad != 0)) {
             fail(kParse);
             return false;
@@ -1595,6 +1692,9 @@ struct LocusRun {
                 return;
             }
             if (areas[mi(entry)]) continue;
+#ifdef MANDO_CL_PHASES
+            ++pc_cand;
+#endif
             for (int64_t dd = ln(); dd < span; dd += 64) {
                 const int64_t pos = entry - 2 * w + dd;
                 int64_t f = areas[mi(pos)] ? 1 : 0, c = 0, p = 0, m = 0;
@@ -1652,7 +1752,13 @@ struct LocusRun {
                     nn += c;
                 }
                 wsync();
+#ifdef MANDO_CL_PHASES
+                const uint64_t tc0 = clock64();
                 cov = determine_cov(nn, center, reverse);
+                pc_cov += clock64() - tc0;
+#else
+                cov = determine_cov(nn, center, reverse);
+#endif
             }
             if (cov <= 0) continue;
             const double prop = round3(best, cov);
@@ -2045,7 +2151,7 @@ struct LocusRun {
             const int32_t id = B.idsort[t];
             const int lo = B.id_lo[id], m = B.id_hi[id] - lo;
             const int32_t k = m < 10000 ? m : 10000;
-            int32_t *perm = m <= kLdsPerm ? lperm : B.perm;
+            int32_t *perm = perm_buf(m);
             mt.permutation(m, perm);
             const int64_t pk = pow2ge(k);
             int64_t tlo = INT64_MAX, thi = INT64_MIN;
@@ -2131,7 +2237,7 @@ struct LocusRun {
         for (int iso = 0; iso < n_iso; ++iso) {
             const int32_t m = O.iso_nmem[iso];
             const int32_t k = m < P->sub_k ? m : P->sub_k;
-            int32_t *perm = m <= kLdsPerm ? lperm : B.perm;
+            int32_t *perm = perm_buf(m);
             mt.permutation(m, perm);
             for (int i = ln(); i < k; i += 64) O.sub[n_sub + i] = O.mem[moff + perm[i]];
             if (ln() == 0) O.iso_nsub[iso] = k;
@@ -2194,6 +2300,9 @@ struct LocusRun {
             printf("[K2 phases] n %d: collect %.2f bins %.2f peaks %.2f dict+sort %.2f identities %.2f ends %.2f Mcyc\n", n,
                    (ph[1] - ph[0]) * 1e-6, (ph[2] - ph[1]) * 1e-6, (ph[3] - ph[2]) * 1e-6, (ph[4] - ph[3]) * 1e-6,
                    (ph[5] - ph[4]) * 1e-6, (ph[6] - ph[5]) * 1e-6);
+        if (ln() == 0)
+            printf("[K2 peaks] n %d: candidates %d characterized %d | cov %.2f perm %.2f cs %.2f Mcyc\n", n, pc_cand,
+                   pc_char, pc_cov * 1e-6, pc_perm * 1e-6, pc_cs * 1e-6);
 #endif
 #undef MANDO_PH
     }
@@ -2239,9 +2348,12 @@ __global__ __launch_bounds__(64) void cluster_locus(Args G) {
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-hipError_t launch_parse(const Args &a, int n_blocks, hipStream_t s) {
+hipError_t launch_parse(const Args &a, int n_blocks, int n_work, hipStream_t s) {
     if (n_blocks <= 0) return hipSuccess;
     hipLaunchKernelGGL(cluster_parse, dim3(n_blocks), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(cluster_cs_count, dim3(n_work), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(cluster_cs_scan, dim3(n_blocks), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(cluster_cs_runs, dim3(n_work), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_locus(const Args &a, int n_blocks, hipStream_t s) {
@@ -2406,6 +2518,19 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     if (!ann.empty()) CL_TRY(hipMemcpyAsync(d_ann.p, ann.data(), ann.size() * 8, hipMemcpyHostToDevice, s));
     CL_TRY(d_order.alloc((size_t)(nrun + 1) * 4));
     if (nrun) CL_TRY(hipMemcpyAsync(d_order.p, run_order.data(), (size_t)nrun * 4, hipMemcpyHostToDevice, s));
+    // cs waves: up to kCsMaxWaves per locus by text size, the largest loci first
+    std::vector<int32_t> work;
+    for (int32_t i : run_order) {
+        const int64_t nm = std::min<int64_t>(kCsMaxWaves, std::max<int64_t>(1, (L[(size_t)i].text_len + kCsTextPerWave - 1) / kCsTextPerWave));
+        for (int64_t m = 0; m < nm; ++m) {
+            work.push_back(i);
+            work.push_back((int32_t)(m | nm << 16));
+        }
+    }
+    const int n_work = (int)(work.size() / 2);
+    DevMem d_work(ctx, 10);
+    CL_TRY(d_work.alloc(work.size() * 4 + 8));
+    if (n_work) CL_TRY(hipMemcpyAsync(d_work.p, work.data(), work.size() * 4, hipMemcpyHostToDevice, s));
     CL_TRY(d_prm.alloc(sizeof(Params)));
     CL_TRY(hipMemcpyAsync(d_prm.p, &prm, sizeof(Params), hipMemcpyHostToDevice, s));
     CL_TRY(d_loci.alloc((size_t)nl * sizeof(Locus)));
@@ -2418,6 +2543,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     G.ann_pos = d_ann.as<int64_t>();
     G.loci = d_loci.as<Locus>();
     G.order = d_order.as<int32_t>();
+    G.work = d_work.as<int32_t>();
     G.stats = d_stats.as<Stats>();
     G.prm = d_prm.as<Params>();
 
@@ -2437,7 +2563,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         CL_TRY(hipMemcpyAsync(d_loci.p, L.data(), (size_t)nl * sizeof(Locus), hipMemcpyHostToDevice, s));
         CL_TRY(hipMemsetAsync(d_stats.p, 0, (size_t)nl * sizeof(Stats), s));
         G.scratch_a = d_a.as<uint8_t>();
-        CL_TRY(launch_parse(G, nrun, s));
+        CL_TRY(launch_parse(G, nrun, n_work, s));
         CL_TRY(hipMemcpyAsync(st.data(), d_stats.p, (size_t)nl * sizeof(Stats), hipMemcpyDeviceToHost, s));
         CL_TRY(hipStreamSynchronize(s));
         bool again = false;
