@@ -749,6 +749,8 @@ struct BPtr {
     int64_t *cov;
     Side s[2];
     int32_t *names, *cur, *perm;
+    int64_t *hv;    // determine_cov: each winner's head value
+    int32_t *hcb;   // histo_cov over the map: records whose coverage set holds the bin at map index 10k..10k+9
     int64_t *win;
     uint8_t *areas[2];
     int32_t *splice, *sc, *ec, *sp, *ep;
@@ -809,6 +811,8 @@ __host__ __device__ inline void carve_b(uint8_t *base, const Stats &S, const Loc
     }
     B.names = (int32_t *)take(hmax * 4);
     B.cur = (int32_t *)take(hmax * 4);
+    B.hv = (int64_t *)take(hmax * 8);
+    B.hcb = (int32_t *)take((L.map_n / 10 + 2) * 4);
     B.perm = (int32_t *)take((n > hmax ? n : hmax) * 4);
     B.win = (int64_t *)take(4 * (4 * (int64_t)w + 1) * 8);
     B.areas[0] = take(L.map_n);
@@ -1099,8 +1103,9 @@ struct LocusRun {
     int32_t n_peaks;
     int32_t ctr[2];  // spliceDict per-side counters
     int32_t n_iso, n_mem, n_sub;
+    int32_t hcb_ok;  // every coverage bin lies in the map, so B.hcb answers histo_cov
 #ifdef MANDO_CL_PHASES  // dev build: cycles inside find_peaks (coverage merge, permutation, cs queries)
-    uint64_t pc_cov = 0, pc_perm = 0, pc_cs = 0;
+    uint64_t pc_cov = 0, pc_perm = 0, pc_cs = 0, pc_csof = 0, pc_bins = 0, pc_side = 0;
     int32_t pc_cand = 0, pc_char = 0;
 #endif
 
@@ -1118,6 +1123,9 @@ struct LocusRun {
 
     // --- collect_reads (SDC:278-331) -----------------------------------------------------------
     __device__ void collect() {
+#ifdef MANDO_CL_PHASES
+        const uint64_t tc0 = clock64();
+#endif
         // cs_of: the last record with this name on the locus chromosome (csDict[name] = cs)
         for (int r0 = 0; r0 < n; r0 += 64) {
             const int r = r0 + ln();
@@ -1158,10 +1166,20 @@ struct LocusRun {
             if (r < n && !A.recs[r].same_chrom) A.recs[r].cs_of = -1;
         }
         wsync();
+#ifdef MANDO_CL_PHASES
+        const uint64_t tc1 = clock64();
+        pc_csof = tc1 - tc0;
+#endif
         // coverage bins per record: myround over each block at stride 10 plus the block's tail, sorted
         // and made unique (cov_set)
         int64_t carry = 0, lo = INT64_MAX, hi = INT64_MIN;
-        int bad = 0;
+        int bad = 0, oob = 0;
+        const int64_t hist_n = L.map_n / 10 + 2;
+        const bool hist_lds = hist_n <= 2 * kSortTile;  // the sort tile is free until build_side
+        if (hist_lds) {
+            for (int64_t i = ln(); i < hist_n; i += 64) reinterpret_cast<int32_t *>(g_sort_lds)[i] = 0;
+            wsync();
+        }
         int32_t hl_carry = 0, hr_carry = 0;
         for (int r0 = 0; r0 < n; r0 += 64) {
             const int r = r0 + ln();
@@ -1188,15 +1206,34 @@ struct LocusRun {
             hr_carry += __shfl(ri_, 63);
             if (act) {
                 int64_t *v = B.cov + coff;
-                int64_t m = 0;
-                int64_t y = 0;
+                int64_t m = 0, y = 0, lastv = INT64_MIN, hadd = -1;
                 bool y_set = false, sorted = true;
+                // histo_cov as a dense count per bin (the reference's histo_cov dict, SDC:318-320),
+                // counted as the set is built while it stays in order (in LDS when the map is small)
+                auto hist = [&](int64_t val, int d) {
+                    const int64_t x = mi(val);
+                    if (x < 0 || x >= L.map_n)
+                        oob = 1;
+                    else if (hist_lds)
+                        atomicAdd(&reinterpret_cast<int32_t *>(g_sort_lds)[x / 10], d);
+                    else
+                        atomicAdd(&B.hcb[x / 10], d);
+                };
+                // a value equal to the previous one is dropped at once (the unique pass would drop it)
+                auto push = [&](int64_t val) {
+                    if (val == lastv) return;
+                    if (val < lastv && sorted) {
+                        sorted = false;
+                        hadd = m;  // v[0, m) are counted; undone before the sort below
+                    }
+                    v[m++] = val;
+                    lastv = val;
+                    if (sorted) hist(val, 1);
+                };
                 for (int x = 0; x < R.nblk && !bad; ++x) {
                     const int64_t sz = A.blk[2 * (R.blk_off + x)], bs = A.blk[2 * (R.blk_off + x) + 1];
                     for (int64_t t = 0; t < sz; t += 10) {
-                        const int64_t val = myround(bs + t);
-                        if (m > 0 && val < v[m - 1]) sorted = false;
-                        v[m++] = val;
+                        push(myround(bs + t));
                         y = t;
                         y_set = true;
                     }
@@ -1204,15 +1241,7 @@ struct LocusRun {
                         bad = 1;  // NameError in the reference
                         break;
                     }
-                    int64_t last = INT64_MIN;
-                    for (int64_t t = y; t < sz; ++t) {
-                        const int64_t val = myround(bs + t);
-                        if (val != last) {
-                            if (m > 0 && val < v[m - 1]) sorted = false;
-                            v[m++] = val;
-                        }
-                        last = val;
-                    }
+                    for (int64_t t = y; t < sz; ++t) push(myround(bs + t));
                     // histogram entries in block order (acc >= 0.9 only)
                     if (!R.acc_lt) {
                         const int64_t be = bs + sz;
@@ -1231,10 +1260,15 @@ struct LocusRun {
                     }
                 }
                 if (!bad) {
-                    if (!sorted) heap_sort(v, m);
-                    int64_t u = 0;
-                    for (int64_t i = 0; i < m; ++i)
-                        if (u == 0 || v[i] != v[u - 1]) v[u++] = v[i];
+                    int64_t u = m;
+                    if (!sorted) {  // blocks out of order: sort, unique, count
+                        for (int64_t i = 0; i < hadd; ++i) hist(v[i], -1);
+                        heap_sort(v, m);
+                        u = 0;
+                        for (int64_t i = 0; i < m; ++i)
+                            if (u == 0 || v[i] != v[u - 1]) v[u++] = v[i];
+                        for (int64_t i = 0; i < u; ++i) hist(v[i], 1);
+                    }
                     A.recs[r].cov_off = (int32_t)coff;
                     A.recs[r].cov_n = (int32_t)u;
                     if (u > 0) {
@@ -1254,12 +1288,30 @@ struct LocusRun {
         }
         bin_lo = wmin(lo);
         bin_hi = wmax(hi);
+        hcb_ok = !wany(oob != 0);
+        wsync();
+        if (hist_lds)
+            for (int64_t i = ln(); i < hist_n; i += 64) B.hcb[i] = reinterpret_cast<int32_t *>(g_sort_lds)[i];
         nbins = bin_lo <= bin_hi ? (bin_hi - bin_lo) / 10 + 1 : 0;
         wsync();
+#ifdef MANDO_CL_PHASES
+        const uint64_t tc2 = clock64();
+        pc_bins = tc2 - tc1;
+#endif
         for (int k = 0; k < 2; ++k) build_side(B.s[k]);
+#ifdef MANDO_CL_PHASES
+        pc_side = clock64() - tc2;
+#endif
     }
 
     __device__ static int64_t myround(int64_t x) {
+        if (x >= 0 && x < 0x7fffffff) {  // 32-bit division for genome positions
+            const uint32_t ux = (uint32_t)x;
+            uint32_t q = ux / 10u;
+            const uint32_t r = ux - 10u * q;
+            if (r > 5 || (r == 5 && (q & 1))) ++q;
+            return 10 * (int64_t)q;
+        }
         int64_t q = x >= 0 ? x / 10 : -((-x + 9) / 10);
         const int64_t r = x - 10 * q;
         if (r > 5 || (r == 5 && (q & 1))) ++q;
@@ -1429,6 +1481,9 @@ struct LocusRun {
 
     // --- determine_cov (SDC:200-224) ------------------------------------------------------------
     __device__ int32_t hcov(int64_t pos) {
+        // pos is a coverage bin, so inside the map; the counts were made by L2 atomics, so the read is
+        // an agent-scope atomic load (never a stale L1 line)
+        if (hcb_ok) return __hip_atomic_load(&B.hcb[mi(pos) / 10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int32_t c = 0;
         for (int r0 = 0; r0 < n; r0 += 64) {
             const int r = r0 + ln();
@@ -1461,12 +1516,17 @@ struct LocusRun {
             if (kstart >= nbins) return 0;
         }
         const int64_t bound = bin_lo + 10 * kstart;
+        const int64_t none = reverse ? INT64_MIN : INT64_MAX;
+        // each winner's head: the absolute index of its first set element at / after the bound (the
+        // last at / before it for the left side) in B.cur, its value in B.hv
+        int64_t best = none;
         for (int c0 = 0; c0 < nn; c0 += 64) {
             const int c = c0 + ln();
             if (c < nn) {
                 const Rec &R = A.recs[B.names[c]];
                 const int64_t *v = B.cov + R.cov_off;
                 int lo = 0, hi = R.cov_n;
+                int32_t at = -1;
                 if (reverse) {  // last element <= bound
                     while (lo < hi) {
                         const int mid = (lo + hi) >> 1;
@@ -1475,7 +1535,7 @@ struct LocusRun {
                         else
                             hi = mid;
                     }
-                    B.cur[c] = lo - 1;
+                    at = lo - 1;
                 } else {  // first element >= bound
                     while (lo < hi) {
                         const int mid = (lo + hi) >> 1;
@@ -1484,35 +1544,37 @@ struct LocusRun {
                         else
                             hi = mid;
                     }
-                    B.cur[c] = lo < R.cov_n ? lo : -1;
+                    at = lo < R.cov_n ? lo : -1;
                 }
+                const int64_t h = at >= 0 ? v[at] : none;
+                B.cur[c] = at >= 0 ? R.cov_off + at : -1;
+                B.hv[c] = h;
+                best = reverse ? (h > best ? h : best) : (h < best ? h : best);
             }
         }
+        int64_t top = reverse ? wmax(best) : wmin(best);
         wsync();
         int64_t cov = 0;
         int counter = 0;
-        while (counter < 4) {
-            // next position over the winners' heads (largest for the left side, smallest for the right)
-            int64_t best = reverse ? INT64_MIN : INT64_MAX;
-            for (int c0 = 0; c0 < nn; c0 += 64) {
-                const int c = c0 + ln();
-                if (c < nn && B.cur[c] >= 0) {
-                    const int64_t h = B.cov[A.recs[B.names[c]].cov_off + B.cur[c]];
-                    best = reverse ? (h > best ? h : best) : (h < best ? h : best);
-                }
-            }
-            const int64_t top = reverse ? wmax(best) : wmin(best);
-            if (top == (reverse ? INT64_MIN : INT64_MAX)) break;
+        // merge step: the winners at the extreme head (`top`) advance; the next extreme is taken in the
+        // same pass
+        while (counter < 4 && top != none) {
             int32_t count = 0;
+            int64_t nb = none;
             for (int c0 = 0; c0 < nn; c0 += 64) {
                 const int c = c0 + ln();
-                if (c < nn && B.cur[c] >= 0) {
-                    const Rec &R = A.recs[B.names[c]];
-                    if (B.cov[R.cov_off + B.cur[c]] == top) {
+                if (c < nn) {
+                    int64_t h = B.hv[c];
+                    if (h == top) {
                         ++count;
-                        const int nx = reverse ? B.cur[c] - 1 : B.cur[c] + 1;
-                        B.cur[c] = (nx >= 0 && nx < R.cov_n) ? nx : -1;
+                        const Rec &R = A.recs[B.names[c]];
+                        const int32_t nx = reverse ? B.cur[c] - 1 : B.cur[c] + 1;
+                        const bool in = nx >= R.cov_off && nx < R.cov_off + R.cov_n;
+                        h = in ? B.cov[nx] : none;
+                        B.cur[c] = in ? nx : -1;
+                        B.hv[c] = h;
                     }
+                    nb = reverse ? (h > nb ? h : nb) : (h < nb ? h : nb);
                 }
             }
             count = wsum(count);
@@ -1522,6 +1584,7 @@ struct LocusRun {
                 const int64_t hc = hcov(top);
                 cov = hc > cov ? hc : cov;
             }
+            top = reverse ? wmax(nb) : wmin(nb);
         }
         return cov;
     }
@@ -2259,6 +2322,7 @@ struct LocusRun {
         }
         for (int64_t p = ln(); p < L.map_n; p += 64) {
             B.areas[0][p] = 0;
+            if (p % 10 == 0) B.hcb[p / 10] = 0;
             B.areas[1][p] = 0;
             B.splice[p] = -1;
             B.sc[p] = 0;
@@ -2301,8 +2365,9 @@ struct LocusRun {
                    (ph[1] - ph[0]) * 1e-6, (ph[2] - ph[1]) * 1e-6, (ph[3] - ph[2]) * 1e-6, (ph[4] - ph[3]) * 1e-6,
                    (ph[5] - ph[4]) * 1e-6, (ph[6] - ph[5]) * 1e-6);
         if (ln() == 0)
-            printf("[K2 peaks] n %d: candidates %d characterized %d | cov %.2f perm %.2f cs %.2f Mcyc\n", n, pc_cand,
-                   pc_char, pc_cov * 1e-6, pc_perm * 1e-6, pc_cs * 1e-6);
+            printf("[K2 peaks] n %d: candidates %d characterized %d | cov %.2f perm %.2f cs %.2f Mcyc | collect: cs_of "
+                   "%.2f bins %.2f sides %.2f\n", n, pc_cand, pc_char, pc_cov * 1e-6, pc_perm * 1e-6, pc_cs * 1e-6,
+                   pc_csof * 1e-6, pc_bins * 1e-6, pc_side * 1e-6);
 #endif
 #undef MANDO_PH
     }
