@@ -873,20 +873,39 @@ __host__ __device__ inline void carve_o(uint8_t *base, const Stats &S, const Loc
 constexpr int64_t kSortTile = 4096;
 extern __shared__ uint64_t g_sort_lds[];  // kSortTile keys
 
+// One compare-exchange pass of the network over keys [0, T) of `a` (LDS or global): the T/2 pairs
+// (i, i + j), bit j of i clear, are enumerated directly (no idle half-wave), four per lane per step with
+// their loads issued together; a pair sorts ascending where ((base + i) & k) == 0.
+template <class K>
+__device__ __forceinline__ void bitonic_pass(K *a, int64_t T, int64_t base, int64_t k, int64_t j) {
+    const int64_t np = T >> 1;
+    for (int64_t p0 = 0; p0 < np; p0 += 4 * 64) {
+        uint64_t x[4], y[4];
+        int64_t ii[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t q = p0 + u * 64 + ln();
+            ii[u] = q < np ? ((q & ~(j - 1)) << 1) | (q & (j - 1)) : -1;
+            if (ii[u] >= 0) {
+                x[u] = a[ii[u]];
+                y[u] = a[ii[u] + j];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (ii[u] >= 0 && (x[u] > y[u]) == (((base + ii[u]) & k) == 0)) {
+                a[ii[u]] = y[u];
+                a[ii[u] + j] = x[u];
+            }
+        }
+    }
+}
+
 __device__ void sort_tile_lds(uint64_t *a, int64_t t0, int64_t T, int64_t k, int64_t j_hi) {
     for (int64_t i = ln(); i < T; i += 64) g_sort_lds[i] = a[t0 + i];
     wsync();
     for (int64_t j = j_hi; j > 0; j >>= 1) {
-        for (int64_t i = ln(); i < T; i += 64) {
-            const int64_t l = i ^ j;
-            if (l > i) {
-                const uint64_t x = g_sort_lds[i], y = g_sort_lds[l];
-                if ((x > y) == (((t0 + i) & k) == 0)) {
-                    g_sort_lds[i] = y;
-                    g_sort_lds[l] = x;
-                }
-            }
-        }
+        bitonic_pass(g_sort_lds, T, t0, k, j);
         wsync();
     }
     for (int64_t i = ln(); i < T; i += 64) a[t0 + i] = g_sort_lds[i];
@@ -901,16 +920,7 @@ __device__ void sort_u64(uint64_t *a, int64_t P) {
         wsync();
         for (int64_t k = 2; k <= T; k <<= 1)
             for (int64_t j = k >> 1; j > 0; j >>= 1) {
-                for (int64_t i = ln(); i < T; i += 64) {
-                    const int64_t l = i ^ j;
-                    if (l > i) {
-                        const uint64_t x = g_sort_lds[i], y = g_sort_lds[l];
-                        if ((x > y) == (((t0 + i) & k) == 0)) {
-                            g_sort_lds[i] = y;
-                            g_sort_lds[l] = x;
-                        }
-                    }
-                }
+                bitonic_pass(g_sort_lds, T, t0, k, j);
                 wsync();
             }
         for (int64_t i = ln(); i < T; i += 64) a[t0 + i] = g_sort_lds[i];
@@ -919,16 +929,7 @@ __device__ void sort_u64(uint64_t *a, int64_t P) {
     // stages k > T: passes j >= T in global memory, then the rest of the stage per tile in LDS
     for (int64_t k = 2 * T; k <= P; k <<= 1) {
         for (int64_t j = k >> 1; j >= T; j >>= 1) {
-            for (int64_t i = ln(); i < P; i += 64) {
-                const int64_t l = i ^ j;
-                if (l > i) {
-                    const uint64_t x = a[i], y = a[l];
-                    if ((x > y) == ((i & k) == 0)) {
-                        a[i] = y;
-                        a[l] = x;
-                    }
-                }
-            }
+            bitonic_pass(a, P, 0, k, j);
             wsync();
         }
         for (int64_t t0 = 0; t0 < P; t0 += T) sort_tile_lds(a, t0, T, k, T >> 1);
