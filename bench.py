@@ -260,6 +260,11 @@ def main():
         if not parity:
             raise SystemExit("GPU D-module output differs from the CPU restatement on the baseline sample")
 
+    # the limiter from measurement: the HBM bytes the PMC passes saw per launch over the launch time, as a
+    # fraction of peak; well below peak the kernel is bound by instruction issue / latency (SQ counters,
+    # DESIGN.md 3.1), not by HBM
+    hbm_util = (traffic / (k_ms / max(1, n_launch) / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic and k_ms > 0 else None
+    bound = "hbm" if hbm_util is not None and hbm_util >= 0.6 else "issue"
     out = {
         "metric": "consensus reads/s (whole node): PSL records / wall s of Mando.py -M D",
         "value": records * args.steps / elapsed,
@@ -295,8 +300,9 @@ def main():
             "gpu_equals_cpu_on_sample": parity,
         },
         "roofline": {
-            "bound": "issue",
+            "bound": bound,
             "roofline": "hbm",
+            "hbm_util": hbm_util,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

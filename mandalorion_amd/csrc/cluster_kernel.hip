@@ -1343,11 +1343,80 @@ struct LocusRun {
 
     // histogram of one side: entries sorted by (position, insertion), distinct keys with their
     // first insertion rank, strand counts, and the candidate order of find_peaks
+    // Stable counting sort of a side's entries by position (keys are (position + bias) << 24 | rank and
+    // the ranks follow the insertion order, so a stable sort by position is the key order): counts per
+    // map position in B.sc (zero outside start_end_sites), an exclusive scan over the map, then the
+    // entries placed in rank order, ties inside a step ranked by lane.  Returns false (nothing
+    // changed) when a position falls outside the map.
+    __device__ bool count_sort_side(Side &d) {
+        const int H = d.H;
+        int32_t *C = B.sc;
+        int oob = 0;
+        for (int i0 = 0; i0 < H; i0 += 64) {
+            const int i = i0 + ln();
+            if (i < H) {
+                const int64_t x = mi((int64_t)(d.sk[i] >> 24) - kPosBias);
+                if (x < 0 || x >= L.map_n)
+                    oob = 1;
+                else
+                    atomicAdd(&C[x], 1);
+            }
+        }
+        wsync();
+        const bool bad = wany(oob != 0);
+        if (!bad) {
+            // exclusive scan of the counts (read with agent-scope loads: they were made by L2 atomics)
+            int64_t carry = 0;
+            for (int64_t x0 = 0; x0 < L.map_n; x0 += 64) {
+                const int64_t x = x0 + ln();
+                const int32_t c = x < L.map_n ? __hip_atomic_load(&C[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                const int32_t ci = wincl(c);
+                if (x < L.map_n && c) C[x] = (int32_t)(carry + ci - c);
+                carry += __shfl(ci, 63);
+            }
+            wsync();
+            for (int i0 = 0; i0 < H; i0 += 64) {
+                const int i = i0 + ln();
+                const bool act = i < H;
+                const uint64_t k = act ? d.sk[i] : ~0ull;
+                const int64_t x = act ? mi((int64_t)(k >> 24) - kPosBias) : -1;
+                int32_t rank = 0, later = 0;
+                for (int t = 0; t < 64; ++t) {
+                    const int64_t xt = __shfl(x, t);
+                    const bool same = act && xt == x;
+                    rank += (same && t < ln()) ? 1 : 0;
+                    later |= (same && t > ln()) ? 1 : 0;
+                }
+                if (act) {
+                    const int32_t dst = C[x] + rank;
+                    d.cand[dst] = k;
+                    if (!later) C[x] = dst + 1;
+                }
+                wsync();
+            }
+            uint64_t *t = d.sk;
+            d.sk = d.cand;
+            d.cand = t;
+        }
+        // B.sc back to zero where this side touched it
+        for (int i0 = 0; i0 < H; i0 += 64) {
+            const int i = i0 + ln();
+            if (i < H) {
+                const int64_t x = mi((int64_t)(d.sk[i] >> 24) - kPosBias);
+                if (x >= 0 && x < L.map_n) C[x] = 0;
+            }
+        }
+        wsync();
+        return !bad;
+    }
+
     __device__ void build_side(Side &d) {
         const int H = d.H;
         for (int64_t i = H + ln(); i < d.P; i += 64) d.sk[i] = ~0ull;
         wsync();
-        sort_u64(d.sk, d.P);
+        // large sides (config 2's ~35k entries): a counting sort over the map instead of the bitonic
+        // network's log^2 passes
+        if (H <= kSortTile || !count_sort_side(d)) sort_u64(d.sk, d.P);
         // records in sorted order; distinct-key flags
         int32_t kc = 0;
         for (int i0 = 0; i0 < H; i0 += 64) {
