@@ -1417,7 +1417,10 @@ struct LocusRun {
         // large sides (config 2's ~35k entries): a counting sort over the map instead of the bitonic
         // network's log^2 passes
         if (H <= kSortTile || !count_sort_side(d)) sort_u64(d.sk, d.P);
-        // records in sorted order; distinct-key flags
+        // records in sorted order; distinct-key flags; strand counts per key (lane per entry: the key
+        // index of entry i is the number of distinct keys up to i, minus one)
+        for (int64_t i = ln(); i < 3 * (int64_t)H; i += 64) d.upmb[i] = 0;
+        wsync();
         int32_t kc = 0;
         for (int i0 = 0; i0 < H; i0 += 64) {
             const int i = i0 + ln();
@@ -1432,12 +1435,15 @@ struct LocusRun {
                 first = (i == 0 || (int64_t)(d.sk[i - 1] >> 24) - kPosBias != pos) ? 1 : 0;
             }
             const int32_t fi = wincl(first);
-            if (first) {
+            if (i < H) {
                 const int32_t u = kc + fi - 1;
-                d.ukey[u] = pos;
-                d.ulo[u] = i;
-                d.ufirst[u] = seq;
-                d.upmb[3 * u] = d.upmb[3 * u + 1] = d.upmb[3 * u + 2] = 0;
+                if (first) {
+                    d.ukey[u] = pos;
+                    d.ulo[u] = i;
+                    d.ufirst[u] = seq;
+                }
+                const int8_t dn = A.recs[d.etmp[seq]].dirn;
+                atomicAdd(&d.upmb[3 * u + (dn == 0 ? 0 : dn == 1 ? 1 : 2)], 1);
             }
             kc += __shfl(fi, 63);
         }
@@ -1446,17 +1452,6 @@ struct LocusRun {
         for (int u0 = 0; u0 < kc; u0 += 64) {
             const int u = u0 + ln();
             if (u < kc) d.ucnt[u] = (u + 1 < kc ? d.ulo[u + 1] : H) - d.ulo[u];
-        }
-        wsync();
-        // strand counts per key (lane per entry)
-        for (int i0 = 0; i0 < H; i0 += 64) {
-            const int i = i0 + ln();
-            if (i < H) {
-                const int64_t pos = (int64_t)(d.sk[i] >> 24) - kPosBias;
-                const int u = find_key(d, pos);
-                const int8_t dn = A.recs[d.erec[i]].dirn;
-                atomicAdd(&d.upmb[3 * u + (dn == 0 ? 0 : dn == 1 ? 1 : 2)], 1);
-            }
         }
         wsync();
         // candidates: count >= min_count, count descending, insertion order on ties
