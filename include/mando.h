@@ -238,6 +238,16 @@ int mando_pack_segments(const uint8_t *const *src, const int8_t *sel, const int6
 int mando_split_loci(const char *psl_path, const char *out_dir, int32_t sort_lines, const char *sorted_out,
                      int64_t *n_records, int64_t *n_loci);
 
+/* The D module's locus roots (defineIsoforms.py:130-139, `roots` of main): every entry of `dir` that is a
+ * regular file whose name holds ".psl", cut at the first ".psl", deduplicated, sorted by
+ * (chromosome bytes, int(start)) (ties by the whole root); sizes[k] = size of <root k>.psl, -1 when no
+ * entry is exactly that name.  Writes the roots NUL-terminated into names (capacity names_cap bytes)
+ * and *n_roots / *names_bytes.  MANDO_E_CAP when names_cap or sizes_cap is too small (both required sizes
+ * are still returned); MANDO_E_ARG when a root's second '~' field is not a plain decimal integer (the
+ * caller then applies Python's int() itself).  threads <= 0: up to 16 threads for the stat calls. */
+int mando_list_roots(const char *dir, int32_t threads, char *names, int64_t names_cap, int64_t *sizes,
+                     int64_t sizes_cap, int64_t *n_roots, int64_t *names_bytes);
+
 /* SAM -> PSL, replacing `python3 emtrey.py -i sam -o psl -m -t T`
  * (emtrey.py:31-193, called at Mando.py:336-341): one PSL line per mapped SAM record, input order, with
  * the accuracy / cs / read-sequence columns when mando_mode != 0.  threads <= 0: all cores. */

@@ -47,6 +47,7 @@ EXPORTED = (
     "mando_comm_destroy",
     "mando_pack_segments",
     "mando_split_loci",
+    "mando_list_roots",
     "mando_sam_to_psl",
     "mando_clean_psl",
     "mando_filter_default_params",
@@ -193,6 +194,8 @@ def load(path: str | None = None):
         lib.mando_orient_segments.argtypes = [_P, _P, _I64, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
         lib.mando_poa_segments.argtypes = [_P, _P, _P, _I64, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]
         lib.mando_split_loci.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _P, _P]
+        lib.mando_list_roots.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, _P,
+                                         ctypes.c_int64, _P, _P]
         lib.mando_sam_to_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, _P]
         lib.mando_clean_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, _P]
         lib.mando_filter_default_params.argtypes = [_P]

@@ -10,7 +10,11 @@
 // Fields are separated by tabs (PSL); GNU sort's blank-separated fields coincide because PSL fields
 // hold no blanks.  The sort's locale is assumed to be C (Mando.py does not set one; under a UTF-8
 // collation the chromosome order could differ).
+#include <dirent.h>
+#include <sys/stat.h>
+
 #include <algorithm>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -150,5 +154,86 @@ extern "C" int mando_split_loci(const char *psl_path, const char *out_dir, int32
     if (rc) return rc;
     if (n_records) *n_records = nrec;
     if (n_loci) *n_loci = nloc;
+    return MANDO_OK;
+}
+
+// mando_list_roots: the directory scan of defineIsoforms.py:130-139 (+ the file sizes the D driver
+// plans its chunks with) without a Python stat per file
+extern "C" int mando_list_roots(const char *dir, int32_t threads, char *names, int64_t names_cap, int64_t *sizes,
+                                int64_t sizes_cap, int64_t *n_roots, int64_t *names_bytes) {
+    if (!dir || !n_roots || !names_bytes || names_cap < 0 || sizes_cap < 0) return MANDO_E_ARG;
+    DIR *d = opendir(dir);
+    if (!d) return MANDO_E_ARG;
+    std::vector<std::string> ents;
+    while (struct dirent *e = readdir(d)) {
+        if (strstr(e->d_name, ".psl")) ents.emplace_back(e->d_name);
+    }
+    closedir(d);
+    const std::string base = std::string(dir) + "/";
+    // regular files only (is_file() follows symlinks, as stat does), sizes from the same stat
+    std::vector<int64_t> fsize(ents.size(), -2);  // -2: not a regular file
+    int nt = threads > 0 ? threads : 16;
+    nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, ents.size() / 256 + 1));
+    auto work = [&](int t) {
+        struct stat st;
+        for (size_t i = (size_t)t; i < ents.size(); i += (size_t)nt)
+            if (stat((base + ents[i]).c_str(), &st) == 0 && S_ISREG(st.st_mode)) fsize[i] = (int64_t)st.st_size;
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto &th : pool) th.join();
+    struct Root {
+        std::string name;
+        size_t clen;  // the chromosome is name[0, clen) (a length: short names move with their string)
+        int64_t start;
+        int64_t size;
+    };
+    std::vector<Root> roots;
+    roots.reserve(ents.size());
+    for (size_t i = 0; i < ents.size(); ++i) {
+        if (fsize[i] == -2) continue;
+        const std::string &n = ents[i];
+        const size_t cut = n.find(".psl");
+        roots.push_back(Root{n.substr(0, cut), 0, 0, cut + 4 == n.size() ? fsize[i] : -1});
+    }
+    // one root per name; the exact <root>.psl entry carries the size
+    std::sort(roots.begin(), roots.end(), [](const Root &a, const Root &b) {
+        return a.name != b.name ? a.name < b.name : a.size > b.size;
+    });
+    roots.erase(std::unique(roots.begin(), roots.end(), [](const Root &a, const Root &b) { return a.name == b.name; }),
+                roots.end());
+    for (Root &r : roots) {
+        const size_t t1 = r.name.find('~');
+        if (t1 == std::string::npos) return MANDO_E_ARG;  // the reference's split('~')[1] raises
+        const size_t t2 = r.name.find('~', t1 + 1);
+        const std::string_view f(r.name.data() + t1 + 1, (t2 == std::string::npos ? r.name.size() : t2) - t1 - 1);
+        if (f.empty() || f.size() > 18) return MANDO_E_ARG;
+        int64_t v = 0;
+        for (char c : f) {
+            if (c < '0' || c > '9') return MANDO_E_ARG;
+            v = v * 10 + (c - '0');
+        }
+        r.clen = t1;
+        r.start = v;
+    }
+    std::sort(roots.begin(), roots.end(), [](const Root &a, const Root &b) {
+        const std::string_view ca(a.name.data(), a.clen), cb(b.name.data(), b.clen);
+        if (ca != cb) return ca < cb;  // bytes (UTF-8 keeps code point order)
+        if (a.start != b.start) return a.start < b.start;
+        return a.name < b.name;
+    });
+    int64_t need = 0;
+    for (const Root &r : roots) need += (int64_t)r.name.size() + 1;
+    *n_roots = (int64_t)roots.size();
+    *names_bytes = need;
+    if (need > names_cap || (int64_t)roots.size() > sizes_cap || (!names && need) || (!sizes && !roots.empty()))
+        return MANDO_E_CAP;
+    int64_t o = 0;
+    for (size_t k = 0; k < roots.size(); ++k) {
+        memcpy(names + o, roots[k].name.c_str(), roots[k].name.size() + 1);
+        o += (int64_t)roots[k].name.size() + 1;
+        sizes[k] = roots[k].size;
+    }
     return MANDO_OK;
 }

@@ -20,6 +20,7 @@ of per-locus results to rank 0 for the writer (RCCL over xGMI).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import os
 import sys
 import threading
@@ -74,7 +75,32 @@ def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0, info: dict |
 
 def _roots(out_tmp: str, sizes: dict | None = None) -> list[str]:
     """Locus roots of tmp_SS (defineIsoforms.py:130-139); sizes (optional) receives each root's
-    <root>.psl size from the same directory scan."""
+    <root>.psl size from the same directory scan.  The scan, the stat calls and the sort run natively
+    (mando_list_roots); a root whose start field is not a plain decimal takes the Python path below,
+    which parses (or raises) exactly as the reference does."""
+    lib = _lib.load()
+    cap_n, cap_b = 1 << 16, 1 << 22
+    for _ in range(2):
+        names = ctypes.create_string_buffer(cap_b)
+        sz = np.empty(cap_n, dtype=np.int64)
+        nr, nb = ctypes.c_int64(), ctypes.c_int64()
+        rc = lib.mando_list_roots(out_tmp.encode(), 0, names, cap_b, _lib.ptr(sz), cap_n, ctypes.byref(nr),
+                                  ctypes.byref(nb))
+        if rc == -4:  # MANDO_E_CAP: the sizes are returned
+            cap_n, cap_b = max(1, nr.value), max(1, nb.value)
+            continue
+        if rc != 0:
+            break
+        roots = [os.fsdecode(x) for x in names.raw[:nb.value].split(b"\0")[:-1]]
+        if sizes is not None:
+            for r, v in zip(roots, sz[:nr.value].tolist()):
+                if v >= 0:
+                    sizes[r] = v
+        return roots
+    return _roots_py(out_tmp, sizes)
+
+
+def _roots_py(out_tmp: str, sizes: dict | None = None) -> list[str]:
     roots = set()
     with os.scandir(out_tmp) as it:
         for e in it:

@@ -53,3 +53,31 @@ def test_mando_cli_P_then_D(tmp_path):
     assert mando.main(["-p", str(tmp_path), "-f", str(fa), "-M", "P"]) == 0
     assert sorted(os.listdir(tmp / "tmp_SS")) == sorted(GOLD["loci"])
     assert hashlib.sha256(open(tmp / "mm2Alignments.clean.sorted.psl", "rb").read()).hexdigest() == GOLD["sorted_sha256"]
+
+
+def test_list_roots_matches_reference_scan(tmp_path):
+    """mando_list_roots (native scan + stat + sort) == the reference's roots loop (defineIsoforms.py:130-139)
+    restated in define._roots_py: sizes only for exact <root>.psl files, '.psl' cut at its first
+    occurrence, directories skipped, symlinks followed, (chrom, int(start)) order."""
+    import random
+
+    from mandalorion_amd import define
+
+    d = tmp_path / "tmp_SS"
+    d.mkdir()
+    rng = random.Random(5)
+    for i in range(3000):
+        c = rng.choice(["chr1", "chr10", "chr2", "chrX", "chrUn_KI270742v1", "é_chr"])
+        s = rng.randrange(0, 10 ** 9)
+        (d / f"{c}~{s}~{s + rng.randrange(1, 10 ** 5)}.psl").write_bytes(b"x" * rng.randrange(0, 50))
+    (d / "chr1~5~9.psl.bak").write_bytes(b"ab")
+    (d / "chr1~7~9.pslx").write_bytes(b"")
+    (d / "dir.psl").mkdir()
+    (d / "chr9~1~2.psl").symlink_to(d / "chr1~7~9.pslx")
+    s1, s2 = {}, {}
+    assert define._roots(str(d), s1) == define._roots_py(str(d), s2)
+    assert s1 == s2
+    # a start Python's int() reads but the native parse does not: the reference's own parse decides
+    (d / "chr3~ 0012~40.psl").write_bytes(b"")
+    s1, s2 = {}, {}
+    assert define._roots(str(d), s1) == define._roots_py(str(d), s2) and s1 == s2
