@@ -190,7 +190,7 @@ class Assembly:
 
 
 def _fasta_and_r2i(name_src, name_sel, name_start, name_len, mem_off, cons_src, cons_sel, cons_start, cons_len,
-                   cons_rc, counter0: int = 0):
+                   cons_rc, counter0: int = 0, fasta_part: bool = True, r2i_part: bool = True):
     """Isoform_Consensi.fasta and reads2isoforms.txt bytes for isoforms in output order
     (defineIsoforms.py:155-166): '>Isoform{k}_{n}\n{consensus}\n' and '{name}\tIsoform{k}_{n}\n'.
     Consensi and names are byte segments of several sources (locus texts, POA outputs), gathered once."""
@@ -207,16 +207,11 @@ def _fasta_and_r2i(name_src, name_sel, name_start, name_len, mem_off, cons_src, 
     nl_pos = len(head)
     sl = hl.copy()  # "\t" + label + "\n" has the same length as ">" + label + "\n"
     ss = nl_pos + 1 + hs
-    # FASTA: [header (aux)] [consensus (its source)] ["\n" (aux)] per isoform; sources: 0 aux, 1.. cons
-    srcs = [aux] + list(cons_src)
-    sel = np.empty(3 * n_iso, dtype=np.int16)
-    st = np.empty(3 * n_iso, dtype=np.int64)
-    ln = np.empty(3 * n_iso, dtype=np.int64)
-    rc = np.zeros(3 * n_iso, dtype=np.int8)
-    sel[0::3], st[0::3], ln[0::3] = 0, hs, hl
-    sel[1::3], st[1::3], ln[1::3], rc[1::3] = 1 + np.asarray(cons_sel), cons_start, cons_len, cons_rc
-    sel[2::3], st[2::3], ln[2::3] = 0, nl_pos, 1
-    fasta, _ = _lib.pack_segments(srcs, st, ln, sel=sel, rc=rc)
+    fasta = r2i = None
+    if fasta_part:
+        fasta = _fasta_bytes(aux, hs, hl, nl_pos, cons_src, cons_sel, cons_start, cons_len, cons_rc)
+    if not r2i_part:
+        return fasta, None
     # reads2isoforms: [name (its source)] [suffix (aux)] per member
     m = int(mem_off[-1])
     iso_of_mem = np.repeat(np.arange(n_iso), n_mem)
@@ -227,6 +222,21 @@ def _fasta_and_r2i(name_src, name_sel, name_start, name_len, mem_off, cons_src, 
     sel[1::2], st[1::2], ln[1::2] = 0, ss[iso_of_mem], sl[iso_of_mem]
     r2i, _ = _lib.pack_segments([aux] + list(name_src), st, ln, sel=sel)
     return fasta, r2i
+
+
+def _fasta_bytes(aux, hs, hl, nl_pos, cons_src, cons_sel, cons_start, cons_len, cons_rc):
+    n_iso = len(hs)
+    # FASTA: [header (aux)] [consensus (its source)] ["\n" (aux)] per isoform; sources: 0 aux, 1.. cons
+    srcs = [aux] + list(cons_src)
+    sel = np.empty(3 * n_iso, dtype=np.int16)
+    st = np.empty(3 * n_iso, dtype=np.int64)
+    ln = np.empty(3 * n_iso, dtype=np.int64)
+    rc = np.zeros(3 * n_iso, dtype=np.int8)
+    sel[0::3], st[0::3], ln[0::3] = 0, hs, hl
+    sel[1::3], st[1::3], ln[1::3], rc[1::3] = 1 + np.asarray(cons_sel), cons_start, cons_len, cons_rc
+    sel[2::3], st[2::3], ln[2::3] = 0, nl_pos, 1
+    fasta, _ = _lib.pack_segments(srcs, st, ln, sel=sel, rc=rc)
+    return fasta
 
 
 def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", splice_site_width: int = 1,
@@ -397,8 +407,29 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             ThreadPoolExecutor(max_workers=n_poa) as gpu_poa:
         cl = [ex.submit(run_cluster, lo, hi) for lo, hi in spans]
         poa_futs = []
+        # one rank: reads2isoforms.txt needs only the clustering, so each chunk's part of it is written
+        # by the host thread (after the chunk's assembly) while the POA runs; the FASTA follows each POA
+        fa = r2 = None
+        r2_futs = []
+        n_iso_before = 0
+        if world == 1:
+            fa = open(out_path + "/Isoform_Consensi.fasta", "wb")
+            r2 = open(out_path + "/reads2isoforms.txt", "wb")
+
+        def write_r2i(res, lo, hi, counter0):
+            tw = time.perf_counter()
+            _write_payload(_names_payload(res, mine[lo:hi]), None, r2, counter0)
+            timeline.append(("write_r2i", tw - t0, time.perf_counter() - t0))
         for k, (lo, hi) in enumerate(spans):
-            res, tcl, (o_a, o_b), tpk = cl[k].result()
+            try:
+                res, tcl, (o_a, o_b), tpk = cl[k].result()
+            except BaseException:
+                if fa is not None:
+                    for f in r2_futs:
+                        f.exception()
+                    fa.close()
+                    r2.close()
+                raise
             add("t_cluster", tcl)
             add("t_pack", tpk)
             tg = time.perf_counter()
@@ -411,20 +442,27 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             add("t_orient", te - tg)
             asm_fut = host.submit(assemble, res, hits, n_hits)
             poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
+            if world == 1:
+                r2_futs.append(host.submit(write_r2i, res, lo, hi, n_iso_before))
+                n_iso_before += res.n_isoforms
         results = []
         if world == 1:
             # one rank: chunks are contiguous runs of the sorted roots and finish in order, so each
-            # chunk's part of both files is written as soon as its POA is done (while the next runs)
+            # chunk's FASTA part is written as soon as its POA is done (while the next runs)
             written = 0
-            with open(out_path + "/Isoform_Consensi.fasta", "wb") as fa, \
-                    open(out_path + "/reads2isoforms.txt", "wb") as r2:
+            try:
                 for f in poa_futs:
                     pl, res = f.result()
                     results.append(res)
                     tw = time.perf_counter()
-                    written += _write_payload(pl, fa, r2, written)
+                    written += _write_payload(pl, fa, None, written)
                     timeline.append(("write", tw - t0, time.perf_counter() - t0))
                     del pl
+                for f in r2_futs:
+                    f.result()
+            finally:
+                fa.close()
+                r2.close()
             stats["written_isoforms"] = written
         else:
             for f in poa_futs:
@@ -455,7 +493,8 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
 
 def _write_payload(payload: dict, fa, r2, counter0: int) -> int:
     """Appends a payload's isoforms to both files in output order (sorted roots x IsoDict order,
-    defineIsoforms.py:155-166), numbering from counter0 + 1; returns the isoform count."""
+    defineIsoforms.py:155-166), numbering from counter0 + 1; returns the isoform count.  fa or r2 None:
+    that file is skipped (reads2isoforms needs only the clustering, so one rank writes it ahead)."""
     order = np.argsort(payload["iso_root"], kind="stable")
     mo = payload["mem_off"]
     cnt = np.diff(mo)[order]
@@ -464,12 +503,19 @@ def _write_payload(payload: dict, fa, r2, counter0: int) -> int:
     # member rows in output order: for each isoform in `order`, mo[i] .. mo[i+1]-1
     midx = (np.repeat(mo[:-1][order] - new_off[:-1], cnt) + np.arange(int(new_off[-1]))
             if len(order) else np.zeros(0, np.int64))
-    fasta, r2i = _fasta_and_r2i(payload["name_src"], payload["n_sel"][midx], payload["n_start"][midx],
-                                payload["n_len"][midx], new_off, payload["cons_src"], payload["c_sel"][order],
-                                payload["c_start"][order], payload["c_len"][order], payload["c_rc"][order],
-                                counter0=counter0)
-    fa.write(memoryview(np.ascontiguousarray(fasta)))
-    r2.write(memoryview(np.ascontiguousarray(r2i)))
+    if fa is not None:
+        cons = [payload[k][order] for k in ("c_sel", "c_start", "c_len", "c_rc")]
+    else:
+        cons = [None] * 4
+    fasta, r2i = _fasta_and_r2i(payload["name_src"], payload["n_sel"][midx] if r2 is not None else None,
+                                payload["n_start"][midx] if r2 is not None else None,
+                                payload["n_len"][midx] if r2 is not None else None, new_off,
+                                payload.get("cons_src"), *cons, counter0=counter0, fasta_part=fa is not None,
+                                r2i_part=r2 is not None)
+    if fa is not None:
+        fa.write(memoryview(np.ascontiguousarray(fasta)))
+    if r2 is not None:
+        r2.write(memoryview(np.ascontiguousarray(r2i)))
     return int(len(order))
 
 
@@ -500,11 +546,16 @@ def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, run_po
         stats["records"] += int(res.n_records)
         stats["poa_reads"] += int(p_grp[-1])
         stats["t_poa"] += t4 - t3
+    return dict(_names_payload(res, root_idx), cons_src=[res.text, cons], c_sel=c_sel.astype(np.int16),
+                c_start=c_start, c_len=c_len, c_rc=c_rc)
+
+
+def _names_payload(res: cluster.ClusterResult, root_idx: Sequence[int]) -> dict:
+    """The part of a chunk's writer payload that the clustering alone fixes (isoform order, member names)."""
     ri = np.asarray(root_idx, dtype=np.int64)
     n_mem = int(res.mem_off[-1])
-    return dict(iso_root=ri[res.iso_locus] if n_iso else np.zeros(0, np.int64),
-                cons_src=[res.text, cons], c_sel=c_sel.astype(np.int16), c_start=c_start, c_len=c_len, c_rc=c_rc,
-                name_src=[res.text], n_sel=np.zeros(n_mem, np.int16), n_start=res.name_off[res.mem],
+    return dict(iso_root=ri[res.iso_locus] if res.n_isoforms else np.zeros(0, np.int64), name_src=[res.text],
+                n_sel=np.zeros(n_mem, np.int16), n_start=res.name_off[res.mem],
                 n_len=res.name_len[res.mem].astype(np.int64), mem_off=res.mem_off)
 
 
