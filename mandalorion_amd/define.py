@@ -166,12 +166,25 @@ class Assembly:
         self.seeding = np.zeros(len(self.poa_iso), dtype=np.uint8)
         if len(self.poa_iso):
             lens = res.seq_len[res.sub].astype(np.int64)
-            gid = np.repeat(np.arange(n_iso), np.diff(sub_off))
-            srt = np.sort((gid.astype(np.int64) << 32) | lens) & 0xffffffff  # lens sorted inside groups
-            lo = sub_off[:-1] + (np.diff(sub_off) - 1) // 2
-            hi = sub_off[:-1] + np.diff(sub_off) // 2
-            med2 = srt[np.minimum(lo, max(n_sub - 1, 0))] + srt[np.minimum(hi, max(n_sub - 1, 0))]
-            self.seeding = (med2[self.poa_iso] >= 16000).astype(np.uint8)
+            m = np.diff(sub_off)
+            # the median can reach 8000 only when the upper middle value does, i.e. when at least
+            # ceil(m/2) of the group's reads are >= 8000; only those groups are sorted
+            n8k = (np.add.reduceat((lens >= 8000).astype(np.int64), np.minimum(sub_off[:-1], n_sub - 1)) if n_sub
+                   else np.zeros(n_iso, np.int64))
+            n8k = np.where(m > 0, n8k, 0)
+            cand = np.zeros(n_iso, dtype=bool)
+            cand[self.poa_iso] = True
+            cand &= n8k >= m - m // 2
+            if cand.any():
+                gid = np.repeat(np.arange(n_iso), m)
+                keep = cand[gid]
+                srt = np.sort((gid[keep].astype(np.int64) << 32) | lens[keep]) & 0xffffffff  # sorted inside groups
+                co = np.zeros(n_iso + 1, dtype=np.int64)
+                np.cumsum(np.where(cand, m, 0), out=co[1:])
+                ci = np.nonzero(cand)[0]
+                med2 = np.zeros(n_iso, dtype=np.int64)
+                med2[ci] = srt[co[ci] + (m[ci] - 1) // 2] + srt[co[ci] + m[ci] // 2]
+                self.seeding = (med2[self.poa_iso] >= 16000).astype(np.uint8)
         self.res = res
 
     def poa_segments(self):
