@@ -417,6 +417,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
 
     n_poa = int(os.environ.get("MANDO_POA_STREAMS", "2")) if len(spans) > 1 else 1
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
+            ThreadPoolExecutor(max_workers=1) as writer, \
             ThreadPoolExecutor(max_workers=n_poa) as gpu_poa:
         cl = [ex.submit(run_cluster, lo, hi) for lo, hi in spans]
         poa_futs = []
@@ -429,53 +430,64 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             fa = open(out_path + "/Isoform_Consensi.fasta", "wb")
             r2 = open(out_path + "/reads2isoforms.txt", "wb")
 
+        fa_futs = []
+
+        def write_fasta(poa_fut, counter0):
+            # one rank: the writer thread appends each chunk's FASTA part as soon as its POA is done (in
+            # chunk order: one thread, FIFO), off the main thread that orients the next chunk meanwhile
+            pl, res = poa_fut.result()
+            tw = time.perf_counter()
+            n = _write_payload(pl, fa, None, counter0)
+            timeline.append(("write", tw - t0, time.perf_counter() - t0))
+            return n, res
+
         def write_r2i(res, lo, hi, counter0):
             tw = time.perf_counter()
             _write_payload(_names_payload(res, mine[lo:hi]), None, r2, counter0)
             timeline.append(("write_r2i", tw - t0, time.perf_counter() - t0))
-        for k, (lo, hi) in enumerate(spans):
-            try:
+        def close_outputs():
+            if fa is not None:
+                for f in r2_futs + fa_futs:
+                    f.exception()
+                fa.close()
+                r2.close()
+
+        try:
+            for k, (lo, hi) in enumerate(spans):
                 res, tcl, (o_a, o_b), tpk = cl[k].result()
-            except BaseException:
-                if fa is not None:
-                    for f in r2_futs:
-                        f.exception()
-                    fa.close()
-                    r2.close()
-                raise
-            add("t_cluster", tcl)
-            add("t_pack", tpk)
-            tg = time.perf_counter()
-            if dev_orient:
-                hits, n_hits = gpu_orient_segments(res, o_a, o_b, res.sub_off, device=device)
-            else:
-                hits, n_hits = orient_fn(o_a, o_b, res.sub_off)
-            te = time.perf_counter()
-            timeline.append(("orient", tg - t0, te - t0))
-            add("t_orient", te - tg)
-            asm_fut = host.submit(assemble, res, hits, n_hits)
-            poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
-            if world == 1:
-                r2_futs.append(host.submit(write_r2i, res, lo, hi, n_iso_before))
-                n_iso_before += res.n_isoforms
+                add("t_cluster", tcl)
+                add("t_pack", tpk)
+                tg = time.perf_counter()
+                if dev_orient:
+                    hits, n_hits = gpu_orient_segments(res, o_a, o_b, res.sub_off, device=device)
+                else:
+                    hits, n_hits = orient_fn(o_a, o_b, res.sub_off)
+                te = time.perf_counter()
+                timeline.append(("orient", tg - t0, te - t0))
+                add("t_orient", te - tg)
+                asm_fut = host.submit(assemble, res, hits, n_hits)
+                poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
+                if world == 1:
+                    r2_futs.append(host.submit(write_r2i, res, lo, hi, n_iso_before))
+                    fa_futs.append(writer.submit(write_fasta, poa_futs[-1], n_iso_before))
+                    n_iso_before += res.n_isoforms
+        except BaseException:
+            close_outputs()
+            raise
         results = []
         if world == 1:
-            # one rank: chunks are contiguous runs of the sorted roots and finish in order, so each
-            # chunk's FASTA part is written as soon as its POA is done (while the next runs)
+            # one rank: chunks are contiguous runs of the sorted roots and finish in order; both files
+            # were written chunk by chunk by the host and writer threads
             written = 0
             try:
-                for f in poa_futs:
-                    pl, res = f.result()
+                for f in fa_futs:
+                    n, res = f.result()
                     results.append(res)
-                    tw = time.perf_counter()
-                    written += _write_payload(pl, fa, None, written)
-                    timeline.append(("write", tw - t0, time.perf_counter() - t0))
-                    del pl
+                    written += n
                 for f in r2_futs:
                     f.result()
             finally:
-                fa.close()
-                r2.close()
+                close_outputs()
             stats["written_isoforms"] = written
         else:
             for f in poa_futs:
