@@ -947,10 +947,25 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
     a.gscratch = nullptr;
     std::vector<int32_t> st((size_t)n_groups);
     std::vector<int32_t> redo;
+    // the first launch takes the groups largest first (bases of the group's reads): the waves pull
+    // groups from a queue, so the launch then ends on small groups instead of a late large one
+    bool first = true;
+    if (n_groups > 1) {
+        std::vector<int64_t> key((size_t)n_groups);
+        for (int64_t g = 0; g < n_groups; ++g)
+            key[(size_t)g] = (int64_t)(seq_off[grp_off[g + 1]] - seq_off[grp_off[g]]) << 24 | (int64_t)(n_groups - 1 - g);
+        std::vector<int32_t> order((size_t)n_groups);
+        for (int64_t g = 0; g < n_groups; ++g) order[(size_t)g] = (int32_t)g;
+        std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return key[(size_t)x] > key[(size_t)y]; });
+        if ((rc = ctx->o_gidx.ensure(sizeof(int32_t) * order.size())) != MANDO_OK) return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->o_gidx.p, order.data(), sizeof(int32_t) * order.size(), hipMemcpyHostToDevice,
+                               ctx->stream));
+        a.gidx = ctx->o_gidx.as<int32_t>();
+    }
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
     ctx->last_launches = 0;
     for (;;) {
-        const int64_t ng = a.gidx ? (int64_t)redo.size() : n_groups;
+        const int64_t ng = first ? n_groups : (int64_t)redo.size();
         a.n_groups = (int32_t)ng;
         const int slots = (int)std::min<int64_t>(ng, (int64_t)ctx->n_cu * mando::orient_blocks_per_cu(a.cap));
         HIP_TRY(hipMemsetAsync(ctx->counter.p, 0, sizeof(int32_t), ctx->stream));
@@ -961,13 +976,14 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         const std::vector<int32_t> prev = redo;
         redo.clear();
-        if (a.gidx) {
+        if (!first) {
             for (int32_t g : prev)
                 if (st[(size_t)g] != 0) redo.push_back(g);
         } else {
             for (int64_t g = 0; g < n_groups; ++g)
                 if (st[(size_t)g] != 0) redo.push_back((int32_t)g);
         }
+        first = false;
         if (redo.empty()) break;
         if (a.cap >= mando::kOrientCapMax)
             return fail(MANDO_E_UNSUPPORTED, "orientation: group " + std::to_string(redo[0]) + " has a read with more than " +
