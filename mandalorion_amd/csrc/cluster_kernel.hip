@@ -2526,6 +2526,25 @@ namespace {
 // none with hipMalloc'd buffers), and a hipFree per call would wait for the whole device.
 std::mutex g_buf_mu;
 std::map<std::pair<const mando_ctx *, int>, std::pair<void *, size_t>> g_bufs;
+// pinned host buffers per context (the K2 output region comes back through one, reused: a fresh
+// pageable vector of that size -- ~25 KB per locus, 0.35 GB per config-3 chunk -- was zero-filled and
+// page-faulted on every call, on the path between the clustering kernels and the orientation launch)
+std::map<std::pair<const mando_ctx *, int>, std::pair<void *, size_t>> g_pinned;
+hipError_t pinned_host(const mando_ctx *ctx, int id, size_t n, uint8_t *&p) {
+    std::lock_guard<std::mutex> g(g_buf_mu);
+    auto &e = g_pinned[{ctx, id}];
+    if (!e.first || e.second < n) {
+        if (e.first) (void)hipHostFree(e.first);
+        e = {nullptr, 0};
+        const size_t cap = n + n / 4;
+        void *q = nullptr;
+        const hipError_t r = hipHostMalloc(&q, cap, hipHostMallocDefault);
+        if (r != hipSuccess) return r;
+        e = {q, cap};
+    }
+    p = static_cast<uint8_t *>(e.first);
+    return hipSuccess;
+}
 
 struct DevMem {
     const mando_ctx *ctx;
@@ -2779,10 +2798,11 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         G.out = d_o.as<uint8_t>();
         G.rec_text = d_rec.as<int64_t>();
         CL_TRY(launch_locus(G, (int)k2_order.size(), s));
-        std::vector<uint8_t> ho((size_t)o_tot + 256);
+        uint8_t *ho = nullptr;
+        CL_TRY(pinned_host(ctx, 0, (size_t)o_tot + 256, ho));
         out.rec_text.resize((size_t)recs * 4);
         CL_TRY(hipMemcpyAsync(st.data(), d_stats.p, (size_t)nl * sizeof(Stats), hipMemcpyDeviceToHost, s));
-        CL_TRY(hipMemcpyAsync(ho.data(), d_o.p, (size_t)o_tot, hipMemcpyDeviceToHost, s));
+        CL_TRY(hipMemcpyAsync(ho, d_o.p, (size_t)o_tot, hipMemcpyDeviceToHost, s));
         if (recs) CL_TRY(hipMemcpyAsync(out.rec_text.data(), d_rec.p, (size_t)recs * 32, hipMemcpyDeviceToHost, s));
         CL_TRY(hipStreamSynchronize(s));
         if (timing)
@@ -2802,7 +2822,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
             const Locus &x = L[(size_t)i];
             int64_t op, onm, om, ons, os;
             o_offsets(y, x, &op, &onm, &om, &ons, &os);
-            const uint8_t *base = ho.data() + x.o_off;
+            const uint8_t *base = ho + x.o_off;
             out.peaks[(size_t)i].assign((const Peak *)(base + op), (const Peak *)(base + op) + y.n_peaks);
             out.iso_nmem[(size_t)i].assign((const int32_t *)(base + onm), (const int32_t *)(base + onm) + y.n_iso);
             out.mem[(size_t)i].assign((const int32_t *)(base + om), (const int32_t *)(base + om) + y.n_mem);
