@@ -147,7 +147,14 @@ class Assembly:
         nh = np.asarray(n_hits, dtype=np.int64)[:n_sub]
         H = hits.shape[1]
         valid = np.arange(H)[None, :] < nh[:, None]
-        signs = np.cumprod(np.where(valid, hits.astype(np.int64), 1), axis=1)
+        # running product of the hit strands (+1 / -1) along each read's hits, one column at a time
+        # (np.cumprod along the short axis took ~45 ms on a config-3 chunk)
+        signs = np.empty((n_sub, H), dtype=np.int8)
+        acc = np.ones(n_sub, dtype=np.int8)
+        for c in range(min(H, int(nh.max()) if n_sub else 0)):
+            acc = acc * np.where(valid[:, c], hits[:, c], 1).astype(np.int8)
+            signs[:, c] = acc
+        signs[:, min(H, int(nh.max()) if n_sub else 0):] = 1
         self.e_read = np.repeat(np.arange(n_sub), nh)            # emission -> subsample slot
         self.e_sign = signs[valid]                                # row-major = hit order per read
         iso_of_sub = np.repeat(np.arange(n_iso), np.diff(sub_off))
