@@ -298,6 +298,10 @@ def main():
                 "reads_per_s": sum(x["reads"] for x in la) / (k_ms / 1e3) if k_ms > 0 else None,
             },
             "gpu_equals_cpu_on_sample": parity,
+            # per timed step (rank 0): the D module's own wall time and its POA kernels' event time, so a
+            # slow step shows where it lost its time
+            "steps_s": [round(x["t_total"], 4) for x in stats],
+            "steps_poa_kernel_ms": [round(sum(y["kernel_ms"] for y in x["poa_launches"]), 1) for x in stats],
         },
         "roofline": {
             "bound": bound,
