@@ -67,8 +67,10 @@ struct PinnedPool {
         if (!p) return;
         std::lock_guard<std::mutex> g(mu);
         free_list.push_back({p, cap});
-        // keep at most the two largest buffers (two chunks in flight)
-        while (free_list.size() > 2) {
+        // keep the four largest buffers: two chunks in flight, plus the previous call's two when their
+        // release (a background thread in the D driver) comes late -- a free() while the next call's
+        // chunks are being read would otherwise recur
+        while (free_list.size() > 4) {
             auto it = std::min_element(free_list.begin(), free_list.end(),
                                        [](const auto &a, const auto &b) { return a.second < b.second; });
             free(it->first);

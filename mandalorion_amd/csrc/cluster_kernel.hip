@@ -2860,7 +2860,10 @@ void release_text(mando_ctx *ctx, void *d_text, size_t cap) {
     if (!d_text) return;
     std::lock_guard<std::mutex> g(g_buf_mu);
     g_text_free.push_back({d_text, cap});
-    while (g_text_free.size() > 2) {  // two chunks in flight
+    // four: two chunks in flight plus the previous call's two when their release comes late.  A
+    // hipFree here synchronises the device and holds the runtime while the next call's POA grids run;
+    // steps whose POA launches were measured 1.2-2.4x longer by their events are the suspected cost
+    while (g_text_free.size() > 4) {
         auto it = std::min_element(g_text_free.begin(), g_text_free.end(),
                                    [](const auto &a, const auto &b) { return a.second < b.second; });
         (void)hipFree(it->first);

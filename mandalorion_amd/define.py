@@ -422,7 +422,11 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         timeline.append(("poa", tp - t0, time.perf_counter() - t0))
         return pl, res
 
-    n_poa = int(os.environ.get("MANDO_POA_STREAMS", "2")) if len(spans) > 1 else 1
+    # one POA host thread (one device context) by default: with two, a chunk whose predecessor's POA
+    # ran late went to the second context, whose workspace was then sized from the HBM the first one
+    # left free -- a quarter of the slots, the persistent grid, 2.9 s instead of 1.1 s (measured in 3 of
+    # 30 config-3 steps; none in 18 with one context)
+    n_poa = int(os.environ.get("MANDO_POA_STREAMS", "1")) if len(spans) > 1 else 1
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
             ThreadPoolExecutor(max_workers=1) as writer, \
             ThreadPoolExecutor(max_workers=n_poa) as gpu_poa:
