@@ -406,9 +406,9 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         return prep
 
     # Staged pipeline over chunks: clustering (one host thread driving the C++ pool, chunks in order) ->
-    # orientation (main thread, GPU slot 1) -> emission assembly (host thread) -> POA (two host threads,
-    # GPU slots 0 and 3: chunk k+1's POA kernel is queued while chunk k's persistent grid drains, so
-    # its waves fill the CUs chunk k's tail leaves idle) -> compaction (host thread).
+    # orientation (main thread, GPU slot 1) -> emission assembly (host thread) -> POA (one host thread,
+    # GPU slot 0, by default; MANDO_POA_STREAMS=2 adds a second on slot 3 so that chunk k+1's grids can
+    # be queued while chunk k's drain) -> compaction (host thread).
     lock = threading.Lock()
 
     def add(key, v):
