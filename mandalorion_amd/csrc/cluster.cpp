@@ -263,6 +263,26 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
             res->seq_len[(size_t)r] = (int32_t)t[3];
             res->rec_locus[(size_t)r] = i;
         }
+    // exact sizes first: the per-locus appends below then never reallocate
+    size_t n_iso = 0, n_mem = 0, n_sub = 0, n_pk = 0;
+    for (int64_t i = 0; i < n_loci; ++i) {
+        if (o.status[(size_t)i] != cl::kOk) continue;
+        n_iso += o.iso_nmem[(size_t)i].size();
+        n_mem += o.mem[(size_t)i].size();
+        n_sub += o.sub[(size_t)i].size();
+        n_pk += o.peaks[(size_t)i].size();
+    }
+    res->iso_locus.reserve(n_iso);
+    res->mem_off.reserve(n_iso + 1);
+    res->sub_off.reserve(n_iso + 1);
+    res->mem.reserve(n_mem);
+    res->sub.reserve(n_sub);
+    res->peak_locus.reserve(n_pk);
+    res->peak_start.reserve(n_pk);
+    res->peak_end.reserve(n_pk);
+    res->peak_type.reserve(n_pk);
+    res->peak_side.reserve(n_pk);
+    res->peak_prop.reserve(n_pk);
     res->mem_off.push_back(0);
     res->sub_off.push_back(0);
     res->locus_status = o.status;
