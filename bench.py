@@ -19,6 +19,17 @@ driver with the CPU restatements (oracle/) injected for orientation and POA, on 
 the same loci, on the box's host cores (rank 0, N=1 only).  That sample's GPU output must be
 byte-identical to the CPU run's.
 
+Launch: under a launcher (WORLD_SIZE set) each process is one rank.  `--gpus N` without one spawns the N
+rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set per child, before anything in the
+parent touches a GPU) and exits with the worst child status.  With N > 1 every rank must end up on RCCL
+(`comm.backend == "rccl"`), else the run fails; `n_gpus` is the communicator's world size.
+`--check-launch` stops after the rendezvous, the data and the LPT plan (no GPU compute): it prints the
+ranks, their backend and their loci, and runs without a device (host transport).
+
+Output parity: after the timed steps the two files of the last step are hashed and compared with
+tests/golden/fullsize_hashes.json (the oracle's output on the same full-size workload, computed in the
+build container by tests/golden/make_fullsize_hashes.py); a mismatch fails the run.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -37,6 +48,32 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
+FULLSIZE_HASHES = os.path.join(ROOT, "tests", "golden", "fullsize_hashes.json")
+# the sources whose code the PMC traffic of profiles/pmc_latest.json describes
+POA_SOURCES = ("poa_kernel.hip", "poa_kernel.h", "seed_kernel.hip", "capi.hip")
+
+
+def poa_sources_sha() -> str:
+    h = hashlib.sha256()
+    for f in POA_SOURCES:
+        with open(os.path.join(ROOT, "mandalorion_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def host_cores() -> dict:
+    """The host CPUs this process may use: affinity, capped by the cgroup CPU quota (cpu.max), and the
+    machine's count (os.cpu_count(), which on the GPU box is the whole host, many times our share)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota": quota, "usable": usable}
 
 WORKLOADS = {
     # BASELINE.json configs[1]: SIRV-like spike-in set, 7 genes x ~10 isoforms, ~50k R2C2 reads
@@ -70,6 +107,9 @@ def parse():
     ap.add_argument("--data-dir", default="", help="where the synthetic tmp_SS goes (default $TMPDIR)")
     ap.add_argument("--threads", type=int, default=0, help="host threads per rank (0: 16 / ranks per node)")
     ap.add_argument("--cpu-loci", type=int, default=640, help="cpu_baseline sample size (loci)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0: the usable host cores)")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="launch, rendezvous, data and shard plan only (no GPU compute); prints the ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return ap.parse_args()
@@ -189,16 +229,71 @@ def cpu_baseline(data: str, n_loci: int, threads: int):
     return out, d, hashes
 
 
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: N rank processes of this script, one per GPU (LOCAL_RANK = GPU),
+    started before this parent touches a GPU; returns the worst exit status."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs) if any(codes) else 0
+
+
+def shard_plan(data: str, world: int) -> list:
+    """The driver's LPT plan (define.define_isoforms): loci per rank, for --check-launch."""
+    from mandalorion_amd import define
+
+    roots = define._roots(os.path.join(data, "tmp_SS"))
+    cost = define._locus_costs(os.path.join(data, "tmp_SS"), roots)
+    load = np.zeros(world)
+    cnt = [0] * world
+    for i in np.argsort(-cost, kind="stable"):
+        k = int(np.argmin(load))
+        load[k] += cost[i]
+        cnt[k] += 1
+    return [{"rank": k, "loci": cnt[k], "cost_share": float(load[k] / max(load.sum(), 1e-9))} for k in range(world)]
+
+
+def fullsize_check(data: str, key: str):
+    """Both output files of the last step against the oracle's full-size hashes (None: no entry)."""
+    if not os.path.exists(FULLSIZE_HASHES):
+        return None
+    ref = json.load(open(FULLSIZE_HASHES)).get(key)
+    if ref is None:
+        return None
+    got = {"isoform_consensi_sha256": sha(os.path.join(data, "Isoform_Consensi.fasta")),
+           "reads2isoforms_sha256": sha(os.path.join(data, "reads2isoforms.txt"))}
+    ok = all(got[k] == ref[k] for k in got)
+    if not ok:
+        raise SystemExit(f"GPU D-module output of {key} differs from the oracle's full-size hashes: {got} vs "
+                         f"{ {k: ref[k] for k in got} }")
+    return True
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if args.gpus != 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     wl = WORKLOADS[args.workload]
     n_loci = args.loci or wl["loci"]
-    threads = args.threads or max(2, 16 // max(1, local_world) if local_world <= 8 else 2)
-    gen_threads = 16 if rank == 0 else threads
+    cores = host_cores()
+    threads = args.threads or max(2, min(16, cores["usable"]) // max(1, local_world))
+    gen_threads = min(16, cores["usable"]) if rank == 0 else threads
     base = args.data_dir or os.environ.get("TMPDIR", "/tmp")
     data = os.path.join(base, f"mando_bench_{args.workload}_{n_loci}")
     os.makedirs(data, exist_ok=True)
@@ -209,17 +304,33 @@ def main():
     if world > 1:
         from mandalorion_amd.comm import Comm
 
-        comm = Comm.from_env(device=local)
+        comm = Comm.from_env(device=local, gpu=False if args.check_launch else None)
+        if comm.backend != "rccl" and not args.check_launch:
+            raise SystemExit(f"rank {rank}: {world} ranks need the RCCL transport, got {comm.backend!r}")
+    n_gpus = comm.world if comm is not None else 1
     if rank == 0:
         records = gen_data(data, wl, n_loci, gen_threads)
     if comm is not None:
         comm.barrier()
     records = int(open(os.path.join(data, "records.txt")).read())
 
+    if args.check_launch:
+        plan = shard_plan(data, world)
+        if comm is not None:
+            comm.barrier()
+            comm.close()
+        if rank == 0:
+            print(json.dumps({"check_launch": True, "n_gpus": n_gpus, "world": world,
+                              "backend": comm.backend if comm is not None else "none", "records": records,
+                              "ranks": plan, "host_cores": cores}), flush=True)
+        return
+
     # CPU baseline first (rank 0 of a 1-GPU run): bounded sample, oracle orientation + POA on host threads
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, cpu_dir, cpu_hashes = cpu_baseline(data, min(args.cpu_loci, n_loci), 16)
+        cpu_threads = args.cpu_threads or cores["usable"]
+        cpu, cpu_dir, cpu_hashes = cpu_baseline(data, min(args.cpu_loci, n_loci), cpu_threads)
+        cpu.update(nproc=cores["nproc"], affinity=cores["affinity"], cgroup_quota=cores["cgroup_quota"])
 
     ctx = _lib.context(local)
     for _ in range(args.warmup):
@@ -235,6 +346,9 @@ def main():
         elapsed = comm.max(elapsed)
     st = stats[-1]
 
+    # the whole output of the last timed step against the oracle's full-size hashes (rank 0 wrote it)
+    full_parity = fullsize_check(data, f"{args.workload}:{n_loci}") if rank == 0 else None
+
     # roofline of the dominant kernel (POA), from this rank's launches of the last timed step:
     # algorithmic bytes per launch = 1 B traceback per DP cell + each read once + each consensus once
     la = st["poa_launches"]
@@ -242,14 +356,21 @@ def main():
     alg = sum(x["cells"] + x["read_bytes"] + x["cons_bytes"] for x in la)
     k_ms = sum(x["kernel_ms"] for x in la)
     achieved = (alg / max(1, n_launch)) / (k_ms / max(1, n_launch) / 1e3) / 1e9 if k_ms > 0 else 0.0
-    traffic = None
+    # HBM traffic from the PMC passes (tools/pmc_traffic.py), only when they were measured on this workload
+    # and on the POA sources benchmarked now
+    traffic, pmc_note = None, "no PMC file"
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
-            if pm.get("workload") == f"{args.workload}:{n_loci}":
+            if pm.get("workload") != f"{args.workload}:{n_loci}":
+                pmc_note = f"PMC file is for {pm.get('workload')}"
+            elif pm.get("poa_sources_sha256") != poa_sources_sha():
+                pmc_note = "PMC file measured on other POA sources (dropped)"
+            else:
                 traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+                pmc_note = f"PMC passes of commit {pm.get('commit', '?')}"
+        except Exception as e:  # noqa: BLE001
+            pmc_note = f"unreadable PMC file: {e}"
 
     # parity of the GPU path on the CPU baseline's sample (byte-identical output files)
     parity = None
@@ -269,7 +390,7 @@ def main():
         "metric": "consensus reads/s (whole node): PSL records / wall s of Mando.py -M D",
         "value": records * args.steps / elapsed,
         "unit": "records/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -285,9 +406,10 @@ def main():
             "isoforms": st["isoforms"],
             "poa_groups_rank0": st["poa_groups"],
             "poa_reads_rank0": st["poa_reads"],
-            "parallelism": f"loci sharded over {world} GPU(s) (LPT on the DP-cost estimate), one all-gather "
+            "parallelism": f"loci sharded over {n_gpus} GPU(s) (LPT on the DP-cost estimate), one all-gather "
                           f"({comm.backend if comm else 'none'}) to the writer on rank 0",
             "host_threads_per_rank": threads,
+            "host_cores": cores,
             "phases_rank0_s": {k: round(st[k], 4) for k in ("t_ingest", "t_cluster", "t_orient", "t_assemble", "t_poa",
                                                              "t_total") if k in st},
             "poa_kernel": {
@@ -298,6 +420,7 @@ def main():
                 "reads_per_s": sum(x["reads"] for x in la) / (k_ms / 1e3) if k_ms > 0 else None,
             },
             "gpu_equals_cpu_on_sample": parity,
+            "full_output_equals_oracle": full_parity,
             # per timed step (rank 0): the D module's own wall time and its POA kernels' event time, so a
             # slow step shows where it lost its time
             "steps_s": [round(x["t_total"], 4) for x in stats],
@@ -312,6 +435,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": pmc_note,
             "kernel": "poa_kernel",
             "note": "integer DP, no MFMA; the kernel is issue/latency-bound (SQ counters: DESIGN.md §3.1)",
         },

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <chrono>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <cstdio>
 #include <cstdlib>
@@ -2576,8 +2577,25 @@ struct DevMem {
     }
 };
 
-// the device copy of a result's locus text outlives the call: a small cache of whole buffers
-std::vector<std::pair<void *, size_t>> g_text_free;
+// the device copy of a result's locus text outlives the call: a small cache of whole buffers, each
+// tagged with the device it lives on (a process driving two GPUs must never get the other's buffer)
+struct TextBuf {
+    void *p;
+    size_t cap;
+    int dev;
+};
+std::vector<TextBuf> g_text_free;
+
+// cluster_gpu reuses per-context scratch (g_bufs) and the pinned K2 output buffer (g_pinned): calls on
+// one context are serialised here; calls on different contexts run concurrently
+std::mutex &ctx_mutex(const mando_ctx *ctx) {
+    static std::mutex mu;
+    static std::map<const mando_ctx *, std::unique_ptr<std::mutex>> m;
+    std::lock_guard<std::mutex> g(mu);
+    auto &e = m[ctx];
+    if (!e) e = std::make_unique<std::mutex>();
+    return *e;
+}
 
 #define CL_TRY(expr)                                                                             \
     do {                                                                                         \
@@ -2602,6 +2620,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     out.sub.assign((size_t)nl, {});
     out.rec_text.clear();
     if (nl == 0) return MANDO_OK;
+    std::lock_guard<std::mutex> ctx_guard(ctx_mutex(ctx));
     CL_TRY(hipSetDevice(mando::ctx_device(ctx)));
     hipStream_t s = mando::ctx_stream(ctx);
 
@@ -2834,18 +2853,19 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
 }
 
 void *acquire_text(mando_ctx *ctx, size_t need, size_t &cap) {
-    (void)ctx;
+    const int dev = mando::ctx_device(ctx);
     {
         std::lock_guard<std::mutex> g(g_buf_mu);
         size_t best = (size_t)-1;
         for (size_t i = 0; i < g_text_free.size(); ++i)
-            if (g_text_free[i].second >= need && (best == (size_t)-1 || g_text_free[i].second < g_text_free[best].second))
+            if (g_text_free[i].dev == dev && g_text_free[i].cap >= need &&
+                (best == (size_t)-1 || g_text_free[i].cap < g_text_free[best].cap))
                 best = i;
         if (best != (size_t)-1) {
-            auto e = g_text_free[best];
+            const TextBuf e = g_text_free[best];
             g_text_free.erase(g_text_free.begin() + (ptrdiff_t)best);
-            cap = e.second;
-            return e.first;
+            cap = e.cap;
+            return e.p;
         }
     }
     constexpr size_t kStep = size_t(256) << 20;
@@ -2856,17 +2876,15 @@ void *acquire_text(mando_ctx *ctx, size_t need, size_t &cap) {
 }
 
 void release_text(mando_ctx *ctx, void *d_text, size_t cap) {
-    (void)ctx;
     if (!d_text) return;
     std::lock_guard<std::mutex> g(g_buf_mu);
-    g_text_free.push_back({d_text, cap});
+    g_text_free.push_back({d_text, cap, mando::ctx_device(ctx)});
     // four: two chunks in flight plus the previous call's two when their release comes late.  A
-    // hipFree here synchronises the device and holds the runtime while the next call's POA grids run;
-    // steps whose POA launches were measured 1.2-2.4x longer by their events are the suspected cost
+    // hipFree synchronises the device, so it is kept off the common path
     while (g_text_free.size() > 4) {
         auto it = std::min_element(g_text_free.begin(), g_text_free.end(),
-                                   [](const auto &a, const auto &b) { return a.second < b.second; });
-        (void)hipFree(it->first);
+                                   [](const TextBuf &a, const TextBuf &b) { return a.cap < b.cap; });
+        (void)hipFree(it->p);
         g_text_free.erase(it);
     }
 }

@@ -484,6 +484,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                     n_iso_before += res.n_isoforms
         except BaseException:
             close_outputs()
+            _close_all(cl, poa_futs)
             raise
         results = []
         if world == 1:
@@ -497,14 +498,21 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                     written += n
                 for f in r2_futs:
                     f.result()
-            finally:
+            except BaseException:
                 close_outputs()
+                _close_all(cl, poa_futs)
+                raise
+            close_outputs()
             stats["written_isoforms"] = written
         else:
-            for f in poa_futs:
-                pl, res = f.result()
-                results.append(res)
-                payloads.append(pl)
+            try:
+                for f in poa_futs:
+                    pl, res = f.result()
+                    results.append(res)
+                    payloads.append(pl)
+            except BaseException:
+                _close_all(cl, poa_futs)
+                raise
     if world > 1:
         tm = time.perf_counter()
         payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
@@ -518,13 +526,31 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             timeline.append(("write", tw - t0, time.perf_counter() - t0))
         del payload
     stats["t_total"] = time.perf_counter() - t0
-    # the chunks' text buffers go back to the pinned pool off the caller's path
+    # the chunks' buffers go back to their pools before returning: every kernel that read them has
+    # completed (the POA calls are synchronous), and no release can then overlap the next call's kernels
     del payloads
-    threading.Thread(target=lambda rs: [r.close() for r in rs], args=(results,), daemon=True).start()
+    for r in results:
+        r.close()
+    stats["t_close"] = time.perf_counter() - t0 - stats["t_total"]
     if verbose and rank == 0:
         print("\t" + " ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in stats.items()
                                if not isinstance(v, list)))
     return stats
+
+
+def _close_all(cluster_futs, poa_futs) -> None:
+    """Error path: wait for every chunk already submitted (clustering, POA) and close the results they
+    produced, so no device text or host text buffer outlives the failed call."""
+    seen = set()
+    for f in list(poa_futs) + list(cluster_futs):
+        try:
+            r = f.result()
+        except BaseException:  # noqa: BLE001 -- the first error is the one re-raised
+            continue
+        res = r[1] if isinstance(r, tuple) and len(r) == 2 else r[0]
+        if id(res) not in seen and hasattr(res, "close"):
+            seen.add(id(res))
+            res.close()
 
 
 def _write_payload(payload: dict, fa, r2, counter0: int) -> int:

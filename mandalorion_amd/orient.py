@@ -29,7 +29,7 @@ def orient_batch(groups: Sequence[Sequence[str | bytes]], device: int = 0, max_h
     if n and int(nh[:n].max()) > max_hits:  # more primaries than max_hits: re-run with room for 8
         if max_hits >= 8:
             raise RuntimeError("a read has more than 8 primary hits")
-        return orient_batch(groups, max_hits=8)
+        return orient_batch(groups, device=device, max_hits=8)
     out, r = [], 0
     for g in groups:
         gl = []

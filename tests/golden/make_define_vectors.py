@@ -45,6 +45,10 @@ DATASETS = {
     "sirv_like": dict(n_loci=7, reads=(6500, 7500), exons=(10, 14), exon_len=(60, 200), isoforms=(9, 11),
                       rev_frac=0.3, seed=20250117),
     "long_seeded": dict(n_loci=3, reads=(5, 9), exons=(8, 10), exon_len=(950, 1150), rev_frac=0.3, seed=777),
+    # BASELINE configs[0]: 100 synthetic loci x 5 reads x ~1 kb (the reference's CPU plumbing case,
+    # Mando.py -M D -> defineIsoforms.py with Mando.py:382-399's argv)
+    "config1": dict(n_loci=100, reads=(5, 5), exons=(3, 5), exon_len=(200, 300), isoforms=(1, 1), rev_frac=0.3,
+                    seed=1001),
 }
 
 STUB_MAPPY = '''

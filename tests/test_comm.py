@@ -78,3 +78,50 @@ def test_rccl_backend_single_rank(gpu_ctx):
         b, cnt = c.allgather_bytes((np.arange(1000) % 251).astype(np.uint8))
         assert cnt.tolist() == [1000] and b.tolist() == [i % 251 for i in range(1000)]
         c.barrier()
+
+
+def _rccl_rank(rank, world, port, q):
+    import os
+
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from mandalorion_amd.comm import Comm
+
+    c = Comm.from_env(device=rank)
+    try:
+        # ragged sizes (rank 1 sends nothing): the padded ncclAllGather + per-slice compaction
+        blob = ((np.arange(rank * 70001 + 13) * (rank + 3)) % 251).astype(np.uint8) if rank != 1 else np.zeros(0, np.uint8)
+        allb, counts = c.allgather_bytes(blob)
+        m = c.max(float(rank) * 1.5)
+        c.barrier()
+        q.put((rank, counts.tolist(), allb.tobytes(), m, c.backend))
+    finally:
+        c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_rccl_allgather_multi_rank(world):
+    """Multi-rank RCCL (one process per GPU): counts all-gather, padded byte all-gather over xGMI and the
+    compaction of every rank's slice.  Needs `world` visible GPUs; skipped on a smaller box."""
+    from mandalorion_amd import _lib
+
+    if _lib.device_count() < world:
+        pytest.skip(f"{world} GPUs needed for {world} RCCL ranks")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rccl_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    sizes = [0 if r == 1 else r * 70001 + 13 for r in range(world)]
+    want = b"".join(((np.arange(sizes[r]) * (r + 3)) % 251).astype(np.uint8).tobytes() for r in range(world))
+    for rank, counts, allb, m, backend in out:
+        assert backend == "rccl"
+        assert counts == sizes
+        assert allb == want
+        assert m == 1.5 * (world - 1)

@@ -93,11 +93,22 @@ def _free_port():
     return p
 
 
-def _shard_rank(rank, world, port, d, use_oracle, q):
+def _shard_rank(rank, world, port, d, use_oracle, q, rccl=False):
     import sys
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from mandalorion_amd.comm import Comm
+
+    if rccl:  # one GPU per rank, RCCL reassembly (the product's multi-GPU path)
+        os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port))
+        c = Comm.from_env(device=rank)
+        try:
+            st = _run(d, comm=c, device=rank)
+            q.put((rank, st["isoforms"], c.backend))
+        finally:
+            c.close()
+        return
 
     kw = {}
     if use_oracle:
@@ -112,7 +123,7 @@ def _shard_rank(rank, world, port, d, use_oracle, q):
         q.put((rank, st["isoforms"], c.backend))
 
 
-def _sharded(d, use_oracle, world=2):
+def _sharded(d, use_oracle, world=2, rccl=False):
     import multiprocessing as mp
 
     for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt"):
@@ -121,7 +132,7 @@ def _sharded(d, use_oracle, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_shard_rank, args=(r, world, port, d, use_oracle, q)) for r in range(world)]
+    ps = [ctx.Process(target=_shard_rank, args=(r, world, port, d, use_oracle, q, rccl)) for r in range(world)]
     for p in ps:
         p.start()
     got = sorted(q.get(timeout=300) for _ in range(world))
@@ -160,3 +171,21 @@ def test_gpu_config4_slice_sharded_equals_one_rank(gpu_ctx, tmp_path):
     _run(d, orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
          consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci)
     assert [open(os.path.join(d, f), "rb").read() for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt")] == one
+
+
+@pytest.mark.gpu
+def test_gpu_config4_slice_two_gpus_rccl_equals_one_rank(gpu_ctx, tmp_path):
+    """Two ranks on two GPUs with the RCCL all-gather: byte-identical to the one-rank files.  Needs two
+    visible GPUs; skipped on a one-GPU box."""
+    from mandalorion_amd import _lib
+
+    if _lib.device_count() < 2:
+        pytest.skip("two GPUs needed for two RCCL ranks")
+    d = str(tmp_path / "c4")
+    synth.write_loci(os.path.join(d, "tmp_SS"), 96, threads=8, **CONFIG4_SLICE)
+    _run(d)
+    one = [open(os.path.join(d, f), "rb").read() for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt")]
+    got = _sharded(d, use_oracle=False, rccl=True)
+    assert all(g[2] == "rccl" for g in got)
+    two = [open(os.path.join(d, f), "rb").read() for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt")]
+    assert one == two

@@ -5,7 +5,10 @@ is doubled; WRITE_SIZE is taken as is.  Counter values are in KiB (rocprofv3 der
 usage: python tools/pmc_traffic.py fetch.csv write.csv WORKLOAD [out.json]"""
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from collections import defaultdict
 
 
@@ -18,13 +21,17 @@ def per_dispatch(path, counter, kernel="poa_kernel"):
 
 
 def main():
+    import bench
+
     fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
     write = per_dispatch(sys.argv[2], "WRITE_SIZE")
     f = sum(fetch) / max(len(fetch), 1) * 1024.0
     w = sum(write) / max(len(write), 1) * 1024.0
     out = {"workload": sys.argv[3], "fetch_size_bytes_raw": f, "write_size_bytes": w,
            "hbm_bytes_per_launch": 2.0 * f + w, "dispatches": [len(fetch), len(write)],
-           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; KiB -> bytes"}
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; KiB -> bytes",
+           # provenance: bench.py uses the traffic only when the POA sources it runs hash the same
+           "commit": os.environ.get("MANDO_COMMIT", "unknown"), "poa_sources_sha256": bench.poa_sources_sha()}
     dst = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_latest.json"
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out))
