@@ -35,10 +35,12 @@ namespace {
 
 // Host buffers for the locus text, kept for reuse (2 MB-aligned, transparent huge pages: a chunk's
 // few GB then costs no first-touch page faults and no munmap on the next call).  They are pageable:
-// the copies to the device are staged by the runtime.  Reusing page-locked buffers instead was
-// measured to hand the kernels stale bytes on MI355X (a rewritten pinned buffer copied again, 12 of 15
-// runs; never with fresh or pageable buffers), and pinning fresh buffers each call costs more than
-// the staging (14k loci: 1.2-1.4 s vs 0.57-0.64 s).
+// the copies to the device are staged by the runtime, and pinning fresh buffers each call costs more
+// than the staging (14k loci: 1.2-1.4 s vs 0.57-0.64 s).  Round 2 also recorded stale bytes with
+// reused page-locked buffers; that change was made together with moving the device text off the
+// stream-ordered pool, whose recycled buffers are the measured cause (cluster_kernel.hip,
+// tools/stale_probe.hip): a reused pinned source (scenario A) and a reused pinned D2H target (G, the
+// K2 output path) gave no stale byte in 15 refills each.
 struct PinnedPool {
     std::mutex mu;
     std::vector<std::pair<char *, size_t>> free_list;

@@ -2521,10 +2521,13 @@ void o_offsets(const Stats &S, const Locus &L, int64_t *peaks, int64_t *nmem, in
 
 namespace {
 
-// Device buffers are hipMalloc'd and kept per context for reuse (grown, never shrunk).  Not the
-// stream-ordered pool: memory it recycles and then refills with a host-to-device copy was measured to
-// give the kernels stale bytes on MI355X / ROCm 7.2 (a recycled text buffer, 11 of 15 repeated calls;
-// none with hipMalloc'd buffers), and a hipFree per call would wait for the whole device.
+// Device buffers are hipMalloc'd and kept per context for reuse (grown, never shrunk).  Never the
+// stream-ordered pool (hipMallocAsync / hipFreeAsync): on MI355X / ROCm 7.2 a pool buffer that is freed
+// and handed out again shows a kernel the buffer's OLD bytes after a completed host-to-device copy of
+// new ones (tools/stale_probe.hip, profiles/r03b_stale_probe.txt: 7-14 of 15 refills stale, 128 MB of
+// 512 MB at a time, even with the copy synchronised before the kernel and the device synchronised
+// before the free; never with a reused hipMalloc buffer).  That is what round 2 saw as "stale bytes"
+// on the recycled text buffer.  A hipFree per call would also wait for the whole device.
 std::mutex g_buf_mu;
 std::map<std::pair<const mando_ctx *, int>, std::pair<void *, size_t>> g_bufs;
 // pinned host buffers per context (the K2 output region comes back through one, reused: a fresh

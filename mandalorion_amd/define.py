@@ -5,15 +5,18 @@ writes <p>/Isoform_Consensi.fasta, <p>/reads2isoforms.txt and <p>/polyAWhiteList
 
 Instead of one forked process per locus calling mappy + an `abpoa` subprocess per isoform
 (defineIsoforms.py:130-153, SpliceDefineConsensus.py:876-931), the whole locus set goes through:
-  1. clustering (libmando `mando_cluster_loci`: host threads read the files, HIP kernels cluster one
-     locus per wave): peaks, isoform groups, RNG replay of every locus' draws and the
+  1. clustering (libmando `mando_cluster_loci`: host threads read the files into HBM, HIP kernels
+     cluster one locus per wave): peaks, isoform groups, RNG replay of every locus' draws and the
      determine_consensus subsample;
   2. orientation of every subsampled read against its isoform's first subsampled read
-     (`mando_orient_batch`, HIP);
+     (`mando_orient_segments`, HIP; the reads are gathered from the locus text already in HBM);
   3. the reference's per-isoform assembly logic (duplicate-primary rebinding, <=2 fallback, median
-     length -> `-S`) on the host;
-  4. one batched POA consensus over all remaining isoforms (`mando_poa_batch`, HIP);
+     length -> `-S`) on the host, on arrays;
+  4. one batched POA consensus over all remaining isoforms (`mando_poa_segments`, HIP, reads again
+     gathered from the device text);
   5. the ordered writer (sorted roots x IsoDict order, `Isoform{k}_{n}`).
+The host-packed entry points (`mando_orient_batch`, `mando_poa_batch`) serve callers holding reads in
+host memory (the abpoa-argv CLI, tests).
 Loci shard across ranks (one process per GPU, mandalorion_amd.comm); the only exchange is one all-gather
 of per-locus results to rank 0 for the writer (RCCL over xGMI).
 """

@@ -2,8 +2,8 @@
 
 Keeps the reference's command-line surface (/root/reference/Mando.py:22-205) so a pipeline that calls
 `Mando.py -M D ...` can switch over unchanged.  Only the D module (defining isoforms) is built here:
-it runs mandalorion_amd.define (clustering on host C++ threads, orientation and POA consensus on the
-GPU) with exactly the arguments Mando.py passes to defineIsoforms.py (Mando.py:382-399).  Module P
+it runs mandalorion_amd.define (clustering, orientation and POA consensus as HIP kernels on the GPU;
+the host reads the locus files and writes the outputs) with exactly the arguments Mando.py passes to defineIsoforms.py (Mando.py:382-399).  Module P
 (SAM -> PSL, clean_psl, sort + locus split: the D module's input) runs natively (mandalorion_amd.psl);
 so do modules F (isoform filters, with minimap2 as the external aligner of the consensi or an existing
 tmp/Isoforms.aligned.out.sam) and Q (quantification) (mandalorion_amd.modules).  Module A (read

@@ -69,6 +69,16 @@ static void copy_pieces(void *d, const uint8_t *h, hipStream_t s) {
     for (size_t o = 0; o < kBytes; o += piece) CK(hipMemcpyAsync((char *)d + o, h + o, piece, hipMemcpyHostToDevice, s));
 }
 
+struct Scn {
+    const char *name;
+    int src;        // 0 pinned default, 1 pinned coherent, 2 pageable
+    bool pool;      // device buffer from hipMallocAsync / hipFreeAsync on s (else one hipMalloc, reused)
+    int reader;     // 0 none, 1 kernel on s2 (event-ordered both ways), 2 kernel on s
+    bool pieces;    // 64 MB copies (else one copy)
+    bool sync_copy; // hipStreamSynchronize between the copy and the check kernel
+    bool sync_free; // hipDeviceSynchronize before the hipFreeAsync (no reliance on events)
+};
+
 int main() {
     hipStream_t s, s2;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -80,42 +90,72 @@ int main() {
     CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     void *dev;
     CK(hipMalloc(&dev, kBytes));
-    const char *names[] = {"A pinned-default reused", "B pinned-coherent reused", "C pool recycled + reader s2",
-                           "D hipMalloc reused + reader s2", "E hipMalloc reused + reader same stream",
-                           "F pageable source"};
-    for (int sc = 0; sc < 6; ++sc) {
+    const Scn scn[] = {
+        {"A pinned-default reused", 0, false, 0, true, false, false},
+        {"B pinned-coherent reused", 1, false, 0, true, false, false},
+        {"C pool recycled + reader s2", 0, true, 1, true, false, false},
+        {"D hipMalloc reused + reader s2", 0, false, 1, true, false, false},
+        {"E hipMalloc reused + reader s", 0, false, 2, true, false, false},
+        {"F pageable source", 2, false, 0, true, false, false},
+        {"C1 pool recycled, no reader", 0, true, 0, true, false, false},
+        {"C2 pool recycled + reader s", 0, true, 2, true, false, false},
+        {"C3 pool + reader s2, one copy", 0, true, 1, false, false, false},
+        {"C4 pool + reader s2, pageable src", 2, true, 1, true, false, false},
+        {"C5 pool + reader s2, sync after copy", 0, true, 1, true, true, false},
+        {"C6 pool + reader s2, device sync before free", 0, true, 1, true, false, true},
+    };
+    for (const Scn &c : scn) {
         uint8_t *h = nullptr;
-        if (sc == 0) CK(hipHostMalloc((void **)&h, kBytes, hipHostMallocDefault));
-        else if (sc == 1) CK(hipHostMalloc((void **)&h, kBytes, hipHostMallocCoherent));
-        else if (sc == 5) h = (uint8_t *)aligned_alloc(4096, kBytes);
-        else CK(hipHostMalloc((void **)&h, kBytes, hipHostMallocDefault));
+        if (c.src == 0) CK(hipHostMalloc((void **)&h, kBytes, hipHostMallocDefault));
+        else if (c.src == 1) CK(hipHostMalloc((void **)&h, kBytes, hipHostMallocCoherent));
+        else h = (uint8_t *)aligned_alloc(4096, kBytes);
         int fails = 0;
         unsigned long long worst = 0;
         for (int it = 0; it < kIters; ++it) {
             fill(h, it);
             void *d = dev;
-            if (sc == 2) CK(hipMallocAsync(&d, kBytes, s));
-            copy_pieces(d, h, s);
+            if (c.pool) CK(hipMallocAsync(&d, kBytes, s));
+            if (c.pieces) copy_pieces(d, h, s);
+            else CK(hipMemcpyAsync(d, h, kBytes, hipMemcpyHostToDevice, s));
+            if (c.sync_copy) CK(hipStreamSynchronize(s));
             const unsigned long long bad = check(d, (uint8_t)(0x10 + it), s, d_bad);
             if (bad) ++fails;
             if (bad > worst) worst = bad;
-            if (sc == 2 || sc == 3) {  // a kernel on another stream reads the buffer before it is reused
+            if (c.reader == 1) {
                 CK(hipEventRecord(ev, s));
                 CK(hipStreamWaitEvent(s2, ev, 0));
                 hipLaunchKernelGGL(reader, dim3(4096), dim3(256), 0, s2, (const uint4 *)d, kBytes / 16, d_sink);
                 CK(hipEventRecord(ev, s2));
                 CK(hipStreamWaitEvent(s, ev, 0));
-            } else if (sc == 4) {
+            } else if (c.reader == 2) {
                 hipLaunchKernelGGL(reader, dim3(4096), dim3(256), 0, s, (const uint4 *)d, kBytes / 16, d_sink);
             }
-            if (sc == 2) CK(hipFreeAsync(d, s));
+            if (c.sync_free) CK(hipDeviceSynchronize());
+            if (c.pool) CK(hipFreeAsync(d, s));
             CK(hipStreamSynchronize(s));
             CK(hipStreamSynchronize(s2));
         }
-        printf("%-40s stale iterations %2d of %d, worst %llu bytes\n", names[sc], fails, kIters, worst);
+        printf("%-46s stale iterations %2d of %d, worst %llu bytes\n", c.name, fails, kIters, worst);
         fflush(stdout);
-        if (sc == 5) free(h);
+        if (c.src == 2) free(h);
         else CK(hipHostFree(h));
+    }
+    // G: D2H into a reused pinned host buffer (the K2 output path): the kernel writes a new pattern, the
+    // copy brings it back, the CPU checks every byte
+    {
+        uint8_t *h = nullptr;
+        CK(hipHostMalloc((void **)&h, kBytes, hipHostMallocDefault));
+        int fails = 0;
+        for (int it = 0; it < kIters; ++it) {
+            CK(hipMemsetAsync(dev, 0x40 + it, kBytes, s));
+            CK(hipMemcpyAsync(h, dev, kBytes, hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+            size_t bad = 0;
+            for (size_t i = 0; i < kBytes; i += 64) bad += h[i] != (uint8_t)(0x40 + it);
+            fails += bad != 0;
+        }
+        printf("%-46s stale iterations %2d of %d\n", "G D2H into reused pinned host", fails, kIters);
+        CK(hipHostFree(h));
     }
     CK(hipFree(dev));
     return 0;
