@@ -1358,6 +1358,44 @@ __device__ __forceinline__ uint32_t pk_scan_umax(uint32_t u) {
 }
 
 
+// The traceback bytes of a lane's two cells (layout in poa_kernel.h).  Every bit of the layout is
+// "a < b" for one pair of values (M < H, X1 < H, X2 < H, F1 < H, Ho1 < X1e, Ho2 < X2e, G1 < P1,
+// G2 < P2), i.e. the sign of the saturating difference d_k = a - b, which has the sign of the exact
+// one.  v_perm's sign-replicating selectors (8..11: bit 15 / 31 of either source) turn two
+// differences into the four bytes [d0.lo, d0.hi, d1.lo, d1.hi] of 0x00 / 0xff; a mask keeps one bit
+// of each (even bits in bytes 0-1, odd bits in bytes 2-3) and the two halves are added: the low 16
+// bits are [column j0's byte, column j0 + 1's byte].
+__device__ __forceinline__ uint32_t tb_pack(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t d4,
+                                            uint32_t d5, uint32_t d6, uint32_t d7) {
+    const uint32_t x01 = __builtin_amdgcn_perm(d1, d0, 0x0B0A0908u);
+    const uint32_t x23 = __builtin_amdgcn_perm(d3, d2, 0x0B0A0908u);
+    const uint32_t x45 = __builtin_amdgcn_perm(d5, d4, 0x0B0A0908u);
+    const uint32_t x67 = __builtin_amdgcn_perm(d7, d6, 0x0B0A0908u);
+    uint32_t acc = x01 & 0x02020101u;
+    acc |= x23 & 0x08080404u;
+    acc |= x45 & 0x20201010u;
+    acc |= x67 & 0x80804040u;
+    return acc + (acc >> 16);
+}
+
+// Leftmost-argmax key of a lane's two 16-bit values hs = (H[j0], H[j0 + 1]): H * 128 + (127 - offset of
+// the column), the larger of the two (c_lo = 127 - 2 lane, c_hi = 126 - 2 lane); one v_mad_i32_i16 per
+// half (op_sel picks the high half).
+__device__ __forceinline__ int pair_key(uint32_t hs, int c_lo, int c_hi) {
+    int a, b;
+    asm("v_mad_i32_i16 %0, %1, %3, %2" : "=v"(a) : "v"(hs), "v"(c_lo), "s"(128));
+    asm("v_mad_i32_i16 %0, %1, %3, %2 op_sel:[1,0,0,0]" : "=v"(b) : "v"(hs), "v"(c_hi), "s"(128));
+    return max(a, b);
+}
+
+// A lane's store into the current row's range of a slot array: the row's base is scalar (SGPR pair),
+// the lane's byte offset an unsigned 32-bit VGPR, so the store takes the global saddr form with no
+// per-row address arithmetic on the vector unit.
+template <class T>
+__device__ __forceinline__ void row_store(gu8 *row_base, uint32_t lane_off, T v) {
+    *reinterpret_cast<GLB T *>(uniptr(row_base) + lane_off) = v;
+}
+
 // ---- 16-bit mode with scalar row control -------------------------------------------------------
 // Everything that is uniform per row (descriptor, predecessor band records, band, fast-path
 // tests, allocation) lives in SGPRs: descriptors come straight from HBM through the scalar cache
@@ -1389,8 +1427,10 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     const uint32_t LJ = (uint32_t)(2 * lane) * 0x10001u + 0x10000u;  // (j0, j0 + 1) - cb0
     const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2s(beg))) |
                                      as_u32(as_s16x2(pk2s(end)) - as_s16x2(J)));
-    const int qbyte = qnib<RW>()[j0 >> 1];
-    const uint32_t sel = (uint32_t)(qbyte & 0xf) | (((uint32_t)qbyte & 0xf0u) << 12) | 0x0C000C00u;
+    const uint32_t qbyte = qnib<RW>()[j0 >> 1];
+    // perm selector (code of j0, 0x0C, code of j0 + 1, 0x0C): the byte copied to bits 12.. puts the
+    // high nibble at bits 16-19
+    const uint32_t sel = ((qbyte * 0x1001u) & 0x000F000Fu) | 0x0C000C00u;
     const uint32_t tlo =
         R.vb < 4 ? (uint32_t)(sc.match + sc.mismatch) << (8 * R.vb) : (uint32_t)sc.mismatch * 0x01010101u;
     const uint32_t S = __builtin_amdgcn_perm((uint32_t)sc.mismatch, tlo, sel);
@@ -1473,15 +1513,15 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     const uint32_t X1e = pk_subs(X1, pk2(e1)), Ho1 = pk_subs(H, pk2(oe1));
     const uint32_t X2e = pk_subs(X2, pk2(e2)), Ho2 = pk_subs(H, pk2(oe2));
     const uint32_t E1 = pk_max(X1e, Ho1), E2 = pk_max(X2e, Ho2);
-    const uint32_t tbv = pk_ne_bit<0>(H, M) | pk_ne_bit<1>(H, X1) | pk_ne_bit<2>(H, X2) | pk_ne_bit<3>(H, F1) |
-                         pk_lt_bit<4>(Ho1, X1e) | pk_lt_bit<5>(Ho2, X2e) | pk_lt_bit<6>(G1, P1) |
-                         pk_lt_bit<7>(G2, P2);
-    *reinterpret_cast<GLB uint16_t *>(tb + (tbbase + j0)) = (uint16_t)__builtin_amdgcn_perm(0u, tbv, 0x0C0C0200u);
+    const uint32_t tbv = tb_pack(pk_subs(M, H), pk_subs(X1, H), pk_subs(X2, H), pk_subs(F1, H), pk_subs(Ho1, X1e),
+                                 pk_subs(Ho2, X2e), pk_subs(G1, P1), pk_subs(G2, P2));
+    // this row's bytes start at ds.tb_used: column j0 = cb0 + 2 lane is at tb_used + 2 lane
+    row_store<uint16_t>(tb + ds.tb_used, 2u * (uint32_t)lane, (uint16_t)tbv);
     if (R.multi) {
-        GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(kp + (kpbase + 3 * j0));
-        kq[0] = (uint16_t)__builtin_amdgcn_perm(K1, MK, 0x0C0C0400u);
-        kq[1] = (uint16_t)__builtin_amdgcn_perm(MK, K2, 0x0C0C0600u);
-        kq[2] = (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u);
+        gu8 *kq = kp + ds.kp_used;
+        row_store<uint16_t>(kq, 6u * (uint32_t)lane, (uint16_t)__builtin_amdgcn_perm(K1, MK, 0x0C0C0400u));
+        row_store<uint16_t>(kq, 6u * (uint32_t)lane + 2u, (uint16_t)__builtin_amdgcn_perm(MK, K2, 0x0C0C0600u));
+        row_store<uint16_t>(kq, 6u * (uint32_t)lane + 4u, (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u));
     }
     const uint32_t Hs = bfi(inv, kNeg2, H);
     uint32_t *wr = reinterpret_cast<uint32_t *>(ring16_row<RW>(sh, R.r & (kRing16 - 1)));
@@ -1498,9 +1538,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         svp[2 * kChunk + j0 + 1] = (int)E2 >> 16;
     }
     ds.r16acc = pk_umin(ds.r16acc, as_u32(as_u16x2(Hs) - as_u16x2(pk2(kR16Low))));
-    const int ca = ((int)(short)(Hs & 0xffff) << 7) | (127 - 2 * lane);
-    const int cbk = (((int)Hs >> 16) << 7) | (126 - 2 * lane);
-    const int mp = readlane(dpp_incl_max(max(ca, cbk), -2147483647 - 1), kWave - 1);
+    const int mp = readlane(dpp_incl_max(pair_key(Hs, 127 - 2 * lane, 126 - 2 * lane), -2147483647 - 1), kWave - 1);
     const int besti = cb0 + 127 - (mp & 127);
     ds.tb_used += R.tbw;
     if (R.multi) ds.kp_used += 3 * R.tbw;
@@ -1551,8 +1589,8 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
         const uint32_t J = (uint32_t)j0 * 0x10001u + 0x10000u;                            // (j0, j0 + 1)
         const uint32_t LJ = (uint32_t)(kChunk * h + 2 * lane) * 0x10001u + 0x10000u;      // the same - cb0
         const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(BEG)) | as_u32(as_s16x2(END) - as_s16x2(J)));
-        const int qbyte = qnib<RW>()[j0 >> 1];
-        const uint32_t sel = (uint32_t)(qbyte & 0xf) | (((uint32_t)qbyte & 0xf0u) << 12) | 0x0C000C00u;
+        const uint32_t qbyte = qnib<RW>()[j0 >> 1];
+        const uint32_t sel = ((qbyte * 0x1001u) & 0x000F000Fu) | 0x0C000C00u;
         const uint32_t S = __builtin_amdgcn_perm((uint32_t)sc.mismatch, tlo, sel);
         const int iw = (j0 >> 1) & (HW - 1), iwp = (iw - 1) & (HW - 1);
         const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0)
@@ -1644,15 +1682,15 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
         const uint32_t X1e = pk_subs(X1, pk2(e1)), Ho1 = pk_subs(H, pk2(oe1));
         const uint32_t X2e = pk_subs(X2, pk2(e2)), Ho2 = pk_subs(H, pk2(oe2));
         const uint32_t E1 = pk_max(X1e, Ho1), E2 = pk_max(X2e, Ho2);
-        const uint32_t tbv = pk_ne_bit<0>(H, Mv[h]) | pk_ne_bit<1>(H, X1) | pk_ne_bit<2>(H, X2) | pk_ne_bit<3>(H, F1) |
-                             pk_lt_bit<4>(Ho1, X1e) | pk_lt_bit<5>(Ho2, X2e) | pk_lt_bit<6>(G1v[h], P1) |
-                             pk_lt_bit<7>(G2v[h], P2);
-        *reinterpret_cast<GLB uint16_t *>(tb + (tbbase + j0)) = (uint16_t)__builtin_amdgcn_perm(0u, tbv, 0x0C0C0200u);
+        const uint32_t tbv = tb_pack(pk_subs(Mv[h], H), pk_subs(X1, H), pk_subs(X2, H), pk_subs(F1, H),
+                                     pk_subs(Ho1, X1e), pk_subs(Ho2, X2e), pk_subs(G1v[h], P1), pk_subs(G2v[h], P2));
+        row_store<uint16_t>(tb + ds.tb_used, (uint32_t)(kChunk * h + 2 * lane), (uint16_t)tbv);
         if (R.multi) {
-            GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(kp + (kpbase + 3 * j0));
-            kq[0] = (uint16_t)__builtin_amdgcn_perm(K1v[h], MKv[h], 0x0C0C0400u);
-            kq[1] = (uint16_t)__builtin_amdgcn_perm(MKv[h], K2v[h], 0x0C0C0600u);
-            kq[2] = (uint16_t)__builtin_amdgcn_perm(K2v[h], K1v[h], 0x0C0C0602u);
+            gu8 *kq = kp + ds.kp_used;
+            const uint32_t ko = (uint32_t)(3 * (kChunk * h + 2 * lane));
+            row_store<uint16_t>(kq, ko, (uint16_t)__builtin_amdgcn_perm(K1v[h], MKv[h], 0x0C0C0400u));
+            row_store<uint16_t>(kq, ko + 2u, (uint16_t)__builtin_amdgcn_perm(MKv[h], K2v[h], 0x0C0C0600u));
+            row_store<uint16_t>(kq, ko + 4u, (uint16_t)__builtin_amdgcn_perm(K2v[h], K1v[h], 0x0C0C0602u));
         }
         const uint32_t inv = invv[h];
         const uint32_t Hs = bfi(inv, kNeg2, H);
@@ -3360,6 +3398,18 @@ __global__ __launch_bounds__(kWave) void wave_selftest_kernel(int *bad) {
         if (dpp_incl_sum(v) != rsum) ++errs;
         const int prevv = lane == 0 ? 12345 : (int)(((lane - 1) * 2654435761u + trial * 40503u) % 1000u) - 500;
         if (dpp_shr1(v, 12345) != prevv) ++errs;
+        // packed-pair helpers of the 16-bit rows: argmax keys (v_mad_i32_i16 with op_sel) and the
+        // traceback bytes from sign bits (v_perm sign selectors)
+        const uint32_t seed = (uint32_t)(lane * 2246822519u + trial * 3266489917u);
+        uint32_t d[8];
+        for (int k = 0; k < 8; ++k) d[k] = (seed * (2u * k + 1u)) ^ (seed >> (k + 3)) ^ (k & 1 ? 0x80000000u : 0x8000u);
+        const uint32_t tb = tb_pack(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+        uint32_t want = 0;
+        for (int k = 0; k < 8; ++k) want |= ((d[k] >> 15) & 1u) << k | ((d[k] >> 31) & 1u) << (8 + k);
+        if ((tb & 0xffffu) != want) ++errs;
+        const uint32_t hs = d[3];
+        const int want_key = max((int)(short)(hs & 0xffff) * 128 + 127 - 2 * lane, (int)(short)(hs >> 16) * 128 + 126 - 2 * lane);
+        if (pair_key(hs, 127 - 2 * lane, 126 - 2 * lane) != want_key) ++errs;
     }
     atomicAdd(bad, errs);
 }
