@@ -368,9 +368,10 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
             }
         }
         if (tot[12] > 0)
-            fprintf(stderr, "[mando prof] backtrack per read: refills %.1f (%.0f cyc each) blocks %.1f walk %.0f cyc/block\n",
-                    tot[13] / reads, tot[12] / std::max(1.0, tot[13]), tot[14] / reads,
-                    (tot[2] - tot[12]) / std::max(1.0, tot[14]));
+            fprintf(stderr, "[mando prof] backtrack per read: refills %.1f (%.0f cyc each) diagonal runs %.1f serial blocks %.1f "
+                            "walk %.0f cyc per run or block\n",
+                    tot[13] / reads, tot[12] / std::max(1.0, tot[13]), tot[16] / reads, tot[14] / reads,
+                    (tot[2] - tot[12]) / std::max(1.0, tot[14] + tot[16]));
         if (getenv("MANDO_BT_STATS"))
             fprintf(stderr, "[mando prof] run stops per read: window %.1f multi %.1f non-adjacent %.1f not-M %.1f\n",
                     tot[8] / reads, tot[9] / reads, tot[10] / reads, tot[11] / reads);

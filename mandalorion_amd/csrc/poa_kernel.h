@@ -40,7 +40,7 @@ constexpr int kTbF1ExtNext = 1 << 6;     // F1[i][j+1] extends F1[i][j] (G1[j] <
 constexpr int kTbF2ExtNext = 1 << 7;
 
 // phases timed when PoaKArgs::prof is set (MANDO_PROF=1)
-constexpr int kProfPhases = 16;  // 0 desc, 1 dp, 2 backtrack, 3 update, 4 consensus, 5 rows, 6 reads,
+constexpr int kProfPhases = 20;  // 0 desc, 1 dp, 2 backtrack, 3 update, 4 consensus, 5 rows, 6 reads, 16 diagonal runs,
                                  // 8.. in-row segments (MANDO_STAMPS builds only)
 
 // per-group status codes written by the kernel (match include/mando.h)

@@ -156,6 +156,8 @@ __device__ __forceinline__ void wave_sync() { __syncthreads(); }
 // same-wave RAW through HBM (spilled rows, far row records): drain this wave's stores first
 __device__ __forceinline__ void hbm_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
 struct RowRec {
     int beg, end, am, soff;
 };
@@ -697,7 +699,7 @@ __device__ __forceinline__ RowRec load_rowrec(const SharedState &sh, const Slot 
         // consumed (readfirstlane) inside the branch so the common path never waits on vmcnt
         hbm_fence();
         const gint *g = s.rinfo + (int64_t)p * kRowInfoInts;
-        x = make_int4(bcast0(g[0]), bcast0(g[1]), bcast0(g[2]), bcast0(g[3]));
+        x = make_int4(bcast0(g[0]), bcast0(g[1]), bcast0(g[4]), bcast0(g[5]));
     }
     RowRec rr;
     rr.beg = x.x;
@@ -770,7 +772,7 @@ __device__ __forceinline__ void pre_records_slow(const PoaRunArgs &a, const Slot
             x = sh.rrow[p % kRowRing];
         } else {
             const gint *g = s.rinfo + (int64_t)p * kRowInfoInts;
-            x = make_int4(g[0], g[1], g[2], g[3]);
+            x = make_int4(g[0], g[1], g[4], g[5]);
         }
         pP = p;
         pB = x.x;
@@ -1106,14 +1108,8 @@ __device__ __forceinline__ int dp_row(const PoaRunArgs &a, const SC &sc, Slot &s
     if (lane == 0) {
         sh.rrow[r % kRowRing] = make_int4(beg, end, besti, soff);
         gint *ri = s.rinfo + (int64_t)r * kRowInfoInts;
-        ri[0] = beg;
-        ri[1] = end;
-        ri[2] = besti;
-        ri[3] = soff;
-        ri[4] = tbbase;
-        ri[5] = kpbase;
-        ri[6] = node;
-        ri[7] = pn;
+        *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
+        *reinterpret_cast<GLB v4i *>(ri + 4) = (v4i){besti, soff, node, pn};
     }
     return kStOk;
 }
@@ -1277,14 +1273,8 @@ __device__ __forceinline__ bool dp_row_fast(const PoaRunArgs &a, const SC &sc, S
     if (lane == 0) {
         sh.rrow[r % kRowRing] = make_int4(beg, end, besti, soff);
         gint *ri = s.rinfo + (int64_t)r * kRowInfoInts;
-        ri[0] = beg;
-        ri[1] = end;
-        ri[2] = besti;
-        ri[3] = soff;
-        ri[4] = tbbase;
-        ri[5] = kpbase;
-        ri[6] = node;
-        ri[7] = pn;
+        *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
+        *reinterpret_cast<GLB v4i *>(ri + 4) = (v4i){besti, soff, node, pn};
     }
     pp.prv_r = r;
     pp.prv_beg = beg;
@@ -1347,16 +1337,61 @@ __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
 }
 // inclusive prefix max over the wave of both halves (unsigned; 0 is the identity, so DPP lanes
 // without a source read 0 via bound_ctrl)
+// The two row_bcast steps leave the lanes of their masked-off rows at `old`: that is the previous
+// step's shifted value, a prefix maximum already folded into u, so no zero-fill is needed.
 __device__ __forceinline__ uint32_t pk_scan_umax(uint32_t u) {
-    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x111, 0xf, 0xf, true));
-    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x112, 0xf, 0xf, true));
-    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x114, 0xf, 0xf, true));
-    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x118, 0xf, 0xf, true));
-    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x142, 0xa, 0xf, true));
-    u = pk_umax(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x143, 0xc, 0xf, true));
+    uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x111, 0xf, 0xf, true);
+    u = pk_umax(u, t);
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x112, 0xf, 0xf, true);
+    u = pk_umax(u, t);
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x114, 0xf, 0xf, true);
+    u = pk_umax(u, t);
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x118, 0xf, 0xf, true);
+    u = pk_umax(u, t);
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)t, (int)u, 0x142, 0xa, 0xf, false);
+    u = pk_umax(u, t);
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)t, (int)u, 0x143, 0xc, 0xf, false);
+    u = pk_umax(u, t);
     return u;
 }
 
+
+// The row's two wave scans in one instruction stream: the inclusive prefix max of the packed F
+// input u (unsigned halves; v_mov_dpp + v_pk_max_u16 per step) and of the argmax key a
+// (v_max_i32_dpp).  The chains are independent, so each fills the other's VALU-write -> DPP-read
+// wait states (two per dependent pair): one s_nop 0 per step instead of two s_nop 1.  The two
+// row_bcast steps of u leave the lanes of their masked-off rows at t, the previous step's shifted
+// value, which is a prefix maximum already folded into u.
+__device__ __forceinline__ void dpp_scan_fa(uint32_t &u, int &a) {
+    uint32_t t;
+    asm volatile(
+        "s_nop 1\n"
+        "v_mov_b32_dpp %2, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_max_i32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf\n"
+        "v_pk_max_u16 %0, %0, %2\n"
+        "s_nop 0\n"
+        "v_max_i32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf\n"
+        "v_mov_b32_dpp %2, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_u16 %0, %0, %2\n"
+        "v_max_i32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 0\n"
+        "v_mov_b32_dpp %2, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_u16 %0, %0, %2\n"
+        "s_nop 0\n"
+        "v_max_i32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf\n"
+        "v_mov_b32_dpp %2, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_u16 %0, %0, %2\n"
+        "v_max_i32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "s_nop 0\n"
+        "v_mov_b32_dpp %2, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "v_pk_max_u16 %0, %0, %2\n"
+        "v_max_i32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        "s_nop 0\n"
+        "v_mov_b32_dpp %2, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        "v_pk_max_u16 %0, %0, %2\n"
+        "s_nop 1\n"
+        : "+v"(u), "+v"(a), "=&v"(t));
+}
 
 // The traceback bytes of a lane's two cells (layout in poa_kernel.h).  Every bit of the layout is
 // "a < b" for one pair of values (M < H, X1 < H, X2 < H, F1 < H, Ho1 < X1e, Ho2 < X2e, G1 < P1,
@@ -1422,19 +1457,22 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     const int kpbase = ds.kp_used - 3 * cb0;
     const int soff = R.far ? ds.sv_used : -1;
     const int svbase = ds.sv_used - cb0;
-    const int j0 = cb0 + 2 * lane;
-    const uint32_t J = (uint32_t)j0 * 0x10001u + 0x10000u;         // (j0, j0 + 1)
+    // lane pair index t = j0 / 2 (cb0 is even): one add, and every per-lane position derives from it
+    // (16-bit rows: columns < 2^16; the mask lets the LDS offsets fold into the instructions)
+    const uint32_t t = (((uint32_t)cb0 >> 1) & 0x7fffu) + ((uint32_t)lane & 63u);
+    const int j0 = (int)(2 * t);
+    const uint32_t J = __umul24(t, 0x20002u) + 0x10000u;             // (j0, j0 + 1)
     const uint32_t LJ = (uint32_t)(2 * lane) * 0x10001u + 0x10000u;  // (j0, j0 + 1) - cb0
     const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(pk2s(beg))) |
                                      as_u32(as_s16x2(pk2s(end)) - as_s16x2(J)));
-    const uint32_t qbyte = qnib<RW>()[j0 >> 1];
+    const uint32_t qbyte = qnib<RW>()[t];
     // perm selector (code of j0, 0x0C, code of j0 + 1, 0x0C): the byte copied to bits 12.. puts the
     // high nibble at bits 16-19
     const uint32_t sel = ((qbyte * 0x1001u) & 0x000F000Fu) | 0x0C000C00u;
     const uint32_t tlo =
         R.vb < 4 ? (uint32_t)(sc.match + sc.mismatch) << (8 * R.vb) : (uint32_t)sc.mismatch * 0x01010101u;
     const uint32_t S = __builtin_amdgcn_perm((uint32_t)sc.mismatch, tlo, sel);
-    const int iw = (j0 >> 1) & (HW - 1), iwp = (iw - 1) & (HW - 1);
+    const uint32_t iw = t & (HW - 1), iwp = (t - 1u) & (HW - 1);
     const uint32_t *w0 = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, R.p0slot));
     uint32_t Hd = __builtin_amdgcn_alignbit(w0[iw], w0[iwp], 16);
     uint32_t X1 = w0[HW + iw], X2 = w0[2 * HW + iw];
@@ -1503,7 +1541,12 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     const uint32_t G1 = pk_adds(H0, LJ1), G2 = pk_adds(H0, LJ2);
     const uint32_t Ga = __builtin_amdgcn_perm(G2, G1, 0x05040100u);
     const uint32_t Gb = __builtin_amdgcn_perm(G2, G1, 0x07060302u);
-    const uint32_t inc = pk_scan_umax(pk_max(Ga, Gb) ^ kNeg2);
+    // the row's leftmost argmax is H0's: F only carries values from the left minus gap penalties, so
+    // it never reaches the row maximum (an argmax cell has H = H0, and H >= H0 everywhere)
+    uint32_t inc = pk_max(Ga, Gb) ^ kNeg2;
+    int amk = pair_key(H0, 127 - 2 * lane, 126 - 2 * lane);
+    dpp_scan_fa(inc, amk);
+    const int mp = readlane(amk, kWave - 1);
     const uint32_t Pa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x138, 0xf, 0xf, true) ^ kNeg2;
     const uint32_t Pb = pk_max(Pa, Ga);
     const uint32_t P1 = __builtin_amdgcn_perm(Pb, Pa, 0x05040100u);
@@ -1538,7 +1581,6 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         svp[2 * kChunk + j0 + 1] = (int)E2 >> 16;
     }
     ds.r16acc = pk_umin(ds.r16acc, as_u32(as_u16x2(Hs) - as_u16x2(pk2(kR16Low))));
-    const int mp = readlane(dpp_incl_max(pair_key(Hs, 127 - 2 * lane, 126 - 2 * lane), -2147483647 - 1), kWave - 1);
     const int besti = cb0 + 127 - (mp & 127);
     ds.tb_used += R.tbw;
     if (R.multi) ds.kp_used += 3 * R.tbw;
@@ -1547,14 +1589,8 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     if (lane == 0) {
         sh.rrow[R.r & (kRowRing - 1)] = make_int4(beg, end, besti, soff);
         gint *ri = rinfo + (int64_t)R.r * kRowInfoInts;
-        ri[0] = beg;
-        ri[1] = end;
-        ri[2] = besti;
-        ri[3] = soff;
-        ri[4] = tbbase;
-        ri[5] = kpbase;
-        ri[6] = R.node;
-        ri[7] = R.pn;
+        *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
+        if (R.far) *reinterpret_cast<GLB v2i *>(ri + 4) = (v2i){besti, soff};
     }
     return besti;
 }
@@ -1721,14 +1757,8 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
     if (lane == 0) {
         sh.rrow[R.r & (kRowRing - 1)] = make_int4(beg, end, besti, soff);
         gint *ri = rinfo + (int64_t)R.r * kRowInfoInts;
-        ri[0] = beg;
-        ri[1] = end;
-        ri[2] = besti;
-        ri[3] = soff;
-        ri[4] = tbbase;
-        ri[5] = kpbase;
-        ri[6] = R.node;
-        ri[7] = R.pn;
+        *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
+        if (R.far) *reinterpret_cast<GLB v2i *>(ri + 4) = (v2i){besti, soff};
     }
     return besti;
 }
@@ -1876,6 +1906,14 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
             }
         }
         if (bad >= 0) {
+#ifdef MANDO_ROW_STATS
+            // fast rows by shape: chain (one predecessor, the previous row), two predecessors, no band
+            // masks, three or more predecessors
+            ds.seg[0] += (R.pn == 1 && (R.r - 1) == prv_r && R.p0slot == (prv_r & (kRing16 - 1)));
+            ds.seg[1] += R.two;
+            ds.seg[2] += R.nomask;
+            ds.seg[3] += R.pn3 >= 3;
+#endif
             int besti;
             if (RW == kChunk || R.end - R.cb0 < kChunk) besti = row16_vec<SC, RW>(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
             else besti = row16w_vec(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
@@ -1985,7 +2023,7 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
     }
     cells += ds.cells;
     if (a.prof && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 7] += nfast;
-#if defined(MANDO_STAMPS) || defined(MANDO_GENPROF)
+#if defined(MANDO_STAMPS) || defined(MANDO_GENPROF) || defined(MANDO_ROW_STATS)
     if (a.prof && lane == 0) {
         int64_t *pf = a.prof + (int64_t)blockIdx.x * kProfPhases;
         for (int k = 0; k < 4; ++k) pf[8 + k] += (int64_t)ds.seg[k];
@@ -2029,7 +2067,9 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
 
 // ---------------------------------------------------------------------------------------------
 // backtrack: fills qnode[q] = aligned node or -1 (insertion) for q in [0, qlen)
-// row record: rinfo[r] = {beg, end, argmax, soff, tbbase, kpbase, node, pre_n}
+// row record: rinfo[r] = {beg, end, tbbase, kpbase, argmax, soff, node, pre_n}; the fast rows write
+// argmax / soff only for far rows (the only ones read back from HBM) and never node / pre_n (the
+// backtrack takes those from the row's descriptor)
 //
 // The walk is inherently serial, so its cost is the latency chain per step.  Walking HBM directly
 // costs three dependent global loads per step (row record -> traceback byte -> predecessor byte).
@@ -2062,7 +2102,7 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
         da = make_int4(di[0].x, di[0].y, di[0].z, di[0].w);
         db = make_int4(di[1].x, di[1].y, di[1].z, di[1].w);
     }
-    const int beg = ra.x, end = ra.y, tbbase = rb.x, kpbase = rb.y, node = rb.z, pn = rb.w;
+    const int beg = ra.x, end = ra.y, tbbase = ra.z, kpbase = ra.w, node = da.x, pn = da.y >> 16;
     const int cb0 = beg & ~1;
     const int tbw = (end - cb0 + 1 + 3) & ~3;
     const bool multi = valid && pn > 1;
@@ -2144,7 +2184,8 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
 // One walk step read straight from HBM (rows too wide for the window, > kPreInline predecessors).
 __device__ __forceinline__ void bt_step_global(const PoaRunArgs &a, const Slot &s, int &i, int &j, int &st) {
     const gint *rb = s.rinfo + (int64_t)i * kRowInfoInts;
-    const int tbbase = rb[4], kpbase = rb[5], node = rb[6], pn = rb[7];
+    const gint *db = s.desc + (int64_t)i * kDescInts;
+    const int tbbase = rb[2], kpbase = rb[3], node = db[0], pn = db[1] >> 16;
     const int t = s.tb[tbbase + j];
     if (st == 1 || st == 2) {
         if (!(t & (st == 1 ? kTbE1Ext : kTbE2Ext))) {
@@ -2272,6 +2313,9 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
             }
             const unsigned long long bad = ~__ballot(okk);
             const int f = bad ? __ffsll((long long)bad) - 1 : kWave;
+#ifdef MANDO_BT_STATS
+            if (a.prof && !(a.dbg & 16) && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 16] += 1;
+#endif
             if (f < kWave && ((__ballot(okm) >> f) & 1ull)) {
                 // lanes [0, f] are all M steps; lane f's leads to predecessor row pr (not f's i-1)
                 if (lane <= f) s.qnode[cj - 1] = nd;
