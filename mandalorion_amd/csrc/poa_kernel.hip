@@ -2087,6 +2087,14 @@ struct BtWin {
     int lo, hi, glob;  // rows [lo, hi] are in the window; glob: single row read from HBM
 };
 
+// binary-lifting tables of the window's first-predecessor chains (the DP's descriptor batch is dead
+// during the backtrack): 6 tables of one byte per window row
+constexpr int kBtLift = 6;
+static_assert(kBtLift * kWave <= kDescBatch * kDescInts * 4, "lifting tables must fit the descriptor batch");
+__device__ __forceinline__ uint8_t *bt_lift(const SharedState &sh) {
+    return reinterpret_cast<uint8_t *>(const_cast<int *>(&sh.desc[0][0]));
+}
+
 template <int RW>
 __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i, int lane, BtWin &w, int kpwin) {
     constexpr int kTbWinR = bt_tb_win<RW>(), kKpWinR = bt_kp_win<RW>();
@@ -2178,6 +2186,18 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
     w.lo = i - cnt + 1;
     w.hi = i;
     w.glob = 0;
+    // first-predecessor chains of the window for the diagonal runs: window index x = w.hi - row;
+    // table s holds the 2^s-th first-predecessor ancestor of each window row (0xff: leaves the window)
+    uint8_t *lift = bt_lift(sh);
+    int x1 = 0xff;
+    if (lane < cnt && da.w >= w.lo && da.w < rr) x1 = i - da.w;
+    lift[lane] = (uint8_t)x1;
+#pragma unroll
+    for (int t = 1; t < kBtLift; ++t) {
+        const int y = lift[(t - 1) * kWave + lane];
+        const int z = y != 0xff ? lift[(t - 1) * kWave + y] : 0xff;
+        lift[t * kWave + lane] = (uint8_t)z;
+    }
     wave_sync();
 }
 
@@ -2287,28 +2307,32 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
             }
         }
         if (st == 0) {
-            // Diagonal run, wave-parallel: lane k checks cell (i-k, j-k) -- an M step whose source
-            // predecessor (the only one, or the one its predecessor byte names) is the row right
-            // above.  Every step before the first lane that fails is taken at once (runs end at
-            // indels and at graph rows out of order, typically tens of cells apart).
-            // The first failing lane's cell, when it is still an M step (its predecessor merely
-            // not the row right above: a branch of the graph), is taken too, so runs continue
-            // through the graph's branches instead of falling back to the serial walk.
-            const int ri = i - lane, cj = j - lane;
+            // Diagonal run, wave-parallel: lane k checks the k-th cell of a run of M steps that follows
+            // the rows' first predecessors -- row R_k = k-th first-predecessor ancestor of i (binary
+            // lifting over the window), column j - k.  The step is taken when the cell is an M step
+            // whose source predecessor (the only one, or the one its predecessor byte names) is the
+            // first one, i.e. R_{k+1}.  Every step before the first lane that fails is taken at once:
+            // runs end at indels, at rows whose M source is another predecessor (that step is taken
+            // too, and the next run starts from its row) and at the window's end.
+            const uint8_t *lift = bt_lift(sh);
+            int x = w.hi - i;
+#pragma unroll
+            for (int t = 0; t < kBtLift; ++t)
+                if ((lane >> t) & 1) x = x != 0xff ? lift[t * kWave + x] : 0xff;
+            const int ri = x != 0xff ? w.hi - x : -1, cj = j - lane;
             bool okk = false, okm = false;
             int nd = 0, pr = -1;
             if (ri >= w.lo && ri > 0 && cj > 0) {
-                const int idx = w.hi - ri;
-                const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][0]);
+                const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[x][0]);
                 const int t = bt_tb<RW>(sh)[m0.x + cj];
                 pr = m0.w;
                 if (m0.y != kKpNone) {
-                    const int4 m1 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][4]);
+                    const int4 m1 = *reinterpret_cast<const int4 *>(&sh.bt.md[x][4]);
                     const int k0 = g_qnib[m0.y + 3 * cj];
                     pr = k0 == 0 ? m0.w : k0 == 1 ? m1.x : k0 == 2 ? m1.y : k0 == 3 ? m1.z : k0 == 4 ? m1.w : -1;
                 }
                 okm = pr >= 0 && !(t & kTbNM);
-                okk = okm && pr == ri - 1;
+                okk = okm && pr == m0.w;
                 nd = m0.z;
             }
             const unsigned long long bad = ~__ballot(okk);
@@ -2317,7 +2341,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
             if (a.prof && !(a.dbg & 16) && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + 16] += 1;
 #endif
             if (f < kWave && ((__ballot(okm) >> f) & 1ull)) {
-                // lanes [0, f] are all M steps; lane f's leads to predecessor row pr (not f's i-1)
+                // lanes [0, f] are all M steps; lane f's leads to another predecessor (or out of the window)
                 if (lane <= f) s.qnode[cj - 1] = nd;
                 i = readlane(pr, f);
                 j -= f + 1;
@@ -2327,7 +2351,7 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
             if (a.prof && f < kWave) {
                 int why = 0;
                 if (ri >= w.lo && ri > 0 && cj > 0) {
-                    const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[w.hi - ri][0]);
+                    const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[x][0]);
                     const int t = bt_tb<RW>(sh)[m0.x + cj];
                     why = (t & kTbNM) ? 3 : 2;
                 }
@@ -2336,8 +2360,9 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
             }
 #endif
             if (f > 0) {
+                // lanes [0, f) are M steps; the walk continues at lane f - 1's source row
                 if (lane < f) s.qnode[cj - 1] = nd;
-                i -= f;
+                i = readlane(pr, f - 1);
                 j -= f;
                 continue;
             }
@@ -2801,45 +2826,128 @@ __device__ __forceinline__ int update_graph(SharedState &sh, const uint8_t *q, i
 // ---------------------------------------------------------------------------------------------
 // heaviest bundling (lane 0): reverse topological sweep, then walk from the source
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int consensus(SharedState &sh, int n, uint8_t *out, int64_t cap,
-                         int &len) {
+// Heaviest bundling, wave-parallel where it can be: per block of 64 rows (last block first) every lane
+// gathers its row's node, out-degree and up to kConsOut (successor row, edge weight) pairs, so the
+// sweep itself -- inherently sequential: a row's score is its best successor's plus the edge weight --
+// reads them from registers (readlane) and the successors' scores from an LDS ring of the last
+// kScRing rows (HBM for successors further ahead), instead of five dependent HBM loads per row.
+// Then the walk from the source reads nxt a block of 64 rows at a time, records the path's rows and
+// the bases are gathered in parallel.  Same choices as the serial form: the heaviest out-edge, ties
+// to the successor with the larger-or-equal score, in out-edge order.
+constexpr int kConsOut = 4;
+constexpr int kScRing = 1024;
+static_assert(kScRing * 4 <= (int)sizeof(DpLds), "score ring must fit the DP scratch");
+__device__ __forceinline__ int consensus(SharedState &sh, int n, uint8_t *out, int64_t cap, int &len, int lane) {
     const PoaRunArgs a = args_of(sh);
     Slot s = slot_of(sh);
-    for (int r = n - 1; r >= 0; --r) {
-        const int v = s.order[r];
-        if (v == kSink) {
-            s.score[r] = 0;
-            s.nxt[r] = -1;
-            continue;
-        }
-        const int on = s.out_n[v];
-        const gint *ol = out_list(s, a, v);
-        const gint *ow = out_wlist(s, a, v);
-        int maxw = -1, maxr = -1;
-        for (int k = 0; k < on; ++k) {
-            const int ro = s.pos[ol[k]];
-            const int wgt = ow[k];
-            if (maxw < wgt) {
-                maxw = wgt;
-                maxr = ro;
-            } else if (maxw == wgt && s.score[maxr] <= s.score[ro]) {
-                maxr = ro;
+    int *ring = reinterpret_cast<int *>(&sh.dp);
+    int err = kStOk;
+    for (int b0 = ((n - 1) / kWave) * kWave; b0 >= 0; b0 -= kWave) {
+        const int r = b0 + lane;
+        int on = 0, sink = 1, ro[kConsOut], wt[kConsOut];
+#pragma unroll
+        for (int k = 0; k < kConsOut; ++k) ro[k] = wt[k] = -1;
+        if (r < n) {
+            const int v = s.order[r];
+            sink = v == kSink;
+            if (!sink) {
+                on = s.out_n[v];
+                const gint *ol = out_list(s, a, v);
+                const gint *ow = out_wlist(s, a, v);
+#pragma unroll
+                for (int k = 0; k < kConsOut; ++k)
+                    if (k < on) {
+                        ro[k] = s.pos[ol[k]];
+                        wt[k] = ow[k];
+                    }
             }
         }
-        if (maxr < 0) return kStInternal;
-        s.score[r] = maxw + s.score[maxr];
-        s.nxt[r] = maxr;
+        int my_sc = 0, my_nx = -1;
+        for (int l = min(kWave, n - b0) - 1; l >= 0; --l) {
+            const int rr = b0 + l;
+            int sc = 0, nx = -1;
+            if (!readlane(sink, l)) {
+                const int o = readlane(on, l);
+                int maxw = -1, maxr = -1, maxs = 0;
+                // a successor's score: the ring holds rows (rr, rr + kScRing], HBM the ones further on
+                auto score_of = [&](int ro_) -> int {
+                    if (ro_ - rr <= kScRing) return bcast0(ring[ro_ & (kScRing - 1)]);
+                    hbm_fence();  // this wave's own stores of earlier blocks (rare: an edge > kScRing rows long)
+                    return bcast0(s.score[ro_]);
+                };
+#pragma unroll
+                for (int k = 0; k < kConsOut; ++k) {
+                    if (k >= o) break;
+                    const int rk = readlane(ro[k], l), wk = readlane(wt[k], l);
+                    if (maxw < wk) {
+                        maxw = wk;
+                        maxr = rk;
+                        maxs = score_of(rk);
+                    } else if (maxw == wk) {
+                        const int sk = score_of(rk);
+                        if (maxs <= sk) {
+                            maxr = rk;
+                            maxs = sk;
+                        }
+                    }
+                }
+                if (o > kConsOut) {  // rare rows with more out-edges: the rest from HBM
+                    const int v = bcast0(s.order[rr]);
+                    const gint *ol = out_list(s, a, v);
+                    const gint *ow = out_wlist(s, a, v);
+                    for (int k = kConsOut; k < o; ++k) {
+                        const int rk = bcast0(s.pos[ol[k]]), wk = bcast0(ow[k]);
+                        if (maxw < wk) {
+                            maxw = wk;
+                            maxr = rk;
+                            maxs = score_of(rk);
+                        } else if (maxw == wk) {
+                            const int sk = score_of(rk);
+                            if (maxs <= sk) {
+                                maxr = rk;
+                                maxs = sk;
+                            }
+                        }
+                    }
+                }
+                if (maxr < 0) err = kStInternal;
+                sc = maxw + maxs;
+                nx = maxr;
+            }
+            if (lane == 0) ring[rr & (kScRing - 1)] = sc;
+            if (lane == l) {
+                my_sc = sc;
+                my_nx = nx;
+            }
+        }
+        if (r < n) {
+            s.score[r] = my_sc;
+            s.nxt[r] = my_nx;
+        }
+        if (err != kStOk) return err;
     }
-    int r = s.nxt[0];
-    int64_t l = 0;
+    hbm_fence();
+    // walk from the source along nxt (a block of 64 rows' successors in registers); the path's rows
+    // are listed in the score array (dead now), then the bases gathered
+    int r = bcast0(s.nxt[0]);
+    int blk = -1, nv = -1;
+    int l = 0;
     while (r >= 0 && r != n - 1) {
-        if (l < cap) out[l] = s.base[s.order[r]];
+        if ((r >> 6) != blk) {
+            blk = r >> 6;
+            const int x = blk * kWave + lane;
+            nv = x < n ? s.nxt[x] : -1;
+        }
+        if (lane == 0) s.score[l] = r;
         ++l;
-        r = s.nxt[r];
         if (l > n) return kStInternal;
+        r = readlane(nv, r & (kWave - 1));
     }
-    len = (int)l;
-    return l <= cap ? kStOk : kStCap;
+    hbm_fence();
+    const int lim = (int)min<int64_t>(l, cap);
+    for (int t = lane; t < lim; t += kWave) out[t] = s.base[s.order[s.score[t]]];
+    len = l;
+    return (int64_t)l <= cap ? kStOk : kStCap;
 }
 
 // SEEDED: the launch holds only -S groups (seeded_main: teams of workgroups over a read's windows);
@@ -2964,12 +3072,9 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
                 int64_t *prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
                 const uint64_t t6 = prof ? clock64() : 0;
                 const int n = bcast0(sh.lead.n);
-                int cst = kStOk, len = 0;
-                if (lane == 0) {
-                    const int64_t cap = a.cons_off[g + 1] - a.cons_off[g];
-                    cst = consensus(sh, n, a.cons + a.cons_off[g], cap, len);
-                }
-                st = bcast0(cst);
+                int len = 0;
+                const int64_t cap = uni64(a.cons_off[g + 1]) - uni64(a.cons_off[g]);
+                st = consensus(sh, n, a.cons + uni64(a.cons_off[g]), cap, len, lane);
                 clen = bcast0(len);
                 if (prof && lane == 0) prof[4] += (int64_t)(clock64() - t6);
             }
@@ -3326,12 +3431,9 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 const PoaRunArgs a = args_of(sh);
                 int64_t *prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
                 uint64_t t6 = prof ? clock64() : 0;
-                int cst = kStOk, len = 0;
-                if (lane == 0) {
-                    const int64_t cap = a.cons_off[g + 1] - a.cons_off[g];
-                    cst = consensus(sh, n, a.cons + a.cons_off[g], cap, len);
-                }
-                st = bcast0(cst);
+                int len = 0;
+                const int64_t cap = uni64(a.cons_off[g + 1]) - uni64(a.cons_off[g]);
+                st = consensus(sh, n, a.cons + uni64(a.cons_off[g]), cap, len, lane);
                 clen = bcast0(len);
                 if (prof && lane == 0) prof[4] += (int64_t)(clock64() - t6);
             }
