@@ -162,6 +162,13 @@ struct RowRec {
     int beg, end, am, soff;
 };
 
+// Predecessor bytes of a multi-predecessor row (the predecessor index of the M, E1 and E2 maxima per
+// cell): rows with at most kKpPackMax predecessors pack them into one byte per cell (k0 | k1 << 2 |
+// k2 << 4), rows with more keep three bytes per cell.  One byte per cell lets the backtrack's LDS
+// window hold three times as many multi-predecessor rows.
+constexpr int kKpPackMax = 4;
+__device__ __forceinline__ int kp_stride(int pn) { return pn <= kKpPackMax ? 1 : 3; }
+constexpr int kNodeKp3 = 1 << 30;  // backtrack window record: the row's predecessor bytes are 3 per cell
 constexpr int kDescBatch = 32;        // row descriptors staged in LDS per refill
 constexpr int kTbWin = 4096;          // backtrack: traceback byte window
 constexpr int kBtRows = 64;           // backtrack: rows per window
@@ -927,12 +934,13 @@ __device__ __forceinline__ int dp_row(const PoaRunArgs &a, const SC &sc, Slot &s
     if (multi && ds.kp_used + 3 * tbw > (int)a.caps.KPC) return kStCap;
     if (spill && ds.sv_used + 3 * wa > (int)a.caps.SVC) return kStCap;
     // 32-bit offsets from the slot's arrays (the stores then use a scalar base + vector offset)
+    const int ks = kp_stride(pn);
     const int tbbase = (int)ds.tb_used - cb0;       // traceback byte of column j: tb[tbbase + j]
-    const int kpbase = (int)ds.kp_used - 3 * cb0;   // predecessor bytes of column j: kp[kpbase + 3j]
+    const int kpbase = (int)ds.kp_used - ks * cb0;  // predecessor byte(s) of column j: kp[kpbase + ks*j]
     const int soff = spill ? (int)ds.sv_used : -1;
     const int svbase = (int)ds.sv_used - cb0;       // plane pl, column j: sv[svbase + pl*wa + j]
     ds.tb_used += tbw;
-    if (multi) ds.kp_used += 3 * tbw;
+    if (multi) ds.kp_used += ks * tbw;
     if (spill) ds.sv_used += 3 * wa;
     ds.cells += end - beg + 1;
     STAMP(ts1);
@@ -1053,10 +1061,15 @@ __device__ __forceinline__ int dp_row(const PoaRunArgs &a, const SC &sc, Slot &s
             const int tb2 = tb_bits(Hb, Mb, X1b, X2b, F1b, oe1, e1, oe2, e2, G1b, P1b, G2b, P2b);
             tpair = ta | (tb2 << 8);
             if ((va || vbb) && multi) {
-                GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + 3 * j0));
-                kq[0] = (uint16_t)(mka | (k1a << 8));
-                kq[1] = (uint16_t)(k2a | (mkb << 8));
-                kq[2] = (uint16_t)(k1b | (k2b << 8));
+                if (ks == 1) {
+                    *reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + j0)) =
+                        (uint16_t)((mka | k1a << 2 | k2a << 4) | (mkb | k1b << 2 | k2b << 4) << 8);
+                } else {
+                    GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + 3 * j0));
+                    kq[0] = (uint16_t)(mka | (k1a << 8));
+                    kq[1] = (uint16_t)(k2a | (mkb << 8));
+                    kq[2] = (uint16_t)(k1b | (k2b << 8));
+                }
             }
             {
                 STAMP(tx);
@@ -1168,7 +1181,7 @@ __device__ __forceinline__ bool dp_row_fast(const PoaRunArgs &a, const SC &sc, S
     if (!__builtin_amdgcn_readfirstlane((int)ok)) return false;
 
     const int tbbase = (int)ds.tb_used - cb0;
-    const int kpbase = (int)ds.kp_used - 3 * cb0;
+    const int kpbase = (int)ds.kp_used - cb0;  // at most two predecessors: packed bytes (kp_stride 1)
     const int soff = far ? (int)ds.sv_used : -1;
     const int svbase = (int)ds.sv_used - cb0;
     const int j0 = cb0 + 2 * lane, j1 = j0 + 1;
@@ -1240,12 +1253,9 @@ __device__ __forceinline__ bool dp_row_fast(const PoaRunArgs &a, const SC &sc, S
     // stores: the traceback pair of every lane (lanes past `end` write into slack the next row
     // overwrites; the caller's capacity test keeps one chunk of slack), ring row, optional planes
     *reinterpret_cast<GLB uint16_t *>(s.tb + (tbbase + j0)) = (uint16_t)(ta | (tb2 << 8));
-    if (multi) {
-        GLB uint16_t *kq = reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + 3 * j0));
-        kq[0] = (uint16_t)(mka | (k1a << 8));
-        kq[1] = (uint16_t)(k2a | (mkb << 8));
-        kq[2] = (uint16_t)(k1b | (k2b << 8));
-    }
+    if (multi)
+        *reinterpret_cast<GLB uint16_t *>(s.kp + (kpbase + j0)) =
+            (uint16_t)((mka | k1a << 2 | k2a << 4) | (mkb | k1b << 2 | k2b << 4) << 8);
     int *ringrow = &sh.dp.ring[r % kRing][0][0];
     *reinterpret_cast<int2 *>(ringrow + ib) = make_int2(va ? Ha : kNegInf, vbb ? Hb : kNegInf);
     *reinterpret_cast<int2 *>(ringrow + kChunk + ib) = make_int2(va ? E1a : kNegInf, vbb ? E1b : kNegInf);
@@ -1267,7 +1277,7 @@ __device__ __forceinline__ bool dp_row_fast(const PoaRunArgs &a, const SC &sc, S
     // bookkeeping (scalar)
     const int begs = bcast0(beg), ends = bcast0(end), tbws = bcast0(tbw);
     ds.tb_used += tbws;
-    if (multi) ds.kp_used += 3 * tbws;
+    if (multi) ds.kp_used += tbws;
     if (far) ds.sv_used += 3 * kChunk;
     ds.cells += ends - begs + 1;
     if (lane == 0) {
@@ -1454,7 +1464,8 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
     const int beg = R.beg, end = R.end, cb0 = R.cb0;
     const int tbbase = ds.tb_used - cb0;
-    const int kpbase = ds.kp_used - 3 * cb0;
+    const int ks = kp_stride(R.pn);
+    const int kpbase = ds.kp_used - ks * cb0;
     const int soff = R.far ? ds.sv_used : -1;
     const int svbase = ds.sv_used - cb0;
     // lane pair index t = j0 / 2 (cb0 is even): one add, and every per-lane position derives from it
@@ -1562,9 +1573,14 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     row_store<uint16_t>(tb + ds.tb_used, 2u * (uint32_t)lane, (uint16_t)tbv);
     if (R.multi) {
         gu8 *kq = kp + ds.kp_used;
-        row_store<uint16_t>(kq, 6u * (uint32_t)lane, (uint16_t)__builtin_amdgcn_perm(K1, MK, 0x0C0C0400u));
-        row_store<uint16_t>(kq, 6u * (uint32_t)lane + 2u, (uint16_t)__builtin_amdgcn_perm(MK, K2, 0x0C0C0600u));
-        row_store<uint16_t>(kq, 6u * (uint32_t)lane + 4u, (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u));
+        if (ks == 1) {  // packed: k < 8 in each half, so the shifts stay inside the halves
+            const uint32_t kb = MK | (K1 << 2) | (K2 << 4);
+            row_store<uint16_t>(kq, 2u * (uint32_t)lane, (uint16_t)__builtin_amdgcn_perm(0u, kb, 0x0C0C0200u));
+        } else {
+            row_store<uint16_t>(kq, 6u * (uint32_t)lane, (uint16_t)__builtin_amdgcn_perm(K1, MK, 0x0C0C0400u));
+            row_store<uint16_t>(kq, 6u * (uint32_t)lane + 2u, (uint16_t)__builtin_amdgcn_perm(MK, K2, 0x0C0C0600u));
+            row_store<uint16_t>(kq, 6u * (uint32_t)lane + 4u, (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u));
+        }
     }
     const uint32_t Hs = bfi(inv, kNeg2, H);
     uint32_t *wr = reinterpret_cast<uint32_t *>(ring16_row<RW>(sh, R.r & (kRing16 - 1)));
@@ -1583,7 +1599,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     ds.r16acc = pk_umin(ds.r16acc, as_u32(as_u16x2(Hs) - as_u16x2(pk2(kR16Low))));
     const int besti = cb0 + 127 - (mp & 127);
     ds.tb_used += R.tbw;
-    if (R.multi) ds.kp_used += 3 * R.tbw;
+    if (R.multi) ds.kp_used += ks * R.tbw;
     if (R.far) ds.sv_used += 3 * kChunk;
     ds.cells += end - beg + 1;
     if (lane == 0) {
@@ -1608,7 +1624,8 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
     const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
     const int beg = R.beg, end = R.end, cb0 = R.cb0;
     const int tbbase = ds.tb_used - cb0;
-    const int kpbase = ds.kp_used - 3 * cb0;
+    const int ks = kp_stride(R.pn);
+    const int kpbase = ds.kp_used - ks * cb0;
     const int soff = R.far ? ds.sv_used : -1;
     const int svbase = ds.sv_used - cb0;
     const uint32_t *w0 = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, R.p0slot));
@@ -1723,10 +1740,15 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
         row_store<uint16_t>(tb + ds.tb_used, (uint32_t)(kChunk * h + 2 * lane), (uint16_t)tbv);
         if (R.multi) {
             gu8 *kq = kp + ds.kp_used;
-            const uint32_t ko = (uint32_t)(3 * (kChunk * h + 2 * lane));
-            row_store<uint16_t>(kq, ko, (uint16_t)__builtin_amdgcn_perm(K1v[h], MKv[h], 0x0C0C0400u));
-            row_store<uint16_t>(kq, ko + 2u, (uint16_t)__builtin_amdgcn_perm(MKv[h], K2v[h], 0x0C0C0600u));
-            row_store<uint16_t>(kq, ko + 4u, (uint16_t)__builtin_amdgcn_perm(K2v[h], K1v[h], 0x0C0C0602u));
+            if (ks == 1) {
+                const uint32_t kb = MKv[h] | (K1v[h] << 2) | (K2v[h] << 4);
+                row_store<uint16_t>(kq, (uint32_t)(kChunk * h + 2 * lane), (uint16_t)__builtin_amdgcn_perm(0u, kb, 0x0C0C0200u));
+            } else {
+                const uint32_t ko = (uint32_t)(3 * (kChunk * h + 2 * lane));
+                row_store<uint16_t>(kq, ko, (uint16_t)__builtin_amdgcn_perm(K1v[h], MKv[h], 0x0C0C0400u));
+                row_store<uint16_t>(kq, ko + 2u, (uint16_t)__builtin_amdgcn_perm(MKv[h], K2v[h], 0x0C0C0600u));
+                row_store<uint16_t>(kq, ko + 4u, (uint16_t)__builtin_amdgcn_perm(K2v[h], K1v[h], 0x0C0C0602u));
+            }
         }
         const uint32_t inv = invv[h];
         const uint32_t Hs = bfi(inv, kNeg2, H);
@@ -1751,7 +1773,7 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
     const int mp = readlane(dpp_incl_max(amv, -2147483647 - 1), kWave - 1);
     const int besti = cb0 + 255 - (mp & 255);
     ds.tb_used += R.tbw;
-    if (R.multi) ds.kp_used += 3 * R.tbw;
+    if (R.multi) ds.kp_used += ks * R.tbw;
     if (R.far) ds.sv_used += 3 * RW;
     ds.cells += end - beg + 1;
     if (lane == 0) {
@@ -2114,8 +2136,9 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
     const int cb0 = beg & ~1;
     const int tbw = (end - cb0 + 1 + 3) & ~3;
     const bool multi = valid && pn > 1;
+    const int ks = kp_stride(pn);
     const int tstart = tbbase + cb0, tend = tstart + tbw;
-    const int kstart = kpbase + 3 * cb0, kend = kstart + 3 * tbw;
+    const int kstart = kpbase + ks * cb0, kend = kstart + ks * tbw;
     const int TE = readlane(tend, 0);
     const unsigned long long mm = __ballot(multi);
     const int fm = mm ? __ffsll((long long)mm) - 1 : 0;
@@ -2176,7 +2199,7 @@ __device__ __forceinline__ void bt_refill(SharedState &sh, const Slot &s, int i,
     if (lane < cnt) {
         md[0] = tbbase - rs16;
         md[1] = multi ? kpbase - ks16 : kKpNone;
-        md[2] = node;
+        md[2] = node | (multi && ks == 3 ? kNodeKp3 : 0);
         md[3] = da.w;
         md[4] = db.x;
         md[5] = db.y;
@@ -2214,10 +2237,14 @@ __device__ __forceinline__ void bt_step_global(const PoaRunArgs &a, const Slot &
         }
     }
     const bool multi = pn > 1;
-    const int ty = st == 0 ? tb_type(t, multi ? s.kp[kpbase + 3 * j + 1] : 0, multi ? s.kp[kpbase + 3 * j + 2] : 0)
-                           : st;
+    // predecessor index of the M / E1 / E2 maximum (field f) of this cell
+    auto kp_at = [&](int f) -> int {
+        if (kp_stride(pn) == 1) return (s.kp[kpbase + j] >> (2 * f)) & 3;
+        return s.kp[kpbase + 3 * j + f];
+    };
+    const int ty = st == 0 ? tb_type(t, multi ? kp_at(1) : 0, multi ? kp_at(2) : 0) : st;
     if (ty <= 2) {
-        const int k = multi ? s.kp[kpbase + 3 * j + ty] : 0;
+        const int k = multi ? kp_at(ty) : 0;
         const int p = (k < kPreInline) ? s.desc[(int64_t)i * kDescInts + 3 + k] : s.xpre[(int64_t)i * a.caps.DCAP + k];
         if (ty == 0) {
             s.qnode[j - 1] = node;
@@ -2244,12 +2271,15 @@ __device__ __forceinline__ void bt_step_lds(const SharedState &sh, const Slot &s
     const int idx = min(max(whi - i, 0), kWave - 1);
     const int4 m0 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][0]);
     const int4 m1 = *reinterpret_cast<const int4 *>(&sh.bt.md[idx][4]);
-    const int woff = m0.x, kof = m0.y, node = m0.z;
+    const int woff = m0.x, kof = m0.y, node = m0.z & ~kNodeKp3;
+    const bool kp3 = (m0.z & kNodeKp3) != 0;
     const int tix = max(woff + j, 1);
     const int t = tbw[tix], tprev = tbw[tix - 1];
     const bool multi = kof != kKpNone;
-    const int kix = multi ? kof + 3 * j : 0;
-    const int k0 = g_qnib[kix], k1 = g_qnib[kix + 1], k2 = g_qnib[kix + 2];
+    const int kix = multi ? kof + (kp3 ? 3 * j : j) : 0;
+    const int kb = g_qnib[kix];
+    const int k0 = kp3 ? kb : kb & 3, k1 = kp3 ? g_qnib[kix + 1] : (kb >> 2) & 3,
+              k2 = kp3 ? g_qnib[kix + 2] : (kb >> 4) & 3;
     const bool isE = st == 1 || st == 2;
     const bool open = isE && !(t & (st == 1 ? kTbE1Ext : kTbE2Ext));
     const int ty = st == 0 ? tb_type(t, multi ? k1 : 0, multi ? k2 : 0) : st;
@@ -2328,12 +2358,12 @@ __device__ __forceinline__ int backtrack(SharedState &sh, int bi, int qlen, int 
                 pr = m0.w;
                 if (m0.y != kKpNone) {
                     const int4 m1 = *reinterpret_cast<const int4 *>(&sh.bt.md[x][4]);
-                    const int k0 = g_qnib[m0.y + 3 * cj];
+                    const int k0 = (m0.z & kNodeKp3) ? g_qnib[m0.y + 3 * cj] : g_qnib[m0.y + cj] & 3;
                     pr = k0 == 0 ? m0.w : k0 == 1 ? m1.x : k0 == 2 ? m1.y : k0 == 3 ? m1.z : k0 == 4 ? m1.w : -1;
                 }
                 okm = pr >= 0 && !(t & kTbNM);
                 okk = okm && pr == m0.w;
-                nd = m0.z;
+                nd = m0.z & ~kNodeKp3;
             }
             const unsigned long long bad = ~__ballot(okk);
             const int f = bad ? __ffsll((long long)bad) - 1 : kWave;
