@@ -23,6 +23,8 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/mando.h"
 #include "cluster_gpu.h"
 #include "internal.h"
@@ -33,14 +35,16 @@ using std::vector;
 
 namespace {
 
-// Host buffers for the locus text, kept for reuse (2 MB-aligned, transparent huge pages: a chunk's
-// few GB then costs no first-touch page faults and no munmap on the next call).  They are pageable:
-// the copies to the device are staged by the runtime, and pinning fresh buffers each call costs more
-// than the staging (14k loci: 1.2-1.4 s vs 0.57-0.64 s).  Round 2 also recorded stale bytes with
+// Host buffers for the locus text, kept for reuse: page-locked (hipHostMalloc, pinned once, reused
+// by later calls), so the readers fread straight into DMA-able memory and the piecewise copies to the
+// device run on the copy engine, asynchronously, instead of a host staging copy plus a blit kernel
+// that competes with the POA grids for CU slots (MANDO_TEXT_PAGEABLE=1: 2 MB-aligned pageable
+// buffers with transparent huge pages, the round-2 layout).  Round 2 recorded stale bytes with
 // reused page-locked buffers; that change was made together with moving the device text off the
 // stream-ordered pool, whose recycled buffers are the measured cause (cluster_kernel.hip,
 // tools/stale_probe.hip): a reused pinned source (scenario A) and a reused pinned D2H target (G, the
-// K2 output path) gave no stale byte in 15 refills each.
+// K2 output path) gave no stale byte in 15 refills each; tests/test_cluster_gpu.py
+// test_repeated_calls_reuse_buffers stays the regression test.
 struct PinnedPool {
     std::mutex mu;
     std::vector<std::pair<char *, size_t>> free_list;
@@ -61,9 +65,21 @@ struct PinnedPool {
         constexpr size_t kStep = size_t(256) << 20;
         cap = (std::max<size_t>(need, 1) + kStep - 1) / kStep * kStep;
         void *p = nullptr;
+        if (!pageable()) {
+            if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+            return static_cast<char *>(p);
+        }
         if (posix_memalign(&p, size_t(2) << 20, cap) != 0) return nullptr;
         (void)madvise(p, cap, MADV_HUGEPAGE);
         return static_cast<char *>(p);
+    }
+    static bool pageable() {
+        static const bool v = getenv("MANDO_TEXT_PAGEABLE") && getenv("MANDO_TEXT_PAGEABLE")[0] == '1';
+        return v;
+    }
+    static void free_buf(char *p) {
+        if (pageable()) free(p);
+        else (void)hipHostFree(p);
     }
     void release(char *p, size_t cap) {
         if (!p) return;
@@ -75,7 +91,7 @@ struct PinnedPool {
         while (free_list.size() > 4) {
             auto it = std::min_element(free_list.begin(), free_list.end(),
                                        [](const auto &a, const auto &b) { return a.second < b.second; });
-            free(it->first);
+            free_buf(it->first);
             free_list.erase(it);
         }
     }

@@ -349,7 +349,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         # with few, large loci (SIRV-like: 7 loci; config 5: 100) one chunk is faster (1.22 -> 0.81 s,
         # 2.51 -> 2.43 s), since a chunk's kernels then run one wave per locus on an idle GPU
         n_chunks = 1 if sizes.sum() < (64 << 20) or len(my_roots) < 1024 else 2
-        fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.3"))] if n_chunks == 2 else None
+        fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.4"))] if n_chunks == 2 else None
         if n_chunks == 2 and os.environ.get("MANDO_CHUNK_FRACS"):  # cumulative byte fractions of the cuts
             fracs = [float(x) for x in os.environ["MANDO_CHUNK_FRACS"].split(",")]
             n_chunks = len(fracs) + 1
