@@ -262,6 +262,9 @@ def _fasta_bytes(aux, hs, hl, nl_pos, cons_src, cons_sel, cons_start, cons_len, 
     return fasta
 
 
+_CHUNK_BYTES = int(os.environ.get("MANDO_CHUNK_BYTES", str(8 << 30)))
+
+
 def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", splice_site_width: int = 1,
                     minimum_read_count: int = 2, white_list_polyA: Sequence[str] = ("0",), threads: int = 0,
                     junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", upstream_buffer: int = 10,
@@ -350,6 +353,13 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         # 2.51 -> 2.43 s), since a chunk's kernels then run one wave per locus on an idle GPU
         n_chunks = 1 if sizes.sum() < (64 << 20) or len(my_roots) < 1024 else 2
         fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.4"))] if n_chunks == 2 else None
+        # large inputs (config 4 on one GPU: ~60 GB of locus text): chunks of at most kChunkBytes, the
+        # first 0.4 of one, so one chunk's text, clustering scratch and the POA workspaces fit in HBM
+        # together
+        k = int(-(-int(sizes.sum()) // _CHUNK_BYTES)) if n_chunks == 2 else 1
+        if k > 1:
+            fracs = [(0.4 + i) / k for i in range(k)]
+            n_chunks = k + 1
         if n_chunks == 2 and os.environ.get("MANDO_CHUNK_FRACS"):  # cumulative byte fractions of the cuts
             fracs = [float(x) for x in os.environ["MANDO_CHUNK_FRACS"].split(",")]
             n_chunks = len(fracs) + 1
@@ -446,13 +456,18 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
 
         fa_futs = []
 
-        def write_fasta(poa_fut, counter0):
+        def write_fasta(poa_fut, counter0, r2_fut):
             # one rank: the writer thread appends each chunk's FASTA part as soon as its POA is done (in
-            # chunk order: one thread, FIFO), off the main thread that orients the next chunk meanwhile
+            # chunk order: one thread, FIFO), off the main thread that orients the next chunk meanwhile;
+            # once both of its parts are written the chunk's buffers (locus text on host and device)
+            # go back to their pools, so a many-chunk run holds only the chunks in flight
             pl, res = poa_fut.result()
             tw = time.perf_counter()
             n = _write_payload(pl, fa, None, counter0)
             timeline.append(("write", tw - t0, time.perf_counter() - t0))
+            r2_fut.result()
+            del pl
+            res.close()
             return n, res
 
         def write_r2i(res, lo, hi, counter0):
@@ -483,7 +498,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                 poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
                 if world == 1:
                     r2_futs.append(host.submit(write_r2i, res, lo, hi, n_iso_before))
-                    fa_futs.append(writer.submit(write_fasta, poa_futs[-1], n_iso_before))
+                    fa_futs.append(writer.submit(write_fasta, poa_futs[-1], n_iso_before, r2_futs[-1]))
                     n_iso_before += res.n_isoforms
         except BaseException:
             close_outputs()
