@@ -38,6 +38,8 @@ EXPORTED = (
     "mando_cluster_device_text",
     "mando_orient_segments",
     "mando_poa_segments",
+    "mando_poa_segments_begin",
+    "mando_poa_end",
     "mando_comm_init",
     "mando_comm_backend",
     "mando_allgather_counts",
@@ -193,6 +195,8 @@ def load(path: str | None = None):
         lib.mando_cluster_device_text.argtypes = [_P, _P, _P]
         lib.mando_orient_segments.argtypes = [_P, _P, _I64, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
         lib.mando_poa_segments.argtypes = [_P, _P, _P, _I64, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]
+        lib.mando_poa_segments_begin.argtypes = [_P, _P, _P, _I64, _P, _P, _P, _P, _I64, _P, _P]
+        lib.mando_poa_end.argtypes = [_P, ctypes.c_int32, _P, _I64, _P, _P, _P]
         lib.mando_split_loci.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _P, _P]
         lib.mando_list_roots.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, _P,
                                          ctypes.c_int64, _P, _P]
