@@ -167,6 +167,11 @@ def load(path: str | None = None):
         p = path or os.environ.get("MANDO_LIB") or LIB_PATH
         if not os.path.exists(p):
             raise MandoError(-7, f"{p} not built (run __graft_entry__.build() or make -C mandalorion_amd/csrc)")
+        # one hardware queue per stream: the D driver drives up to 8 streams (POA: narrow / wide / -S
+        # lanes and two batch io streams; orientation; clustering; the reassembly), and streams that share
+        # one of HIP's default 4 queues run one after the other (a long POA grid held back the launches
+        # queued behind it on another stream).  Read when HIP initialises, i.e. at the first call below.
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "12")
         lib = ctypes.CDLL(p)
         lib.mando_last_error.restype = ctypes.c_char_p
         lib.mando_last_error.argtypes = []

@@ -5,6 +5,7 @@
 #include <mutex>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -186,6 +187,14 @@ struct mando_ctx {
 
 namespace {
 
+// MANDO_LAUNCH_LOG: host-side timestamps (ms, steady clock) of the launch path's steps
+void hlog(const char *what, int lane) {
+    static const bool on = getenv("MANDO_LAUNCH_LOG") != nullptr;
+    if (!on) return;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    fprintf(stderr, "[mando host] %.1f lane %d %s\n", ms, lane, what);
+}
+
 constexpr int kMaxWavesPerCu = 16;  // upper bound on resident POA waves per CU
 // groups whose band 2w + 1 (at their mean read length) is wider than this run in the wide-ring
 // launch: their rows mostly exceed one 128-column chunk (the band also drifts with the argmax)
@@ -283,12 +292,15 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     if (const char *ev = getenv("MANDO_POA_DBG")) a.dbg = atoi(ev);
     // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget
     size_t free_b = 0, total_b = 0;
+    hlog("enter", lane);
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    hlog("meminfo", lane);
     const size_t budget = std::max<size_t>((size_t)1 << 30, (size_t)(kWsShare * (double)free_b) + ws.bytes);
     // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
     const int per_cu = mando::poa_blocks_per_cu(a, cap);
+    hlog("occupancy", lane);
     // -S teams: when the seeded groups are too few to fill the resident waves, each gets a team of
     // up to kMaxTeam one-wave workgroups that align a read's windows side by side
     int team = 1;
@@ -309,7 +321,9 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     if ((size_t)(teams * team * a.slot_bytes) > ws.bytes || (size_t)(teams * team) * 4 > busyb.bytes ||
         (sp && (size_t)teams * sizeof(mando::TeamBox) > boxb.bytes))
         HIP_TRY(hipStreamSynchronize(stream));
+    hlog("growth check", lane);
     int rc = ws.ensure((size_t)(teams * team * a.slot_bytes));
+    hlog("ws", lane);
     while (rc == MANDO_E_NOMEM && teams > 1) {  // memory taken by others since hipMemGetInfo: fewer slots
         (void)hipGetLastError();                 // clear the failed allocation's error state
         teams /= 2;
@@ -348,6 +362,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.ws = ws.as<char>();
     a.counter = counter.as<int32_t>();
     HIP_TRY(hipMemsetAsync(a.counter, 0, sizeof(int32_t), stream));
+    hlog("memsets", lane);
     const char *pe = getenv("MANDO_PROF");
     const bool prof = pe && pe[0] == '1';
     if (prof) {
@@ -364,6 +379,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     if (ev_s) HIP_TRY(hipEventRecord(ev_s, stream));
     HIP_TRY(mando::launch_poa(a, (int)grid, stream));
     if (ev_e) HIP_TRY(hipEventRecord(ev_e, stream));
+    hlog("launched", lane);
     if (prof) {
         std::vector<int64_t> h((size_t)grid * mando::kProfPhases);
         HIP_TRY(hipMemcpyAsync(h.data(), profb.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
@@ -703,8 +719,12 @@ void build_lists(PoaCall *c) {
 }
 
 // Queues c->todo's launches (c->lists, whose group lists are already on the device): each kind on its
-// own lane, after the batch's staging; the io stream then waits for every launch.  Lanes run the
-// launches of consecutive batches in order, so batch k + 1's grids start as batch k's drain.
+// own lane, after the batch's staging.  Lanes run the launches of consecutive batches in order, so
+// batch k + 1's grids start as batch k's drain.  Nothing on the device waits for a launch's end: a
+// stream-wait on another stream's event is a barrier packet in the waiting stream's hardware queue,
+// and streams share the process's hardware queues (GPU_MAX_HW_QUEUES) -- an io stream waiting there
+// for the wide launch held back a narrow launch queued behind it (measured: chunk 1's two launches
+// ran one after the other, 0.58 -> 1.05 s).  mando_poa_end waits for the launch events on the host.
 int enqueue_launches(mando_ctx *ctx, PoaCall *c) {
     // the kind holding the heaviest group is enqueued first (its groups take the CUs first)
     int korder[3] = {0, 1, 2};
@@ -715,7 +735,6 @@ int enqueue_launches(mando_ctx *ctx, PoaCall *c) {
             kcost[kind] = std::max(kcost[kind], (double)(q.sum - q.first_len) * (double)q.first_len);
         }
     std::stable_sort(korder, korder + 3, [&](int x, int y) { return kcost[x] > kcost[y]; });
-    HIP_TRY(hipStreamWaitEvent(c->io, c->ev_staged, 0));
     for (int ki = 0; ki < 3; ++ki) {
         const int kind = korder[ki];
         const std::vector<int32_t> &L = c->lists[kind];
@@ -740,7 +759,6 @@ int enqueue_launches(mando_ctx *ctx, PoaCall *c) {
                               c->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &c->sp : nullptr, c->ev_s[kind],
                               c->ev_e[kind], kind);
         if (rc) return rc;
-        HIP_TRY(hipStreamWaitEvent(c->io, c->ev_e[kind], 0));
         c->launched[kind] = true;
         c->launches += 1;
     }
@@ -879,6 +897,8 @@ int poa_end_impl(mando_ctx *ctx, int32_t ticket, uint8_t *cons_out, int64_t cons
     std::vector<int64_t> cells((size_t)n_groups);
     int rc;
     for (;;) {
+        for (int k = 0; k < 3; ++k)
+            if (c->launched[k]) HIP_TRY(hipEventSynchronize(c->ev_e[k]));
         HIP_TRY(hipStreamSynchronize(c->io));
         for (int k = 0; k < 3; ++k) {
             if (!c->launched[k]) continue;

@@ -1021,9 +1021,15 @@ struct MT {
         }
         return v;
     }
-    // permutation(n): Fisher-Yates from the top.  The wave tempers the stream's next outputs one per
-    // lane; random_interval's rejection draws (mask, then accept iff <= i) are resolved in order on the
-    // scalar side (readlane), consuming exactly the outputs interval() would; lane 0 swaps.
+    // permutation(n): Fisher-Yates from the top (numpy's shuffle: for i = n-1 .. 1, j = interval(i),
+    // swap(perm[i], perm[j])), 64 stream outputs at a time, one per lane.
+    // Draws: lane t's output serves draw i - (outputs accepted before t); random_interval accepts it iff
+    // (output & mask(i)) <= i.  Assuming every lane from `start` on is accepted, the first lane that
+    // fails is rejected (consumed, the rest shift by one) or lies past i = 1 (not consumed); each ballot
+    // round settles one rejection, consuming exactly the outputs interval() would.
+    // Swaps: the accepted lanes' swaps (d, v) run in lane order; a prefix of lanes that touch no
+    // position an earlier lane of the block touches (v_s == d_t or v_s == v_t for s < t; d_s == v_t
+    // is impossible since v_t <= d_t < d_s) run at once, then the rest.
     __device__ void permutation(int32_t n, int32_t *perm) {
         for (int i = ln(); i < n; i += 64) perm[i] = i;
         wsync();
@@ -1035,22 +1041,54 @@ struct MT {
             }
             const int m = 624 - pos < 64 ? 624 - pos : 64;
             const uint32_t y = ln() < m ? temper(key[pos + ln()]) : 0u;
-            int k = 0;
-            for (; k < m && i >= 1; ++k) {
-                const uint32_t mask = 0xffffffffu >> __clz(i);
-                const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)y, k) & mask;
-                if (v <= (uint32_t)i) {
-                    if (ln() == 0) {
-                        const int32_t t = perm[i];
-                        perm[i] = perm[v];
-                        perm[v] = t;
-                    }
-                    --i;
+            int start = 0, cur = i;
+            int32_t dl = 0, vl = 0;
+            uint64_t acc = 0;
+            while (start < m) {
+                const int d = cur - (ln() - start);
+                const uint32_t v = y & (0xffffffffu >> __clz(d > 1 ? d : 1));
+                const bool in = ln() >= start && ln() < m;
+                const uint64_t bad = __ballot(in && (d < 1 || v > (uint32_t)d));
+                const int f = bad ? (int)__ffsll((unsigned long long)bad) - 1 : m;
+                if (ln() >= start && ln() < f) {
+                    dl = d;
+                    vl = (int32_t)v;
                 }
+                acc |= (f >= 64 ? ~0ull : ((1ull << f) - 1)) & ~((1ull << start) - 1);
+                cur -= f - start;
+                if (f >= m || cur < 1) {  // block used up, or every draw made (lane f not consumed)
+                    start = f;
+                    break;
+                }
+                start = f + 1;  // rejected: consumed
             }
-            pos += k;
+            pos += start;
+            i = cur;
+            uint64_t rem = acc;
+            while (rem) {
+                bool conf = false;
+                for (uint64_t it = rem; it; it &= it - 1) {
+                    const int sl = (int)__ffsll((unsigned long long)it) - 1;
+                    const int32_t vs = __builtin_amdgcn_readlane(vl, sl);
+                    conf |= ln() > sl && (dl == vs || vl == vs);
+                }
+                const uint64_t cb = __ballot(conf && ((rem >> ln()) & 1ull));
+                const int c = cb ? (int)__ffsll((unsigned long long)cb) - 1 : 64;
+                const bool mine = ((rem >> ln()) & 1ull) && ln() < c;
+                int32_t pa = 0, pb = 0;
+                if (mine) {
+                    pa = perm[dl];
+                    pb = perm[vl];
+                }
+                if (mine) {
+                    perm[vl] = pa;
+                    perm[dl] = pb;
+                }
+                rem &= c >= 64 ? 0ull : ~((1ull << c) - 1);
+                if (rem) wsync();
+            }
+            wsync();
         }
-        wsync();
     }
 };
 
