@@ -199,21 +199,6 @@ int mando_poa_segments(mando_ctx *ctx, const mando_poa_params *params, const uin
                        const int64_t *off, const int32_t *len, const int8_t *rc, const int64_t *grp_off,
                        int64_t n_groups, const uint8_t *seeding_per_group, uint8_t *cons_out, int64_t cons_cap,
                        int64_t *cons_off, int64_t *cells_out);
-/* mando_poa_segments in two halves, so a caller can queue the next batch while one drains (the D
- * driver's chunks: batch k + 1 is staged and its launches queued behind batch k's on the same lanes,
- * and its groups take the CUs as batch k's last groups finish).  _begin plans, stages and queues the
- * batch and returns at once with a ticket; mando_poa_end(ticket) waits for it, re-runs any group whose
- * workspace capacity was exceeded and writes the same outputs as mando_poa_segments.  At most two
- * batches per context are in flight (a third _begin fails with MANDO_E_ARG); d_text must stay valid
- * until the batch's mando_poa_end returns; tickets are ended in any order, once.
- * timing (optional, 3 doubles): the batch's kernel span in ms, and its first launch start and last
- * launch end in ms after the context's creation (batches in flight overlap). */
-int mando_poa_segments_begin(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *d_text,
-                             int64_t text_len, const int64_t *off, const int32_t *len, const int8_t *rc,
-                             const int64_t *grp_off, int64_t n_groups, const uint8_t *seeding_per_group,
-                             int32_t *ticket);
-int mando_poa_end(mando_ctx *ctx, int32_t ticket, uint8_t *cons_out, int64_t cons_cap, int64_t *cons_off,
-                  int64_t *cells_out, double *timing);
 
 /* ------------------------------------------------------------------------------------------------
  * Reassembly of the sharded D module: loci are split over ranks (one process per

@@ -38,8 +38,6 @@ EXPORTED = (
     "mando_cluster_device_text",
     "mando_orient_segments",
     "mando_poa_segments",
-    "mando_poa_segments_begin",
-    "mando_poa_end",
     "mando_comm_init",
     "mando_comm_backend",
     "mando_allgather_counts",
@@ -167,11 +165,6 @@ def load(path: str | None = None):
         p = path or os.environ.get("MANDO_LIB") or LIB_PATH
         if not os.path.exists(p):
             raise MandoError(-7, f"{p} not built (run __graft_entry__.build() or make -C mandalorion_amd/csrc)")
-        # one hardware queue per stream: the D driver drives up to 8 streams (POA: narrow / wide / -S
-        # lanes and two batch io streams; orientation; clustering; the reassembly), and streams that share
-        # one of HIP's default 4 queues run one after the other (a long POA grid held back the launches
-        # queued behind it on another stream).  Read when HIP initialises, i.e. at the first call below.
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "12")
         lib = ctypes.CDLL(p)
         lib.mando_last_error.restype = ctypes.c_char_p
         lib.mando_last_error.argtypes = []
@@ -200,8 +193,6 @@ def load(path: str | None = None):
         lib.mando_cluster_device_text.argtypes = [_P, _P, _P]
         lib.mando_orient_segments.argtypes = [_P, _P, _I64, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
         lib.mando_poa_segments.argtypes = [_P, _P, _P, _I64, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]
-        lib.mando_poa_segments_begin.argtypes = [_P, _P, _P, _I64, _P, _P, _P, _P, _I64, _P, _P]
-        lib.mando_poa_end.argtypes = [_P, ctypes.c_int32, _P, _I64, _P, _P, _P]
         lib.mando_split_loci.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _P, _P]
         lib.mando_list_roots.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, _P,
                                          ctypes.c_int64, _P, _P]

@@ -2,10 +2,7 @@
 // planning for the POA kernel (capacity estimates, LPT work order, overflow re-runs).
 #include <hip/hip_runtime.h>
 
-#include <mutex>
-
 #include <algorithm>
-#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -131,11 +128,6 @@ struct EncInit {
 
 }  // namespace
 
-namespace {
-struct PoaCall;
-void poa_call_free(PoaCall *c);
-}  // namespace
-
 struct mando_ctx {
     int device = 0;
     int n_cu = 256;
@@ -144,10 +136,12 @@ struct mando_ctx {
     int last_launches = 0;
     bool timed = false;
     DevBuf ws, counter, prof, o_gidx;
-    DevBuf seq, seq_off, grp_off;  // orientation batches
+    DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
     DevBuf o_hits, o_strand, o_status;
-    DevBuf s_items, s_scratch, s_redo, s_counter;                          // -S partition (seed kernel)
+    DevBuf s_items, s_item_of, s_n, s_t, s_q, s_scratch, s_redo, gorder2;  // -S partition
+    DevBuf gorder_w;                                                       // wide-launch groups
     DevBuf g_off, g_len, g_rc, g_dst;                                      // segment gather
+    DevBuf cons_txt;                                                       // decoded consensi
     DevBuf o_scratch;                                                      // long-read orientation slabs
     // extra POA lanes: a batch's launches of different kinds (narrow, wide, seeded) run side by side,
     // each with its own stream and workspace
@@ -156,22 +150,12 @@ struct mando_ctx {
     DevBuf lane_ws[2], lane_counter[2], lane_prof[2];
     DevBuf boxes, lane_boxes[2];  // -S team mailboxes
     DevBuf busy, lane_busy[2];    // one-group launches: workspace slot flags
-    // POA batches in flight (mando_poa_segments_begin / mando_poa_end): two, alternating.  A batch's
-    // staging and copy-back run on its own io stream, its launches on the lanes (narrow: stream, wide:
-    // lane_stream[0], -S: lane_stream[1]; a lane's launches of consecutive batches run in order), so
-    // batch k + 1 is staged and queued while batch k's last groups drain.
-    PoaCall *calls[2] = {nullptr, nullptr};
-    int call_next = 0;
-    hipEvent_t ev_ref = nullptr;  // origin of the batches' launch intervals (mando_poa_end timing)
-    std::mutex poa_mu;            // staging, launches and lane workspace growth
-    float last_ms = -1.0f;        // kernel span of the last ended batch (mando_last_kernel_ms)
     ~mando_ctx() {
-        for (int k = 0; k < 2; ++k) poa_call_free(calls[k]);
-        if (ev_ref) (void)hipEventDestroy(ev_ref);
-        for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &o_hits, &o_strand, &o_status, &o_gidx,
-                          &s_items, &s_scratch, &s_redo, &s_counter, &g_off, &g_len, &g_rc, &g_dst, &o_scratch,
-                          &lane_ws[0], &lane_ws[1], &lane_counter[0], &lane_counter[1], &lane_prof[0],
-                          &lane_prof[1], &boxes, &lane_boxes[0],
+        for (DevBuf *b : {&ws, &counter, &prof, &seq, &seq_off, &grp_off, &gorder, &cons, &cons_off,
+                          &cons_len, &cells, &status, &o_hits, &o_strand, &o_status, &o_gidx, &s_items,
+                          &s_item_of, &s_n, &s_t, &s_q, &s_scratch, &s_redo, &gorder2, &g_off, &g_len, &g_rc,
+                          &g_dst, &cons_txt, &o_scratch, &lane_ws[0], &lane_ws[1], &lane_counter[0],
+                          &lane_counter[1], &lane_prof[0], &lane_prof[1], &gorder_w, &boxes, &lane_boxes[0],
                           &lane_boxes[1], &busy, &lane_busy[0], &lane_busy[1]})
             b->release();
         if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -186,14 +170,6 @@ struct mando_ctx {
 };
 
 namespace {
-
-// MANDO_LAUNCH_LOG: host-side timestamps (ms, steady clock) of the launch path's steps
-void hlog(const char *what, int lane) {
-    static const bool on = getenv("MANDO_LAUNCH_LOG") != nullptr;
-    if (!on) return;
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-    fprintf(stderr, "[mando host] %.1f lane %d %s\n", ms, lane, what);
-}
 
 constexpr int kMaxWavesPerCu = 16;  // upper bound on resident POA waves per CU
 // groups whose band 2w + 1 (at their mean read length) is wider than this run in the wide-ring
@@ -248,8 +224,8 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
                  const uint8_t *d_seq, const int64_t *d_seq_off, const int64_t *d_grp_off,
                  const int32_t *d_gorder, int64_t n_groups, uint8_t *d_cons,
                  const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
-                 int32_t *d_status, int max_per_cu, const SeedPlan *sp = nullptr, hipEvent_t ev_s = nullptr,
-                 hipEvent_t ev_e = nullptr, int lane = 0) {
+                 int32_t *d_status, int max_per_cu, const SeedPlan *sp = nullptr, bool ev_start = true,
+                 bool ev_end = true, int lane = 0) {
     // lane k > 0: the context's extra stream and workspace k - 1 (launches of other kinds alongside)
     hipStream_t stream = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
     DevBuf &ws = lane ? ctx->lane_ws[lane - 1] : ctx->ws;
@@ -292,15 +268,12 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     if (const char *ev = getenv("MANDO_POA_DBG")) a.dbg = atoi(ev);
     // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget
     size_t free_b = 0, total_b = 0;
-    hlog("enter", lane);
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    hlog("meminfo", lane);
     const size_t budget = std::max<size_t>((size_t)1 << 30, (size_t)(kWsShare * (double)free_b) + ws.bytes);
     // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
     const int per_cu = mando::poa_blocks_per_cu(a, cap);
-    hlog("occupancy", lane);
     // -S teams: when the seeded groups are too few to fill the resident waves, each gets a team of
     // up to kMaxTeam one-wave workgroups that align a read's windows side by side
     int team = 1;
@@ -316,14 +289,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
                 a.slot_bytes / 1e6, (long long)(teams * team), team, per_cu, (int)a.caps.QC, mando::poa_dyn_lds(a),
                 free_b / 1e9, budget / 1e9);
     if (teams < 1) teams = 1;
-    // a lane's previous launch (an earlier batch still draining) may be using its buffers: growing
-    // them waits for it (the slot count only shrinks below, so this covers the flags and mailboxes too)
-    if ((size_t)(teams * team * a.slot_bytes) > ws.bytes || (size_t)(teams * team) * 4 > busyb.bytes ||
-        (sp && (size_t)teams * sizeof(mando::TeamBox) > boxb.bytes))
-        HIP_TRY(hipStreamSynchronize(stream));
-    hlog("growth check", lane);
     int rc = ws.ensure((size_t)(teams * team * a.slot_bytes));
-    hlog("ws", lane);
     while (rc == MANDO_E_NOMEM && teams > 1) {  // memory taken by others since hipMemGetInfo: fewer slots
         (void)hipGetLastError();                 // clear the failed allocation's error state
         teams /= 2;
@@ -362,7 +328,6 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.ws = ws.as<char>();
     a.counter = counter.as<int32_t>();
     HIP_TRY(hipMemsetAsync(a.counter, 0, sizeof(int32_t), stream));
-    hlog("memsets", lane);
     const char *pe = getenv("MANDO_PROF");
     const bool prof = pe && pe[0] == '1';
     if (prof) {
@@ -371,15 +336,10 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         HIP_TRY(hipMemsetAsync(profb.p, 0, (size_t)grid * mando::kProfPhases * 8, stream));
         a.prof = profb.as<int64_t>();
     }
-    if (getenv("MANDO_LAUNCH_LOG"))
-        fprintf(stderr, "[mando launch] lane %d groups %lld slots %lld team %d waves/CU %d one_group %d grid %lld "
-                        "slot %.1f MB ws %.1f GB (free %.1f GB)\n",
-                lane, (long long)n_groups, (long long)slots, team, per_cu, a.one_group, (long long)grid,
-                a.slot_bytes / 1e6, ws.bytes / 1e9, free_b / 1e9);
-    if (ev_s) HIP_TRY(hipEventRecord(ev_s, stream));
+    if (ev_start) HIP_TRY(hipEventRecord(ctx->ev0, stream));
     HIP_TRY(mando::launch_poa(a, (int)grid, stream));
-    if (ev_e) HIP_TRY(hipEventRecord(ev_e, stream));
-    hlog("launched", lane);
+    if (ev_end) HIP_TRY(hipEventRecord(ctx->ev1, stream));
+    ctx->timed = true;
     if (prof) {
         std::vector<int64_t> h((size_t)grid * mando::kProfPhases);
         HIP_TRY(hipMemcpyAsync(h.data(), profb.p, h.size() * 8, hipMemcpyDeviceToHost, stream));
@@ -422,59 +382,12 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     return MANDO_OK;
 }
 
-// One POA batch between mando_poa_segments_begin and mando_poa_end: its device buffers (reads,
-// consensi, per-group results, -S partitions), its copy-back stream and its launch events, and the
-// host-side plan the retries and the collection need.
-struct PoaCall {
-    DevBuf seq, seq_off, grp_off, gorder[3], cons, cons_off, cons_len, cells, status;
-    DevBuf g_off, g_len, g_rc, g_dst, cons_txt;
-    DevBuf s_item_of, s_n, s_t, s_q;  // -S partitions (read by the seeded launch)
-    hipStream_t io = nullptr;
-    hipEvent_t ev_staged = nullptr, ev_s[3] = {nullptr, nullptr, nullptr}, ev_e[3] = {nullptr, nullptr, nullptr};
-    bool busy = false;
-    int32_t gen = 0;
-    mando_poa_params p{};
-    int64_t n_groups = 0;
-    std::vector<GroupStat> gs;
-    std::vector<int64_t> soff, goff, ccap;
-    std::vector<uint8_t> seeded;
-    std::vector<int32_t> todo, lists[3];
-    SeedPlan sp;
-    int attempt = 0, launches = 0;
-    bool launched[3] = {false, false, false};
-    double t_first = 1e300, t_last = -1e300;  // ms after ctx->ev_ref
-    ~PoaCall() {
-        for (DevBuf *b : {&seq, &seq_off, &grp_off, &gorder[0], &gorder[1], &gorder[2], &cons, &cons_off, &cons_len,
-                          &cells, &status, &g_off, &g_len, &g_rc, &g_dst, &cons_txt, &s_item_of, &s_n, &s_t, &s_q})
-            b->release();
-        for (int k = 0; k < 3; ++k) {
-            if (ev_s[k]) (void)hipEventDestroy(ev_s[k]);
-            if (ev_e[k]) (void)hipEventDestroy(ev_e[k]);
-        }
-        if (ev_staged) (void)hipEventDestroy(ev_staged);
-        if (io) (void)hipStreamDestroy(io);
-    }
-    int init() {
-        HIP_TRY(hipStreamCreateWithFlags(&io, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&ev_staged, hipEventDisableTiming));
-        for (int k = 0; k < 3; ++k) {
-            HIP_TRY(hipEventCreate(&ev_s[k]));
-            HIP_TRY(hipEventCreate(&ev_e[k]));
-        }
-        return MANDO_OK;
-    }
-};
-
-void poa_call_free(PoaCall *c) { delete c; }
-
 // -S partitions of every seeded group (seed_kernel.hip): items pair each non-empty read after a group's
 // first with the previous non-empty read; the reads are already encoded on the device (ctx->seq).
 // Items over the launch's LDS capacity are re-run at twice the capacity.
 template <class IsSeeded>
-int plan_seeds(mando_ctx *ctx, PoaCall *c, const mando_poa_params &p, const std::vector<int64_t> &soff,
-               const int64_t *grp_off, int64_t n_groups, IsSeeded seeded_group, SeedPlan &sp, hipStream_t stream) {
-    const uint8_t *d_seq = c->seq.as<uint8_t>();
-    const int64_t *d_seq_off = c->seq_off.as<int64_t>();
+int plan_seeds(mando_ctx *ctx, const mando_poa_params &p, const std::vector<int64_t> &soff, const int64_t *grp_off,
+               int64_t n_groups, IsSeeded seeded_group, SeedPlan &sp) {
     if (p.k < 1 || p.k > 19 || p.w < 1 || p.min_w < p.k)
         return fail(MANDO_E_UNSUPPORTED, "-S needs 1 <= k <= 19, w >= 1, min_w >= k on this build");
     const int64_t n_reads = (int64_t)soff.size() - 1;
@@ -500,42 +413,42 @@ int plan_seeds(mando_ctx *ctx, PoaCall *c, const mando_poa_params &p, const std:
     const int64_t n_items = (int64_t)items.size() / 2;
     int rc;
     if ((rc = ctx->s_items.ensure(std::max<size_t>(items.size(), 1) * 4)) ||
-        (rc = c->s_item_of.ensure(item_of.size() * 4)) ||
-        (rc = c->s_n.ensure((size_t)std::max<int64_t>(n_items, 1) * 4)) ||
-        (rc = c->s_t.ensure((size_t)std::max<int64_t>(n_items, 1) * (size_t)pc * 4)) ||
-        (rc = c->s_q.ensure((size_t)std::max<int64_t>(n_items, 1) * (size_t)pc * 4)) ||
-        (rc = ctx->s_counter.ensure(256)))
+        (rc = ctx->s_item_of.ensure(item_of.size() * 4)) ||
+        (rc = ctx->s_n.ensure((size_t)std::max<int64_t>(n_items, 1) * 4)) ||
+        (rc = ctx->s_t.ensure((size_t)std::max<int64_t>(n_items, 1) * (size_t)pc * 4)) ||
+        (rc = ctx->s_q.ensure((size_t)std::max<int64_t>(n_items, 1) * (size_t)pc * 4)) ||
+        (rc = ctx->counter.ensure(256)))
         return rc;
     if (!items.empty())
-        HIP_TRY(hipMemcpyAsync(ctx->s_items.p, items.data(), items.size() * 4, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(c->s_item_of.p, item_of.data(), item_of.size() * 4, hipMemcpyHostToDevice, stream));
-    sp.par_item = c->s_item_of.as<int32_t>();
-    sp.par_n = c->s_n.as<int32_t>();
-    sp.par_t = c->s_t.as<int32_t>();
-    sp.par_q = c->s_q.as<int32_t>();
+        HIP_TRY(hipMemcpyAsync(ctx->s_items.p, items.data(), items.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->s_item_of.p, item_of.data(), item_of.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    sp.par_item = ctx->s_item_of.as<int32_t>();
+    sp.par_n = ctx->s_n.as<int32_t>();
+    sp.par_t = ctx->s_t.as<int32_t>();
+    sp.par_q = ctx->s_q.as<int32_t>();
     sp.pc = (int32_t)pc;
     sp.k = p.k;
     if (n_items == 0) {
-        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
         return MANDO_OK;
     }
     // minimizer capacity: ~2 per w+1 positions, with room for ties
     int cap = 1024;
     while (cap < mando::kSeedCapMax && cap < 3 * max_len / (p.w + 1)) cap *= 2;
     mando::SeedArgs a{};
-    a.seq = d_seq;
-    a.seq_off = d_seq_off;
+    a.seq = ctx->seq.as<uint8_t>();
+    a.seq_off = ctx->seq_off.as<int64_t>();
     a.items = ctx->s_items.as<int32_t>();
     a.k = p.k;
     a.w = p.w;
     a.min_w = p.min_w;
     a.max_occ = mando::kSeedMaxOcc;
     a.pc = (int32_t)pc;
-    a.par_n = c->s_n.as<int32_t>();
-    a.par_t = c->s_t.as<int32_t>();
-    a.par_q = c->s_q.as<int32_t>();
+    a.par_n = ctx->s_n.as<int32_t>();
+    a.par_t = ctx->s_t.as<int32_t>();
+    a.par_q = ctx->s_q.as<int32_t>();
     a.max_len = (int32_t)max_len;
-    a.counter = ctx->s_counter.as<int32_t>();
+    a.counter = ctx->counter.as<int32_t>();
     std::vector<int32_t> redo, nres((size_t)n_items);
     for (;;) {
         a.cap = cap;
@@ -545,10 +458,10 @@ int plan_seeds(mando_ctx *ctx, PoaCall *c, const mando_poa_params &p, const std:
         a.scratch_words = mando::seed_scratch_words((int)max_len, cap);
         if ((rc = ctx->s_scratch.ensure((size_t)blocks * (size_t)a.scratch_words * 8))) return rc;
         a.scratch = ctx->s_scratch.as<uint64_t>();
-        HIP_TRY(hipMemsetAsync(a.counter, 0, 4, stream));
-        HIP_TRY(mando::launch_seed(a, blocks, stream));
-        HIP_TRY(hipMemcpyAsync(nres.data(), c->s_n.p, nres.size() * 4, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
+        HIP_TRY(hipMemsetAsync(a.counter, 0, 4, ctx->stream));
+        HIP_TRY(mando::launch_seed(a, blocks, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(nres.data(), ctx->s_n.p, nres.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
         std::vector<int32_t> again;
         for (int64_t i = 0; i < n_items; ++i) {
             if (nres[(size_t)i] == -2) return fail(MANDO_E_INTERNAL, "-S: more kept anchors than the read allows");
@@ -561,7 +474,7 @@ int plan_seeds(mando_ctx *ctx, PoaCall *c, const mando_poa_params &p, const std:
         cap *= 2;
         redo.swap(again);
         if ((rc = ctx->s_redo.ensure(redo.size() * 4))) return rc;
-        HIP_TRY(hipMemcpyAsync(ctx->s_redo.p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(ctx->s_redo.p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     }
     return MANDO_OK;
 }
@@ -621,8 +534,7 @@ int mando_ctx_create(int device_ordinal, mando_ctx **out) {
     c->device = device_ordinal;
     c->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ev_ref) != hipSuccess || hipEventRecord(c->ev_ref, c->stream) != hipSuccess) {
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return fail(MANDO_E_HIP, "stream/event creation failed");
     }
@@ -633,7 +545,7 @@ int mando_ctx_create(int device_ordinal, mando_ctx **out) {
 void mando_ctx_destroy(mando_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipDeviceSynchronize();
+    (void)hipStreamSynchronize(ctx->stream);
     delete ctx;
 }
 
@@ -657,9 +569,7 @@ int mando_ctx_set_priority(mando_ctx *ctx, int high) {
 }
 
 float mando_last_kernel_ms(mando_ctx *ctx) {
-    if (!ctx) return -1.0f;
-    if (ctx->last_ms >= 0.0f) return ctx->last_ms;
-    if (!ctx->timed) return -1.0f;
+    if (!ctx || !ctx->timed) return -1.0f;
     float ms = -1.0f;
     if (hipEventSynchronize(ctx->ev1) != hipSuccess) return -1.0f;
     if (hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) != hipSuccess) return -1.0f;
@@ -683,12 +593,8 @@ int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const
     const int64_t w = params->band_b + (int64_t)(params->band_f * (float)max_read_len);
     caps.wide = 2 * w + 1 > kWideBand;
     ctx->last_launches = 1;
-    ctx->last_ms = -1.0f;
-    ctx->timed = true;
-    std::lock_guard<std::mutex> g(ctx->poa_mu);
     return launch_batch(ctx, *params, caps, d_seqs, d_seq_off, d_grp_off, nullptr, n_groups,
-                        d_cons, d_cons_off, d_cons_len, d_cells, d_status, kMaxWavesPerCu, nullptr, ctx->ev0,
-                        ctx->ev1);
+                        d_cons, d_cons_off, d_cons_len, d_cells, d_status, kMaxWavesPerCu);
 }
 
 }  // extern "C"
@@ -697,240 +603,170 @@ namespace {
 
 // Stages the reads of a batch as ASCII into ctx->seq (soff: their offsets there); returns a status.
 using StageFn = std::function<int(mando_ctx *)>;
-// Stages a POA batch's reads as ASCII into c->seq on `stream`.
-using PoaStageFn = std::function<int(PoaCall *, hipStream_t)>;
 
-hipStream_t lane_of(mando_ctx *ctx, int lane) { return lane ? ctx->lane_stream[lane - 1] : ctx->stream; }
-
-// the kind of launch a group runs in: 0 unseeded with a band of one chunk, 1 unseeded with a wider band
-// (2w + 1 at the group's mean read length; the wide-ring instantiation), 2 -S
-int group_kind(const PoaCall *c, int32_t g) {
-    if (c->seeded[(size_t)g]) return 2;
-    const GroupStat &q = c->gs[(size_t)g];
-    const int64_t mean = q.sum / std::max<int64_t>(1, q.nreads);
-    const int64_t w = c->p.band_b + (int64_t)(c->p.band_f * (float)mean);
-    return 2 * w + 1 > kWideBand ? 1 : 0;
-}
-
-// c->todo's groups in their launch lists (LPT order is kept: todo is in it)
-void build_lists(PoaCall *c) {
-    for (int k = 0; k < 3; ++k) c->lists[k].clear();
-    for (int32_t g : c->todo) c->lists[group_kind(c, g)].push_back(g);
-}
-
-// Queues c->todo's launches (c->lists, whose group lists are already on the device): each kind on its
-// own lane, after the batch's staging.  Lanes run the launches of consecutive batches in order, so
-// batch k + 1's grids start as batch k's drain.  Nothing on the device waits for a launch's end: a
-// stream-wait on another stream's event is a barrier packet in the waiting stream's hardware queue,
-// and streams share the process's hardware queues (GPU_MAX_HW_QUEUES) -- an io stream waiting there
-// for the wide launch held back a narrow launch queued behind it (measured: chunk 1's two launches
-// ran one after the other, 0.58 -> 1.05 s).  mando_poa_end waits for the launch events on the host.
-int enqueue_launches(mando_ctx *ctx, PoaCall *c) {
-    // the kind holding the heaviest group is enqueued first (its groups take the CUs first)
-    int korder[3] = {0, 1, 2};
-    double kcost[3] = {0, 0, 0};
-    for (int kind = 0; kind < 3; ++kind)
-        for (int32_t g : c->lists[kind]) {
-            const GroupStat &q = c->gs[(size_t)g];
-            kcost[kind] = std::max(kcost[kind], (double)(q.sum - q.first_len) * (double)q.first_len);
-        }
-    std::stable_sort(korder, korder + 3, [&](int x, int y) { return kcost[x] > kcost[y]; });
-    for (int ki = 0; ki < 3; ++ki) {
-        const int kind = korder[ki];
-        const std::vector<int32_t> &L = c->lists[kind];
-        c->launched[kind] = false;
-        if (L.empty()) continue;
-        hipStream_t lst = lane_of(ctx, kind);
-        HIP_TRY(hipStreamWaitEvent(lst, c->ev_staged, 0));
-        int64_t mf = 0, ms = 0, ml = 0, mr = 0;
-        for (int32_t g : L) {
-            const GroupStat &q = c->gs[(size_t)g];
-            mf = std::max(mf, q.first_len);
-            ms = std::max(ms, q.sum);
-            ml = std::max(ml, q.maxlen);
-            mr = std::max(mr, q.nreads);
-        }
-        mando::PoaCaps caps = plan_caps(c->p, mf, ms, ml, mr, c->attempt);
-        caps.seeded = kind == 2;
-        caps.wide = kind == 1;
-        int rc = launch_batch(ctx, c->p, caps, c->seq.as<uint8_t>(), c->seq_off.as<int64_t>(), c->grp_off.as<int64_t>(),
-                              c->gorder[kind].as<int32_t>(), (int64_t)L.size(), c->cons.as<uint8_t>(),
-                              c->cons_off.as<int64_t>(), c->cons_len.as<int32_t>(), c->cells.as<int64_t>(),
-                              c->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &c->sp : nullptr, c->ev_s[kind],
-                              c->ev_e[kind], kind);
-        if (rc) return rc;
-        c->launched[kind] = true;
-        c->launches += 1;
-    }
-    return MANDO_OK;
-}
-
-// the group lists of c->lists onto the device (on the staging stream, before ev_staged)
-int stage_lists(PoaCall *c, hipStream_t st) {
-    for (int kind = 0; kind < 3; ++kind) {
-        const std::vector<int32_t> &L = c->lists[kind];
-        if (L.empty()) continue;
-        int rc = c->gorder[kind].ensure(L.size() * 5);  // a quarter of slack
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(c->gorder[kind].p, L.data(), L.size() * 4, hipMemcpyHostToDevice, st));
-    }
-    return MANDO_OK;
-}
-
-int ensure_lanes(mando_ctx *ctx) {
-    if (ctx->ev_fork) return MANDO_OK;
-    for (int k = 0; k < 2; ++k) {
-        HIP_TRY(hipStreamCreateWithFlags(&ctx->lane_stream[k], hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&ctx->ev_lane[k], hipEventDisableTiming));
-    }
-    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-    return MANDO_OK;
-}
-
-// First half of a POA batch once its reads' layout (soff) is known: plan, stage + encode, queue the
-// launches; returns with the batch in flight (*ticket names it for poa_end_impl).
-int poa_begin_impl(mando_ctx *ctx, const mando_poa_params *params, std::vector<int64_t> &&soff, const int64_t *grp_off,
-                   int64_t n_groups, const uint8_t *seeding_per_group, const PoaStageFn &stage, int32_t *ticket) {
-    std::lock_guard<std::mutex> lk(ctx->poa_mu);
-    HIP_TRY(hipSetDevice(ctx->device));
-    int rc;
-    if ((rc = ensure_lanes(ctx))) return rc;
-    const int slot = ctx->call_next;
-    PoaCall *&c = ctx->calls[slot];
-    if (!c) {
-        c = new PoaCall();
-        if ((rc = c->init())) {
-            delete c;
-            c = nullptr;
-            return rc;
-        }
-    }
-    if (c->busy) return fail(MANDO_E_ARG, "two POA batches already in flight on this context (end one first)");
-    c->p = *params;
-    c->n_groups = n_groups;
-    c->soff = std::move(soff);
-    const std::vector<int64_t> &so = c->soff;
+// The POA batch once its reads' layout (soff) is known: stage + encode, plan, launch, collect.
+int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::vector<int64_t> &soff,
+                   const int64_t *grp_off, int64_t n_groups, const uint8_t *seeding_per_group, uint8_t *cons_out,
+                   int64_t cons_cap, int64_t *cons_off, int64_t *cells_out, const StageFn &stage) {
+    // -S for a group: seeding_per_group[g], or params->seeding for every group
+    auto seeded_group = [&](int64_t g) {
+        return seeding_per_group ? seeding_per_group[g] != 0 : params->seeding != 0;
+    };
     const int64_t n_reads = grp_off[n_groups];
-    const int64_t total = so[(size_t)n_reads];
+    const int64_t total = soff[(size_t)n_reads];
+    HIP_TRY(hipSetDevice(ctx->device));
+
     // per-group statistics (the bases are staged as ASCII and encoded on the device)
-    c->gs.assign((size_t)n_groups, GroupStat{});
-    c->ccap.assign((size_t)n_groups + 1, 0);
-    c->goff.assign(grp_off, grp_off + n_groups + 1);
-    c->seeded.assign((size_t)n_groups, 0);
-    bool any_seeded = false;
+    std::vector<GroupStat> gs((size_t)n_groups);
+    int64_t max_first = 0, max_sum = 0, max_len = 0, max_nreads = 0;
+    std::vector<int64_t> ccap((size_t)n_groups + 1, 0);
     for (int64_t g = 0; g < n_groups; ++g) {
-        GroupStat &q = c->gs[(size_t)g];
-        q.nreads = grp_off[g + 1] - grp_off[g];
+        GroupStat &s = gs[(size_t)g];
+        s.nreads = grp_off[g + 1] - grp_off[g];
         for (int64_t r = grp_off[g]; r < grp_off[g + 1]; ++r) {
-            const int64_t L = so[(size_t)r + 1] - so[(size_t)r];
-            if (L > 0 && q.first_len == 0) q.first_len = L;
-            q.sum += L;
-            q.maxlen = std::max(q.maxlen, L);
+            const int64_t L = soff[(size_t)r + 1] - soff[(size_t)r];
+            if (L > 0 && s.first_len == 0) s.first_len = L;
+            s.sum += L;
+            s.maxlen = std::max(s.maxlen, L);
         }
-        c->ccap[(size_t)g + 1] = c->ccap[(size_t)g] + 2 * q.maxlen + 256;
-        c->seeded[(size_t)g] = seeding_per_group ? seeding_per_group[g] != 0 : params->seeding != 0;
-        any_seeded |= c->seeded[(size_t)g] != 0;
+        max_first = std::max(max_first, s.first_len);
+        max_sum = std::max(max_sum, s.sum);
+        max_len = std::max(max_len, s.maxlen);
+        max_nreads = std::max(max_nreads, s.nreads);
+        ccap[(size_t)g + 1] = ccap[(size_t)g] + 2 * s.maxlen + 256;
     }
     // LPT order: most DP work first
-    c->todo.resize((size_t)n_groups);
-    std::iota(c->todo.begin(), c->todo.end(), 0);
-    std::stable_sort(c->todo.begin(), c->todo.end(), [&](int32_t x, int32_t y) {
-        const GroupStat &a = c->gs[(size_t)x], &b = c->gs[(size_t)y];
-        return (double)(a.sum - a.first_len) * (double)a.first_len > (double)(b.sum - b.first_len) * (double)b.first_len;
+    std::vector<int32_t> order((size_t)n_groups);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+        const GroupStat &a = gs[(size_t)x], &b = gs[(size_t)y];
+        return (double)(a.sum - a.first_len) * (double)a.first_len >
+               (double)(b.sum - b.first_len) * (double)b.first_len;
     });
-    c->attempt = 0;
-    c->launches = 0;
-    c->t_first = 1e300;
-    c->t_last = -1e300;
-    build_lists(c);
-    // buffers with a quarter of slack: a batch slot's buffers are reallocated (a device-wide wait)
-    // only when a batch outgrows them by more
-    auto grow = [](size_t b) { return b + b / 4; };
-    if ((rc = c->seq.ensure(grow((size_t)std::max<int64_t>(total, 1)))) || (rc = c->seq_off.ensure(grow(so.size() * 8))) ||
-        (rc = c->grp_off.ensure(grow(((size_t)n_groups + 1) * 8))) ||
-        (rc = c->cons_off.ensure(grow(((size_t)n_groups + 1) * 8))) ||
-        (rc = c->cons.ensure(grow((size_t)c->ccap[(size_t)n_groups]))) ||
-        (rc = c->cons_len.ensure(grow((size_t)n_groups * 4))) || (rc = c->cells.ensure(grow((size_t)n_groups * 8))) ||
-        (rc = c->status.ensure(grow((size_t)n_groups * 4))))
-        return rc;
-    // staging on the batch's io stream (idle: the batch slot's previous batch has ended): every
-    // host-to-device copy first (they are small), then the gather and encode kernels
-    hipStream_t st = c->io;
-    HIP_TRY(hipMemcpyAsync(c->seq_off.p, so.data(), so.size() * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(c->grp_off.p, c->goff.data(), c->goff.size() * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(c->cons_off.p, c->ccap.data(), c->ccap.size() * 8, hipMemcpyHostToDevice, st));
-    if ((rc = stage_lists(c, st))) return rc;
-    if (total > 0) {
-        if ((rc = stage(c, st))) return rc;
-        HIP_TRY(mando::launch_encode(c->seq.as<uint8_t>(), total, st));
-    }
-    // -S groups: their window partitions first (seed kernel over every read of a seeded group paired
-    // with the group's previous non-empty read); synchronous
-    if (any_seeded) {
-        auto sg = [&](int64_t g) { return c->seeded[(size_t)g] != 0; };
-        if ((rc = plan_seeds(ctx, c, *params, so, grp_off, n_groups, sg, c->sp, st))) return rc;
-    }
-    HIP_TRY(hipEventRecord(c->ev_staged, st));
-    if ((rc = enqueue_launches(ctx, c))) return rc;
-    c->busy = true;
-    c->gen = (c->gen + 1) & 0x3fffffff;
-    *ticket = c->gen * 2 + slot;
-    ctx->call_next ^= 1;
-    return MANDO_OK;
-}
 
-// Second half: waits for the batch, re-runs the groups whose workspace capacity was exceeded, and
-// collects the consensi (decoded to ASCII and packed back to back on the device, then one copy).
-int poa_end_impl(mando_ctx *ctx, int32_t ticket, uint8_t *cons_out, int64_t cons_cap, int64_t *cons_off,
-                 int64_t *cells_out, double *timing) {
-    const int slot = ticket & 1;
-    PoaCall *c = ctx->calls[slot];
-    if (ticket < 0 || !c || !c->busy || c->gen != ticket / 2)
-        return fail(MANDO_E_ARG, "mando_poa_end: no POA batch in flight under this ticket");
-    HIP_TRY(hipSetDevice(ctx->device));
-    struct Done {
-        PoaCall *c;
-        ~Done() { c->busy = false; }
-    } done{c};
-    const int64_t n_groups = c->n_groups;
+    int rc;
+    if ((rc = ctx->seq.ensure((size_t)std::max<int64_t>(total, 1))) || (rc = ctx->seq_off.ensure(soff.size() * 8)) ||
+        (rc = ctx->grp_off.ensure(((size_t)n_groups + 1) * 8)) ||
+        (rc = ctx->gorder.ensure((size_t)n_groups * 4)) ||
+        (rc = ctx->cons_off.ensure(((size_t)n_groups + 1) * 8)) ||
+        (rc = ctx->cons.ensure((size_t)ccap[(size_t)n_groups])) ||
+        (rc = ctx->cons_len.ensure((size_t)n_groups * 4)) ||
+        (rc = ctx->cells.ensure((size_t)n_groups * 8)) ||
+        (rc = ctx->status.ensure((size_t)n_groups * 4)))
+        return rc;
+    std::vector<int64_t> goff((size_t)n_groups + 1);
+    for (int64_t g = 0; g <= n_groups; ++g) goff[(size_t)g] = grp_off[g];
+    if (total > 0) {
+        if ((rc = stage(ctx))) return rc;
+        HIP_TRY(mando::launch_encode(ctx->seq.as<uint8_t>(), total, ctx->stream));
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->seq_off.p, soff.data(), soff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->grp_off.p, goff.data(), goff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->cons_off.p, ccap.data(), ccap.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+
+    // -S groups: their window partitions first (seed kernel over every read of a seeded group paired
+    // with the group's previous non-empty read)
+    SeedPlan sp;
+    bool any_seeded = false;
+    for (int64_t g = 0; g < n_groups && !any_seeded; ++g) any_seeded = seeded_group(g);
+    if (any_seeded) {
+        rc = plan_seeds(ctx, *params, soff, grp_off, n_groups, seeded_group, sp);
+        if (rc) return rc;
+    }
+
     std::vector<int32_t> st((size_t)n_groups), clen((size_t)n_groups);
     std::vector<int64_t> cells((size_t)n_groups);
-    int rc;
-    for (;;) {
-        for (int k = 0; k < 3; ++k)
-            if (c->launched[k]) HIP_TRY(hipEventSynchronize(c->ev_e[k]));
-        HIP_TRY(hipStreamSynchronize(c->io));
-        for (int k = 0; k < 3; ++k) {
-            if (!c->launched[k]) continue;
-            float a = 0, b = 0;
-            HIP_TRY(hipEventElapsedTime(&a, ctx->ev_ref, c->ev_s[k]));
-            HIP_TRY(hipEventElapsedTime(&b, ctx->ev_ref, c->ev_e[k]));
-            c->t_first = std::min(c->t_first, (double)a);
-            c->t_last = std::max(c->t_last, (double)b);
+    std::vector<int32_t> todo = order;
+    ctx->last_launches = 0;
+    for (int attempt = 0; attempt < 4 && !todo.empty(); ++attempt) {
+        // unseeded and seeded groups run as two launches of the two kernel instantiations
+        // three kinds of launch: unseeded groups with bands of one chunk, unseeded groups whose band
+        // (2w + 1 at their mean read length) exceeds one chunk (the wide-ring instantiation), -S groups
+        std::vector<int32_t> lists[3];
+        for (int32_t g : todo) {
+            const GroupStat &q = gs[(size_t)g];
+            const int64_t mean = q.sum / std::max<int64_t>(1, q.nreads);
+            const int64_t w = params->band_b + (int64_t)(params->band_f * (float)mean);
+            lists[seeded_group(g) ? 2 : (2 * w + 1 > kWideBand ? 1 : 0)].push_back(g);
         }
-        HIP_TRY(hipMemcpyAsync(st.data(), c->status.p, st.size() * 4, hipMemcpyDeviceToHost, c->io));
-        HIP_TRY(hipStreamSynchronize(c->io));
+        // several kinds: each runs on its own lane (stream + workspace), concurrently, after everything
+        // staged so far on the first stream
+        int nk = 0;
+        for (int kind = 0; kind < 3; ++kind) nk += !lists[kind].empty();
+        if (nk > 1) {
+            if (!ctx->ev_fork) {
+                HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+                for (int k = 0; k < 2; ++k) {
+                    HIP_TRY(hipStreamCreateWithFlags(&ctx->lane_stream[k], hipStreamNonBlocking));
+                    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_lane[k], hipEventDisableTiming));
+                }
+            }
+            HIP_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+            for (int k = 0; k < nk - 1; ++k) HIP_TRY(hipStreamWaitEvent(ctx->lane_stream[k], ctx->ev_fork, 0));
+        }
+        // the kind holding the heaviest group is enqueued first (its slots take the CUs first: a
+        // persistent launch holds them until its queue drains)
+        int korder[3] = {0, 1, 2};
+        double kcost[3] = {0, 0, 0};
+        for (int kind = 0; kind < 3; ++kind)
+            for (int32_t g : lists[kind]) {
+                const GroupStat &q = gs[(size_t)g];
+                kcost[kind] = std::max(kcost[kind], (double)(q.sum - q.first_len) * (double)q.first_len);
+            }
+        std::stable_sort(korder, korder + 3, [&](int x, int y) { return kcost[x] > kcost[y]; });
+        int lane = 0;
+        for (int ki = 0; ki < 3; ++ki) {
+            const int kind = korder[ki];
+            const std::vector<int32_t> &L = lists[kind];
+            if (L.empty()) continue;
+            hipStream_t lst = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
+            int64_t mf = 0, ms = 0, ml = 0, mr = 0;
+            for (int32_t g : L) {
+                mf = std::max(mf, gs[(size_t)g].first_len);
+                ms = std::max(ms, gs[(size_t)g].sum);
+                ml = std::max(ml, gs[(size_t)g].maxlen);
+                mr = std::max(mr, gs[(size_t)g].nreads);
+            }
+            mando::PoaCaps caps = plan_caps(*params, mf, ms, ml, mr, attempt);
+            caps.seeded = kind == 2;
+            caps.wide = kind == 1;
+            DevBuf &gb = kind == 0 ? ctx->gorder : (kind == 1 ? ctx->gorder_w : ctx->gorder2);
+            if ((rc = gb.ensure(L.size() * 4))) return rc;
+            HIP_TRY(hipMemcpyAsync(gb.p, L.data(), L.size() * 4, hipMemcpyHostToDevice, lst));
+            rc = launch_batch(ctx, *params, caps, ctx->seq.as<uint8_t>(), ctx->seq_off.as<int64_t>(),
+                              ctx->grp_off.as<int64_t>(), gb.as<int32_t>(), (int64_t)L.size(),
+                              ctx->cons.as<uint8_t>(), ctx->cons_off.as<int64_t>(),
+                              ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
+                              ctx->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &sp : nullptr, lane == 0,
+                              nk == 1, lane);
+            if (rc) return rc;
+            ctx->last_launches += 1;
+            ++lane;
+        }
+        if (nk > 1) {  // join the extra lanes; the batch's timing ends when every launch has
+            for (int k = 0; k < nk - 1; ++k) {
+                HIP_TRY(hipEventRecord(ctx->ev_lane[k], ctx->lane_stream[k]));
+                HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_lane[k], 0));
+            }
+            HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+        }
+        HIP_TRY(hipMemcpyAsync(st.data(), ctx->status.p, st.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(clen.data(), ctx->cons_len.p, clen.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(cells.data(), ctx->cells.p, cells.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
         std::vector<int32_t> again;
-        for (int32_t g : c->todo) {
+        for (int32_t g : todo) {
             if (st[(size_t)g] == mando::kStCap) again.push_back(g);
             else if (st[(size_t)g] != mando::kStOk)
                 return fail(MANDO_E_INTERNAL, "POA kernel reported status " + std::to_string(st[(size_t)g]) +
                                                   " for group " + std::to_string(g));
         }
-        if (again.empty()) break;
-        if (++c->attempt >= 4) return fail(MANDO_E_INTERNAL, "POA workspace capacity still exceeded after retries");
-        // re-run at larger capacities (the lanes may still hold the next batch's launches: these queue
-        // behind them)
-        std::lock_guard<std::mutex> lk(ctx->poa_mu);
-        c->todo.swap(again);
-        build_lists(c);
-        if ((rc = stage_lists(c, c->io))) return rc;
-        HIP_TRY(hipEventRecord(c->ev_staged, c->io));
-        if ((rc = enqueue_launches(ctx, c))) return rc;
+        todo.swap(again);
     }
-    HIP_TRY(hipMemcpyAsync(clen.data(), c->cons_len.p, clen.size() * 4, hipMemcpyDeviceToHost, c->io));
-    HIP_TRY(hipMemcpyAsync(cells.data(), c->cells.p, cells.size() * 8, hipMemcpyDeviceToHost, c->io));
-    HIP_TRY(hipStreamSynchronize(c->io));
+    if (!todo.empty())
+        return fail(MANDO_E_INTERNAL, "POA workspace capacity still exceeded after retries");
+
+    // consensi: decoded to ASCII and packed back to back on the device, then one copy of the used bytes
     int64_t used = 0;
     cons_off[0] = 0;
     for (int64_t g = 0; g < n_groups; ++g) {
@@ -939,36 +775,19 @@ int poa_end_impl(mando_ctx *ctx, int32_t ticket, uint8_t *cons_out, int64_t cons
         if (cells_out) cells_out[g] = cells[(size_t)g];
     }
     if (cons_out && used > 0 && used <= cons_cap) {
-        if ((rc = c->g_dst.ensure(((size_t)n_groups + 1) * 8)) || (rc = c->g_len.ensure((size_t)n_groups * 4)) ||
-            (rc = c->g_off.ensure((size_t)(n_groups + 1) * 8)) || (rc = c->cons_txt.ensure((size_t)used + 16)))
+        if ((rc = ctx->g_dst.ensure(((size_t)n_groups + 1) * 8)) || (rc = ctx->g_len.ensure((size_t)n_groups * 4)) ||
+            (rc = ctx->g_off.ensure((size_t)(n_groups + 1) * 8)) || (rc = ctx->cons_txt.ensure((size_t)used + 16)))
             return rc;
-        HIP_TRY(hipMemcpyAsync(c->g_dst.p, cons_off, ((size_t)n_groups + 1) * 8, hipMemcpyHostToDevice, c->io));
-        HIP_TRY(hipMemcpyAsync(c->g_len.p, clen.data(), (size_t)n_groups * 4, hipMemcpyHostToDevice, c->io));
-        HIP_TRY(hipMemcpyAsync(c->g_off.p, c->ccap.data(), ((size_t)n_groups + 1) * 8, hipMemcpyHostToDevice, c->io));
+        HIP_TRY(hipMemcpyAsync(ctx->g_dst.p, cons_off, ((size_t)n_groups + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->g_len.p, clen.data(), (size_t)n_groups * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(ctx->g_off.p, ccap.data(), ((size_t)n_groups + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
         const int blocks = (int)std::min<int64_t>(n_groups, (int64_t)ctx->n_cu * 32);
-        hipLaunchKernelGGL(decode_cons_kernel, dim3(blocks), dim3(256), 0, c->io, c->cons.as<uint8_t>(),
-                           c->g_off.as<int64_t>(), c->g_len.as<int32_t>(), c->g_dst.as<int64_t>(), n_groups,
-                           c->cons_txt.as<uint8_t>());
+        hipLaunchKernelGGL(decode_cons_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ctx->cons.as<uint8_t>(),
+                           ctx->g_off.as<int64_t>(), ctx->g_len.as<int32_t>(), ctx->g_dst.as<int64_t>(), n_groups,
+                           ctx->cons_txt.as<uint8_t>());
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(cons_out, c->cons_txt.p, (size_t)used, hipMemcpyDeviceToHost, c->io));
-        HIP_TRY(hipStreamSynchronize(c->io));
-    }
-    if (getenv("MANDO_LAUNCH_LOG")) {
-        for (int k = 0; k < 3; ++k) {
-            if (!c->launched[k]) continue;
-            float a = 0, b = 0;
-            (void)hipEventElapsedTime(&a, ctx->ev_ref, c->ev_s[k]);
-            (void)hipEventElapsedTime(&b, ctx->ev_ref, c->ev_e[k]);
-            fprintf(stderr, "[mando launch] batch %d kind %d: %.1f -> %.1f ms (%.1f ms)\n", ticket, k, a, b, b - a);
-        }
-    }
-    const double span = c->t_last >= c->t_first ? c->t_last - c->t_first : 0.0;
-    ctx->last_ms = (float)span;
-    ctx->last_launches = c->launches;
-    if (timing) {
-        timing[0] = span;
-        timing[1] = c->t_first < 1e299 ? c->t_first : 0.0;
-        timing[2] = c->t_last > -1e299 ? c->t_last : 0.0;
+        HIP_TRY(hipMemcpyAsync(cons_out, ctx->cons_txt.p, (size_t)used, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
     if (used > cons_cap || (!cons_out && used > 0)) return fail(MANDO_E_CAP, "cons_out too small");
     return MANDO_OK;
@@ -992,43 +811,24 @@ int segment_layout(const int64_t *off, const int32_t *len, int64_t n, int64_t te
     return MANDO_OK;
 }
 
-// read r = text[off[r] .. + len[r]) (reverse-complemented when rc[r]) -> dst + soff[r], on `stream`
-int gather_into(const uint8_t *d_text, const int64_t *off, const int32_t *len, const int8_t *rc,
-                const std::vector<int64_t> &soff, DevBuf &goff, DevBuf &glen, DevBuf &gdst, DevBuf &grc, uint8_t *dst,
-                int n_cu, hipStream_t stream) {
+int gather_stage(mando_ctx *ctx, const uint8_t *d_text, const int64_t *off, const int32_t *len, const int8_t *rc,
+                 const std::vector<int64_t> &soff) {
     const int64_t n = (int64_t)soff.size() - 1;
     if (n <= 0) return MANDO_OK;
     int e;
-    if ((e = goff.ensure((size_t)n * 8)) || (e = glen.ensure((size_t)n * 4)) || (e = gdst.ensure((size_t)n * 8)) ||
-        (rc && (e = grc.ensure((size_t)n))))
+    if ((e = ctx->g_off.ensure((size_t)n * 8)) || (e = ctx->g_len.ensure((size_t)n * 4)) ||
+        (e = ctx->g_dst.ensure((size_t)n * 8)) || (rc && (e = ctx->g_rc.ensure((size_t)n))))
         return e;
-    HIP_TRY(hipMemcpyAsync(goff.p, off, (size_t)n * 8, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(glen.p, len, (size_t)n * 4, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(gdst.p, soff.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream));
-    if (rc) HIP_TRY(hipMemcpyAsync(grc.p, rc, (size_t)n, hipMemcpyHostToDevice, stream));
-    const int blocks = (int)std::min<int64_t>(n, (int64_t)n_cu * 32);
-    hipLaunchKernelGGL(gather_kernel, dim3(blocks), dim3(256), 0, stream, d_text, goff.as<int64_t>(),
-                       glen.as<int32_t>(), rc ? grc.as<int8_t>() : nullptr, gdst.as<int64_t>(), n, dst);
+    HIP_TRY(hipMemcpyAsync(ctx->g_off.p, off, (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->g_len.p, len, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->g_dst.p, soff.data(), (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (rc) HIP_TRY(hipMemcpyAsync(ctx->g_rc.p, rc, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    const int blocks = (int)std::min<int64_t>(n, (int64_t)ctx->n_cu * 32);
+    hipLaunchKernelGGL(gather_kernel, dim3(blocks), dim3(256), 0, ctx->stream, d_text, ctx->g_off.as<int64_t>(),
+                       ctx->g_len.as<int32_t>(), rc ? ctx->g_rc.as<int8_t>() : nullptr, ctx->g_dst.as<int64_t>(), n,
+                       ctx->seq.as<uint8_t>());
     HIP_TRY(hipGetLastError());
     return MANDO_OK;
-}
-
-int gather_stage(mando_ctx *ctx, const uint8_t *d_text, const int64_t *off, const int32_t *len, const int8_t *rc,
-                 const std::vector<int64_t> &soff) {
-    return gather_into(d_text, off, len, rc, soff, ctx->g_off, ctx->g_len, ctx->g_dst, ctx->g_rc,
-                       ctx->seq.as<uint8_t>(), ctx->n_cu, ctx->stream);
-}
-
-// argument checks and layout of mando_poa_segments(_begin)
-int segments_prepare(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *d_text, int64_t text_len,
-                     const int64_t *off, const int32_t *len, const int64_t *grp_off, int64_t n_groups,
-                     std::vector<int64_t> &soff) {
-    if (!ctx || !params || !grp_off || n_groups < 0) return fail(MANDO_E_ARG, "mando_poa_segments: bad argument");
-    int e = check_groups(grp_off, n_groups);
-    if (e) return e;
-    const int64_t n_reads = grp_off[n_groups];
-    if (n_reads > 0 && (!d_text || !off || !len)) return fail(MANDO_E_ARG, "mando_poa_segments: null segments");
-    return segment_layout(off, len, n_reads, text_len, soff);
 }
 
 }  // namespace
@@ -1054,37 +854,12 @@ int mando_poa_batch(mando_ctx *ctx, const mando_poa_params *params, const uint8_
     if (total > 0 && !seqs) return fail(MANDO_E_ARG, "null seqs");
     std::vector<int64_t> soff((size_t)n_reads + 1);
     for (int64_t r = 0; r <= n_reads; ++r) soff[(size_t)r] = seq_off[r] - seq_off[0];
-    int32_t ticket = -1;
-    rc = poa_begin_impl(ctx, params, std::move(soff), grp_off, n_groups, seeding_per_group,
-                        [&](PoaCall *c, hipStream_t st) -> int {
-                            HIP_TRY(hipMemcpyAsync(c->seq.p, seqs + seq_off[0], (size_t)total, hipMemcpyHostToDevice, st));
-                            return MANDO_OK;
-                        },
-                        &ticket);
-    if (rc) return rc;
-    return poa_end_impl(ctx, ticket, cons_out, cons_cap, cons_off, cells_out, nullptr);
-}
-
-int mando_poa_segments_begin(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *d_text, int64_t text_len,
-                             const int64_t *off, const int32_t *len, const int8_t *rc, const int64_t *grp_off,
-                             int64_t n_groups, const uint8_t *seeding_per_group, int32_t *ticket) {
-    if (!ticket) return fail(MANDO_E_ARG, "mando_poa_segments_begin: null ticket");
-    std::vector<int64_t> soff;
-    int e = segments_prepare(ctx, params, d_text, text_len, off, len, grp_off, n_groups, soff);
-    if (e) return e;
-    const int n_cu = ctx->n_cu;
-    return poa_begin_impl(ctx, params, std::move(soff), grp_off, n_groups, seeding_per_group,
-                          [&](PoaCall *c, hipStream_t st) {
-                              return gather_into(d_text, off, len, rc, c->soff, c->g_off, c->g_len, c->g_dst, c->g_rc,
-                                                 c->seq.as<uint8_t>(), n_cu, st);
-                          },
-                          ticket);
-}
-
-int mando_poa_end(mando_ctx *ctx, int32_t ticket, uint8_t *cons_out, int64_t cons_cap, int64_t *cons_off,
-                  int64_t *cells_out, double *timing) {
-    if (!ctx || !cons_off || cons_cap < 0) return fail(MANDO_E_ARG, "mando_poa_end: bad argument");
-    return poa_end_impl(ctx, ticket, cons_out, cons_cap, cons_off, cells_out, timing);
+    return poa_batch_impl(ctx, params, soff, grp_off, n_groups, seeding_per_group, cons_out, cons_cap, cons_off,
+                          cells_out, [&](mando_ctx *c) -> int {
+                              HIP_TRY(hipMemcpyAsync(c->seq.p, seqs + seq_off[0], (size_t)total, hipMemcpyHostToDevice,
+                                                     c->stream));
+                              return MANDO_OK;
+                          });
 }
 
 int mando_poa_segments(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *d_text, int64_t text_len,
@@ -1097,11 +872,14 @@ int mando_poa_segments(mando_ctx *ctx, const mando_poa_params *params, const uin
         cons_off[0] = 0;
         return MANDO_OK;
     }
-    int32_t ticket = -1;
-    int e = mando_poa_segments_begin(ctx, params, d_text, text_len, off, len, rc, grp_off, n_groups, seeding_per_group,
-                                     &ticket);
+    int e = check_groups(grp_off, n_groups);
     if (e) return e;
-    return poa_end_impl(ctx, ticket, cons_out, cons_cap, cons_off, cells_out, nullptr);
+    const int64_t n_reads = grp_off[n_groups];
+    if (n_reads > 0 && (!d_text || !off || !len)) return fail(MANDO_E_ARG, "mando_poa_segments: null segments");
+    std::vector<int64_t> soff;
+    if ((e = segment_layout(off, len, n_reads, text_len, soff))) return e;
+    return poa_batch_impl(ctx, params, soff, grp_off, n_groups, seeding_per_group, cons_out, cons_cap, cons_off,
+                          cells_out, [&](mando_ctx *c) { return gather_stage(c, d_text, off, len, rc, soff); });
 }
 
 int mando_selftest(mando_ctx *ctx, int *bad) {

@@ -308,25 +308,6 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         if dev_poa:
             return _gpu_poa(res, *prep[1:], asm.seeding)
         return consensus_fn(*prep[1:], asm.seeding)
-
-    def _gpu_poa_begin(res, off, length, rc, g, sd):
-        # the POA batch queued (mando_poa_segments_begin) on slot 0: its launches run behind the previous
-        # chunk's on the same lanes
-        from . import poa
-
-        info = {}
-        d, n = res.device_text()
-        b = poa.poa_segments_begin(d, n, off, length, rc, g, seeding=sd, device=device, info=info, slot=0)
-        info["read_bytes"] = int(np.asarray(length, dtype=np.int64).sum())
-        info["reads"] = int(g[-1])
-        return b
-
-    def _gpu_poa_end(b):
-        out = b.end()
-        if "kernel_ms" in b.info:
-            b.info["cons_bytes"] = int(out[1][-1])
-            poa_launches.append(b.info)
-        return out
     out_path = path + "/"
     out_tmp = out_path + "/tmp_SS"
     wl = list(white_list_polyA)
@@ -371,7 +352,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         # with few, large loci (SIRV-like: 7 loci; config 5: 100) one chunk is faster (1.22 -> 0.81 s,
         # 2.51 -> 2.43 s), since a chunk's kernels then run one wave per locus on an idle GPU
         n_chunks = 1 if sizes.sum() < (64 << 20) or len(my_roots) < 1024 else 2
-        fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.4"))] if n_chunks == 2 else None
+        fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.3"))] if n_chunks == 2 else None
         # large inputs (config 4 on one GPU: ~60 GB of locus text): chunks of at most kChunkBytes, the
         # first 0.4 of one, so one chunk's text, clustering scratch and the POA workspaces fit in HBM
         # together
@@ -454,42 +435,14 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         timeline.append(("poa", tp - t0, time.perf_counter() - t0))
         return pl, res
 
-    # HIP POA with several chunks: a chunk's batch is queued (begin) by the POA thread as soon as its
-    # assembly is ready, and collected (end) by the collector thread in chunk order; two batches are in
-    # flight at most (the context's two batch slots), so chunk k + 1's launches wait on the lanes behind
-    # chunk k's and take the CUs as its last groups finish, instead of after chunk k's collection
-    poa_async = dev_poa and len(spans) > 1 and os.environ.get("MANDO_POA_ASYNC", "1") == "1"
-    in_flight = threading.Semaphore(2)
-
-    def poa_begin_job(res, asm_fut):
-        prep = asm_fut.result()
-        in_flight.acquire()
-        try:
-            tp = time.perf_counter()
-            b = _gpu_poa_begin(res, *prep[1:], prep[0].seeding)
-            timeline.append(("poa_queue", tp - t0, time.perf_counter() - t0))
-            return prep, b, tp
-        except BaseException:
-            in_flight.release()
-            raise
-
-    def poa_end_job(begin_fut, res, lo, hi):
-        prep, b, tp = begin_fut.result()
-        try:
-            pl = _poa_chunk(res, mine[lo:hi], prep, lambda _r, _p: _gpu_poa_end(b), stats, lock)
-        finally:
-            in_flight.release()
-        timeline.append(("poa", tp - t0, time.perf_counter() - t0))
-        return pl, res
-
     # one POA host thread (one device context) by default: with two, a chunk whose predecessor's POA
     # ran late went to the second context, whose workspace was then sized from the HBM the first one
     # left free -- a quarter of the slots, the persistent grid, 2.9 s instead of 1.1 s (measured in 3 of
     # 30 config-3 steps; none in 18 with one context)
-    n_poa = int(os.environ.get("MANDO_POA_STREAMS", "1")) if len(spans) > 1 and not poa_async else 1
+    n_poa = int(os.environ.get("MANDO_POA_STREAMS", "1")) if len(spans) > 1 else 1
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
             ThreadPoolExecutor(max_workers=1) as writer, \
-            ThreadPoolExecutor(max_workers=n_poa) as gpu_poa, ThreadPoolExecutor(max_workers=1) as collector:
+            ThreadPoolExecutor(max_workers=n_poa) as gpu_poa:
         cl = [ex.submit(run_cluster, lo, hi) for lo, hi in spans]
         poa_futs = []
         # one rank: reads2isoforms.txt needs only the clustering, so each chunk's part of it is written
@@ -542,11 +495,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                 timeline.append(("orient", tg - t0, te - t0))
                 add("t_orient", te - tg)
                 asm_fut = host.submit(assemble, res, hits, n_hits)
-                if poa_async:
-                    poa_futs.append(collector.submit(poa_end_job, gpu_poa.submit(poa_begin_job, res, asm_fut),
-                                                     res, lo, hi))
-                else:
-                    poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
+                poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
                 if world == 1:
                     r2_futs.append(host.submit(write_r2i, res, lo, hi, n_iso_before))
                     fa_futs.append(writer.submit(write_fasta, poa_futs[-1], n_iso_before, r2_futs[-1]))

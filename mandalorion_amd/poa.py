@@ -133,55 +133,3 @@ def poa_consensus_segments(d_text: int, text_len: int, off: np.ndarray, length: 
             info["kernel_ms"] = ctx.last_kernel_ms()
             info["launches"] = ctx.last_kernel_launches()
     return cons[:int(cons_off[-1])], cons_off
-
-
-class PoaBatch:
-    """A POA batch in flight (mando_poa_segments_begin): `end()` waits for it and returns what
-    poa_consensus_segments returns.  The device text and the host arrays stay referenced until then."""
-
-    def __init__(self, ctx, ticket: int, keep: tuple, n: int, cap: int, info: dict | None):
-        self.ctx, self.ticket, self.keep, self.n, self.cap, self.info = ctx, ticket, keep, n, cap, info
-        self.done = False
-
-    def end(self):
-        if self.done:
-            raise RuntimeError("PoaBatch.end() called twice")
-        self.done = True
-        n = self.n
-        cons = np.empty(self.cap, dtype=np.uint8)
-        cons_off = np.zeros(n + 1, dtype=np.int64)
-        cells = np.zeros(max(n, 1), dtype=np.int64) if self.info is not None else None
-        timing = np.zeros(3, dtype=np.float64)
-        if n > 0:
-            _lib.check(self.ctx.lib.mando_poa_end(self.ctx.handle, self.ticket, _lib.ptr(cons), self.cap,
-                                                  _lib.ptr(cons_off), _lib.ptr(cells), _lib.ptr(timing)))
-            if self.info is not None:
-                self.info["cells"] = int(cells[:n].sum())
-                self.info["kernel_ms"] = float(timing[0])
-                self.info["kernel_start_ms"] = float(timing[1])
-                self.info["kernel_end_ms"] = float(timing[2])
-                self.info["launches"] = self.ctx.last_kernel_launches()
-        self.keep = None
-        return cons[:int(cons_off[-1])], cons_off
-
-
-def poa_segments_begin(d_text: int, text_len: int, off: np.ndarray, length: np.ndarray, rc: np.ndarray | None,
-                       grp_off: np.ndarray, seeding=None, device: int = 0, params: _lib.PoaParams | None = None,
-                       info: dict | None = None, slot: int = 0) -> PoaBatch:
-    """poa_consensus_segments split in two (mando_poa_segments_begin / mando_poa_end): returns once the
-    batch is queued; at most two batches per slot are in flight."""
-    ctx = _lib.context(device, slot)
-    p = params or _lib.PoaParams.defaults()
-    n = int(len(grp_off)) - 1
-    off = np.ascontiguousarray(off, dtype=np.int64)
-    length = np.ascontiguousarray(length, dtype=np.int32)
-    rc = None if rc is None else np.ascontiguousarray(rc, dtype=np.int8)
-    grp_off = np.ascontiguousarray(grp_off, dtype=np.int64)
-    seed_arr = None if seeding is None else np.ascontiguousarray(np.asarray(seeding, dtype=np.uint8))
-    cap = int(length.sum()) * 2 + 1024
-    ticket = _lib.ctypes.c_int32(-1)
-    if n > 0:
-        _lib.check(ctx.lib.mando_poa_segments_begin(ctx.handle, _lib.ctypes.byref(p), _lib.ctypes.c_void_p(d_text),
-                                                    int(text_len), _lib.ptr(off), _lib.ptr(length), _lib.ptr(rc),
-                                                    _lib.ptr(grp_off), n, _lib.ptr(seed_arr), _lib.ctypes.byref(ticket)))
-    return PoaBatch(ctx, ticket.value, (off, length, rc, grp_off, seed_arr, p), n, cap, info)
