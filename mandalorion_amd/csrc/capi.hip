@@ -181,6 +181,9 @@ constexpr int64_t kWideBand = 112;
 // share of the free HBM the POA workspace may take (one slot per resident wave; deep, long groups
 // need ~100 MB per slot, so the share decides how many waves run)
 constexpr double kWsShare = MANDO_WS_SHARE;
+// ... and at most this share of the device's HBM: a many-chunk run (config 4 on one GPU, ~60 GB of locus
+// text) keeps two chunks' text, clustering scratch and orientation buffers next to the workspaces
+constexpr double kWsTotalShare = 0.45;
 
 struct GroupStat {
     int64_t nreads = 0, first_len = 0, sum = 0, maxlen = 0;
@@ -269,7 +272,9 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget
     size_t free_b = 0, total_b = 0;
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    const size_t budget = std::max<size_t>((size_t)1 << 30, (size_t)(kWsShare * (double)free_b) + ws.bytes);
+    const size_t budget = std::max<size_t>(
+        (size_t)1 << 30, std::min<size_t>((size_t)(kWsShare * (double)free_b) + ws.bytes,
+                                          (size_t)(kWsTotalShare * (double)total_b)));
     // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
