@@ -1440,6 +1440,16 @@ template <class T>
 __device__ __forceinline__ void row_store(gu8 *row_base, uint32_t lane_off, T v) {
     *reinterpret_cast<GLB T *>(uniptr(row_base) + lane_off) = v;
 }
+// A lane's 16-bit store at byte uoff + lane_off of a slot array (base: the array, loop-invariant in
+// SGPRs; uoff: the row's uniform offset).  The per-row offset is folded into the lane's zero-extended
+// 32-bit offset, so the compiler selects the saddr form (one v_add per store) instead of building the
+// 64-bit row address on the scalar unit (s_ashr + s_add + s_addc) and a 64-bit lane address.  (An
+// inline-asm store of the same form faulted: the compiler does not see a VMEM instruction in an asm
+// statement, so it places no wait states between a VALU write of the base SGPRs -- v_readlane of a
+// spilled SGPR -- and the store's read of them.)
+__device__ __forceinline__ void row_store16(gu8 *base, int uoff, uint32_t lane_off, uint32_t v) {
+    *reinterpret_cast<GLB uint16_t *>(base + (uint64_t)((uint32_t)uoff + lane_off)) = (uint16_t)v;
+}
 
 // ---- 16-bit mode with scalar row control -------------------------------------------------------
 // Everything that is uniform per row (descriptor, predecessor band records, band, fast-path
@@ -1457,7 +1467,8 @@ struct Row16 {
     int pn3;                      // predecessor count when >= 3 (predecessors 2.. are read in row16_vec)
 };
 
-template <class SC, int RW>
+// ONE: the row has exactly one predecessor (no second-predecessor merge, no predecessor bytes)
+template <class SC, int RW, bool ONE = false>
 __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *sv, gint *rinfo, SharedState &sh,
                                          int lane, const Row16 &R, DpState &ds) {
     constexpr int HW = RW / 2;  // ring words per plane
@@ -1498,7 +1509,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
         X2 = bfi(me, kNeg2, X2);
     }
     uint32_t MK = 0, K1 = 0, K2 = 0;
-    if (R.two) {
+    if (!ONE && R.two) {
         const uint32_t *w1 = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, R.p1slot));
         uint32_t Hd1 = __builtin_amdgcn_alignbit(w1[iw], w1[iwp], 16);
         uint32_t X11 = w1[HW + iw], X21 = w1[2 * HW + iw];
@@ -1520,7 +1531,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     }
     // predecessors 2.. of a multi-predecessor row (records re-read from the LDS row ring; the first
     // strictly larger value names the predecessor, as in dp_row)
-    for (int k = 2; k < R.pn3; ++k) {
+    for (int k = 2; k < (ONE ? 0 : R.pn3); ++k) {
         const int p = bcast0(sh.desc[R.r & (kDescBatch - 1)][3 + k]);
         const int4 x = sh.rrow[p & (kRowRing - 1)];
         const int bk = bcast0(x.x), ek = bcast0(x.y);
@@ -1570,16 +1581,15 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     const uint32_t tbv = tb_pack(pk_subs(M, H), pk_subs(X1, H), pk_subs(X2, H), pk_subs(F1, H), pk_subs(Ho1, X1e),
                                  pk_subs(Ho2, X2e), pk_subs(G1, P1), pk_subs(G2, P2));
     // this row's bytes start at ds.tb_used: column j0 = cb0 + 2 lane is at tb_used + 2 lane
-    row_store<uint16_t>(tb + ds.tb_used, 2u * (uint32_t)lane, (uint16_t)tbv);
-    if (R.multi) {
-        gu8 *kq = kp + ds.kp_used;
+    row_store16(tb, ds.tb_used, 2u * (uint32_t)lane, tbv);
+    if (!ONE && R.multi) {
         if (ks == 1) {  // packed: k < 8 in each half, so the shifts stay inside the halves
             const uint32_t kb = MK | (K1 << 2) | (K2 << 4);
-            row_store<uint16_t>(kq, 2u * (uint32_t)lane, (uint16_t)__builtin_amdgcn_perm(0u, kb, 0x0C0C0200u));
+            row_store16(kp, ds.kp_used, 2u * (uint32_t)lane, __builtin_amdgcn_perm(0u, kb, 0x0C0C0200u));
         } else {
-            row_store<uint16_t>(kq, 6u * (uint32_t)lane, (uint16_t)__builtin_amdgcn_perm(K1, MK, 0x0C0C0400u));
-            row_store<uint16_t>(kq, 6u * (uint32_t)lane + 2u, (uint16_t)__builtin_amdgcn_perm(MK, K2, 0x0C0C0600u));
-            row_store<uint16_t>(kq, 6u * (uint32_t)lane + 4u, (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u));
+            row_store16(kp, ds.kp_used, 6u * (uint32_t)lane, __builtin_amdgcn_perm(K1, MK, 0x0C0C0400u));
+            row_store16(kp, ds.kp_used, 6u * (uint32_t)lane + 2u, __builtin_amdgcn_perm(MK, K2, 0x0C0C0600u));
+            row_store16(kp, ds.kp_used, 6u * (uint32_t)lane + 4u, __builtin_amdgcn_perm(K2, K1, 0x0C0C0602u));
         }
     }
     const uint32_t Hs = bfi(inv, kNeg2, H);
@@ -1599,7 +1609,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     ds.r16acc = pk_umin(ds.r16acc, as_u32(as_u16x2(Hs) - as_u16x2(pk2(kR16Low))));
     const int besti = cb0 + 127 - (mp & 127);
     ds.tb_used += R.tbw;
-    if (R.multi) ds.kp_used += ks * R.tbw;
+    if (!ONE && R.multi) ds.kp_used += ks * R.tbw;
     if (R.far) ds.sv_used += 3 * kChunk;
     ds.cells += end - beg + 1;
     if (lane == 0) {
@@ -1861,11 +1871,71 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         const int dp1 = np1;
         nA = *reinterpret_cast<const int4 *>(&sh.desc[(i + 1) & (kDescBatch - 1)][0]);
         np1 = sh.desc[(i + 1) & (kDescBatch - 1)][4];
+        const int node = bcast0(dA.x), d1 = bcast0(dA.y), rem = bcast0(dA.z), p0 = bcast0(dA.w);
+        const int p1 = bcast0(dp1);
+        // one predecessor, in the LDS ring (~60 % of the config-3 rows): its own, shorter band /
+        // fast-path computation and row instance (row16_vec<..., ONE>), DP 2,781 -> 2,468 cycles per
+        // row with the saddr traceback stores.  Its own row record (Q, not R: sharing one struct with
+        // the general path kept R's fields live around the loop, a dozen s_mov per row), and
+        // structured if/else only (an early `continue` left the CFG structurizer a per-row dispatch
+        // through a VGPR selector).  Measured and dropped (profiles/r03d_poa_kernel_ab.txt): the same
+        // specialisation for two-predecessor rows (+7 %: register pressure spilled SGPRs into VGPR
+        // lanes on the row path) and the next descriptor's LDS address kept in a VGPR (+4 %).
+        const uint32_t shape = (uint32_t)d1 & 0xffff8000u;  // fast-row bit | predecessor count
+        bool done = false;
+        if (shape == 0x18000u) {
+            Row16 Q;
+            int bad1;
+            int am0;
+            if (p0 == prv_r) {
+                Q.b0 = prv_beg;
+                Q.e0 = prv_end;
+                am0 = prv_am;
+            } else {
+                const int4 x = sh.rrow[p0 & (kRowRing - 1)];
+                Q.b0 = bcast0(x.x);
+                Q.e0 = bcast0(x.y);
+                am0 = bcast0(x.z);
+            }
+            const int xr = qlen - rem;
+            Q.beg = max(0, min(am0 + 1, xr) - w);
+            Q.end = min(qlen, max(am0 + 1, xr) + w);
+            Q.cb0 = Q.beg & ~1;
+            const int span = Q.end - Q.cb0 + 1;
+            Q.tbw = (span + 3) & ~3;
+            const int pc0 = Q.b0 & ~1;
+            bad1 = (RW - span) | (RW - 1 - (Q.e0 - pc0));
+            if constexpr (CAP) bad1 |= (tb_lim - ds.tb_used) | (kp_lim - ds.kp_used) | (sv_lim - ds.sv_used);
+            Q.nomask = RW == kChunk && ((Q.beg - 1 - pc0) | (pc0 + kChunk - 1 - Q.end)) >= 0;
+            Q.r = r;
+            Q.node = node;
+            Q.vb = d1 & 0xff;
+            Q.pn = 1;
+            Q.far = (d1 >> 8) & 1;
+            Q.two = Q.multi = Q.pn3 = 0;
+            Q.p0slot = Q.p1slot = p0 & (kRing16 - 1);
+            Q.b1 = Q.b0;
+            Q.e1 = Q.e0;
+            if (bad1 >= 0) {
+#ifdef MANDO_ROW_STATS
+                ds.seg[0] += (Q.r - 1) == prv_r && Q.p0slot == (prv_r & (kRing16 - 1));
+                ds.seg[2] += Q.nomask;
+#endif
+                int besti;
+                if (RW == kChunk || Q.end - Q.cb0 < kChunk) besti = row16_vec<SC, RW, true>(sc, tb, kp, sv, rinfo, sh, lane, Q, ds);
+                else besti = row16w_vec(sc, tb, kp, sv, rinfo, sh, lane, Q, ds);
+                prv_r = r;
+                prv_beg = Q.beg;
+                prv_end = Q.end;
+                prv_am = besti;
+                ++nfast;
+                done = true;
+            }
+        }
+        if (!done) {
         int bad = -1;
         Row16 R;
         {
-            const int node = bcast0(dA.x), d1 = bcast0(dA.y), rem = bcast0(dA.z), p0 = bcast0(dA.w);
-            const int p1 = bcast0(dp1);
             if (d1 & 0xC000) {  // 1-kPreInline predecessors, all in the LDS ring (build_desc)
                 int am0, am1;
                 if (p0 == prv_r) {
@@ -1969,6 +2039,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
             prv_beg = bcast0(x.x);
             prv_end = bcast0(x.y);
             prv_am = bcast0(x.z);
+        }
         }
     }
         return kStOk;
@@ -2091,7 +2162,9 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
 // backtrack: fills qnode[q] = aligned node or -1 (insertion) for q in [0, qlen)
 // row record: rinfo[r] = {beg, end, tbbase, kpbase, argmax, soff, node, pre_n}; the fast rows write
 // argmax / soff only for far rows (the only ones read back from HBM) and never node / pre_n (the
-// backtrack takes those from the row's descriptor)
+// backtrack takes those from the row's descriptor).  (Putting argmax / soff first, so that the LDS
+// ring and the record share one register tuple, cost the backtrack a second load per window row:
+// +9 % backtrack cycles for -1 % DP cycles, measured r03 kab3 v4 / v5.)
 //
 // The walk is inherently serial, so its cost is the latency chain per step.  Walking HBM directly
 // costs three dependent global loads per step (row record -> traceback byte -> predecessor byte).
