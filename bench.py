@@ -97,6 +97,36 @@ WORKLOADS = {
 }
 
 
+def log(msg: str) -> None:
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+class heartbeat:
+    """A line on stderr every 30 s while a long, silent call (data generation) runs."""
+
+    def __init__(self, what: str):
+        self.what = what
+
+    def __enter__(self):
+        import threading
+
+        self.stop = threading.Event()
+        t0 = time.perf_counter()
+
+        def beat():
+            while not self.stop.wait(30.0):
+                log(f"{self.what}: {time.perf_counter() - t0:.0f} s")
+
+        self.th = threading.Thread(target=beat, daemon=True)
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join()
+        return False
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -309,7 +339,10 @@ def main():
             raise SystemExit(f"rank {rank}: {world} ranks need the RCCL transport, got {comm.backend!r}")
     n_gpus = comm.world if comm is not None else 1
     if rank == 0:
-        records = gen_data(data, wl, n_loci, gen_threads)
+        tg = time.perf_counter()
+        with heartbeat("synthetic data"):
+            records = gen_data(data, wl, n_loci, gen_threads)
+        log(f"data: {records} records in {data} ({time.perf_counter() - tg:.1f} s)")
     if comm is not None:
         comm.barrier()
     records = int(open(os.path.join(data, "records.txt")).read())
@@ -333,12 +366,19 @@ def main():
         cpu.update(nproc=cores["nproc"], affinity=cores["affinity"], cgroup_quota=cores["cgroup_quota"])
 
     ctx = _lib.context(local)
-    for _ in range(args.warmup):
+    for k in range(args.warmup):
+        tw = time.perf_counter()
         run_define(data, threads, local, comm)
+        if rank == 0:
+            log(f"warmup step {k}: {time.perf_counter() - tw:.3f} s")
     if comm is not None:
         comm.barrier()
     t0 = time.perf_counter()
-    stats = [run_define(data, threads, local, comm) for _ in range(args.steps)]
+    stats = []
+    for k in range(args.steps):
+        stats.append(run_define(data, threads, local, comm))
+        if rank == 0:  # progress on stderr (a long run must not look idle); one line per step
+            log(f"step {k}: {stats[-1]['t_total']:.3f} s")
     if comm is not None:
         comm.barrier()
     elapsed = time.perf_counter() - t0
