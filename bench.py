@@ -398,7 +398,7 @@ def main():
     achieved = (alg / max(1, n_launch)) / (k_ms / max(1, n_launch) / 1e3) / 1e9 if k_ms > 0 else 0.0
     # HBM traffic from the PMC passes (tools/pmc_traffic.py), only when they were measured on this workload
     # and on the POA sources benchmarked now
-    traffic, pmc_note = None, "no PMC file"
+    traffic, traffic_raw, pmc_note = None, None, "no PMC file"
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
@@ -408,6 +408,7 @@ def main():
                 pmc_note = "PMC file measured on other POA sources (dropped)"
             else:
                 traffic = pm.get("hbm_bytes_per_launch")
+                traffic_raw = pm.get("hbm_bytes_per_launch_raw")
                 pmc_note = f"PMC passes of commit {pm.get('commit', '?')}"
         except Exception as e:  # noqa: BLE001
             pmc_note = f"unreadable PMC file: {e}"
@@ -475,6 +476,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_raw": traffic_raw,
             "traffic_source": pmc_note,
             "kernel": "poa_kernel",
             "note": "integer DP, no MFMA; the kernel is issue/latency-bound (SQ counters: DESIGN.md §3.1)",
