@@ -182,8 +182,10 @@ constexpr int64_t kWideBand = 112;
 // need ~100 MB per slot, so the share decides how many waves run)
 constexpr double kWsShare = MANDO_WS_SHARE;
 // ... and at most this share of the device's HBM: a many-chunk run (config 4 on one GPU, ~60 GB of locus
-// text) keeps two chunks' text, clustering scratch and orientation buffers next to the workspaces
-constexpr double kWsTotalShare = 0.45;
+// text) keeps two chunks' text, clustering scratch and orientation buffers next to the workspaces.
+// 0.45 was too tight: a config-3 chunk's narrow launch then got half the slots it needs for the
+// one-group grid (persistent grid, POA kernels +25 %, measured r03 abt3)
+constexpr double kWsTotalShare = 0.6;
 
 struct GroupStat {
     int64_t nreads = 0, first_len = 0, sum = 0, maxlen = 0;
@@ -289,7 +291,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     }
     int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, (int64_t)ctx->n_cu * per_cu / team));
     while (teams > 1 && (size_t)(teams * team * a.slot_bytes) > budget) teams /= 2;
-    if (getenv("MANDO_PROF"))
+    if (getenv("MANDO_PROF") || getenv("MANDO_WS_LOG"))
         fprintf(stderr, "[mando prof] slot workspace %.1f MB, %lld slots, team %d, %d waves per CU (longest read %d, %d B of LDS) (free %.1f GB, budget %.1f GB)\n",
                 a.slot_bytes / 1e6, (long long)(teams * team), team, per_cu, (int)a.caps.QC, mando::poa_dyn_lds(a),
                 free_b / 1e9, budget / 1e9);

@@ -34,3 +34,7 @@ for w in config2 config5; do
   timeout -k 10 400 $B --workload $w > $D/bench_$w.json 2> $D/bench_$w.err || { echo "$w failed"; tail -5 $D/bench_$w.err; exit 1; }
   python3 -c "import json; d=json.load(open('$D/bench_$w.json')); print('$w', round(d['ms_per_step'], 1), d['config']['phases_rank0_s'], d['config'].get('full_output_equals_oracle'))"
 done
+if [ -n "$C4" ]; then
+  timeout -k 10 900 $B --workload config4 --steps 1 --warmup 1 > $D/bench_config4.json 2> $D/bench_config4.err || { echo "config4 failed"; tail -5 $D/bench_config4.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$D/bench_config4.json')); print('config4', d['value'], round(d['ms_per_step'], 1), d['config']['phases_rank0_s'])"
+fi
