@@ -171,6 +171,13 @@ struct mando_ctx {
 
 namespace {
 
+// one wave that waits `ticks` of the 100 MHz real-time counter (the stagger between POA launch kinds)
+constexpr int64_t kStaggerTicks = 5000;  // 50 us
+__global__ void stagger_kernel(int64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(10);
+}
+
 constexpr int kMaxWavesPerCu = 16;  // upper bound on resident POA waves per CU
 // groups whose band 2w + 1 (at their mean read length) is wider than this run in the wide-ring
 // launch: their rows mostly exceed one 128-column chunk (the band also drifts with the argmax)
@@ -186,6 +193,13 @@ constexpr double kWsShare = MANDO_WS_SHARE;
 // 0.45 was too tight: a config-3 chunk's narrow launch then got half the slots it needs for the
 // one-group grid (persistent grid, POA kernels +25 %, measured r03 abt3)
 constexpr double kWsTotalShare = 0.6;
+// MANDO_POA_WS_SHARE overrides it: the D driver sets 0.45 when it runs an input in many byte-capped chunks
+// (config 4 on one GPU), whose in-flight chunks' text and clustering scratch need the rest
+double ws_total_share() {
+    const char *ev = getenv("MANDO_POA_WS_SHARE");
+    const double v = ev ? atof(ev) : kWsTotalShare;
+    return v > 0.05 && v <= 0.95 ? v : kWsTotalShare;
+}
 
 struct GroupStat {
     int64_t nreads = 0, first_len = 0, sum = 0, maxlen = 0;
@@ -276,7 +290,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     HIP_TRY(hipMemGetInfo(&free_b, &total_b));
     const size_t budget = std::max<size_t>(
         (size_t)1 << 30, std::min<size_t>((size_t)(kWsShare * (double)free_b) + ws.bytes,
-                                          (size_t)(kWsTotalShare * (double)total_b)));
+                                          (size_t)(ws_total_share() * (double)total_b)));
     // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
@@ -727,6 +741,16 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
             const std::vector<int32_t> &L = lists[kind];
             if (L.empty()) continue;
             hipStream_t lst = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
+            // MANDO_POA_STAGGER=1 (experiment, off by default): the other kinds start once the first
+            // (heaviest) kind's kernel is about to dispatch (ctx->ev0 is recorded right before it) and
+            // a short delay has passed, so its few long groups take their CUs before the other grids'
+            // workgroups fill the chip (a probe for the intermittent slow wide launches)
+            static const bool stagger = getenv("MANDO_POA_STAGGER") && getenv("MANDO_POA_STAGGER")[0] == '1';
+            if (lane && stagger) {
+                HIP_TRY(hipStreamWaitEvent(lst, ctx->ev0, 0));
+                hipLaunchKernelGGL(stagger_kernel, dim3(1), dim3(64), 0, lst, kStaggerTicks);
+                HIP_TRY(hipGetLastError());
+            }
             int64_t mf = 0, ms = 0, ml = 0, mr = 0;
             for (int32_t g : L) {
                 mf = std::max(mf, gs[(size_t)g].first_len);

@@ -3316,6 +3316,8 @@ __device__ __forceinline__ void seeded_main(SharedState &sh, TeamBox *box, int m
 
 template <class SC, bool SEEDED, int RW>
 __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
+    constexpr int kPrioDp = 0;                             // DP rows (see the unseeded read loop)
+    constexpr int kPrioSerial = kPrioDp + kSerialPrio;     // descriptors, backtrack, update, consensus
     static_assert(RW == kChunk || (RW == kWideRing && !SEEDED), "wide rings: unseeded launches");
     __shared__ SharedState sh;
     const int lane = lane_id();
@@ -3485,13 +3487,15 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 // The serial, latency-bound phases (descriptors, backtrack, graph update, consensus) issue
                 // ahead of the co-resident waves' DP rows (s_setprio 1; the DP runs at 0): those waves
                 // return to their DP sooner, the SIMD's issue slots stay busy (config-3 kernel -3.5 %).
-                __builtin_amdgcn_s_setprio(kSerialPrio);
+                // (Running a wide launch's waves two levels higher changed neither the mean step nor
+                // the slow steps: 10-step lines interleaved twice, r03 prio1.)
+                __builtin_amdgcn_s_setprio(kPrioSerial);
                 uint64_t t0 = prof ? clock64() : 0;
                 const bool try16 = r16_eligible<SC, RW>(sc, qlen) && !(args_of(sh).dbg & 1);
                 build_desc(sh, n, lane, try16 ? kRing16 : kRing);
                 uint64_t t1 = prof ? clock64() : 0;
                 int bi = -1;
-                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_s_setprio(kPrioDp);
                 // 16-bit mode when the read's score range allows it; a read that leaves the safe
                 // range is re-aligned in 32-bit mode (the graph is untouched until update_graph)
                 st = try16 ? run_dp<SC, true, RW>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
@@ -3517,7 +3521,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 }
                 wave_sync();
                 uint64_t t3 = prof ? clock64() : 0;
-                __builtin_amdgcn_s_setprio(kSerialPrio);
+                __builtin_amdgcn_s_setprio(kPrioSerial);
                 st = backtrack<RW>(sh, bi, qlen, n, lane);
                 if (st != kStOk) break;
                 wave_sync();

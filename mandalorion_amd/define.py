@@ -360,6 +360,8 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         if k > 1:
             fracs = [(0.4 + i) / k for i in range(k)]
             n_chunks = k + 1
+            # the POA workspaces leave room for the chunks in flight (capi.hip ws_total_share)
+            os.environ.setdefault("MANDO_POA_WS_SHARE", "0.45")
         if n_chunks == 2 and os.environ.get("MANDO_CHUNK_FRACS"):  # cumulative byte fractions of the cuts
             fracs = [float(x) for x in os.environ["MANDO_CHUNK_FRACS"].split(",")]
             n_chunks = len(fracs) + 1

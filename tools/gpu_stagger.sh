@@ -1,5 +1,5 @@
-# GPU box: POA parity, then config-3 bench lines with and without the launch-kind stagger (10 steps each,
-# interleaved twice).
+# GPU box: POA parity, then config-3 bench lines with and without the launch-kind stagger
+# (MANDO_POA_STAGGER=1; 10 steps each, interleaved twice).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -7,4 +7,4 @@ D=gpurun_out/${1:-stag}
 mkdir -p $D
 timeout -k 10 600 python -u -m pytest tests/test_poa_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > $D/pytest.log 2>&1
 rc=$?; tail -1 $D/pytest.log; [ $rc -eq 0 ] || exit $rc
-STEPS=10 bash tools/gpu_ab_trees.sh ${1:-stag} "stag|.|" "nostag|.|MANDO_LIB=abl/nostag/libmando.so"
+STEPS=10 bash tools/gpu_ab_trees.sh ${1:-stag} "stag|.|MANDO_POA_STAGGER=1" "nostag|.|"
