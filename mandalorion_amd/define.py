@@ -263,6 +263,9 @@ def _fasta_bytes(aux, hs, hl, nl_pos, cons_src, cons_sel, cons_start, cons_len, 
 
 
 _CHUNK_BYTES = int(os.environ.get("MANDO_CHUNK_BYTES", str(8 << 30)))
+# inputs with at least this much locus text run in two chunks (or more, past _CHUNK_BYTES); 10,000
+# config-3 loci are 3.1 GB, 20,000 are 6.2 GB
+_TWO_CHUNK_BYTES = int(os.environ.get("MANDO_TWO_CHUNK_BYTES", str(4 << 30)))
 
 
 def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", splice_site_width: int = 1,
@@ -348,10 +351,14 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     if n_chunks <= 0 and os.environ.get("MANDO_CHUNKS"):
         n_chunks = int(os.environ["MANDO_CHUNKS"])
     if n_chunks <= 0:
-        # two chunks only when each still holds enough loci to fill the GPU's clustering and POA waves:
-        # with few, large loci (SIRV-like: 7 loci; config 5: 100) one chunk is faster (1.22 -> 0.81 s,
-        # 2.51 -> 2.43 s), since a chunk's kernels then run one wave per locus on an idle GPU
-        n_chunks = 1 if sizes.sum() < (64 << 20) or len(my_roots) < 1024 else 2
+        # two chunks only for large inputs.  Every POA launch lasts at least as long as its longest group
+        # on one wave (a 50-read, 5-6 kb locus: ~0.4 s), so a second chunk pays that floor again; it
+        # pays off only when the overlap of chunk 2's file reading and clustering with chunk 1's POA is
+        # worth more.  Measured per-step, config-3 data, one GPU (r03 share1 / share2): 2,500 loci 0.48 s
+        # in one chunk against 0.81 s in two, 5,000 0.58 / 0.88 s, 10,000 0.91 / 1.03 s, 20,000 1.80 /
+        # 1.69 s.  The per-rank share of a multi-GPU run is such a smaller input.  Few, large loci
+        # (SIRV-like: 7 loci; config 5: 100) also run in one chunk (1.22 -> 0.81 s, 2.51 -> 2.43 s).
+        n_chunks = 1 if sizes.sum() < (_TWO_CHUNK_BYTES) or len(my_roots) < 1024 else 2
         fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.3"))] if n_chunks == 2 else None
         # large inputs (config 4 on one GPU: ~60 GB of locus text): chunks of at most kChunkBytes, the
         # first 0.4 of one, so one chunk's text, clustering scratch and the POA workspaces fit in HBM
