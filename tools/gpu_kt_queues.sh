@@ -1,5 +1,5 @@
 # GPU box: kernel trace of the config-3 stage timeline (two D passes), kernels listed with their HW queue
-# and stream for the last pass.  usage: Q=4 ASYNC=1 bash tools/gpu_kt_queues.sh TAG
+# and stream for the last pass.  usage: Q=4 bash tools/gpu_kt_queues.sh TAG
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 D=gpurun_out/${1:-ktq}
