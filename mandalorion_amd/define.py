@@ -264,8 +264,12 @@ def _fasta_bytes(aux, hs, hl, nl_pos, cons_src, cons_sel, cons_start, cons_len, 
 
 _CHUNK_BYTES = int(os.environ.get("MANDO_CHUNK_BYTES", str(8 << 30)))
 # inputs with at least this much locus text run in two chunks (or more, past _CHUNK_BYTES); 10,000
-# config-3 loci are 3.1 GB, 20,000 are 6.2 GB
-_TWO_CHUNK_BYTES = int(os.environ.get("MANDO_TWO_CHUNK_BYTES", str(4 << 30)))
+# config-3 loci are 3.1 GB, 20,000 are 6.2 GB.  At 20,000 loci one chunk and two have the same mean step
+# (1.78 / 1.77 s over 24 steps each), but two chunks put chunk 2's clustering and orientation kernels
+# beside chunk 1's POA, and in about one step in four the wide POA launch then runs 3x slower (POA
+# kernels 1.61-1.67 s against 1.32 s); one chunk has no such step (1,245-1,251 ms in all 24), so inputs
+# below one byte-capped chunk run in one (r03 onechunk)
+_TWO_CHUNK_BYTES = int(os.environ.get("MANDO_TWO_CHUNK_BYTES", str(8 << 30)))
 
 
 def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", splice_site_width: int = 1,
