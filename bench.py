@@ -322,7 +322,8 @@ def main():
     wl = WORKLOADS[args.workload]
     n_loci = args.loci or wl["loci"]
     cores = host_cores()
-    threads = args.threads or max(2, min(16, cores["usable"]) // max(1, local_world))
+    # host threads per rank: the usable cores per GPU of this node (a rank drives one GPU), at most 16
+    threads = args.threads or max(2, min(16, cores["usable"] // max(1, local_world)))
     gen_threads = min(16, cores["usable"]) if rank == 0 else threads
     base = args.data_dir or os.environ.get("TMPDIR", "/tmp")
     data = os.path.join(base, f"mando_bench_{args.workload}_{n_loci}")

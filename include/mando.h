@@ -101,6 +101,18 @@ float mando_last_kernel_ms(mando_ctx *ctx);
 /* Number of kernel launches issued by the most recent batch call (the roofline divides by it). */
 int mando_last_kernel_launches(mando_ctx *ctx);
 
+/* Caps the POA workspaces of this ctx (every launch kind together) at `bytes` of HBM for the calls
+ * that follow; 0 restores the default policy (a share of the free HBM at launch time).  The D driver
+ * (defineIsoforms.py:130-166's per-locus Pool, here one call per chunk) sets it per call from its chunk
+ * plan: the locus text, clustering scratch and gathered reads of the chunks in flight are reserved
+ * first, so no free-memory query races with the clustering thread's allocations. */
+int mando_ctx_set_poa_budget(mando_ctx *ctx, int64_t bytes);
+/* The device's HBM and the bytes this ctx's POA workspaces hold now (either may be NULL). */
+int mando_ctx_memory(mando_ctx *ctx, int64_t *total_bytes, int64_t *poa_ws_bytes);
+/* Workspace slots and budget of the most recent batch's launches by kind [narrow, wide, -S] (0: that
+ * kind did not run); either array may be NULL, else holds 3 entries. */
+int mando_poa_last_slots(mando_ctx *ctx, int64_t *slots, int64_t *budgets);
+
 /* Read orientation (mappy map-ont strand / primary-hit replacement).  For each group the
  * reference sequence is the group's first read.  For every read r, n_hits[r] is the number of primary
  * hits (0 = unmapped; the reference then drops the read) and hit_strands[r*max_hits + h] (+1 / -1) the

@@ -28,6 +28,9 @@ EXPORTED = (
     "mando_ctx_set_priority",
     "mando_last_kernel_ms",
     "mando_last_kernel_launches",
+    "mando_ctx_set_poa_budget",
+    "mando_ctx_memory",
+    "mando_poa_last_slots",
     "mando_orient_batch",
     "mando_selftest",
     "mando_mt_permutation",
@@ -182,6 +185,9 @@ def load(path: str | None = None):
         lib.mando_last_kernel_ms.argtypes = [_P]
         lib.mando_last_kernel_ms.restype = ctypes.c_float
         lib.mando_last_kernel_launches.argtypes = [_P]
+        lib.mando_ctx_set_poa_budget.argtypes = [_P, _I64]
+        lib.mando_ctx_memory.argtypes = [_P, _P, _P]
+        lib.mando_poa_last_slots.argtypes = [_P, _P, _P]
         lib.mando_orient_batch.argtypes = [_P, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
         lib.mando_mt_permutation.argtypes = [ctypes.c_uint32, _P, _P, _I64, _P, _I64]
         lib.mando_cluster_default_params.argtypes = [_P]
@@ -299,6 +305,22 @@ class Context:
 
     def last_kernel_launches(self) -> int:
         return int(self.lib.mando_last_kernel_launches(self.handle))
+
+    def set_poa_budget(self, nbytes: int) -> None:
+        """Explicit cap on this ctx's POA workspaces (0: the library's default policy)."""
+        check(self.lib.mando_ctx_set_poa_budget(self.handle, int(nbytes)))
+
+    def memory(self) -> tuple[int, int]:
+        """(device HBM bytes, bytes held by this ctx's POA workspaces)."""
+        tot, ws = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(self.lib.mando_ctx_memory(self.handle, ctypes.byref(tot), ctypes.byref(ws)))
+        return tot.value, ws.value
+
+    def last_slots(self) -> tuple[list[int], list[int]]:
+        """Workspace slots and budgets of the last POA batch by kind (narrow, wide, -S)."""
+        s, b = (ctypes.c_int64 * 3)(), (ctypes.c_int64 * 3)()
+        check(self.lib.mando_poa_last_slots(self.handle, s, b))
+        return list(s), list(b)
 
     def selftest(self) -> int:
         bad = ctypes.c_int(-1)

@@ -135,6 +135,10 @@ struct mando_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_launches = 0;
     bool timed = false;
+    int64_t total_mem = 0;    // device HBM (hipDeviceProp_t::totalGlobalMem)
+    int64_t poa_budget = 0;   // mando_ctx_set_poa_budget: explicit cap on the POA workspaces (0: default policy)
+    int64_t last_slots[3] = {0, 0, 0};  // slots of the last batch's launches by kind (narrow, wide, seeded)
+    int64_t last_budget[3] = {0, 0, 0}; // the workspace budget each of them was sized with
     DevBuf ws, counter, prof, o_gidx;
     DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
     DevBuf o_hits, o_strand, o_status;
@@ -188,18 +192,12 @@ constexpr int64_t kWideBand = 112;
 // share of the free HBM the POA workspace may take (one slot per resident wave; deep, long groups
 // need ~100 MB per slot, so the share decides how many waves run)
 constexpr double kWsShare = MANDO_WS_SHARE;
-// ... and at most this share of the device's HBM: a many-chunk run (config 4 on one GPU, ~60 GB of locus
-// text) keeps two chunks' text, clustering scratch and orientation buffers next to the workspaces.
-// 0.45 was too tight: a config-3 chunk's narrow launch then got half the slots it needs for the
-// one-group grid (persistent grid, POA kernels +25 %, measured r03 abt3)
+// ... and at most this share of the device's HBM (the default policy, for callers that set no explicit
+// budget).  0.45 was too tight for a config-3 chunk's narrow launch: half the slots it needs for the
+// one-group grid (persistent grid, POA kernels +25 %, measured r03 abt3).  A many-chunk run (config 4 on
+// one GPU) keeps its in-flight chunks' text and clustering scratch next to the workspaces: the D driver
+// passes an explicit budget for it (mando_ctx_set_poa_budget).
 constexpr double kWsTotalShare = 0.6;
-// MANDO_POA_WS_SHARE overrides it: the D driver sets 0.45 when it runs an input in many byte-capped chunks
-// (config 4 on one GPU), whose in-flight chunks' text and clustering scratch need the rest
-double ws_total_share() {
-    const char *ev = getenv("MANDO_POA_WS_SHARE");
-    const double v = ev ? atof(ev) : kWsTotalShare;
-    return v > 0.05 && v <= 0.95 ? v : kWsTotalShare;
-}
 
 struct GroupStat {
     int64_t nreads = 0, first_len = 0, sum = 0, maxlen = 0;
@@ -244,7 +242,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
                  const int32_t *d_gorder, int64_t n_groups, uint8_t *d_cons,
                  const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
                  int32_t *d_status, int max_per_cu, const SeedPlan *sp = nullptr, bool ev_start = true,
-                 bool ev_end = true, int lane = 0) {
+                 bool ev_end = true, int lane = 0, int kind = 0) {
     // lane k > 0: the context's extra stream and workspace k - 1 (launches of other kinds alongside)
     hipStream_t stream = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
     DevBuf &ws = lane ? ctx->lane_ws[lane - 1] : ctx->ws;
@@ -285,12 +283,23 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.qlds = mando::poa_qlds_bytes(caps.QC);
     a.dbg = 0;
     if (const char *ev = getenv("MANDO_POA_DBG")) a.dbg = atoi(ev);
-    // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget
-    size_t free_b = 0, total_b = 0;
-    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    const size_t budget = std::max<size_t>(
-        (size_t)1 << 30, std::min<size_t>((size_t)(kWsShare * (double)free_b) + ws.bytes,
-                                          (size_t)(ws_total_share() * (double)total_b)));
+    // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget.  With an
+    // explicit budget (mando_ctx_set_poa_budget: the D driver's per-call plan, which knows the chunks in
+    // flight) the launch takes what the other lanes' workspaces leave of it -- no free-memory query, which
+    // would race with the clustering thread's allocations; otherwise a share of the free HBM.
+    size_t free_b = 0, total_b = (size_t)ctx->total_mem;
+    size_t budget;
+    if (ctx->poa_budget > 0) {
+        size_t others = 0;
+        for (DevBuf *b : {&ctx->ws, &ctx->lane_ws[0], &ctx->lane_ws[1]})
+            if (b != &ws) others += b->bytes;
+        const size_t cap = (size_t)ctx->poa_budget;
+        budget = std::max<size_t>((size_t)1 << 30, cap > others ? cap - others : 0);
+    } else {
+        HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+        budget = std::max<size_t>((size_t)1 << 30, std::min<size_t>((size_t)(kWsShare * (double)free_b) + ws.bytes,
+                                                                    (size_t)(kWsTotalShare * (double)total_b)));
+    }
     // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
@@ -318,6 +327,8 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     }
     if (rc) return rc;
     const int64_t slots = teams * team;
+    ctx->last_slots[kind] = slots;
+    ctx->last_budget[kind] = (int64_t)budget;
     a.team = team;
     a.boxes = nullptr;
     if (sp) {  // seeded launches run as teams (of one, when the groups fill the chip)
@@ -554,6 +565,7 @@ int mando_ctx_create(int device_ordinal, mando_ctx **out) {
     mando_ctx *c = new mando_ctx();
     c->device = device_ordinal;
     c->n_cu = prop.multiProcessorCount;
+    c->total_mem = (int64_t)prop.totalGlobalMem;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
@@ -598,6 +610,28 @@ float mando_last_kernel_ms(mando_ctx *ctx) {
 }
 
 int mando_last_kernel_launches(mando_ctx *ctx) { return ctx ? ctx->last_launches : 0; }
+
+int mando_ctx_set_poa_budget(mando_ctx *ctx, int64_t bytes) {
+    if (!ctx || bytes < 0) return fail(MANDO_E_ARG, "mando_ctx_set_poa_budget: bad argument");
+    ctx->poa_budget = bytes;
+    return MANDO_OK;
+}
+
+int mando_ctx_memory(mando_ctx *ctx, int64_t *total_bytes, int64_t *poa_ws_bytes) {
+    if (!ctx) return fail(MANDO_E_ARG, "null ctx");
+    if (total_bytes) *total_bytes = ctx->total_mem;
+    if (poa_ws_bytes) *poa_ws_bytes = (int64_t)(ctx->ws.bytes + ctx->lane_ws[0].bytes + ctx->lane_ws[1].bytes);
+    return MANDO_OK;
+}
+
+int mando_poa_last_slots(mando_ctx *ctx, int64_t *slots, int64_t *budgets) {
+    if (!ctx) return fail(MANDO_E_ARG, "null ctx");
+    for (int k = 0; k < 3; ++k) {
+        if (slots) slots[k] = ctx->last_slots[k];
+        if (budgets) budgets[k] = ctx->last_budget[k];
+    }
+    return MANDO_OK;
+}
 
 int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const uint8_t *d_seqs,
                            const int64_t *d_seq_off, const int64_t *d_grp_off, int64_t n_groups,
@@ -675,6 +709,9 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
         (rc = ctx->cells.ensure((size_t)n_groups * 8)) ||
         (rc = ctx->status.ensure((size_t)n_groups * 4)))
         return rc;
+    if (getenv("MANDO_WS_LOG"))
+        fprintf(stderr, "[mando ws] poa: groups %lld bases %.3f GB (seq buffer %.3f GB, consensus %.3f GB)\n",
+                (long long)n_groups, total / 1e9, ctx->seq.bytes / 1e9, ctx->cons.bytes / 1e9);
     std::vector<int64_t> goff((size_t)n_groups + 1);
     for (int64_t g = 0; g <= n_groups; ++g) goff[(size_t)g] = grp_off[g];
     if (total > 0) {
@@ -699,6 +736,7 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
     std::vector<int64_t> cells((size_t)n_groups);
     std::vector<int32_t> todo = order;
     ctx->last_launches = 0;
+    for (int k = 0; k < 3; ++k) ctx->last_slots[k] = ctx->last_budget[k] = 0;
     for (int attempt = 0; attempt < 4 && !todo.empty(); ++attempt) {
         // unseeded and seeded groups run as two launches of the two kernel instantiations
         // three kinds of launch: unseeded groups with bands of one chunk, unseeded groups whose band
@@ -769,7 +807,7 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                               ctx->cons.as<uint8_t>(), ctx->cons_off.as<int64_t>(),
                               ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
                               ctx->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &sp : nullptr, lane == 0,
-                              nk == 1, lane);
+                              nk == 1, lane, kind);
             if (rc) return rc;
             ctx->last_launches += 1;
             ++lane;
@@ -938,6 +976,9 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
     HIP_TRY(hipSetDevice(ctx->device));
     int rc;
     if ((rc = ctx->seq.ensure((size_t)std::max<int64_t>(total, 1) + 16)) != MANDO_OK) return rc;
+    if (getenv("MANDO_WS_LOG"))
+        fprintf(stderr, "[mando ws] orient: reads %lld bases %.3f GB (seq buffer %.3f GB)\n", (long long)n_reads,
+                total / 1e9, ctx->seq.bytes / 1e9);
     if ((rc = ctx->seq_off.ensure(sizeof(int64_t) * (size_t)(n_reads + 1))) != MANDO_OK) return rc;
     if ((rc = ctx->grp_off.ensure(sizeof(int64_t) * (size_t)(n_groups + 1))) != MANDO_OK) return rc;
     if ((rc = ctx->o_strand.ensure((size_t)std::max<int64_t>(n_reads, 1) * (size_t)max_hits)) != MANDO_OK) return rc;

@@ -45,53 +45,77 @@ namespace {
 // tools/stale_probe.hip): a reused pinned source (scenario A) and a reused pinned D2H target (G, the
 // K2 output path) gave no stale byte in 15 refills each; tests/test_cluster_gpu.py
 // test_repeated_calls_reuse_buffers stays the regression test.
+struct HostBuf {
+    char *p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;  // hipHostMalloc (else posix_memalign + THP: the fallback, or MANDO_TEXT_PAGEABLE=1)
+};
 struct PinnedPool {
+    // page-locked bytes the pool keeps between calls: the four largest buffers of a config-4 run
+    // (8 GiB chunks) fit, more is returned to the system
+    static constexpr size_t kKeepPinned = size_t(40) << 30;
     std::mutex mu;
-    std::vector<std::pair<char *, size_t>> free_list;
-    char *acquire(size_t need, size_t &cap) {
+    std::vector<HostBuf> free_list;
+    HostBuf acquire(size_t need) {
         {
             std::lock_guard<std::mutex> g(mu);
             size_t best = (size_t)-1;
             for (size_t i = 0; i < free_list.size(); ++i)
-                if (free_list[i].second >= need && (best == (size_t)-1 || free_list[i].second < free_list[best].second))
+                if (free_list[i].cap >= need && (best == (size_t)-1 || free_list[i].cap < free_list[best].cap))
                     best = i;
             if (best != (size_t)-1) {
-                auto e = free_list[best];
+                const HostBuf e = free_list[best];
                 free_list.erase(free_list.begin() + (ptrdiff_t)best);
-                cap = e.second;
-                return e.first;
+                return e;
             }
         }
         constexpr size_t kStep = size_t(256) << 20;
-        cap = (std::max<size_t>(need, 1) + kStep - 1) / kStep * kStep;
+        HostBuf b;
+        b.cap = (std::max<size_t>(need, 1) + kStep - 1) / kStep * kStep;
         void *p = nullptr;
         if (!pageable()) {
-            if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
-            return static_cast<char *>(p);
+            if (hipHostMalloc(&p, b.cap, hipHostMallocDefault) == hipSuccess) {
+                b.p = static_cast<char *>(p);
+                b.pinned = true;
+                return b;
+            }
+            (void)hipGetLastError();  // page-locking failed (host memory limits): a pageable buffer instead
+            p = nullptr;
         }
-        if (posix_memalign(&p, size_t(2) << 20, cap) != 0) return nullptr;
-        (void)madvise(p, cap, MADV_HUGEPAGE);
-        return static_cast<char *>(p);
+        if (posix_memalign(&p, size_t(2) << 20, b.cap) != 0) return HostBuf{};
+        (void)madvise(p, b.cap, MADV_HUGEPAGE);
+        b.p = static_cast<char *>(p);
+        return b;
     }
     static bool pageable() {
         static const bool v = getenv("MANDO_TEXT_PAGEABLE") && getenv("MANDO_TEXT_PAGEABLE")[0] == '1';
         return v;
     }
-    static void free_buf(char *p) {
-        if (pageable()) free(p);
-        else (void)hipHostFree(p);
+    static void free_buf(const HostBuf &b) {
+        if (b.pinned) (void)hipHostFree(b.p);
+        else free(b.p);
     }
-    void release(char *p, size_t cap) {
-        if (!p) return;
+    void release(const HostBuf &b) {
+        if (!b.p) return;
         std::lock_guard<std::mutex> g(mu);
-        free_list.push_back({p, cap});
-        // keep the four largest buffers: two chunks in flight, plus the previous call's two when their
-        // release (a background thread in the D driver) comes late -- a free() while the next call's
-        // chunks are being read would otherwise recur
-        while (free_list.size() > 4) {
+        free_list.push_back(b);
+        // keep the four largest buffers (two chunks in flight, plus the previous call's two when their
+        // release -- a background thread in the D driver -- comes late: a free() while the next call's
+        // chunks are being read would otherwise recur), and at most kKeepPinned page-locked bytes
+        auto pinned_bytes = [&] {
+            size_t t = 0;
+            for (const HostBuf &x : free_list) t += x.pinned ? x.cap : 0;
+            return t;
+        };
+        while (free_list.size() > 4 || pinned_bytes() > kKeepPinned) {
             auto it = std::min_element(free_list.begin(), free_list.end(),
-                                       [](const auto &a, const auto &b) { return a.second < b.second; });
-            free_buf(it->first);
+                                       [](const HostBuf &a, const HostBuf &b) { return a.cap < b.cap; });
+            if (free_list.size() <= 4) {  // over the pinned cap: drop the smallest page-locked one
+                it = free_list.end();
+                for (auto j = free_list.begin(); j != free_list.end(); ++j)
+                    if (j->pinned && (it == free_list.end() || j->cap < it->cap)) it = j;
+            }
+            free_buf(*it);
             free_list.erase(it);
         }
     }
@@ -106,7 +130,7 @@ PinnedPool &pool() {
 struct mando_cluster_result {
     // all locus files, in a buffer from the pool (returned to it on destruction)
     char *text_p = nullptr;
-    size_t text_cap = 0;
+    HostBuf text_buf;
     size_t text_len = 0;
     vector<int64_t> name_off, seq_off, rec_locus;
     vector<int32_t> name_len, seq_len;
@@ -121,7 +145,7 @@ struct mando_cluster_result {
     size_t d_cap = 0;
     ~mando_cluster_result() {
         mando::cl::release_text(ctx, d_text, d_cap);
-        pool().release(text_p, text_cap);
+        pool().release(text_buf);
     }
 };
 
@@ -194,8 +218,9 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     const double t_size = secs();
     for (int64_t i = 0; i < n_loci; ++i) foff[(size_t)i + 1] = foff[(size_t)i] + std::max<int64_t>(0, fsize[(size_t)i]);
     res->text_len = (size_t)foff[(size_t)n_loci];
-    res->text_p = pool().acquire(res->text_len + 64, res->text_cap);
-    if (!res->text_p) return mando::set_error(MANDO_E_NOMEM, "cluster: pinned host buffer");
+    res->text_buf = pool().acquire(res->text_len + 64);
+    res->text_p = res->text_buf.p;
+    if (!res->text_p) return mando::set_error(MANDO_E_NOMEM, "cluster: host text buffer");
     // device copy of the text, filled piecewise while later files are still being read
     hipStream_t stream = mando::ctx_stream(ctx);
     size_t d_cap = 0;

@@ -2763,6 +2763,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     const bool timing = getenv("MANDO_CL_TIME") != nullptr;
     const auto tk0 = std::chrono::steady_clock::now();
     int k1_runs = 0;
+    int64_t a_last = 0;
     for (int attempt = 0; attempt < 3; ++attempt) {
         ++k1_runs;
         int64_t a_tot = 0;
@@ -2772,6 +2773,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
             a_tot += al256(scratch_a_bytes(x.line_cap, x.op_cap, x.blk_cap));
         }
         CL_TRY(d_a.alloc((size_t)a_tot + 256));
+        a_last = a_tot;
         CL_TRY(hipMemcpyAsync(d_loci.p, L.data(), (size_t)nl * sizeof(Locus), hipMemcpyHostToDevice, s));
         G.scratch_a = d_a.as<uint8_t>();
         CL_TRY(launch_parse(G, nrun, n_work, s));
@@ -2848,6 +2850,9 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         CL_TRY(d_b.alloc((size_t)b_tot + 256));
         CL_TRY(d_o.alloc((size_t)o_tot + 256));
         CL_TRY(d_rec.alloc((size_t)(recs + 1) * 32));
+        if (getenv("MANDO_WS_LOG"))  // device bytes of one chunk's clustering (the D driver's HBM plan)
+            fprintf(stderr, "[mando ws] cluster: loci %lld text %.3f GB scratch a %.3f b %.3f out %.3f rec %.3f GB\n",
+                    (long long)nl, in.foff[nl] / 1e9, a_last / 1e9, b_tot / 1e9, o_tot / 1e9, (recs + 1) * 32 / 1e9);
         // loci not run by K2 must not be: mark them in the stats copy the kernel reads
         for (int64_t i = 0; i < nl; ++i)
             if (out.status[(size_t)i] != kOk && st[(size_t)i].status == kOk) st[(size_t)i].status = out.status[(size_t)i];

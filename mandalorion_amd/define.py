@@ -270,6 +270,52 @@ _CHUNK_BYTES = int(os.environ.get("MANDO_CHUNK_BYTES", str(8 << 30)))
 # kernels 1.61-1.67 s against 1.32 s); one chunk has no such step (1,245-1,251 ms in all 24), so inputs
 # below one byte-capped chunk run in one (r03 onechunk)
 _TWO_CHUNK_BYTES = int(os.environ.get("MANDO_TWO_CHUNK_BYTES", str(8 << 30)))
+# fewer loci than this always run in one chunk (a few large loci: SIRV-like, config 5)
+_MIN_LOCI_CHUNKED = 1024
+
+
+def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0) -> tuple[int, list | None]:
+    """(chunks, cumulative byte fractions of the cuts or None for equal chunks).  n_chunks > 0 (or
+    MANDO_CHUNKS) forces the count; a two-chunk plan cuts at MANDO_FIRST_CHUNK (0.3) of the bytes, or at
+    MANDO_CHUNK_FRACS (comma-separated cumulative fractions, any count)."""
+    fracs = None
+    if n_chunks <= 0 and os.environ.get("MANDO_CHUNKS"):
+        n_chunks = int(os.environ["MANDO_CHUNKS"])
+    if n_chunks <= 0:
+        if text_bytes < _TWO_CHUNK_BYTES or n_loci < _MIN_LOCI_CHUNKED:
+            n_chunks = 1
+        else:
+            k = -(-text_bytes // _CHUNK_BYTES)
+            if k > 1:
+                fracs = [(0.4 + i) / k for i in range(k)]
+                n_chunks = k + 1
+            else:
+                n_chunks = 2
+    if n_chunks == 2 and fracs is None:
+        if os.environ.get("MANDO_CHUNK_FRACS"):
+            fracs = [float(x) for x in os.environ["MANDO_CHUNK_FRACS"].split(",")]
+            n_chunks = len(fracs) + 1
+        else:
+            fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.3"))]
+    return max(1, min(n_chunks, max(1, n_loci))), fracs
+
+
+# HBM plan of one call (bytes per byte of a chunk's locus text, measured on config 3 / config 4 chunks with
+# MANDO_WS_LOG=1, DESIGN.md §6): the device text itself (pool buffers rounded to 256 MB: the chunks in
+# flight -- clustering k+1, POA k, writing k-1 -- plus one cached), the clustering scratch of the largest
+# chunk (K1 records, cs runs, K2 maps and outputs; one per call, reused) and the reads gathered for
+# orientation and for the POA (one copy each)
+_HBM_USABLE = 0.92
+_CLUSTER_SCRATCH_PER_TEXT = 1.5
+_GATHERED_PER_TEXT = 0.5
+
+
+def poa_budget(total_hbm: int, span_text: list) -> int:
+    """Bytes the POA workspaces may take in a call whose chunks hold span_text bytes of locus text."""
+    big = max(span_text) if span_text else 0
+    pool = min(len(span_text), 4) * (big + (256 << 20))
+    reserve = pool + int((_CLUSTER_SCRATCH_PER_TEXT + 2 * _GATHERED_PER_TEXT) * big) + (4 << 30)
+    return max(4 << 30, int(_HBM_USABLE * total_hbm) - reserve)
 
 
 def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", splice_site_width: int = 1,
@@ -344,39 +390,12 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     t1 = time.perf_counter()
     timeline = [("ingest", 0.0, t1 - t0)]
     # Chunked pipeline: clustering of chunk k+1 (host C++ threads, GIL released) overlaps orientation +
-    # POA of chunk k on the GPU.  Chunks are contiguous runs of sorted roots.  The POA kernel is
-    # persistent (one grid, LPT over the launch's groups), so every launch ends in a tail that only its
-    # largest groups occupy: few, large launches are best.  The default is two chunks, the first holding
-    # ~30 % of the bytes: its POA starts while the rest is still being clustered, and that POA plus the
-    # rest's clustering end at about the same time (measured: 1 chunk 3.70 s, 2 equal 3.97 s, 4 equal
-    # 3.83 s on config 3).
+    # POA of chunk k on the GPU.  Chunks are contiguous runs of sorted roots.  Every POA launch lasts at
+    # least as long as its longest group, so few, large launches are best: inputs below one byte-capped
+    # chunk (_TWO_CHUNK_BYTES of locus text) run in one chunk, larger ones (config 4 on one GPU: ~60 GB)
+    # in chunks of at most _CHUNK_BYTES, the first 0.4 of one, so that its POA starts early.
     sizes = np.array([root_size.get(r, 0) for r in my_roots], dtype=np.int64)
-    fracs = None
-    if n_chunks <= 0 and os.environ.get("MANDO_CHUNKS"):
-        n_chunks = int(os.environ["MANDO_CHUNKS"])
-    if n_chunks <= 0:
-        # two chunks only for large inputs.  Every POA launch lasts at least as long as its longest group
-        # on one wave (a 50-read, 5-6 kb locus: ~0.4 s), so a second chunk pays that floor again; it
-        # pays off only when the overlap of chunk 2's file reading and clustering with chunk 1's POA is
-        # worth more.  Measured per-step, config-3 data, one GPU (r03 share1 / share2): 2,500 loci 0.48 s
-        # in one chunk against 0.81 s in two, 5,000 0.58 / 0.88 s, 10,000 0.91 / 1.03 s, 20,000 1.80 /
-        # 1.69 s.  The per-rank share of a multi-GPU run is such a smaller input.  Few, large loci
-        # (SIRV-like: 7 loci; config 5: 100) also run in one chunk (1.22 -> 0.81 s, 2.51 -> 2.43 s).
-        n_chunks = 1 if sizes.sum() < (_TWO_CHUNK_BYTES) or len(my_roots) < 1024 else 2
-        fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.3"))] if n_chunks == 2 else None
-        # large inputs (config 4 on one GPU: ~60 GB of locus text): chunks of at most kChunkBytes, the
-        # first 0.4 of one, so one chunk's text, clustering scratch and the POA workspaces fit in HBM
-        # together
-        k = int(-(-int(sizes.sum()) // _CHUNK_BYTES)) if n_chunks == 2 else 1
-        if k > 1:
-            fracs = [(0.4 + i) / k for i in range(k)]
-            n_chunks = k + 1
-            # the POA workspaces leave room for the chunks in flight (capi.hip ws_total_share)
-            os.environ.setdefault("MANDO_POA_WS_SHARE", "0.45")
-        if n_chunks == 2 and os.environ.get("MANDO_CHUNK_FRACS"):  # cumulative byte fractions of the cuts
-            fracs = [float(x) for x in os.environ["MANDO_CHUNK_FRACS"].split(",")]
-            n_chunks = len(fracs) + 1
-    n_chunks = max(1, min(n_chunks, len(my_roots)))
+    n_chunks, fracs = _chunk_plan(int(sizes.sum()), len(my_roots), n_chunks)
     cuts = [0]
     if n_chunks > 1:
         cs = np.cumsum(sizes)
@@ -386,6 +405,14 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     cuts.append(len(my_roots))
     cuts = sorted(set(min(max(c, 0), len(my_roots)) for c in cuts))
     spans = [(cuts[k], cuts[k + 1]) for k in range(len(cuts) - 1) if cuts[k + 1] > cuts[k]] or [(0, 0)]
+    # the POA workspaces' HBM budget for this call, from the chunk plan (no free-memory query: the
+    # clustering thread allocates the next chunk's buffers while a POA launch sizes its workspace)
+    n_poa = int(os.environ.get("MANDO_POA_STREAMS", "1")) if len(spans) > 1 else 1
+    if dev_poa:
+        span_text = [int(sizes[lo:hi].sum()) for lo, hi in spans]
+        for k in range(n_poa):
+            pctx = _lib.context(device, 3 * k)
+            pctx.set_poa_budget(poa_budget(pctx.memory()[0], span_text) // n_poa)
 
     # with several chunks in flight, two cores stay with the GPU driver, assembly and compaction threads
     n_cpu = threads if threads > 0 else (os.cpu_count() or 1)
@@ -446,13 +473,19 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         tp = time.perf_counter()
         pl = _poa_chunk(res, mine[lo:hi], prep, run_poa, stats, lock)
         timeline.append(("poa", tp - t0, time.perf_counter() - t0))
+        if world > 1:
+            # several ranks: the chunk's results are gathered at the end, so its referenced bytes are
+            # copied out now and its buffers (locus text on host and device) go back to their pools --
+            # a many-chunk rank share holds only the chunks in flight
+            del prep
+            pl = _compact(pl)
+            res.close()
         return pl, res
 
-    # one POA host thread (one device context) by default: with two, a chunk whose predecessor's POA
-    # ran late went to the second context, whose workspace was then sized from the HBM the first one
-    # left free -- a quarter of the slots, the persistent grid, 2.9 s instead of 1.1 s (measured in 3 of
-    # 30 config-3 steps; none in 18 with one context)
-    n_poa = int(os.environ.get("MANDO_POA_STREAMS", "1")) if len(spans) > 1 else 1
+    # one POA host thread (one device context, n_poa above) by default: with two, a chunk whose
+    # predecessor's POA ran late went to the second context, whose workspace was then sized from the HBM
+    # the first one left free -- a quarter of the slots, the persistent grid, 2.9 s instead of 1.1 s
+    # (measured in 3 of 30 config-3 steps; none in 18 with one context)
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
             ThreadPoolExecutor(max_workers=1) as writer, \
             ThreadPoolExecutor(max_workers=n_poa) as gpu_poa:
@@ -567,6 +600,30 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         print("\t" + " ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in stats.items()
                                if not isinstance(v, list)))
     return stats
+
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (the POA roofline's peak, as in bench.py)
+
+
+def metrics(stats: dict, world: int = 1) -> dict:
+    """One run's metrics line (written next to Mando.log as JSON): throughput of the whole
+    D module and of the POA kernels, with the POA roofline inputs (algorithmic bytes = 1 B per DP cell +
+    each read + each consensus, over the launches' HIP-event time)."""
+    la = stats.get("poa_launches", [])
+    k_ms = sum(x["kernel_ms"] for x in la)
+    cells = sum(x["cells"] for x in la)
+    alg = sum(x["cells"] + x["read_bytes"] + x["cons_bytes"] for x in la)
+    t = stats.get("t_total", 0.0)
+    gbs = alg / (k_ms / 1e3) / 1e9 if k_ms > 0 else None
+    return {"module": "D", "ranks": world, "loci": stats.get("loci"), "records_rank0": stats.get("records"),
+            "isoforms_rank0": stats.get("isoforms"), "poa_groups_rank0": stats.get("poa_groups"),
+            "poa_reads_rank0": stats.get("poa_reads"), "wall_s": round(t, 4),
+            "records_per_s_rank0": stats["records"] / t if t > 0 and stats.get("records") else None,
+            "poa_launches": sum(x["launches"] for x in la), "poa_kernel_ms": round(k_ms, 2), "dp_cells": cells,
+            "gcups": cells / (k_ms / 1e3) / 1e9 if k_ms > 0 else None,
+            "poa_algorithmic_GBps": gbs, "poa_hbm_roofline_frac": gbs / HBM_PEAK_GBS if gbs else None,
+            "phases_s": {k: round(stats[k], 4) for k in ("t_ingest", "t_cluster", "t_orient", "t_assemble", "t_poa")
+                         if k in stats}, "chunks": stats.get("chunks")}
 
 
 def _close_all(cluster_futs, poa_futs) -> None:

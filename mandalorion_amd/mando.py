@@ -188,7 +188,7 @@ def _run_modules(a, path: str, temp_path: str, fasta_list: list, comm, rank: int
         from . import define
 
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        define.define_isoforms(temp_path, cutoff=0.1, genome_file=a.genome_annotation,
+        st = define.define_isoforms(temp_path, cutoff=0.1, genome_file=a.genome_annotation,
                                splice_site_width=int(a.splice_site_window),
                                minimum_read_count=int(a.minimum_feature_count),
                                white_list_polyA=a.white_list_polyA.split(","), threads=int(a.minimap2_threads),
@@ -197,9 +197,14 @@ def _run_modules(a, path: str, temp_path: str, fasta_list: list, comm, rank: int
                                verbose=True)
         if rank == 0:
             # Mando.py:400: the read -> isoform table is also kept next to the outputs
+            import json
             import shutil
 
             shutil.copy(temp_path + "/reads2isoforms.txt", path + "Mando_isoforms.read_stat.txt")
+            # this build's metrics line next to Mando.log (one JSON object per run)
+            with open(path + "/Mando.metrics.jsonl", "a") as fh:
+                fh.write(json.dumps(dict(define.metrics(st, comm.world if comm is not None else 1),
+                                         time=strftime("%Y-%m-%d %H:%M:%S", localtime()))) + "\n")
     return 0
 
 

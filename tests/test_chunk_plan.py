@@ -1,0 +1,77 @@
+"""The D driver's chunk plan and HBM budget (host logic, no GPU): defineIsoforms.py:130-166's per-locus
+Pool becomes a few pipelined chunks; the POA workspace budget of a call is derived from its plan
+(mando_ctx_set_poa_budget), never from process-global state."""
+from __future__ import annotations
+
+import os
+
+import pytest
+
+from mandalorion_amd import define
+
+GB = 1 << 30
+
+
+@pytest.fixture(autouse=True)
+def _clean_env(monkeypatch):
+    for k in ("MANDO_CHUNKS", "MANDO_FIRST_CHUNK", "MANDO_CHUNK_FRACS"):
+        monkeypatch.delenv(k, raising=False)
+
+
+def test_small_inputs_run_in_one_chunk():
+    assert define._chunk_plan(6 * GB, 20000) == (1, None)      # config 3: 6.2 GB of locus text
+    assert define._chunk_plan(100 * GB, 7) == (1, None)        # few large loci (SIRV-like)
+
+
+def test_byte_capped_chunks():
+    n, fr = define._chunk_plan(20 * GB, 60000)
+    k = -(-20 * GB // define._CHUNK_BYTES)
+    assert n == k + 1 and fr == pytest.approx([(0.4 + i) / k for i in range(k)])
+    assert fr[0] * 20 * GB < define._CHUNK_BYTES                # the first chunk is the smallest
+
+
+def test_two_chunks_take_the_first_chunk_fraction(monkeypatch):
+    assert define._chunk_plan(GB, 100, n_chunks=2) == (2, [0.3])
+    monkeypatch.setenv("MANDO_FIRST_CHUNK", "0.5")
+    assert define._chunk_plan(GB, 100, n_chunks=2) == (2, [0.5])
+    monkeypatch.setenv("MANDO_CHUNKS", "2")
+    assert define._chunk_plan(GB, 100) == (2, [0.5])
+    monkeypatch.setenv("MANDO_CHUNK_FRACS", "0.2,0.6")
+    assert define._chunk_plan(GB, 100) == (3, [0.2, 0.6])
+    assert define._chunk_plan(GB, 100, n_chunks=3) == (3, None)  # forced counts other than 2: equal chunks
+
+
+def test_chunk_count_never_exceeds_loci():
+    assert define._chunk_plan(GB, 2, n_chunks=5) == (2, None)
+
+
+def test_poa_budget_reserves_the_chunks_in_flight():
+    total = 288 * 10**9
+    one = define.poa_budget(total, [6 * GB])
+    many = define.poa_budget(total, [3 * GB] + [8 * GB] * 7)
+    assert 4 * GB <= many < one < define._HBM_USABLE * total
+    # four pool buffers of the largest chunk, its clustering scratch and gathered reads, 4 GiB of margin
+    big = 8 * GB
+    want = int(define._HBM_USABLE * total) - 4 * (big + (256 << 20)) - int(
+        (define._CLUSTER_SCRATCH_PER_TEXT + 2 * define._GATHERED_PER_TEXT) * big) - 4 * GB
+    assert many == want
+    assert define.poa_budget(16 * GB, [8 * GB] * 4) == 4 * GB  # never below the floor
+
+
+def test_no_process_environment_side_effects():
+    before = dict(os.environ)
+    define._chunk_plan(80 * GB, 200000)
+    define.poa_budget(288 * 10**9, [8 * GB] * 10)
+    assert dict(os.environ) == before
+
+
+def test_metrics_line():
+    st = {"loci": 10, "records": 500, "isoforms": 12, "poa_groups": 11, "poa_reads": 400, "t_total": 2.0,
+          "t_cluster": 0.5, "chunks": 1,
+          "poa_launches": [{"cells": 8 * 10**9, "read_bytes": 10**6, "cons_bytes": 10**4, "kernel_ms": 1000.0,
+                            "launches": 2, "reads": 400}]}
+    m = define.metrics(st)
+    assert m["records_per_s_rank0"] == 250 and m["gcups"] == pytest.approx(8.0)
+    assert m["poa_algorithmic_GBps"] == pytest.approx((8 * 10**9 + 10**6 + 10**4) / 1e9)
+    assert m["poa_hbm_roofline_frac"] == pytest.approx(m["poa_algorithmic_GBps"] / 8000.0)
+    assert define.metrics({"t_total": 1.0, "records": 0})["gcups"] is None

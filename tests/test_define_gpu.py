@@ -58,3 +58,36 @@ def test_define_gpu_chunked_pipeline(gpu_ctx, tmp_path):
     st = _run(d, info["gtf"], n_chunks=3)
     assert st["chunks"] == 3 and len(st["poa_launches"]) == 3
     assert (read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")) == one
+
+
+@pytest.mark.gpu
+def test_define_gpu_byte_capped_chunks_then_one_chunk(gpu_ctx, tmp_path, monkeypatch):
+    """The byte-capped many-chunk branch (config 4's plan, thresholds lowered to this small input), then a
+    one-chunk call in the same process: same files each time, and the one-chunk call's POA workspaces are
+    sized exactly as before the many-chunk call (its budget comes from its own plan; nothing of the
+    many-chunk plan survives in the process)."""
+    from mandalorion_amd import _lib
+
+    d = str(tmp_path)
+    loci = simdata.make_dataset(simdata.fixture_specs())
+    info = simdata.write_dataset(loci, d)
+    read = lambda f: open(os.path.join(d, f), "rb").read()
+    pctx = _lib.context(0, 0)
+    env0 = dict(os.environ)
+    _run(d, info["gtf"])
+    one = read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")
+    slots1 = pctx.last_slots()
+    text = sum(os.path.getsize(os.path.join(d, "tmp_SS", f)) for f in os.listdir(os.path.join(d, "tmp_SS")))
+    with monkeypatch.context() as m:
+        m.setattr(define, "_TWO_CHUNK_BYTES", 1)
+        m.setattr(define, "_MIN_LOCI_CHUNKED", 1)
+        m.setattr(define, "_CHUNK_BYTES", text // 3 + 1)
+        st = _run(d, info["gtf"])
+        assert st["chunks"] >= 4 and len(st["poa_launches"]) >= 3
+        assert (read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")) == one
+        # the many-chunk call's launches were sized from its own (smaller) budget
+        assert sum(pctx.last_slots()[1]) <= sum(slots1[1])
+    assert dict(os.environ) == env0
+    _run(d, info["gtf"])
+    assert (read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")) == one
+    assert pctx.last_slots() == slots1

@@ -57,6 +57,11 @@ def _check(p):
     assert os.path.exists(os.path.join(tmp, "polyAWhiteList.bed"))
     headers = [l[1:].rstrip("\n") for l in open(os.path.join(tmp, "Isoform_Consensi.fasta")) if l.startswith(">")]
     assert headers == ref["isoform_headers"]
+    # the metrics line next to Mando.log: one JSON object per run
+    m = json.loads(open(os.path.join(p, "Mando.metrics.jsonl")).read().splitlines()[-1])
+    assert (m["module"], m["ranks"], m["records_rank0"]) == ("D", 1, C1["inputs"]["records"])
+    assert m["isoforms_rank0"] == len(ref["isoform_headers"]) and m["wall_s"] > 0
+    return m
 
 
 def test_mando_cli_module_d_config1_with_oracle(tmp_path, monkeypatch):
@@ -103,4 +108,5 @@ def test_mando_cli_module_d_config1_gpu(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "Mando.py"), "-M", "D", "-p", p, "--seed", str(GOLD["seed"])],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    _check(p)
+    m = _check(p)
+    assert m["poa_kernel_ms"] > 0 and m["dp_cells"] > 0 and 0 < m["poa_hbm_roofline_frac"] < 1
