@@ -49,6 +49,7 @@ class ClusterResult:
         self._lib = _lib.load()
         self._h = handle
         self._free = free or self._lib.mando_cluster_free
+        self.on_close = None  # called once, when the result's buffers are released
         v = _lib.ClusterView()
         _lib.check((view_get or self._lib.mando_cluster_view_get)(handle, ctypes.byref(v)))
         self.n_loci = v.n_loci
@@ -91,6 +92,9 @@ class ClusterResult:
             self._free(self._h)
             self._h = None
             self.text = np.zeros(0, dtype=np.uint8)
+            cb, self.on_close = self.on_close, None
+            if cb is not None:
+                cb()
 
     def __del__(self):
         try:

@@ -175,6 +175,9 @@ struct mando_ctx {
 
 namespace {
 
+// the workspace of a POA launch kind (0 narrow, 1 wide, 2 -S)
+DevBuf &kind_ws(mando_ctx *ctx, int kind) { return kind == 0 ? ctx->ws : ctx->lane_ws[kind - 1]; }
+
 // one wave that waits `ticks` of the 100 MHz real-time counter (the stagger between POA launch kinds)
 constexpr int64_t kStaggerTicks = 5000;  // 50 us
 __global__ void stagger_kernel(int64_t ticks) {
@@ -234,6 +237,37 @@ struct SeedPlan {
     int32_t pc = 0, k = 0;
 };
 
+// waves per workgroup of wide launches: 2 (two-chunk rows split over two waves, poa_kernel.hip
+// row16w_half) with MANDO_POA_W2=1; one wave per group by default
+int poa_wide_waves() {
+    const char *ev = getenv("MANDO_POA_W2");
+    return ev && ev[0] == '1' ? 2 : 1;
+}
+
+// The workspace bytes a launch kind wants: one slot per resident workgroup (a team of them per -S
+// group when the groups are few), at most one per group -- what its one-group grid needs.
+size_t kind_want(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps &caps, int64_t n_groups, bool seeded,
+                 int max_per_cu) {
+    mando::PoaKArgs a{};
+    a.caps = caps;
+    a.qlds = mando::poa_qlds_bytes(caps.QC);
+    a.nw = caps.wide && !seeded ? poa_wide_waves() : 1;
+    a.match = p.match;
+    a.mismatch = p.mismatch;
+    a.o1 = p.gap_open1;
+    a.e1 = p.gap_ext1;
+    a.o2 = p.gap_open2;
+    a.e2 = p.gap_ext2;
+    int cap = max_per_cu;
+    if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
+    const int per_cu = mando::poa_blocks_per_cu(a, cap);
+    const int64_t resident = (int64_t)ctx->n_cu * per_cu;
+    int64_t team = 1;
+    if (seeded) team = std::max<int64_t>(1, std::min<int64_t>(mando::kMaxTeam, resident / std::max<int64_t>(1, n_groups)));
+    const int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, resident / team));
+    return (size_t)(teams * team) * (size_t)mando::make_layout(caps).total;
+}
+
 // One POA launch over n_groups groups (d_gorder: their indices).  sp != null: the groups are -S
 // groups (the seeded kernel instantiation).  ev_start / ev_end: record the ctx's timing events around
 // this launch (a batch of several launches times from the first start to the last end).
@@ -242,10 +276,11 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
                  const int32_t *d_gorder, int64_t n_groups, uint8_t *d_cons,
                  const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
                  int32_t *d_status, int max_per_cu, const SeedPlan *sp = nullptr, bool ev_start = true,
-                 bool ev_end = true, int lane = 0, int kind = 0) {
-    // lane k > 0: the context's extra stream and workspace k - 1 (launches of other kinds alongside)
+                 bool ev_end = true, int lane = 0, int kind = 0, size_t granted = 0) {
+    // lane k > 0: the context's extra stream k - 1 (launches of other kinds alongside); the workspace
+    // belongs to the launch kind (kind_ws), so a kind keeps its workspace from batch to batch
     hipStream_t stream = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
-    DevBuf &ws = lane ? ctx->lane_ws[lane - 1] : ctx->ws;
+    DevBuf &ws = kind_ws(ctx, kind);
     DevBuf &counter = lane ? ctx->lane_counter[lane - 1] : ctx->counter;
     DevBuf &profb = lane ? ctx->lane_prof[lane - 1] : ctx->prof;
     DevBuf &boxb = lane ? ctx->lane_boxes[lane - 1] : ctx->boxes;
@@ -283,18 +318,17 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.qlds = mando::poa_qlds_bytes(caps.QC);
     a.dbg = 0;
     if (const char *ev = getenv("MANDO_POA_DBG")) a.dbg = atoi(ev);
+    // wide launches: two-wave workgroups (the two-chunk rows split over both waves, poa_kernel.hip
+    // row16w_half) with MANDO_POA_W2=1; one wave per group by default
+    a.nw = caps.wide && !sp ? poa_wide_waves() : 1;
     // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget.  With an
     // explicit budget (mando_ctx_set_poa_budget: the D driver's per-call plan, which knows the chunks in
     // flight) the launch takes what the other lanes' workspaces leave of it -- no free-memory query, which
     // would race with the clustering thread's allocations; otherwise a share of the free HBM.
     size_t free_b = 0, total_b = (size_t)ctx->total_mem;
     size_t budget;
-    if (ctx->poa_budget > 0) {
-        size_t others = 0;
-        for (DevBuf *b : {&ctx->ws, &ctx->lane_ws[0], &ctx->lane_ws[1]})
-            if (b != &ws) others += b->bytes;
-        const size_t cap = (size_t)ctx->poa_budget;
-        budget = std::max<size_t>((size_t)1 << 30, cap > others ? cap - others : 0);
+    if (granted > 0) {
+        budget = granted;  // this kind's share of the explicit budget (poa_batch_impl grant_budgets)
     } else {
         HIP_TRY(hipMemGetInfo(&free_b, &total_b));
         budget = std::max<size_t>((size_t)1 << 30, std::min<size_t>((size_t)(kWsShare * (double)free_b) + ws.bytes,
@@ -313,7 +347,12 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         if (const char *ev = getenv("MANDO_TEAM")) team = std::max(1, std::min(mando::kMaxTeam, atoi(ev)));
     }
     int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, (int64_t)ctx->n_cu * per_cu / team));
-    while (teams > 1 && (size_t)(teams * team * a.slot_bytes) > budget) teams /= 2;
+    if (granted > 0) {
+        teams = std::max<int64_t>(1, std::min<int64_t>(teams, (int64_t)(budget / ((size_t)team * a.slot_bytes))));
+        if (ws.bytes > (size_t)(teams * team * a.slot_bytes) + (budget >> 3)) ws.release();  // give back the rest
+    } else {
+        while (teams > 1 && (size_t)(teams * team * a.slot_bytes) > budget) teams /= 2;
+    }
     if (getenv("MANDO_PROF") || getenv("MANDO_WS_LOG"))
         fprintf(stderr, "[mando prof] slot workspace %.1f MB, %lld slots, team %d, %d waves per CU (longest read %d, %d B of LDS) (free %.1f GB, budget %.1f GB)\n",
                 a.slot_bytes / 1e6, (long long)(teams * team), team, per_cu, (int)a.caps.QC, mando::poa_dyn_lds(a),
@@ -773,6 +812,47 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                 kcost[kind] = std::max(kcost[kind], (double)(q.sum - q.first_len) * (double)q.first_len);
             }
         std::stable_sort(korder, korder + 3, [&](int x, int y) { return kcost[x] > kcost[y]; });
+        mando::PoaCaps kcaps[3];
+        for (int kind = 0; kind < 3; ++kind) {
+            int64_t mf = 0, ms = 0, ml = 0, mr = 0;
+            for (int32_t g : lists[kind]) {
+                mf = std::max(mf, gs[(size_t)g].first_len);
+                ms = std::max(ms, gs[(size_t)g].sum);
+                ml = std::max(ml, gs[(size_t)g].maxlen);
+                mr = std::max(mr, gs[(size_t)g].nreads);
+            }
+            kcaps[kind] = plan_caps(*params, mf, ms, ml, mr, attempt);
+            kcaps[kind].seeded = kind == 2;
+            kcaps[kind].wide = kind == 1;
+        }
+        // an explicit budget (mando_ctx_set_poa_budget) is shared by the batch's kinds: each kind wants the
+        // workspace of its resident waves (one-group grids need that many slots); every kind first gets
+        // up to an eighth of the budget, then the rest goes to the kinds in launch order (heaviest group
+        // first) up to what they want.  Workspaces of kinds absent from the batch, and the excess of
+        // larger ones, are released before any launch.
+        size_t grant[3] = {0, 0, 0};
+        if (ctx->poa_budget > 0) {
+            const size_t B = (size_t)ctx->poa_budget;
+            size_t want[3] = {0, 0, 0}, rem = B;
+            for (int kind = 0; kind < 3; ++kind)
+                if (!lists[kind].empty())
+                    want[kind] = kind_want(ctx, *params, kcaps[kind], (int64_t)lists[kind].size(), kind == 2,
+                                           kMaxWavesPerCu);
+            for (int kind = 0; kind < 3; ++kind) {
+                grant[kind] = std::min(want[kind], B / 8);
+                rem -= std::min(rem, grant[kind]);
+            }
+            for (int ki = 0; ki < 3; ++ki) {
+                const int kind = korder[ki];
+                const size_t more = std::min(rem, want[kind] - grant[kind]);
+                grant[kind] += more;
+                rem -= more;
+            }
+            for (int kind = 0; kind < 3; ++kind) {
+                DevBuf &w = kind_ws(ctx, kind);
+                if (lists[kind].empty() || w.bytes > grant[kind]) w.release();
+            }
+        }
         int lane = 0;
         for (int ki = 0; ki < 3; ++ki) {
             const int kind = korder[ki];
@@ -789,16 +869,7 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                 hipLaunchKernelGGL(stagger_kernel, dim3(1), dim3(64), 0, lst, kStaggerTicks);
                 HIP_TRY(hipGetLastError());
             }
-            int64_t mf = 0, ms = 0, ml = 0, mr = 0;
-            for (int32_t g : L) {
-                mf = std::max(mf, gs[(size_t)g].first_len);
-                ms = std::max(ms, gs[(size_t)g].sum);
-                ml = std::max(ml, gs[(size_t)g].maxlen);
-                mr = std::max(mr, gs[(size_t)g].nreads);
-            }
-            mando::PoaCaps caps = plan_caps(*params, mf, ms, ml, mr, attempt);
-            caps.seeded = kind == 2;
-            caps.wide = kind == 1;
+            const mando::PoaCaps &caps = kcaps[kind];
             DevBuf &gb = kind == 0 ? ctx->gorder : (kind == 1 ? ctx->gorder_w : ctx->gorder2);
             if ((rc = gb.ensure(L.size() * 4))) return rc;
             HIP_TRY(hipMemcpyAsync(gb.p, L.data(), L.size() * 4, hipMemcpyHostToDevice, lst));
@@ -807,7 +878,7 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                               ctx->cons.as<uint8_t>(), ctx->cons_off.as<int64_t>(),
                               ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
                               ctx->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &sp : nullptr, lane == 0,
-                              nk == 1, lane, kind);
+                              nk == 1, lane, kind, grant[kind]);
             if (rc) return rc;
             ctx->last_launches += 1;
             ++lane;

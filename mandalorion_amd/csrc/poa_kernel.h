@@ -159,7 +159,10 @@ struct PoaRunArgs {
 };
 struct PoaKArgs : PoaRunArgs {
     SlotLayout lay;
+    int32_t nw = 1;  // waves per workgroup: 2 runs a wide launch's two-chunk rows over two waves
 };
+// waves per workgroup of a launch (two-wave workgroups for wide launches only)
+inline int poa_waves(const PoaKArgs &a) { return a.caps.wide && !a.caps.seeded && a.nw == 2 ? 2 : 1; }
 
 // A team's mailbox (see poa_kernel.hip, "-S teams").  claim = job << 40 | np << 20 | next window.
 struct alignas(64) TeamBox {

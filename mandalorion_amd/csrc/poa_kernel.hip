@@ -150,8 +150,17 @@ __device__ __forceinline__ int out_cap(const PoaRunArgs &a, int v) {
     return v == kSrc ? a.caps.BIGCAP : a.caps.DCAP;
 }
 
-// wave-level barrier that also orders this wave's global/LDS memory traffic
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }
+// wave-level barrier that also orders this wave's global/LDS memory traffic.  Wave-local (no s_barrier):
+// in a two-wave workgroup (wide launches, below) the serial phases run on wave 0 alone while wave 1 waits
+// for DP rows; a one-wave workgroup's __syncthreads() compiles to exactly this (the backend drops the
+// s_barrier of a single-wave workgroup).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// workgroup barrier of a two-wave workgroup (its waves' LDS and global writes ordered across it)
+__device__ __forceinline__ void group_barrier() { __syncthreads(); }
 
 // same-wave RAW through HBM (spilled rows, far row records): drain this wave's stores first
 __device__ __forceinline__ void hbm_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
@@ -1795,13 +1804,297 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
     return besti;
 }
 
+// ---- wide rows over two waves (wide launches with two-wave workgroups, PoaKArgs::nw == 2) ----------
+// A group of long reads runs on one wave for its whole life, so a launch lasts at least its longest
+// group's one-wave latency (config 5's 8.5 kb groups, config 3's 5-6 kb ones, the per-rank floor of the
+// multi-GPU split).  In a two-wave workgroup wave 0 runs the group as before (descriptors, one-chunk rows,
+// backtrack, graph update, consensus) and wave 1 takes the upper 128-column half of every two-chunk fast
+// row: wave 0 posts the row's control (band, predecessors, allocation) in LDS and both waves pass a
+// workgroup barrier (B0); each computes its half up to the F prefix scan and its half's argmax key, the
+// two exchange the lower half's F total (the upper half's carry-in) and the keys through LDS (barrier BX),
+// and each finishes its half: traceback bytes, predecessor bytes, ring and spill columns.  The next row's
+// B0 orders the ring halves for both waves' predecessor reads.  A one-chunk or generic row after a split
+// row first passes a B0 with a no-op command (wave 0 then reads ring columns wave 1 wrote).  Per split row
+// each wave issues one half's VALU work instead of both halves' (row16w_vec), at the cost of two barriers.
+// The argmax comes from H0 (before F) in both waves: F only carries values from the left minus gap
+// penalties, so it never reaches the row maximum and the leftmost argmax cell of H is that of H0.
+constexpr int kW2Row = 1, kW2Nop = 2, kW2End = 3, kW2Exit = 4;
+struct W2Cmd {
+    int op, r, beg, end, cb0, tbw, vb, pn, b0, e0, b1, e1, p0slot, p1slot, two, far, multi, pn3;
+    int tb_used, kp_used, sv_used, pad0, pad1, pad2;
+};
+static_assert(sizeof(W2Cmd) == 96, "the command is read as six int4");
+struct W2Lds {
+    W2Cmd cmd;
+    int carry, am0, am1, flag;
+};
+__device__ __forceinline__ W2Lds &w2lds() {
+    __shared__ W2Lds v;
+    return v;
+}
+
+// wave 0: publish a split row's control (and the allocation counters of this read) for wave 1
+__device__ __forceinline__ void w2_post_row(const Row16 &R, const DpState &ds, int lane) {
+    W2Lds &X = w2lds();
+    if (lane == 0) {
+        int4 *c = reinterpret_cast<int4 *>(&X.cmd);
+        c[0] = make_int4(kW2Row, R.r, R.beg, R.end);
+        c[1] = make_int4(R.cb0, R.tbw, R.vb, R.pn);
+        c[2] = make_int4(R.b0, R.e0, R.b1, R.e1);
+        c[3] = make_int4(R.p0slot, R.p1slot, R.two, R.far);
+        c[4] = make_int4(R.multi, R.pn3, ds.tb_used, ds.kp_used);
+        c[5] = make_int4(ds.sv_used, 0, 0, 0);
+    }
+}
+__device__ __forceinline__ void w2_post_op(int op, int lane) {
+    if (lane == 0) w2lds().cmd.op = op;
+}
+
+// One half (h: 0 lower, 1 upper; wave-uniform) of a two-chunk fast row, computed by wave h of a two-wave
+// workgroup; the same cells, bytes and ring values as row16w_vec's half h.  Returns the row's argmax.
+template <class SC>
+__device__ __forceinline__ int row16w_half(const SC &sc, gu8 *tb, gu8 *kp, gint *sv, gint *rinfo, SharedState &sh,
+                                           int lane, const Row16 &R, DpState &ds, int h) {
+    constexpr int RW = kWideRing, HW = RW / 2;
+    W2Lds &X = w2lds();
+    const int e1 = sc.e1, e2 = sc.e2, oe1 = sc.o1 + sc.e1, oe2 = sc.o2 + sc.e2;
+    const int beg = R.beg, end = R.end, cb0 = R.cb0;
+    const int tbbase = ds.tb_used - cb0;
+    const int ks = kp_stride(R.pn);
+    const int kpbase = ds.kp_used - ks * cb0;
+    const int soff = R.far ? ds.sv_used : -1;
+    const int svbase = ds.sv_used - cb0;
+    const uint32_t *w0 = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, R.p0slot));
+    const uint32_t *w1 = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, R.p1slot));
+    const uint32_t tlo =
+        R.vb < 4 ? (uint32_t)(sc.match + sc.mismatch) << (8 * R.vb) : (uint32_t)sc.mismatch * 0x01010101u;
+    const uint32_t B0 = pk2s(R.b0), E0 = pk2s(R.e0), B1 = pk2s(R.b1), E1b = pk2s(R.e1);
+    const uint32_t BEG = pk2s(beg), END = pk2s(end);
+    const int c0 = kChunk * h + 2 * lane;  // the lane's first column, relative to cb0
+    const int j0 = cb0 + c0;
+    const uint32_t J = (uint32_t)j0 * 0x10001u + 0x10000u;  // (j0, j0 + 1)
+    const uint32_t LJ = (uint32_t)c0 * 0x10001u + 0x10000u;  // the same - cb0
+    const uint32_t inv = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(BEG)) | as_u32(as_s16x2(END) - as_s16x2(J)));
+    const uint32_t qbyte = qnib<RW>()[j0 >> 1];
+    const uint32_t sel = ((qbyte * 0x1001u) & 0x000F000Fu) | 0x0C000C00u;
+    const uint32_t S = __builtin_amdgcn_perm((uint32_t)sc.mismatch, tlo, sel);
+    const int iw = (j0 >> 1) & (HW - 1), iwp = (iw - 1) & (HW - 1);
+    const uint32_t JD = as_u32(as_s16x2(J) - (s16x2){1, 1});  // (j0 - 1, j0)
+    uint32_t Hd = __builtin_amdgcn_alignbit(w0[iw], w0[iwp], 16);
+    uint32_t X1 = w0[HW + iw], X2 = w0[2 * HW + iw];
+    {
+        const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(B0)) | as_u32(as_s16x2(E0) - as_s16x2(JD)));
+        const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(B0)) | as_u32(as_s16x2(E0) - as_s16x2(J)));
+        Hd = bfi(md, kNeg2, Hd);
+        X1 = bfi(me, kNeg2, X1);
+        X2 = bfi(me, kNeg2, X2);
+    }
+    uint32_t MK = 0, K1 = 0, K2 = 0;
+    if (R.two) {
+        uint32_t Hd1 = __builtin_amdgcn_alignbit(w1[iw], w1[iwp], 16);
+        uint32_t X11 = w1[HW + iw], X21 = w1[2 * HW + iw];
+        const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(B1)) | as_u32(as_s16x2(E1b) - as_s16x2(JD)));
+        const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(B1)) | as_u32(as_s16x2(E1b) - as_s16x2(J)));
+        Hd1 = bfi(md, kNeg2, Hd1);
+        X11 = bfi(me, kNeg2, X11);
+        X21 = bfi(me, kNeg2, X21);
+        MK = pk_lt_bit<0>(Hd, Hd1);
+        K1 = pk_lt_bit<0>(X1, X11);
+        K2 = pk_lt_bit<0>(X2, X21);
+        Hd = pk_max(Hd, Hd1);
+        X1 = pk_max(X1, X11);
+        X2 = pk_max(X2, X21);
+    }
+    for (int k = 2; k < R.pn3; ++k) {  // the first strictly larger value names the predecessor
+        const int p = bcast0(sh.desc[R.r & (kDescBatch - 1)][3 + k]);
+        const int4 xr = sh.rrow[p & (kRowRing - 1)];
+        const uint32_t Bk = pk2s(xr.x), Ek = pk2s(xr.y);
+        const uint32_t *wk = reinterpret_cast<const uint32_t *>(ring16_row<RW>(sh, p & (kRing16 - 1)));
+        uint32_t Hdk = __builtin_amdgcn_alignbit(wk[iw], wk[iwp], 16);
+        uint32_t X1k = wk[HW + iw], X2k = wk[2 * HW + iw];
+        const uint32_t md = pk_neg_mask(as_u32(as_s16x2(JD) - as_s16x2(Bk)) | as_u32(as_s16x2(Ek) - as_s16x2(JD)));
+        const uint32_t me = pk_neg_mask(as_u32(as_s16x2(J) - as_s16x2(Bk)) | as_u32(as_s16x2(Ek) - as_s16x2(J)));
+        Hdk = bfi(md, kNeg2, Hdk);
+        X1k = bfi(me, kNeg2, X1k);
+        X2k = bfi(me, kNeg2, X2k);
+        const uint32_t kk = pk2(k);
+        MK = bfi(pk_neg_mask(pk_subs(Hd, Hdk)), kk, MK);
+        K1 = bfi(pk_neg_mask(pk_subs(X1, X1k)), kk, K1);
+        K2 = bfi(pk_neg_mask(pk_subs(X2, X2k)), kk, K2);
+        Hd = pk_max(Hd, Hdk);
+        X1 = pk_max(X1, X1k);
+        X2 = pk_max(X2, X2k);
+    }
+    const uint32_t M = pk_subs(pk_adds(Hd, S), pk2(sc.mismatch));
+    const uint32_t H0 = bfi(inv, kNeg2, pk_max(M, pk_max(X1, X2)));
+    const uint32_t LJ1 = as_u32(as_u16x2(LJ) * (u16x2){(unsigned short)e1, (unsigned short)e1});
+    const uint32_t LJ2 = as_u32(as_u16x2(LJ) * (u16x2){(unsigned short)e2, (unsigned short)e2});
+    const uint32_t G1 = pk_adds(H0, LJ1), G2 = pk_adds(H0, LJ2);
+    const uint32_t Ga = __builtin_amdgcn_perm(G2, G1, 0x05040100u);
+    const uint32_t Gb = __builtin_amdgcn_perm(G2, G1, 0x07060302u);
+    // the half's F prefix scan and its argmax key (H0 << 8 | 255 - column offset) in one DPP stream
+    uint32_t inc = pk_max(Ga, Gb) ^ kNeg2;
+    int amk = max(((int)(short)(H0 & 0xffff) << 8) | (255 - c0), (((int)H0 >> 16) << 8) | (254 - c0));
+    dpp_scan_fa(inc, amk);
+    // exchange: the lower half's F total (the upper half's carry-in) and both halves' argmax keys
+    const int myam = readlane(amk, kWave - 1);
+    if (h == 0) {
+        const int tot = readlane((int)inc, kWave - 1);
+        if (lane == 0) {
+            X.carry = tot;
+            X.am0 = myam;
+        }
+    } else if (lane == 0) {
+        X.am1 = myam;
+    }
+    group_barrier();  // BX
+    const int other = bcast0(h ? X.am0 : X.am1);
+    const uint32_t carry = h ? (uint32_t)bcast0(X.carry) : 0u;
+    const int mp = max(myam, other);
+    const int besti = cb0 + 255 - (mp & 255);
+    uint32_t Pa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x138, 0xf, 0xf, true);
+    Pa = pk_umax(Pa, carry) ^ kNeg2;  // carry 0 (the identity) in the lower half
+    const uint32_t Pb = pk_max(Pa, Ga);
+    const uint32_t P1 = __builtin_amdgcn_perm(Pb, Pa, 0x05040100u);
+    const uint32_t P2 = __builtin_amdgcn_perm(Pb, Pa, 0x07060302u);
+    const uint32_t F1 = pk_subs(P1, LJ1 + pk2(oe1 - e1)), F2 = pk_subs(P2, LJ2 + pk2(oe2 - e2));
+    const uint32_t H = pk_max(H0, pk_max(F1, F2));
+    const uint32_t X1e = pk_subs(X1, pk2(e1)), Ho1 = pk_subs(H, pk2(oe1));
+    const uint32_t X2e = pk_subs(X2, pk2(e2)), Ho2 = pk_subs(H, pk2(oe2));
+    const uint32_t E1 = pk_max(X1e, Ho1), E2 = pk_max(X2e, Ho2);
+    const uint32_t tbv = tb_pack(pk_subs(M, H), pk_subs(X1, H), pk_subs(X2, H), pk_subs(F1, H), pk_subs(Ho1, X1e),
+                                 pk_subs(Ho2, X2e), pk_subs(G1, P1), pk_subs(G2, P2));
+    row_store<uint16_t>(tb + ds.tb_used, (uint32_t)c0, (uint16_t)tbv);
+    if (R.multi) {
+        gu8 *kq = kp + ds.kp_used;
+        if (ks == 1) {
+            const uint32_t kb = MK | (K1 << 2) | (K2 << 4);
+            row_store<uint16_t>(kq, (uint32_t)c0, (uint16_t)__builtin_amdgcn_perm(0u, kb, 0x0C0C0200u));
+        } else {
+            const uint32_t ko = (uint32_t)(3 * c0);
+            row_store<uint16_t>(kq, ko, (uint16_t)__builtin_amdgcn_perm(K1, MK, 0x0C0C0400u));
+            row_store<uint16_t>(kq, ko + 2u, (uint16_t)__builtin_amdgcn_perm(MK, K2, 0x0C0C0600u));
+            row_store<uint16_t>(kq, ko + 4u, (uint16_t)__builtin_amdgcn_perm(K2, K1, 0x0C0C0602u));
+        }
+    }
+    uint32_t *wr = reinterpret_cast<uint32_t *>(ring16_row<RW>(sh, R.r & (kRing16 - 1)));
+    const uint32_t Hs = bfi(inv, kNeg2, H);
+    wr[iw] = Hs;
+    wr[HW + iw] = bfi(inv, kNeg2, E1);
+    wr[2 * HW + iw] = bfi(inv, kNeg2, E2);
+    if (R.far) {  // spill planes of a two-chunk row: stride RW (row_spill_width)
+        gint *svp = sv + svbase;
+        svp[j0] = (int)(short)(H & 0xffff);
+        svp[j0 + 1] = (int)H >> 16;
+        svp[RW + j0] = (int)(short)(E1 & 0xffff);
+        svp[RW + j0 + 1] = (int)E1 >> 16;
+        svp[2 * RW + j0] = (int)(short)(E2 & 0xffff);
+        svp[2 * RW + j0 + 1] = (int)E2 >> 16;
+    }
+    ds.r16acc = pk_umin(ds.r16acc, as_u32(as_u16x2(Hs) - as_u16x2(pk2(kR16Low))));
+    ds.tb_used += R.tbw;
+    if (R.multi) ds.kp_used += ks * R.tbw;
+    if (R.far) ds.sv_used += 3 * RW;
+    ds.cells += end - beg + 1;
+    if (h == 0 && lane == 0) {
+        sh.rrow[R.r & (kRowRing - 1)] = make_int4(beg, end, besti, soff);
+        gint *ri = rinfo + (int64_t)R.r * kRowInfoInts;
+        *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
+        if (R.far) *reinterpret_cast<GLB v2i *>(ri + 4) = (v2i){besti, soff};
+    }
+    return besti;
+}
+
+// Wave 1 of a two-wave workgroup: upper halves of the split rows wave 0 posts, until the exit command.
+// At the end of every read's DP (kW2End) it reports whether any of its cells came near the 16-bit -inf
+// band (the read is then re-aligned in 32-bit mode, by wave 0 alone).
+template <class SC>
+__device__ __forceinline__ void w2_helper(SharedState &sh, int lane) {
+    W2Lds &X = w2lds();
+    gu8 *tb, *kp;
+    gint *sv, *rinfo;
+    SC sc;
+    {
+        const Slot s = slot_of(sh);
+        tb = s.tb;
+        kp = s.kp;
+        sv = s.sv;
+        rinfo = s.rinfo;
+        if constexpr (!std::is_same<SC, DefaultScores>::value) {
+            const PoaRunArgs a = args_of(sh);
+            sc = SC{a.match, a.mismatch, a.o1, a.e1, a.o2, a.e2};
+        }
+    }
+    DpState ds{0, 0, 0, 0, 0xffffffffu, 0, {0, 0, 0, 0}};
+    int spilled = 0;
+    for (;;) {
+        // a far row's spill columns may be read by wave 0 (a later row whose predecessor left the ring):
+        // they are complete before the next barrier (the workgroup barrier orders LDS, not pending stores)
+        if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        spilled = 0;
+        group_barrier();  // B0
+        const int4 c0 = *reinterpret_cast<const int4 *>(&X.cmd);
+        const int op = bcast0(c0.x);
+        if (op == kW2Exit) break;
+        if (op == kW2Nop) continue;
+        if (op == kW2End) {
+            // the read's traceback / predecessor bytes are complete before wave 0's backtrack reads them
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t m = min(ds.r16acc & 0xffffu, ds.r16acc >> 16);
+            const unsigned long long nearinf = __ballot(m < (uint32_t)(kR16High - kR16Low));
+            if (lane == 0) X.flag = nearinf ? 1 : 0;
+            ds.r16acc = 0xffffffffu;
+            group_barrier();  // the flag is read by wave 0
+            continue;
+        }
+        const int4 *c = reinterpret_cast<const int4 *>(&X.cmd);
+        const int4 c1 = c[1], c2 = c[2], c3 = c[3], c4 = c[4], c5 = c[5];
+        Row16 R;
+        R.r = bcast0(c0.y);
+        R.beg = bcast0(c0.z);
+        R.end = bcast0(c0.w);
+        R.cb0 = bcast0(c1.x);
+        R.tbw = bcast0(c1.y);
+        R.vb = bcast0(c1.z);
+        R.pn = bcast0(c1.w);
+        R.b0 = bcast0(c2.x);
+        R.e0 = bcast0(c2.y);
+        R.b1 = bcast0(c2.z);
+        R.e1 = bcast0(c2.w);
+        R.p0slot = bcast0(c3.x);
+        R.p1slot = bcast0(c3.y);
+        R.two = bcast0(c3.z);
+        R.far = bcast0(c3.w);
+        R.multi = bcast0(c4.x);
+        R.pn3 = bcast0(c4.y);
+        ds.tb_used = bcast0(c4.z);
+        ds.kp_used = bcast0(c4.w);
+        ds.sv_used = bcast0(c5.x);
+        row16w_half<SC>(sc, tb, kp, sv, rinfo, sh, lane, R, ds, 1);
+        spilled = R.far;
+    }
+}
+
 // The row loop of 16-bit mode (same rows, same results as run_dp<SC, true>).  The per-row
 // control is written for the scalar unit: tests accumulate as sign bits into one word
 // (`bad < 0` = take the generic row) rather than as bools, which the compiler would keep as
 // 64-bit lane masks.
-template <class SC, int RW>
+template <class SC, int RW, int NW = 1>
 __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen, int n, int lane, int w,
                                         DpState &ds, int &nfast) {
+    static_assert(NW == 1 || RW == kWideRing, "two-wave rows: wide launches");
+    // NW == 2: the previous row was split over both waves, so wave 1 may still be writing its ring
+    // half; a row wave 0 computes alone first passes a B0 with a no-op command
+    int split = 0;
+    auto sync_alone = [&]() {
+        if constexpr (NW > 1) {
+            if (split) {
+                w2_post_op(kW2Nop, lane);
+                group_barrier();
+                split = 0;
+            }
+        }
+    };
     gu8 *tb, *kp;
     gint *sv, *rinfo, *desc;
     int tb_lim, kp_lim, sv_lim;
@@ -1922,8 +2215,17 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
                 ds.seg[2] += Q.nomask;
 #endif
                 int besti;
-                if (RW == kChunk || Q.end - Q.cb0 < kChunk) besti = row16_vec<SC, RW, true>(sc, tb, kp, sv, rinfo, sh, lane, Q, ds);
-                else besti = row16w_vec(sc, tb, kp, sv, rinfo, sh, lane, Q, ds);
+                if (RW == kChunk || Q.end - Q.cb0 < kChunk) {
+                    sync_alone();
+                    besti = row16_vec<SC, RW, true>(sc, tb, kp, sv, rinfo, sh, lane, Q, ds);
+                } else if constexpr (NW > 1) {
+                    w2_post_row(Q, ds, lane);
+                    group_barrier();  // B0
+                    split = 1;
+                    besti = row16w_half<SC>(sc, tb, kp, sv, rinfo, sh, lane, Q, ds, 0);
+                } else {
+                    besti = row16w_vec(sc, tb, kp, sv, rinfo, sh, lane, Q, ds);
+                }
                 prv_r = r;
                 prv_beg = Q.beg;
                 prv_end = Q.end;
@@ -2007,14 +2309,24 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
             ds.seg[3] += R.pn3 >= 3;
 #endif
             int besti;
-            if (RW == kChunk || R.end - R.cb0 < kChunk) besti = row16_vec<SC, RW>(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
-            else besti = row16w_vec(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
+            if (RW == kChunk || R.end - R.cb0 < kChunk) {
+                sync_alone();
+                besti = row16_vec<SC, RW>(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
+            } else if constexpr (NW > 1) {
+                w2_post_row(R, ds, lane);
+                group_barrier();  // B0
+                split = 1;
+                besti = row16w_half<SC>(sc, tb, kp, sv, rinfo, sh, lane, R, ds, 0);
+            } else {
+                besti = row16w_vec(sc, tb, kp, sv, rinfo, sh, lane, R, ds);
+            }
             prv_r = r;
             prv_beg = R.beg;
             prv_end = R.end;
             prv_am = besti;
             ++nfast;
         } else {
+            sync_alone();
             Slot s = slot_of(sh);
             const PoaRunArgs a = args_of(sh);
 #ifdef MANDO_GENPROF
@@ -2054,7 +2366,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
 // banded DP over all rows of the current graph for read q (qlen): writes the traceback bytes and
 // returns the start row of the backtrack in bi_out (or -1)
 // ---------------------------------------------------------------------------------------------
-template <class SC, bool R16, int RW = kChunk>
+template <class SC, bool R16, int RW = kChunk, int NW = 1>
 __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8_t *q, int qlen,
                       int n, int lane, int64_t &cells, int &bi_out) {
     const PoaRunArgs a = args_of(sh);
@@ -2073,7 +2385,15 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
     }
     int nfast = 0;
     if constexpr (R16) {
-        const int st = run_dp16<SC, RW>(sh, sc, qlen, n, lane, w, ds, nfast);
+        const int st = run_dp16<SC, RW, NW>(sh, sc, qlen, n, lane, w, ds, nfast);
+        if constexpr (NW > 1) {
+            // end of the read's rows: wave 1 has written its last ring half and reports whether its cells
+            // came near the 16-bit -inf band
+            w2_post_op(kW2End, lane);
+            group_barrier();  // B0
+            group_barrier();  // wave 1's flag
+            if (bcast0(w2lds().flag)) ds.r16bad = 1;
+        }
         if (st != kStOk) return st;
     } else {
     RowPipe pp;
@@ -3314,13 +3634,26 @@ __device__ __forceinline__ void seeded_main(SharedState &sh, TeamBox *box, int m
     }
 }
 
-template <class SC, bool SEEDED, int RW>
-__global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
+#ifndef MANDO_WIDE_WPE
+#define MANDO_WIDE_WPE 4  // waves per SIMD the one-wave wide instantiation is compiled for (register budget)
+#endif
+template <class SC, bool SEEDED, int RW, int NW = 1>
+__global__ __launch_bounds__(kWave * NW, NW > 1 ? 2 : (RW == kWideRing ? MANDO_WIDE_WPE : 4)) void poa_kernel(PoaKArgs ka) {
     constexpr int kPrioDp = 0;                             // DP rows (see the unseeded read loop)
     constexpr int kPrioSerial = kPrioDp + kSerialPrio;     // descriptors, backtrack, update, consensus
     static_assert(RW == kChunk || (RW == kWideRing && !SEEDED), "wide rings: unseeded launches");
+    static_assert(NW == 1 || (NW == 2 && RW == kWideRing), "two-wave workgroups: wide launches");
     __shared__ SharedState sh;
     const int lane = lane_id();
+    if constexpr (NW > 1) {
+        // wave 1 of a two-wave workgroup: upper halves of the wide rows (w2_helper), once wave 0 has set
+        // up the workgroup's LDS state
+        if (bcast0((int)(threadIdx.x >> 6)) != 0) {
+            group_barrier();
+            w2_helper<SC>(sh, lane);
+            return;
+        }
+    }
     if (lane == 0) sh.args = ka;
     wave_sync();
     const PoaKArgs &a = ka;
@@ -3409,6 +3742,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
         sh.slot_idx = sidx;
     }
     wave_sync();
+    if constexpr (NW > 1) group_barrier();  // wave 1 may read the LDS state now
 
     if constexpr (SEEDED) {
         if (member > 0 && (a.dbg & 8)) return;  // MANDO_POA_DBG bit 3: helpers absent (leaders align alone)
@@ -3498,7 +3832,7 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
                 __builtin_amdgcn_s_setprio(kPrioDp);
                 // 16-bit mode when the read's score range allows it; a read that leaves the safe
                 // range is re-aligned in 32-bit mode (the graph is untouched until update_graph)
-                st = try16 ? run_dp<SC, true, RW>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
+                st = try16 ? run_dp<SC, true, RW, NW>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
                 if (st == kStRetry32) {
                     if (prof && lane == 0) prof[15] += 1;
                     if (try16) {  // descriptors of the 32-bit ring (far / fast flags depend on its depth)
@@ -3553,6 +3887,10 @@ __global__ __launch_bounds__(kWave, 4) void poa_kernel(PoaKArgs ka) {
         }
         wave_sync();
     }
+    if constexpr (NW > 1) {  // wave 1 leaves its loop
+        w2_post_op(kW2Exit, lane);
+        group_barrier();
+    }
     if (ka.one_group) {  // the slot is free again (this group's stores are done first)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -3602,6 +3940,8 @@ template <class F>
 static auto by_kind(const PoaKArgs &a, F &&f) {
     const bool dflt = default_scores(a);
     if (a.caps.seeded) return dflt ? f(poa_kernel<DefaultScores, true, kChunk>) : f(poa_kernel<RuntimeScores, true, kChunk>);
+    if (a.caps.wide && a.nw == 2)
+        return dflt ? f(poa_kernel<DefaultScores, false, kWideRing, 2>) : f(poa_kernel<RuntimeScores, false, kWideRing, 2>);
     if (a.caps.wide)
         return dflt ? f(poa_kernel<DefaultScores, false, kWideRing>) : f(poa_kernel<RuntimeScores, false, kWideRing>);
     return dflt ? f(poa_kernel<DefaultScores, false, kChunk>) : f(poa_kernel<RuntimeScores, false, kChunk>);
@@ -3610,7 +3950,9 @@ static auto by_kind(const PoaKArgs &a, F &&f) {
 int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
     int nb = by_kind(a, [&](auto kern) {
         int v = 0;
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kern, kWave, poa_dyn_lds(a)) == hipSuccess ? v : 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, kern, kWave * poa_waves(a), poa_dyn_lds(a)) == hipSuccess
+                   ? v
+                   : 0;
     });
     if (nb < 1) nb = 8;
     return nb < cap ? nb : cap;
@@ -3618,7 +3960,7 @@ int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
 
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream) {
     by_kind(a, [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(n_slots), dim3(kWave), poa_dyn_lds(a), stream, a);
+        hipLaunchKernelGGL(kern, dim3(n_slots), dim3(kWave * poa_waves(a)), poa_dyn_lds(a), stream, a);
         return 0;
     });
     return hipGetLastError();

@@ -272,6 +272,23 @@ _CHUNK_BYTES = int(os.environ.get("MANDO_CHUNK_BYTES", str(8 << 30)))
 _TWO_CHUNK_BYTES = int(os.environ.get("MANDO_TWO_CHUNK_BYTES", str(8 << 30)))
 # fewer loci than this always run in one chunk (a few large loci: SIRV-like, config 5)
 _MIN_LOCI_CHUNKED = 1024
+# heaviest-first plans: the share of the estimated POA cost that goes into the first chunk (0: off, the
+# default -- measured on config 3 it did not pay, DESIGN.md §5: chunk B's clustering and orientation run
+# 2x slower beside chunk A's POA, which lasts its longest group anyway)
+_HEAVY_FRAC = float(os.environ.get("MANDO_HEAVY_FRAC", "0"))
+
+
+def _heavy_first(sizes: np.ndarray, frac: float) -> tuple[np.ndarray, np.ndarray]:
+    """Loci of the heaviest-first plan: (chunk A, chunk B) as sorted index arrays.  The POA cost of a
+    locus is n L^2 (L its read length, n its reads) and its file holds ~n L bytes, so with
+    the depth fixed by the subsample the cost grows as the file size squared; A takes the largest loci
+    until it holds `frac` of that cost."""
+    cost = sizes.astype(np.float64) ** 2
+    order = np.argsort(-cost, kind="stable")
+    cs = np.cumsum(cost[order])
+    k = int(np.searchsorted(cs, frac * cs[-1])) + 1 if len(cs) and cs[-1] > 0 else 0
+    k = min(max(k, 1), max(len(order) - 1, 1))
+    return np.sort(order[:k]), np.sort(order[k:])
 
 
 def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0) -> tuple[int, list | None]:
@@ -300,14 +317,17 @@ def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0) -> tuple[int, l
     return max(1, min(n_chunks, max(1, n_loci))), fracs
 
 
-# HBM plan of one call (bytes per byte of a chunk's locus text, measured on config 3 / config 4 chunks with
-# MANDO_WS_LOG=1): the device text itself (pool buffers rounded to 256 MB: the chunks in
-# flight -- clustering k+1, POA k, writing k-1 -- plus one cached), the clustering scratch of the largest
-# chunk (K1 records, cs runs, K2 maps and outputs; one per call, reused) and the reads gathered for
-# orientation and for the POA (one copy each)
+# HBM plan of one call (bytes per byte of a chunk's locus text, measured on config-4 chunks with
+# MANDO_WS_LOG=1: profiles/r04c_config4_ws_log.txt): the device text itself (pool buffers rounded to
+# 256 MB: the chunks in flight -- clustering k+1, POA k, writing k-1 -- plus one cached), the clustering
+# scratch of the largest chunk (K1 records and cs runs 2.56x the text, K2 maps and outputs 1.98x; one set
+# per call, reused, allocated with 1/4 headroom) and the reads gathered for orientation and for the POA
+# (0.42x each)
 _HBM_USABLE = 0.92
-_CLUSTER_SCRATCH_PER_TEXT = 1.5
-_GATHERED_PER_TEXT = 0.5
+# chunks whose buffers may be alive at once (clustering k+2 while k+1 waits for the POA and k is written)
+_MAX_INFLIGHT = 3
+_CLUSTER_SCRATCH_PER_TEXT = 1.25 * 4.55
+_GATHERED_PER_TEXT = 0.42
 
 
 def poa_budget(total_hbm: int, span_text: list) -> int:
@@ -389,40 +409,71 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
            if bidx else None)
     t1 = time.perf_counter()
     timeline = [("ingest", 0.0, t1 - t0)]
+    explicit_chunks = n_chunks
     # Chunked pipeline: clustering of chunk k+1 (host C++ threads, GIL released) overlaps orientation +
-    # POA of chunk k on the GPU.  Chunks are contiguous runs of sorted roots.  Every POA launch lasts at
-    # least as long as its longest group, so few, large launches are best: inputs below one byte-capped
-    # chunk (_TWO_CHUNK_BYTES of locus text) run in one chunk, larger ones (config 4 on one GPU: ~60 GB)
-    # in chunks of at most _CHUNK_BYTES, the first 0.4 of one, so that its POA starts early.
+    # POA of chunk k on the GPU.  Every POA launch lasts at least as long as its longest group, so few,
+    # large launches are best:
+    # * inputs above one byte-capped chunk (config 4 on one GPU: ~60 GB of locus text) run in contiguous
+    #   chunks of at most _CHUNK_BYTES, the first 0.4 of one, so that its POA starts early;
+    # * smaller inputs with many loci (config 3, a multi-GPU rank's share) run "heaviest first": chunk A
+    #   holds the loci of the largest POA cost (~_HEAVY_FRAC of it: the longest groups, whose one-wave
+    #   latency sets every launch's floor) and is clustered, oriented and launched first; chunk B (the
+    #   rest) is clustered, oriented and assembled while A's POA runs, and its POA is launched on a second
+    #   device context beside it.  Outputs are written once both are done (sorted roots);
+    # * few loci (SIRV-like, config 5) run in one chunk.
     sizes = np.array([root_size.get(r, 0) for r in my_roots], dtype=np.int64)
     n_chunks, fracs = _chunk_plan(int(sizes.sum()), len(my_roots), n_chunks)
-    cuts = [0]
-    if n_chunks > 1:
-        cs = np.cumsum(sizes)
-        fr = fracs or [k / n_chunks for k in range(1, n_chunks)]
-        for f in fr:
-            cuts.append(int(np.searchsorted(cs, cs[-1] * f)) + 1)
-    cuts.append(len(my_roots))
-    cuts = sorted(set(min(max(c, 0), len(my_roots)) for c in cuts))
-    spans = [(cuts[k], cuts[k + 1]) for k in range(len(cuts) - 1) if cuts[k + 1] > cuts[k]] or [(0, 0)]
+    heavy = (n_chunks == 1 and len(my_roots) >= _MIN_LOCI_CHUNKED and _HEAVY_FRAC > 0
+             and os.environ.get("MANDO_CHUNKS") is None and explicit_chunks <= 0)
+    if heavy:
+        parts = list(_heavy_first(sizes, _HEAVY_FRAC))
+    else:
+        cuts = [0]
+        if n_chunks > 1:
+            cs = np.cumsum(sizes)
+            fr = fracs or [k / n_chunks for k in range(1, n_chunks)]
+            for f in fr:
+                cuts.append(int(np.searchsorted(cs, cs[-1] * f)) + 1)
+        cuts.append(len(my_roots))
+        cuts = sorted(set(min(max(c, 0), len(my_roots)) for c in cuts))
+        parts = [np.arange(cuts[k], cuts[k + 1]) for k in range(len(cuts) - 1) if cuts[k + 1] > cuts[k]]
+        parts = parts or [np.arange(0)]
+    # one rank and contiguous chunks: each chunk's part of both files is written as soon as it is done
+    stream_out = world == 1 and not heavy
+    mine_a = np.asarray(mine, dtype=np.int64)
     # the POA workspaces' HBM budget for this call, from the chunk plan (no free-memory query: the
     # clustering thread allocates the next chunk's buffers while a POA launch sizes its workspace)
-    n_poa = int(os.environ.get("MANDO_POA_STREAMS", "1")) if len(spans) > 1 else 1
+    n_poa = 2 if heavy else (int(os.environ.get("MANDO_POA_STREAMS", "1")) if len(parts) > 1 else 1)
     if dev_poa:
-        span_text = [int(sizes[lo:hi].sum()) for lo, hi in spans]
+        span_text = [int(sizes[ix].sum()) for ix in parts]
         for k in range(n_poa):
             pctx = _lib.context(device, 3 * k)
             pctx.set_poa_budget(poa_budget(pctx.memory()[0], span_text) // n_poa)
 
     # with several chunks in flight, two cores stay with the GPU driver, assembly and compaction threads
     n_cpu = threads if threads > 0 else (os.cpu_count() or 1)
-    cl_threads = max(1, n_cpu - 2) if len(spans) > 1 and n_cpu > 4 else threads
+    cl_threads = max(1, n_cpu - 2) if len(parts) > 1 and n_cpu > 4 else threads
 
-    def run_cluster(lo, hi):
+    # backpressure: at most _MAX_INFLIGHT chunks hold their buffers (locus text on host and device,
+    # clustering results) at once -- clustering runs ahead of the POA otherwise, and a many-chunk input
+    # (config 4 on one GPU; any input under the CPU restatements) would hold every chunk at once
+    inflight = threading.BoundedSemaphore(_MAX_INFLIGHT)
+
+    def run_cluster(ix):
+        inflight.acquire()
+        try:
+            r = _run_cluster(ix)
+        except BaseException:
+            inflight.release()
+            raise
+        return r
+
+    def _run_cluster(ix):
         # clustering (host C++ threads, GIL released), then the orientation input: the subsampled reads
         tc = time.perf_counter()
         r = (cluster_fn or cluster.cluster_loci)(
-            [os.path.join(out_tmp, x + ".psl") for x in my_roots[lo:hi]], chroms[lo:hi], ann=ann[lo:hi] if ann else None,
+            [os.path.join(out_tmp, my_roots[i] + ".psl") for i in ix], [chroms[i] for i in ix],
+            ann=[ann[i] for i in ix] if ann else None,
             device=device, cutoff=cutoff, splice_site_width=splice_site_width,
             minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
             downstream_buffer=downstream_buffer, junctions=junctions, seed=seed, threads=cl_threads)
@@ -433,8 +484,9 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             i = int(bad[0])
             code = int(r.locus_status[i])
             r.close()
-            raise RuntimeError(f"locus {my_roots[lo + i]}: {cluster.STATUS.get(code, code)} "
+            raise RuntimeError(f"locus {my_roots[ix[i]]}: {cluster.STATUS.get(code, code)} "
                                "(the reference's locus worker raises here)")
+        r.on_close = inflight.release  # the chunk leaves the pipeline when its buffers are released
         if dev_orient:
             o_in = (r.seq_off[r.sub], r.seq_len[r.sub])
         else:
@@ -445,7 +497,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
 
     stats = {"loci": len(roots), "isoforms": 0, "poa_groups": 0, "records": 0, "poa_reads": 0,
              "t_ingest": t1 - t0, "t_cluster": 0.0, "t_pack": 0.0, "t_orient": 0.0, "t_assemble": 0.0,
-             "t_poa": 0.0, "chunks": len(spans), "poa_launches": poa_launches}
+             "t_poa": 0.0, "chunks": len(parts), "heavy_first": heavy, "poa_launches": poa_launches}
     payloads = []
     stats["timeline"] = timeline
 
@@ -460,18 +512,18 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
 
     # Staged pipeline over chunks: clustering (one host thread driving the C++ pool, chunks in order) ->
     # orientation (main thread, GPU slot 1) -> emission assembly (host thread) -> POA (one host thread,
-    # GPU slot 0, by default; MANDO_POA_STREAMS=2 adds a second on slot 3 so that chunk k+1's grids can
-    # be queued while chunk k's drain) -> compaction (host thread).
+    # GPU slot 0, by default; heaviest-first plans and MANDO_POA_STREAMS=2 add a second on slot 3 so that
+    # chunk k+1's grids run beside chunk k's) -> writer.
     lock = threading.Lock()
 
     def add(key, v):
         with lock:
             stats[key] += v
 
-    def poa_job(res, asm_fut, lo, hi):
+    def poa_job(res, asm_fut, ix):
         prep = asm_fut.result()
         tp = time.perf_counter()
-        pl = _poa_chunk(res, mine[lo:hi], prep, run_poa, stats, lock)
+        pl = _poa_chunk(res, mine_a[ix], prep, run_poa, stats, lock)
         timeline.append(("poa", tp - t0, time.perf_counter() - t0))
         if world > 1:
             # several ranks: the chunk's results are gathered at the end, so its referenced bytes are
@@ -482,21 +534,21 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             res.close()
         return pl, res
 
-    # one POA host thread (one device context, n_poa above) by default: with two, a chunk whose
-    # predecessor's POA ran late went to the second context, whose workspace was then sized from the HBM
-    # the first one left free -- a quarter of the slots, the persistent grid, 2.9 s instead of 1.1 s
-    # (measured in 3 of 30 config-3 steps; none in 18 with one context)
+    # POA host threads (n_poa above), one device context each: each context's workspaces have their own
+    # explicit budget (a share of the call's plan), so a second context never sizes its workspace from
+    # the HBM the first one left free (r02: a quarter of the slots, the persistent grid, 2.9 s, in 3 of
+    # 30 config-3 steps when it did)
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
             ThreadPoolExecutor(max_workers=1) as writer, \
             ThreadPoolExecutor(max_workers=n_poa) as gpu_poa:
-        cl = [ex.submit(run_cluster, lo, hi) for lo, hi in spans]
+        cl = [ex.submit(run_cluster, ix) for ix in parts]
         poa_futs = []
         # one rank: reads2isoforms.txt needs only the clustering, so each chunk's part of it is written
         # by the host thread (after the chunk's assembly) while the POA runs; the FASTA follows each POA
         fa = r2 = None
         r2_futs = []
         n_iso_before = 0
-        if world == 1:
+        if stream_out:
             fa = open(out_path + "/Isoform_Consensi.fasta", "wb")
             r2 = open(out_path + "/reads2isoforms.txt", "wb")
 
@@ -516,9 +568,9 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             res.close()
             return n, res
 
-        def write_r2i(res, lo, hi, counter0):
+        def write_r2i(res, ix, counter0):
             tw = time.perf_counter()
-            _write_payload(_names_payload(res, mine[lo:hi]), None, r2, counter0)
+            _write_payload(_names_payload(res, mine_a[ix]), None, r2, counter0)
             timeline.append(("write_r2i", tw - t0, time.perf_counter() - t0))
         def close_outputs():
             if fa is not None:
@@ -528,7 +580,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                 r2.close()
 
         try:
-            for k, (lo, hi) in enumerate(spans):
+            for k, ix in enumerate(parts):
                 res, tcl, (o_a, o_b), tpk = cl[k].result()
                 add("t_cluster", tcl)
                 add("t_pack", tpk)
@@ -541,9 +593,9 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                 timeline.append(("orient", tg - t0, te - t0))
                 add("t_orient", te - tg)
                 asm_fut = host.submit(assemble, res, hits, n_hits)
-                poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, lo, hi))
-                if world == 1:
-                    r2_futs.append(host.submit(write_r2i, res, lo, hi, n_iso_before))
+                poa_futs.append(gpu_poa.submit(poa_job, res, asm_fut, ix))
+                if stream_out:
+                    r2_futs.append(host.submit(write_r2i, res, ix, n_iso_before))
                     fa_futs.append(writer.submit(write_fasta, poa_futs[-1], n_iso_before, r2_futs[-1]))
                     n_iso_before += res.n_isoforms
         except BaseException:
@@ -551,7 +603,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             _close_all(cl, poa_futs)
             raise
         results = []
-        if world == 1:
+        if stream_out:
             # one rank: chunks are contiguous runs of the sorted roots and finish in order; both files
             # were written chunk by chunk by the host and writer threads
             written = 0
@@ -577,10 +629,11 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             except BaseException:
                 _close_all(cl, poa_futs)
                 raise
-    if world > 1:
+    if not stream_out:
         tm = time.perf_counter()
         payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
-        payload = _gather(payload, comm)
+        if world > 1:
+            payload = _gather(payload, comm)
         timeline.append(("merge", tm - t0, time.perf_counter() - t0))
         if rank == 0:
             tw = time.perf_counter()

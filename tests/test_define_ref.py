@@ -72,6 +72,34 @@ def test_driver_with_oracle_equals_reference(tmp_path, name):
     assert sum(seeded) == GOLD["datasets"][name]["reference"]["n_seeded_calls"]
 
 
+@pytest.mark.parametrize("name", ["config1", "r2c2_rev"])
+def test_driver_heaviest_first_equals_reference(tmp_path, name, monkeypatch):
+    """The heaviest-first two-chunk plan (chunk A: the loci of largest POA cost, chunk B: the rest, two POA
+    threads, one write at the end in sorted-root order) writes the reference's exact files."""
+    from oracle import orient as oref
+    from oracle import poa as opoa
+
+    monkeypatch.setattr(define, "_MIN_LOCI_CHUNKED", 1)
+    monkeypatch.setattr(define, "_HEAVY_FRAC", 0.3)
+    d = _dataset(tmp_path, name)
+    st = _run(d, orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
+              consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci)
+    assert st["heavy_first"] and st["chunks"] == 2
+    _check(d, name, st)
+
+
+def test_heavy_first_split():
+    import numpy as np
+
+    sizes = np.array([10, 50, 20, 40, 30, 5], dtype=np.int64)
+    a, b = define._heavy_first(sizes, 0.5)
+    assert list(a) == [1, 3] and list(b) == [0, 2, 4, 5]   # 50^2 + 40^2 >= half of the sum of squares
+    a, b = define._heavy_first(sizes, 0.0)
+    assert list(a) == [1] and len(b) == 5                  # never empty
+    a, b = define._heavy_first(sizes, 1.0)
+    assert len(a) == 5 and len(b) == 1                     # nor the second
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(GOLD["datasets"]))
 def test_gpu_driver_equals_reference(gpu_ctx, tmp_path, name):
@@ -153,6 +181,19 @@ def test_sharded_two_ranks_equals_reference(tmp_path):
 
 # BASELINE configs[3] shape (10M mixed R2C2 + PacBio 2-4 kb, sharded): a small slice of it
 CONFIG4_SLICE = dict(reads=(40, 60), exons=(5, 12), exon_len=(130, 570), pacbio_frac=0.2, rev_frac=0.5, seed=4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["config1", "sirv_like"])
+def test_gpu_driver_heaviest_first_equals_reference(gpu_ctx, tmp_path, name, monkeypatch):
+    """The product path with the heaviest-first plan: two POA launches on two device contexts side by side
+    (the second chunk clustered and oriented while the first one's POA runs): the reference's files."""
+    monkeypatch.setattr(define, "_MIN_LOCI_CHUNKED", 1)
+    monkeypatch.setattr(define, "_HEAVY_FRAC", 0.3)
+    d = _dataset(tmp_path, name)
+    st = _run(d)
+    assert st["heavy_first"] and len(st["poa_launches"]) == 2
+    _check(d, name, st)
 
 
 @pytest.mark.gpu

@@ -112,6 +112,30 @@ def test_grid_modes_and_launch_kinds(monkeypatch, persistent):
     _check(narrow + wide + longer)
 
 
+@pytest.mark.parametrize("waves", ["1", "2"])
+def test_wide_launch_waves_per_group(monkeypatch, waves):
+    """Wide launches with one or two waves per group (MANDO_POA_W2=1: every two-chunk fast row split over
+    the two waves of the group's workgroup, poa_kernel.hip row16w_half; one-chunk, generic and 32-bit rows
+    stay on wave 0): the same bytes and DP cells as the oracle.  The batch spans bands just over one chunk
+    (5-6 kb), two full chunks (8-9 kb, 16-bit shifted), 32-bit rows (> 10.1 kb), deep and shallow groups,
+    and rows with several predecessors (indels shared by several reads)."""
+    monkeypatch.setenv("MANDO_POA_W2", waves)
+    _, mid = poa_cases.noisy_groups(6, (5000, 6000), (6, 30), seed=91)
+    _, long_g = poa_cases.noisy_groups(3, (8000, 9000), (4, 12), seed=92)
+    _, longer = poa_cases.noisy_groups(1, (10500, 11000), (3, 4), seed=93)
+    rng = np.random.default_rng(94)
+    t = synth.random_template(rng, 6000).tobytes().decode()
+    ins = synth.random_template(rng, 300).tobytes().decode()
+    branchy = [[t, t[:2500] + ins + t[2500:], t, t[:2000] + t[2600:], t[:2500] + ins + t[2500:], t[:4000] + "N" * 30 + t[4030:], t]]
+    _check(mid + long_g + longer + branchy)
+
+
+def test_wide_two_waves_deep_long_group(monkeypatch):
+    """Config-5's unseeded shape (one wave per group is its critical path): 40 reads x ~8.5 kb, two waves."""
+    monkeypatch.setenv("MANDO_POA_W2", "1")
+    _check(poa_cases.noisy_groups(1, (8300, 8700), (40, 40), seed=95)[1])
+
+
 @pytest.mark.parametrize("team", ["1", "3", "8"])
 def test_seeded_team_sizes(monkeypatch, team):
     """-S teams (poa_kernel.hip "-S teams"): a read's windows aligned by 1 (solo), 3 or 8 workgroups

@@ -4,7 +4,7 @@
 set -e
 name=$1; flags=$2
 root=$(cd "$(dirname "$0")/.." && pwd)
-out=$root/build/$name
+out=$root/${VARIANT_DIR:-build}/$name
 mkdir -p $out
 make -s -j8 -C $root/mandalorion_amd/csrc OUT=$out "HIPFLAGS=--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -munsafe-fp-atomics $flags" $out/libmando.so
 echo "built $out/libmando.so"
