@@ -141,6 +141,8 @@ def parse():
     ap.add_argument("--check-launch", action="store_true",
                     help="launch, rendezvous, data and shard plan only (no GPU compute); prints the ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--share", type=int, default=0,
+                    help="one GPU runs rank 0's loci of an N-rank LPT plan (the per-rank load of an N-GPU run)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     return ap.parse_args()
 
@@ -210,9 +212,14 @@ def cpu_fns(threads: int):
     return orient_fn, consensus_fn, pool
 
 
+SHARE = None  # (rank, N) with --share N: every D pass runs that rank's loci only
+
+
 def run_define(d, threads, device, comm=None, **kw):
     from mandalorion_amd import define
 
+    if SHARE is not None and comm is None and "share" not in kw and "orient_fn" not in kw:
+        kw["share"] = SHARE
     return define.define_isoforms(d, threads=threads, device=device, comm=comm, **kw)
 
 
@@ -282,8 +289,9 @@ def shard_plan(data: str, world: int) -> list:
     """The driver's LPT plan (define.define_isoforms): loci per rank, for --check-launch."""
     from mandalorion_amd import define
 
-    roots = define._roots(os.path.join(data, "tmp_SS"))
-    cost = define._locus_costs(os.path.join(data, "tmp_SS"), roots)
+    root_size: dict = {}
+    roots = define._roots(os.path.join(data, "tmp_SS"), root_size)
+    cost = define._size_costs(roots, root_size)
     load = np.zeros(world)
     cnt = [0] * world
     for i in np.argsort(-cost, kind="stable"):
@@ -321,6 +329,12 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     wl = WORKLOADS[args.workload]
     n_loci = args.loci or wl["loci"]
+    global SHARE
+    if args.share > 1:
+        if args.gpus != 1 or "WORLD_SIZE" in os.environ:
+            raise SystemExit("--share runs one rank's load on one GPU (no launcher, --gpus 1)")
+        SHARE = (0, args.share)
+        args.no_cpu_baseline = True
     cores = host_cores()
     # host threads per rank: the usable cores per GPU of this node (a rank drives one GPU), at most 16
     threads = args.threads or max(2, min(16, cores["usable"] // max(1, local_world)))
@@ -388,7 +402,9 @@ def main():
     st = stats[-1]
 
     # the whole output of the last timed step against the oracle's full-size hashes (rank 0 wrote it)
-    full_parity = fullsize_check(data, f"{args.workload}:{n_loci}") if rank == 0 else None
+    full_parity = fullsize_check(data, f"{args.workload}:{n_loci}") if rank == 0 and SHARE is None else None
+    if SHARE is not None:  # one rank's load: its own records
+        records = stats[-1]["records"]
 
     # roofline of the dominant kernel (POA), from this rank's launches of the last timed step:
     # algorithmic bytes per launch = 1 B traceback per DP cell + each read once + each consensus once
@@ -442,7 +458,8 @@ def main():
         "dtype": "int16",
         "data": "synthetic PSL loci (libmando_synth, seed 20250117): no real reads in the container",
         "config": {
-            "workload": wl["text"] + (f" (loci overridden: {n_loci})" if args.loci else ""),
+            "workload": wl["text"] + (f" (loci overridden: {n_loci})" if args.loci else "")
+                        + (f" -- rank 0's share of a {SHARE[1]}-rank LPT plan, run alone on one GPU" if SHARE else ""),
             "records": records,
             "loci": st["loci"],
             "isoforms": st["isoforms"],
@@ -453,7 +470,8 @@ def main():
             "host_threads_per_rank": threads,
             "host_cores": cores,
             "phases_rank0_s": {k: round(st[k], 4) for k in ("t_ingest", "t_cluster", "t_orient", "t_assemble", "t_poa",
-                                                             "t_total") if k in st},
+                                                             "t_merge", "t_write", "t_total") if k in st},
+            "chunks": st.get("chunks"),
             "poa_kernel": {
                 "launches": n_launch,
                 "kernel_ms_total": k_ms,

@@ -232,6 +232,10 @@ int mando_allgather_counts(mando_comm *comm, int64_t n, int64_t *counts);
 /* recv = every rank's send bytes concatenated in rank order; recv_counts from mando_allgather_counts */
 int mando_allgather_bytes(mando_comm *comm, const uint8_t *send, int64_t n, uint8_t *recv,
                           const int64_t *recv_counts);
+/* Every rank's bytes on rank 0 only, in rank order (recv_counts from mando_allgather_counts; recv may be
+ * NULL on the other ranks): RCCL point-to-point sends to rank 0 between GPUs (xGMI), the TCP star without
+ * a device.  The D driver's reassembly (defineIsoforms.py:155-166's writer is rank 0). */
+int mando_gather_bytes(mando_comm *comm, const uint8_t *send, int64_t n, uint8_t *recv, const int64_t *recv_counts);
 /* *v = max over ranks of *v (the benchmark's max-over-ranks wall time) */
 int mando_allreduce_max_f64(mando_comm *comm, double *v);
 int mando_comm_barrier(mando_comm *comm);

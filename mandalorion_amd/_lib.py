@@ -45,6 +45,7 @@ EXPORTED = (
     "mando_comm_backend",
     "mando_allgather_counts",
     "mando_allgather_bytes",
+    "mando_gather_bytes",
     "mando_allreduce_max_f64",
     "mando_comm_barrier",
     "mando_comm_destroy",
@@ -216,6 +217,7 @@ def load(path: str | None = None):
         lib.mando_comm_backend.argtypes = [_P]
         lib.mando_allgather_counts.argtypes = [_P, _I64, _P]
         lib.mando_allgather_bytes.argtypes = [_P, _P, _I64, _P, _P]
+        lib.mando_gather_bytes.argtypes = [_P, _P, _I64, _P, _P]
         lib.mando_allreduce_max_f64.argtypes = [_P, _P]
         lib.mando_comm_barrier.argtypes = [_P]
         lib.mando_comm_destroy.argtypes = [_P]

@@ -64,6 +64,16 @@ class Comm:
                                                   _lib.ptr(counts)))
         return out[:int(counts.sum())], counts
 
+    def gather_bytes(self, blob: np.ndarray) -> tuple[np.ndarray | None, np.ndarray]:
+        """Every rank's uint8 blob, concatenated in rank order, on rank 0 (None elsewhere), plus the counts."""
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        counts = self.allgather_counts(blob.size)
+        out = np.empty(max(int(counts.sum()), 1), dtype=np.uint8) if self.rank == 0 else None
+        send = blob if blob.size else np.zeros(1, dtype=np.uint8)
+        _lib.check(self.lib.mando_gather_bytes(self.handle, _lib.ptr(send), int(blob.size), _lib.ptr(out),
+                                               _lib.ptr(counts)))
+        return (out[:int(counts.sum())] if out is not None else None), counts
+
     def max(self, v: float) -> float:
         x = ctypes.c_double(float(v))
         _lib.check(self.lib.mando_allreduce_max_f64(self.handle, ctypes.byref(x)))

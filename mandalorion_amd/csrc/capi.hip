@@ -349,7 +349,14 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, (int64_t)ctx->n_cu * per_cu / team));
     if (granted > 0) {
         teams = std::max<int64_t>(1, std::min<int64_t>(teams, (int64_t)(budget / ((size_t)team * a.slot_bytes))));
-        if (ws.bytes > (size_t)(teams * team * a.slot_bytes) + (budget >> 3)) ws.release();  // give back the rest
+        // a workspace that must grow gets 1/8 of headroom within the grant, so the next chunk's slightly
+        // larger slots do not reallocate it
+        const size_t need = (size_t)(teams * team * a.slot_bytes);
+        if (ws.bytes < need) {
+            ws.release();
+            int rc0 = ws.ensure(std::min(budget, need + need / 8));
+            if (rc0) return rc0;
+        }
     } else {
         while (teams > 1 && (size_t)(teams * team * a.slot_bytes) > budget) teams /= 2;
     }
@@ -848,10 +855,18 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                 grant[kind] += more;
                 rem -= more;
             }
-            for (int kind = 0; kind < 3; ++kind) {
-                DevBuf &w = kind_ws(ctx, kind);
-                if (lists[kind].empty() || w.bytes > grant[kind]) w.release();
-            }
+            // a kind keeps a workspace larger than its grant while everything held fits the budget (a
+            // hipFree synchronises the device and a fresh hipMalloc of ~100 GB costs seconds): absent
+            // kinds' workspaces go first, then the excess of the others
+            auto held = [&] {
+                size_t t = 0;
+                for (int kind = 0; kind < 3; ++kind) t += std::max(kind_ws(ctx, kind).bytes, grant[kind]);
+                return t;
+            };
+            for (int kind = 0; kind < 3 && held() > B; ++kind)
+                if (lists[kind].empty()) kind_ws(ctx, kind).release();
+            for (int kind = 0; kind < 3 && held() > B; ++kind)
+                if (kind_ws(ctx, kind).bytes > grant[kind]) kind_ws(ctx, kind).release();
         }
         int lane = 0;
         for (int ki = 0; ki < 3; ++ki) {

@@ -186,6 +186,29 @@ int star_allgather(mando_comm *c, const void *send, int64_t n, std::vector<uint8
     return tot > 0 ? recv_all(c->fd[0], all->data(), (size_t)tot) : MANDO_OK;
 }
 
+// every rank's bytes on rank 0 only (rank order; the other ranks receive nothing)
+int star_gather(mando_comm *c, const void *send, int64_t n, std::vector<uint8_t> *all, std::vector<int64_t> *counts) {
+    const int R = c->nranks;
+    counts->assign((size_t)R, 0);
+    if (c->rank != 0) {
+        int rc = send_all(c->fd[0], &n, 8);
+        if (!rc && n > 0) rc = send_all(c->fd[0], send, (size_t)n);
+        return rc;
+    }
+    all->assign(static_cast<const uint8_t *>(send), static_cast<const uint8_t *>(send) + n);
+    (*counts)[0] = n;
+    for (int r = 1; r < R; ++r) {
+        int64_t k = 0;
+        int rc = recv_all(c->fd[(size_t)r], &k, 8);
+        if (rc) return rc;
+        const size_t at = all->size();
+        all->resize(at + (size_t)k);
+        if (k > 0 && (rc = recv_all(c->fd[(size_t)r], all->data() + at, (size_t)k))) return rc;
+        (*counts)[(size_t)r] = k;
+    }
+    return MANDO_OK;
+}
+
 int nccl_fail(ncclResult_t r, const char *what) {
     return mando::set_error(MANDO_E_INTERNAL, std::string(what) + ": " + ncclGetErrorString(r));
 }
@@ -313,6 +336,64 @@ int mando_allgather_bytes(mando_comm *c, const uint8_t *send, int64_t n, uint8_t
         if (recv_counts[root] == 0) continue;
         if (hipMemcpyAsync(recv + off[(size_t)root], static_cast<uint8_t *>(c->drecv) + (size_t)root * (size_t)maxc,
                            (size_t)recv_counts[root], hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+            return mando::set_error(MANDO_E_HIP, "comm: D2H copy failed");
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: stream sync failed");
+    return MANDO_OK;
+}
+
+int mando_gather_bytes(mando_comm *c, const uint8_t *send, int64_t n, uint8_t *recv, const int64_t *recv_counts) {
+    if (!c || !recv_counts || n < 0 || (n > 0 && !send)) return mando::set_error(MANDO_E_ARG, "mando_gather_bytes: bad argument");
+    const int R = c->nranks;
+    if (recv_counts[c->rank] != n) return mando::set_error(MANDO_E_ARG, "mando_gather_bytes: recv_counts[rank] != n");
+    std::vector<int64_t> off((size_t)R + 1, 0);
+    for (int r = 0; r < R; ++r) {
+        if (recv_counts[r] < 0) return mando::set_error(MANDO_E_ARG, "mando_gather_bytes: negative count");
+        off[(size_t)r + 1] = off[(size_t)r] + recv_counts[r];
+    }
+    const int64_t tot = off[(size_t)R];
+    const bool root = c->rank == 0;
+    if (root && tot > 0 && !recv) return mando::set_error(MANDO_E_ARG, "mando_gather_bytes: null recv on rank 0");
+    if (R == 1) {
+        if (n > 0) memcpy(recv, send, (size_t)n);
+        return MANDO_OK;
+    }
+    if (!c->nccl) {
+        std::vector<uint8_t> all;
+        std::vector<int64_t> cnt;
+        int rc = star_gather(c, send, n, &all, &cnt);
+        if (rc || !root) return rc;
+        for (int r = 0; r < R; ++r)
+            if (cnt[(size_t)r] != recv_counts[r]) return mando::set_error(MANDO_E_ARG, "mando_gather_bytes: counts disagree");
+        if (tot > 0) memcpy(recv, all.data(), (size_t)tot);
+        return MANDO_OK;
+    }
+    // RCCL: point-to-point sends to rank 0 in one group (rank 0 receives each rank's bytes at its
+    // offset); no rank but 0 holds more than its own bytes, unlike the padded all-gather
+    if (hipSetDevice(c->device) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: hipSetDevice failed");
+    int rc = ensure_dev(&c->dsend, &c->dsend_cap, (size_t)std::max<int64_t>(n, 1));
+    if (!rc && root) rc = ensure_dev(&c->drecv, &c->drecv_cap, (size_t)std::max<int64_t>(tot, 1));
+    if (rc) return rc;
+    if (n > 0 && hipMemcpyAsync(c->dsend, send, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return mando::set_error(MANDO_E_HIP, "comm: H2D copy failed");
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) {
+        if (root) {
+            for (int p = 1; p < R && r == ncclSuccess; ++p)
+                if (recv_counts[p] > 0)
+                    r = ncclRecv(static_cast<uint8_t *>(c->drecv) + off[(size_t)p], (size_t)recv_counts[p], ncclUint8, p,
+                                 c->nccl, c->stream);
+        } else if (n > 0) {
+            r = ncclSend(c->dsend, (size_t)n, ncclUint8, 0, c->nccl, c->stream);
+        }
+        const ncclResult_t e = ncclGroupEnd();
+        if (r == ncclSuccess) r = e;
+    }
+    if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv gather");
+    if (root) {
+        if (n > 0) memcpy(recv, send, (size_t)n);  // rank 0's own bytes never leave the host
+        if (tot > n && hipMemcpyAsync(recv + n, static_cast<uint8_t *>(c->drecv) + n, (size_t)(tot - n),
+                                      hipMemcpyDeviceToHost, c->stream) != hipSuccess)
             return mando::set_error(MANDO_E_HIP, "comm: D2H copy failed");
     }
     if (hipStreamSynchronize(c->stream) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: stream sync failed");

@@ -115,26 +115,14 @@ def _roots_py(out_tmp: str, sizes: dict | None = None) -> list[str]:
     return sorted(roots, key=lambda x: (x.split("~")[0], int(x.split("~")[1])))
 
 
-def _locus_costs(out_tmp: str, roots: list[str]) -> np.ndarray:
-    """Per-locus POA cost estimate: n reads of length L cost n * L * (2w + 1) * 1.1 L
-    with w = 10 + 0.01 L (rows ~ 1.1 L graph nodes, band 2w+1).  L is the first record's qSize (col 10)
-    and n ~ file size / that record's length: one small read per file, no parse of the locus."""
-    from concurrent.futures import ThreadPoolExecutor
-
-    def one(r):
-        f = os.path.join(out_tmp, r + ".psl")
-        size = os.path.getsize(f)
-        with open(f, "rb") as fh:
-            line = fh.readline()
-        try:
-            L = float(line.split(b"\t", 11)[10])
-        except (IndexError, ValueError):
-            L = 1.0
-        n = size / max(1, len(line))
-        return n * L * (2 * (10 + 0.01 * L) + 1) * 1.1 * L
-
-    with ThreadPoolExecutor(max_workers=8) as ex:
-        return np.fromiter(ex.map(one, roots), dtype=np.float64, count=len(roots))
+def _size_costs(roots: list[str], root_size: dict) -> np.ndarray:
+    """Per-locus POA cost estimate for the shard plan, from the file sizes the root scan returns (no
+    per-file I/O): a locus of n reads of length L costs ~n L^2 (n L (2w+1) 1.1 L) and
+    its file holds ~n L bytes, so with the read count bounded by the subsample the cost grows as the
+    size squared.  Reading each file's first record instead (round 3) took 1 s per rank per step on
+    20,000 loci and 8-9 s on 200,000 (r04f), on the critical path of every rank."""
+    sz = np.fromiter((root_size.get(r, 0) for r in roots), dtype=np.float64, count=len(roots))
+    return sz * sz
 
 
 class Assembly:
@@ -262,7 +250,12 @@ def _fasta_bytes(aux, hs, hl, nl_pos, cons_src, cons_sel, cons_start, cons_len, 
     return fasta
 
 
-_CHUNK_BYTES = int(os.environ.get("MANDO_CHUNK_BYTES", str(8 << 30)))
+# inputs of more than _TWO_CHUNK_BYTES of locus text run in chunks of at most this many bytes: a 4 GiB chunk's
+# text, clustering scratch and gathered reads (about 7x the text, three chunks in flight) leave room for
+# both POA launch kinds' one-group grids in a 288 GB HBM (config 4 on one GPU; r04e: 8 GiB chunks left
+# the narrow launch 3,440 of its 3,840 slots, a persistent grid that held the CUs the next chunk's
+# orientation waited for)
+_CHUNK_BYTES = int(os.environ.get("MANDO_CHUNK_BYTES", str(4 << 30)))
 # inputs with at least this much locus text run in two chunks (or more, past _CHUNK_BYTES); 10,000
 # config-3 loci are 3.1 GB, 20,000 are 6.2 GB.  At 20,000 loci one chunk and two have the same mean step
 # (1.78 / 1.77 s over 24 steps each), but two chunks put chunk 2's clustering and orientation kernels
@@ -343,13 +336,17 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                     junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", upstream_buffer: int = 10,
                     downstream_buffer: int = 50, seed: int = 0, device: int = 0,
                     orient_fn: Callable | None = None, consensus_fn: Callable | None = None,
-                    cluster_fn: Callable | None = None, comm=None, verbose: bool = False, n_chunks: int = 0) -> dict:
+                    cluster_fn: Callable | None = None, comm=None, verbose: bool = False, n_chunks: int = 0,
+                    share: tuple[int, int] | None = None) -> dict:
     """Runs the D module on <path>/tmp_SS/*.psl.  orient_fn(seqs, seq_off, grp_off) -> (hits, n_hits),
     consensus_fn(seqs, seq_off, grp_off, seeding) -> (cons bytes, cons_off) and cluster_fn (the signature
     of cluster.cluster_loci) default to the HIP path.
-    comm (mandalorion_amd.comm.Comm, optional): shard the loci over comm.world ranks; rank 0 writes."""
+    comm (mandalorion_amd.comm.Comm, optional): shard the loci over comm.world ranks; rank 0 writes.
+    share (r, N), without comm: run only rank r's loci of an N-rank plan, as one process writing its own
+    files (the per-rank load of a multi-GPU run, measured on one GPU)."""
     t0 = time.perf_counter()
     rank, world = (comm.rank, comm.world) if comm is not None else (0, 1)
+    plan_rank, plan_world = (rank, world) if share is None or comm is not None else share
     # the HIP path keeps the reads on the device (gathered from the clustering's device text); injected
     # host functions get them packed
     dev_orient = orient_fn is None
@@ -393,15 +390,15 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     roots = _roots(out_tmp, root_size)
     # shard loci over ranks: LPT on the DP-cost estimate of SURVEY.md §8(e), results regathered in root order
     mine = list(range(len(roots)))
-    if world > 1:
-        cost = _locus_costs(out_tmp, roots)
-        load = np.zeros(world)
+    if plan_world > 1:
+        cost = _size_costs(roots, root_size)
+        load = np.zeros(plan_world)
         owner = np.zeros(len(roots), dtype=np.int64)
         for i in np.argsort(-cost, kind="stable"):
             k = int(np.argmin(load))
             owner[i] = k
             load[k] += cost[i]
-        mine = [i for i in range(len(roots)) if owner[i] == rank]
+        mine = [i for i in range(len(roots)) if owner[i] == plan_rank]
     my_roots = [roots[i] for i in mine]
     chroms = [r.split("~")[0] for r in my_roots]
     bidx = gtf.BoundsIndex(left, right)
@@ -643,6 +640,9 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             timeline.append(("write", tw - t0, time.perf_counter() - t0))
         del payload
     stats["t_total"] = time.perf_counter() - t0
+    # host time of the output stages (summed over chunks; streamed writes overlap the POA of later chunks)
+    stats["t_write"] = sum(b - a for n, a, b in timeline if n in ("write", "write_r2i"))
+    stats["t_merge"] = sum(b - a for n, a, b in timeline if n == "merge")
     # the chunks' buffers go back to their pools before returning: every kernel that read them has
     # completed (the POA calls are synchronous), and no release can then overlap the next call's kernels
     del payloads
@@ -778,14 +778,14 @@ _FIELDS = ("iso_root", "c_start", "c_len", "n_start", "n_len", "mem_off")
 
 
 def _gather(payload: dict, comm) -> dict:
-    """Reassembly on rank 0: one all-gather of each rank's compacted results (RCCL over
-    xGMI between GPUs, the rendezvous sockets on CPU).  Each rank ships its isoforms' root indices,
-    consensus bytes and member names; only rank 0 unpacks them for the writer."""
+    """Reassembly on rank 0: one gather of each rank's compacted results to the writer
+    (RCCL point-to-point sends over xGMI between GPUs, the rendezvous sockets on CPU).  Each rank ships its
+    isoforms' root indices, consensus bytes and member names; only rank 0 receives and unpacks them."""
     p = _compact(payload)
     arrays = [np.ascontiguousarray(p[f]) for f in _FIELDS] + [p["cons_src"][0], p["name_src"][0]]
     hdr = np.array([a.nbytes for a in arrays] + [a.dtype.num for a in arrays], dtype=np.int64)
     blob = np.concatenate([hdr.view(np.uint8)] + [a.view(np.uint8).ravel() for a in arrays])
-    allb, counts = comm.allgather_bytes(blob)
+    allb, counts = comm.gather_bytes(blob)
     if comm.rank != 0:
         return payload
     parts = []

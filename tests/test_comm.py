@@ -23,6 +23,9 @@ def _rank(rank, world, port, q):
     with Comm(world, rank, "127.0.0.1", port, timeout_s=60) as c:
         blob = np.full(rank * 1000 + 3, rank + 1, dtype=np.uint8) if rank != 1 else np.zeros(0, np.uint8)
         allb, counts = c.allgather_bytes(blob)
+        g, gc = c.gather_bytes(blob)
+        assert gc.tolist() == counts.tolist()
+        assert (g is None) == (rank != 0) and (g is None or g.tobytes() == allb.tobytes())
         m = c.max(float(rank) * 1.5)
         c.barrier()
         q.put((rank, counts.tolist(), allb.tobytes(), m, c.backend))
@@ -55,6 +58,8 @@ def test_single_rank_needs_no_peers():
     with Comm(1, 0) as c:
         b, cnt = c.allgather_bytes(np.arange(10, dtype=np.uint8))
         assert cnt.tolist() == [10] and b.tolist() == list(range(10))
+        g, gc = c.gather_bytes(np.arange(7, dtype=np.uint8))
+        assert gc.tolist() == [7] and g.tolist() == list(range(7))
         assert c.max(2.5) == 2.5
         c.barrier()
 
@@ -77,6 +82,8 @@ def test_rccl_backend_single_rank(gpu_ctx):
         assert c.backend == "rccl"
         b, cnt = c.allgather_bytes((np.arange(1000) % 251).astype(np.uint8))
         assert cnt.tolist() == [1000] and b.tolist() == [i % 251 for i in range(1000)]
+        g, gc = c.gather_bytes((np.arange(999) % 13).astype(np.uint8))
+        assert gc.tolist() == [999] and g.tolist() == [i % 13 for i in range(999)]
         c.barrier()
 
 
@@ -92,6 +99,10 @@ def _rccl_rank(rank, world, port, q):
         # ragged sizes (rank 1 sends nothing): the padded ncclAllGather + per-slice compaction
         blob = ((np.arange(rank * 70001 + 13) * (rank + 3)) % 251).astype(np.uint8) if rank != 1 else np.zeros(0, np.uint8)
         allb, counts = c.allgather_bytes(blob)
+        # the writer's gather: point-to-point sends to rank 0 (ragged, one empty)
+        g, gc = c.gather_bytes(blob)
+        assert gc.tolist() == counts.tolist()
+        assert (g is None) == (rank != 0) and (g is None or g.tobytes() == allb.tobytes())
         m = c.max(float(rank) * 1.5)
         c.barrier()
         q.put((rank, counts.tolist(), allb.tobytes(), m, c.backend))

@@ -88,6 +88,27 @@ def test_driver_heaviest_first_equals_reference(tmp_path, name, monkeypatch):
     _check(d, name, st)
 
 
+def test_driver_rank_shares_partition_the_loci(tmp_path):
+    """share=(r, N) runs rank r's loci of the N-rank LPT plan alone (bench.py --share): the shares of a
+    2-rank plan together hold every record and isoform of the one-rank run, each exactly once."""
+    from oracle import orient as oref
+    from oracle import poa as opoa
+
+    d = _dataset(tmp_path, "config1")
+    kw = dict(orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
+              consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci)
+    full = _run(d, **kw)
+    names = lambda: sorted(l.split("\t")[0] for l in open(os.path.join(d, "reads2isoforms.txt")))
+    all_reads = names()
+    got, reads = [], []
+    for r in range(2):
+        st = _run(d, share=(r, 2), **kw)
+        got.append((st["records"], st["isoforms"]))
+        reads += names()
+    assert sum(x[0] for x in got) == full["records"] and sum(x[1] for x in got) == full["isoforms"]
+    assert all(x[0] > 0 for x in got) and sorted(reads) == all_reads
+
+
 def test_heavy_first_split():
     import numpy as np
 
