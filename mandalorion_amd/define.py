@@ -82,7 +82,9 @@ def _roots(out_tmp: str, sizes: dict | None = None) -> list[str]:
     (mando_list_roots); a root whose start field is not a plain decimal takes the Python path below,
     which parses (or raises) exactly as the reference does."""
     lib = _lib.load()
-    cap_n, cap_b = 1 << 16, 1 << 22
+    # room for 512k roots in the first call (a second call repeats the whole scan: 200,000 loci took
+    # two, 0.5 s per rank, r04g)
+    cap_n, cap_b = 1 << 19, 1 << 24
     for _ in range(2):
         names = ctypes.create_string_buffer(cap_b)
         sz = np.empty(cap_n, dtype=np.int64)
@@ -200,6 +202,47 @@ class Assembly:
         return seqs, so, grp
 
 
+def _label_lines(k: np.ndarray, m: np.ndarray, first: int) -> tuple[np.ndarray, np.ndarray]:
+    """The bytes of the lines chr(first) + 'Isoform{k}_{m}' + '\n' for every (k, m) (non-negative), back
+    to back, and their lengths -- vectorised (a Python f-string per isoform took 0.45 s for config 4's
+    400,000 isoforms on the writer's critical path)."""
+    k = np.asarray(k, dtype=np.int64)
+    m = np.asarray(m, dtype=np.int64)
+    n = len(k)
+
+    def ndig(x):
+        d = np.ones(len(x), dtype=np.int64)
+        p = 10
+        for _ in range(18):
+            d += x >= p
+            p *= 10
+        return d
+
+    dk, dm = ndig(k), ndig(m)
+    pre = b"_Isoform"  # the first byte is replaced by `first`
+    ln = len(pre) + dk + 1 + dm + 1
+    end = np.cumsum(ln)
+    st = end - ln
+    out = np.empty(int(end[-1]) if n else 0, dtype=np.uint8)
+    if not n:
+        return out, ln
+    for j, c in enumerate(pre):
+        out[st + j] = c
+    out[st] = first
+
+    def put(x, dx, at):  # decimal digits of x, most significant first, at byte offsets `at`
+        for j in range(int(dx.max())):
+            live = j < dx
+            p = np.power(10, np.maximum(dx - 1 - j, 0))
+            out[(at + j)[live]] = (ord("0") + (x // p) % 10)[live]
+
+    put(k, dk, st + len(pre))
+    out[st + len(pre) + dk] = ord("_")
+    put(m, dm, st + len(pre) + dk + 1)
+    out[end - 1] = ord("\n")
+    return out, ln
+
+
 def _fasta_and_r2i(name_src, name_sel, name_start, name_len, mem_off, cons_src, cons_sel, cons_start, cons_len,
                    cons_rc, counter0: int = 0, fasta_part: bool = True, r2i_part: bool = True):
     """Isoform_Consensi.fasta and reads2isoforms.txt bytes for isoforms in output order
@@ -207,11 +250,10 @@ def _fasta_and_r2i(name_src, name_sel, name_start, name_len, mem_off, cons_src, 
     Consensi and names are byte segments of several sources (locus texts, POA outputs), gathered once."""
     n_iso = len(mem_off) - 1
     n_mem = np.diff(mem_off)
-    labels = [f"Isoform{counter0 + i + 1}_{int(n_mem[i])}" for i in range(n_iso)]
-    head = "".join(f">{l}\n" for l in labels).encode()
-    suf = "".join(f"\t{l}\n" for l in labels).encode()
-    aux = np.frombuffer(head + b"\n" + suf or b"\0", dtype=np.uint8)
-    hl = np.array([len(l) + 2 for l in labels], dtype=np.int64)
+    head, hl = _label_lines(np.arange(counter0 + 1, counter0 + 1 + n_iso, dtype=np.int64), n_mem, ord(">"))
+    suf = head.copy()
+    suf[np.cumsum(hl) - hl] = ord("\t")
+    aux = np.concatenate([head, np.frombuffer(b"\n", np.uint8), suf])
     hs = np.zeros(n_iso, dtype=np.int64)
     if n_iso:
         hs[1:] = np.cumsum(hl)[:-1]
@@ -716,10 +758,35 @@ def _write_payload(payload: dict, fa, r2, counter0: int) -> int:
                                 payload.get("cons_src"), *cons, counter0=counter0, fasta_part=fa is not None,
                                 r2i_part=r2 is not None)
     if fa is not None:
-        fa.write(memoryview(np.ascontiguousarray(fasta)))
+        _write_big(fa, fasta)
     if r2 is not None:
-        r2.write(memoryview(np.ascontiguousarray(r2i)))
+        _write_big(r2, r2i)
     return int(len(order))
+
+
+def _write_big(fh, arr: np.ndarray, piece: int = 64 << 20) -> None:
+    """Appends arr to the open file: large buffers as parallel pwrite()s of 64 MB pieces (the page-cache
+    copy of one write() call runs at ~1.5 GB/s; rank 0 writes a whole 10M-record output at the end of a
+    multi-GPU run), small ones with one write()."""
+    buf = memoryview(np.ascontiguousarray(arr)).cast("B")
+    n = len(buf)
+    if n < 4 * piece:
+        fh.write(buf)
+        return
+    from concurrent.futures import ThreadPoolExecutor
+
+    fh.flush()
+    fd, at = fh.fileno(), fh.tell()
+
+    def one(o):
+        v = buf[o:o + piece]
+        done = 0
+        while done < len(v):
+            done += os.pwrite(fd, v[done:], at + o + done)
+
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        list(ex.map(one, range(0, n, piece)))
+    fh.seek(at + n)
 
 
 def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, run_poa, stats: dict, lock):

@@ -75,3 +75,27 @@ def test_metrics_line():
     assert m["poa_algorithmic_GBps"] == pytest.approx((8 * 10**9 + 10**6 + 10**4) / 1e9)
     assert m["poa_hbm_roofline_frac"] == pytest.approx(m["poa_algorithmic_GBps"] / 8000.0)
     assert define.metrics({"t_total": 1.0, "records": 0})["gcups"] is None
+
+
+def test_isoform_label_lines():
+    import numpy as np
+
+    k = np.array([1, 9, 10, 99, 100, 12345, 7, 10**12])
+    m = np.array([1, 0, 10, 123, 5, 2, 99999, 3])
+    b, ln = define._label_lines(k, m, ord(">"))
+    assert b.tobytes() == "".join(f">Isoform{a}_{c}\n" for a, c in zip(k, m)).encode()
+    assert list(ln) == [len(f">Isoform{a}_{c}\n") for a, c in zip(k, m)]
+    assert define._label_lines(np.zeros(0, np.int64), np.zeros(0, np.int64), 9)[0].size == 0
+
+
+def test_write_big_appends_in_order(tmp_path):
+    import numpy as np
+
+    a = (np.arange(5 << 20) % 251).astype(np.uint8)
+    p = tmp_path / "out"
+    with open(p, "wb") as fh:
+        fh.write(b"head")
+        define._write_big(fh, a, piece=1 << 20)   # 5 parallel pwrite pieces
+        fh.write(b"tail")
+    got = p.read_bytes()
+    assert got == b"head" + a.tobytes() + b"tail"
