@@ -109,6 +109,38 @@ def test_driver_rank_shares_partition_the_loci(tmp_path):
     assert all(x[0] > 0 for x in got) and sorted(reads) == all_reads
 
 
+def test_driver_three_rank_reassembly_in_one_process(tmp_path):
+    """The 3-rank reassembly with the transport replaced by an in-process hand-over (the rehearsal of
+    tools/rank_rehearsal.py): ranks 1 and 2 run their shares and hand their compacted payloads over, rank 0
+    runs its share, receives them and writes files byte-identical to the reference's."""
+    import numpy as np
+    from oracle import orient as oref
+    from oracle import poa as opoa
+
+    store = {}
+
+    class Rec:
+        def __init__(self, rank):
+            self.rank, self.world = rank, 3
+
+        def gather_bytes(self, blob):
+            store[self.rank] = np.array(blob, copy=True)
+            if self.rank:
+                return None, None
+            parts = [store[r] for r in range(3)]
+            return np.concatenate(parts), np.array([p.size for p in parts])
+
+    d = _dataset(tmp_path, "r2c2_rev")
+    kw = dict(orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
+              consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci)
+    groups = 0
+    for r in (1, 2, 0):
+        st = _run(d, comm=Rec(r), **kw)
+        groups += st["poa_groups"]
+    st["poa_groups"] = groups  # each rank counts its own POA calls
+    _check(d, "r2c2_rev", st)
+
+
 def test_heavy_first_split():
     import numpy as np
 

@@ -1,0 +1,93 @@
+"""Rehearsal of an N-rank D-module run on one GPU: the ranks run one after another in
+this process, each on its own share of the LPT plan, exactly as define_isoforms runs them under a real
+communicator -- except the transport: ranks 1..N-1 hand their compacted payload to a recording stand-in
+for mando_gather_bytes, and rank 0 receives those bytes from it.  Rank 0 then merges and writes the
+whole output, so the rehearsal measures every rank's step and rank 0's reassembly (merge + write) on the
+full-size data set, and checks the reassembled files against the one-rank run.
+
+The predicted N-GPU step = max over ranks of (the rank's own step) + rank 0's gather-side work; the RCCL
+transfer itself (bytes into rank 0 over xGMI) is estimated, not measured (one GPU here).
+
+usage: python tools/rank_rehearsal.py <data dir with tmp_SS> N [threads]
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class _Recorder:
+    """A rank r != 0: its gather_bytes call hands the blob to the shared store and returns nothing."""
+
+    def __init__(self, rank, world, store):
+        self.rank, self.world, self.store = rank, world, store
+
+    def gather_bytes(self, blob):
+        self.store[self.rank] = np.array(blob, dtype=np.uint8, copy=True)
+        return None, None
+
+
+class _Root:
+    """Rank 0: receives every recorded blob (its own first), as mando_gather_bytes would on the writer."""
+
+    def __init__(self, world, store):
+        self.rank, self.world, self.store = 0, world, store
+
+    def gather_bytes(self, blob):
+        self.store[0] = np.array(blob, dtype=np.uint8, copy=True)
+        parts = [self.store[r] for r in range(self.world)]
+        return np.concatenate(parts), np.array([p.size for p in parts], dtype=np.int64)
+
+
+def sha(p):
+    h = hashlib.sha256()
+    with open(p, "rb") as fh:
+        for b in iter(lambda: fh.read(1 << 24), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
+def main():
+    from mandalorion_amd import define
+
+    d, n = sys.argv[1], int(sys.argv[2])
+    threads = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+    files = ("Isoform_Consensi.fasta", "reads2isoforms.txt")
+    ref = {f: sha(os.path.join(d, f)) for f in files} if all(os.path.exists(os.path.join(d, f)) for f in files) else None
+    store: dict = {}
+    out = {"ranks": n, "rank_s": {}, "payload_bytes": {}}
+    # warm the caches (files, device buffers) once, as the bench's warmup step does
+    define.define_isoforms(d, threads=threads, share=(1 % n, n))
+    for r in list(range(1, n)) + [0]:
+        comm = _Root(n, store) if r == 0 else _Recorder(r, n, store)
+        t0 = time.perf_counter()
+        st = define.define_isoforms(d, threads=threads, comm=comm)
+        out["rank_s"][r] = round(time.perf_counter() - t0, 4)
+        if r:
+            out["payload_bytes"][r] = int(store[r].size)
+        else:
+            out["payload_bytes"][0] = int(store[0].size)
+            out["rank0_phases_s"] = {k: round(st[k], 4) for k in ("t_ingest", "t_cluster", "t_orient", "t_poa",
+                                                                   "t_merge", "t_write", "t_total")}
+            out["rank0_compute_s"] = round(st["t_total"] - st["t_merge"] - st["t_write"], 4)
+    got = {f: sha(os.path.join(d, f)) for f in files}
+    out["reassembled_equals_one_rank"] = (got == ref) if ref else None
+    out["reassembled_sha256"] = got
+    # predicted N-GPU step: the slowest rank's own work, then rank 0's merge + write of everything, plus
+    # the transfer of the other ranks' payloads into rank 0 (RCCL p2p over xGMI, estimated at 50 GB/s)
+    others = max(v for r, v in out["rank_s"].items() if r != 0) if n > 1 else 0.0
+    xfer = sum(v for r, v in out["payload_bytes"].items() if r != 0) / 50e9
+    out["predicted_step_s"] = round(max(others, out["rank0_compute_s"]) + out["rank0_phases_s"]["t_merge"]
+                                    + out["rank0_phases_s"]["t_write"] + xfer, 4)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
