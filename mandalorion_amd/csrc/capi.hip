@@ -1,6 +1,7 @@
 // capi.hip — C-ABI of libmando (declared in include/mando.h): contexts, device buffers, batch
 // planning for the POA kernel (capacity estimates, LPT work order, overflow re-runs).
 #include <hip/hip_runtime.h>
+#include <chrono>
 
 #include <algorithm>
 #include <cstdio>
@@ -41,7 +42,12 @@ struct DevBuf {
         p = nullptr;
         bytes = 0;
         size_t nb = std::max<size_t>(need, 256);
+        const auto t0 = std::chrono::steady_clock::now();
         hipError_t e = hipMalloc(&p, nb);
+        static const bool log = getenv("MANDO_WS_LOG") != nullptr;
+        if (log && nb > ((size_t)1 << 30))
+            fprintf(stderr, "[mando ws] hipMalloc %.2f GB: %.3f s\n", nb / 1e9,
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
         if (e != hipSuccess) {
             p = nullptr;
             return fail(MANDO_E_NOMEM, std::string("hipMalloc(") + std::to_string(nb) +

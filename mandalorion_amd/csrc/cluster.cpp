@@ -7,6 +7,7 @@
 //
 // Also mando_pack_segments, the byte gather the D driver uses to build the orientation / POA inputs
 // and the output files.
+#include "threads.h"
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -196,7 +197,7 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     const bool timing = getenv("MANDO_CL_TIME") != nullptr;
     const auto t_0 = std::chrono::steady_clock::now();
     auto secs = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_0).count(); };
-    int nth = prm->threads > 0 ? prm->threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    int nth = prm->threads > 0 ? prm->threads : mando::usable_threads();
     nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n_loci));
     // read every locus file into one buffer: sizes first (stat, on the reader threads), then reads
     vector<int64_t> fsize((size_t)n_loci, 0), foff((size_t)n_loci + 1, 0);
@@ -402,7 +403,7 @@ int mando_pack_segments(const uint8_t *const *src, const int8_t *sel, const int6
                         const int8_t *rc, int64_t n, uint8_t *out, const int64_t *out_off, int32_t threads) {
     if (n < 0 || (n > 0 && (!src || !starts || !lens || !out || !out_off))) return MANDO_E_ARG;
     const mando::CompTable &comp = mando::comp_table();
-    int nth = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    int nth = threads > 0 ? threads : mando::usable_threads();
     nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n / 256));
     auto work = [&](int64_t a, int64_t b) {
         for (int64_t i = a; i < b; ++i) {

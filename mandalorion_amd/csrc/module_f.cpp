@@ -11,6 +11,7 @@
 // Chromosomes are processed in parallel (independent, like the reference's Pool) and written in
 // sorted order.  Where the reference picks "the first element of a set" (reason texts only) this
 // picks the smallest name.
+#include "threads.h"
 #include <zlib.h>
 
 #include <algorithm>
@@ -669,7 +670,7 @@ int mando_filter_isoforms(const mando_filter_params *P, const char *isoform_fast
     vector<vector<Iso>> isos(chroms.size());
     vector<ChrOut> outs(chroms.size());
     std::atomic<size_t> next{0};
-    int nth = P->threads > 0 ? P->threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    int nth = P->threads > 0 ? P->threads : mando::usable_threads();
     nth = (int)std::min<size_t>((size_t)nth, std::max<size_t>(1, chroms.size()));
     auto work = [&]() {
         for (size_t i; (i = next.fetch_add(1)) < chroms.size();) {

@@ -10,6 +10,7 @@
 // Fields are separated by tabs (PSL); GNU sort's blank-separated fields coincide because PSL fields
 // hold no blanks.  The sort's locale is assumed to be C (Mando.py does not set one; under a UTF-8
 // collation the chromosome order could differ).
+#include "threads.h"
 #include <dirent.h>
 #include <sys/stat.h>
 
@@ -172,7 +173,7 @@ extern "C" int mando_list_roots(const char *dir, int32_t threads, char *names, i
     const std::string base = std::string(dir) + "/";
     // regular files only (is_file() follows symlinks, as stat does), sizes from the same stat
     std::vector<int64_t> fsize(ents.size(), -2);  // -2: not a regular file
-    int nt = threads > 0 ? threads : 16;
+    int nt = threads > 0 ? threads : mando::usable_threads();
     nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, ents.size() / 256 + 1));
     auto work = [&](int t) {
         struct stat st;

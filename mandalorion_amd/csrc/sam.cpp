@@ -5,6 +5,7 @@
 // including their output formatting: Python `repr` of the float accuracy, `','.join(...)+','` lists,
 // the strand flip by the `ts:A:-` tag and mappy.revcomp of '-' strand sequences.  Lines keep input
 // order.  Known reference crash cases (no cs tag in -m mode, zero-length alignment) return an error.
+#include "threads.h"
 #include <algorithm>
 #include <atomic>
 #include <charconv>
@@ -292,7 +293,7 @@ int mando_sam_to_psl(const char *sam_path, const char *psl_path, int32_t mando_m
     std::vector<string> out((size_t)n);
     std::vector<char> keep((size_t)n, 0);
     std::atomic<int> err{0};
-    int nth = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    int nth = threads > 0 ? threads : mando::usable_threads();
     nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n / 1024));
     auto work = [&](int64_t a0, int64_t a1) {
         std::vector<string_view> a;
