@@ -271,7 +271,10 @@ size_t kind_want(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     int64_t team = 1;
     if (seeded) team = std::max<int64_t>(1, std::min<int64_t>(mando::kMaxTeam, resident / std::max<int64_t>(1, n_groups)));
     const int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, resident / team));
-    return (size_t)(teams * team) * (size_t)mando::make_layout(caps).total;
+    // 1/8 of headroom: the next batch's slots are a little larger or smaller, and reallocating a ~150 GB
+    // workspace costs 3-4 s of hipMalloc (r04i)
+    const size_t b = (size_t)(teams * team) * (size_t)mando::make_layout(caps).total;
+    return b + b / 8;
 }
 
 // One POA launch over n_groups groups (d_gorder: their indices).  sp != null: the groups are -S
