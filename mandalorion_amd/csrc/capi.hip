@@ -227,8 +227,14 @@ mando::PoaCaps plan_caps(const mando_poa_params &p, int64_t max_first, int64_t m
     const int64_t w = p.band_b + (int64_t)(p.band_f * (float)max_len);
     const int64_t rowb = ((2 * w + 1 + 96) + 3) & ~int64_t(3);
     c.TBC = nc * rowb * (int64_t)(attempt + 1);
-    c.KPC = 3 * c.TBC / (attempt == 0 ? 2 : 1);
-    c.SVC = c.TBC / (attempt == 0 ? 2 : 1) * 3;
+    // predecessor bytes (multi-predecessor rows: one byte per cell for up to 4 predecessors) and spill
+    // planes (3 x 128 ints per row whose successor is >= 8 rows later) are sized for the common graph
+    // first: 0.75 byte and 0.25 int per traceback byte (a group that needs more -- deep branching,
+    // many far rows -- reports a capacity status and re-runs alone with 1.5 / 1.5, then 3 / 3).  The old
+    // first sizes (1.5 / 1.5) made a config-4 slot 46 MB and the narrow launch's one-group workspace
+    // 177 GB, whose hipMalloc took 4 s whenever it grew (r04i/j).
+    c.KPC = attempt == 0 ? 3 * c.TBC / 4 : (attempt == 1 ? 3 * c.TBC / 2 : 3 * c.TBC);
+    c.SVC = attempt == 0 ? c.TBC / 4 : (attempt == 1 ? 3 * c.TBC / 2 : 3 * c.TBC);
     // the kernel keeps its per-read usage counters in 32 bits
     const int64_t lim = int64_t(1) << 30;
     c.TBC = std::min(c.TBC, lim);
@@ -901,7 +907,8 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                               ctx->grp_off.as<int64_t>(), gb.as<int32_t>(), (int64_t)L.size(),
                               ctx->cons.as<uint8_t>(), ctx->cons_off.as<int64_t>(),
                               ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
-                              ctx->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &sp : nullptr, lane == 0,
+                              ctx->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &sp : nullptr,
+                              lane == 0 && attempt == 0,  // the batch's time runs from the first attempt
                               nk == 1, lane, kind, grant[kind]);
             if (rc) return rc;
             ctx->last_launches += 1;
@@ -925,6 +932,9 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                 return fail(MANDO_E_INTERNAL, "POA kernel reported status " + std::to_string(st[(size_t)g]) +
                                                   " for group " + std::to_string(g));
         }
+        if (!again.empty() && getenv("MANDO_WS_LOG"))
+            fprintf(stderr, "[mando ws] poa: %zu of %zu groups re-run with larger capacities (attempt %d)\n",
+                    again.size(), todo.size(), attempt + 1);
         todo.swap(again);
     }
     if (!todo.empty())

@@ -9,7 +9,7 @@ mkdir -p $D
 timeout -k 10 300 python -u -m pytest tests/test_define_ref.py -m gpu -x -q --timeout 300 --timeout-method thread > $D/pytest.log 2>&1
 rc=$?; tail -1 $D/pytest.log; [ $rc -eq 0 ] || exit $rc
 for w in config4 config3; do
-  for w2 in 0 1; do
+  for w2 in 1; do
     st=2; [ $w = config3 ] && st=4
     MANDO_POA_W2=$w2 timeout -k 10 900 python3 bench.py --no-cpu-baseline --workload $w --steps $st --warmup 1 > $D/bench_${w}_w$w2.json 2> $D/bench_${w}_w$w2.err || { echo "$w failed"; tail -5 $D/bench_${w}_w$w2.err; exit 1; }
     python3 -c "import json; d=json.load(open('$D/bench_${w}_w$w2.json')); c=d['config']; print('$w N=1 w2=$w2', round(d['value']), round(d['ms_per_step'], 1), c['steps_s'], c['phases_rank0_s'], c.get('full_output_equals_oracle'))"
