@@ -228,13 +228,16 @@ mando::PoaCaps plan_caps(const mando_poa_params &p, int64_t max_first, int64_t m
     const int64_t rowb = ((2 * w + 1 + 96) + 3) & ~int64_t(3);
     c.TBC = nc * rowb * (int64_t)(attempt + 1);
     // predecessor bytes (multi-predecessor rows: one byte per cell for up to 4 predecessors) and spill
-    // planes (3 x 128 ints per row whose successor is >= 8 rows later) are sized for the common graph
-    // first: 0.75 byte and 0.25 int per traceback byte (a group that needs more -- deep branching,
-    // many far rows -- reports a capacity status and re-runs alone with 1.5 / 1.5, then 3 / 3).  The old
-    // first sizes (1.5 / 1.5) made a config-4 slot 46 MB and the narrow launch's one-group workspace
-    // 177 GB, whose hipMalloc took 4 s whenever it grew (r04i/j).
-    c.KPC = attempt == 0 ? 3 * c.TBC / 4 : (attempt == 1 ? 3 * c.TBC / 2 : 3 * c.TBC);
-    c.SVC = attempt == 0 ? c.TBC / 4 : (attempt == 1 ? 3 * c.TBC / 2 : 3 * c.TBC);
+    // planes (3 x 128 ints per row whose successor is >= 8 rows later), per traceback byte: 0.75 byte
+    // and 1.5 ints first; a group that needs more reports a capacity status and re-runs alone with
+    // 1.5 / 1.5, then 3 / 3.  Measured on config 3 (profiles/r04_caps_sweep.txt): no group needs more than
+    // 0.75 predecessor bytes, but 9 need more than 0.75 spill ints (73 more than 0.5): any re-run is a
+    // second launch that pays its heaviest group's one-wave latency again (POA 1.26 -> 1.58 s), so the
+    // spill planes keep their room.
+    static const double kp0 = getenv("MANDO_KPC_FRAC") ? atof(getenv("MANDO_KPC_FRAC")) : 0.75;
+    static const double sv0 = getenv("MANDO_SVC_FRAC") ? atof(getenv("MANDO_SVC_FRAC")) : 1.5;
+    c.KPC = attempt == 0 ? (int64_t)(kp0 * (double)c.TBC) : (attempt == 1 ? 3 * c.TBC / 2 : 3 * c.TBC);
+    c.SVC = attempt == 0 ? (int64_t)(sv0 * (double)c.TBC) : (attempt == 1 ? 3 * c.TBC / 2 : 3 * c.TBC);
     // the kernel keeps its per-read usage counters in 32 bits
     const int64_t lim = int64_t(1) << 30;
     c.TBC = std::min(c.TBC, lim);
@@ -250,10 +253,11 @@ struct SeedPlan {
 };
 
 // waves per workgroup of wide launches: 2 (two-chunk rows split over two waves, poa_kernel.hip
-// row16w_half) with MANDO_POA_W2=1; one wave per group by default
+// row16w_half); MANDO_POA_W2=0 keeps one wave per group.  Measured (r04): config 5 -6.5 %, lone 8.5 kb
+// groups -7.5 % (of which -4 % is the 256-VGPR budget of the two-wave instantiation), configs 3 and 4 unchanged
 int poa_wide_waves() {
     const char *ev = getenv("MANDO_POA_W2");
-    return ev && ev[0] == '1' ? 2 : 1;
+    return ev && ev[0] == '0' ? 1 : 2;
 }
 
 // The workspace bytes a launch kind wants: one slot per resident workgroup (a team of them per -S
@@ -334,7 +338,8 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.dbg = 0;
     if (const char *ev = getenv("MANDO_POA_DBG")) a.dbg = atoi(ev);
     // wide launches: two-wave workgroups (the two-chunk rows split over both waves, poa_kernel.hip
-    // row16w_half) with MANDO_POA_W2=1; one wave per group by default
+    // row16w_half); MANDO_POA_W2=0 keeps one wave per group.  Measured (r04): config 5 -6.5 %, lone 8.5 kb
+// groups -7.5 % (of which -4 % is the 256-VGPR budget of the two-wave instantiation), configs 3 and 4 unchanged
     a.nw = caps.wide && !sp ? poa_wide_waves() : 1;
     // slots: enough one-wave workgroups to fill every CU several times, bounded by HBM budget.  With an
     // explicit budget (mando_ctx_set_poa_budget: the D driver's per-call plan, which knows the chunks in
