@@ -11,6 +11,8 @@
 // hold no blanks.  The sort's locale is assumed to be C (Mando.py does not set one; under a UTF-8
 // collation the chromosome order could differ).
 #include "threads.h"
+#include <fcntl.h>
+#include <unistd.h>
 #include <dirent.h>
 #include <sys/stat.h>
 
@@ -175,15 +177,19 @@ extern "C" int mando_list_roots(const char *dir, int32_t threads, char *names, i
     std::vector<int64_t> fsize(ents.size(), -2);  // -2: not a regular file
     int nt = threads > 0 ? threads : mando::usable_threads();
     nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, ents.size() / 256 + 1));
+    const int dfd = open(dir, O_RDONLY | O_DIRECTORY);
     auto work = [&](int t) {
         struct stat st;
-        for (size_t i = (size_t)t; i < ents.size(); i += (size_t)nt)
-            if (stat((base + ents[i]).c_str(), &st) == 0 && S_ISREG(st.st_mode)) fsize[i] = (int64_t)st.st_size;
+        for (size_t i = (size_t)t; i < ents.size(); i += (size_t)nt) {
+            const int r = dfd >= 0 ? fstatat(dfd, ents[i].c_str(), &st, 0) : stat((base + ents[i]).c_str(), &st);
+            if (r == 0 && S_ISREG(st.st_mode)) fsize[i] = (int64_t)st.st_size;
+        }
     };
     std::vector<std::thread> pool;
     for (int t = 1; t < nt; ++t) pool.emplace_back(work, t);
     work(0);
     for (auto &th : pool) th.join();
+    if (dfd >= 0) close(dfd);
     struct Root {
         std::string name;
         size_t clen;  // the chromosome is name[0, clen) (a length: short names move with their string)
@@ -198,12 +204,17 @@ extern "C" int mando_list_roots(const char *dir, int32_t threads, char *names, i
         const size_t cut = n.find(".psl");
         roots.push_back(Root{n.substr(0, cut), 0, 0, cut + 4 == n.size() ? fsize[i] : -1});
     }
-    // one root per name; the exact <root>.psl entry carries the size
-    std::sort(roots.begin(), roots.end(), [](const Root &a, const Root &b) {
-        return a.name != b.name ? a.name < b.name : a.size > b.size;
-    });
-    roots.erase(std::unique(roots.begin(), roots.end(), [](const Root &a, const Root &b) { return a.name == b.name; }),
-                roots.end());
+    // one root per name; the exact <root>.psl entry carries the size (only an entry with more after
+    // ".psl" -- a.psl.bak -- can repeat a root: the usual directory needs no de-duplication pass)
+    bool extra = false;
+    for (const Root &r : roots) extra |= r.size < 0;
+    if (extra) {
+        std::sort(roots.begin(), roots.end(), [](const Root &a, const Root &b) {
+            return a.name != b.name ? a.name < b.name : a.size > b.size;
+        });
+        roots.erase(std::unique(roots.begin(), roots.end(), [](const Root &a, const Root &b) { return a.name == b.name; }),
+                    roots.end());
+    }
     for (Root &r : roots) {
         const size_t t1 = r.name.find('~');
         if (t1 == std::string::npos) return MANDO_E_ARG;  // the reference's split('~')[1] raises

@@ -96,11 +96,9 @@ def _roots(out_tmp: str, sizes: dict | None = None) -> list[str]:
             continue
         if rc != 0:
             break
-        roots = [os.fsdecode(x) for x in names.raw[:nb.value].split(b"\0")[:-1]]
+        roots = names.raw[:nb.value].decode("utf-8", "surrogateescape").split("\0")[:-1]
         if sizes is not None:
-            for r, v in zip(roots, sz[:nr.value].tolist()):
-                if v >= 0:
-                    sizes[r] = v
+            sizes.update((r, v) for r, v in zip(roots, sz[:nr.value].tolist()) if v >= 0)
         return roots
     return _roots_py(out_tmp, sizes)
 
