@@ -372,7 +372,12 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         // a workspace that must grow gets 1/8 of headroom within the grant, so the next chunk's slightly
         // larger slots do not reallocate it
         const size_t need = (size_t)(teams * team * a.slot_bytes);
-        if (ws.bytes < need) {
+        if (ws.bytes < need && ws.bytes >= need - need / 4) {
+            // a workspace a little too small for this batch's (larger) slots: fewer slots rather than a
+            // reallocation (a hipMalloc of ~150 GB costs 3-4 s; a few per cent fewer slots at most turn a
+            // one-group grid into the persistent one, +25 % of the kernel)
+            teams = std::max<int64_t>(1, (int64_t)(ws.bytes / ((size_t)team * a.slot_bytes)));
+        } else if (ws.bytes < need) {
             ws.release();
             int rc0 = ws.ensure(std::min(budget, need + need / 8));
             if (rc0) return rc0;

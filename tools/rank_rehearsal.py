@@ -63,10 +63,11 @@ def main():
     ref = {f: sha(os.path.join(d, f)) for f in files} if all(os.path.exists(os.path.join(d, f)) for f in files) else None
     store: dict = {}
     out = {"ranks": n, "rank_s": {}, "payload_bytes": {}}
-    # warm the caches (files, device buffers) once, as the bench's warmup step does
-    define.define_isoforms(d, threads=threads, share=(1 % n, n))
     for r in list(range(1, n)) + [0]:
         comm = _Root(n, store) if r == 0 else _Recorder(r, n, store)
+        # each rank's warmup step (its own process in a real run: files cached, device buffers sized for
+        # its share), then the timed step
+        define.define_isoforms(d, threads=threads, share=(r, n))
         t0 = time.perf_counter()
         st = define.define_isoforms(d, threads=threads, comm=comm)
         out["rank_s"][r] = round(time.perf_counter() - t0, 4)
