@@ -188,8 +188,11 @@ inline int poa_qlds_bytes(int64_t max_len) {
 // Resident workgroups per CU for these arguments (LDS / register limited), at most cap.
 int poa_blocks_per_cu(const PoaKArgs &a, int cap);
 
-// dynamic LDS of a launch: the read's nibbles, plus the wide ring in a wide launch
+constexpr int kLeadBytes = 80;  // -S launches: the team leader's state after the read (poa_kernel.hip LeadState)
+// dynamic LDS of a launch: the read's nibbles, plus the wide ring in a wide launch, plus the leader's
+// state in a -S launch
 inline int poa_dyn_lds(const PoaKArgs &a) {
+    if (a.caps.seeded) return ((a.qlds + 15) & ~15) + kLeadBytes;
     // a wide launch's backtrack windows use 16 KB of it (poa_kernel.hip bt_tb_win / bt_kp_win)
     return a.caps.wide ? (a.qlds + kWideRingBytes > 16384 ? a.qlds + kWideRingBytes : 16384) : a.qlds;
 }

@@ -178,7 +178,12 @@ struct RowRec {
 constexpr int kKpPackMax = 4;
 __device__ __forceinline__ int kp_stride(int pn) { return pn <= kKpPackMax ? 1 : 3; }
 constexpr int kNodeKp3 = 1 << 30;  // backtrack window record: the row's predecessor bytes are 3 per cell
-constexpr int kDescBatch = 32;        // row descriptors staged in LDS per refill
+#ifndef MANDO_DESC_BATCH
+#define MANDO_DESC_BATCH 16
+#endif
+// row descriptors staged in LDS per refill: 16 rows (512 B) keep a narrow launch with reads up to ~4.6 kb
+// at 16 workgroups per CU (10,240 B of LDS each); 32 rows left it at 15 (r04)
+constexpr int kDescBatch = MANDO_DESC_BATCH;
 constexpr int kTbWin = 4096;          // backtrack: traceback byte window
 constexpr int kBtRows = 64;           // backtrack: rows per window
 constexpr int kKpWinMax = 2048;       // backtrack: predecessor-byte window (in the read buffer)
@@ -215,16 +220,22 @@ struct alignas(16) SharedState {
     gint *desc_full, *xpre_full, *qnode_full;
     uint64_t tmark;                 // MANDO_PROF: the last phase boundary of the -S path (prof_mark)
     int slot_idx;                   // this workgroup's workspace slot (one_group launches claim one)
-    // -S team leader (seeded launches): the group / read in progress between jobs (seeded_main)
-    struct {
-        int64_t r1, rd, cells;
-        uint64_t job;
-        int g, n, ng, st, pending, active, np, item, qlen;
-    } lead;
+
 };
 static_assert(sizeof(BtLds) <= sizeof(DpLds), "backtrack window must fit the DP scratch");
+// -S team leader (seeded launches): the group / read in progress between jobs (seeded_main).  In the
+// dynamic LDS after the read's buffer (poa_dyn_lds), so one-wave unseeded workgroups do not carry it.
+struct LeadState {
+    int64_t r1, rd, cells;
+    uint64_t job;
+    int g, n, ng, st, pending, active, np, item, qlen;
+};
+static_assert(sizeof(LeadState) <= kLeadBytes, "poa_kernel.h kLeadBytes");
 
 extern __shared__ __attribute__((aligned(16))) uint8_t g_qnib[];  // dynamic: the read, 4-bit codes
+__device__ __forceinline__ LeadState &lead_of(SharedState &sh) {
+    return *reinterpret_cast<LeadState *>(g_qnib + ((bcast0(sh.args.qlds) + 15) & ~15));
+}
 
 // Ring geometry by launch kind: RW = kChunk keeps the ring in the static LDS (col & 127); a wide launch
 // (RW = kWideRing) keeps 256-column rows at the start of the dynamic LDS and the read's nibbles after it.
@@ -2114,9 +2125,10 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
     int prv_r = -1, prv_beg = 0, prv_end = 0, prv_am = 0;
     // Descriptor batches reach LDS one batch ahead: lane l holds ints [4l, 4l+4) of the next 32 rows
     // (loaded while the current batch's rows run), so the batch refill waits on no HBM round trip.
-    static_assert(kDescBatch * kDescInts == 4 * kWave, "one int4 per lane per descriptor batch");
+    static_assert(kDescBatch * kDescInts <= 4 * kWave && kDescInts == 8, "one int4 per lane per descriptor batch");
+    const bool pl = (lane >> 1) < kDescBatch;  // the lanes that carry the batch (two per row)
     int4 pf = make_int4(0, 0, 0, 0);
-    if ((lane >> 1) < n) {
+    if (pl && (lane >> 1) < n) {
         const GLB int4 *g = reinterpret_cast<const GLB int4 *>(desc + 4 * lane);
         pf = make_int4(g->x, g->y, g->z, g->w);
     }
@@ -2126,10 +2138,10 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
     // Batches of kDescBatch rows; row 0 (the source row) is peeled off the first batch, so the row
     // loop carries no batch-boundary or first-row tests.
     for (int b0 = 0, i0 = 1; b0 < n - 1; b0 += kDescBatch, i0 = 0) {
-        if (b0 + (lane >> 1) < n) *reinterpret_cast<int4 *>(&sh.desc[0][0] + 4 * lane) = pf;
+        if (pl && b0 + (lane >> 1) < n) *reinterpret_cast<int4 *>(&sh.desc[0][0] + 4 * lane) = pf;
         {
             const int rn = b0 + kDescBatch;
-            if (rn < n && rn + (lane >> 1) < n) {
+            if (pl && rn < n && rn + (lane >> 1) < n) {
                 const GLB int4 *g = reinterpret_cast<const GLB int4 *>(desc + (int64_t)rn * kDescInts + 4 * lane);
                 pf = make_int4(g->x, g->y, g->z, g->w);
             }
@@ -3393,8 +3405,8 @@ template <class SC>
 __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int lane) {
     __builtin_amdgcn_s_setprio(kSerialPrio);
     for (;;) {
-        if (bcast0(sh.lead.pending)) {  // every window of the job has been claimed: wait for the rest
-            const int np = bcast0(sh.lead.np);
+        if (bcast0(lead_of(sh).pending)) {  // every window of the job has been claimed: wait for the rest
+            const int np = bcast0(lead_of(sh).np);
             int late = 0;
             {
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -3416,8 +3428,8 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
             }
             st = bcast0(st);
             const int64_t cells = uni64(readlane64(c, 0));
-            const int64_t rd = uni64(sh.lead.rd);
-            int n = bcast0(sh.lead.n), ng = bcast0(sh.lead.ng);
+            const int64_t rd = uni64(lead_of(sh).rd);
+            int n = bcast0(lead_of(sh).n), ng = bcast0(lead_of(sh).ng);
             if (st == kStOk) {
                 const uint8_t *q;
                 const int qlen = (int)read_len(sh, rd, q);
@@ -3432,19 +3444,19 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
                 }
             }
             if (lane == 0) {
-                sh.lead.pending = 0;
-                sh.lead.st = st;
-                sh.lead.n = n;
-                sh.lead.ng = ng;
-                sh.lead.cells += cells;
-                sh.lead.rd = rd + 1;
+                lead_of(sh).pending = 0;
+                lead_of(sh).st = st;
+                lead_of(sh).n = n;
+                lead_of(sh).ng = ng;
+                lead_of(sh).cells += cells;
+                lead_of(sh).rd = rd + 1;
             }
             wave_sync();
         }
-        if (bcast0(sh.lead.active)) {  // the group's next read, or its end
-            int st = bcast0(sh.lead.st);
-            int64_t rd = uni64(sh.lead.rd);
-            const int64_t r1 = uni64(sh.lead.r1);
+        if (bcast0(lead_of(sh).active)) {  // the group's next read, or its end
+            int st = bcast0(lead_of(sh).st);
+            int64_t rd = uni64(lead_of(sh).rd);
+            const int64_t r1 = uni64(lead_of(sh).r1);
             if (st == kStOk) {
                 const uint8_t *q = nullptr;
                 int64_t L = 0;
@@ -3458,12 +3470,12 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
                         if (np < 0 || np >= (1 << 20) - 1) st = kStInternal;
                     }
                     if (st == kStOk) {  // publish the read as the team's next job
-                        const int n = bcast0(sh.lead.n);
+                        const int n = bcast0(lead_of(sh).n);
                         prof_mark(sh, lane, -1);
                         build_desc(sh, n, lane, kRing);
                         wave_sync();
                         prof_mark(sh, lane, 0);
-                        const uint64_t job = sh.lead.job % 0xfffffeull + 1;
+                        const uint64_t job = lead_of(sh).job % 0xfffffeull + 1;
                         if (lane == 0) {  // every earlier job is done: nobody else writes the box now
                             __hip_atomic_store(&box->rd, rd, MANDO_RLX_AGENT);
                             __hip_atomic_store(&box->qlen, (int)L, MANDO_RLX_AGENT);
@@ -3475,12 +3487,12 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
                         team_release();  // the descriptors, tnode and the job's words, then the claim word
                         if (lane == 0) {
                             __hip_atomic_store(&box->claim, (job << 40) | ((uint64_t)np << 20), MANDO_RLX_AGENT);
-                            sh.lead.job = job;
-                            sh.lead.pending = 1;
-                            sh.lead.np = np;
-                            sh.lead.item = item;
-                            sh.lead.qlen = (int)L;
-                            sh.lead.rd = rd;
+                            lead_of(sh).job = job;
+                            lead_of(sh).pending = 1;
+                            lead_of(sh).np = np;
+                            lead_of(sh).item = item;
+                            lead_of(sh).qlen = (int)L;
+                            lead_of(sh).rd = rd;
                         }
                         wave_sync();
                         return 1;
@@ -3489,12 +3501,12 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
             }
             // the group is done (every read aligned, or a failure)
             int clen = 0;
-            const int g = bcast0(sh.lead.g);
+            const int g = bcast0(lead_of(sh).g);
             if (st == kStOk) {
                 const PoaRunArgs a = args_of(sh);
                 int64_t *prof = a.prof ? a.prof + (int64_t)blockIdx.x * kProfPhases : nullptr;
                 const uint64_t t6 = prof ? clock64() : 0;
-                const int n = bcast0(sh.lead.n);
+                const int n = bcast0(lead_of(sh).n);
                 int len = 0;
                 const int64_t cap = uni64(a.cons_off[g + 1]) - uni64(a.cons_off[g]);
                 st = consensus(sh, n, a.cons + uni64(a.cons_off[g]), cap, len, lane);
@@ -3505,8 +3517,8 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
                 const PoaRunArgs a = args_of(sh);
                 a.status[g] = st;
                 a.cons_len[g] = clen;
-                a.cells[g] = sh.lead.cells;
-                sh.lead.active = 0;
+                a.cells[g] = lead_of(sh).cells;
+                lead_of(sh).active = 0;
             }
             wave_sync();
             continue;
@@ -3550,15 +3562,15 @@ __device__ __forceinline__ int leader_advance(SharedState &sh, TeamBox *box, int
         }
         if (lane == 0) {
             if (first < r1) {
-                sh.lead.r1 = r1;
-                sh.lead.rd = first + 1;
-                sh.lead.cells = 0;
-                sh.lead.g = g;
-                sh.lead.n = n;
-                sh.lead.ng = 0;
-                sh.lead.st = st;
-                sh.lead.pending = 0;
-                sh.lead.active = 1;
+                lead_of(sh).r1 = r1;
+                lead_of(sh).rd = first + 1;
+                lead_of(sh).cells = 0;
+                lead_of(sh).g = g;
+                lead_of(sh).n = n;
+                lead_of(sh).ng = 0;
+                lead_of(sh).st = st;
+                lead_of(sh).pending = 0;
+                lead_of(sh).active = 1;
             } else {  // no read: an empty consensus
                 const PoaRunArgs a = args_of(sh);
                 a.status[g] = kStOk;
@@ -3578,9 +3590,9 @@ __device__ __forceinline__ void seeded_main(SharedState &sh, TeamBox *box, int m
         sc = SC{a.match, a.mismatch, a.o1, a.e1, a.o2, a.e2};
     }
     if (lane == 0) {
-        sh.lead.job = 0;
-        sh.lead.pending = 0;
-        sh.lead.active = 0;
+        lead_of(sh).job = 0;
+        lead_of(sh).pending = 0;
+        lead_of(sh).active = 0;
     }
     wave_sync();
     uint64_t last = 0;
@@ -3590,11 +3602,11 @@ __device__ __forceinline__ void seeded_main(SharedState &sh, TeamBox *box, int m
         int qlen = 0, item = 0, np = 0;
         if (member == 0) {
             if (!leader_advance<SC>(sh, box, lane)) return;
-            job = (uint64_t)uni64((int64_t)sh.lead.job);
-            rd = uni64(sh.lead.rd);
-            qlen = bcast0(sh.lead.qlen);
-            item = bcast0(sh.lead.item);
-            np = bcast0(sh.lead.np);
+            job = (uint64_t)uni64((int64_t)lead_of(sh).job);
+            rd = uni64(lead_of(sh).rd);
+            qlen = bcast0(lead_of(sh).qlen);
+            item = bcast0(lead_of(sh).item);
+            np = bcast0(lead_of(sh).np);
         } else {
             uint64_t c = 0;
             {
