@@ -292,13 +292,10 @@ def shard_plan(data: str, world: int) -> list:
     root_size: dict = {}
     roots = define._roots(os.path.join(data, "tmp_SS"), root_size)
     cost = define._size_costs(roots, root_size)
-    load = np.zeros(world)
-    cnt = [0] * world
-    for i in np.argsort(-cost, kind="stable"):
-        k = int(np.argmin(load))
-        load[k] += cost[i]
-        cnt[k] += 1
-    return [{"rank": k, "loci": cnt[k], "cost_share": float(load[k] / max(load.sum(), 1e-9))} for k in range(world)]
+    owner = define._lpt_owner(cost, world)
+    cnt = np.bincount(owner, minlength=world)
+    load = np.bincount(owner, weights=cost, minlength=world)
+    return [{"rank": k, "loci": int(cnt[k]), "cost_share": float(load[k] / max(load.sum(), 1e-9))} for k in range(world)]
 
 
 def fullsize_check(data: str, key: str):

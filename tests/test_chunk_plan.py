@@ -99,3 +99,19 @@ def test_write_big_appends_in_order(tmp_path):
         fh.write(b"tail")
     got = p.read_bytes()
     assert got == b"head" + a.tobytes() + b"tail"
+
+
+def test_shard_plan_balances_and_is_lpt_for_the_heaviest():
+    import numpy as np
+
+    rng = np.random.default_rng(3)
+    cost = rng.uniform(1, 100, 5000) ** 2
+    owner = define._lpt_owner(cost, 8, head=16)
+    load = np.bincount(owner, weights=cost, minlength=8)
+    assert load.max() / load.mean() < 1.001
+    # the heaviest 8 go to 8 different ranks, the 9th to the least-loaded of them
+    top = np.argsort(-cost, kind="stable")
+    assert sorted(owner[top[:8]]) == list(range(8))
+    assert owner[top[8]] == owner[top[7]]
+    assert define._lpt_owner(np.array([5.0, 1.0]), 4).tolist() == [0, 1]
+    assert define._lpt_owner(np.zeros(0), 3).size == 0
