@@ -50,6 +50,7 @@ EXPORTED = (
     "mando_comm_barrier",
     "mando_comm_destroy",
     "mando_pack_segments",
+    "mando_format_outputs",
     "mando_split_loci",
     "mando_list_roots",
     "mando_sam_to_psl",
@@ -212,6 +213,7 @@ def load(path: str | None = None):
         lib.mando_psl_to_gtf.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         lib.mando_quantify.argtypes = [_P, ctypes.c_int32] + [ctypes.c_char_p] * 4
         lib.mando_pack_segments.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, ctypes.c_int32]
+        lib.mando_format_outputs.argtypes = [_I64, _I64] + [_P] * 11 + [_P, _I64, _P, _P, _I64, _P, ctypes.c_int32]
         lib.mando_comm_init.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                         ctypes.c_double, _P]
         lib.mando_comm_backend.argtypes = [_P]
@@ -270,6 +272,47 @@ def pack_segments(srcs: list[np.ndarray], starts: np.ndarray, lens: np.ndarray, 
     rc_a = None if rc is None else np.ascontiguousarray(rc, dtype=np.int8)
     check(lib.mando_pack_segments(ptrs, ptr(sel_a), ptr(starts), ptr(lens), ptr(rc_a), n, ptr(out), ptr(off), threads))
     return out[:int(off[-1])], off
+
+
+def format_outputs(order: np.ndarray, mem_off: np.ndarray, counter0: int, cons: tuple | None, names: tuple | None,
+                   threads: int = 0) -> tuple[np.ndarray | None, np.ndarray | None]:
+    """The Isoform_Consensi.fasta and reads2isoforms.txt bytes of the isoforms `order` (see
+    mando_format_outputs).  cons = (srcs, sel, start, len, rc), names = (srcs, sel, start, len); either None
+    skips that file.  Returns (fasta bytes or None, r2i bytes or None) as uint8 arrays."""
+    lib = load()
+    order = np.ascontiguousarray(order, dtype=np.int64)
+    mem_off = np.ascontiguousarray(mem_off, dtype=np.int64)
+    keep = []
+
+    def srcs_of(lst):
+        k = [np.ascontiguousarray(s, dtype=np.uint8) for s in lst]
+        keep.extend(k)
+        return (ctypes.c_void_p * max(len(k), 1))(*[x.ctypes.data for x in k])
+
+    def arr(a, dt):
+        return None if a is None else np.ascontiguousarray(a, dtype=dt)
+
+    c = [None] * 5 if cons is None else [srcs_of(cons[0]), arr(cons[1], np.int16), arr(cons[2], np.int64),
+                                          arr(cons[3], np.int64), arr(cons[4], np.int8)]
+    n = [None] * 4 if names is None else [srcs_of(names[0]), arr(names[1], np.int16), arr(names[2], np.int64),
+                                           arr(names[3], np.int64)]
+    fl, rl = ctypes.c_int64(0), ctypes.c_int64(0)
+
+    def call(fa, fcap, r2, rcap):
+        return lib.mando_format_outputs(len(order), counter0, ptr(order), ptr(mem_off), c[0], ptr(c[1]),
+                                        ptr(c[2]), ptr(c[3]), ptr(c[4]), n[0], ptr(n[1]), ptr(n[2]), ptr(n[3]),
+                                        fa, fcap, ctypes.byref(fl), r2, rcap, ctypes.byref(rl), threads)
+
+    # sizes first (zero capacities: MANDO_E_CAP with both lengths set), then the fill
+    dummy = ctypes.c_uint8()
+    rc = call(ctypes.byref(dummy) if cons is not None else None, 0,
+              ctypes.byref(dummy) if names is not None else None, 0)
+    if rc not in (0, -4):
+        check(rc)
+    fasta = np.empty(max(fl.value, 1), np.uint8) if cons is not None else None
+    r2i = np.empty(max(rl.value, 1), np.uint8) if names is not None else None
+    check(call(ptr(fasta), fl.value if fasta is not None else 0, ptr(r2i), rl.value if r2i is not None else 0))
+    return (None if fasta is None else fasta[:fl.value]), (None if r2i is None else r2i[:rl.value])
 
 
 class Context:

@@ -1,0 +1,132 @@
+// writer.cpp — the bytes of the D module's two output files (defineIsoforms.py:155-166), formatted on host
+// threads straight from the payload arrays: one pass over the isoforms in output order, no per-member
+// intermediate arrays (the numpy form built ~20 segments-arrays of 10M entries for config 4's 10M records
+// and took ~0.5 s of the writer's critical path on rank 0).
+//   FASTA:            ">Isoform{k}_{m}\n" + consensus (reverse-complemented when rc) + "\n"
+//   reads2isoforms:   "{name}\tIsoform{k}_{m}\n" per member
+// with k = counter0 + 1 + (position in output order) and m = the isoform's member count.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/mando.h"
+#include "revcomp.h"
+#include "threads.h"
+
+namespace {
+
+int dec_len(int64_t x) {
+    int d = 1;
+    while (x >= 10) {
+        x /= 10;
+        ++d;
+    }
+    return d;
+}
+
+uint8_t *put_dec(uint8_t *p, int64_t x, int d) {
+    for (int i = d - 1; i >= 0; --i) {
+        p[i] = (uint8_t)('0' + x % 10);
+        x /= 10;
+    }
+    return p + d;
+}
+
+// "Isoform{k}_{m}"
+int label_len(int64_t k, int64_t m) { return 7 + dec_len(k) + 1 + dec_len(m); }
+uint8_t *put_label(uint8_t *p, int64_t k, int64_t m) {
+    memcpy(p, "Isoform", 7);
+    p = put_dec(p + 7, k, dec_len(k));
+    *p++ = '_';
+    return put_dec(p, m, dec_len(m));
+}
+
+template <class F>
+void parallel(int64_t n, int threads, F &&f) {
+    int nt = threads > 0 ? threads : mando::usable_threads();
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, n / 4096 + 1));
+    if (nt <= 1) {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t chunk = (n + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+        const int64_t a = t * chunk, b = std::min<int64_t>(n, a + chunk);
+        if (a < b) th.emplace_back(f, a, b);
+    }
+    for (auto &x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" int mando_format_outputs(int64_t n_iso, int64_t counter0, const int64_t *order, const int64_t *mem_off,
+                                    const uint8_t *const *cons_src, const int16_t *cons_sel, const int64_t *cons_start,
+                                    const int64_t *cons_len, const int8_t *cons_rc, const uint8_t *const *name_src,
+                                    const int16_t *name_sel, const int64_t *name_start, const int64_t *name_len,
+                                    uint8_t *fasta, int64_t fasta_cap, int64_t *fasta_len, uint8_t *r2i,
+                                    int64_t r2i_cap, int64_t *r2i_len, int32_t threads) {
+    if (n_iso < 0 || !order || !mem_off || (fasta && (!fasta_len || !cons_src || !cons_start || !cons_len)) ||
+        (r2i && (!r2i_len || !name_src || !name_start || !name_len)))
+        return MANDO_E_ARG;
+    // pass 1: each isoform's bytes in both files (per output position), then offsets by a prefix sum
+    std::vector<int64_t> fo((size_t)n_iso + 1, 0), ro((size_t)n_iso + 1, 0);
+    parallel(n_iso, threads, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            const int64_t g = order[i], m = mem_off[g + 1] - mem_off[g];
+            const int L = label_len(counter0 + 1 + i, m);
+            if (fasta) fo[(size_t)i + 1] = L + 2 + cons_len[g] + 1;
+            if (r2i) {
+                int64_t s = 0;
+                for (int64_t j = mem_off[g]; j < mem_off[g + 1]; ++j) s += name_len[j];
+                ro[(size_t)i + 1] = s + m * (L + 2);
+            }
+        }
+    });
+    for (int64_t i = 0; i < n_iso; ++i) {
+        fo[(size_t)i + 1] += fo[(size_t)i];
+        ro[(size_t)i + 1] += ro[(size_t)i];
+    }
+    if (fasta) *fasta_len = fo[(size_t)n_iso];
+    if (r2i) *r2i_len = ro[(size_t)n_iso];
+    if ((fasta && fo[(size_t)n_iso] > fasta_cap) || (r2i && ro[(size_t)n_iso] > r2i_cap)) return MANDO_E_CAP;
+    const mando::CompTable &comp = mando::comp_table();
+    // pass 2: fill, isoform ranges on threads
+    parallel(n_iso, threads, [&](int64_t a, int64_t b) {
+        uint8_t lab[64];
+        for (int64_t i = a; i < b; ++i) {
+            const int64_t g = order[i], m = mem_off[g + 1] - mem_off[g];
+            const int L = (int)(put_label(lab, counter0 + 1 + i, m) - lab);
+            if (fasta) {
+                uint8_t *p = fasta + fo[(size_t)i];
+                *p++ = '>';
+                memcpy(p, lab, (size_t)L);
+                p += L;
+                *p++ = '\n';
+                const uint8_t *s = cons_src[cons_sel ? cons_sel[g] : 0] + cons_start[g];
+                const int64_t n = cons_len[g];
+                if (cons_rc && cons_rc[g]) {
+                    for (int64_t k = 0; k < n; ++k) p[k] = comp.t[s[n - 1 - k]];
+                } else {
+                    memcpy(p, s, (size_t)n);
+                }
+                p[n] = '\n';
+            }
+            if (r2i) {
+                uint8_t *p = r2i + ro[(size_t)i];
+                for (int64_t j = mem_off[g]; j < mem_off[g + 1]; ++j) {
+                    const int64_t n = name_len[j];
+                    memcpy(p, name_src[name_sel ? name_sel[j] : 0] + name_start[j], (size_t)n);
+                    p += n;
+                    *p++ = '\t';
+                    memcpy(p, lab, (size_t)L);
+                    p += L;
+                    *p++ = '\n';
+                }
+            }
+        }
+    });
+    return MANDO_OK;
+}

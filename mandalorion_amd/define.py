@@ -223,96 +223,6 @@ class Assembly:
         return seqs, so, grp
 
 
-def _label_lines(k: np.ndarray, m: np.ndarray, first: int) -> tuple[np.ndarray, np.ndarray]:
-    """The bytes of the lines chr(first) + 'Isoform{k}_{m}' + '\n' for every (k, m) (non-negative), back
-    to back, and their lengths -- vectorised (a Python f-string per isoform took 0.45 s for config 4's
-    400,000 isoforms on the writer's critical path)."""
-    k = np.asarray(k, dtype=np.int64)
-    m = np.asarray(m, dtype=np.int64)
-    n = len(k)
-
-    def ndig(x):
-        d = np.ones(len(x), dtype=np.int64)
-        p = 10
-        for _ in range(18):
-            d += x >= p
-            p *= 10
-        return d
-
-    dk, dm = ndig(k), ndig(m)
-    pre = b"_Isoform"  # the first byte is replaced by `first`
-    ln = len(pre) + dk + 1 + dm + 1
-    end = np.cumsum(ln)
-    st = end - ln
-    out = np.empty(int(end[-1]) if n else 0, dtype=np.uint8)
-    if not n:
-        return out, ln
-    for j, c in enumerate(pre):
-        out[st + j] = c
-    out[st] = first
-
-    def put(x, dx, at):  # decimal digits of x, most significant first, at byte offsets `at`
-        for j in range(int(dx.max())):
-            live = j < dx
-            p = np.power(10, np.maximum(dx - 1 - j, 0))
-            out[(at + j)[live]] = (ord("0") + (x // p) % 10)[live]
-
-    put(k, dk, st + len(pre))
-    out[st + len(pre) + dk] = ord("_")
-    put(m, dm, st + len(pre) + dk + 1)
-    out[end - 1] = ord("\n")
-    return out, ln
-
-
-def _fasta_and_r2i(name_src, name_sel, name_start, name_len, mem_off, cons_src, cons_sel, cons_start, cons_len,
-                   cons_rc, counter0: int = 0, fasta_part: bool = True, r2i_part: bool = True):
-    """Isoform_Consensi.fasta and reads2isoforms.txt bytes for isoforms in output order
-    (defineIsoforms.py:155-166): '>Isoform{k}_{n}\n{consensus}\n' and '{name}\tIsoform{k}_{n}\n'.
-    Consensi and names are byte segments of several sources (locus texts, POA outputs), gathered once."""
-    n_iso = len(mem_off) - 1
-    n_mem = np.diff(mem_off)
-    head, hl = _label_lines(np.arange(counter0 + 1, counter0 + 1 + n_iso, dtype=np.int64), n_mem, ord(">"))
-    suf = head.copy()
-    suf[np.cumsum(hl) - hl] = ord("\t")
-    aux = np.concatenate([head, np.frombuffer(b"\n", np.uint8), suf])
-    hs = np.zeros(n_iso, dtype=np.int64)
-    if n_iso:
-        hs[1:] = np.cumsum(hl)[:-1]
-    nl_pos = len(head)
-    sl = hl.copy()  # "\t" + label + "\n" has the same length as ">" + label + "\n"
-    ss = nl_pos + 1 + hs
-    fasta = r2i = None
-    if fasta_part:
-        fasta = _fasta_bytes(aux, hs, hl, nl_pos, cons_src, cons_sel, cons_start, cons_len, cons_rc)
-    if not r2i_part:
-        return fasta, None
-    # reads2isoforms: [name (its source)] [suffix (aux)] per member
-    m = int(mem_off[-1])
-    iso_of_mem = np.repeat(np.arange(n_iso), n_mem)
-    sel = np.empty(2 * m, dtype=np.int16)
-    st = np.empty(2 * m, dtype=np.int64)
-    ln = np.empty(2 * m, dtype=np.int64)
-    sel[0::2], st[0::2], ln[0::2] = 1 + np.asarray(name_sel), name_start, name_len
-    sel[1::2], st[1::2], ln[1::2] = 0, ss[iso_of_mem], sl[iso_of_mem]
-    r2i, _ = _lib.pack_segments([aux] + list(name_src), st, ln, sel=sel)
-    return fasta, r2i
-
-
-def _fasta_bytes(aux, hs, hl, nl_pos, cons_src, cons_sel, cons_start, cons_len, cons_rc):
-    n_iso = len(hs)
-    # FASTA: [header (aux)] [consensus (its source)] ["\n" (aux)] per isoform; sources: 0 aux, 1.. cons
-    srcs = [aux] + list(cons_src)
-    sel = np.empty(3 * n_iso, dtype=np.int16)
-    st = np.empty(3 * n_iso, dtype=np.int64)
-    ln = np.empty(3 * n_iso, dtype=np.int64)
-    rc = np.zeros(3 * n_iso, dtype=np.int8)
-    sel[0::3], st[0::3], ln[0::3] = 0, hs, hl
-    sel[1::3], st[1::3], ln[1::3], rc[1::3] = 1 + np.asarray(cons_sel), cons_start, cons_len, cons_rc
-    sel[2::3], st[2::3], ln[2::3] = 0, nl_pos, 1
-    fasta, _ = _lib.pack_segments(srcs, st, ln, sel=sel, rc=rc)
-    return fasta
-
-
 # inputs of more than _TWO_CHUNK_BYTES of locus text run in chunks of at most this many bytes: a 4 GiB chunk's
 # text, clustering scratch and gathered reads (about 7x the text, three chunks in flight) leave room for
 # both POA launch kinds' one-group grids in a 288 GB HBM (config 4 on one GPU; r04e: 8 GiB chunks left
@@ -754,24 +664,15 @@ def _close_all(cluster_futs, poa_futs) -> None:
 def _write_payload(payload: dict, fa, r2, counter0: int) -> int:
     """Appends a payload's isoforms to both files in output order (sorted roots x IsoDict order,
     defineIsoforms.py:155-166), numbering from counter0 + 1; returns the isoform count.  fa or r2 None:
-    that file is skipped (reads2isoforms needs only the clustering, so one rank writes it ahead)."""
+    that file is skipped (reads2isoforms needs only the clustering, so one rank writes it ahead).  The
+    bytes come from mando_format_outputs, one threaded pass straight over the payload arrays."""
     order = np.argsort(payload["iso_root"], kind="stable")
-    mo = payload["mem_off"]
-    cnt = np.diff(mo)[order]
-    new_off = np.zeros(len(order) + 1, dtype=np.int64)
-    np.cumsum(cnt, out=new_off[1:])
-    # member rows in output order: for each isoform in `order`, mo[i] .. mo[i+1]-1
-    midx = (np.repeat(mo[:-1][order] - new_off[:-1], cnt) + np.arange(int(new_off[-1]))
-            if len(order) else np.zeros(0, np.int64))
+    cons = names = None
     if fa is not None:
-        cons = [payload[k][order] for k in ("c_sel", "c_start", "c_len", "c_rc")]
-    else:
-        cons = [None] * 4
-    fasta, r2i = _fasta_and_r2i(payload["name_src"], payload["n_sel"][midx] if r2 is not None else None,
-                                payload["n_start"][midx] if r2 is not None else None,
-                                payload["n_len"][midx] if r2 is not None else None, new_off,
-                                payload.get("cons_src"), *cons, counter0=counter0, fasta_part=fa is not None,
-                                r2i_part=r2 is not None)
+        cons = (payload["cons_src"], payload["c_sel"], payload["c_start"], payload["c_len"], payload["c_rc"])
+    if r2 is not None:
+        names = (payload["name_src"], payload["n_sel"], payload["n_start"], payload["n_len"])
+    fasta, r2i = _lib.format_outputs(order, payload["mem_off"], counter0, cons, names)
     if fa is not None:
         _write_big(fa, fasta)
     if r2 is not None:

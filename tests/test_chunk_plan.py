@@ -77,15 +77,50 @@ def test_metrics_line():
     assert define.metrics({"t_total": 1.0, "records": 0})["gcups"] is None
 
 
-def test_isoform_label_lines():
+def _py_outputs(order, mem_off, counter0, cons, names):
+    """defineIsoforms.py:155-166 written the plain way: one f-string per isoform and per member."""
+    comp = bytes.maketrans(b"ACGTNacgtn", b"TGCANtgcan")
+    fa, r2 = [], []
+    for i, g in enumerate(order):
+        lab = f"Isoform{counter0 + 1 + i}_{mem_off[g + 1] - mem_off[g]}".encode()
+        srcs, sel, st, ln, rc = cons
+        c = bytes(srcs[sel[g]][st[g]:st[g] + ln[g]])
+        fa.append(b">" + lab + b"\n" + (c[::-1].translate(comp) if rc[g] else c) + b"\n")
+        srcs, sel, st, ln = names
+        for j in range(mem_off[g], mem_off[g + 1]):
+            r2.append(bytes(srcs[sel[j]][st[j]:st[j] + ln[j]]) + b"\t" + lab + b"\n")
+    return b"".join(fa), b"".join(r2)
+
+
+@pytest.mark.parametrize("n_iso,counter0", [(0, 0), (1, 0), (37, 9), (20000, 99995)])
+def test_format_outputs_matches_the_per_isoform_loop(n_iso, counter0):
     import numpy as np
 
-    k = np.array([1, 9, 10, 99, 100, 12345, 7, 10**12])
-    m = np.array([1, 0, 10, 123, 5, 2, 99999, 3])
-    b, ln = define._label_lines(k, m, ord(">"))
-    assert b.tobytes() == "".join(f">Isoform{a}_{c}\n" for a, c in zip(k, m)).encode()
-    assert list(ln) == [len(f">Isoform{a}_{c}\n") for a, c in zip(k, m)]
-    assert define._label_lines(np.zeros(0, np.int64), np.zeros(0, np.int64), 9)[0].size == 0
+    from mandalorion_amd import _lib
+
+    rng = np.random.default_rng(n_iso)
+    text = [rng.choice(np.frombuffer(b"ACGTNacgtn", np.uint8), 5000), rng.choice(np.frombuffer(b"ACGT", np.uint8), 300)]
+    m = rng.integers(0, 12, n_iso)
+    mem_off = np.zeros(n_iso + 1, np.int64)
+    np.cumsum(m, out=mem_off[1:])
+    c_sel = rng.integers(0, 2, n_iso).astype(np.int16)
+    c_len = rng.integers(0, 200, n_iso)
+    c_start = np.array([rng.integers(0, len(text[s]) - ln + 1) for s, ln in zip(c_sel, c_len)], np.int64)
+    c_rc = rng.integers(0, 2, n_iso).astype(np.int8)
+    nm = int(mem_off[-1])
+    n_sel = rng.integers(0, 2, nm).astype(np.int16)
+    n_len = rng.integers(1, 40, nm)
+    n_start = np.array([rng.integers(0, len(text[s]) - ln + 1) for s, ln in zip(n_sel, n_len)], np.int64)
+    order = rng.permutation(n_iso)
+    cons = (text, c_sel, c_start, c_len, c_rc)
+    names = (text, n_sel, n_start, n_len)
+    fa, r2 = _lib.format_outputs(order, mem_off, counter0, cons, names, threads=4)
+    want = _py_outputs(order, mem_off, counter0, cons, names)
+    assert fa.tobytes() == want[0] and r2.tobytes() == want[1]
+    fa2, none = _lib.format_outputs(order, mem_off, counter0, cons, None)
+    assert none is None and fa2.tobytes() == want[0]
+    none, r22 = _lib.format_outputs(order, mem_off, counter0, None, names, threads=1)
+    assert none is None and r22.tobytes() == want[1]
 
 
 def test_write_big_appends_in_order(tmp_path):
