@@ -248,20 +248,29 @@ int mando_pack_segments(const uint8_t *const *src, const int8_t *sel, const int6
                         const int64_t *lens, const int8_t *rc, int64_t n, uint8_t *out,
                         const int64_t *out_off, int32_t threads);
 
-/* The D module's two output files for n_iso isoforms, numbered counter0+1.. in output order
- * (replaces the per-isoform write loop of defineIsoforms.py:155-166):
+/* The D module's two output files for n_iso isoforms (replaces the per-isoform write loop of
+ * defineIsoforms.py:155-166):
  *   fasta: ">Isoform{k}_{m}\n{consensus}\n"        r2i: "{name}\tIsoform{k}_{m}\n" per member
- * isoform i of the output is payload isoform g = order[i]; its members are mem_off[g]..mem_off[g+1]-1
- * (m of them).  consensus g = cons_src[cons_sel[g]] + cons_start[g], cons_len[g] bytes, reverse-
- * complemented when cons_rc && cons_rc[g]; name j = name_src[name_sel[j]] + name_start[j], name_len[j]
- * bytes (a NULL selector means source 0).  fasta or r2i NULL: that file is skipped.  Sets *fasta_len /
- * *r2i_len; MANDO_E_CAP (sizes still set, nothing written) when a capacity is too small. */
-int mando_format_outputs(int64_t n_iso, int64_t counter0, const int64_t *order, const int64_t *mem_off,
-                         const uint8_t *const *cons_src, const int16_t *cons_sel, const int64_t *cons_start,
-                         const int64_t *cons_len, const int8_t *cons_rc, const uint8_t *const *name_src,
-                         const int16_t *name_sel, const int64_t *name_start, const int64_t *name_len,
-                         uint8_t *fasta, int64_t fasta_cap, int64_t *fasta_len, uint8_t *r2i, int64_t r2i_cap,
-                         int64_t *r2i_len, int32_t threads);
+ * isoform i of the output is payload isoform g = order[i], numbered k = iso_k[i] (iso_k NULL: counter0+1+i);
+ * its members are mem_off[g]..mem_off[g+1]-1 (m of them).  consensus g = cons_src[cons_sel[g]] +
+ * cons_start[g], cons_len[g] bytes, reverse-complemented when cons_rc && cons_rc[g]; name j =
+ * name_src[name_sel[j]] + name_start[j], name_len[j] bytes (a NULL selector means source 0).  fasta or
+ * r2i NULL: that file is skipped.  Sets *fasta_len / *r2i_len and, when non-NULL, fasta_off / r2i_off
+ * (n_iso + 1 entries: where output isoform i starts); MANDO_E_CAP (sizes and offsets still set, nothing
+ * written) when a capacity is too small. */
+int mando_format_outputs(int64_t n_iso, int64_t counter0, const int64_t *iso_k, const int64_t *order,
+                         const int64_t *mem_off, const uint8_t *const *cons_src, const int16_t *cons_sel,
+                         const int64_t *cons_start, const int64_t *cons_len, const int8_t *cons_rc,
+                         const uint8_t *const *name_src, const int16_t *name_sel, const int64_t *name_start,
+                         const int64_t *name_len, uint8_t *fasta, int64_t fasta_cap, int64_t *fasta_len,
+                         uint8_t *r2i, int64_t r2i_cap, int64_t *r2i_len, int64_t *fasta_off, int64_t *r2i_off,
+                         int32_t threads);
+
+/* Block i of buf (src_off[i], len[i] bytes) written at file offset dst_off[i] of the open descriptor fd
+ * with pwrite (the per-root blocks a rank places into the shared output files; neighbouring blocks
+ * contiguous on both sides go out as one call).  threads <= 0: up to 8. */
+int mando_write_blocks(int32_t fd, const uint8_t *buf, const int64_t *src_off, const int64_t *dst_off,
+                       const int64_t *len, int64_t n, int32_t threads);
 
 /* PSL ingest + locus split: `sort -k 14,14 -k 16,17n` (C locale) of the clean
  * PSL (Mando.py:343-349) when sort_lines != 0, optional write of the sorted file, then

@@ -51,6 +51,7 @@ EXPORTED = (
     "mando_comm_destroy",
     "mando_pack_segments",
     "mando_format_outputs",
+    "mando_write_blocks",
     "mando_split_loci",
     "mando_list_roots",
     "mando_sam_to_psl",
@@ -213,7 +214,9 @@ def load(path: str | None = None):
         lib.mando_psl_to_gtf.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         lib.mando_quantify.argtypes = [_P, ctypes.c_int32] + [ctypes.c_char_p] * 4
         lib.mando_pack_segments.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, ctypes.c_int32]
-        lib.mando_format_outputs.argtypes = [_I64, _I64] + [_P] * 11 + [_P, _I64, _P, _P, _I64, _P, ctypes.c_int32]
+        lib.mando_format_outputs.argtypes = [_I64, _I64] + [_P] * 12 + [_P, _I64, _P, _P, _I64, _P, _P, _P,
+                                                                         ctypes.c_int32]
+        lib.mando_write_blocks.argtypes = [ctypes.c_int32, _P, _P, _P, _P, _I64, ctypes.c_int32]
         lib.mando_comm_init.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                         ctypes.c_double, _P]
         lib.mando_comm_backend.argtypes = [_P]
@@ -275,13 +278,18 @@ def pack_segments(srcs: list[np.ndarray], starts: np.ndarray, lens: np.ndarray, 
 
 
 def format_outputs(order: np.ndarray, mem_off: np.ndarray, counter0: int, cons: tuple | None, names: tuple | None,
-                   threads: int = 0) -> tuple[np.ndarray | None, np.ndarray | None]:
+                   threads: int = 0, iso_k: np.ndarray | None = None, offsets: bool = False):
     """The Isoform_Consensi.fasta and reads2isoforms.txt bytes of the isoforms `order` (see
     mando_format_outputs).  cons = (srcs, sel, start, len, rc), names = (srcs, sel, start, len); either None
-    skips that file.  Returns (fasta bytes or None, r2i bytes or None) as uint8 arrays."""
+    skips that file.  iso_k: each output isoform's number (default counter0 + 1 + position).  Returns
+    (fasta bytes or None, r2i bytes or None) as uint8 arrays, plus both files' per-isoform start offsets
+    (n + 1 entries each) when offsets."""
     lib = load()
     order = np.ascontiguousarray(order, dtype=np.int64)
     mem_off = np.ascontiguousarray(mem_off, dtype=np.int64)
+    kk = None if iso_k is None else np.ascontiguousarray(iso_k, dtype=np.int64)
+    if kk is not None and len(kk) != len(order):
+        raise ValueError("format_outputs: iso_k and order differ in length")
     keep = []
 
     def srcs_of(lst):
@@ -297,11 +305,14 @@ def format_outputs(order: np.ndarray, mem_off: np.ndarray, counter0: int, cons: 
     n = [None] * 4 if names is None else [srcs_of(names[0]), arr(names[1], np.int16), arr(names[2], np.int64),
                                            arr(names[3], np.int64)]
     fl, rl = ctypes.c_int64(0), ctypes.c_int64(0)
+    fo = np.empty(len(order) + 1, np.int64)
+    ro = np.empty(len(order) + 1, np.int64)
 
     def call(fa, fcap, r2, rcap):
-        return lib.mando_format_outputs(len(order), counter0, ptr(order), ptr(mem_off), c[0], ptr(c[1]),
+        return lib.mando_format_outputs(len(order), counter0, ptr(kk), ptr(order), ptr(mem_off), c[0], ptr(c[1]),
                                         ptr(c[2]), ptr(c[3]), ptr(c[4]), n[0], ptr(n[1]), ptr(n[2]), ptr(n[3]),
-                                        fa, fcap, ctypes.byref(fl), r2, rcap, ctypes.byref(rl), threads)
+                                        fa, fcap, ctypes.byref(fl), r2, rcap, ctypes.byref(rl), ptr(fo), ptr(ro),
+                                        threads)
 
     # sizes first (zero capacities: MANDO_E_CAP with both lengths set), then the fill
     dummy = ctypes.c_uint8()
@@ -312,7 +323,21 @@ def format_outputs(order: np.ndarray, mem_off: np.ndarray, counter0: int, cons: 
     fasta = np.empty(max(fl.value, 1), np.uint8) if cons is not None else None
     r2i = np.empty(max(rl.value, 1), np.uint8) if names is not None else None
     check(call(ptr(fasta), fl.value if fasta is not None else 0, ptr(r2i), rl.value if r2i is not None else 0))
-    return (None if fasta is None else fasta[:fl.value]), (None if r2i is None else r2i[:rl.value])
+    out = (None if fasta is None else fasta[:fl.value]), (None if r2i is None else r2i[:rl.value])
+    return out + (fo, ro) if offsets else out
+
+
+def write_blocks(fd: int, buf: np.ndarray, src_off: np.ndarray, dst_off: np.ndarray, length: np.ndarray,
+                 threads: int = 0) -> None:
+    """pwrite block i of buf (src_off[i], length[i] bytes) at offset dst_off[i] of fd (mando_write_blocks)."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    a = [np.ascontiguousarray(x, dtype=np.int64) for x in (src_off, dst_off, length)]
+    if not (len(a[0]) == len(a[1]) == len(a[2])):
+        raise ValueError("write_blocks: offset and length arrays differ in length")
+    if len(a[0]) and int((a[0] + a[2]).max()) > buf.size:
+        raise ValueError("write_blocks: a block runs past the buffer")
+    check(load().mando_write_blocks(int(fd), ptr(buf) if buf.size else None, ptr(a[0]), ptr(a[1]), ptr(a[2]),
+                                    len(a[0]), threads))
 
 
 class Context:

@@ -4,14 +4,19 @@
 // and took ~0.5 s of the writer's critical path on rank 0).
 //   FASTA:            ">Isoform{k}_{m}\n" + consensus (reverse-complemented when rc) + "\n"
 //   reads2isoforms:   "{name}\tIsoform{k}_{m}\n" per member
-// with k = counter0 + 1 + (position in output order) and m = the isoform's member count.
+// with k = counter0 + 1 + (position in output order), or iso_k[position], and m = the isoform's member
+// count.
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <cerrno>
 #include <cstdint>
 #include <cstring>
 #include <thread>
 #include <vector>
 
-#include "../../include/mando.h"
+#include "internal.h"
 #include "revcomp.h"
 #include "threads.h"
 
@@ -62,22 +67,30 @@ void parallel(int64_t n, int threads, F &&f) {
 
 }  // namespace
 
-extern "C" int mando_format_outputs(int64_t n_iso, int64_t counter0, const int64_t *order, const int64_t *mem_off,
+extern "C" int mando_format_outputs(int64_t n_iso, int64_t counter0, const int64_t *iso_k, const int64_t *order,
+                                    const int64_t *mem_off,
                                     const uint8_t *const *cons_src, const int16_t *cons_sel, const int64_t *cons_start,
                                     const int64_t *cons_len, const int8_t *cons_rc, const uint8_t *const *name_src,
                                     const int16_t *name_sel, const int64_t *name_start, const int64_t *name_len,
                                     uint8_t *fasta, int64_t fasta_cap, int64_t *fasta_len, uint8_t *r2i,
-                                    int64_t r2i_cap, int64_t *r2i_len, int32_t threads) {
+                                    int64_t r2i_cap, int64_t *r2i_len, int64_t *fasta_off, int64_t *r2i_off,
+                                    int32_t threads) {
     if (n_iso < 0 || !order || !mem_off || (fasta && (!fasta_len || !cons_src || !cons_start || !cons_len)) ||
         (r2i && (!r2i_len || !name_src || !name_start || !name_len)))
         return MANDO_E_ARG;
     // pass 1: each isoform's bytes in both files (per output position), then offsets by a prefix sum
-    std::vector<int64_t> fo((size_t)n_iso + 1, 0), ro((size_t)n_iso + 1, 0);
+    std::vector<int64_t> fo_own, ro_own;
+    if (!fasta_off) fo_own.resize((size_t)n_iso + 1);
+    if (!r2i_off) ro_own.resize((size_t)n_iso + 1);
+    int64_t *fo = fasta_off ? fasta_off : fo_own.data(), *ro = r2i_off ? r2i_off : ro_own.data();
+    fo[0] = ro[0] = 0;
+    auto num = [&](int64_t i) { return iso_k ? iso_k[i] : counter0 + 1 + i; };
     parallel(n_iso, threads, [&](int64_t a, int64_t b) {
         for (int64_t i = a; i < b; ++i) {
             const int64_t g = order[i], m = mem_off[g + 1] - mem_off[g];
-            const int L = label_len(counter0 + 1 + i, m);
-            if (fasta) fo[(size_t)i + 1] = L + 2 + cons_len[g] + 1;
+            const int L = label_len(num(i), m);
+            fo[(size_t)i + 1] = fasta ? L + 2 + cons_len[g] + 1 : 0;
+            ro[(size_t)i + 1] = 0;
             if (r2i) {
                 int64_t s = 0;
                 for (int64_t j = mem_off[g]; j < mem_off[g + 1]; ++j) s += name_len[j];
@@ -98,7 +111,7 @@ extern "C" int mando_format_outputs(int64_t n_iso, int64_t counter0, const int64
         uint8_t lab[64];
         for (int64_t i = a; i < b; ++i) {
             const int64_t g = order[i], m = mem_off[g + 1] - mem_off[g];
-            const int L = (int)(put_label(lab, counter0 + 1 + i, m) - lab);
+            const int L = (int)(put_label(lab, num(i), m) - lab);
             if (fasta) {
                 uint8_t *p = fasta + fo[(size_t)i];
                 *p++ = '>';
@@ -128,5 +141,55 @@ extern "C" int mando_format_outputs(int64_t n_iso, int64_t counter0, const int64
             }
         }
     });
+    return MANDO_OK;
+}
+
+extern "C" int mando_write_blocks(int32_t fd, const uint8_t *buf, const int64_t *src_off, const int64_t *dst_off,
+                                  const int64_t *len, int64_t n, int32_t threads) {
+    if (fd < 0 || n < 0 || (n && (!buf || !src_off || !dst_off || !len))) return MANDO_E_ARG;
+    // neighbouring blocks that are contiguous on both sides become one pwrite
+    struct Piece {
+        int64_t src, dst, n;
+    };
+    std::vector<Piece> pc;
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (len[i] < 0) return MANDO_E_ARG;
+        if (len[i] == 0) continue;
+        total += len[i];
+        if (!pc.empty() && pc.back().src + pc.back().n == src_off[i] && pc.back().dst + pc.back().n == dst_off[i])
+            pc.back().n += len[i];
+        else
+            pc.push_back({src_off[i], dst_off[i], len[i]});
+    }
+    // threads take runs of pieces of about equal bytes (the page-cache copy is the cost)
+    int nt = threads > 0 ? threads : std::min(8, mando::usable_threads());
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>(nt, total >> 22));
+    std::vector<size_t> cut{0};
+    for (size_t q = 0, acc = 0; q < pc.size(); ++q) {
+        acc += (size_t)pc[q].n;
+        if (acc * nt >= (size_t)total * cut.size() && cut.size() < (size_t)nt) cut.push_back(q + 1);
+    }
+    cut.push_back(pc.size());
+    std::atomic<int> err{0};
+    auto work = [&](size_t a, size_t b) {
+        for (size_t q = a; q < b && !err.load(std::memory_order_relaxed); ++q) {
+            int64_t done = 0;
+            while (done < pc[q].n) {
+                const ssize_t w = pwrite(fd, buf + pc[q].src + done, (size_t)(pc[q].n - done), pc[q].dst + done);
+                if (w < 0) {
+                    if (errno == EINTR) continue;
+                    err.store(errno);
+                    return;
+                }
+                done += w;
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 0; t + 1 < cut.size(); ++t)
+        if (cut[t] < cut[t + 1]) th.emplace_back(work, cut[t], cut[t + 1]);
+    for (auto &x : th) x.join();
+    if (err.load()) return mando::set_error(MANDO_E_INTERNAL, std::string("pwrite: ") + strerror(err.load()));
     return MANDO_OK;
 }

@@ -292,6 +292,11 @@ def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0) -> tuple[int, l
 _HBM_USABLE = 0.92
 # chunks whose buffers may be alive at once (clustering k+2 while k+1 waits for the POA and k is written)
 _MAX_INFLIGHT = 3
+# multi-rank reassembly: "place" -- the ranks exchange per-root isoform counts and byte sizes (two small
+# all-gathers) and each writes its own roots' bytes into the shared output files; reads2isoforms.txt is
+# placed while the POA runs (it needs only the clustering).  "gather" -- every rank's results go to rank
+# 0 (one RCCL gather), which writes both files (ranks on nodes that share no output directory).
+_REASSEMBLY = os.environ.get("MANDO_REASSEMBLY", "place")
 _CLUSTER_SCRATCH_PER_TEXT = 1.25 * 4.55
 _GATHERED_PER_TEXT = 0.42
 
@@ -404,6 +409,8 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         parts = parts or [np.arange(0)]
     # one rank and contiguous chunks: each chunk's part of both files is written as soon as it is done
     stream_out = world == 1 and not heavy
+    placed = world > 1 and _REASSEMBLY == "place"
+    names_parts: dict = {}
     mine_a = np.asarray(mine, dtype=np.int64)
     # the POA workspaces' HBM budget for this call, from the chunk plan (no free-memory query: the
     # clustering thread allocates the next chunk's buffers while a POA launch sizes its workspace)
@@ -423,13 +430,17 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     # (config 4 on one GPU; any input under the CPU restatements) would hold every chunk at once
     inflight = threading.BoundedSemaphore(_MAX_INFLIGHT)
 
-    def run_cluster(ix):
+    def run_cluster(k, ix):
         inflight.acquire()
         try:
             r = _run_cluster(ix)
         except BaseException:
             inflight.release()
             raise
+        if placed:
+            # the chunk's isoform order and member names, copied out: reads2isoforms.txt is placed from
+            # them while the POA runs (the chunk's buffers go back to their pools after its POA)
+            names_parts[k] = _compact_names(_names_payload(r[0], mine_a[ix]))
         return r
 
     def _run_cluster(ix):
@@ -494,7 +505,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             # copied out now and its buffers (locus text on host and device) go back to their pools --
             # a many-chunk rank share holds only the chunks in flight
             del prep
-            pl = _compact(pl)
+            pl = _compact_cons(pl) if placed else _compact(pl)
             res.close()
         return pl, res
 
@@ -505,7 +516,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
             ThreadPoolExecutor(max_workers=1) as writer, \
             ThreadPoolExecutor(max_workers=n_poa) as gpu_poa:
-        cl = [ex.submit(run_cluster, ix) for ix in parts]
+        cl = [ex.submit(run_cluster, k, ix) for k, ix in enumerate(parts)]
         poa_futs = []
         # one rank: reads2isoforms.txt needs only the clustering, so each chunk's part of it is written
         # by the host thread (after the chunk's assembly) while the POA runs; the FASTA follows each POA
@@ -562,6 +573,11 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                     r2_futs.append(host.submit(write_r2i, res, ix, n_iso_before))
                     fa_futs.append(writer.submit(write_fasta, poa_futs[-1], n_iso_before, r2_futs[-1]))
                     n_iso_before += res.n_isoforms
+            if placed:
+                # every chunk is clustered: number this rank's isoforms and place its reads2isoforms.txt
+                # blocks (writer thread) while the POA runs
+                place_fut = writer.submit(_place_r2i, [names_parts[k] for k in range(len(parts))], comm,
+                                          len(roots), out_path, timeline, t0)
         except BaseException:
             close_outputs()
             _close_all(cl, poa_futs)
@@ -593,7 +609,15 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             except BaseException:
                 _close_all(cl, poa_futs)
                 raise
-    if not stream_out:
+    if placed:
+        tm = time.perf_counter()
+        cons = _merge_cons(payloads)
+        timeline.append(("merge", tm - t0, time.perf_counter() - t0))
+        tw = time.perf_counter()
+        stats["written_isoforms"] = _place_fasta(cons, place_fut.result(), comm, len(roots), out_path)
+        timeline.append(("write", tw - t0, time.perf_counter() - t0))
+        del cons
+    elif not stream_out:
         tm = time.perf_counter()
         payload = payloads[0] if len(payloads) == 1 else _merge(payloads)
         if world > 1:
@@ -609,6 +633,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     stats["t_total"] = time.perf_counter() - t0
     # host time of the output stages (summed over chunks; streamed writes overlap the POA of later chunks)
     stats["t_write"] = sum(b - a for n, a, b in timeline if n in ("write", "write_r2i"))
+    stats["reassembly"] = ("place" if placed else "gather") if world > 1 else "none"
     stats["t_merge"] = sum(b - a for n, a, b in timeline if n == "merge")
     # the chunks' buffers go back to their pools before returning: every kernel that read them has
     # completed (the POA calls are synchronous), and no release can then overlap the next call's kernels
@@ -755,6 +780,105 @@ def _compact(payload: dict) -> dict:
     return dict(iso_root=payload["iso_root"], cons_src=[ct], c_sel=np.zeros(n_iso, np.int16), c_start=co[:-1],
                 c_len=payload["c_len"], c_rc=np.zeros(n_iso, np.int8), name_src=[names],
                 n_sel=np.zeros(n_mem, np.int16), n_start=noff[:-1], n_len=payload["n_len"], mem_off=payload["mem_off"])
+
+
+def _compact_names(p: dict) -> dict:
+    """A names payload with its member names copied into one buffer (independent of the chunk's text)."""
+    names, noff = _lib.pack_segments(p["name_src"], p["n_start"], p["n_len"], sel=p["n_sel"])
+    return dict(iso_root=np.array(p["iso_root"], copy=True), mem_off=np.array(p["mem_off"], copy=True),
+                name_src=[names], n_sel=np.zeros(len(p["n_len"]), np.int16), n_start=noff[:-1],
+                n_len=np.array(p["n_len"], copy=True))
+
+
+def _compact_cons(p: dict) -> dict:
+    """The consensus part of a payload, copied into one buffer (the names were copied at clustering)."""
+    ct, co = _lib.pack_segments(p["cons_src"], p["c_start"], p["c_len"], sel=p["c_sel"], rc=p["c_rc"])
+    n_iso = len(p["c_len"])
+    return dict(iso_root=p["iso_root"], cons_src=[ct], c_sel=np.zeros(n_iso, np.int16), c_start=co[:-1],
+                c_len=np.array(p["c_len"], copy=True), c_rc=np.zeros(n_iso, np.int8))
+
+
+def _merge_cons(parts: list) -> tuple:
+    """The chunks' consensi (compacted, chunk order) as one (srcs, sel, start, len, rc) tuple."""
+    sel = [np.full(len(p["c_len"]), k, np.int16) for k, p in enumerate(parts)]
+    cat = lambda f, dt: np.concatenate([p[f] for p in parts]).astype(dt) if parts else np.zeros(0, dt)
+    return ([p["cons_src"][0] for p in parts], np.concatenate(sel) if sel else np.zeros(0, np.int16),
+            cat("c_start", np.int64), cat("c_len", np.int64), np.zeros(sum(len(s) for s in sel), np.int8))
+
+
+def _exchange_per_root(comm, n_roots: int, roots: np.ndarray, *vals: np.ndarray) -> list:
+    """One all-gather of (root, values...) for this rank's roots; returns each value as a dense per-root
+    array over all ranks (every root belongs to one rank)."""
+    m = len(roots)
+    blob = np.concatenate([np.array([m], np.int64), np.asarray(roots, np.int64)]
+                          + [np.asarray(v, np.int64) for v in vals]).view(np.uint8)
+    allb, counts = comm.allgather_bytes(blob)
+    out = [np.zeros(n_roots, np.int64) for _ in vals]
+    base = 0
+    for c in counts:
+        part = allb[base:base + int(c)].view(np.int64)
+        base += int(c)
+        k = int(part[0])
+        r = part[1:1 + k]
+        for j, o in enumerate(out):
+            o[r] = part[1 + k * (j + 1):1 + k * (j + 2)]
+    return out
+
+
+def _place(path: str, buf: np.ndarray, src: np.ndarray, roots: np.ndarray, sizes: np.ndarray,
+           g_sizes: np.ndarray) -> None:
+    """Writes this rank's per-root blocks of buf at their offsets in the shared file (its size the total
+    of every rank's blocks: each rank sets it, and the blocks of all ranks tile it, so no rank truncates
+    another's bytes and no stale byte survives)."""
+    goff = np.zeros(len(g_sizes) + 1, np.int64)
+    np.cumsum(g_sizes, out=goff[1:])
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+    try:
+        os.ftruncate(fd, int(goff[-1]))
+        _lib.write_blocks(fd, buf, src, goff[roots], sizes)
+    finally:
+        os.close(fd)
+
+
+def _place_r2i(parts: list, comm, n_roots: int, out_path: str, timeline: list, t0: float) -> tuple:
+    """Placement reassembly, clustering half (defineIsoforms.py:155-166 numbers isoforms in sorted-root
+    order across all loci): the ranks exchange per-root isoform counts, number their own isoforms from
+    them and place their reads2isoforms.txt blocks.  Returns what the FASTA half needs."""
+    tw = time.perf_counter()
+    cat = lambda f: np.concatenate([p[f] for p in parts]) if parts else np.zeros(0, np.int64)
+    iso_root = cat("iso_root")
+    mem_off = np.zeros(1, np.int64)
+    if parts:
+        mem_off = np.concatenate([np.zeros(1, np.int64)] + [p["mem_off"][1:] + b for p, b in zip(
+            parts, np.cumsum([0] + [int(p["mem_off"][-1]) for p in parts[:-1]]))])
+    names = ([p["name_src"][0] for p in parts],
+             np.concatenate([np.full(len(p["n_len"]), k, np.int16) for k, p in enumerate(parts)])
+             if parts else np.zeros(0, np.int16), cat("n_start"), cat("n_len"))
+    order = np.argsort(iso_root, kind="stable")
+    rs = iso_root[order]
+    ur, first, cnt = np.unique(rs, return_index=True, return_counts=True)
+    g_cnt, = _exchange_per_root(comm, n_roots, ur, cnt)
+    kbase = np.zeros(n_roots + 1, np.int64)
+    np.cumsum(g_cnt, out=kbase[1:])
+    k = kbase[rs] + 1 + (np.arange(len(rs), dtype=np.int64) - np.repeat(first, cnt))
+    _, r2i, _, ro = _lib.format_outputs(order, mem_off, 0, None, names, iso_k=k, offsets=True)
+    sz = ro[first + cnt] - ro[first]
+    g_sz, = _exchange_per_root(comm, n_roots, ur, sz)
+    _place(out_path + "/reads2isoforms.txt", r2i, ro[first], ur, sz, g_sz)
+    timeline.append(("write_r2i", tw - t0, time.perf_counter() - t0))
+    return order, mem_off, k, ur, first, cnt
+
+
+def _place_fasta(cons: tuple, numbered: tuple, comm, n_roots: int, out_path: str) -> int:
+    """Placement reassembly, POA half: per-root FASTA sizes exchanged, blocks placed, then one barrier
+    (every rank's blocks of both files are written when any rank returns)."""
+    order, mem_off, k, ur, first, cnt = numbered
+    fasta, _, fo, _ = _lib.format_outputs(order, mem_off, 0, cons, None, iso_k=k, offsets=True)
+    sz = fo[first + cnt] - fo[first]
+    g_sz, = _exchange_per_root(comm, n_roots, ur, sz)
+    _place(out_path + "/Isoform_Consensi.fasta", fasta, fo[first], ur, sz, g_sz)
+    comm.barrier()
+    return int(len(order))
 
 
 _FIELDS = ("iso_root", "c_start", "c_len", "n_start", "n_len", "mem_off")

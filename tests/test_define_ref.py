@@ -109,14 +109,15 @@ def test_driver_rank_shares_partition_the_loci(tmp_path):
     assert all(x[0] > 0 for x in got) and sorted(reads) == all_reads
 
 
-def test_driver_three_rank_reassembly_in_one_process(tmp_path):
-    """The 3-rank reassembly with the transport replaced by an in-process hand-over (the rehearsal of
-    tools/rank_rehearsal.py): ranks 1 and 2 run their shares and hand their compacted payloads over, rank 0
-    runs its share, receives them and writes files byte-identical to the reference's."""
+def test_driver_three_rank_reassembly_in_one_process(tmp_path, monkeypatch):
+    """The 3-rank gather reassembly (MANDO_REASSEMBLY=gather) with the transport replaced by an in-process
+    hand-over: ranks 1 and 2 run their shares and hand their compacted payloads over, rank 0 runs its
+    share, receives them and writes files byte-identical to the reference's."""
     import numpy as np
     from oracle import orient as oref
     from oracle import poa as opoa
 
+    monkeypatch.setattr(define, "_REASSEMBLY", "gather")
     store = {}
 
     class Rec:
@@ -136,9 +137,54 @@ def test_driver_three_rank_reassembly_in_one_process(tmp_path):
     groups = 0
     for r in (1, 2, 0):
         st = _run(d, comm=Rec(r), **kw)
+        assert st["reassembly"] == "gather"
         groups += st["poa_groups"]
     st["poa_groups"] = groups  # each rank counts its own POA calls
-    _check(d, "r2c2_rev", st)
+    _check(d, name="r2c2_rev", st=st)
+
+
+class PlaceRehearsal:
+    """In-process stand-in for a communicator under placement reassembly: call c of allgather_bytes
+    returns every rank's latest contribution to call c (ranks that have not made it yet: an empty one).
+    Ranks run one after another, so three passes over the ranks make every exchange complete: the counts
+    (call 0) after the first, the sizes computed from them after the second, the placed bytes after the
+    third (tools/rank_rehearsal.py uses the same scheme)."""
+
+    def __init__(self, rank, world, store):
+        self.rank, self.world, self.store, self.calls = rank, world, store, 0
+
+    def allgather_bytes(self, blob):
+        import numpy as np
+
+        c = self.store.setdefault(self.calls, {})
+        self.calls += 1
+        c[self.rank] = np.array(blob, dtype=np.uint8, copy=True)
+        empty = np.zeros(1, np.int64).view(np.uint8)
+        parts = [c.get(r, empty) for r in range(self.world)]
+        return np.concatenate(parts), np.array([p.size for p in parts], dtype=np.int64)
+
+    def barrier(self):
+        pass
+
+
+def test_driver_three_rank_placement_in_one_process(tmp_path):
+    """The 3-rank placement reassembly (the default): the ranks exchange per-root isoform counts and byte
+    sizes and each writes its own roots' blocks of both files; the files are the reference's bytes."""
+    from oracle import orient as oref
+    from oracle import poa as opoa
+
+    d = _dataset(tmp_path, "r2c2_rev")
+    kw = dict(orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
+              consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci)
+    store = {}
+    for _ in range(3):
+        groups = 0
+        for r in range(3):
+            st = _run(d, comm=PlaceRehearsal(r, 3, store), **kw)
+            assert st["reassembly"] == "place"
+            groups += st["poa_groups"]
+    st["poa_groups"] = groups
+    _check(d, name="r2c2_rev", st=st)
 
 
 def test_heavy_first_split():

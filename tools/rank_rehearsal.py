@@ -1,12 +1,18 @@
 """Rehearsal of an N-rank D-module run on one GPU: the ranks run one after another in
 this process, each on its own share of the LPT plan, exactly as define_isoforms runs them under a real
-communicator -- except the transport: ranks 1..N-1 hand their compacted payload to a recording stand-in
-for mando_gather_bytes, and rank 0 receives those bytes from it.  Rank 0 then merges and writes the
-whole output, so the rehearsal measures every rank's step and rank 0's reassembly (merge + write) on the
-full-size data set, and checks the reassembled files against the one-rank run.
+communicator -- except the transport, an in-process stand-in.
 
-The predicted N-GPU step = max over ranks of (the rank's own step) + rank 0's gather-side work; the RCCL
-transfer itself (bytes into rank 0 over xGMI) is estimated, not measured (one GPU here).
+* placement reassembly (the default): allgather_bytes call c returns every rank's latest contribution to
+  call c.  Three passes over the ranks: the first warms each rank's share (its own process in a real run:
+  files cached, device buffers sized) and completes the count exchange, the second completes the size
+  exchanges, the third is timed and its placed files are checked against the one-rank run.
+* gather reassembly (MANDO_REASSEMBLY=gather): ranks 1..N-1 hand their compacted payload to a recording
+  stand-in for mando_gather_bytes, and rank 0 receives those bytes from it, then merges and writes.
+
+The predicted N-GPU step = max over ranks of the rank's own step (+ rank 0's gather-side work and the
+estimated RCCL transfer for gather).  Placement: the ranks' FASTA blocks go into one file at the same
+time in a real run, and buffered writes to one file serialise in the kernel, so the prediction also
+reports the step with every rank's FASTA placement serialised (an upper bound).
 
 usage: python tools/rank_rehearsal.py <data dir with tmp_SS> N [threads]
 """
@@ -21,6 +27,24 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class _Place:
+    """Placement stand-in: call c of allgather_bytes returns every rank's latest contribution to call c."""
+
+    def __init__(self, rank, world, store):
+        self.rank, self.world, self.store, self.calls = rank, world, store, 0
+
+    def allgather_bytes(self, blob):
+        c = self.store.setdefault(self.calls, {})
+        self.calls += 1
+        c[self.rank] = np.array(blob, dtype=np.uint8, copy=True)
+        empty = np.zeros(1, np.int64).view(np.uint8)
+        parts = [c.get(r, empty) for r in range(self.world)]
+        return np.concatenate(parts), np.array([p.size for p in parts], dtype=np.int64)
+
+    def barrier(self):
+        pass
 
 
 class _Recorder:
@@ -54,6 +78,34 @@ def sha(p):
     return h.hexdigest()
 
 
+def _span(st, name):
+    return sum(b - a for n, a, b in st["timeline"] if n == name)
+
+
+def main_place(d, n, threads, ref, files):
+    from mandalorion_amd import define
+
+    store: dict = {}
+    out = {"ranks": n, "reassembly": "place", "rank_s": {}, "rank_phases_s": {}}
+    for p in range(3):
+        for r in range(n):
+            t0 = time.perf_counter()
+            st = define.define_isoforms(d, threads=threads, comm=_Place(r, n, store))
+            if p == 2:
+                out["rank_s"][r] = round(time.perf_counter() - t0, 4)
+                ph = {k: round(st[k], 4) for k in ("t_ingest", "t_cluster", "t_orient", "t_poa", "t_merge", "t_total")}
+                ph["place_r2i"] = round(_span(st, "write_r2i"), 4)     # overlapped with the POA
+                ph["place_fasta"] = round(_span(st, "write"), 4)      # after it, ends with the barrier
+                out["rank_phases_s"][r] = ph
+    got = {f: sha(os.path.join(d, f)) for f in files}
+    out["reassembled_equals_one_rank"] = (got == ref) if ref else None
+    out["reassembled_sha256"] = got
+    out["predicted_step_s"] = round(max(out["rank_s"].values()), 4)
+    pf = [v["place_fasta"] for v in out["rank_phases_s"].values()]
+    out["predicted_step_serial_fasta_s"] = round(max(v - f for v, f in zip(out["rank_s"].values(), pf)) + sum(pf), 4)
+    print(json.dumps(out), flush=True)
+
+
 def main():
     from mandalorion_amd import define
 
@@ -61,6 +113,8 @@ def main():
     threads = int(sys.argv[3]) if len(sys.argv) > 3 else 16
     files = ("Isoform_Consensi.fasta", "reads2isoforms.txt")
     ref = {f: sha(os.path.join(d, f)) for f in files} if all(os.path.exists(os.path.join(d, f)) for f in files) else None
+    if define._REASSEMBLY == "place":
+        return main_place(d, n, threads, ref, files)
     store: dict = {}
     out = {"ranks": n, "rank_s": {}, "payload_bytes": {}}
     for r in list(range(1, n)) + [0]:
