@@ -295,7 +295,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
                  const int32_t *d_gorder, int64_t n_groups, uint8_t *d_cons,
                  const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
                  int32_t *d_status, int max_per_cu, const SeedPlan *sp = nullptr, bool ev_start = true,
-                 bool ev_end = true, int lane = 0, int kind = 0, size_t granted = 0) {
+                 bool ev_end = true, int lane = 0, int kind = 0, size_t granted = 0, int32_t n_heavy = 0) {
     // lane k > 0: the context's extra stream k - 1 (launches of other kinds alongside); the workspace
     // belongs to the launch kind (kind_ws), so a kind keeps its workspace from batch to batch
     hipStream_t stream = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
@@ -318,6 +318,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.grp_off = d_grp_off;
     a.gorder = d_gorder;
     a.n_groups = (int32_t)n_groups;
+    a.n_heavy = sp ? 0 : n_heavy;
     a.cons = d_cons;
     a.cons_off = d_cons_off;
     a.cons_len = d_cons_len;
@@ -910,6 +911,18 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                 HIP_TRY(hipGetLastError());
             }
             const mando::PoaCaps &caps = kcaps[kind];
+            // the heaviest groups of the launch (DP-cost estimate within MANDO_POA_HEAVY_PRIO of the
+            // largest, L is in LPT order) run at a higher wave priority
+            static const double hprio = getenv("MANDO_POA_HEAVY_PRIO") ? atof(getenv("MANDO_POA_HEAVY_PRIO")) : 0.0;
+            int32_t n_heavy = 0;
+            if (hprio > 0) {
+                auto cost = [&](int32_t g) {
+                    const GroupStat &q = gs[(size_t)g];
+                    return (double)(q.sum - q.first_len) * (double)q.first_len;
+                };
+                const double c0 = cost(L[0]);
+                while (n_heavy < (int32_t)L.size() && cost(L[(size_t)n_heavy]) >= hprio * c0) ++n_heavy;
+            }
             DevBuf &gb = kind == 0 ? ctx->gorder : (kind == 1 ? ctx->gorder_w : ctx->gorder2);
             if ((rc = gb.ensure(L.size() * 4))) return rc;
             HIP_TRY(hipMemcpyAsync(gb.p, L.data(), L.size() * 4, hipMemcpyHostToDevice, lst));
@@ -919,7 +932,7 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                               ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
                               ctx->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &sp : nullptr,
                               lane == 0 && attempt == 0,  // the batch's time runs from the first attempt
-                              nk == 1, lane, kind, grant[kind]);
+                              nk == 1, lane, kind, grant[kind], n_heavy);
             if (rc) return rc;
             ctx->last_launches += 1;
             ++lane;

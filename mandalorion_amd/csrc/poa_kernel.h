@@ -155,6 +155,7 @@ struct PoaRunArgs {
     // a free workspace slot of n_slots (slot_busy, zeroed before the launch) for its group; workgroups
     // of other kernels get CUs as groups finish.  0: persistent slots pulling groups from `counter`.
     int32_t one_group, n_slots;
+    int32_t n_heavy;  // groups gorder[0 .. n_heavy) (the heaviest) run at a higher wave priority
     int32_t *slot_busy;
 };
 struct PoaKArgs : PoaRunArgs {

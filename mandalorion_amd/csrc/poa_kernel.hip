@@ -220,6 +220,7 @@ struct alignas(16) SharedState {
     gint *desc_full, *xpre_full, *qnode_full;
     uint64_t tmark;                 // MANDO_PROF: the last phase boundary of the -S path (prof_mark)
     int slot_idx;                   // this workgroup's workspace slot (one_group launches claim one)
+    int boost;                      // the group is one of the launch's heaviest (wave priority +2)
 
 };
 static_assert(sizeof(BtLds) <= sizeof(DpLds), "backtrack window must fit the DP scratch");
@@ -3788,8 +3789,23 @@ __global__ __launch_bounds__(kWave * NW, NW > 1 ? 2 : (RW == kWideRing ? MANDO_W
         if (lane == 0) {
             sh.slot.order = sh.order0;
             sh.slot.order2 = sh.order1;
+            sh.boost = gi < args_of(sh).n_heavy;
         }
         wave_sync();
+        // the launch's heaviest groups (n_heavy, LPT order: the first gi) run two priority levels above
+        // the rest, so on a shared SIMD their rows issue first: a launch lasts as long as its longest group
+        auto prio_serial = [&] {
+            if (bcast0(sh.boost))
+                __builtin_amdgcn_s_setprio(kPrioSerial + 2);
+            else
+                __builtin_amdgcn_s_setprio(kPrioSerial);
+        };
+        auto prio_dp = [&] {
+            if (bcast0(sh.boost))
+                __builtin_amdgcn_s_setprio(kPrioDp + 2);
+            else
+                __builtin_amdgcn_s_setprio(kPrioDp);
+        };
         int st = kStOk;
         int n = 0, ng = 0;
         int64_t cells = 0;
@@ -3835,13 +3851,13 @@ __global__ __launch_bounds__(kWave * NW, NW > 1 ? 2 : (RW == kWideRing ? MANDO_W
                 // return to their DP sooner, the SIMD's issue slots stay busy (config-3 kernel -3.5 %).
                 // (Running a wide launch's waves two levels higher changed neither the mean step nor
                 // the slow steps: 10-step lines interleaved twice, r03 prio1.)
-                __builtin_amdgcn_s_setprio(kPrioSerial);
+                prio_serial();
                 uint64_t t0 = prof ? clock64() : 0;
                 const bool try16 = r16_eligible<SC, RW>(sc, qlen) && !(args_of(sh).dbg & 1);
                 build_desc(sh, n, lane, try16 ? kRing16 : kRing);
                 uint64_t t1 = prof ? clock64() : 0;
                 int bi = -1;
-                __builtin_amdgcn_s_setprio(kPrioDp);
+                prio_dp();
                 // 16-bit mode when the read's score range allows it; a read that leaves the safe
                 // range is re-aligned in 32-bit mode (the graph is untouched until update_graph)
                 st = try16 ? run_dp<SC, true, RW, NW>(sh, sc, q, qlen, n, lane, cells, bi) : kStRetry32;
@@ -3867,7 +3883,7 @@ __global__ __launch_bounds__(kWave * NW, NW > 1 ? 2 : (RW == kWideRing ? MANDO_W
                 }
                 wave_sync();
                 uint64_t t3 = prof ? clock64() : 0;
-                __builtin_amdgcn_s_setprio(kPrioSerial);
+                prio_serial();
                 st = backtrack<RW>(sh, bi, qlen, n, lane);
                 if (st != kStOk) break;
                 wave_sync();
