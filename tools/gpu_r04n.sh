@@ -11,6 +11,6 @@ for w in config3 config4; do
   python3 -c "import json; d=json.load(open('$D/bench_$w.json')); c=d['config']; print('$w N=1', round(d['value']), round(d['ms_per_step'], 1), c['steps_s'], c['phases_rank0_s'], c.get('full_output_equals_oracle'))"
   for n in 2 4 8; do
     timeout -k 10 900 python3 tools/rank_rehearsal.py /tmp/mando_bench_${w}_$([ $w = config4 ] && echo 200000 || echo 20000) $n 16 > $D/rehearsal_${w}_$n.json 2> $D/rehearsal_${w}_$n.err || { echo "rehearsal $w $n failed"; tail -5 $D/rehearsal_${w}_$n.err; exit 1; }
-    python3 -c "import json; d=json.load(open('$D/rehearsal_${w}_$n.json')); print('rehearsal $w', $n, d['rank_s'], d['rank0_phases_s'], 'pred', d['predicted_step_s'], 'eq', d['reassembled_equals_one_rank'])"
+    python3 -c "import json; d=json.load(open('$D/rehearsal_${w}_$n.json')); print('rehearsal $w', $n, d['rank_s'], d.get('rank_phases_s', {}).get('0', d.get('rank0_phases_s')), 'pred', d['predicted_step_s'], d.get('predicted_step_serial_fasta_s'), 'eq', d['reassembled_equals_one_rank'])"
   done
 done
