@@ -3,15 +3,18 @@
 
 Headline (`value`): PSL records / wall second of the whole D module — locus PSL files on disk ->
 clustering -> orientation (HIP) -> batched POA consensus (HIP) -> Isoform_Consensi.fasta +
-reads2isoforms.txt closed — on BASELINE.json configs[2]: 20,000 synthetic loci x 50 R2C2-shaped reads
-of ~3 kb (1M PSL records; 30 % of the reads on the '-' strand), seed 20250117.  One step = one full
-`define_isoforms` pass over the data set; the clock runs from the start of locus ingest until both
+reads2isoforms.txt closed — by default on BASELINE.json configs[3], the north star's 10M-read strong-scaling
+set, which fits one MI355X: 200,000 synthetic loci x 40-60 reads of 2-4 kb (80 % R2C2 / 20 % PacBio error
+profiles, half of the reads on the '-' strand; ~10M PSL records, 62 GB of locus text), seed 20250117.
+`--workload config3` is configs[2] (20,000 loci x 50 R2C2 reads of ~3 kb, 1M records).  One step = one
+full `define_isoforms` pass over the data set; the clock runs from the start of locus ingest until both
 output files are closed.
 
 Multi-GPU (`--gpus N`, one process per GPU under the driver's launcher): strong scaling.  The same data
 set is sharded over the ranks by the §8(e) cost estimate (LPT); each rank clusters, orients and runs
-the POA on its loci; one all-gather (RCCL over xGMI, libmando mando_comm_*) brings the results to rank
-0, which writes the files.  value = records / max-over-ranks wall time.
+the POA on its loci; the ranks exchange per-root isoform counts and byte sizes (RCCL all-gathers over
+xGMI, libmando mando_comm_*) and each writes its own roots' bytes into the shared output files.
+value = records / max-over-ranks wall time.
 
 Also reported: the POA kernel's roofline (algorithmic bytes per launch / launch time from HIP events on
 the launch stream), the POA kernel rate (reads through POA / kernel time), and `cpu_baseline`: the same
@@ -132,7 +135,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config3")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config4")
     ap.add_argument("--loci", type=int, default=0, help="override the workload's locus count")
     ap.add_argument("--data-dir", default="", help="where the synthetic tmp_SS goes (default $TMPDIR)")
     ap.add_argument("--threads", type=int, default=0, help="host threads per rank (0: 16 / ranks per node)")
@@ -289,9 +292,9 @@ def shard_plan(data: str, world: int) -> list:
     """The driver's LPT plan (define.define_isoforms): loci per rank, for --check-launch."""
     from mandalorion_amd import define
 
-    root_size: dict = {}
-    roots = define._roots(os.path.join(data, "tmp_SS"), root_size)
-    cost = define._size_costs(roots, root_size)
+    size_arr: list = []
+    roots = define._roots(os.path.join(data, "tmp_SS"), size_array=size_arr)
+    cost = define._size_costs(size_arr[0])
     owner = define._lpt_owner(cost, world)
     cnt = np.bincount(owner, minlength=world)
     load = np.bincount(owner, weights=cost, minlength=world)

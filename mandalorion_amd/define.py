@@ -76,11 +76,13 @@ def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0, info: dict |
     return poa.poa_consensus_packed(seqs, seq_off, grp_off, seeding=seeding, device=device, info=info, slot=slot)
 
 
-def _roots(out_tmp: str, sizes: dict | None = None) -> list[str]:
+def _roots(out_tmp: str, sizes: dict | None = None, size_array: list | None = None) -> list[str]:
     """Locus roots of tmp_SS (defineIsoforms.py:130-139); sizes (optional) receives each root's
-    <root>.psl size from the same directory scan.  The scan, the stat calls and the sort run natively
-    (mando_list_roots); a root whose start field is not a plain decimal takes the Python path below,
-    which parses (or raises) exactly as the reference does."""
+    <root>.psl size from the same directory scan, size_array (a list, optional) one int64 array of them
+    aligned with the roots (0: no exact <root>.psl entry) -- no per-root dictionary work on 200,000 loci.
+    The scan, the stat calls and the sort run natively (mando_list_roots); a root whose start field is
+    not a plain decimal takes the Python path below, which parses (or raises) exactly as the reference
+    does."""
     lib = _lib.load()
     # room for 512k roots in the first call (a second call repeats the whole scan: 200,000 loci took
     # two, 0.5 s per rank, r04g)
@@ -99,8 +101,16 @@ def _roots(out_tmp: str, sizes: dict | None = None) -> list[str]:
         roots = names.raw[:nb.value].decode("utf-8", "surrogateescape").split("\0")[:-1]
         if sizes is not None:
             sizes.update((r, v) for r, v in zip(roots, sz[:nr.value].tolist()) if v >= 0)
+        if size_array is not None:
+            size_array.append(np.maximum(sz[:nr.value], 0))
         return roots
-    return _roots_py(out_tmp, sizes)
+    d: dict = {}
+    roots = _roots_py(out_tmp, d)
+    if sizes is not None:
+        sizes.update(d)
+    if size_array is not None:
+        size_array.append(np.array([d.get(r, 0) for r in roots], dtype=np.int64))
+    return roots
 
 
 def _roots_py(out_tmp: str, sizes: dict | None = None) -> list[str]:
@@ -115,13 +125,13 @@ def _roots_py(out_tmp: str, sizes: dict | None = None) -> list[str]:
     return sorted(roots, key=lambda x: (x.split("~")[0], int(x.split("~")[1])))
 
 
-def _size_costs(roots: list[str], root_size: dict) -> np.ndarray:
+def _size_costs(sizes: np.ndarray) -> np.ndarray:
     """Per-locus POA cost estimate for the shard plan, from the file sizes the root scan returns (no
     per-file I/O): a locus of n reads of length L costs ~n L^2 (n L (2w+1) 1.1 L) and
     its file holds ~n L bytes, so with the read count bounded by the subsample the cost grows as the
     size squared.  Reading each file's first record instead (round 3) took 1 s per rank per step on
     20,000 loci and 8-9 s on 200,000 (r04f), on the critical path of every rank."""
-    sz = np.fromiter((root_size.get(r, 0) for r in roots), dtype=np.float64, count=len(roots))
+    sz = np.asarray(sizes, dtype=np.float64)
     return sz * sz
 
 
@@ -364,12 +374,13 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         _, left, right, poly = gtf.parse_genome(genome_file, wl)
     if rank == 0:
         gtf.write_polya_bed(out_path + "/polyAWhiteList.bed", poly, wl)
-    root_size: dict = {}
-    roots = _roots(out_tmp, root_size)
+    size_arr: list = []
+    roots = _roots(out_tmp, size_array=size_arr)
+    root_sizes = size_arr[0]
     # shard loci over ranks: LPT on the DP-cost estimate of SURVEY.md §8(e), results regathered in root order
     mine = list(range(len(roots)))
     if plan_world > 1:
-        owner = _lpt_owner(_size_costs(roots, root_size), plan_world)
+        owner = _lpt_owner(_size_costs(root_sizes), plan_world)
         mine = np.nonzero(owner == plan_rank)[0].tolist()
     my_roots = [roots[i] for i in mine]
     chroms = [r.split("~")[0] for r in my_roots]
@@ -390,7 +401,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     #   rest) is clustered, oriented and assembled while A's POA runs, and its POA is launched on a second
     #   device context beside it.  Outputs are written once both are done (sorted roots);
     # * few loci (SIRV-like, config 5) run in one chunk.
-    sizes = np.array([root_size.get(r, 0) for r in my_roots], dtype=np.int64)
+    sizes = root_sizes[np.asarray(mine, dtype=np.int64)]
     n_chunks, fracs = _chunk_plan(int(sizes.sum()), len(my_roots), n_chunks)
     heavy = (n_chunks == 1 and len(my_roots) >= _MIN_LOCI_CHUNKED and _HEAVY_FRAC > 0
              and os.environ.get("MANDO_CHUNKS") is None and explicit_chunks <= 0)
