@@ -2056,6 +2056,11 @@ __device__ __forceinline__ void w2_helper(SharedState &sh, int lane) {
             const unsigned long long nearinf = __ballot(m < (uint32_t)(kR16High - kR16Low));
             if (lane == 0) X.flag = nearinf ? 1 : 0;
             ds.r16acc = 0xffffffffu;
+            // the group's wave priority (a heavy group's rows issue first, as wave 0's do)
+            if (bcast0(sh.boost))
+                __builtin_amdgcn_s_setprio(2);
+            else
+                __builtin_amdgcn_s_setprio(0);
             group_barrier();  // the flag is read by wave 0
             continue;
         }
