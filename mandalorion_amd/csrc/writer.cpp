@@ -6,6 +6,7 @@
 //   reads2isoforms:   "{name}\tIsoform{k}_{m}\n" per member
 // with k = counter0 + 1 + (position in output order), or iso_k[position], and m = the isoform's member
 // count.
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -171,9 +172,26 @@ extern "C" int mando_write_blocks(int32_t fd, const uint8_t *buf, const int64_t 
         if (acc * nt >= (size_t)total * cut.size() && cut.size() < (size_t)nt) cut.push_back(q + 1);
     }
     cut.push_back(pc.size());
+    if (pc.empty()) return MANDO_OK;
+    // Through a shared mapping of the file range the blocks span (the caller has sized the file): page
+    // faults on one file scale over processes, while buffered pwrite()s into one file serialise on its
+    // inode lock (8 ranks placing 1 GB into one file: 0.35-0.44 s mapped, 0.9-1.4 s with pwrite).  A
+    // descriptor that cannot be mapped (not opened for reading and writing, a pipe) takes pwrite().
+    int64_t lo = INT64_MAX, hi = 0;
+    for (const Piece &q : pc) {
+        lo = std::min(lo, q.dst);
+        hi = std::max(hi, q.dst + q.n);
+    }
+    const int64_t pg = (int64_t)sysconf(_SC_PAGESIZE);
+    const int64_t base = lo / pg * pg;
+    void *map = mmap(nullptr, (size_t)(hi - base), PROT_WRITE, MAP_SHARED, fd, (off_t)base);
     std::atomic<int> err{0};
     auto work = [&](size_t a, size_t b) {
         for (size_t q = a; q < b && !err.load(std::memory_order_relaxed); ++q) {
+            if (map != MAP_FAILED) {
+                memcpy(static_cast<uint8_t *>(map) + (pc[q].dst - base), buf + pc[q].src, (size_t)pc[q].n);
+                continue;
+            }
             int64_t done = 0;
             while (done < pc[q].n) {
                 const ssize_t w = pwrite(fd, buf + pc[q].src + done, (size_t)(pc[q].n - done), pc[q].dst + done);
@@ -190,6 +208,7 @@ extern "C" int mando_write_blocks(int32_t fd, const uint8_t *buf, const int64_t 
     for (size_t t = 0; t + 1 < cut.size(); ++t)
         if (cut[t] < cut[t + 1]) th.emplace_back(work, cut[t], cut[t + 1]);
     for (auto &x : th) x.join();
+    if (map != MAP_FAILED) munmap(map, (size_t)(hi - base));
     if (err.load()) return mando::set_error(MANDO_E_INTERNAL, std::string("pwrite: ") + strerror(err.load()));
     return MANDO_OK;
 }

@@ -843,7 +843,7 @@ def _place(path: str, buf: np.ndarray, src: np.ndarray, roots: np.ndarray, sizes
     another's bytes and no stale byte survives)."""
     goff = np.zeros(len(g_sizes) + 1, np.int64)
     np.cumsum(g_sizes, out=goff[1:])
-    fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+    fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o644)  # read-write: mando_write_blocks maps the file
     try:
         os.ftruncate(fd, int(goff[-1]))
         _lib.write_blocks(fd, buf, src, goff[roots], sizes)

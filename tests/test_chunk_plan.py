@@ -150,3 +150,37 @@ def test_shard_plan_balances_and_is_lpt_for_the_heaviest():
     assert owner[top[8]] == owner[top[7]]
     assert define._lpt_owner(np.array([5.0, 1.0]), 4).tolist() == [0, 1]
     assert define._lpt_owner(np.zeros(0), 3).size == 0
+
+
+@pytest.mark.parametrize("flags", ["rw", "wo"])
+def test_write_blocks_places_every_block(tmp_path, flags):
+    """mando_write_blocks: blocks of a buffer land at their file offsets (through a shared mapping when the
+    descriptor is read-write, pwrite() otherwise), neighbouring blocks coalesced, empty ones skipped."""
+    import numpy as np
+
+    from mandalorion_amd import _lib
+
+    rng = np.random.default_rng(3)
+    n = 5000
+    ln = rng.integers(0, 3000, n)
+    dst = np.zeros(n, np.int64)
+    np.cumsum(ln[:-1], out=dst[1:])
+    perm = rng.permutation(n)                       # the buffer holds the blocks in another order
+    src = np.zeros(n, np.int64)
+    np.cumsum(ln[perm][:-1], out=src[1:])
+    src_of = np.empty(n, np.int64)
+    src_of[perm] = src
+    want = rng.integers(0, 256, int(ln.sum()), dtype=np.uint8)
+    buf = np.empty_like(want)
+    for i in range(n):
+        buf[src_of[i]:src_of[i] + ln[i]] = want[dst[i]:dst[i] + ln[i]]
+    p = tmp_path / "f"
+    with open(p, "wb") as fh:
+        fh.write(b"\xee" * (len(want) + 10))          # stale bytes everywhere
+    fd = os.open(p, os.O_RDWR if flags == "rw" else os.O_WRONLY)
+    try:
+        os.ftruncate(fd, len(want))
+        _lib.write_blocks(fd, buf, src_of, dst, ln, threads=4)
+    finally:
+        os.close(fd)
+    assert p.read_bytes() == want.tobytes()
