@@ -270,9 +270,13 @@ def _sharded(d, use_oracle, world=2, rccl=False):
     return got
 
 
-def test_sharded_two_ranks_equals_reference(tmp_path):
+@pytest.mark.parametrize("world,mode", [(2, "place"), (3, "place"), (2, "gather")])
+def test_sharded_ranks_equal_reference(tmp_path, monkeypatch, world, mode):
+    """world rank processes over the host transport, placement (the default) or gather reassembly: the
+    reference's files."""
     d = _dataset(tmp_path, "r2c2_rev")
-    _sharded(d, use_oracle=True)
+    monkeypatch.setenv("MANDO_REASSEMBLY", mode)
+    _sharded(d, use_oracle=True, world=world)
     ref = GOLD["datasets"]["r2c2_rev"]["reference"]
     assert sha(os.path.join(d, "reads2isoforms.txt")) == ref["reads2isoforms_sha256"]
     assert sha(os.path.join(d, "Isoform_Consensi.fasta")) == ref["isoform_consensi_sha256"]
@@ -296,14 +300,20 @@ def test_gpu_driver_heaviest_first_equals_reference(gpu_ctx, tmp_path, name, mon
 
 
 @pytest.mark.gpu
-def test_gpu_config4_slice_sharded_equals_one_rank(gpu_ctx, tmp_path):
+@pytest.mark.parametrize("world,mode", [(2, "place"), (3, "place"), (2, "gather")])
+def test_gpu_config4_slice_sharded_equals_one_rank(gpu_ctx, tmp_path, monkeypatch, world, mode):
+    """world rank processes on the one GPU (host transport), each placing its blocks into the shared
+    files at once (or gathering to rank 0): byte-identical to the one-rank files."""
     d = str(tmp_path / "c4")
     synth.write_loci(os.path.join(d, "tmp_SS"), 96, threads=8, **CONFIG4_SLICE)
     _run(d)
     one = [open(os.path.join(d, f), "rb").read() for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt")]
-    _sharded(d, use_oracle=False)
+    monkeypatch.setenv("MANDO_REASSEMBLY", mode)  # read by the spawned ranks' define module
+    _sharded(d, use_oracle=False, world=world)
     two = [open(os.path.join(d, f), "rb").read() for f in ("Isoform_Consensi.fasta", "reads2isoforms.txt")]
     assert one == two
+    if world > 2 or mode != "place":
+        return
     # and the one-rank GPU files equal the CPU restatements' on the same slice
     from oracle import orient as oref
     from oracle import poa as opoa
