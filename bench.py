@@ -139,7 +139,7 @@ def parse():
     ap.add_argument("--loci", type=int, default=0, help="override the workload's locus count")
     ap.add_argument("--data-dir", default="", help="where the synthetic tmp_SS goes (default $TMPDIR)")
     ap.add_argument("--threads", type=int, default=0, help="host threads per rank (0: 16 / ranks per node)")
-    ap.add_argument("--cpu-loci", type=int, default=640, help="cpu_baseline sample size (loci)")
+    ap.add_argument("--cpu-loci", type=int, default=2000, help="cpu_baseline sample size (loci): 10-30 s of CPU work")
     ap.add_argument("--cpu-threads", type=int, default=0, help="cpu_baseline threads (0: the usable host cores)")
     ap.add_argument("--check-launch", action="store_true",
                     help="launch, rendezvous, data and shard plan only (no GPU compute); prints the ranks")
