@@ -276,6 +276,7 @@ size_t kind_want(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.e2 = p.gap_ext2;
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
+    mando::occ_cap(a);
     const int per_cu = mando::poa_blocks_per_cu(a, cap);
     const int64_t resident = (int64_t)ctx->n_cu * per_cu;
     int64_t team = 1;
@@ -358,6 +359,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
+    mando::occ_cap(a);
     const int per_cu = mando::poa_blocks_per_cu(a, cap);
     // -S teams: when the seeded groups are too few to fill the resident waves, each gets a team of
     // up to kMaxTeam one-wave workgroups that align a read's windows side by side

@@ -3991,6 +3991,13 @@ int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
     return nb < cap ? nb : cap;
 }
 
+void occ_cap(PoaKArgs &a) {
+    static const int k = getenv("MANDO_POA_OCC") ? atoi(getenv("MANDO_POA_OCC")) : 0;
+    a.lds_pad = 0;
+    if (k <= 0 || a.caps.wide || a.caps.seeded) return;
+    while (a.lds_pad < 65536 && poa_blocks_per_cu(a, 64) > k) a.lds_pad += 256;
+}
+
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream) {
     by_kind(a, [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(n_slots), dim3(kWave * poa_waves(a)), poa_dyn_lds(a), stream, a);
