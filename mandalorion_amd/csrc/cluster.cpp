@@ -36,6 +36,24 @@ using std::vector;
 
 namespace {
 
+// one copy stream per device for the locus text (sub-batched calls: the clustering kernels of the
+// first loci run on the context's stream while the rest of the text is still being copied)
+hipStream_t copy_stream(int device) {
+    static std::mutex mu;
+    static std::vector<hipStream_t> streams;
+    std::lock_guard<std::mutex> g(mu);
+    if ((int)streams.size() <= device) streams.resize((size_t)device + 1, nullptr);
+    if (!streams[(size_t)device]) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        if (hipStreamCreateWithFlags(&streams[(size_t)device], hipStreamNonBlocking) != hipSuccess)
+            streams[(size_t)device] = nullptr;
+        (void)hipSetDevice(cur);
+    }
+    return streams[(size_t)device];
+}
+
 // Host buffers for the locus text, kept for reuse: page-locked (hipHostMalloc, pinned once, reused
 // by later calls), so the readers fread straight into DMA-able memory and the piecewise copies to the
 // device run on the copy engine, asynchronously, instead of a host staging copy plus a blit kernel
@@ -253,9 +271,63 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
             cv.notify_one();
         }
     };
+    in.text = res->text_p;
+    in.d_text = d_text;
+    in.text_len = (int64_t)res->text_len;
+    in.foff = foff.data();
+    in.fstatus = fstatus.data();
+    in.chroms = chroms;
+    in.ann_pos = ann_pos;
+    in.ann_off = ann_off;
+    // Sub-batches: the loci split into up to four byte-balanced ranges, each clustered (K1, K2) on the
+    // context's stream by a worker thread as soon as its text is on the device, while the readers and the
+    // copy stream bring in the rest -- the kernels of the first ranges run under the reading and the
+    // copy instead of after them.  Results are the same: every locus replays its own RNG state.
+    hipStream_t cstream = stream;
+    int nsub = (n_loci >= 1024 && res->text_len >= (size_t(256) << 20)) ? 4 : 1;
+    if (const char *ev = getenv("MANDO_CL_SUB")) nsub = std::max(1, std::min(16, atoi(ev)));
+    if (nsub > 1 && !(cstream = copy_stream(mando::ctx_device(ctx)))) {
+        cstream = stream;
+        nsub = 1;
+    }
+    vector<int64_t> bounds((size_t)nsub + 1, n_loci);
+    bounds[0] = 0;
+    for (int k = 1; k < nsub; ++k)
+        bounds[(size_t)k] = (int64_t)(std::lower_bound(foff.begin(), foff.begin() + n_loci,
+                                                       (int64_t)((double)res->text_len * k / nsub)) - foff.begin());
+    for (int k = 1; k <= nsub; ++k) bounds[(size_t)k] = std::max(bounds[(size_t)k], bounds[(size_t)k - 1]);
+    vector<cl::ClusterOut> parts((size_t)nsub);
+    vector<hipEvent_t> ready((size_t)nsub, nullptr);
+    vector<int> part_rc((size_t)nsub, MANDO_OK);
+    int copied = 0;  // sub-batches whose text has been copied (events recorded)
+    std::mutex pmu;
+    std::condition_variable pcv;
+    bool copy_failed = false;
+    auto worker = [&]() {
+        for (int k = 0; k < nsub; ++k) {
+            {
+                std::unique_lock<std::mutex> lk(pmu);
+                pcv.wait(lk, [&] { return copied > k || copy_failed; });
+                if (copied <= k) return;
+            }
+            cl::ClusterIn ik = in;
+            const int64_t a = bounds[(size_t)k], b = bounds[(size_t)k + 1];
+            ik.n_loci = b - a;
+            ik.foff = in.foff + a;
+            ik.fstatus = in.fstatus + a;
+            ik.chroms = in.chroms + a;
+            if (in.ann_off) ik.ann_off = in.ann_off + 4 * a;
+            ik.ready = ready[(size_t)k];
+            part_rc[(size_t)k] = cl::cluster_gpu(ctx, ik, parts[(size_t)k]);
+            if (part_rc[(size_t)k] != MANDO_OK) return;
+        }
+    };
+    int copy_rc = MANDO_OK;
     {
         vector<std::thread> th;
         for (int t = 0; t < nth; ++t) th.emplace_back(reader);
+        std::thread wk;
+        if (nsub > 1) wk = std::thread(worker);
         // copy the completed prefix in >= 64 MB pieces as the readers advance
         constexpr int64_t kPiece = int64_t(64) << 20;
         int64_t upto = 0, sent = 0;
@@ -267,29 +339,69 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
             }
             while (upto < n_loci && done[(size_t)upto].load(std::memory_order_acquire)) ++upto;
             const int64_t avail = foff[(size_t)upto];
-            if (avail - sent >= kPiece || (upto == n_loci && avail > sent)) {
+            // a sub-batch's last file read: its text goes out now, whatever the piece size
+            const bool edge = nsub > 1 && copied < nsub && upto >= bounds[(size_t)copied + 1];
+            if (avail - sent >= kPiece || (edge && avail > sent) || (upto == n_loci && avail > sent)) {
                 if (hipMemcpyAsync((char *)d_text + sent, res->text_p + sent, (size_t)(avail - sent),
-                                   hipMemcpyHostToDevice, stream) != hipSuccess) {
-                    for (auto &t : th) t.join();
-                    return mando::set_error(MANDO_E_HIP, "cluster: text copy to the device");
+                                   hipMemcpyHostToDevice, cstream) != hipSuccess) {
+                    copy_rc = mando::set_error(MANDO_E_HIP, "cluster: text copy to the device");
+                    break;
                 }
                 sent = avail;
             }
+            while (nsub > 1 && copied < nsub && upto >= bounds[(size_t)copied + 1] && sent >= foff[(size_t)bounds[(size_t)copied + 1]]) {
+                hipEvent_t e = nullptr;
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess ||
+                    hipEventRecord(e, cstream) != hipSuccess) {
+                    copy_rc = mando::set_error(MANDO_E_HIP, "cluster: copy event");
+                    break;
+                }
+                ready[(size_t)copied] = e;
+                std::lock_guard<std::mutex> g(pmu);
+                ++copied;
+                pcv.notify_one();
+            }
+            if (copy_rc != MANDO_OK) break;
+        }
+        if (copy_rc != MANDO_OK) {
+            next.store(n_loci);  // stop the readers
+            std::lock_guard<std::mutex> g(pmu);
+            copy_failed = true;
+            pcv.notify_one();
         }
         for (auto &t : th) t.join();
+        if (wk.joinable()) wk.join();
     }
+    for (hipEvent_t e : ready)
+        if (e) (void)hipEventDestroy(e);
+    if (copy_rc != MANDO_OK) return copy_rc;
     const double t_read = secs();
-    in.text = res->text_p;
-    in.d_text = d_text;
-    in.text_len = (int64_t)res->text_len;
-    in.foff = foff.data();
-    in.fstatus = fstatus.data();
-    in.chroms = chroms;
-    in.ann_pos = ann_pos;
-    in.ann_off = ann_off;
     cl::ClusterOut o;
-    const int rc = cl::cluster_gpu(ctx, in, o);
-    if (rc != MANDO_OK) return rc;
+    if (nsub == 1) {
+        const int rc = cl::cluster_gpu(ctx, in, o);
+        if (rc != MANDO_OK) return rc;
+    } else {
+        for (int k = 0; k < nsub; ++k)
+            if (part_rc[(size_t)k] != MANDO_OK) return part_rc[(size_t)k];
+        // the sub-batches' outputs, concatenated in locus order (record bases shifted)
+        o.rec_base.assign(1, 0);
+        for (int k = 0; k < nsub; ++k) {
+            cl::ClusterOut &q = parts[(size_t)k];
+            const int64_t base = o.rec_base.back();
+            o.status.insert(o.status.end(), q.status.begin(), q.status.end());
+            o.n_rec.insert(o.n_rec.end(), q.n_rec.begin(), q.n_rec.end());
+            for (size_t i = 1; i < q.rec_base.size(); ++i) o.rec_base.push_back(base + q.rec_base[i]);
+            o.rec_text.insert(o.rec_text.end(), q.rec_text.begin(), q.rec_text.end());
+            auto mv = [](auto &dst, auto &src) {
+                for (auto &x : src) dst.push_back(std::move(x));
+            };
+            mv(o.peaks, q.peaks);
+            mv(o.iso_nmem, q.iso_nmem);
+            mv(o.mem, q.mem);
+            mv(o.iso_nsub, q.iso_nsub);
+            mv(o.sub, q.sub);
+        }
+    }
     const double t_gpu = secs();
     // flatten: records in locus order, isoforms in locus then IsoDict order
     const int64_t nr = o.rec_base[(size_t)n_loci];

@@ -137,6 +137,7 @@ struct ClusterIn {
     int32_t w, min_count, up, down, sub_k;
     std::vector<std::string> junctions;
     uint32_t seed;
+    hipEvent_t ready = nullptr;  // the text of these loci is on the device once this event completes
 };
 struct ClusterOut {
     std::vector<int32_t> status, n_rec;

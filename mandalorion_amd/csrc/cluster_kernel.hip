@@ -2664,6 +2664,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     std::lock_guard<std::mutex> ctx_guard(ctx_mutex(ctx));
     CL_TRY(hipSetDevice(mando::ctx_device(ctx)));
     hipStream_t s = mando::ctx_stream(ctx);
+    if (in.ready) CL_TRY(hipStreamWaitEvent(s, in.ready, 0));
 
     // parameters + the RNG state every locus starts from
     Params prm;

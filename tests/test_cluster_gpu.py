@@ -110,6 +110,20 @@ def test_bench_shapes(tmp_path, shape):
              minimum_read_count=3, poa_subsample=150, cutoff=0.25, junctions="gtag,gcag")
 
 
+@pytest.mark.parametrize("sub", ["3", "5"])
+def test_sub_batched_calls_equal_the_restatement(tmp_path, monkeypatch, sub):
+    """MANDO_CL_SUB: the loci clustered in byte-balanced sub-batches, each as soon as its text is on the
+    device (copy stream + event), the rest still being read: the restatement's results, locus by locus
+    (the default sub-batches only large calls: >= 1024 loci and 256 MB of text)."""
+    d = str(tmp_path)
+    synth.write_loci(os.path.join(d, "tmp_SS"), 300, threads=8, seed=17, reads=(40, 60), exon_len=(130, 570),
+                     pacbio_frac=0.2, rev_frac=0.5)
+    _, paths, chroms, _ = _inputs(d)
+    monkeypatch.setenv("MANDO_CL_SUB", sub)
+    n_ok, _ = _compare(paths, chroms, seed=5)
+    assert n_ok == 300
+
+
 def _edit_lines(src, dst, fn):
     lines = open(src).read().split("\n")
     if lines and lines[-1] == "":
