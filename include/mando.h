@@ -153,6 +153,10 @@ typedef struct {
     uint32_t seed;              /* numpy global RNG seed every locus starts from */
     int32_t threads;            /* host threads reading the locus files (0 = all hardware threads) */
     int32_t poa_subsample;      /* determine_consensus subsample size (100) */
+    mando_ctx *orient_ctx;      /* NULL (default), or a context of the same device: every isoform's
+                                   subsample is oriented on it (mando_orient_segments, SDC:895-907) as
+                                   its loci are clustered, and the view carries the hit strands */
+    int32_t orient_max_hits;    /* first attempt's hit capacity per read (4); reads with more re-run at 8 */
 } mando_cluster_params;
 
 typedef struct mando_cluster_result mando_cluster_result;
@@ -183,6 +187,10 @@ typedef struct {
     const char *peak_type;         /* '5' / '3' */
     const char *peak_side;         /* 'l' / 'r' */
     const double *peak_prop;       /* round(prop, 3), -1 for annotated ('A') bins */
+    int32_t orient_max_hits;       /* 0: not oriented (no orient_ctx, or a read with more than 8 primary
+                                      hits: the caller orients and reports it); else H: */
+    const int8_t *orient_hits;     /* sub[] x H hit strands (+1 / -1), as mando_orient_segments writes them */
+    const int32_t *orient_n_hits;  /* primary hits per subsampled read */
 } mando_cluster_view;
 
 void mando_cluster_default_params(mando_cluster_params *p);

@@ -119,6 +119,8 @@ class ClusterParams(ctypes.Structure):
         ("seed", ctypes.c_uint32),
         ("threads", ctypes.c_int32),
         ("poa_subsample", ctypes.c_int32),
+        ("orient_ctx", ctypes.c_void_p),
+        ("orient_max_hits", ctypes.c_int32),
     ]
 
     @classmethod
@@ -153,6 +155,9 @@ class ClusterView(ctypes.Structure):
         ("peak_type", ctypes.POINTER(ctypes.c_char)),
         ("peak_side", ctypes.POINTER(ctypes.c_char)),
         ("peak_prop", ctypes.POINTER(ctypes.c_double)),
+        ("orient_max_hits", ctypes.c_int32),
+        ("orient_hits", ctypes.POINTER(ctypes.c_int8)),
+        ("orient_n_hits", ctypes.POINTER(ctypes.c_int32)),
     ]
 
 

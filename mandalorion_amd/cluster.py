@@ -76,6 +76,13 @@ class ClusterResult:
         self.peak_type = bytes(_arr(v.peak_type, npk, np.uint8)).decode() if npk else ""
         self.peak_side = bytes(_arr(v.peak_side, npk, np.uint8)).decode() if npk else ""
         self.peak_prop = _arr(v.peak_prop, npk, np.float64)
+        # the subsampled reads' orientation, when the call ran it (orient=True): sub x H hit strands
+        H = int(getattr(v, "orient_max_hits", 0) or 0)
+        self.orient_hits = self.orient_n_hits = None
+        if H > 0:
+            ns = int(self.sub_off[-1])
+            self.orient_hits = _arr(v.orient_hits, ns * H, np.int8).reshape(ns, H)
+            self.orient_n_hits = _arr(v.orient_n_hits, ns, np.int32)
 
     def device_text(self) -> tuple[int, int]:
         """(device pointer, length) of the locus text on the GPU the clustering ran on (0 for the
@@ -160,11 +167,15 @@ def c_inputs(paths: list[str], chroms: list[str], ann):
 
 
 def cluster_loci(paths: list[str], chroms: list[str], ann: list[list[list[int]]] | None = None,
-                 device: int = 0, slot: int = 4, **params) -> ClusterResult:
+                 device: int = 0, slot: int = 4, orient: bool = False, **params) -> ClusterResult:
     """Cluster every locus file on the GPU.  ann[i] = [left '5', left '3', right '5', right '3'] position
-    lists; params as cluster_params (threads: host threads reading the files)."""
+    lists; params as cluster_params (threads: host threads reading the files).  orient: every isoform's
+    subsample is also oriented (on the device's orientation context, slot 1) as its loci are clustered;
+    the result then holds orient_hits / orient_n_hits (None when a read had more than 8 primary hits)."""
     lib = _lib.load()
     p = cluster_params(**params)
+    if orient:
+        p.orient_ctx = _lib.context(device, slot=1).handle.value
     n, cpaths, cchroms, ann_pos, ann_off = c_inputs(paths, chroms, ann)
     ctx = _lib.context(device, slot=slot)
     h = ctypes.c_void_p()

@@ -38,6 +38,56 @@ namespace {
 
 // one copy stream per device for the locus text (sub-batched calls: the clustering kernels of the
 // first loci run on the context's stream while the rest of the text is still being copied)
+// Orientation of one batch of clustered loci (their isoforms' subsamples, in the order the result lists
+// them: loci, isoforms, draw order; the first read of each group is its reference), as the D driver
+// would run it after the whole call (SDC:895-907): H hits per read, re-run at 8 when a read has more;
+// H = 0 when even 8 do not hold them (the caller then orients and reports it).
+struct OrientPart {
+    vector<int8_t> hits;
+    vector<int32_t> nh;
+    int H = 0;
+};
+int orient_part(mando_ctx *octx, const void *d_text, int64_t text_len, const mando::cl::ClusterOut &q, int h0,
+                OrientPart &op) {
+    vector<int64_t> off, grp{0};
+    vector<int32_t> len;
+    for (size_t i = 0; i < q.status.size(); ++i) {
+        if (q.status[i] != mando::cl::kOk) continue;
+        const int64_t base = q.rec_base[i];
+        const auto &ns = q.iso_nsub[i];
+        const auto &ss = q.sub[i];
+        size_t ps = 0;
+        for (size_t k = 0; k < ns.size(); ++k) {
+            for (int32_t t = 0; t < ns[k]; ++t) {
+                const int64_t r = base + ss[ps++];
+                off.push_back(q.rec_text[(size_t)(4 * r + 2)]);
+                len.push_back((int32_t)q.rec_text[(size_t)(4 * r + 3)]);
+            }
+            grp.push_back((int64_t)off.size());
+        }
+    }
+    const int64_t n = (int64_t)off.size(), ng = (int64_t)grp.size() - 1;
+    for (int H = std::max(1, std::min(8, h0));; H = 8) {
+        op.hits.assign((size_t)std::max<int64_t>(n, 1) * (size_t)H, 0);
+        op.nh.assign((size_t)std::max<int64_t>(n, 1), 0);
+        const int rc = mando_orient_segments(octx, static_cast<const uint8_t *>(d_text), text_len, off.data(),
+                                             len.data(), grp.data(), ng, op.hits.data(), H, op.nh.data());
+        if (rc != MANDO_OK) return rc;
+        int32_t mx = 0;
+        for (int64_t r = 0; r < n; ++r) mx = std::max(mx, op.nh[(size_t)r]);
+        op.hits.resize((size_t)n * (size_t)H);
+        op.nh.resize((size_t)n);
+        if (mx <= H) {
+            op.H = H;
+            return MANDO_OK;
+        }
+        if (H >= 8) {
+            op.H = 0;
+            return MANDO_OK;
+        }
+    }
+}
+
 hipStream_t copy_stream(int device) {
     static std::mutex mu;
     static std::vector<hipStream_t> streams;
@@ -158,6 +208,10 @@ struct mando_cluster_result {
     vector<char> peak_type, peak_side;
     vector<double> peak_prop;
     vector<int32_t> locus_status;
+    // orientation of the subsampled reads (orient_ctx): sub.size() x o_H strands, hits per read
+    int32_t o_H = 0;
+    vector<int8_t> o_hits;
+    vector<int32_t> o_nh;
     // the same text on the device (freed stream-ordered on the clustering context's stream)
     mando_ctx *ctx = nullptr;
     void *d_text = nullptr;
@@ -181,6 +235,8 @@ void mando_cluster_default_params(mando_cluster_params *p) {
     p->seed = 0;
     p->threads = 0;
     p->poa_subsample = 100;
+    p->orient_ctx = nullptr;
+    p->orient_max_hits = 4;
 }
 
 int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const char *const *psl_paths,
@@ -303,6 +359,8 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     std::mutex pmu;
     std::condition_variable pcv;
     bool copy_failed = false;
+    int clustered = 0;  // sub-batches clustered (the orientation worker follows)
+    bool cluster_failed = false;
     auto worker = [&]() {
         for (int k = 0; k < nsub; ++k) {
             {
@@ -319,15 +377,40 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
             if (in.ann_off) ik.ann_off = in.ann_off + 4 * a;
             ik.ready = ready[(size_t)k];
             part_rc[(size_t)k] = cl::cluster_gpu(ctx, ik, parts[(size_t)k]);
-            if (part_rc[(size_t)k] != MANDO_OK) return;
+            std::lock_guard<std::mutex> g(pmu);
+            if (part_rc[(size_t)k] != MANDO_OK) {
+                cluster_failed = true;
+                pcv.notify_all();
+                return;
+            }
+            ++clustered;
+            pcv.notify_all();
+        }
+    };
+    // orientation of each sub-batch on prm->orient_ctx as soon as it is clustered, beside the
+    // clustering of the next one
+    mando_ctx *octx = prm->orient_ctx;
+    vector<OrientPart> oparts((size_t)nsub);
+    vector<int> orient_rc((size_t)nsub, MANDO_OK);
+    auto orienter = [&]() {
+        for (int k = 0; k < nsub; ++k) {
+            {
+                std::unique_lock<std::mutex> lk(pmu);
+                pcv.wait(lk, [&] { return clustered > k || cluster_failed; });
+                if (clustered <= k) return;
+            }
+            orient_rc[(size_t)k] = orient_part(octx, d_text, (int64_t)res->text_len, parts[(size_t)k],
+                                               prm->orient_max_hits, oparts[(size_t)k]);
+            if (orient_rc[(size_t)k] != MANDO_OK) return;
         }
     };
     int copy_rc = MANDO_OK;
     {
         vector<std::thread> th;
         for (int t = 0; t < nth; ++t) th.emplace_back(reader);
-        std::thread wk;
+        std::thread wk, ow;
         if (nsub > 1) wk = std::thread(worker);
+        if (nsub > 1 && octx) ow = std::thread(orienter);
         // copy the completed prefix in >= 64 MB pieces as the readers advance
         constexpr int64_t kPiece = int64_t(64) << 20;
         int64_t upto = 0, sent = 0;
@@ -359,7 +442,7 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
                 ready[(size_t)copied] = e;
                 std::lock_guard<std::mutex> g(pmu);
                 ++copied;
-                pcv.notify_one();
+                pcv.notify_all();
             }
             if (copy_rc != MANDO_OK) break;
         }
@@ -367,10 +450,18 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
             next.store(n_loci);  // stop the readers
             std::lock_guard<std::mutex> g(pmu);
             copy_failed = true;
-            pcv.notify_one();
+            pcv.notify_all();
         }
         for (auto &t : th) t.join();
         if (wk.joinable()) wk.join();
+        if (ow.joinable()) {  // a clustering worker that stopped early releases the orientation worker
+            {
+                std::lock_guard<std::mutex> g(pmu);
+                if (clustered < nsub) cluster_failed = true;
+                pcv.notify_all();
+            }
+            ow.join();
+        }
     }
     for (hipEvent_t e : ready)
         if (e) (void)hipEventDestroy(e);
@@ -380,9 +471,15 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     if (nsub == 1) {
         const int rc = cl::cluster_gpu(ctx, in, o);
         if (rc != MANDO_OK) return rc;
+        if (octx) {
+            const int orc = orient_part(octx, d_text, (int64_t)res->text_len, o, prm->orient_max_hits, oparts[0]);
+            if (orc != MANDO_OK) return orc;
+        }
     } else {
         for (int k = 0; k < nsub; ++k)
             if (part_rc[(size_t)k] != MANDO_OK) return part_rc[(size_t)k];
+        for (int k = 0; k < nsub && octx; ++k)
+            if (orient_rc[(size_t)k] != MANDO_OK) return orient_rc[(size_t)k];
         // the sub-batches' outputs, concatenated in locus order (record bases shifted)
         o.rec_base.assign(1, 0);
         for (int k = 0; k < nsub; ++k) {
@@ -464,6 +561,27 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
             res->peak_prop.push_back(pk.prop);
         }
     }
+    if (octx) {  // the sub-batches' hit strands, in the result's subsample order, at one width
+        int H = 0;
+        size_t rows = 0;
+        for (const OrientPart &q : oparts) {
+            H = (q.H == 0 || H < 0) ? -1 : std::max(H, q.H);
+            rows += q.nh.size();
+        }
+        if (H > 0 && rows == res->sub.size()) {
+            res->o_H = H;
+            res->o_hits.assign(rows * (size_t)H, 0);
+            res->o_nh.resize(rows);
+            size_t r0 = 0;
+            for (const OrientPart &q : oparts) {
+                for (size_t r = 0; r < q.nh.size(); ++r) {
+                    res->o_nh[r0 + r] = q.nh[r];
+                    memcpy(&res->o_hits[(r0 + r) * (size_t)H], &q.hits[r * (size_t)q.H], (size_t)q.H);
+                }
+                r0 += q.nh.size();
+            }
+        }
+    }
     if (timing)
         fprintf(stderr, "[cluster] %lld loci, %.1f MB: sizes %.3f s, read + copy %.3f s, kernels %.3f s, flatten %.3f s\n",
                 (long long)n_loci, res->text_len / 1e6, t_size, t_read - t_size, t_gpu - t_read, secs() - t_gpu);
@@ -496,6 +614,9 @@ int mando_cluster_view_get(const mando_cluster_result *r, mando_cluster_view *v)
     v->peak_type = r->peak_type.data();
     v->peak_side = r->peak_side.data();
     v->peak_prop = r->peak_prop.data();
+    v->orient_max_hits = r->o_H;
+    v->orient_hits = r->o_hits.data();
+    v->orient_n_hits = r->o_nh.data();
     return MANDO_OK;
 }
 

@@ -462,7 +462,10 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             ann=[ann[i] for i in ix] if ann else None,
             device=device, cutoff=cutoff, splice_site_width=splice_site_width,
             minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
-            downstream_buffer=downstream_buffer, junctions=junctions, seed=seed, threads=cl_threads)
+            downstream_buffer=downstream_buffer, junctions=junctions, seed=seed, threads=cl_threads,
+            # the HIP path orients each sub-batch of loci inside the call, beside the next one's clustering
+            **({"orient": True} if cluster_fn is None and dev_orient and os.environ.get("MANDO_ORIENT_IN_CLUSTER", "1") != "0"
+               else {}))
         te = time.perf_counter()
         timeline.append(("cluster", tc - t0, te - t0))
         bad = np.nonzero(r.locus_status != 0)[0]
@@ -473,7 +476,9 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             raise RuntimeError(f"locus {my_roots[ix[i]]}: {cluster.STATUS.get(code, code)} "
                                "(the reference's locus worker raises here)")
         r.on_close = inflight.release  # the chunk leaves the pipeline when its buffers are released
-        if dev_orient:
+        if dev_orient and getattr(r, "orient_hits", None) is not None:
+            o_in = (None, None)  # oriented inside the clustering call
+        elif dev_orient:
             o_in = (r.seq_off[r.sub], r.seq_len[r.sub])
         else:
             o_in = _lib.pack_segments([r.text], r.seq_off[r.sub], r.seq_len[r.sub])
@@ -571,7 +576,9 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
                 add("t_cluster", tcl)
                 add("t_pack", tpk)
                 tg = time.perf_counter()
-                if dev_orient:
+                if dev_orient and getattr(res, "orient_hits", None) is not None:
+                    hits, n_hits = res.orient_hits, res.orient_n_hits
+                elif dev_orient:
                     hits, n_hits = gpu_orient_segments(res, o_a, o_b, res.sub_off, device=device)
                 else:
                     hits, n_hits = orient_fn(o_a, o_b, res.sub_off)

@@ -207,6 +207,17 @@ def test_gpu_driver_equals_reference(gpu_ctx, tmp_path, name):
     _check(d, name, st)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["config1", "r2c2_rev", "long_seeded"])
+def test_gpu_driver_sub_batched_clustering_equals_reference(gpu_ctx, tmp_path, monkeypatch, name):
+    """Clustering in 3 sub-batches with each one's orientation run inside the call beside the next one's
+    clustering (the large-input path, forced by MANDO_CL_SUB): the reference's files."""
+    monkeypatch.setenv("MANDO_CL_SUB", "3")
+    d = _dataset(tmp_path, name)
+    st = _run(d)
+    _check(d, name, st)
+
+
 # ---------------------------------------------------------------------------------------------
 # sharded runs (SURVEY.md §8(e)): loci LPT-sharded over 2 ranks, one all-gather to rank 0's writer
 # ---------------------------------------------------------------------------------------------
