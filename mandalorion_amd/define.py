@@ -463,8 +463,10 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             device=device, cutoff=cutoff, splice_site_width=splice_site_width,
             minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
             downstream_buffer=downstream_buffer, junctions=junctions, seed=seed, threads=cl_threads,
-            # the HIP path orients each sub-batch of loci inside the call, beside the next one's clustering
-            **({"orient": True} if cluster_fn is None and dev_orient and os.environ.get("MANDO_ORIENT_IN_CLUSTER", "1") != "0"
+            # MANDO_ORIENT_IN_CLUSTER=1: each sub-batch of loci oriented inside the call, beside the next
+            # one's clustering -- measured neutral (both are throughput-bound kernels sharing the CUs,
+            # profiles/r04v_orient_in_cluster_ab.jsonl), so off by default
+            **({"orient": True} if cluster_fn is None and dev_orient and os.environ.get("MANDO_ORIENT_IN_CLUSTER", "0") == "1"
                else {}))
         te = time.perf_counter()
         timeline.append(("cluster", tc - t0, te - t0))

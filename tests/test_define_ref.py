@@ -213,6 +213,7 @@ def test_gpu_driver_sub_batched_clustering_equals_reference(gpu_ctx, tmp_path, m
     """Clustering in 3 sub-batches with each one's orientation run inside the call beside the next one's
     clustering (the large-input path, forced by MANDO_CL_SUB): the reference's files."""
     monkeypatch.setenv("MANDO_CL_SUB", "3")
+    monkeypatch.setenv("MANDO_ORIENT_IN_CLUSTER", "1")
     d = _dataset(tmp_path, name)
     st = _run(d)
     _check(d, name, st)
