@@ -1472,6 +1472,22 @@ __device__ __forceinline__ void row_store16(gu8 *base, int uoff, uint32_t lane_o
     *reinterpret_cast<GLB uint16_t *>(base + (uint64_t)((uint32_t)uoff + lane_off)) = (uint16_t)v;
 }
 
+// A fast row's record in HBM (lane 0): {beg, end, tbbase, kpbase} and, for a row whose successor is
+// far, {argmax, spill offset}.  MANDO_RINFO_SADDR: the store in the saddr form (the slot's base in SGPRs,
+// the row's 32-bit byte offset in a VGPR) instead of a 64-bit address built on the scalar unit.
+__device__ __forceinline__ void row_record(gint *rinfo, int r, int beg, int end, int tbbase, int kpbase, int far,
+                                           int besti, int soff) {
+#ifdef MANDO_RINFO_SADDR
+    const uint32_t off = (uint32_t)r * (uint32_t)(kRowInfoInts * 4);
+    row_store(reinterpret_cast<gu8 *>(rinfo), off, (v4i){beg, end, tbbase, kpbase});
+    if (far) row_store(reinterpret_cast<gu8 *>(rinfo), off + 16u, (v2i){besti, soff});
+#else
+    gint *ri = rinfo + (int64_t)r * kRowInfoInts;
+    *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
+    if (far) *reinterpret_cast<GLB v2i *>(ri + 4) = (v2i){besti, soff};
+#endif
+}
+
 // ---- 16-bit mode with scalar row control -------------------------------------------------------
 // Everything that is uniform per row (descriptor, predecessor band records, band, fast-path
 // tests, allocation) lives in SGPRs: descriptors come straight from HBM through the scalar cache
@@ -1635,9 +1651,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     ds.cells += end - beg + 1;
     if (lane == 0) {
         sh.rrow[R.r & (kRowRing - 1)] = make_int4(beg, end, besti, soff);
-        gint *ri = rinfo + (int64_t)R.r * kRowInfoInts;
-        *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
-        if (R.far) *reinterpret_cast<GLB v2i *>(ri + 4) = (v2i){besti, soff};
+        row_record(rinfo, R.r, beg, end, tbbase, kpbase, R.far, besti, soff);
     }
     return besti;
 }
@@ -1809,9 +1823,7 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
     ds.cells += end - beg + 1;
     if (lane == 0) {
         sh.rrow[R.r & (kRowRing - 1)] = make_int4(beg, end, besti, soff);
-        gint *ri = rinfo + (int64_t)R.r * kRowInfoInts;
-        *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
-        if (R.far) *reinterpret_cast<GLB v2i *>(ri + 4) = (v2i){besti, soff};
+        row_record(rinfo, R.r, beg, end, tbbase, kpbase, R.far, besti, soff);
     }
     return besti;
 }
@@ -2010,9 +2022,7 @@ __device__ __forceinline__ int row16w_half(const SC &sc, gu8 *tb, gu8 *kp, gint 
     ds.cells += end - beg + 1;
     if (h == 0 && lane == 0) {
         sh.rrow[R.r & (kRowRing - 1)] = make_int4(beg, end, besti, soff);
-        gint *ri = rinfo + (int64_t)R.r * kRowInfoInts;
-        *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
-        if (R.far) *reinterpret_cast<GLB v2i *>(ri + 4) = (v2i){besti, soff};
+        row_record(rinfo, R.r, beg, end, tbbase, kpbase, R.far, besti, soff);
     }
     return besti;
 }
