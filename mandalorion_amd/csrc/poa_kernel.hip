@@ -1473,19 +1473,20 @@ __device__ __forceinline__ void row_store16(gu8 *base, int uoff, uint32_t lane_o
 }
 
 // A fast row's record in HBM (lane 0): {beg, end, tbbase, kpbase} and, for a row whose successor is
-// far, {argmax, spill offset}.  MANDO_RINFO_SADDR: the store in the saddr form (the slot's base in SGPRs,
-// the row's 32-bit byte offset in a VGPR) instead of a 64-bit address built on the scalar unit.
+// far, {argmax, spill offset}; stored in the saddr form (the slot's base in SGPRs, the row's 32-bit byte
+// offset in a VGPR) instead of through a 64-bit address built on the scalar unit per row: SGPR spills
+// 295 -> 267, DP 2,621 -> 2,547 cycles per row, kernel -2 % (profiles/r04x_rinfo_saddr_ab.txt).
 __device__ __forceinline__ void row_record(gint *rinfo, int r, int beg, int end, int tbbase, int kpbase, int far,
                                            int besti, int soff) {
-#ifdef MANDO_RINFO_SADDR
     const uint32_t off = (uint32_t)r * (uint32_t)(kRowInfoInts * 4);
     row_store(reinterpret_cast<gu8 *>(rinfo), off, (v4i){beg, end, tbbase, kpbase});
     if (far) row_store(reinterpret_cast<gu8 *>(rinfo), off + 16u, (v2i){besti, soff});
-#else
-    gint *ri = rinfo + (int64_t)r * kRowInfoInts;
-    *reinterpret_cast<GLB v4i *>(ri) = (v4i){beg, end, tbbase, kpbase};
-    if (far) *reinterpret_cast<GLB v2i *>(ri + 4) = (v2i){besti, soff};
-#endif
+}
+
+// The spill planes' base on the row path: held in SGPRs by the row loop, or (MANDO_LEAN_SGPR: sv null)
+// re-read from the slot in LDS by the rare rows that spill, so the loop holds two SGPRs fewer.
+__device__ __forceinline__ gint *sv_or_slot(const SharedState &sh, gint *sv) {
+    return sv ? sv : uniptr(sh.slot.sv);
 }
 
 // ---- 16-bit mode with scalar row control -------------------------------------------------------
@@ -1635,7 +1636,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     wr[HW + iw] = bfi(inv, kNeg2, E1);
     wr[2 * HW + iw] = bfi(inv, kNeg2, E2);
     if (R.far) {
-        gint *svp = sv + svbase;
+        gint *svp = sv_or_slot(sh, sv) + svbase;
         svp[j0] = (int)(short)(H & 0xffff);
         svp[j0 + 1] = (int)H >> 16;
         svp[kChunk + j0] = (int)(short)(E1 & 0xffff);
@@ -1762,7 +1763,7 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
     // the lower half's total (both F planes, biased) is the carry into the upper half
     const uint32_t carry = (uint32_t)__builtin_amdgcn_readlane((int)incv[0], kWave - 1);
     uint32_t *wr = reinterpret_cast<uint32_t *>(ring16_row<RW>(sh, R.r & (kRing16 - 1)));
-    gint *svp = sv + svbase;
+    gint *svp = sv_or_slot(sh, sv) + svbase;
     int amv = -2147483647 - 1;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -2007,7 +2008,7 @@ __device__ __forceinline__ int row16w_half(const SC &sc, gu8 *tb, gu8 *kp, gint 
     wr[HW + iw] = bfi(inv, kNeg2, E1);
     wr[2 * HW + iw] = bfi(inv, kNeg2, E2);
     if (R.far) {  // spill planes of a two-chunk row: stride RW (row_spill_width)
-        gint *svp = sv + svbase;
+        gint *svp = sv_or_slot(sh, sv) + svbase;
         svp[j0] = (int)(short)(H & 0xffff);
         svp[j0 + 1] = (int)H >> 16;
         svp[RW + j0] = (int)(short)(E1 & 0xffff);
@@ -2130,7 +2131,11 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         const PoaRunArgs a = args_of(sh);
         tb = s.tb;
         kp = s.kp;
+#ifdef MANDO_LEAN_SGPR
+        sv = nullptr;  // far rows re-read it (sv_or_slot), the batch refill re-reads desc
+#else
         sv = s.sv;
+#endif
         rinfo = s.rinfo;
         desc = s.desc;
         // a fast row allocates at most tbw + one chunk of slack
@@ -2158,7 +2163,12 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         {
             const int rn = b0 + kDescBatch;
             if (pl && rn < n && rn + (lane >> 1) < n) {
+#ifdef MANDO_LEAN_SGPR
+                const GLB int4 *g =
+                    reinterpret_cast<const GLB int4 *>(uniptr(sh.slot.desc) + (int64_t)rn * kDescInts + 4 * lane);
+#else
                 const GLB int4 *g = reinterpret_cast<const GLB int4 *>(desc + (int64_t)rn * kDescInts + 4 * lane);
+#endif
                 pf = make_int4(g->x, g->y, g->z, g->w);
             }
         }
