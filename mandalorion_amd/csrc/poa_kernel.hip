@@ -1483,12 +1483,6 @@ __device__ __forceinline__ void row_record(gint *rinfo, int r, int beg, int end,
     if (far) row_store(reinterpret_cast<gu8 *>(rinfo), off + 16u, (v2i){besti, soff});
 }
 
-// The spill planes' base on the row path: held in SGPRs by the row loop, or (MANDO_LEAN_SGPR: sv null)
-// re-read from the slot in LDS by the rare rows that spill, so the loop holds two SGPRs fewer.
-__device__ __forceinline__ gint *sv_or_slot(const SharedState &sh, gint *sv) {
-    return sv ? sv : uniptr(sh.slot.sv);
-}
-
 // ---- 16-bit mode with scalar row control -------------------------------------------------------
 // Everything that is uniform per row (descriptor, predecessor band records, band, fast-path
 // tests, allocation) lives in SGPRs: descriptors come straight from HBM through the scalar cache
@@ -1636,7 +1630,7 @@ __device__ __forceinline__ int row16_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *s
     wr[HW + iw] = bfi(inv, kNeg2, E1);
     wr[2 * HW + iw] = bfi(inv, kNeg2, E2);
     if (R.far) {
-        gint *svp = sv_or_slot(sh, sv) + svbase;
+        gint *svp = sv + svbase;
         svp[j0] = (int)(short)(H & 0xffff);
         svp[j0 + 1] = (int)H >> 16;
         svp[kChunk + j0] = (int)(short)(E1 & 0xffff);
@@ -1763,7 +1757,7 @@ __device__ __forceinline__ int row16w_vec(const SC &sc, gu8 *tb, gu8 *kp, gint *
     // the lower half's total (both F planes, biased) is the carry into the upper half
     const uint32_t carry = (uint32_t)__builtin_amdgcn_readlane((int)incv[0], kWave - 1);
     uint32_t *wr = reinterpret_cast<uint32_t *>(ring16_row<RW>(sh, R.r & (kRing16 - 1)));
-    gint *svp = sv_or_slot(sh, sv) + svbase;
+    gint *svp = sv + svbase;
     int amv = -2147483647 - 1;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -2008,7 +2002,7 @@ __device__ __forceinline__ int row16w_half(const SC &sc, gu8 *tb, gu8 *kp, gint 
     wr[HW + iw] = bfi(inv, kNeg2, E1);
     wr[2 * HW + iw] = bfi(inv, kNeg2, E2);
     if (R.far) {  // spill planes of a two-chunk row: stride RW (row_spill_width)
-        gint *svp = sv_or_slot(sh, sv) + svbase;
+        gint *svp = sv + svbase;
         svp[j0] = (int)(short)(H & 0xffff);
         svp[j0 + 1] = (int)H >> 16;
         svp[RW + j0] = (int)(short)(E1 & 0xffff);
@@ -2131,11 +2125,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         const PoaRunArgs a = args_of(sh);
         tb = s.tb;
         kp = s.kp;
-#ifdef MANDO_LEAN_SGPR
-        sv = nullptr;  // far rows re-read it (sv_or_slot), the batch refill re-reads desc
-#else
         sv = s.sv;
-#endif
         rinfo = s.rinfo;
         desc = s.desc;
         // a fast row allocates at most tbw + one chunk of slack
@@ -2163,12 +2153,7 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         {
             const int rn = b0 + kDescBatch;
             if (pl && rn < n && rn + (lane >> 1) < n) {
-#ifdef MANDO_LEAN_SGPR
-                const GLB int4 *g =
-                    reinterpret_cast<const GLB int4 *>(uniptr(sh.slot.desc) + (int64_t)rn * kDescInts + 4 * lane);
-#else
                 const GLB int4 *g = reinterpret_cast<const GLB int4 *>(desc + (int64_t)rn * kDescInts + 4 * lane);
-#endif
                 pf = make_int4(g->x, g->y, g->z, g->w);
             }
         }
