@@ -107,6 +107,10 @@ int mando_last_kernel_launches(mando_ctx *ctx);
  * plan: the locus text, clustering scratch and gathered reads of the chunks in flight are reserved
  * first, so no free-memory query races with the clustering thread's allocations. */
 int mando_ctx_set_poa_budget(mando_ctx *ctx, int64_t bytes);
+/* Restricts the ctx's streams (its own and its POA launch lanes) to the CUs whose bits are set in
+ * mask (n_words 32-bit words, bit i = CU i of the device; hipExtStreamCreateWithCUMask); n_words 0
+ * restores every CU.  Waits for the streams.  (The D driver's MANDO_POA_FREE_CUS experiment.) */
+int mando_ctx_set_cu_mask(mando_ctx *ctx, const uint32_t *mask, int32_t n_words);
 /* The device's HBM and the bytes this ctx's POA workspaces hold now (either may be NULL). */
 int mando_ctx_memory(mando_ctx *ctx, int64_t *total_bytes, int64_t *poa_ws_bytes);
 /* Workspace slots and budget of the most recent batch's launches by kind [narrow, wide, -S] (0: that

@@ -30,6 +30,7 @@ EXPORTED = (
     "mando_last_kernel_launches",
     "mando_ctx_set_poa_budget",
     "mando_ctx_memory",
+    "mando_ctx_set_cu_mask",
     "mando_poa_last_slots",
     "mando_orient_batch",
     "mando_selftest",
@@ -195,6 +196,7 @@ def load(path: str | None = None):
         lib.mando_last_kernel_launches.argtypes = [_P]
         lib.mando_ctx_set_poa_budget.argtypes = [_P, _I64]
         lib.mando_ctx_memory.argtypes = [_P, _P, _P]
+        lib.mando_ctx_set_cu_mask.argtypes = [_P, _P, ctypes.c_int32]
         lib.mando_poa_last_slots.argtypes = [_P, _P, _P]
         lib.mando_orient_batch.argtypes = [_P, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
         lib.mando_mt_permutation.argtypes = [ctypes.c_uint32, _P, _P, _I64, _P, _I64]
@@ -384,6 +386,16 @@ class Context:
     def set_poa_budget(self, nbytes: int) -> None:
         """Explicit cap on this ctx's POA workspaces (0: the library's default policy)."""
         check(self.lib.mando_ctx_set_poa_budget(self.handle, int(nbytes)))
+
+    def set_cu_mask(self, cus: "list[int] | None") -> None:
+        """Restrict this ctx's streams to the given CU indices (None: every CU)."""
+        if not cus:
+            check(self.lib.mando_ctx_set_cu_mask(self.handle, None, 0))
+            return
+        words = (ctypes.c_uint32 * ((max(cus) // 32) + 1))()
+        for c in cus:
+            words[c // 32] |= 1 << (c % 32)
+        check(self.lib.mando_ctx_set_cu_mask(self.handle, words, len(words)))
 
     def memory(self) -> tuple[int, int]:
         """(device HBM bytes, bytes held by this ctx's POA workspaces)."""

@@ -137,6 +137,7 @@ struct EncInit {
 struct mando_ctx {
     int device = 0;
     int n_cu = 256;
+    int n_cu_act = 256;  // CUs the ctx's streams may use (mando_ctx_set_cu_mask)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_launches = 0;
@@ -145,6 +146,7 @@ struct mando_ctx {
     int64_t poa_budget = 0;   // mando_ctx_set_poa_budget: explicit cap on the POA workspaces (0: default policy)
     int64_t last_slots[3] = {0, 0, 0};  // slots of the last batch's launches by kind (narrow, wide, seeded)
     int64_t last_budget[3] = {0, 0, 0}; // the workspace budget each of them was sized with
+    std::vector<uint32_t> cu_mask;      // mando_ctx_set_cu_mask (empty: every CU)
     DevBuf ws, counter, prof, o_gidx;
     DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
     DevBuf o_hits, o_strand, o_status;
@@ -278,7 +280,7 @@ size_t kind_want(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
     mando::occ_cap(a);
     const int per_cu = mando::poa_blocks_per_cu(a, cap);
-    const int64_t resident = (int64_t)ctx->n_cu * per_cu;
+    const int64_t resident = (int64_t)ctx->n_cu_act * per_cu;
     int64_t team = 1;
     if (seeded) team = std::max<int64_t>(1, std::min<int64_t>(mando::kMaxTeam, resident / std::max<int64_t>(1, n_groups)));
     const int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, resident / team));
@@ -365,11 +367,11 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     // up to kMaxTeam one-wave workgroups that align a read's windows side by side
     int team = 1;
     if (sp) {
-        const int64_t resident = (int64_t)ctx->n_cu * per_cu;
+        const int64_t resident = (int64_t)ctx->n_cu_act * per_cu;
         team = (int)std::max<int64_t>(1, std::min<int64_t>(mando::kMaxTeam, resident / std::max<int64_t>(1, n_groups)));
         if (const char *ev = getenv("MANDO_TEAM")) team = std::max(1, std::min(mando::kMaxTeam, atoi(ev)));
     }
-    int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, (int64_t)ctx->n_cu * per_cu / team));
+    int64_t teams = std::min<int64_t>(n_groups, std::max<int64_t>(1, (int64_t)ctx->n_cu_act * per_cu / team));
     if (granted > 0) {
         teams = std::max<int64_t>(1, std::min<int64_t>(teams, (int64_t)(budget / ((size_t)team * a.slot_bytes))));
         // a workspace that must grow gets 1/8 of headroom within the grant, so the next chunk's slightly
@@ -419,7 +421,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         // every resident workgroup must find a slot (a waiting one would hold its CU): one-group grids
         // only when the workspace covers the resident waves, or the groups
         const char *pe0 = getenv("MANDO_POA_PERSISTENT");
-        const bool enough = slots >= std::min<int64_t>(n_groups, (int64_t)ctx->n_cu * per_cu);
+        const bool enough = slots >= std::min<int64_t>(n_groups, (int64_t)ctx->n_cu_act * per_cu);
         if (!(pe0 && pe0[0] == '1') && enough) {
             a.one_group = 1;
             a.n_slots = (int32_t)slots;
@@ -639,6 +641,7 @@ int mando_ctx_create(int device_ordinal, mando_ctx **out) {
     mando_ctx *c = new mando_ctx();
     c->device = device_ordinal;
     c->n_cu = prop.multiProcessorCount;
+    c->n_cu_act = c->n_cu;
     c->total_mem = (int64_t)prop.totalGlobalMem;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -672,6 +675,31 @@ int mando_ctx_set_priority(mando_ctx *ctx, int high) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     (void)hipStreamDestroy(ctx->stream);
     ctx->stream = s;
+    return MANDO_OK;
+}
+
+int mando_ctx_set_cu_mask(mando_ctx *ctx, const uint32_t *mask, int32_t n_words) {
+    if (!ctx || n_words < 0 || (n_words > 0 && !mask)) return fail(MANDO_E_ARG, "mando_ctx_set_cu_mask: bad argument");
+    std::vector<uint32_t> m(mask, mask + n_words);
+    if (m == ctx->cu_mask) return MANDO_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto make = [&](hipStream_t &st) -> hipError_t {
+        if (st) {
+            const hipError_t e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return e;
+            (void)hipStreamDestroy(st);
+            st = nullptr;
+        }
+        return m.empty() ? hipStreamCreateWithFlags(&st, hipStreamNonBlocking)
+                         : hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data());
+    };
+    HIP_TRY(make(ctx->stream));
+    for (int k = 0; k < 2; ++k)
+        if (ctx->lane_stream[k]) HIP_TRY(make(ctx->lane_stream[k]));
+    ctx->cu_mask = m;
+    int on = 0;
+    for (int i = 0; i < ctx->n_cu && i / 32 < (int)m.size(); ++i) on += (m[(size_t)i / 32] >> (i % 32)) & 1u;
+    ctx->n_cu_act = m.empty() ? ctx->n_cu : std::max(1, on);
     return MANDO_OK;
 }
 
@@ -830,7 +858,11 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
             if (!ctx->ev_fork) {
                 HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
                 for (int k = 0; k < 2; ++k) {
-                    HIP_TRY(hipStreamCreateWithFlags(&ctx->lane_stream[k], hipStreamNonBlocking));
+                    if (ctx->cu_mask.empty())
+                        HIP_TRY(hipStreamCreateWithFlags(&ctx->lane_stream[k], hipStreamNonBlocking));
+                    else
+                        HIP_TRY(hipExtStreamCreateWithCUMask(&ctx->lane_stream[k], (uint32_t)ctx->cu_mask.size(),
+                                                             ctx->cu_mask.data()));
                     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_lane[k], hipEventDisableTiming));
                 }
             }

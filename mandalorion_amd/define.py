@@ -428,9 +428,14 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     n_poa = 2 if heavy else (int(os.environ.get("MANDO_POA_STREAMS", "1")) if len(parts) > 1 else 1)
     if dev_poa:
         span_text = [int(sizes[ix].sum()) for ix in parts]
+        # MANDO_POA_FREE_CUS=k (experiment): with several chunks, the POA streams leave the device's first k
+        # CUs to the next chunk's clustering and orientation kernels (which otherwise get CUs only as the
+        # running POA grid's workgroups retire)
+        free_cus = int(os.environ.get("MANDO_POA_FREE_CUS", "0")) if len(parts) > 1 else 0
         for k in range(n_poa):
             pctx = _lib.context(device, 3 * k)
             pctx.set_poa_budget(poa_budget(pctx.memory()[0], span_text) // n_poa)
+            pctx.set_cu_mask(list(range(free_cus, 256)) if free_cus > 0 else None)
 
     # with several chunks in flight, two cores stay with the GPU driver, assembly and compaction threads
     n_cpu = threads if threads > 0 else (os.cpu_count() or 1)
