@@ -61,6 +61,24 @@ def test_define_gpu_chunked_pipeline(gpu_ctx, tmp_path):
 
 
 @pytest.mark.gpu
+def test_define_gpu_chunks_with_poa_cu_mask(gpu_ctx, tmp_path, monkeypatch):
+    """MANDO_POA_FREE_CUS: the POA streams of a chunked call restricted to CUs 32.. (mando_ctx_set_cu_mask),
+    then a one-chunk call on every CU again: both write the one-chunk run's files."""
+    d = str(tmp_path)
+    loci = simdata.make_dataset(simdata.fixture_specs())
+    info = simdata.write_dataset(loci, d)
+    read = lambda f: open(os.path.join(d, f), "rb").read()
+    _run(d, info["gtf"])
+    one = read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")
+    monkeypatch.setenv("MANDO_POA_FREE_CUS", "32")
+    st = _run(d, info["gtf"], n_chunks=3)
+    assert st["chunks"] == 3
+    assert (read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")) == one
+    _run(d, info["gtf"])  # one chunk: the mask is lifted
+    assert (read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")) == one
+
+
+@pytest.mark.gpu
 def test_define_gpu_byte_capped_chunks_then_one_chunk(gpu_ctx, tmp_path, monkeypatch):
     """The byte-capped many-chunk branch (config 4's plan, thresholds lowered to this small input), then a
     one-chunk call in the same process: same files each time, and the one-chunk call's POA workspaces are
