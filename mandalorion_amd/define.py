@@ -125,6 +125,36 @@ def _roots_py(out_tmp: str, sizes: dict | None = None) -> list[str]:
     return sorted(roots, key=lambda x: (x.split("~")[0], int(x.split("~")[1])))
 
 
+def _shared_roots(out_tmp: str, comm) -> tuple[list[str], np.ndarray]:
+    """The root list and sizes of rank 0's scan on every rank (one all-gather; other ranks send nothing)."""
+    err = None
+    if comm.rank == 0:
+        try:
+            sa: list = []
+            roots = _roots(out_tmp, size_array=sa)
+            names = "\0".join(roots).encode("utf-8", "surrogateescape")
+            sizes = np.asarray(sa[0], dtype=np.int64)
+            blob = np.concatenate([np.array([len(roots), len(names)], np.int64).view(np.uint8),
+                                   sizes.view(np.uint8), np.frombuffer(names, np.uint8)])
+        except Exception as e:  # the other ranks learn of it (n = -1) instead of waiting for a list
+            err = e
+            blob = np.array([-1, 0], np.int64).view(np.uint8)
+    else:
+        blob = np.zeros(0, np.uint8)
+    allb, counts = comm.allgather_bytes(blob)
+    if err is not None:
+        raise err
+    if comm.rank == 0:
+        return roots, sizes
+    part = allb[:int(counts[0])]
+    n, nb = (int(x) for x in part[:16].view(np.int64))
+    if n < 0:
+        raise RuntimeError("rank 0 could not list the locus roots (its error is the first one raised)")
+    sizes = part[16:16 + 8 * n].view(np.int64).copy()
+    names = part[16 + 8 * n:16 + 8 * n + nb].tobytes().decode("utf-8", "surrogateescape")
+    return (names.split("\0") if n else []), sizes
+
+
 def _size_costs(sizes: np.ndarray) -> np.ndarray:
     """Per-locus POA cost estimate for the shard plan, from the file sizes the root scan returns (no
     per-file I/O): a locus of n reads of length L costs ~n L^2 (n L (2w+1) 1.1 L) and
@@ -374,9 +404,15 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
         _, left, right, poly = gtf.parse_genome(genome_file, wl)
     if rank == 0:
         gtf.write_polya_bed(out_path + "/polyAWhiteList.bed", poly, wl)
-    size_arr: list = []
-    roots = _roots(out_tmp, size_array=size_arr)
-    root_sizes = size_arr[0]
+    if world > 1 and hasattr(comm, "allgather_bytes"):
+        # one root scan (rank 0's, as the reference lists the roots once in its parent process,
+        # defineIsoforms.py:130-139), shared with the other ranks: eight ranks stat-ing the same 200,000
+        # files at once contend for the directory
+        roots, root_sizes = _shared_roots(out_tmp, comm)
+    else:
+        size_arr: list = []
+        roots = _roots(out_tmp, size_array=size_arr)
+        root_sizes = size_arr[0]
     # shard loci over ranks: LPT on the DP-cost estimate of SURVEY.md §8(e), results regathered in root order
     mine = list(range(len(roots)))
     if plan_world > 1:
