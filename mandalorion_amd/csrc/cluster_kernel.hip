@@ -235,11 +235,11 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
 // bits 0..3 <- the 0x80 bits of bytes 0..3 (no two partial products share a bit, so no carries)
 __device__ __forceinline__ uint32_t byte_bits(uint32_t z) { return ((z >> 7) * 0x00204081u) >> 21 & 0xfu; }
 // 16-bit masks of the tabs and the cs operators among the 16 bytes of v
-__device__ __forceinline__ uint32_t tab_mask16(const uint4 v) {
-    const uint32_t K = 0x09090909u;
+__device__ __forceinline__ uint32_t byte_mask16(const uint4 v, uint32_t K) {  // K: the byte in all four lanes
     return byte_bits(zero_bytes(v.x ^ K)) | byte_bits(zero_bytes(v.y ^ K)) << 4 |
            byte_bits(zero_bytes(v.z ^ K)) << 8 | byte_bits(zero_bytes(v.w ^ K)) << 12;
 }
+__device__ __forceinline__ uint32_t tab_mask16(const uint4 v) { return byte_mask16(v, 0x09090909u); }
 __device__ __forceinline__ uint32_t op_mask16(const uint4 v) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t om = 0;
@@ -352,33 +352,37 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
 #ifdef MANDO_CL_PHASES
     const uint64_t k1t0 = clock64();
 #endif
-    // 1. line ends: coalesced 16-byte chunks, newline masks compacted in text order
+    // 1. line ends: coalesced 16-byte chunks, newline masks compacted in text order; kLineUnroll
+    //    chunks per lane are loaded before any is scanned (one load in flight per lane left the wave
+    //    waiting on HBM latency: ~55 M cycles for a 22 MB config-2 locus)
+    constexpr int kLineUnroll = 16;
     const uintptr_t base = (uintptr_t)T & ~(uintptr_t)15;
     const int pad0 = (int)((uintptr_t)T - base);
     const int64_t nch = (pad0 + n + 15) >> 4;
     int32_t nl = 0;
-    for (int64_t c0 = 0; c0 < nch; c0 += 64) {
-        const int64_t c = c0 + ln();
-        uint32_t m = 0;
-        if (c < nch) {
-            const uint4 v = ((const uint4 *)base)[c];
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int64_t c00 = 0; c00 < nch; c00 += 64 * kLineUnroll) {
+        uint4 vv[kLineUnroll];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int64_t pos = c * 16 + k - pad0;
-                if (((w[k >> 2] >> ((k & 3) * 8)) & 0xffu) == '\n' && pos >= 0 && pos < n) m |= 1u << k;
+        for (int u = 0; u < kLineUnroll; ++u) {
+            const int64_t c = c00 + u * 64 + ln();
+            vv[u] = c < nch ? ((const uint4 *)base)[c] : uint4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < kLineUnroll; ++u) {
+            const int64_t c = c00 + u * 64 + ln();
+            // newline bytes at text positions [0, n) of the chunk (bytes k with 0 <= c * 16 + k - pad0 < n)
+            uint32_t m = c < nch ? byte_mask16(vv[u], 0x0a0a0a0au) & span_mask16(pad0 - c * 16, pad0 + n - c * 16) : 0u;
+            const int cnt = __popc(m);
+            const int incl = wincl(cnt);
+            int idx = nl + incl - cnt;
+            while (m) {
+                const int k = __ffs(m) - 1;
+                m &= m - 1;
+                if (idx < L.line_cap) A.line_end[idx] = (int32_t)(c * 16 + k - pad0);
+                ++idx;
             }
+            nl += __shfl(incl, 63);
         }
-        const int cnt = __popc(m);
-        const int incl = wincl(cnt);
-        int idx = nl + incl - cnt;
-        while (m) {
-            const int k = __ffs(m) - 1;
-            m &= m - 1;
-            if (idx < L.line_cap) A.line_end[idx] = (int32_t)(c * 16 + k - pad0);
-            ++idx;
-        }
-        nl += __shfl(incl, 63);
     }
     const bool tail = n > 0 && T[n - 1] != '\n';
     const int32_t nrec = nl + (tail ? 1 : 0);
@@ -420,8 +424,13 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
             int f8a = 0, f8b = 0, f9a = 0, f9b = 0, f10a = 0, f10b = 0, f11a = 0, f11b = 0, f12a = 0, f12b = 0;
             int f13a = 0, f13b = 0, f15a = 0, f15b = 0, f16a = 0, f16b = 0, f21a = 0, f21b = 0;
             bool done = false;
-            for (int i = a; i < b && !done; ++i) {
-                if (T[i] == '\t') {
+            // the tabs of [a, b) in order, from aligned 16-byte chunks (the chunks the line scan read)
+            for (uintptr_t ch = ((uintptr_t)(T + a)) & ~(uintptr_t)15; ch < (uintptr_t)(T + b) && !done; ch += 16) {
+                const int64_t c0 = (int64_t)(ch - (uintptr_t)T);
+                uint32_t tm = tab_mask16(*(const uint4 *)ch) & span_mask16(a - c0, b - c0);
+                while (tm && !done) {
+                    const int i = (int)(c0 + __ffs(tm) - 1);
+                    tm &= tm - 1;
                     switch (k) {
                         case 8: f8a = fs; f8b = i; break;
                         case 9: f9a = fs; f9b = i; break;
@@ -459,9 +468,16 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
                 R.same_chrom = R.chrom_len == L.chrom_len && bytes_eq(T + R.chrom_off, lchrom, L.chrom_len);
                 R.tstart = to_i64(T, f15a, f15b, ok);
                 R.tend = to_i64(T, f16a, f16b, ok);
-                int c18 = 0, c20 = 0;
-                for (int i = f18a; i < f18b; ++i) c18 += T[i] == ',';
-                for (int i = f20a; i < f20b; ++i) c20 += T[i] == ',';
+                // commas of columns 18 and 20, from aligned 16-byte chunks
+                auto commas = [&](int lo, int hi) {
+                    int c = 0;
+                    for (uintptr_t ch = ((uintptr_t)(T + lo)) & ~(uintptr_t)15; ch < (uintptr_t)(T + hi); ch += 16) {
+                        const int64_t c0 = (int64_t)(ch - (uintptr_t)T);
+                        c += __popc(byte_mask16(*(const uint4 *)ch, 0x2c2c2c2cu) & span_mask16(lo - c0, hi - c0));
+                    }
+                    return c;
+                };
+                const int c18 = commas(f18a, f18b), c20 = commas(f20a, f20b);
                 if (c18 != c20) ok = false;
                 nb = c18;
                 R.acc_lt = acc_below_09(T, f21a, f21b, ok);
