@@ -269,6 +269,12 @@ class Assembly:
 # the narrow launch 3,440 of its 3,840 slots, a persistent grid that held the CUs the next chunk's
 # orientation waited for)
 _CHUNK_BYTES = int(os.environ.get("MANDO_CHUNK_BYTES", str(4 << 30)))
+# inputs of at least _BIG_INPUT_BYTES (config 4 on one or two GPUs: 62 / 31 GB) run in 6 GiB chunks unless
+# MANDO_CHUNK_BYTES is set: config 4 14.2-14.4 s per step against 14.7 s with 4 GiB (5 / 7 GiB 14.4-14.6 s),
+# rank 0's 2-rank share 7.24-7.32 against 7.55-7.56 s; rank 0's 4-rank share (15.5 GB) had one 1 s slower
+# step in each 6 GiB run and keeps 4 GiB (profiles/r04cb_chunk_bytes_ab.txt)
+_BIG_INPUT_BYTES = 24 << 30
+_BIG_CHUNK_BYTES = _CHUNK_BYTES if "MANDO_CHUNK_BYTES" in os.environ else 6 << 30
 # inputs with at least this much locus text run in two chunks (or more, past _CHUNK_BYTES); 10,000
 # config-3 loci are 3.1 GB, 20,000 are 6.2 GB.  At 20,000 loci one chunk and two have the same mean step
 # (1.78 / 1.77 s over 24 steps each), but two chunks put chunk 2's clustering and orientation kernels
@@ -308,7 +314,7 @@ def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0) -> tuple[int, l
         if text_bytes < _TWO_CHUNK_BYTES or n_loci < _MIN_LOCI_CHUNKED:
             n_chunks = 1
         else:
-            k = -(-text_bytes // _CHUNK_BYTES)
+            k = -(-text_bytes // (_BIG_CHUNK_BYTES if text_bytes >= _BIG_INPUT_BYTES else _CHUNK_BYTES))
             if k > 1:
                 fracs = [(0.4 + i) / k for i in range(k)]
                 n_chunks = k + 1
