@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 D=gpurun_out/${TAG:-r04n}
 mkdir -p $D
-for w in config3 config4; do
+for w in ${WS:-config3 config4}; do
   st=3; [ $w = config4 ] && st=2
   timeout -k 10 900 python3 bench.py --no-cpu-baseline --workload $w --steps $st --warmup 1 > $D/bench_$w.json 2> $D/bench_$w.err || { echo "$w failed"; tail -5 $D/bench_$w.err; exit 1; }
   python3 -c "import json; d=json.load(open('$D/bench_$w.json')); c=d['config']; print('$w N=1', round(d['value']), round(d['ms_per_step'], 1), c['steps_s'], c['phases_rank0_s'], c.get('full_output_equals_oracle'))"
