@@ -300,6 +300,17 @@ int mando_split_loci(const char *psl_path, const char *out_dir, int32_t sort_lin
 int mando_list_roots(const char *dir, int32_t threads, char *names, int64_t names_cap, int64_t *sizes,
                      int64_t sizes_cap, int64_t *n_roots, int64_t *names_bytes);
 
+/* The same roots without their sizes: readdir's entry type decides where it can (only symlinks and
+ * entries of unknown type are stat'ed), so listing 200,000 loci costs one directory read.  The
+ * multi-rank driver lists on rank 0 and has every rank stat a slice (mando_root_sizes), replacing rank
+ * 0's 200,000 stat calls (defineIsoforms.py:130-139 as in mando_list_roots; same return codes). */
+int mando_list_root_names(const char *dir, char *names, int64_t names_cap, int64_t *n_roots, int64_t *names_bytes);
+
+/* sizes[i] = size of <dir>/<root i>.psl if that is a regular file (symlinks followed), else -1, for n
+ * NUL-terminated roots stored back to back in names (a slice of mando_list_root_names' output).
+ * threads <= 0: up to 16 threads. */
+int mando_root_sizes(const char *dir, const char *names, int64_t n, int32_t threads, int64_t *sizes);
+
 /* SAM -> PSL, replacing `python3 emtrey.py -i sam -o psl -m -t T`
  * (emtrey.py:31-193, called at Mando.py:336-341): one PSL line per mapped SAM record, input order, with
  * the accuracy / cs / read-sequence columns when mando_mode != 0.  threads <= 0: all cores. */

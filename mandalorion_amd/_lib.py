@@ -55,6 +55,8 @@ EXPORTED = (
     "mando_write_blocks",
     "mando_split_loci",
     "mando_list_roots",
+    "mando_list_root_names",
+    "mando_root_sizes",
     "mando_sam_to_psl",
     "mando_clean_psl",
     "mando_filter_default_params",
@@ -212,6 +214,8 @@ def load(path: str | None = None):
         lib.mando_split_loci.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _P, _P]
         lib.mando_list_roots.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, _P,
                                          ctypes.c_int64, _P, _P]
+        lib.mando_list_root_names.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64, _P, _P]
+        lib.mando_root_sizes.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, _P]
         lib.mando_sam_to_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, _P]
         lib.mando_clean_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, _P]
         lib.mando_filter_default_params.argtypes = [_P]

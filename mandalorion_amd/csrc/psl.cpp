@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <thread>
+#include <unordered_map>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -160,29 +161,40 @@ extern "C" int mando_split_loci(const char *psl_path, const char *out_dir, int32
     return MANDO_OK;
 }
 
-// mando_list_roots: the directory scan of defineIsoforms.py:130-139 (+ the file sizes the D driver
-// plans its chunks with) without a Python stat per file
-extern "C" int mando_list_roots(const char *dir, int32_t threads, char *names, int64_t names_cap, int64_t *sizes,
-                                int64_t sizes_cap, int64_t *n_roots, int64_t *names_bytes) {
+// The directory scan of defineIsoforms.py:130-139 (+ the file sizes the D driver plans its chunks
+// with) without a Python stat per file.  with_sizes == false (mando_list_root_names): the entry type
+// comes from readdir's d_type where it answers (DT_REG: a regular file, DT_DIR etc.: not one), and only
+// symlinks and DT_UNKNOWN entries are stat'ed (is_file() follows symlinks, as stat does).
+namespace {
+int list_roots(const char *dir, int32_t threads, bool with_sizes, char *names, int64_t names_cap, int64_t *sizes,
+               int64_t sizes_cap, int64_t *n_roots, int64_t *names_bytes) {
     if (!dir || !n_roots || !names_bytes || names_cap < 0 || sizes_cap < 0) return MANDO_E_ARG;
     DIR *d = opendir(dir);
     if (!d) return MANDO_E_ARG;
     std::vector<std::string> ents;
+    std::vector<int64_t> fsize;  // -2: not a regular file, -3: to be stat'ed
     while (struct dirent *e = readdir(d)) {
-        if (strstr(e->d_name, ".psl")) ents.emplace_back(e->d_name);
+        if (!strstr(e->d_name, ".psl")) continue;
+        ents.emplace_back(e->d_name);
+        fsize.push_back(with_sizes || e->d_type == DT_LNK || e->d_type == DT_UNKNOWN ? -3
+                        : e->d_type == DT_REG                                     ? 0
+                                                                                   : -2);
     }
     closedir(d);
     const std::string base = std::string(dir) + "/";
-    // regular files only (is_file() follows symlinks, as stat does), sizes from the same stat
-    std::vector<int64_t> fsize(ents.size(), -2);  // -2: not a regular file
+    // regular files only, sizes from the same stat
+    std::vector<size_t> todo;
+    for (size_t i = 0; i < ents.size(); ++i)
+        if (fsize[i] == -3) todo.push_back(i);
     int nt = threads > 0 ? threads : mando::usable_threads();
-    nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, ents.size() / 256 + 1));
+    nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, todo.size() / 256 + 1));
     const int dfd = open(dir, O_RDONLY | O_DIRECTORY);
     auto work = [&](int t) {
         struct stat st;
-        for (size_t i = (size_t)t; i < ents.size(); i += (size_t)nt) {
+        for (size_t k = (size_t)t; k < todo.size(); k += (size_t)nt) {
+            const size_t i = todo[k];
             const int r = dfd >= 0 ? fstatat(dfd, ents[i].c_str(), &st, 0) : stat((base + ents[i]).c_str(), &st);
-            if (r == 0 && S_ISREG(st.st_mode)) fsize[i] = (int64_t)st.st_size;
+            fsize[i] = (r == 0 && S_ISREG(st.st_mode)) ? (int64_t)st.st_size : -2;
         }
     };
     std::vector<std::thread> pool;
@@ -229,23 +241,83 @@ extern "C" int mando_list_roots(const char *dir, int32_t threads, char *names, i
         r.clen = t1;
         r.start = v;
     }
-    std::sort(roots.begin(), roots.end(), [](const Root &a, const Root &b) {
-        const std::string_view ca(a.name.data(), a.clen), cb(b.name.data(), b.clen);
-        if (ca != cb) return ca < cb;  // bytes (UTF-8 keeps code point order)
+    // order by (chromosome bytes, start, root): chromosomes ranked once (a few dozen distinct names), then
+    // an index sort on (rank, start) -- string compares only on the rare (chromosome, start) ties
+    std::unordered_map<std::string_view, int32_t> chrom_rank;
+    for (const Root &r : roots) chrom_rank.try_emplace(std::string_view(r.name.data(), r.clen), 0);
+    {
+        std::vector<std::string_view> ch;
+        ch.reserve(chrom_rank.size());
+        for (const auto &kv : chrom_rank) ch.push_back(kv.first);
+        std::sort(ch.begin(), ch.end());  // bytes (UTF-8 keeps code point order)
+        for (size_t k = 0; k < ch.size(); ++k) chrom_rank[ch[k]] = (int32_t)k;
+    }
+    struct Key {
+        int32_t chrom;
+        int32_t idx;
+        int64_t start;
+    };
+    std::vector<Key> key(roots.size());
+    for (size_t i = 0; i < roots.size(); ++i)
+        key[i] = Key{chrom_rank[std::string_view(roots[i].name.data(), roots[i].clen)], (int32_t)i, roots[i].start};
+    std::sort(key.begin(), key.end(), [&](const Key &a, const Key &b) {
+        if (a.chrom != b.chrom) return a.chrom < b.chrom;
         if (a.start != b.start) return a.start < b.start;
-        return a.name < b.name;
+        return roots[(size_t)a.idx].name < roots[(size_t)b.idx].name;
     });
     int64_t need = 0;
     for (const Root &r : roots) need += (int64_t)r.name.size() + 1;
     *n_roots = (int64_t)roots.size();
     *names_bytes = need;
-    if (need > names_cap || (int64_t)roots.size() > sizes_cap || (!names && need) || (!sizes && !roots.empty()))
+    if (need > names_cap || (int64_t)roots.size() > sizes_cap || (!names && need) || (with_sizes && !sizes && !roots.empty()))
         return MANDO_E_CAP;
     int64_t o = 0;
     for (size_t k = 0; k < roots.size(); ++k) {
-        memcpy(names + o, roots[k].name.c_str(), roots[k].name.size() + 1);
-        o += (int64_t)roots[k].name.size() + 1;
-        sizes[k] = roots[k].size;
+        const Root &r = roots[(size_t)key[k].idx];
+        memcpy(names + o, r.name.c_str(), r.name.size() + 1);
+        o += (int64_t)r.name.size() + 1;
+        if (with_sizes) sizes[k] = r.size;
     }
+    return MANDO_OK;
+}
+}  // namespace
+
+extern "C" int mando_list_roots(const char *dir, int32_t threads, char *names, int64_t names_cap, int64_t *sizes,
+                                int64_t sizes_cap, int64_t *n_roots, int64_t *names_bytes) {
+    return list_roots(dir, threads, true, names, names_cap, sizes, sizes_cap, n_roots, names_bytes);
+}
+
+extern "C" int mando_list_root_names(const char *dir, char *names, int64_t names_cap, int64_t *n_roots,
+                                     int64_t *names_bytes) {
+    return list_roots(dir, 0, false, names, names_cap, nullptr, INT64_MAX, n_roots, names_bytes);
+}
+
+// sizes[i] = size of <dir>/<root i>.psl when that is a regular file (symlinks followed), else -1; the
+// roots are n NUL-terminated names back to back (a slice of mando_list_root_names' output)
+extern "C" int mando_root_sizes(const char *dir, const char *names, int64_t n, int32_t threads, int64_t *sizes) {
+    if (!dir || n < 0 || (n && (!names || !sizes))) return MANDO_E_ARG;
+    std::vector<const char *> nm((size_t)n);
+    for (int64_t i = 0, o = 0; i < n; ++i) {
+        nm[(size_t)i] = names + o;
+        o += (int64_t)strlen(names + o) + 1;
+    }
+    int nt = threads > 0 ? threads : mando::usable_threads();
+    nt = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)nt, n / 256 + 1));
+    const int dfd = open(dir, O_RDONLY | O_DIRECTORY);
+    if (dfd < 0) return MANDO_E_ARG;
+    auto work = [&](int t) {
+        struct stat st;
+        std::string f;
+        for (int64_t i = t; i < n; i += nt) {
+            f.assign(nm[(size_t)i]);
+            f += ".psl";
+            sizes[i] = (fstatat(dfd, f.c_str(), &st, 0) == 0 && S_ISREG(st.st_mode)) ? (int64_t)st.st_size : -1;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto &th : pool) th.join();
+    close(dfd);
     return MANDO_OK;
 }

@@ -77,7 +77,52 @@ def test_list_roots_matches_reference_scan(tmp_path):
     s1, s2 = {}, {}
     assert define._roots(str(d), s1) == define._roots_py(str(d), s2)
     assert s1 == s2
+    # the multi-rank scan: names from one directory read, sizes stat'ed per slice
+    names = define._root_names(str(d))
+    assert names == define._roots_py(str(d))
+    assert define._root_sizes(str(d), names).tolist() == [s2.get(r, 0) for r in names]
     # a start Python's int() reads but the native parse does not: the reference's own parse decides
     (d / "chr3~ 0012~40.psl").write_bytes(b"")
     s1, s2 = {}, {}
     assert define._roots(str(d), s1) == define._roots_py(str(d), s2) and s1 == s2
+    assert define._root_names(str(d)) == define._roots_py(str(d))
+
+
+class _Gather:
+    """In-process all-gather over ranks run one after another: call c returns what every rank has
+    contributed to call c so far (so the last rank sees everything)."""
+
+    def __init__(self, rank, world, store):
+        self.rank, self.world, self.store, self.calls = rank, world, store, 0
+
+    def allgather_bytes(self, blob):
+        import numpy as np
+
+        c = self.store.setdefault(self.calls, {})
+        self.calls += 1
+        c[self.rank] = np.array(blob, dtype=np.uint8, copy=True)
+        parts = [c.get(r, np.zeros(0, np.uint8)) for r in range(self.world)]
+        return np.concatenate(parts), np.array([p.size for p in parts], dtype=np.int64)
+
+
+def test_shared_roots_slices_equal_one_scan(tmp_path):
+    """_shared_roots (rank 0 lists, every rank stats its slice) gives every rank the roots and sizes of
+    one mando_list_roots scan; a slice not yet contributed (rank 0 runs first here) is stat'ed locally."""
+    import numpy as np
+
+    from mandalorion_amd import define
+
+    d = tmp_path / "tmp_SS"
+    d.mkdir()
+    for i in range(1000):
+        (d / f"chr{i % 7}~{i * 37}~{i * 37 + 5}.psl").write_bytes(b"y" * (i % 23))
+    (d / "chr1~5~9.psl.bak").write_bytes(b"ab")
+    sa = []
+    ref = define._roots(str(d), size_array=sa)
+    store = {}
+    world = 3
+    out = [define._shared_roots(str(d), _Gather(r, world, store)) for r in range(world)]
+    for roots, sizes in out:
+        assert roots == ref and np.array_equal(sizes, sa[0])
+    assert [len(store[1][r]) for r in range(world)] == [8 * (len(ref) * (r + 1) // world - len(ref) * r // world)
+                                                         for r in range(world)]
