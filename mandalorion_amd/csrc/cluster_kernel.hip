@@ -1165,6 +1165,7 @@ struct LocusRun {
     int32_t hcb_ok;  // every coverage bin lies in the map, so B.hcb answers histo_cov
 #ifdef MANDO_CL_PHASES  // dev build: cycles inside find_peaks (coverage merge, permutation, cs queries)
     uint64_t pc_cov = 0, pc_perm = 0, pc_cs = 0, pc_csof = 0, pc_bins = 0, pc_side = 0;
+    uint64_t pc_sd_sort = 0, pc_sd_keys = 0, pc_sd_cand = 0;
     int32_t pc_cand = 0, pc_char = 0;
 #endif
 
@@ -1474,7 +1475,14 @@ struct LocusRun {
         wsync();
         // large sides (config 2's ~35k entries): a counting sort over the map instead of the bitonic
         // network's log^2 passes
+#ifdef MANDO_CL_PHASES
+        const uint64_t ts0 = clock64();
+#endif
         if (H <= kSortTile || !count_sort_side(d)) sort_u64(d.sk, d.P);
+#ifdef MANDO_CL_PHASES
+        const uint64_t ts1 = clock64();
+        pc_sd_sort += ts1 - ts0;
+#endif
         // records in sorted order; distinct-key flags; strand counts per key (lane per entry: the key
         // index of entry i is the number of distinct keys up to i, minus one)
         for (int64_t i = ln(); i < 3 * (int64_t)H; i += 64) d.upmb[i] = 0;
@@ -1507,6 +1515,10 @@ struct LocusRun {
         }
         d.nkeys = kc;
         wsync();
+#ifdef MANDO_CL_PHASES
+        const uint64_t ts2 = clock64();
+        pc_sd_keys += ts2 - ts1;
+#endif
         for (int u0 = 0; u0 < kc; u0 += 64) {
             const int u = u0 + ln();
             if (u < kc) d.ucnt[u] = (u + 1 < kc ? d.ulo[u + 1] : H) - d.ulo[u];
@@ -1528,6 +1540,9 @@ struct LocusRun {
         for (int64_t i = cc + ln(); i < d.P; i += 64) d.cand[i] = ~0ull;
         wsync();
         sort_u64(d.cand, pow2ge(cc));
+#ifdef MANDO_CL_PHASES
+        pc_sd_cand += clock64() - ts2;
+#endif
     }
 
     __device__ int find_key(const Side &d, int64_t pos) const {
@@ -2491,6 +2506,9 @@ struct LocusRun {
             printf("[K2 peaks] n %d: candidates %d characterized %d | cov %.2f perm %.2f cs %.2f Mcyc | collect: cs_of "
                    "%.2f bins %.2f sides %.2f\n", n, pc_cand, pc_char, pc_cov * 1e-6, pc_perm * 1e-6, pc_cs * 1e-6,
                    pc_csof * 1e-6, pc_bins * 1e-6, pc_side * 1e-6);
+        if (ln() == 0)
+            printf("[K2 sides] n %d: H %d %d | sort %.2f keys %.2f cand %.2f Mcyc\n", n, B.s[0].H, B.s[1].H,
+                   pc_sd_sort * 1e-6, pc_sd_keys * 1e-6, pc_sd_cand * 1e-6);
 #endif
 #undef MANDO_PH
     }
