@@ -206,11 +206,22 @@ def _size_costs(sizes: np.ndarray) -> np.ndarray:
     return sz * sz
 
 
-def _lpt_owner(cost: np.ndarray, world: int, head: int = 64) -> np.ndarray:
+# the shard plan's loci after the LPT head: "snake" (default: round-robin by load) or "ranges" --
+# contiguous runs of roots, so that each rank's blocks of the output files are one region and the ranks
+# place them into disjoint pages (8 processes placing 1 GB into one file through shared mappings: 0.35-0.39
+# s for contiguous ranges against 0.52-0.60 s for interleaved roots).  Rehearsed on config 4 (r04rg,
+# DESIGN.md §6) the ranges balance the POA worse (8 ranks: POA 1.42-1.69 s against 1.44-1.52 s; 2 ranks:
+# 6.65 / 6.00 s against 5.89 / 5.90 s), so they stay opt-in
+_SHARD_REST = os.environ.get("MANDO_SHARD_PLAN", "snake")
+
+
+def _lpt_owner(cost: np.ndarray, world: int, head: int = 64, rest_plan: str | None = None) -> np.ndarray:
     """The shard plan (every rank computes the same one): loci by cost, descending; the heaviest
-    head x world go to the least-loaded rank one at a time (LPT: they set the launches' floors), the rest
-    in a snake over the ranks ordered by load (a Python argmin per locus took 0.4-0.8 s for 200,000 loci
-    on every rank, r04)."""
+    head x world go to the least-loaded rank one at a time (LPT: they set the launches' floors).  The
+    rest ("ranges"): in root order, cut into one contiguous range per rank, rank r's range holding the
+    cost that brings its load to the mean (a locus belongs to the range its cost midpoint falls in);
+    or ("snake") in a snake over the ranks ordered by load.  Vectorised: a Python argmin per locus took
+    0.4-0.8 s for 200,000 loci on every rank (r04)."""
     import heapq
 
     order = np.argsort(-cost, kind="stable")
@@ -222,10 +233,24 @@ def _lpt_owner(cost: np.ndarray, world: int, head: int = 64) -> np.ndarray:
         owner[i] = r
         heapq.heapreplace(h, (ld + float(cost[i]), r))
     rest = order[k:]
-    if len(rest):
+    if len(rest) and (rest_plan or _SHARD_REST) == "snake":
         by_load = np.array([r for _, r in sorted(h)], dtype=np.int64)
         m = np.arange(len(rest)) % (2 * world)
         owner[rest] = by_load[np.where(m < world, m, 2 * world - 1 - m)]
+    elif len(rest):
+        rest = np.sort(rest)
+        c = np.asarray(cost, dtype=np.float64)[rest]
+        loads = np.zeros(world)
+        for ld, r in h:
+            loads[r] = ld
+        if not c.sum() > 0:  # no cost information: equal locus counts
+            c, loads = np.ones(len(rest)), np.zeros(world)
+        cap = np.maximum(0.0, (loads.sum() + c.sum()) / world - loads)
+        cap *= c.sum() / cap.sum()
+        cuts = np.searchsorted(np.cumsum(c) - c / 2, np.cumsum(cap)[:-1])
+        cuts = np.concatenate([[0], cuts, [len(rest)]])
+        for r in range(world):
+            owner[rest[cuts[r]:cuts[r + 1]]] = r
     return owner
 
 
