@@ -64,6 +64,15 @@ def poa_sources_sha() -> str:
     return h.hexdigest()
 
 
+def plan_signature() -> dict:
+    """The D driver's chunk-plan constants: a PMC file measured under another plan describes other launches."""
+    from mandalorion_amd import define
+
+    return {"chunk_bytes": define._CHUNK_BYTES, "big_chunk_bytes": define._BIG_CHUNK_BYTES,
+            "big_input_bytes": define._BIG_INPUT_BYTES, "two_chunk_bytes": define._TWO_CHUNK_BYTES,
+            "min_loci_chunked": define._MIN_LOCI_CHUNKED}
+
+
 def host_cores() -> dict:
     """The host CPUs this process may use: affinity, capped by the cgroup CPU quota (cpu.max), and the
     machine's count (os.cpu_count(), which on the GPU box is the whole host, many times our share)."""
@@ -406,15 +415,18 @@ def main():
     if SHARE is not None:  # one rank's load: its own records
         records = stats[-1]["records"]
 
-    # roofline of the dominant kernel (POA), from this rank's launches of the last timed step:
-    # algorithmic bytes per launch = 1 B traceback per DP cell + each read once + each consensus once
+    # roofline of the dominant kernel (POA), from this rank's launches of the last timed step, per step:
+    # algorithmic bytes = 1 B traceback per DP cell + each read once + each consensus once, over the POA
+    # launches' HIP-event time (a batch's launch kinds run side by side: its time runs from the first
+    # launch's start to the last one's end)
     la = st["poa_launches"]
     n_launch = sum(x["launches"] for x in la)
     alg = sum(x["cells"] + x["read_bytes"] + x["cons_bytes"] for x in la)
     k_ms = sum(x["kernel_ms"] for x in la)
-    achieved = (alg / max(1, n_launch)) / (k_ms / max(1, n_launch) / 1e3) / 1e9 if k_ms > 0 else 0.0
-    # HBM traffic from the PMC passes (tools/pmc_traffic.py), only when they were measured on this workload
-    # and on the POA sources benchmarked now
+    achieved = alg / (k_ms / 1e3) / 1e9 if k_ms > 0 else 0.0
+    # HBM traffic per step from the PMC passes (tools/pmc_traffic.py: one step's POA dispatches), only when
+    # they were measured on this workload, on the POA sources benchmarked now, under the same chunk plan,
+    # chunk count and POA dispatch count as this step
     traffic, traffic_raw, pmc_note = None, None, "no PMC file"
     if os.path.exists(args.pmc_json):
         try:
@@ -423,10 +435,16 @@ def main():
                 pmc_note = f"PMC file is for {pm.get('workload')}"
             elif pm.get("poa_sources_sha256") != poa_sources_sha():
                 pmc_note = "PMC file measured on other POA sources (dropped)"
+            elif pm.get("plan") != plan_signature() or pm.get("chunks") != st.get("chunks"):
+                pmc_note = (f"PMC file measured under another chunk plan ({pm.get('chunks')} chunks, "
+                            f"{pm.get('plan')}; this step: {st.get('chunks')}) (dropped)")
+            elif pm.get("poa_dispatches_per_step") != n_launch:
+                pmc_note = (f"PMC file saw {pm.get('poa_dispatches_per_step')} POA dispatches per step, this "
+                            f"step {n_launch} (dropped)")
             else:
-                traffic = pm.get("hbm_bytes_per_launch")
-                traffic_raw = pm.get("hbm_bytes_per_launch_raw")
-                pmc_note = f"PMC passes of commit {pm.get('commit', '?')}"
+                traffic = pm.get("hbm_bytes_per_step")
+                traffic_raw = pm.get("hbm_bytes_per_step_raw")
+                pmc_note = f"PMC passes of commit {pm.get('commit', '?')}, {n_launch} POA dispatches per step"
         except Exception as e:  # noqa: BLE001
             pmc_note = f"unreadable PMC file: {e}"
 
@@ -439,10 +457,10 @@ def main():
         if not parity:
             raise SystemExit("GPU D-module output differs from the CPU restatement on the baseline sample")
 
-    # the limiter from measurement: the HBM bytes the PMC passes saw per launch over the launch time, as a
-    # fraction of peak; well below peak the kernel is bound by instruction issue / latency (SQ counters,
-    # DESIGN.md 3.1), not by HBM
-    hbm_util = (traffic / (k_ms / max(1, n_launch) / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic and k_ms > 0 else None
+    # the limiter from measurement: the HBM bytes the PMC passes saw per step over this step's POA launch
+    # time, as a fraction of peak; well below peak the kernel is bound by instruction issue / latency (SQ
+    # counters), not by HBM
+    hbm_util = (traffic / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic and k_ms > 0 else None
     bound = "hbm" if hbm_util is not None and hbm_util >= 0.6 else "issue"
     out = {
         "metric": "consensus reads/s (whole node): PSL records / wall s of Mando.py -M D",
@@ -496,6 +514,9 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_raw": traffic_raw,
+            "traffic_unit": "HBM bytes per step (all POA dispatches of one step)",
+            "achieved_unit": "algorithmic GB/s over the step's POA launch time",
+            "poa_dispatches_per_step": n_launch,
             "traffic_source": pmc_note,
             "kernel": "poa_kernel",
             "note": "integer DP, no MFMA; the kernel is issue/latency-bound (SQ counters: DESIGN.md §3.1)",

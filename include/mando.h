@@ -90,11 +90,6 @@ int mando_poa_batch_device(mando_ctx *ctx, const mando_poa_params *params, const
                            int32_t *d_status);
 int mando_ctx_sync(mando_ctx *ctx);
 
-/* Gives the ctx's stream the device's highest (high != 0) or default scheduling priority: work queued
- * on it is dispatched ahead of other streams' pending workgroups (the D pipeline's clustering and
- * orientation streams, whose kernels would otherwise queue behind a POA grid).  Waits for the stream. */
-int mando_ctx_set_priority(mando_ctx *ctx, int high);
-
 /* Device-time of the most recent POA / orientation launch on the ctx stream, from HIP events
  * recorded around the kernel on that stream (milliseconds). */
 float mando_last_kernel_ms(mando_ctx *ctx);
@@ -107,12 +102,17 @@ int mando_last_kernel_launches(mando_ctx *ctx);
  * plan: the locus text, clustering scratch and gathered reads of the chunks in flight are reserved
  * first, so no free-memory query races with the clustering thread's allocations. */
 int mando_ctx_set_poa_budget(mando_ctx *ctx, int64_t bytes);
-/* Restricts the ctx's streams (its own and its POA launch lanes) to the CUs whose bits are set in
- * mask (n_words 32-bit words, bit i = CU i of the device; hipExtStreamCreateWithCUMask); n_words 0
- * restores every CU.  Waits for the streams.  (The D driver's MANDO_POA_FREE_CUS experiment.) */
-int mando_ctx_set_cu_mask(mando_ctx *ctx, const uint32_t *mask, int32_t n_words);
 /* The device's HBM and the bytes this ctx's POA workspaces hold now (either may be NULL). */
 int mando_ctx_memory(mando_ctx *ctx, int64_t *total_bytes, int64_t *poa_ws_bytes);
+/* Free and total HBM of a device now (hipMemGetInfo; either may be NULL). */
+int mando_device_memory(int device_ordinal, int64_t *free_bytes, int64_t *total_bytes);
+/* The clustering's cached device buffers on a device (the idle locus-text buffers and the per-context
+ * scratch, kept between calls for reuse): frees idle text buffers larger than text_cap_max bytes and,
+ * when the scratch of the device's contexts holds more than scratch_max bytes, all of that scratch
+ * (negative limits: keep).  held_bytes (may be NULL) receives what the caches hold afterwards.  The D
+ * driver calls it at the start of a call whose chunk plan is smaller than an earlier call's, so that
+ * its HBM plan (mando_ctx_set_poa_budget) is not undercut by buffers a larger plan left behind. */
+int mando_cache_trim(int device_ordinal, int64_t text_cap_max, int64_t scratch_max, int64_t *held_bytes);
 /* Workspace slots and budget of the most recent batch's launches by kind [narrow, wide, -S] (0: that
  * kind did not run); either array may be NULL, else holds 3 entries. */
 int mando_poa_last_slots(mando_ctx *ctx, int64_t *slots, int64_t *budgets);

@@ -25,12 +25,12 @@ EXPORTED = (
     "mando_poa_batch",
     "mando_poa_batch_device",
     "mando_ctx_sync",
-    "mando_ctx_set_priority",
     "mando_last_kernel_ms",
     "mando_last_kernel_launches",
     "mando_ctx_set_poa_budget",
     "mando_ctx_memory",
-    "mando_ctx_set_cu_mask",
+    "mando_device_memory",
+    "mando_cache_trim",
     "mando_poa_last_slots",
     "mando_orient_batch",
     "mando_selftest",
@@ -190,7 +190,6 @@ def load(path: str | None = None):
         lib.mando_ctx_destroy.argtypes = [_P]
         lib.mando_ctx_destroy.restype = None
         lib.mando_ctx_sync.argtypes = [_P]
-        lib.mando_ctx_set_priority.argtypes = [_P, ctypes.c_int]
         lib.mando_poa_batch.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]
         lib.mando_poa_batch_device.argtypes = [_P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P]
         lib.mando_last_kernel_ms.argtypes = [_P]
@@ -198,7 +197,8 @@ def load(path: str | None = None):
         lib.mando_last_kernel_launches.argtypes = [_P]
         lib.mando_ctx_set_poa_budget.argtypes = [_P, _I64]
         lib.mando_ctx_memory.argtypes = [_P, _P, _P]
-        lib.mando_ctx_set_cu_mask.argtypes = [_P, _P, ctypes.c_int32]
+        lib.mando_device_memory.argtypes = [ctypes.c_int, _P, _P]
+        lib.mando_cache_trim.argtypes = [ctypes.c_int, _I64, _I64, _P]
         lib.mando_poa_last_slots.argtypes = [_P, _P, _P]
         lib.mando_orient_batch.argtypes = [_P, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
         lib.mando_mt_permutation.argtypes = [ctypes.c_uint32, _P, _P, _I64, _P, _I64]
@@ -391,16 +391,6 @@ class Context:
         """Explicit cap on this ctx's POA workspaces (0: the library's default policy)."""
         check(self.lib.mando_ctx_set_poa_budget(self.handle, int(nbytes)))
 
-    def set_cu_mask(self, cus: "list[int] | None") -> None:
-        """Restrict this ctx's streams to the given CU indices (None: every CU)."""
-        if not cus:
-            check(self.lib.mando_ctx_set_cu_mask(self.handle, None, 0))
-            return
-        words = (ctypes.c_uint32 * ((max(cus) // 32) + 1))()
-        for c in cus:
-            words[c // 32] |= 1 << (c % 32)
-        check(self.lib.mando_ctx_set_cu_mask(self.handle, words, len(words)))
-
     def memory(self) -> tuple[int, int]:
         """(device HBM bytes, bytes held by this ctx's POA workspaces)."""
         tot, ws = ctypes.c_int64(0), ctypes.c_int64(0)
@@ -422,13 +412,6 @@ class Context:
 _ctx_cache: dict[tuple[int, int], Context] = {}
 
 
-# slots whose streams can get the high scheduling priority (MANDO_STREAM_PRIO=1): orientation (1) and
-# clustering (4), whose short kernels sit on the D pipeline's critical path between two POA grids.  Off
-# by default: measured on config 3, the clustering kernels then ran during the first POA grid (0.53 ->
-# 0.13 s) but the POA grids slowed down 2-3x while high-priority work was pending (2.40 -> 3.90 s).
-HIGH_PRIORITY_SLOTS = (1, 4)
-
-
 def context(device: int = 0, slot: int = 0) -> Context:
     """Per-(device, slot) context: each slot owns a HIP stream and its device buffers, so two host threads
     can drive the same GPU at once (the D pipeline orients chunk k+1 on slot 1 while chunk k's POA runs
@@ -436,7 +419,22 @@ def context(device: int = 0, slot: int = 0) -> Context:
     c = _ctx_cache.get((device, slot))
     if c is None or c.handle is None:
         c = Context(device)
-        if slot in HIGH_PRIORITY_SLOTS and os.environ.get("MANDO_STREAM_PRIO", "0") == "1":
-            check(c.lib.mando_ctx_set_priority(c.handle, 1))
         _ctx_cache[(device, slot)] = c
     return c
+
+
+def device_memory(device: int = 0) -> tuple[int, int]:
+    """(free, total) HBM bytes of a device now."""
+    lib = load()
+    f, t = ctypes.c_int64(0), ctypes.c_int64(0)
+    check(lib.mando_device_memory(int(device), ctypes.byref(f), ctypes.byref(t)))
+    return f.value, t.value
+
+
+def cache_trim(device: int, text_cap_max: int = -1, scratch_max: int = -1) -> int:
+    """Frees the clustering's cached device buffers above the given sizes (mando_cache_trim); returns
+    the bytes the caches hold afterwards."""
+    lib = load()
+    held = ctypes.c_int64(0)
+    check(lib.mando_cache_trim(int(device), int(text_cap_max), int(scratch_max), ctypes.byref(held)))
+    return held.value

@@ -137,7 +137,7 @@ struct EncInit {
 struct mando_ctx {
     int device = 0;
     int n_cu = 256;
-    int n_cu_act = 256;  // CUs the ctx's streams may use (mando_ctx_set_cu_mask)
+    int n_cu_act = 256;  // CUs the ctx's streams may use
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_launches = 0;
@@ -146,7 +146,6 @@ struct mando_ctx {
     int64_t poa_budget = 0;   // mando_ctx_set_poa_budget: explicit cap on the POA workspaces (0: default policy)
     int64_t last_slots[3] = {0, 0, 0};  // slots of the last batch's launches by kind (narrow, wide, seeded)
     int64_t last_budget[3] = {0, 0, 0}; // the workspace budget each of them was sized with
-    std::vector<uint32_t> cu_mask;      // mando_ctx_set_cu_mask (empty: every CU)
     DevBuf ws, counter, prof, o_gidx;
     DevBuf seq, seq_off, grp_off, gorder, cons, cons_off, cons_len, cells, status;
     DevBuf o_hits, o_strand, o_status;
@@ -185,13 +184,6 @@ namespace {
 
 // the workspace of a POA launch kind (0 narrow, 1 wide, 2 -S)
 DevBuf &kind_ws(mando_ctx *ctx, int kind) { return kind == 0 ? ctx->ws : ctx->lane_ws[kind - 1]; }
-
-// one wave that waits `ticks` of the 100 MHz real-time counter (the stagger between POA launch kinds)
-constexpr int64_t kStaggerTicks = 5000;  // 50 us
-__global__ void stagger_kernel(int64_t ticks) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(10);
-}
 
 constexpr int kMaxWavesPerCu = 16;  // upper bound on resident POA waves per CU
 // groups whose band 2w + 1 (at their mean read length) is wider than this run in the wide-ring
@@ -236,8 +228,7 @@ mando::PoaCaps plan_caps(const mando_poa_params &p, int64_t max_first, int64_t m
     // 0.75 predecessor bytes, but 9 need more than 0.75 spill ints (73 more than 0.5): any re-run is a
     // second launch that pays its heaviest group's one-wave latency again (POA 1.26 -> 1.58 s), so the
     // spill planes keep their room.
-    static const double kp0 = getenv("MANDO_KPC_FRAC") ? atof(getenv("MANDO_KPC_FRAC")) : 0.75;
-    static const double sv0 = getenv("MANDO_SVC_FRAC") ? atof(getenv("MANDO_SVC_FRAC")) : 1.5;
+    constexpr double kp0 = 0.75, sv0 = 1.5;
     c.KPC = attempt == 0 ? (int64_t)(kp0 * (double)c.TBC) : (attempt == 1 ? 3 * c.TBC / 2 : 3 * c.TBC);
     c.SVC = attempt == 0 ? (int64_t)(sv0 * (double)c.TBC) : (attempt == 1 ? 3 * c.TBC / 2 : 3 * c.TBC);
     // the kernel keeps its per-read usage counters in 32 bits
@@ -278,7 +269,6 @@ size_t kind_want(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.e2 = p.gap_ext2;
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
-    mando::occ_cap(a);
     const int per_cu = mando::poa_blocks_per_cu(a, cap);
     const int64_t resident = (int64_t)ctx->n_cu_act * per_cu;
     int64_t team = 1;
@@ -298,7 +288,7 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
                  const int32_t *d_gorder, int64_t n_groups, uint8_t *d_cons,
                  const int64_t *d_cons_off, int32_t *d_cons_len, int64_t *d_cells,
                  int32_t *d_status, int max_per_cu, const SeedPlan *sp = nullptr, bool ev_start = true,
-                 bool ev_end = true, int lane = 0, int kind = 0, size_t granted = 0, int32_t n_heavy = 0) {
+                 bool ev_end = true, int lane = 0, int kind = 0, size_t granted = 0) {
     // lane k > 0: the context's extra stream k - 1 (launches of other kinds alongside); the workspace
     // belongs to the launch kind (kind_ws), so a kind keeps its workspace from batch to batch
     hipStream_t stream = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
@@ -321,7 +311,6 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     a.grp_off = d_grp_off;
     a.gorder = d_gorder;
     a.n_groups = (int32_t)n_groups;
-    a.n_heavy = sp ? 0 : n_heavy;
     a.cons = d_cons;
     a.cons_off = d_cons_off;
     a.cons_len = d_cons_len;
@@ -361,7 +350,6 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
     // resident one-wave workgroups per CU at this batch's LDS footprint (occupancy API)
     int cap = max_per_cu;
     if (const char *ev = getenv("MANDO_WAVES_PER_CU")) cap = std::max(1, atoi(ev));
-    mando::occ_cap(a);
     const int per_cu = mando::poa_blocks_per_cu(a, cap);
     // -S teams: when the seeded groups are too few to fill the resident waves, each gets a team of
     // up to kMaxTeam one-wave workgroups that align a read's windows side by side
@@ -384,8 +372,14 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
             teams = std::max<int64_t>(1, (int64_t)(ws.bytes / ((size_t)team * a.slot_bytes)));
         } else if (ws.bytes < need) {
             ws.release();
-            int rc0 = ws.ensure(std::min(budget, need + need / 8));
-            if (rc0) return rc0;
+            const int rc0 = ws.ensure(std::min(budget, need + need / 8));
+            if (rc0 == MANDO_E_NOMEM) {
+                // HBM held outside this grant (another context or process on the device): the halving
+                // retry below finds the slots that fit, as the free-memory path does
+                (void)hipGetLastError();
+            } else if (rc0) {
+                return rc0;
+            }
         }
     } else {
         while (teams > 1 && (size_t)(teams * team * a.slot_bytes) > budget) teams /= 2;
@@ -412,17 +406,17 @@ int launch_batch(mando_ctx *ctx, const mando_poa_params &p, const mando::PoaCaps
         HIP_TRY(hipMemsetAsync(boxb.p, 0, (size_t)teams * sizeof(mando::TeamBox), stream));
         a.boxes = boxb.as<mando::TeamBox>();
     }
-    // unseeded launches run one workgroup per group by default (MANDO_POA_PERSISTENT=1: persistent
-    // slots): as groups finish, the CUs are shared with the other kernels in flight (clustering and
-    // orientation of later chunks, other POA launches) instead of being held to the launch's end
+    // unseeded launches run one workgroup per group when the slots cover the resident waves (else the
+    // persistent grid over the slots): as groups finish, the CUs are shared with the other kernels in
+    // flight (clustering and orientation of later chunks, other POA launches) instead of being held to
+    // the launch's end
     int64_t grid = slots;
     a.one_group = 0;
     if (!sp) {
         // every resident workgroup must find a slot (a waiting one would hold its CU): one-group grids
         // only when the workspace covers the resident waves, or the groups
-        const char *pe0 = getenv("MANDO_POA_PERSISTENT");
         const bool enough = slots >= std::min<int64_t>(n_groups, (int64_t)ctx->n_cu_act * per_cu);
-        if (!(pe0 && pe0[0] == '1') && enough) {
+        if (enough) {
             a.one_group = 1;
             a.n_slots = (int32_t)slots;
             grid = n_groups;
@@ -665,44 +659,6 @@ int mando_ctx_sync(mando_ctx *ctx) {
     return MANDO_OK;
 }
 
-int mando_ctx_set_priority(mando_ctx *ctx, int high) {
-    if (!ctx) return fail(MANDO_E_ARG, "null ctx");
-    HIP_TRY(hipSetDevice(ctx->device));
-    int least = 0, greatest = 0;
-    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    hipStream_t s = nullptr;
-    HIP_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    (void)hipStreamDestroy(ctx->stream);
-    ctx->stream = s;
-    return MANDO_OK;
-}
-
-int mando_ctx_set_cu_mask(mando_ctx *ctx, const uint32_t *mask, int32_t n_words) {
-    if (!ctx || n_words < 0 || (n_words > 0 && !mask)) return fail(MANDO_E_ARG, "mando_ctx_set_cu_mask: bad argument");
-    std::vector<uint32_t> m(mask, mask + n_words);
-    if (m == ctx->cu_mask) return MANDO_OK;
-    HIP_TRY(hipSetDevice(ctx->device));
-    auto make = [&](hipStream_t &st) -> hipError_t {
-        if (st) {
-            const hipError_t e = hipStreamSynchronize(st);
-            if (e != hipSuccess) return e;
-            (void)hipStreamDestroy(st);
-            st = nullptr;
-        }
-        return m.empty() ? hipStreamCreateWithFlags(&st, hipStreamNonBlocking)
-                         : hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data());
-    };
-    HIP_TRY(make(ctx->stream));
-    for (int k = 0; k < 2; ++k)
-        if (ctx->lane_stream[k]) HIP_TRY(make(ctx->lane_stream[k]));
-    ctx->cu_mask = m;
-    int on = 0;
-    for (int i = 0; i < ctx->n_cu && i / 32 < (int)m.size(); ++i) on += (m[(size_t)i / 32] >> (i % 32)) & 1u;
-    ctx->n_cu_act = m.empty() ? ctx->n_cu : std::max(1, on);
-    return MANDO_OK;
-}
-
 float mando_last_kernel_ms(mando_ctx *ctx) {
     if (!ctx || !ctx->timed) return -1.0f;
     float ms = -1.0f;
@@ -723,6 +679,18 @@ int mando_ctx_memory(mando_ctx *ctx, int64_t *total_bytes, int64_t *poa_ws_bytes
     if (!ctx) return fail(MANDO_E_ARG, "null ctx");
     if (total_bytes) *total_bytes = ctx->total_mem;
     if (poa_ws_bytes) *poa_ws_bytes = (int64_t)(ctx->ws.bytes + ctx->lane_ws[0].bytes + ctx->lane_ws[1].bytes);
+    return MANDO_OK;
+}
+
+int mando_device_memory(int device_ordinal, int64_t *free_bytes, int64_t *total_bytes) {
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device_ordinal < 0 || device_ordinal >= n) return fail(MANDO_E_ARG, "mando_device_memory: bad device");
+    HIP_TRY(hipSetDevice(device_ordinal));
+    size_t f = 0, t = 0;
+    HIP_TRY(hipMemGetInfo(&f, &t));
+    if (free_bytes) *free_bytes = (int64_t)f;
+    if (total_bytes) *total_bytes = (int64_t)t;
     return MANDO_OK;
 }
 
@@ -858,11 +826,7 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
             if (!ctx->ev_fork) {
                 HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
                 for (int k = 0; k < 2; ++k) {
-                    if (ctx->cu_mask.empty())
-                        HIP_TRY(hipStreamCreateWithFlags(&ctx->lane_stream[k], hipStreamNonBlocking));
-                    else
-                        HIP_TRY(hipExtStreamCreateWithCUMask(&ctx->lane_stream[k], (uint32_t)ctx->cu_mask.size(),
-                                                             ctx->cu_mask.data()));
+                    HIP_TRY(hipStreamCreateWithFlags(&ctx->lane_stream[k], hipStreamNonBlocking));
                     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_lane[k], hipEventDisableTiming));
                 }
             }
@@ -934,29 +898,7 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
             const std::vector<int32_t> &L = lists[kind];
             if (L.empty()) continue;
             hipStream_t lst = lane ? ctx->lane_stream[lane - 1] : ctx->stream;
-            // MANDO_POA_STAGGER=1 (experiment, off by default): the other kinds start once the first
-            // (heaviest) kind's kernel is about to dispatch (ctx->ev0 is recorded right before it) and
-            // a short delay has passed, so its few long groups take their CUs before the other grids'
-            // workgroups fill the chip (a probe for the intermittent slow wide launches)
-            static const bool stagger = getenv("MANDO_POA_STAGGER") && getenv("MANDO_POA_STAGGER")[0] == '1';
-            if (lane && stagger) {
-                HIP_TRY(hipStreamWaitEvent(lst, ctx->ev0, 0));
-                hipLaunchKernelGGL(stagger_kernel, dim3(1), dim3(64), 0, lst, kStaggerTicks);
-                HIP_TRY(hipGetLastError());
-            }
             const mando::PoaCaps &caps = kcaps[kind];
-            // the heaviest groups of the launch (DP-cost estimate within MANDO_POA_HEAVY_PRIO of the
-            // largest, L is in LPT order) run at a higher wave priority
-            static const double hprio = getenv("MANDO_POA_HEAVY_PRIO") ? atof(getenv("MANDO_POA_HEAVY_PRIO")) : 0.0;
-            int32_t n_heavy = 0;
-            if (hprio > 0) {
-                auto cost = [&](int32_t g) {
-                    const GroupStat &q = gs[(size_t)g];
-                    return (double)(q.sum - q.first_len) * (double)q.first_len;
-                };
-                const double c0 = cost(L[0]);
-                while (n_heavy < (int32_t)L.size() && cost(L[(size_t)n_heavy]) >= hprio * c0) ++n_heavy;
-            }
             DevBuf &gb = kind == 0 ? ctx->gorder : (kind == 1 ? ctx->gorder_w : ctx->gorder2);
             if ((rc = gb.ensure(L.size() * 4))) return rc;
             HIP_TRY(hipMemcpyAsync(gb.p, L.data(), L.size() * 4, hipMemcpyHostToDevice, lst));
@@ -966,7 +908,7 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
                               ctx->cons_len.as<int32_t>(), ctx->cells.as<int64_t>(),
                               ctx->status.as<int32_t>(), kMaxWavesPerCu, kind == 2 ? &sp : nullptr,
                               lane == 0 && attempt == 0,  // the batch's time runs from the first attempt
-                              nk == 1, lane, kind, grant[kind], n_heavy);
+                              nk == 1, lane, kind, grant[kind]);
             if (rc) return rc;
             ctx->last_launches += 1;
             ++lane;

@@ -107,8 +107,8 @@ hipStream_t copy_stream(int device) {
 // Host buffers for the locus text, kept for reuse: page-locked (hipHostMalloc, pinned once, reused
 // by later calls), so the readers fread straight into DMA-able memory and the piecewise copies to the
 // device run on the copy engine, asynchronously, instead of a host staging copy plus a blit kernel
-// that competes with the POA grids for CU slots (MANDO_TEXT_PAGEABLE=1: 2 MB-aligned pageable
-// buffers with transparent huge pages, the round-2 layout).  Round 2 recorded stale bytes with
+// that competes with the POA grids for CU slots (2 MB-aligned pageable buffers with transparent huge
+// pages only when page-locking fails).  Round 2 recorded stale bytes with
 // reused page-locked buffers; that change was made together with moving the device text off the
 // stream-ordered pool, whose recycled buffers are the measured cause (cluster_kernel.hip,
 // tools/stale_probe.hip): a reused pinned source (scenario A) and a reused pinned D2H target (G, the
@@ -117,7 +117,7 @@ hipStream_t copy_stream(int device) {
 struct HostBuf {
     char *p = nullptr;
     size_t cap = 0;
-    bool pinned = false;  // hipHostMalloc (else posix_memalign + THP: the fallback, or MANDO_TEXT_PAGEABLE=1)
+    bool pinned = false;  // hipHostMalloc (else posix_memalign + THP: the fallback)
 };
 struct PinnedPool {
     // page-locked bytes the pool keeps between calls: the four largest buffers of a config-4 run
@@ -142,23 +142,17 @@ struct PinnedPool {
         HostBuf b;
         b.cap = (std::max<size_t>(need, 1) + kStep - 1) / kStep * kStep;
         void *p = nullptr;
-        if (!pageable()) {
-            if (hipHostMalloc(&p, b.cap, hipHostMallocDefault) == hipSuccess) {
-                b.p = static_cast<char *>(p);
-                b.pinned = true;
-                return b;
-            }
-            (void)hipGetLastError();  // page-locking failed (host memory limits): a pageable buffer instead
-            p = nullptr;
+        if (hipHostMalloc(&p, b.cap, hipHostMallocDefault) == hipSuccess) {
+            b.p = static_cast<char *>(p);
+            b.pinned = true;
+            return b;
         }
+        (void)hipGetLastError();  // page-locking failed (host memory limits): a pageable buffer instead
+        p = nullptr;
         if (posix_memalign(&p, size_t(2) << 20, b.cap) != 0) return HostBuf{};
         (void)madvise(p, b.cap, MADV_HUGEPAGE);
         b.p = static_cast<char *>(p);
         return b;
-    }
-    static bool pageable() {
-        static const bool v = getenv("MANDO_TEXT_PAGEABLE") && getenv("MANDO_TEXT_PAGEABLE")[0] == '1';
-        return v;
     }
     static void free_buf(const HostBuf &b) {
         if (b.pinned) (void)hipHostFree(b.p);

@@ -2970,5 +2970,49 @@ void release_text(mando_ctx *ctx, void *d_text, size_t cap) {
     }
 }
 
+// Frees cached buffers of a device that a larger, earlier call left behind (mando_cache_trim).  The
+// scratch of a context whose call is running is skipped (its mutex is held; that call needs it).
+int64_t cache_trim(int dev, int64_t text_cap_max, int64_t scratch_max) {
+    std::vector<void *> drop;
+    std::lock_guard<std::mutex> g(g_buf_mu);
+    if (text_cap_max >= 0) {
+        for (size_t i = 0; i < g_text_free.size();) {
+            if (g_text_free[i].dev == dev && g_text_free[i].cap > (size_t)text_cap_max) {
+                drop.push_back(g_text_free[i].p);
+                g_text_free.erase(g_text_free.begin() + (ptrdiff_t)i);
+            } else {
+                ++i;
+            }
+        }
+    }
+    size_t scratch = 0;
+    for (auto &e : g_bufs)
+        if (e.second.first && mando::ctx_device(e.first.first) == dev) scratch += e.second.second;
+    if (scratch_max >= 0 && scratch > (size_t)scratch_max)
+        for (auto &e : g_bufs) {
+            if (!e.second.first || mando::ctx_device(e.first.first) != dev) continue;
+            std::unique_lock<std::mutex> lk(ctx_mutex(e.first.first), std::try_to_lock);
+            if (!lk.owns_lock()) continue;
+            drop.push_back(e.second.first);
+            e.second = {nullptr, 0};
+        }
+    for (void *p : drop) (void)hipFree(p);
+    int64_t held = 0;
+    for (const TextBuf &t : g_text_free)
+        if (t.dev == dev) held += (int64_t)t.cap;
+    for (auto &e : g_bufs)
+        if (e.second.first && mando::ctx_device(e.first.first) == dev) held += (int64_t)e.second.second;
+    return held;
+}
+
 }  // namespace cl
 }  // namespace mando
+
+extern "C" int mando_cache_trim(int32_t device_ordinal, int64_t text_cap_max, int64_t scratch_max,
+                                int64_t *held_bytes) {
+    if (device_ordinal < 0) return MANDO_E_ARG;
+    if (hipSetDevice(device_ordinal) != hipSuccess) return MANDO_E_HIP;
+    const int64_t h = mando::cl::cache_trim(device_ordinal, text_cap_max, scratch_max);
+    if (held_bytes) *held_bytes = h;
+    return MANDO_OK;
+}

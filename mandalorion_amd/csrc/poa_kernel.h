@@ -155,13 +155,11 @@ struct PoaRunArgs {
     // a free workspace slot of n_slots (slot_busy, zeroed before the launch) for its group; workgroups
     // of other kernels get CUs as groups finish.  0: persistent slots pulling groups from `counter`.
     int32_t one_group, n_slots;
-    int32_t n_heavy;  // groups gorder[0 .. n_heavy) (the heaviest) run at a higher wave priority
     int32_t *slot_busy;
 };
 struct PoaKArgs : PoaRunArgs {
     SlotLayout lay;
     int32_t nw = 1;  // waves per workgroup: 2 runs a wide launch's two-chunk rows over two waves
-    int32_t lds_pad = 0;  // unused dynamic LDS that caps the resident workgroups per CU (occ_cap)
 };
 // waves per workgroup of a launch (two-wave workgroups for wide launches only)
 inline int poa_waves(const PoaKArgs &a) { return a.caps.wide && !a.caps.seeded && a.nw == 2 ? 2 : 1; }
@@ -189,9 +187,6 @@ inline int poa_qlds_bytes(int64_t max_len) {
 
 // Resident workgroups per CU for these arguments (LDS / register limited), at most cap.
 int poa_blocks_per_cu(const PoaKArgs &a, int cap);
-// MANDO_POA_OCC=k (experiment): narrow launches padded with unused dynamic LDS so that at most k
-// workgroups fit a CU, leaving wave slots to other streams' kernels; sets a.lds_pad
-void occ_cap(PoaKArgs &a);
 
 constexpr int kLeadBytes = 80;  // -S launches: the team leader's state after the read (poa_kernel.hip LeadState)
 // dynamic LDS of a launch: the read's nibbles, plus the wide ring in a wide launch, plus the leader's
@@ -199,7 +194,7 @@ constexpr int kLeadBytes = 80;  // -S launches: the team leader's state after th
 inline int poa_dyn_lds(const PoaKArgs &a) {
     if (a.caps.seeded) return ((a.qlds + 15) & ~15) + kLeadBytes;
     // a wide launch's backtrack windows use 16 KB of it (poa_kernel.hip bt_tb_win / bt_kp_win)
-    return a.caps.wide ? (a.qlds + kWideRingBytes > 16384 ? a.qlds + kWideRingBytes : 16384) : a.qlds + a.lds_pad;
+    return a.caps.wide ? (a.qlds + kWideRingBytes > 16384 ? a.qlds + kWideRingBytes : 16384) : a.qlds;
 }
 
 // Launch the persistent POA kernel on `stream` with `n_slots` one-wave workgroups.

@@ -220,7 +220,6 @@ struct alignas(16) SharedState {
     gint *desc_full, *xpre_full, *qnode_full;
     uint64_t tmark;                 // MANDO_PROF: the last phase boundary of the -S path (prof_mark)
     int slot_idx;                   // this workgroup's workspace slot (one_group launches claim one)
-    int boost;                      // the group is one of the launch's heaviest (wave priority +2)
 
 };
 static_assert(sizeof(BtLds) <= sizeof(DpLds), "backtrack window must fit the DP scratch");
@@ -2061,11 +2060,6 @@ __device__ __forceinline__ void w2_helper(SharedState &sh, int lane) {
             const unsigned long long nearinf = __ballot(m < (uint32_t)(kR16High - kR16Low));
             if (lane == 0) X.flag = nearinf ? 1 : 0;
             ds.r16acc = 0xffffffffu;
-            // the group's wave priority (a heavy group's rows issue first, as wave 0's do)
-            if (bcast0(sh.boost))
-                __builtin_amdgcn_s_setprio(2);
-            else
-                __builtin_amdgcn_s_setprio(0);
             group_barrier();  // the flag is read by wave 0
             continue;
         }
@@ -3799,23 +3793,10 @@ __global__ __launch_bounds__(kWave * NW, NW > 1 ? 2 : (RW == kWideRing ? MANDO_W
         if (lane == 0) {
             sh.slot.order = sh.order0;
             sh.slot.order2 = sh.order1;
-            sh.boost = gi < args_of(sh).n_heavy;
         }
         wave_sync();
-        // the launch's heaviest groups (n_heavy, LPT order: the first gi) run two priority levels above
-        // the rest, so on a shared SIMD their rows issue first: a launch lasts as long as its longest group
-        auto prio_serial = [&] {
-            if (bcast0(sh.boost))
-                __builtin_amdgcn_s_setprio(kPrioSerial + 2);
-            else
-                __builtin_amdgcn_s_setprio(kPrioSerial);
-        };
-        auto prio_dp = [&] {
-            if (bcast0(sh.boost))
-                __builtin_amdgcn_s_setprio(kPrioDp + 2);
-            else
-                __builtin_amdgcn_s_setprio(kPrioDp);
-        };
+        auto prio_serial = [&] { __builtin_amdgcn_s_setprio(kPrioSerial); };
+        auto prio_dp = [&] { __builtin_amdgcn_s_setprio(kPrioDp); };
         int st = kStOk;
         int n = 0, ng = 0;
         int64_t cells = 0;
@@ -3994,13 +3975,6 @@ int poa_blocks_per_cu(const PoaKArgs &a, int cap) {
     });
     if (nb < 1) nb = 8;
     return nb < cap ? nb : cap;
-}
-
-void occ_cap(PoaKArgs &a) {
-    static const int k = getenv("MANDO_POA_OCC") ? atoi(getenv("MANDO_POA_OCC")) : 0;
-    a.lds_pad = 0;
-    if (k <= 0 || a.caps.wide || a.caps.seeded) return;
-    while (a.lds_pad < 65536 && poa_blocks_per_cu(a, 64) > k) a.lds_pad += 256;
 }
 
 hipError_t launch_poa(const PoaKArgs &a, int n_slots, hipStream_t stream) {

@@ -7,6 +7,8 @@
 // with k = counter0 + 1 + (position in output order), or iso_k[position], and m = the isoform's member
 // count.
 #include <sys/mman.h>
+#include <sys/vfs.h>
+#include <fcntl.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -145,6 +147,30 @@ extern "C" int mando_format_outputs(int64_t n_iso, int64_t counter0, const int64
     return MANDO_OK;
 }
 
+namespace {
+// true for a file on a local file system (the shared-mapping path of mando_write_blocks); network and
+// cluster file systems (NFS, SMB, Lustre, GPFS, Ceph, BeeGFS, FUSE mounts) take pwrite()
+bool local_fs(int fd) {
+    struct statfs sf;
+    if (fstatfs(fd, &sf) != 0) return false;
+    switch ((unsigned long)sf.f_type) {
+        case 0x6969UL:      // NFS
+        case 0xFF534D42UL:  // CIFS
+        case 0xFE534D42UL:  // SMB2
+        case 0x517BUL:      // SMB
+        case 0x0BD00BD0UL:  // Lustre
+        case 0x47504653UL:  // GPFS
+        case 0x00C36400UL:  // Ceph
+        case 0x19830326UL:  // BeeGFS
+        case 0x65735546UL:  // FUSE
+        case 0x01021997UL:  // 9p
+            return false;
+        default:
+            return true;
+    }
+}
+}  // namespace
+
 extern "C" int mando_write_blocks(int32_t fd, const uint8_t *buf, const int64_t *src_off, const int64_t *dst_off,
                                   const int64_t *len, int64_t n, int32_t threads) {
     if (fd < 0 || n < 0 || (n && (!buf || !src_off || !dst_off || !len))) return MANDO_E_ARG;
@@ -182,9 +208,19 @@ extern "C" int mando_write_blocks(int32_t fd, const uint8_t *buf, const int64_t 
         lo = std::min(lo, q.dst);
         hi = std::max(hi, q.dst + q.n);
     }
+    // The mapping only on a local file system, and only over blocks allocated first: a store into a hole
+    // that the disk cannot back would raise SIGBUS (and leave the other ranks waiting in their barrier),
+    // where fallocate() reports ENOSPC as an error; and on a network file system two nodes' dirty pages
+    // of one page would overwrite each other's bytes, where pwrite() writes only its own.
     const int64_t pg = (int64_t)sysconf(_SC_PAGESIZE);
     const int64_t base = lo / pg * pg;
-    void *map = mmap(nullptr, (size_t)(hi - base), PROT_WRITE, MAP_SHARED, fd, (off_t)base);
+    void *map = MAP_FAILED;
+    if (local_fs(fd)) {
+        if (fallocate(fd, 0, (off_t)lo, (off_t)(hi - lo)) == 0)
+            map = mmap(nullptr, (size_t)(hi - base), PROT_WRITE, MAP_SHARED, fd, (off_t)base);
+        else if (errno != EOPNOTSUPP && errno != ENOSYS && errno != EINVAL)
+            return mando::set_error(MANDO_E_INTERNAL, std::string("fallocate: ") + strerror(errno));
+    }
     std::atomic<int> err{0};
     auto work = [&](size_t a, size_t b) {
         for (size_t q = a; q < b && !err.load(std::memory_order_relaxed); ++q) {

@@ -206,22 +206,13 @@ def _size_costs(sizes: np.ndarray) -> np.ndarray:
     return sz * sz
 
 
-# the shard plan's loci after the LPT head: "snake" (default: round-robin by load) or "ranges" --
-# contiguous runs of roots, so that each rank's blocks of the output files are one region and the ranks
-# place them into disjoint pages (8 processes placing 1 GB into one file through shared mappings: 0.35-0.39
-# s for contiguous ranges against 0.52-0.60 s for interleaved roots).  Rehearsed on config 4 (r04rg,
-# DESIGN.md §6) the ranges balance the POA worse (8 ranks: POA 1.42-1.69 s against 1.44-1.52 s; 2 ranks:
-# 6.65 / 6.00 s against 5.89 / 5.90 s), so they stay opt-in
-_SHARD_REST = os.environ.get("MANDO_SHARD_PLAN", "snake")
-
-
-def _lpt_owner(cost: np.ndarray, world: int, head: int = 64, rest_plan: str | None = None) -> np.ndarray:
+def _lpt_owner(cost: np.ndarray, world: int, head: int = 64) -> np.ndarray:
     """The shard plan (every rank computes the same one): loci by cost, descending; the heaviest
-    head x world go to the least-loaded rank one at a time (LPT: they set the launches' floors).  The
-    rest ("ranges"): in root order, cut into one contiguous range per rank, rank r's range holding the
-    cost that brings its load to the mean (a locus belongs to the range its cost midpoint falls in);
-    or ("snake") in a snake over the ranks ordered by load.  Vectorised: a Python argmin per locus took
-    0.4-0.8 s for 200,000 loci on every rank (r04)."""
+    head x world go to the least-loaded rank one at a time (LPT: they set the launches' floors), the
+    rest in a snake over the ranks ordered by load.  Vectorised: a Python argmin per locus took 0.4-0.8 s
+    for 200,000 loci on every rank (r04).  (Contiguous root ranges per rank after the head balanced the
+    POA worse in the round-4 rehearsal -- 8 ranks: POA 1.42-1.69 s against 1.44-1.52 s -- and were
+    dropped.)"""
     import heapq
 
     order = np.argsort(-cost, kind="stable")
@@ -233,24 +224,10 @@ def _lpt_owner(cost: np.ndarray, world: int, head: int = 64, rest_plan: str | No
         owner[i] = r
         heapq.heapreplace(h, (ld + float(cost[i]), r))
     rest = order[k:]
-    if len(rest) and (rest_plan or _SHARD_REST) == "snake":
+    if len(rest):
         by_load = np.array([r for _, r in sorted(h)], dtype=np.int64)
         m = np.arange(len(rest)) % (2 * world)
         owner[rest] = by_load[np.where(m < world, m, 2 * world - 1 - m)]
-    elif len(rest):
-        rest = np.sort(rest)
-        c = np.asarray(cost, dtype=np.float64)[rest]
-        loads = np.zeros(world)
-        for ld, r in h:
-            loads[r] = ld
-        if not c.sum() > 0:  # no cost information: equal locus counts
-            c, loads = np.ones(len(rest)), np.zeros(world)
-        cap = np.maximum(0.0, (loads.sum() + c.sum()) / world - loads)
-        cap *= c.sum() / cap.sum()
-        cuts = np.searchsorted(np.cumsum(c) - c / 2, np.cumsum(cap)[:-1])
-        cuts = np.concatenate([[0], cuts, [len(rest)]])
-        for r in range(world):
-            owner[rest[cuts[r]:cuts[r + 1]]] = r
     return owner
 
 
@@ -347,33 +324,16 @@ _BIG_CHUNK_BYTES = _CHUNK_BYTES if "MANDO_CHUNK_BYTES" in os.environ else 6 << 3
 # beside chunk 1's POA, and in about one step in four the wide POA launch then runs 3x slower (POA
 # kernels 1.61-1.67 s against 1.32 s); one chunk has no such step (1,245-1,251 ms in all 24), so inputs
 # below one byte-capped chunk run in one (r03 onechunk)
-_TWO_CHUNK_BYTES = int(os.environ.get("MANDO_TWO_CHUNK_BYTES", str(8 << 30)))
+_TWO_CHUNK_BYTES = 8 << 30
 # fewer loci than this always run in one chunk (a few large loci: SIRV-like, config 5)
 _MIN_LOCI_CHUNKED = 1024
-# heaviest-first plans: the share of the estimated POA cost that goes into the first chunk (0: off, the
-# default -- measured on config 3 it did not pay, DESIGN.md §5: chunk B's clustering and orientation run
-# 2x slower beside chunk A's POA, which lasts its longest group anyway)
-_HEAVY_FRAC = float(os.environ.get("MANDO_HEAVY_FRAC", "0"))
-
-
-def _heavy_first(sizes: np.ndarray, frac: float) -> tuple[np.ndarray, np.ndarray]:
-    """Loci of the heaviest-first plan: (chunk A, chunk B) as sorted index arrays.  The POA cost of a
-    locus is n L^2 (L its read length, n its reads) and its file holds ~n L bytes, so with
-    the depth fixed by the subsample the cost grows as the file size squared; A takes the largest loci
-    until it holds `frac` of that cost."""
-    cost = sizes.astype(np.float64) ** 2
-    order = np.argsort(-cost, kind="stable")
-    cs = np.cumsum(cost[order])
-    k = int(np.searchsorted(cs, frac * cs[-1])) + 1 if len(cs) and cs[-1] > 0 else 0
-    k = min(max(k, 1), max(len(order) - 1, 1))
-    return np.sort(order[:k]), np.sort(order[k:])
-
-
-def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0) -> tuple[int, list | None]:
+def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0,
+                fracs: list | None = None) -> tuple[int, list | None]:
     """(chunks, cumulative byte fractions of the cuts or None for equal chunks).  n_chunks > 0 (or
-    MANDO_CHUNKS) forces the count; a two-chunk plan cuts at MANDO_FIRST_CHUNK (0.3) of the bytes, or at
-    MANDO_CHUNK_FRACS (comma-separated cumulative fractions, any count)."""
-    fracs = None
+    MANDO_CHUNKS) forces the count; a two-chunk plan cuts at 0.3 of the bytes unless `fracs` (cumulative
+    fractions of the cuts, any count) is given."""
+    if fracs:
+        return max(1, min(len(fracs) + 1, max(1, n_loci))), list(fracs)
     if n_chunks <= 0 and os.environ.get("MANDO_CHUNKS"):
         n_chunks = int(os.environ["MANDO_CHUNKS"])
     if n_chunks <= 0:
@@ -387,11 +347,7 @@ def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0) -> tuple[int, l
             else:
                 n_chunks = 2
     if n_chunks == 2 and fracs is None:
-        if os.environ.get("MANDO_CHUNK_FRACS"):
-            fracs = [float(x) for x in os.environ["MANDO_CHUNK_FRACS"].split(",")]
-            n_chunks = len(fracs) + 1
-        else:
-            fracs = [float(os.environ.get("MANDO_FIRST_CHUNK", "0.3"))]
+        fracs = [0.3]
     return max(1, min(n_chunks, max(1, n_loci))), fracs
 
 
@@ -421,13 +377,25 @@ def poa_budget(total_hbm: int, span_text: list) -> int:
     return max(4 << 30, int(_HBM_USABLE * total_hbm) - reserve)
 
 
-def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", splice_site_width: int = 1,
-                    minimum_read_count: int = 2, white_list_polyA: Sequence[str] = ("0",), threads: int = 0,
-                    junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", upstream_buffer: int = 10,
-                    downstream_buffer: int = 50, seed: int = 0, device: int = 0,
-                    orient_fn: Callable | None = None, consensus_fn: Callable | None = None,
-                    cluster_fn: Callable | None = None, comm=None, verbose: bool = False, n_chunks: int = 0,
-                    share: tuple[int, int] | None = None) -> dict:
+def define_isoforms(path: str, *args, device: int = 0, consensus_fn: Callable | None = None, **kw) -> dict:
+    """Runs the D module on <path>/tmp_SS/*.psl (arguments: _define_isoforms).  The POA context's workspace
+    budget is the call's own: it goes back to the library's default policy when the call returns, so a
+    later direct POA call on the same context does not inherit this call's chunk plan."""
+    try:
+        return _define_isoforms(path, *args, device=device, consensus_fn=consensus_fn, **kw)
+    finally:
+        c = _lib._ctx_cache.get((device, 0)) if consensus_fn is None else None
+        if c is not None and c.handle is not None:
+            c.set_poa_budget(0)
+
+
+def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", splice_site_width: int = 1,
+                     minimum_read_count: int = 2, white_list_polyA: Sequence[str] = ("0",), threads: int = 0,
+                     junctions: str = "gtag,gcag,atac,ctac,ctgc,gtat", upstream_buffer: int = 10,
+                     downstream_buffer: int = 50, seed: int = 0, device: int = 0,
+                     orient_fn: Callable | None = None, consensus_fn: Callable | None = None,
+                     cluster_fn: Callable | None = None, comm=None, verbose: bool = False, n_chunks: int = 0,
+                     share: tuple[int, int] | None = None, chunk_fracs: list | None = None) -> dict:
     """Runs the D module on <path>/tmp_SS/*.psl.  orient_fn(seqs, seq_off, grp_off) -> (hits, n_hits),
     consensus_fn(seqs, seq_off, grp_off, seeding) -> (cons bytes, cons_off) and cluster_fn (the signature
     of cluster.cluster_loci) default to the HIP path.
@@ -497,53 +465,49 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
            if bidx else None)
     t1 = time.perf_counter()
     timeline = [("ingest", 0.0, t1 - t0)]
-    explicit_chunks = n_chunks
     # Chunked pipeline: clustering of chunk k+1 (host C++ threads, GIL released) overlaps orientation +
     # POA of chunk k on the GPU.  Every POA launch lasts at least as long as its longest group, so few,
     # large launches are best:
     # * inputs above one byte-capped chunk (config 4 on one GPU: ~60 GB of locus text) run in contiguous
     #   chunks of at most _CHUNK_BYTES, the first 0.4 of one, so that its POA starts early;
-    # * smaller inputs with many loci (config 3, a multi-GPU rank's share) run "heaviest first": chunk A
-    #   holds the loci of the largest POA cost (~_HEAVY_FRAC of it: the longest groups, whose one-wave
-    #   latency sets every launch's floor) and is clustered, oriented and launched first; chunk B (the
-    #   rest) is clustered, oriented and assembled while A's POA runs, and its POA is launched on a second
-    #   device context beside it.  Outputs are written once both are done (sorted roots);
-    # * few loci (SIRV-like, config 5) run in one chunk.
+    # * smaller inputs (config 3, a multi-GPU rank's share) and few loci (SIRV-like, config 5) run in
+    #   one chunk.
     sizes = root_sizes[np.asarray(mine, dtype=np.int64)]
-    n_chunks, fracs = _chunk_plan(int(sizes.sum()), len(my_roots), n_chunks)
-    heavy = (n_chunks == 1 and len(my_roots) >= _MIN_LOCI_CHUNKED and _HEAVY_FRAC > 0
-             and os.environ.get("MANDO_CHUNKS") is None and explicit_chunks <= 0)
-    if heavy:
-        parts = list(_heavy_first(sizes, _HEAVY_FRAC))
-    else:
-        cuts = [0]
-        if n_chunks > 1:
-            cs = np.cumsum(sizes)
-            fr = fracs or [k / n_chunks for k in range(1, n_chunks)]
-            for f in fr:
-                cuts.append(int(np.searchsorted(cs, cs[-1] * f)) + 1)
-        cuts.append(len(my_roots))
-        cuts = sorted(set(min(max(c, 0), len(my_roots)) for c in cuts))
-        parts = [np.arange(cuts[k], cuts[k + 1]) for k in range(len(cuts) - 1) if cuts[k + 1] > cuts[k]]
-        parts = parts or [np.arange(0)]
-    # one rank and contiguous chunks: each chunk's part of both files is written as soon as it is done
-    stream_out = world == 1 and not heavy
+    n_chunks, fracs = _chunk_plan(int(sizes.sum()), len(my_roots), n_chunks, chunk_fracs)
+    cuts = [0]
+    if n_chunks > 1:
+        cs = np.cumsum(sizes)
+        fr = fracs or [k / n_chunks for k in range(1, n_chunks)]
+        for f in fr:
+            cuts.append(int(np.searchsorted(cs, cs[-1] * f)) + 1)
+    cuts.append(len(my_roots))
+    cuts = sorted(set(min(max(c, 0), len(my_roots)) for c in cuts))
+    parts = [np.arange(cuts[k], cuts[k + 1]) for k in range(len(cuts) - 1) if cuts[k + 1] > cuts[k]]
+    parts = parts or [np.arange(0)]
+    # one rank: each chunk's part of both files is written as soon as it is done
+    stream_out = world == 1
     placed = world > 1 and _REASSEMBLY == "place"
     names_parts: dict = {}
     mine_a = np.asarray(mine, dtype=np.int64)
-    # the POA workspaces' HBM budget for this call, from the chunk plan (no free-memory query: the
-    # clustering thread allocates the next chunk's buffers while a POA launch sizes its workspace)
-    n_poa = 2 if heavy else (int(os.environ.get("MANDO_POA_STREAMS", "1")) if len(parts) > 1 else 1)
-    if dev_poa:
+    # the POA workspaces' HBM budget for this call, from the chunk plan (no free-memory query during the
+    # call: the clustering thread allocates the next chunk's buffers while a POA launch sizes its
+    # workspace).  The plan reserves this call's clustering buffers; buffers an earlier, larger call left
+    # in the clustering's caches are freed first, or they would sit in HBM the plan counts as the POA's
+    # (round 4: a rank-share call after a 6 GiB-chunk call asked for 176 GB of POA workspace that the
+    # earlier call's caches still held, MANDO_E_NOMEM).
+    pctx = None
+    hbm = {}
+    if dev_poa or cluster_fn is None:
         span_text = [int(sizes[ix].sum()) for ix in parts]
-        # MANDO_POA_FREE_CUS=k (experiment): with several chunks, the POA streams leave the device's first k
-        # CUs to the next chunk's clustering and orientation kernels (which otherwise get CUs only as the
-        # running POA grid's workgroups retire)
-        free_cus = int(os.environ.get("MANDO_POA_FREE_CUS", "0")) if len(parts) > 1 else 0
-        for k in range(n_poa):
-            pctx = _lib.context(device, 3 * k)
-            pctx.set_poa_budget(poa_budget(pctx.memory()[0], span_text) // n_poa)
-            pctx.set_cu_mask(list(range(free_cus, 256)) if free_cus > 0 else None)
+        big = max(span_text) if span_text else 0
+        held = _lib.cache_trim(device, text_cap_max=big + (512 << 20),
+                               scratch_max=int(1.25 * _CLUSTER_SCRATCH_PER_TEXT * big) + (1 << 30))
+        hbm = {"cache_held_start": held}
+    if dev_poa:
+        pctx = _lib.context(device, 0)
+        total_hbm = pctx.memory()[0]
+        hbm.update(total=total_hbm, poa_budget=poa_budget(total_hbm, span_text))
+        pctx.set_poa_budget(hbm["poa_budget"])
 
     # with several chunks in flight, two cores stay with the GPU driver, assembly and compaction threads
     n_cpu = threads if threads > 0 else (os.cpu_count() or 1)
@@ -575,12 +539,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             ann=[ann[i] for i in ix] if ann else None,
             device=device, cutoff=cutoff, splice_site_width=splice_site_width,
             minimum_read_count=minimum_read_count, upstream_buffer=upstream_buffer,
-            downstream_buffer=downstream_buffer, junctions=junctions, seed=seed, threads=cl_threads,
-            # MANDO_ORIENT_IN_CLUSTER=1: each sub-batch of loci oriented inside the call, beside the next
-            # one's clustering -- measured neutral (both are throughput-bound kernels sharing the CUs,
-            # profiles/r04v_orient_in_cluster_ab.jsonl), so off by default
-            **({"orient": True} if cluster_fn is None and dev_orient and os.environ.get("MANDO_ORIENT_IN_CLUSTER", "0") == "1"
-               else {}))
+            downstream_buffer=downstream_buffer, junctions=junctions, seed=seed, threads=cl_threads)
         te = time.perf_counter()
         timeline.append(("cluster", tc - t0, te - t0))
         bad = np.nonzero(r.locus_status != 0)[0]
@@ -603,9 +562,10 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
 
     stats = {"loci": len(roots), "isoforms": 0, "poa_groups": 0, "records": 0, "poa_reads": 0,
              "t_ingest": t1 - t0, "t_cluster": 0.0, "t_pack": 0.0, "t_orient": 0.0, "t_assemble": 0.0,
-             "t_poa": 0.0, "chunks": len(parts), "heavy_first": heavy, "poa_launches": poa_launches}
+             "t_poa": 0.0, "chunks": len(parts), "poa_launches": poa_launches}
     payloads = []
     stats["timeline"] = timeline
+    stats["hbm"] = hbm
 
     def assemble(res, hits, n_hits):
         ta = time.perf_counter()
@@ -618,8 +578,7 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
 
     # Staged pipeline over chunks: clustering (one host thread driving the C++ pool, chunks in order) ->
     # orientation (main thread, GPU slot 1) -> emission assembly (host thread) -> POA (one host thread,
-    # GPU slot 0, by default; heaviest-first plans and MANDO_POA_STREAMS=2 add a second on slot 3 so that
-    # chunk k+1's grids run beside chunk k's) -> writer.
+    # GPU slot 0) -> writer.
     lock = threading.Lock()
 
     def add(key, v):
@@ -640,13 +599,11 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
             res.close()
         return pl, res
 
-    # POA host threads (n_poa above), one device context each: each context's workspaces have their own
-    # explicit budget (a share of the call's plan), so a second context never sizes its workspace from
-    # the HBM the first one left free (r02: a quarter of the slots, the persistent grid, 2.9 s, in 3 of
-    # 30 config-3 steps when it did)
+    # one POA host thread and device context (r02: a second context sized its workspace from the HBM the
+    # first one left free -- a quarter of the slots, the persistent grid, 2.9 s, in 3 of 30 config-3 steps)
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
             ThreadPoolExecutor(max_workers=1) as writer, \
-            ThreadPoolExecutor(max_workers=n_poa) as gpu_poa:
+            ThreadPoolExecutor(max_workers=1) as gpu_poa:
         cl = [ex.submit(run_cluster, k, ix) for k, ix in enumerate(parts)]
         poa_futs = []
         # one rank: reads2isoforms.txt needs only the clustering, so each chunk's part of it is written
@@ -774,6 +731,10 @@ def define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", s
     for r in results:
         r.close()
     stats["t_close"] = time.perf_counter() - t0 - stats["t_total"]
+    if hbm:  # what the call's device buffers hold once it is done (caches and POA workspaces, kept for reuse)
+        hbm["cache_held_end"] = _lib.cache_trim(device)
+        if pctx is not None:
+            hbm["poa_ws_held"] = pctx.memory()[1]
     if verbose and rank == 0:
         print("\t" + " ".join(f"{k}={v:.3f}" if isinstance(v, float) else f"{k}={v}" for k, v in stats.items()
                                if not isinstance(v, list)))

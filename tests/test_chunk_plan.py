@@ -14,7 +14,7 @@ GB = 1 << 30
 
 @pytest.fixture(autouse=True)
 def _clean_env(monkeypatch):
-    for k in ("MANDO_CHUNKS", "MANDO_FIRST_CHUNK", "MANDO_CHUNK_FRACS"):
+    for k in ("MANDO_CHUNKS",):
         monkeypatch.delenv(k, raising=False)
 
 
@@ -32,12 +32,10 @@ def test_byte_capped_chunks():
 
 def test_two_chunks_take_the_first_chunk_fraction(monkeypatch):
     assert define._chunk_plan(GB, 100, n_chunks=2) == (2, [0.3])
-    monkeypatch.setenv("MANDO_FIRST_CHUNK", "0.5")
-    assert define._chunk_plan(GB, 100, n_chunks=2) == (2, [0.5])
+    assert define._chunk_plan(GB, 100, fracs=[0.5]) == (2, [0.5])
     monkeypatch.setenv("MANDO_CHUNKS", "2")
-    assert define._chunk_plan(GB, 100) == (2, [0.5])
-    monkeypatch.setenv("MANDO_CHUNK_FRACS", "0.2,0.6")
-    assert define._chunk_plan(GB, 100) == (3, [0.2, 0.6])
+    assert define._chunk_plan(GB, 100) == (2, [0.3])
+    assert define._chunk_plan(GB, 100, fracs=[0.2, 0.6]) == (3, [0.2, 0.6])
     assert define._chunk_plan(GB, 100, n_chunks=3) == (3, None)  # forced counts other than 2: equal chunks
 
 
@@ -136,24 +134,14 @@ def test_write_big_appends_in_order(tmp_path):
     assert got == b"head" + a.tobytes() + b"tail"
 
 
-@pytest.mark.parametrize("rest", ["ranges", "snake"])
-def test_shard_plan_balances_and_is_lpt_for_the_heaviest(rest):
+def test_shard_plan_balances_and_is_lpt_for_the_heaviest():
     import numpy as np
 
     rng = np.random.default_rng(3)
     cost = rng.uniform(1, 100, 5000) ** 2
-    owner = define._lpt_owner(cost, 8, head=16, rest_plan=rest)
+    owner = define._lpt_owner(cost, 8, head=16)
     load = np.bincount(owner, weights=cost, minlength=8)
-    # ranges: cut at locus boundaries (one locus is up to 0.5 % of a rank's load); snake: finer
-    assert load.max() / load.mean() < (1.01 if rest == "ranges" else 1.001)
-    if rest == "ranges":  # past the LPT head, each rank's loci are one contiguous run of roots
-        head = set(np.argsort(-cost, kind="stable")[:16 * 8].tolist())
-        for r in range(8):
-            idx = [i for i in np.nonzero(owner == r)[0].tolist() if i not in head]
-            runs = [i for i in range(len(cost)) if i not in head]
-            pos = [runs.index(i) for i in idx]
-            assert pos == list(range(pos[0], pos[0] + len(pos)))
-        assert define._lpt_owner(np.zeros(10), 3, head=0, rest_plan="ranges").tolist() == [0] * 3 + [1] * 4 + [2] * 3
+    assert load.max() / load.mean() < 1.001
     # the heaviest 8 go to 8 different ranks, the 9th to the least-loaded of them
     top = np.argsort(-cost, kind="stable")
     assert sorted(owner[top[:8]]) == list(range(8))

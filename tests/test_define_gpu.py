@@ -61,24 +61,6 @@ def test_define_gpu_chunked_pipeline(gpu_ctx, tmp_path):
 
 
 @pytest.mark.gpu
-def test_define_gpu_chunks_with_poa_cu_mask(gpu_ctx, tmp_path, monkeypatch):
-    """MANDO_POA_FREE_CUS: the POA streams of a chunked call restricted to CUs 32.. (mando_ctx_set_cu_mask),
-    then a one-chunk call on every CU again: both write the one-chunk run's files."""
-    d = str(tmp_path)
-    loci = simdata.make_dataset(simdata.fixture_specs())
-    info = simdata.write_dataset(loci, d)
-    read = lambda f: open(os.path.join(d, f), "rb").read()
-    _run(d, info["gtf"])
-    one = read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")
-    monkeypatch.setenv("MANDO_POA_FREE_CUS", "32")
-    st = _run(d, info["gtf"], n_chunks=3)
-    assert st["chunks"] == 3
-    assert (read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")) == one
-    _run(d, info["gtf"])  # one chunk: the mask is lifted
-    assert (read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")) == one
-
-
-@pytest.mark.gpu
 def test_define_gpu_byte_capped_chunks_then_one_chunk(gpu_ctx, tmp_path, monkeypatch):
     """The byte-capped many-chunk branch (config 4's plan, thresholds lowered to this small input), then a
     one-chunk call in the same process: same files each time, and the one-chunk call's POA workspaces are
@@ -109,3 +91,30 @@ def test_define_gpu_byte_capped_chunks_then_one_chunk(gpu_ctx, tmp_path, monkeyp
     _run(d, info["gtf"])
     assert (read("Isoform_Consensi.fasta"), read("reads2isoforms.txt")) == one
     assert pctx.last_slots() == slots1
+
+
+@pytest.mark.gpu
+def test_define_gpu_hbm_plan_after_a_larger_call(gpu_ctx, tmp_path):
+    """A whole-input call, then a rank-share call (a smaller plan) in the same process -- the round-4
+    rehearsal's sequence, whose second call ran out of HBM: the clustering caches the larger call left
+    are trimmed to the second call's plan, so what they hold plus the POA grant stays within the usable
+    HBM, the POA workspaces stay within their grant, and the share's files hold its own loci."""
+    from mandalorion_amd import _lib
+
+    d = str(tmp_path)
+    loci = simdata.make_dataset(simdata.fixture_specs())
+    info = simdata.write_dataset(loci, d)
+    st1 = _run(d, info["gtf"])
+    st2 = _run(d, info["gtf"], share=(0, 4))
+    for st in (st1, st2):
+        h = st["hbm"]
+        assert h["cache_held_start"] + h["poa_budget"] <= define._HBM_USABLE * h["total"]
+        assert h["poa_ws_held"] <= h["poa_budget"]
+    # the share's caches were trimmed to its (smaller) largest chunk before its POA grant was sized
+    assert st2["hbm"]["cache_held_start"] <= st1["hbm"]["cache_held_end"]
+    assert 0 < st2["records"] < st1["records"]
+    # the budget is the call's own: back to the library's default policy afterwards
+    pctx = _lib.context(0, 0)
+    free0, total = _lib.device_memory(0)
+    assert 0 < free0 <= total
+    assert pctx.memory()[1] <= st1["hbm"]["poa_budget"]

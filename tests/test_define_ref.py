@@ -73,18 +73,17 @@ def test_driver_with_oracle_equals_reference(tmp_path, name):
 
 
 @pytest.mark.parametrize("name", ["config1", "r2c2_rev"])
-def test_driver_heaviest_first_equals_reference(tmp_path, name, monkeypatch):
-    """The heaviest-first two-chunk plan (chunk A: the loci of largest POA cost, chunk B: the rest, two POA
-    threads, one write at the end in sorted-root order) writes the reference's exact files."""
+def test_driver_uneven_chunks_equals_reference(tmp_path, name):
+    """A three-chunk plan with uneven cuts (0.2 / 0.7 of the bytes: each chunk's part of both files
+    streamed out as its POA finishes) writes the reference's exact files."""
     from oracle import orient as oref
     from oracle import poa as opoa
 
-    monkeypatch.setattr(define, "_MIN_LOCI_CHUNKED", 1)
-    monkeypatch.setattr(define, "_HEAVY_FRAC", 0.3)
     d = _dataset(tmp_path, name)
     st = _run(d, orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
-              consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci)
-    assert st["heavy_first"] and st["chunks"] == 2
+              consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci,
+              chunk_fracs=[0.2, 0.7])
+    assert st["chunks"] == 3
     _check(d, name, st)
 
 
@@ -187,18 +186,6 @@ def test_driver_three_rank_placement_in_one_process(tmp_path):
     _check(d, name="r2c2_rev", st=st)
 
 
-def test_heavy_first_split():
-    import numpy as np
-
-    sizes = np.array([10, 50, 20, 40, 30, 5], dtype=np.int64)
-    a, b = define._heavy_first(sizes, 0.5)
-    assert list(a) == [1, 3] and list(b) == [0, 2, 4, 5]   # 50^2 + 40^2 >= half of the sum of squares
-    a, b = define._heavy_first(sizes, 0.0)
-    assert list(a) == [1] and len(b) == 5                  # never empty
-    a, b = define._heavy_first(sizes, 1.0)
-    assert len(a) == 5 and len(b) == 1                     # nor the second
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(GOLD["datasets"]))
 def test_gpu_driver_equals_reference(gpu_ctx, tmp_path, name):
@@ -210,10 +197,9 @@ def test_gpu_driver_equals_reference(gpu_ctx, tmp_path, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["config1", "r2c2_rev", "long_seeded"])
 def test_gpu_driver_sub_batched_clustering_equals_reference(gpu_ctx, tmp_path, monkeypatch, name):
-    """Clustering in 3 sub-batches with each one's orientation run inside the call beside the next one's
-    clustering (the large-input path, forced by MANDO_CL_SUB): the reference's files."""
+    """Clustering in 3 sub-batches overlapped with the reading and copy (the large-input path, forced by
+    MANDO_CL_SUB): the reference's files."""
     monkeypatch.setenv("MANDO_CL_SUB", "3")
-    monkeypatch.setenv("MANDO_ORIENT_IN_CLUSTER", "1")
     d = _dataset(tmp_path, name)
     st = _run(d)
     _check(d, name, st)
@@ -300,14 +286,12 @@ CONFIG4_SLICE = dict(reads=(40, 60), exons=(5, 12), exon_len=(130, 570), pacbio_
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["config1", "sirv_like"])
-def test_gpu_driver_heaviest_first_equals_reference(gpu_ctx, tmp_path, name, monkeypatch):
-    """The product path with the heaviest-first plan: two POA launches on two device contexts side by side
-    (the second chunk clustered and oriented while the first one's POA runs): the reference's files."""
-    monkeypatch.setattr(define, "_MIN_LOCI_CHUNKED", 1)
-    monkeypatch.setattr(define, "_HEAVY_FRAC", 0.3)
+def test_gpu_driver_two_chunks_equals_reference(gpu_ctx, tmp_path, name):
+    """The product path in two pipelined chunks (the second clustered and oriented while the first one's
+    POA runs): two POA launches, the reference's files."""
     d = _dataset(tmp_path, name)
-    st = _run(d)
-    assert st["heavy_first"] and len(st["poa_launches"]) == 2
+    st = _run(d, n_chunks=2)
+    assert st["chunks"] == 2 and len(st["poa_launches"]) == 2
     _check(d, name, st)
 
 

@@ -100,21 +100,32 @@ def test_seeded_groups_mixed_with_unseeded():
     _check(groups, seeding=seeding)
 
 
-@pytest.mark.parametrize("persistent", ["0", "1"])
-def test_grid_modes_and_launch_kinds(monkeypatch, persistent):
+@pytest.mark.parametrize("persistent", [False, True])
+def test_grid_modes_and_launch_kinds(gpu_ctx, persistent):
     """One-group grids (a workgroup per group, workspace slots claimed from a flag array) and the
-    persistent grid give the same consensi; the batch spans the narrow (3 kb), wide (6-9 kb: 256-column
-    ring rows, 16-bit mode shifted past 6.4 kb) and 32-bit wide (> 10.1 kb) launch kinds at once."""
-    monkeypatch.setenv("MANDO_POA_PERSISTENT", persistent)
+    persistent grid (fewer slots than groups: a 1 GiB workspace budget) give the same consensi; the batch
+    spans the narrow (3 kb), wide (6-9 kb: 256-column ring rows, 16-bit mode shifted past 6.4 kb) and
+    32-bit wide (> 10.1 kb) launch kinds at once."""
+    from mandalorion_amd import _lib
+
     _, narrow = poa_cases.noisy_groups(40, (2700, 3300), (4, 12), seed=81)
     _, wide = poa_cases.noisy_groups(4, (6000, 9000), (4, 10), seed=82)
     _, longer = poa_cases.noisy_groups(2, (10500, 11500), (3, 5), seed=83)
-    _check(narrow + wide + longer)
+    ctx = _lib.context(0, 0)
+    ctx.set_poa_budget((1 << 30) if persistent else 0)
+    try:
+        _check(narrow + wide + longer)
+        if persistent:
+            slots, _ = ctx.last_slots()
+            assert 0 < slots[0] < 40  # the narrow launch ran fewer slots than groups: the persistent grid
+    finally:
+        ctx.set_poa_budget(0)
 
 
-@pytest.mark.parametrize("waves", ["1", "2"])
+@pytest.mark.parametrize("waves", ["0", "2"])
 def test_wide_launch_waves_per_group(monkeypatch, waves):
-    """Wide launches with one or two waves per group (MANDO_POA_W2=1: every two-chunk fast row split over
+    """Wide launches with one or two waves per group (MANDO_POA_W2=0: one wave; 2, the default: every
+    two-chunk fast row split over
     the two waves of the group's workgroup, poa_kernel.hip row16w_half; one-chunk, generic and 32-bit rows
     stay on wave 0): the same bytes and DP cells as the oracle.  The batch spans bands just over one chunk
     (5-6 kb), two full chunks (8-9 kb, 16-bit shifted), 32-bit rows (> 10.1 kb), deep and shallow groups,
@@ -132,7 +143,7 @@ def test_wide_launch_waves_per_group(monkeypatch, waves):
 
 def test_wide_two_waves_deep_long_group(monkeypatch):
     """Config-5's unseeded shape (one wave per group is its critical path): 40 reads x ~8.5 kb, two waves."""
-    monkeypatch.setenv("MANDO_POA_W2", "1")
+    monkeypatch.setenv("MANDO_POA_W2", "2")
     _check(poa_cases.noisy_groups(1, (8300, 8700), (40, 40), seed=95)[1])
 
 

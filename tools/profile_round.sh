@@ -13,7 +13,8 @@ B="python3 bench.py --no-cpu-baseline --workload $WL"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $D/pmcf -o f --output-format csv -- $B --steps 1 --warmup 0 > $D/pmcf.out 2>&1 || { echo "pmcf failed"; tail -5 $D/pmcf.out; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $D/pmcw -o w --output-format csv -- $B --steps 1 --warmup 0 > $D/pmcw.out 2>&1 || { echo "pmcw failed"; tail -5 $D/pmcw.out; exit 1; }
 F=$(find $D/pmcf -name "*counter_collection.csv" | head -1); W=$(find $D/pmcw -name "*counter_collection.csv" | head -1)
-python3 tools/pmc_traffic.py $F $W $KEY $D/pmc_latest.json || exit 1
+CH=$(python3 -c "import json; print([json.loads(l) for l in open('$D/pmcf.out') if l.startswith('{\"metric')][-1]['config']['chunks'])") || exit 1
+python3 tools/pmc_traffic.py $F $W $KEY $CH $D/pmc_latest.json || exit 1
 timeout -k 10 600 python3 bench.py --workload $WL --pmc-json $D/pmc_latest.json > $D/bench.json 2> $D/bench.err || { echo "bench failed"; tail -5 $D/bench.err; exit 1; }
 cat $D/bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-format csv -- $B --steps 3 --warmup 1 --pmc-json $D/pmc_latest.json > $D/prof.out 2>&1 || { echo "prof failed"; exit 1; }
