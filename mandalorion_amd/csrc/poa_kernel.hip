@@ -2091,6 +2091,704 @@ __device__ __forceinline__ void w2_helper(SharedState &sh, int lane) {
     }
 }
 
+// ---- fast rows, hand-scheduled (narrow launches, default scores) -------------------------------
+// The row loop above, for the rows that make up ~90 % of a narrow launch (config-3/4 rows: one
+// predecessor 60 %, two 30 %): fast rows (bit 15 of the descriptor) with one or two predecessors in
+// the LDS ring, in batches whose capacity check passed.  Written as one asm loop because the
+// compiler's form of the same row spends ~110 scalar instructions on it (bool masks materialised as
+// 64-bit lane masks, register copies at the joins of the row kinds, SGPRs reloaded from VGPR lanes,
+// lane-0 record stores through exec save / restore) next to ~110 vector ones, and at four waves per
+// SIMD both issue ports are saturated (DESIGN.md §3.1 issue model); here the row's control is ~60
+// scalar instructions and the vector stream is the same cells as row16_vec.  Every value follows
+// run_dp16 / row16_vec exactly (same band, masks, traceback and predecessor bytes, ring and spill
+// planes, row records); tests/test_poa_gpu.py compares the bytes with the oracle.
+// The loop leaves at the batch end or at the first row it does not take (the C++ row handles it):
+// nothing of that row has been written then.  Hazards (gfx950) are padded inside the string: DPP
+// reads two wait states after a VALU write, v_readlane after the scans, VMEM reads of SGPRs written
+// by a VALU before the block (s_nop 4).  Exec is the whole wave here (run_dp16 runs wave-uniform);
+// the row records are stored with exec = lane 0 and exec is restored to all lanes.
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(lds_u8 *)(const_cast<void *>(p));
+}
+
+__device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb, gu8 *kp, gint *sv, gint *rinfo,
+                                             int b0, int i, int iend, int qlen, int w, int &prv_r, int &prv_beg,
+                                             int &prv_end, int &prv_am, DpState &ds) {
+    using SC = DefaultScores;
+    static_assert(SC::match == 5 && SC::mismatch == 4 && SC::o1 == 4 && SC::e1 == 2 && SC::o2 == 24 && SC::e2 == 1,
+                  "the constants below are abPOA's defaults");
+    static_assert(kRing16 == 8 && kChunk == 128 && kRowRing == 32 && kDescInts == 8 && kRowInfoInts == 8,
+                  "LDS / HBM geometry the block assumes");
+    // lane constants (as in row16_vec): the lane's two columns relative to the chunk, times the gap
+    // extensions, and the argmax key offsets
+    const uint32_t LJ = (uint32_t)(2 * lane) * 0x10001u + 0x10000u;
+    const uint32_t LJ1 = as_u32(as_u16x2(LJ) * (u16x2){2, 2});
+    const uint32_t LJ2 = LJ;
+    const uint32_t FJ1 = LJ1 + pk2(SC::o1 + SC::e1 - SC::e1), FJ2 = LJ2 + pk2(SC::o2 + SC::e2 - SC::e2);
+    const int clo = 127 - 2 * lane, chi = 126 - 2 * lane;
+    const uint32_t vlane = (uint32_t)lane, vlane2 = 2u * (uint32_t)lane, vlane8 = 8u * (uint32_t)lane;
+    const uint32_t vkneg = kNeg2, v10000 = 0x10000u;
+    const uint32_t Ldesc = lds_addr(&sh.desc[0][0]), Lrrow = lds_addr(&sh.rrow[0]);
+    const uint32_t Lring = lds_addr(ring16_row<kChunk>(sh, 0)), Lq = lds_addr(qnib<kChunk>());
+    const uint64_t tbp = (uint64_t)uni64((int64_t)tb), kpp = (uint64_t)uni64((int64_t)kp);
+    const uint64_t svp = (uint64_t)uni64((int64_t)sv), rip = (uint64_t)uni64((int64_t)rinfo);
+    int pr = prv_r, pb = prv_beg, pe = prv_end, pa = prv_am;
+    int tbu = ds.tb_used, kpu = ds.kp_used, svu = ds.sv_used, cel = ds.cells;
+    uint32_t r16 = ds.r16acc;
+    int d1, rem, p0, p1, rb1, re1, ra1, x, y, z, beg, end, cb0, spm, pc0, pc1, tlo, pkb, pke, base1, mp, besti, r, pwb,
+        i0, c20002, c128, cr16, cq, cth;
+    uint32_t va, vd1, vrem, vp0, vp1, t, J, q, iw, a0, w0, w0p, inv, m1, m2, m3, sel, S, Hd, X1, X2, Hd1,
+        X11, X21, MK, K1, K2, M, H0, G1, G2, Ga, Gb, inc, amk, t1, Pa, Pb, P1, P2, F1, F2, H, X1e, Ho1, X2e, Ho2, E1,
+        E2, d0, dd, x01, x23, x45, x67, voff;
+    const uint32_t csel0 = 0x05040100u, csel1 = 0x07060302u, cseltb = 0x0B0A0908u, cselkp = 0x0C0C0200u;
+    const uint32_t m01 = 0x02020101u, m23 = 0x08080404u, m45 = 0x20201010u, m67 = 0x80804040u, v0c0c = 0x0C000C00u;
+    asm volatile(
+        "s_nop 4\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "s_mov_b32 %[c20002], 0x20002\n"
+        "s_movk_i32 %[c128], 0x80\n"
+        "s_movk_i32 %[cr16], 0x7918\n"
+        "s_mov_b32 %[cq], 0xf000f\n"
+        "s_mov_b32 %[cth], 0x4040404\n"
+        "s_mov_b32 %[i0], %[i]\n"
+        "s_and_b32 %[x], %[pr], 7\n"
+        "s_mulk_i32 %[x], 0x300\n"
+        "s_add_u32 %[pwb], %[x], %[Lring]\n"
+        "L_top%=:\n"
+        "s_cmp_ge_i32 %[i], %[iend]\n"
+        "s_cbranch_scc1 L_out%=\n"
+        "s_lshl_b32 %[x], %[i], 5\n"
+        "s_add_u32 %[x], %[x], %[Ldesc]\n"
+        "v_mov_b32 %[va], %[x]\n"
+        "ds_read_b32 %[vd1], %[va] offset:4\n"
+        "ds_read_b32 %[vrem], %[va] offset:8\n"
+        "ds_read_b32 %[vp0], %[va] offset:12\n"
+        "ds_read_b32 %[vp1], %[va] offset:16\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 %[d1], %[vd1]\n"
+        "v_readfirstlane_b32 %[p0], %[vp0]\n"
+        "v_readfirstlane_b32 %[rem], %[vrem]\n"
+        "s_and_b32 %[y], %[d1], 0xffffc000\n"
+        "s_cmp_eq_u32 %[y], 0x18000\n"
+        "s_cbranch_scc0 L_two%=\n"
+        "s_cmp_eq_u32 %[p0], %[pr]\n"
+        "s_cbranch_scc1 L_p0ok1%=\n"
+        "s_and_b32 %[x], %[p0], 31\n"
+        "s_lshl_b32 %[x], %[x], 4\n"
+        "s_add_u32 %[x], %[x], %[Lrrow]\n"
+        "v_mov_b32 %[va], %[x]\n"
+        "ds_read_b32 %[vd1], %[va]\n"
+        "ds_read_b32 %[vrem], %[va] offset:4\n"
+        "ds_read_b32 %[vp0], %[va] offset:8\n"
+        "s_and_b32 %[x], %[p0], 7\n"
+        "s_mulk_i32 %[x], 0x300\n"
+        "s_add_u32 %[pwb], %[x], %[Lring]\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 %[pb], %[vd1]\n"
+        "v_readfirstlane_b32 %[pe], %[vrem]\n"
+        "v_readfirstlane_b32 %[pa], %[vp0]\n"
+        "s_mov_b32 %[pr], %[p0]\n"
+        "L_p0ok1%=:\n"
+        "s_sub_i32 %[x], %[qlen], %[rem]\n"
+        "s_add_i32 %[z], %[pa], 1\n"
+        "s_min_i32 %[y], %[z], %[x]\n"
+        "s_max_i32 %[z], %[z], %[x]\n"
+        "s_sub_i32 %[y], %[y], %[w]\n"
+        "s_add_i32 %[z], %[z], %[w]\n"
+        "s_max_i32 %[beg], %[y], 0\n"
+        "s_min_i32 %[end], %[z], %[qlen]\n"
+        "s_and_b32 %[cb0], %[beg], -2\n"
+        "s_sub_i32 %[spm], %[end], %[cb0]\n"
+        "s_and_b32 %[pc0], %[pb], -2\n"
+        "s_sub_i32 %[x], %[pe], %[pc0]\n"
+        "s_max_i32 %[x], %[x], %[spm]\n"
+        "s_cmpk_gt_i32 %[x], 0x7f\n"
+        "s_cbranch_scc1 L_out%=\n"
+        "s_bfe_u32 %[z], %[d1], 0x80000\n"
+        "s_lshl_b32 %[x], %[z], 3\n"
+        "s_lshl_b32 %[tlo], 9, %[x]\n"
+        "s_cmp_gt_u32 %[z], 3\n"
+        "s_cselect_b32 %[tlo], %[cth], %[tlo]\n"
+        "s_pack_ll_b32_b16 %[pkb], %[beg], %[beg]\n"
+        "s_pack_ll_b32_b16 %[pke], %[end], %[end]\n"
+        "s_bfe_u32 %[x], %[cb0], 0xf0001\n"
+        "v_add_u32 %[t], %[x], %[vlane]\n"
+        "v_mad_u32_u24 %[J], %[t], %[c20002], %[v10000]\n"
+        "v_add_u32 %[va], %[Lq], %[t]\n"
+        "ds_read_u8 %[q], %[va]\n"
+        "v_and_b32 %[iw], 63, %[t]\n"
+        "v_lshl_add_u32 %[a0], %[iw], 2, %[pwb]\n"
+        "ds_read_b32 %[w0], %[a0]\n"
+        "ds_read_b32 %[X1], %[a0] offset:256\n"
+        "ds_read_b32 %[X2], %[a0] offset:512\n"
+        "v_pk_sub_i16 %[m1], %[J], %[pkb]\n"
+        "v_pk_sub_i16 %[m2], %[pke], %[J]\n"
+        "v_or_b32 %[m1], %[m1], %[m2]\n"
+        "v_pk_ashrrev_i16 %[inv], 15, %[m1] op_sel_hi:[0,1]\n"
+        "s_waitcnt lgkmcnt(3)\n"
+        "v_mul_u32_u24 %[sel], 0x1001, %[q]\n"
+        "v_and_or_b32 %[sel], %[sel], %[cq], %[v0c0c]\n"
+        "v_perm_b32 %[S], 4, %[tlo], %[sel]\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_mov_b32_dpp %[w0p], %[w0] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
+        "v_alignbit_b32 %[Hd], %[w0], %[w0p], 16\n"
+        "s_cmp_le_i32 %[beg], %[pc0]\n"
+        "s_cbranch_scc1 L_mask1%=\n"
+        "s_add_u32 %[x], %[pc0], 0x7f\n"
+        "s_cmp_le_i32 %[end], %[x]\n"
+        "s_cbranch_scc1 L_nomask1%=\n"
+        "L_mask1%=:\n"
+        "s_pack_ll_b32_b16 %[x], %[pb], %[pb]\n"
+        "s_pack_ll_b32_b16 %[y], %[pe], %[pe]\n"
+        "v_pk_add_u16 %[m3], %[J], -1\n"
+        "v_pk_sub_i16 %[m1], %[m3], %[x]\n"
+        "v_pk_sub_i16 %[m2], %[y], %[m3]\n"
+        "v_or_b32 %[m1], %[m1], %[m2]\n"
+        "v_pk_ashrrev_i16 %[m1], 15, %[m1] op_sel_hi:[0,1]\n"
+        "v_pk_sub_i16 %[m2], %[J], %[x]\n"
+        "v_pk_sub_i16 %[m3], %[y], %[J]\n"
+        "v_or_b32 %[m2], %[m2], %[m3]\n"
+        "v_pk_ashrrev_i16 %[m2], 15, %[m2] op_sel_hi:[0,1]\n"
+        "v_bfi_b32 %[Hd], %[m1], %[vkneg], %[Hd]\n"
+        "v_bfi_b32 %[X1], %[m2], %[vkneg], %[X1]\n"
+        "v_bfi_b32 %[X2], %[m2], %[vkneg], %[X2]\n"
+        "L_nomask1%=:\n"
+        "v_pk_add_i16 %[M], %[Hd], %[S] clamp\n"
+        "v_pk_add_i16 %[M], %[M], -4 op_sel_hi:[1,0] clamp\n"
+        "v_pk_max_i16 %[t1], %[X1], %[X2]\n"
+        "v_pk_max_i16 %[t1], %[M], %[t1]\n"
+        "v_bfi_b32 %[H0], %[inv], %[vkneg], %[t1]\n"
+        "v_pk_add_i16 %[G1], %[H0], %[LJ1] clamp\n"
+        "v_pk_add_i16 %[G2], %[H0], %[LJ2] clamp\n"
+        "v_perm_b32 %[Ga], %[G2], %[G1], %[csel0]\n"
+        "v_perm_b32 %[Gb], %[G2], %[G1], %[csel1]\n"
+        "v_pk_max_i16 %[inc], %[Ga], %[Gb]\n"
+        "v_xor_b32 %[inc], 0x80008000, %[inc]\n"
+        "v_mad_i32_i16 %[amk], %[H0], %[c128], %[clo]\n"
+        "v_mad_i32_i16 %[t1], %[H0], %[c128], %[chi] op_sel:[1,0,0,0]\n"
+        "v_max_i32 %[amk], %[amk], %[t1]\n"
+        "s_nop 1\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:1 row_mask:0xf bank_mask:0xf\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "s_nop 0\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:2 row_mask:0xf bank_mask:0xf\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:4 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 0\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "s_nop 0\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:8 row_mask:0xf bank_mask:0xf\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "s_nop 0\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        "s_nop 0\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "s_nop 1\n"
+        "v_readlane_b32 %[mp], %[amk], 63\n"
+        "v_xor_b32_dpp %[Pa], %[inc], %[vkneg] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_i16 %[Pb], %[Pa], %[Ga]\n"
+        "v_perm_b32 %[P1], %[Pb], %[Pa], %[csel0]\n"
+        "v_perm_b32 %[P2], %[Pb], %[Pa], %[csel1]\n"
+        "v_pk_sub_i16 %[F1], %[P1], %[FJ1] clamp\n"
+        "v_pk_sub_i16 %[F2], %[P2], %[FJ2] clamp\n"
+        "v_pk_max_i16 %[H], %[F1], %[F2]\n"
+        "v_pk_max_i16 %[H], %[H0], %[H]\n"
+        "v_pk_add_i16 %[X1e], %[X1], -2 op_sel_hi:[1,0] clamp\n"
+        "v_pk_add_i16 %[Ho1], %[H], -6 op_sel_hi:[1,0] clamp\n"
+        "v_pk_add_i16 %[X2e], %[X2], -1 clamp\n"
+        "v_pk_sub_i16 %[Ho2], %[H], 25 op_sel_hi:[1,0] clamp\n"
+        "v_pk_max_i16 %[E1], %[X1e], %[Ho1]\n"
+        "v_pk_max_i16 %[E2], %[X2e], %[Ho2]\n"
+        "v_pk_sub_i16 %[d0], %[M], %[H] clamp\n"
+        "v_pk_sub_i16 %[dd], %[X1], %[H] clamp\n"
+        "v_perm_b32 %[x01], %[dd], %[d0], %[cseltb]\n"
+        "v_pk_sub_i16 %[d0], %[X2], %[H] clamp\n"
+        "v_pk_sub_i16 %[dd], %[F1], %[H] clamp\n"
+        "v_perm_b32 %[x23], %[dd], %[d0], %[cseltb]\n"
+        "v_pk_sub_i16 %[d0], %[Ho1], %[X1e] clamp\n"
+        "v_pk_sub_i16 %[dd], %[Ho2], %[X2e] clamp\n"
+        "v_perm_b32 %[x45], %[dd], %[d0], %[cseltb]\n"
+        "v_pk_sub_i16 %[d0], %[G1], %[P1] clamp\n"
+        "v_pk_sub_i16 %[dd], %[G2], %[P2] clamp\n"
+        "v_perm_b32 %[x67], %[dd], %[d0], %[cseltb]\n"
+        "v_and_b32 %[x67], %[x67], %[m67]\n"
+        "v_and_or_b32 %[x67], %[x45], %[m45], %[x67]\n"
+        "v_and_or_b32 %[x67], %[x23], %[m23], %[x67]\n"
+        "v_and_or_b32 %[x67], %[x01], %[m01], %[x67]\n"
+        "v_or_b32_sdwa %[x67], %[x67], %[x67] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
+        "v_add_u32 %[voff], %[tbu], %[vlane2]\n"
+        "global_store_short %[voff], %[x67], %[tbp]\n"
+        "v_bfi_b32 %[Hd], %[inv], %[vkneg], %[H]\n"
+        "v_bfi_b32 %[m1], %[inv], %[vkneg], %[E1]\n"
+        "v_bfi_b32 %[m2], %[inv], %[vkneg], %[E2]\n"
+        "s_add_u32 %[r], %[b0], %[i]\n"
+        "s_and_b32 %[y], %[r], 7\n"
+        "s_mulk_i32 %[y], 0x300\n"
+        "s_add_u32 %[y], %[y], %[Lring]\n"
+        "v_lshl_add_u32 %[a0], %[iw], 2, %[y]\n"
+        "ds_write_b32 %[a0], %[Hd]\n"
+        "ds_write_b32 %[a0], %[m1] offset:256\n"
+        "ds_write_b32 %[a0], %[m2] offset:512\n"
+        "v_pk_add_u16 %[t1], %[Hd], %[cr16] op_sel_hi:[1,0]\n"
+        "v_pk_min_u16 %[r16], %[r16], %[t1]\n"
+        "s_and_b32 %[x], %[mp], 0x7f\n"
+        "s_sub_i32 %[besti], %[cb0], %[x]\n"
+        "s_addk_i32 %[besti], 0x7f\n"
+        "s_bitcmp1_b32 %[d1], 8\n"
+        "s_cbranch_scc1 L_far1%=\n"
+        "s_sub_i32 %[x], %[tbu], %[cb0]\n"
+        "s_sub_i32 %[z], %[kpu], %[cb0]\n"
+        "v_mov_b32 v120, %[beg]\n"
+        "v_mov_b32 v121, %[end]\n"
+        "v_mov_b32 v122, %[x]\n"
+        "v_mov_b32 v123, %[z]\n"
+        "v_mov_b32 v124, %[besti]\n"
+        "s_and_b32 %[x], %[r], 31\n"
+        "s_lshl_b32 %[x], %[x], 4\n"
+        "s_add_u32 %[x], %[x], %[Lrrow]\n"
+        "v_mov_b32 %[a0], %[x]\n"
+        "s_lshl_b32 %[x], %[r], 5\n"
+        "v_mov_b32 %[voff], %[x]\n"
+        "v_mov_b32 v125, -1\n"
+        "s_mov_b64 exec, 1\n"
+        "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
+        "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
+        "s_mov_b64 exec, -1\n"
+        "s_sub_i32 %[x], %[end], %[beg]\n"
+        "s_add_i32 %[cel], %[cel], %[x]\n"
+        "s_add_i32 %[x], %[spm], 4\n"
+        "s_and_b32 %[x], %[x], -4\n"
+        "s_add_i32 %[tbu], %[tbu], %[x]\n"
+        "s_mov_b32 %[pr], %[r]\n"
+        "s_mov_b32 %[pb], %[beg]\n"
+        "s_mov_b32 %[pe], %[end]\n"
+        "s_mov_b32 %[pa], %[besti]\n"
+        "s_mov_b32 %[pwb], %[y]\n"
+        "s_add_i32 %[i], %[i], 1\n"
+        "s_branch L_top%=\n"
+        "L_far1%=:\n"
+        "s_lshl_b32 %[x], %[svu], 2\n"
+        "v_add_u32 %[voff], %[x], %[vlane8]\n"
+        "v_bfe_i32 v120, %[H], 0, 16\n"
+        "v_ashrrev_i32 v121, 16, %[H]\n"
+        "v_bfe_i32 v122, %[E1], 0, 16\n"
+        "v_ashrrev_i32 v123, 16, %[E1]\n"
+        "v_bfe_i32 v124, %[E2], 0, 16\n"
+        "v_ashrrev_i32 v125, 16, %[E2]\n"
+        "global_store_dwordx2 %[voff], v[120:121], %[svp]\n"
+        "global_store_dwordx2 %[voff], v[122:123], %[svp] offset:512\n"
+        "global_store_dwordx2 %[voff], v[124:125], %[svp] offset:1024\n"
+        "s_sub_i32 %[x], %[tbu], %[cb0]\n"
+        "s_sub_i32 %[z], %[kpu], %[cb0]\n"
+        "v_mov_b32 v120, %[beg]\n"
+        "v_mov_b32 v121, %[end]\n"
+        "v_mov_b32 v122, %[x]\n"
+        "v_mov_b32 v123, %[z]\n"
+        "v_mov_b32 v124, %[besti]\n"
+        "s_and_b32 %[x], %[r], 31\n"
+        "s_lshl_b32 %[x], %[x], 4\n"
+        "s_add_u32 %[x], %[x], %[Lrrow]\n"
+        "v_mov_b32 %[a0], %[x]\n"
+        "s_lshl_b32 %[x], %[r], 5\n"
+        "v_mov_b32 %[voff], %[x]\n"
+        "v_mov_b32 v125, %[svu]\n"
+        "s_mov_b64 exec, 1\n"
+        "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
+        "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
+        "global_store_dwordx2 %[voff], v[124:125], %[rip] offset:16\n"
+        "s_addk_i32 %[svu], 0x180\n"
+        "s_mov_b64 exec, -1\n"
+        "s_sub_i32 %[x], %[end], %[beg]\n"
+        "s_add_i32 %[cel], %[cel], %[x]\n"
+        "s_add_i32 %[x], %[spm], 4\n"
+        "s_and_b32 %[x], %[x], -4\n"
+        "s_add_i32 %[tbu], %[tbu], %[x]\n"
+        "s_mov_b32 %[pr], %[r]\n"
+        "s_mov_b32 %[pb], %[beg]\n"
+        "s_mov_b32 %[pe], %[end]\n"
+        "s_mov_b32 %[pa], %[besti]\n"
+        "s_mov_b32 %[pwb], %[y]\n"
+        "s_add_i32 %[i], %[i], 1\n"
+        "s_branch L_top%=\n"
+        "L_two%=:\n"
+        "s_cmp_lg_u32 %[y], 0x28000\n"
+        "s_cbranch_scc1 L_out%=\n"
+        "v_readfirstlane_b32 %[p1], %[vp1]\n"
+        "s_cmp_eq_u32 %[p1], %[pr]\n"
+        "s_cbranch_scc0 L_p1lds%=\n"
+        "s_mov_b32 %[rb1], %[pb]\n"
+        "s_mov_b32 %[re1], %[pe]\n"
+        "s_mov_b32 %[ra1], %[pa]\n"
+        "s_mov_b32 %[base1], %[pwb]\n"
+        "s_branch L_p1ok%=\n"
+        "L_p1lds%=:\n"
+        "s_and_b32 %[x], %[p1], 31\n"
+        "s_lshl_b32 %[x], %[x], 4\n"
+        "s_add_u32 %[x], %[x], %[Lrrow]\n"
+        "v_mov_b32 %[va], %[x]\n"
+        "ds_read_b32 %[vd1], %[va]\n"
+        "ds_read_b32 %[vrem], %[va] offset:4\n"
+        "ds_read_b32 %[vp0], %[va] offset:8\n"
+        "s_and_b32 %[x], %[p1], 7\n"
+        "s_mulk_i32 %[x], 0x300\n"
+        "s_add_u32 %[base1], %[x], %[Lring]\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 %[rb1], %[vd1]\n"
+        "v_readfirstlane_b32 %[re1], %[vrem]\n"
+        "v_readfirstlane_b32 %[ra1], %[vp0]\n"
+        "L_p1ok%=:\n"
+        "s_cmp_eq_u32 %[p0], %[pr]\n"
+        "s_cbranch_scc1 L_p0ok2%=\n"
+        "s_and_b32 %[x], %[p0], 31\n"
+        "s_lshl_b32 %[x], %[x], 4\n"
+        "s_add_u32 %[x], %[x], %[Lrrow]\n"
+        "v_mov_b32 %[va], %[x]\n"
+        "ds_read_b32 %[vd1], %[va]\n"
+        "ds_read_b32 %[vrem], %[va] offset:4\n"
+        "ds_read_b32 %[vp0], %[va] offset:8\n"
+        "s_and_b32 %[x], %[p0], 7\n"
+        "s_mulk_i32 %[x], 0x300\n"
+        "s_add_u32 %[pwb], %[x], %[Lring]\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 %[pb], %[vd1]\n"
+        "v_readfirstlane_b32 %[pe], %[vrem]\n"
+        "v_readfirstlane_b32 %[pa], %[vp0]\n"
+        "s_mov_b32 %[pr], %[p0]\n"
+        "L_p0ok2%=:\n"
+        "s_sub_i32 %[x], %[qlen], %[rem]\n"
+        "s_min_i32 %[y], %[pa], %[ra1]\n"
+        "s_max_i32 %[z], %[pa], %[ra1]\n"
+        "s_add_i32 %[y], %[y], 1\n"
+        "s_add_i32 %[z], %[z], 1\n"
+        "s_min_i32 %[y], %[y], %[x]\n"
+        "s_max_i32 %[z], %[z], %[x]\n"
+        "s_sub_i32 %[y], %[y], %[w]\n"
+        "s_add_i32 %[z], %[z], %[w]\n"
+        "s_max_i32 %[beg], %[y], 0\n"
+        "s_min_i32 %[end], %[z], %[qlen]\n"
+        "s_and_b32 %[cb0], %[beg], -2\n"
+        "s_sub_i32 %[spm], %[end], %[cb0]\n"
+        "s_and_b32 %[pc0], %[pb], -2\n"
+        "s_sub_i32 %[x], %[pe], %[pc0]\n"
+        "s_max_i32 %[x], %[x], %[spm]\n"
+        "s_and_b32 %[pc1], %[rb1], -2\n"
+        "s_sub_i32 %[y], %[re1], %[pc1]\n"
+        "s_max_i32 %[x], %[x], %[y]\n"
+        "s_cmpk_gt_i32 %[x], 0x7f\n"
+        "s_cbranch_scc1 L_out%=\n"
+        "s_bfe_u32 %[z], %[d1], 0x80000\n"
+        "s_lshl_b32 %[x], %[z], 3\n"
+        "s_lshl_b32 %[tlo], 9, %[x]\n"
+        "s_cmp_gt_u32 %[z], 3\n"
+        "s_cselect_b32 %[tlo], %[cth], %[tlo]\n"
+        "s_pack_ll_b32_b16 %[pkb], %[beg], %[beg]\n"
+        "s_pack_ll_b32_b16 %[pke], %[end], %[end]\n"
+        "s_bfe_u32 %[x], %[cb0], 0xf0001\n"
+        "v_add_u32 %[t], %[x], %[vlane]\n"
+        "v_mad_u32_u24 %[J], %[t], %[c20002], %[v10000]\n"
+        "v_add_u32 %[va], %[Lq], %[t]\n"
+        "ds_read_u8 %[q], %[va]\n"
+        "v_and_b32 %[iw], 63, %[t]\n"
+        "v_lshl_add_u32 %[a0], %[iw], 2, %[pwb]\n"
+        "ds_read_b32 %[w0], %[a0]\n"
+        "ds_read_b32 %[X1], %[a0] offset:256\n"
+        "ds_read_b32 %[X2], %[a0] offset:512\n"
+        "v_pk_sub_i16 %[m1], %[J], %[pkb]\n"
+        "v_pk_sub_i16 %[m2], %[pke], %[J]\n"
+        "v_or_b32 %[m1], %[m1], %[m2]\n"
+        "v_pk_ashrrev_i16 %[inv], 15, %[m1] op_sel_hi:[0,1]\n"
+        "s_waitcnt lgkmcnt(3)\n"
+        "v_mul_u32_u24 %[sel], 0x1001, %[q]\n"
+        "v_and_or_b32 %[sel], %[sel], %[cq], %[v0c0c]\n"
+        "v_perm_b32 %[S], 4, %[tlo], %[sel]\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_mov_b32_dpp %[w0p], %[w0] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
+        "v_alignbit_b32 %[Hd], %[w0], %[w0p], 16\n"
+        "s_max_i32 %[x], %[pc0], %[pc1]\n"
+        "s_cmp_le_i32 %[beg], %[x]\n"
+        "s_cbranch_scc1 L_mask2%=\n"
+        "s_min_i32 %[x], %[pc0], %[pc1]\n"
+        "s_addk_i32 %[x], 0x7f\n"
+        "s_cmp_le_i32 %[end], %[x]\n"
+        "s_cbranch_scc1 L_nomask2%=\n"
+        "L_mask2%=:\n"
+        "s_pack_ll_b32_b16 %[x], %[pb], %[pb]\n"
+        "s_pack_ll_b32_b16 %[y], %[pe], %[pe]\n"
+        "v_pk_add_u16 %[m3], %[J], -1\n"
+        "v_pk_sub_i16 %[m1], %[m3], %[x]\n"
+        "v_pk_sub_i16 %[m2], %[y], %[m3]\n"
+        "v_or_b32 %[m1], %[m1], %[m2]\n"
+        "v_pk_ashrrev_i16 %[m1], 15, %[m1] op_sel_hi:[0,1]\n"
+        "v_pk_sub_i16 %[m2], %[J], %[x]\n"
+        "v_pk_sub_i16 %[m3], %[y], %[J]\n"
+        "v_or_b32 %[m2], %[m2], %[m3]\n"
+        "v_pk_ashrrev_i16 %[m2], 15, %[m2] op_sel_hi:[0,1]\n"
+        "v_bfi_b32 %[Hd], %[m1], %[vkneg], %[Hd]\n"
+        "v_bfi_b32 %[X1], %[m2], %[vkneg], %[X1]\n"
+        "v_bfi_b32 %[X2], %[m2], %[vkneg], %[X2]\n"
+        "v_lshl_add_u32 %[a0], %[iw], 2, %[base1]\n"
+        "ds_read_b32 %[w0], %[a0]\n"
+        "ds_read_b32 %[X11], %[a0] offset:256\n"
+        "ds_read_b32 %[X21], %[a0] offset:512\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_mov_b32_dpp %[w0p], %[w0] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
+        "v_alignbit_b32 %[Hd1], %[w0], %[w0p], 16\n"
+        "s_pack_ll_b32_b16 %[x], %[rb1], %[rb1]\n"
+        "s_pack_ll_b32_b16 %[y], %[re1], %[re1]\n"
+        "v_pk_add_u16 %[m3], %[J], -1\n"
+        "v_pk_sub_i16 %[m1], %[m3], %[x]\n"
+        "v_pk_sub_i16 %[m2], %[y], %[m3]\n"
+        "v_or_b32 %[m1], %[m1], %[m2]\n"
+        "v_pk_ashrrev_i16 %[m1], 15, %[m1] op_sel_hi:[0,1]\n"
+        "v_pk_sub_i16 %[m2], %[J], %[x]\n"
+        "v_pk_sub_i16 %[m3], %[y], %[J]\n"
+        "v_or_b32 %[m2], %[m2], %[m3]\n"
+        "v_pk_ashrrev_i16 %[m2], 15, %[m2] op_sel_hi:[0,1]\n"
+        "v_bfi_b32 %[Hd1], %[m1], %[vkneg], %[Hd1]\n"
+        "v_bfi_b32 %[X11], %[m2], %[vkneg], %[X11]\n"
+        "v_bfi_b32 %[X21], %[m2], %[vkneg], %[X21]\n"
+        "s_branch L_merge2%=\n"
+        "L_nomask2%=:\n"
+        "v_lshl_add_u32 %[a0], %[iw], 2, %[base1]\n"
+        "ds_read_b32 %[w0], %[a0]\n"
+        "ds_read_b32 %[X11], %[a0] offset:256\n"
+        "ds_read_b32 %[X21], %[a0] offset:512\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_mov_b32_dpp %[w0p], %[w0] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
+        "v_alignbit_b32 %[Hd1], %[w0], %[w0p], 16\n"
+        "L_merge2%=:\n"
+        "v_pk_sub_i16 %[MK], %[Hd], %[Hd1] clamp\n"
+        "v_pk_lshrrev_b16 %[MK], 15, %[MK] op_sel_hi:[0,1]\n"
+        "v_pk_sub_i16 %[K1], %[X1], %[X11] clamp\n"
+        "v_pk_lshrrev_b16 %[K1], 15, %[K1] op_sel_hi:[0,1]\n"
+        "v_pk_sub_i16 %[K2], %[X2], %[X21] clamp\n"
+        "v_pk_lshrrev_b16 %[K2], 15, %[K2] op_sel_hi:[0,1]\n"
+        "v_pk_max_i16 %[Hd], %[Hd], %[Hd1]\n"
+        "v_pk_max_i16 %[X1], %[X1], %[X11]\n"
+        "v_pk_max_i16 %[X2], %[X2], %[X21]\n"
+        "v_pk_add_i16 %[M], %[Hd], %[S] clamp\n"
+        "v_pk_add_i16 %[M], %[M], -4 op_sel_hi:[1,0] clamp\n"
+        "v_pk_max_i16 %[t1], %[X1], %[X2]\n"
+        "v_pk_max_i16 %[t1], %[M], %[t1]\n"
+        "v_bfi_b32 %[H0], %[inv], %[vkneg], %[t1]\n"
+        "v_pk_add_i16 %[G1], %[H0], %[LJ1] clamp\n"
+        "v_pk_add_i16 %[G2], %[H0], %[LJ2] clamp\n"
+        "v_perm_b32 %[Ga], %[G2], %[G1], %[csel0]\n"
+        "v_perm_b32 %[Gb], %[G2], %[G1], %[csel1]\n"
+        "v_pk_max_i16 %[inc], %[Ga], %[Gb]\n"
+        "v_xor_b32 %[inc], 0x80008000, %[inc]\n"
+        "v_mad_i32_i16 %[amk], %[H0], %[c128], %[clo]\n"
+        "v_mad_i32_i16 %[t1], %[H0], %[c128], %[chi] op_sel:[1,0,0,0]\n"
+        "v_max_i32 %[amk], %[amk], %[t1]\n"
+        "s_nop 1\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:1 row_mask:0xf bank_mask:0xf\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "s_nop 0\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:2 row_mask:0xf bank_mask:0xf\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:4 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 0\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "s_nop 0\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:8 row_mask:0xf bank_mask:0xf\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "s_nop 0\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "v_max_i32_dpp %[amk], %[amk], %[amk] row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        "s_nop 0\n"
+        "v_mov_b32_dpp %[t1], %[inc] row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
+        "s_nop 1\n"
+        "v_readlane_b32 %[mp], %[amk], 63\n"
+        "v_xor_b32_dpp %[Pa], %[inc], %[vkneg] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_pk_max_i16 %[Pb], %[Pa], %[Ga]\n"
+        "v_perm_b32 %[P1], %[Pb], %[Pa], %[csel0]\n"
+        "v_perm_b32 %[P2], %[Pb], %[Pa], %[csel1]\n"
+        "v_pk_sub_i16 %[F1], %[P1], %[FJ1] clamp\n"
+        "v_pk_sub_i16 %[F2], %[P2], %[FJ2] clamp\n"
+        "v_pk_max_i16 %[H], %[F1], %[F2]\n"
+        "v_pk_max_i16 %[H], %[H0], %[H]\n"
+        "v_pk_add_i16 %[X1e], %[X1], -2 op_sel_hi:[1,0] clamp\n"
+        "v_pk_add_i16 %[Ho1], %[H], -6 op_sel_hi:[1,0] clamp\n"
+        "v_pk_add_i16 %[X2e], %[X2], -1 clamp\n"
+        "v_pk_sub_i16 %[Ho2], %[H], 25 op_sel_hi:[1,0] clamp\n"
+        "v_pk_max_i16 %[E1], %[X1e], %[Ho1]\n"
+        "v_pk_max_i16 %[E2], %[X2e], %[Ho2]\n"
+        "v_pk_sub_i16 %[d0], %[M], %[H] clamp\n"
+        "v_pk_sub_i16 %[dd], %[X1], %[H] clamp\n"
+        "v_perm_b32 %[x01], %[dd], %[d0], %[cseltb]\n"
+        "v_pk_sub_i16 %[d0], %[X2], %[H] clamp\n"
+        "v_pk_sub_i16 %[dd], %[F1], %[H] clamp\n"
+        "v_perm_b32 %[x23], %[dd], %[d0], %[cseltb]\n"
+        "v_pk_sub_i16 %[d0], %[Ho1], %[X1e] clamp\n"
+        "v_pk_sub_i16 %[dd], %[Ho2], %[X2e] clamp\n"
+        "v_perm_b32 %[x45], %[dd], %[d0], %[cseltb]\n"
+        "v_pk_sub_i16 %[d0], %[G1], %[P1] clamp\n"
+        "v_pk_sub_i16 %[dd], %[G2], %[P2] clamp\n"
+        "v_perm_b32 %[x67], %[dd], %[d0], %[cseltb]\n"
+        "v_and_b32 %[x67], %[x67], %[m67]\n"
+        "v_and_or_b32 %[x67], %[x45], %[m45], %[x67]\n"
+        "v_and_or_b32 %[x67], %[x23], %[m23], %[x67]\n"
+        "v_and_or_b32 %[x67], %[x01], %[m01], %[x67]\n"
+        "v_or_b32_sdwa %[x67], %[x67], %[x67] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
+        "v_add_u32 %[voff], %[tbu], %[vlane2]\n"
+        "global_store_short %[voff], %[x67], %[tbp]\n"
+        "v_lshlrev_b32 %[K1], 2, %[K1]\n"
+        "v_lshlrev_b32 %[K2], 4, %[K2]\n"
+        "v_or3_b32 %[MK], %[MK], %[K1], %[K2]\n"
+        "v_perm_b32 %[MK], 0, %[MK], %[cselkp]\n"
+        "v_add_u32 %[voff], %[kpu], %[vlane2]\n"
+        "global_store_short %[voff], %[MK], %[kpp]\n"
+        "v_bfi_b32 %[Hd], %[inv], %[vkneg], %[H]\n"
+        "v_bfi_b32 %[m1], %[inv], %[vkneg], %[E1]\n"
+        "v_bfi_b32 %[m2], %[inv], %[vkneg], %[E2]\n"
+        "s_add_u32 %[r], %[b0], %[i]\n"
+        "s_and_b32 %[y], %[r], 7\n"
+        "s_mulk_i32 %[y], 0x300\n"
+        "s_add_u32 %[y], %[y], %[Lring]\n"
+        "v_lshl_add_u32 %[a0], %[iw], 2, %[y]\n"
+        "ds_write_b32 %[a0], %[Hd]\n"
+        "ds_write_b32 %[a0], %[m1] offset:256\n"
+        "ds_write_b32 %[a0], %[m2] offset:512\n"
+        "v_pk_add_u16 %[t1], %[Hd], %[cr16] op_sel_hi:[1,0]\n"
+        "v_pk_min_u16 %[r16], %[r16], %[t1]\n"
+        "s_and_b32 %[x], %[mp], 0x7f\n"
+        "s_sub_i32 %[besti], %[cb0], %[x]\n"
+        "s_addk_i32 %[besti], 0x7f\n"
+        "s_bitcmp1_b32 %[d1], 8\n"
+        "s_cbranch_scc1 L_far2%=\n"
+        "s_sub_i32 %[x], %[tbu], %[cb0]\n"
+        "s_sub_i32 %[z], %[kpu], %[cb0]\n"
+        "v_mov_b32 v120, %[beg]\n"
+        "v_mov_b32 v121, %[end]\n"
+        "v_mov_b32 v122, %[x]\n"
+        "v_mov_b32 v123, %[z]\n"
+        "v_mov_b32 v124, %[besti]\n"
+        "s_and_b32 %[x], %[r], 31\n"
+        "s_lshl_b32 %[x], %[x], 4\n"
+        "s_add_u32 %[x], %[x], %[Lrrow]\n"
+        "v_mov_b32 %[a0], %[x]\n"
+        "s_lshl_b32 %[x], %[r], 5\n"
+        "v_mov_b32 %[voff], %[x]\n"
+        "v_mov_b32 v125, -1\n"
+        "s_mov_b64 exec, 1\n"
+        "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
+        "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
+        "s_mov_b64 exec, -1\n"
+        "s_sub_i32 %[x], %[end], %[beg]\n"
+        "s_add_i32 %[cel], %[cel], %[x]\n"
+        "s_add_i32 %[x], %[spm], 4\n"
+        "s_and_b32 %[x], %[x], -4\n"
+        "s_add_i32 %[tbu], %[tbu], %[x]\n"
+        "s_add_i32 %[kpu], %[kpu], %[x]\n"
+        "s_mov_b32 %[pr], %[r]\n"
+        "s_mov_b32 %[pb], %[beg]\n"
+        "s_mov_b32 %[pe], %[end]\n"
+        "s_mov_b32 %[pa], %[besti]\n"
+        "s_mov_b32 %[pwb], %[y]\n"
+        "s_add_i32 %[i], %[i], 1\n"
+        "s_branch L_top%=\n"
+        "L_far2%=:\n"
+        "s_lshl_b32 %[x], %[svu], 2\n"
+        "v_add_u32 %[voff], %[x], %[vlane8]\n"
+        "v_bfe_i32 v120, %[H], 0, 16\n"
+        "v_ashrrev_i32 v121, 16, %[H]\n"
+        "v_bfe_i32 v122, %[E1], 0, 16\n"
+        "v_ashrrev_i32 v123, 16, %[E1]\n"
+        "v_bfe_i32 v124, %[E2], 0, 16\n"
+        "v_ashrrev_i32 v125, 16, %[E2]\n"
+        "global_store_dwordx2 %[voff], v[120:121], %[svp]\n"
+        "global_store_dwordx2 %[voff], v[122:123], %[svp] offset:512\n"
+        "global_store_dwordx2 %[voff], v[124:125], %[svp] offset:1024\n"
+        "s_sub_i32 %[x], %[tbu], %[cb0]\n"
+        "s_sub_i32 %[z], %[kpu], %[cb0]\n"
+        "v_mov_b32 v120, %[beg]\n"
+        "v_mov_b32 v121, %[end]\n"
+        "v_mov_b32 v122, %[x]\n"
+        "v_mov_b32 v123, %[z]\n"
+        "v_mov_b32 v124, %[besti]\n"
+        "s_and_b32 %[x], %[r], 31\n"
+        "s_lshl_b32 %[x], %[x], 4\n"
+        "s_add_u32 %[x], %[x], %[Lrrow]\n"
+        "v_mov_b32 %[a0], %[x]\n"
+        "s_lshl_b32 %[x], %[r], 5\n"
+        "v_mov_b32 %[voff], %[x]\n"
+        "v_mov_b32 v125, %[svu]\n"
+        "s_mov_b64 exec, 1\n"
+        "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
+        "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
+        "global_store_dwordx2 %[voff], v[124:125], %[rip] offset:16\n"
+        "s_addk_i32 %[svu], 0x180\n"
+        "s_mov_b64 exec, -1\n"
+        "s_sub_i32 %[x], %[end], %[beg]\n"
+        "s_add_i32 %[cel], %[cel], %[x]\n"
+        "s_add_i32 %[x], %[spm], 4\n"
+        "s_and_b32 %[x], %[x], -4\n"
+        "s_add_i32 %[tbu], %[tbu], %[x]\n"
+        "s_add_i32 %[kpu], %[kpu], %[x]\n"
+        "s_mov_b32 %[pr], %[r]\n"
+        "s_mov_b32 %[pb], %[beg]\n"
+        "s_mov_b32 %[pe], %[end]\n"
+        "s_mov_b32 %[pa], %[besti]\n"
+        "s_mov_b32 %[pwb], %[y]\n"
+        "s_add_i32 %[i], %[i], 1\n"
+        "s_branch L_top%=\n"
+        "L_out%=:\n"
+        "s_sub_i32 %[x], %[i], %[i0]\n"
+        "s_add_i32 %[cel], %[cel], %[x]\n"
+        "s_nop 1\n"
+        : [i] "+s"(i), [pr] "+s"(pr), [pb] "+s"(pb), [pe] "+s"(pe), [pa] "+s"(pa), [tbu] "+s"(tbu),
+          [kpu] "+s"(kpu), [svu] "+s"(svu), [cel] "+s"(cel), [r16] "+v"(r16),
+          [d1] "=&s"(d1), [rem] "=&s"(rem), [p0] "=&s"(p0), [p1] "=&s"(p1), [rb1] "=&s"(rb1), [re1] "=&s"(re1),
+          [ra1] "=&s"(ra1), [x] "=&s"(x), [y] "=&s"(y), [z] "=&s"(z), [beg] "=&s"(beg), [end] "=&s"(end),
+          [cb0] "=&s"(cb0), [spm] "=&s"(spm), [pc0] "=&s"(pc0), [pc1] "=&s"(pc1), [tlo] "=&s"(tlo), [pkb] "=&s"(pkb),
+          [pke] "=&s"(pke), [base1] "=&s"(base1), [mp] "=&s"(mp), [besti] "=&s"(besti), [r] "=&s"(r),
+          [pwb] "=&s"(pwb), [i0] "=&s"(i0), [c20002] "=&s"(c20002), [c128] "=&s"(c128), [cr16] "=&s"(cr16),
+          [cq] "=&s"(cq), [cth] "=&s"(cth),
+          [va] "=&v"(va), [vd1] "=&v"(vd1), [vrem] "=&v"(vrem), [vp0] "=&v"(vp0), [vp1] "=&v"(vp1), [t] "=&v"(t),
+          [J] "=&v"(J), [q] "=&v"(q), [iw] "=&v"(iw), [a0] "=&v"(a0),
+          [w0] "=&v"(w0), [w0p] "=&v"(w0p), [inv] "=&v"(inv), [m1] "=&v"(m1), [m2] "=&v"(m2), [m3] "=&v"(m3),
+          [sel] "=&v"(sel), [S] "=&v"(S), [Hd] "=&v"(Hd), [X1] "=&v"(X1), [X2] "=&v"(X2), [Hd1] "=&v"(Hd1),
+          [X11] "=&v"(X11), [X21] "=&v"(X21), [MK] "=&v"(MK), [K1] "=&v"(K1), [K2] "=&v"(K2), [M] "=&v"(M),
+          [H0] "=&v"(H0), [G1] "=&v"(G1), [G2] "=&v"(G2), [Ga] "=&v"(Ga), [Gb] "=&v"(Gb), [inc] "=&v"(inc),
+          [amk] "=&v"(amk), [t1] "=&v"(t1), [Pa] "=&v"(Pa), [Pb] "=&v"(Pb), [P1] "=&v"(P1), [P2] "=&v"(P2),
+          [F1] "=&v"(F1), [F2] "=&v"(F2), [H] "=&v"(H), [X1e] "=&v"(X1e), [Ho1] "=&v"(Ho1), [X2e] "=&v"(X2e),
+          [Ho2] "=&v"(Ho2), [E1] "=&v"(E1), [E2] "=&v"(E2), [d0] "=&v"(d0), [dd] "=&v"(dd), [x01] "=&v"(x01),
+          [x23] "=&v"(x23), [x45] "=&v"(x45), [x67] "=&v"(x67), [voff] "=&v"(voff)
+        : [iend] "s"(iend), [b0] "s"(b0), [qlen] "s"(qlen), [w] "s"(w), [Ldesc] "s"(Ldesc), [Lrrow] "s"(Lrrow),
+          [Lring] "s"(Lring), [Lq] "s"(Lq), [tbp] "s"(tbp), [kpp] "s"(kpp), [svp] "s"(svp), [rip] "s"(rip),
+          [vlane] "v"(vlane), [vlane2] "v"(vlane2), [vlane8] "v"(vlane8), [LJ1] "v"(LJ1), [LJ2] "v"(LJ2),
+          [FJ1] "v"(FJ1), [FJ2] "v"(FJ2), [clo] "v"(clo), [chi] "v"(chi), [vkneg] "v"(vkneg), [v10000] "v"(v10000),
+          [csel0] "v"(csel0), [csel1] "v"(csel1), [cseltb] "v"(cseltb), [cselkp] "v"(cselkp), [m01] "v"(m01),
+          [m23] "v"(m23), [m45] "v"(m45), [m67] "v"(m67), [v0c0c] "v"(v0c0c)
+        : "memory", "scc", "v120", "v121", "v122", "v123", "v124", "v125");
+    prv_r = pr;
+    prv_beg = pb;
+    prv_end = pe;
+    prv_am = pa;
+    ds.tb_used = tbu;
+    ds.kp_used = kpu;
+    ds.sv_used = svu;
+    ds.cells = cel;
+    ds.r16acc = r16;
+    return i;
+}
+
 // The row loop of 16-bit mode (same rows, same results as run_dp<SC, true>).  The per-row
 // control is written for the scalar unit: tests accumulate as sign bits into one word
 // (`bad < 0` = take the generic row) rather than as bools, which the compiler would keep as
@@ -2176,6 +2874,18 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         auto rows = [&](auto capchk) -> int {
         constexpr bool CAP = decltype(capchk)::value;
     for (int i = i0; i < iend; ++i) {
+        if constexpr (RW == kChunk && NW == 1 && !CAP && std::is_same<SC, DefaultScores>::value) {
+            // the fast rows with one or two predecessors in the ring (~90 % of the rows), hand-scheduled
+            const int j = fast_rows_asm(sh, lane, tb, kp, sv, rinfo, b0, i, iend, qlen, w, prv_r, prv_beg, prv_end,
+                                        prv_am, ds);
+            if (j != i) {
+                nfast += j - i;
+                i = j;
+                if (i >= iend) break;
+                nA = *reinterpret_cast<const int4 *>(&sh.desc[i][0]);
+                np1 = sh.desc[i][4];
+            }
+        }
         const int r = b0 + i;
         const int4 dA = nA;
         const int dp1 = np1;

@@ -103,7 +103,7 @@ def test_seeded_groups_mixed_with_unseeded():
 @pytest.mark.parametrize("persistent", [False, True])
 def test_grid_modes_and_launch_kinds(gpu_ctx, persistent):
     """One-group grids (a workgroup per group, workspace slots claimed from a flag array) and the
-    persistent grid (fewer slots than groups: a 1 GiB workspace budget) give the same consensi; the batch
+    persistent grid (fewer slots than groups: a 128 MiB workspace budget) give the same consensi; the batch
     spans the narrow (3 kb), wide (6-9 kb: 256-column ring rows, 16-bit mode shifted past 6.4 kb) and
     32-bit wide (> 10.1 kb) launch kinds at once."""
     from mandalorion_amd import _lib
@@ -112,7 +112,7 @@ def test_grid_modes_and_launch_kinds(gpu_ctx, persistent):
     _, wide = poa_cases.noisy_groups(4, (6000, 9000), (4, 10), seed=82)
     _, longer = poa_cases.noisy_groups(2, (10500, 11500), (3, 5), seed=83)
     ctx = _lib.context(0, 0)
-    ctx.set_poa_budget((1 << 30) if persistent else 0)
+    ctx.set_poa_budget((128 << 20) if persistent else 0)
     try:
         _check(narrow + wide + longer)
         if persistent:
