@@ -2120,15 +2120,6 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
                   "the constants below are abPOA's defaults");
     static_assert(kRing16 == 8 && kChunk == 128 && kRowRing == 32 && kDescInts == 8 && kRowInfoInts == 8,
                   "LDS / HBM geometry the block assumes");
-    // lane constants (as in row16_vec): the lane's two columns relative to the chunk, times the gap
-    // extensions, and the argmax key offsets
-    const uint32_t LJ = (uint32_t)(2 * lane) * 0x10001u + 0x10000u;
-    const uint32_t LJ1 = as_u32(as_u16x2(LJ) * (u16x2){2, 2});
-    const uint32_t LJ2 = LJ;
-    const uint32_t FJ1 = LJ1 + pk2(SC::o1 + SC::e1 - SC::e1), FJ2 = LJ2 + pk2(SC::o2 + SC::e2 - SC::e2);
-    const int clo = 127 - 2 * lane, chi = 126 - 2 * lane;
-    const uint32_t vlane = (uint32_t)lane, vlane2 = 2u * (uint32_t)lane, vlane8 = 8u * (uint32_t)lane;
-    const uint32_t vkneg = kNeg2, v10000 = 0x10000u;
     const uint32_t Ldesc = lds_addr(&sh.desc[0][0]), Lrrow = lds_addr(&sh.rrow[0]);
     const uint32_t Lring = lds_addr(ring16_row<kChunk>(sh, 0)), Lq = lds_addr(qnib<kChunk>());
     const uint64_t tbp = (uint64_t)uni64((int64_t)tb), kpp = (uint64_t)uni64((int64_t)kp);
@@ -2136,13 +2127,17 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
     int pr = prv_r, pb = prv_beg, pe = prv_end, pa = prv_am;
     int tbu = ds.tb_used, kpu = ds.kp_used, svu = ds.sv_used, cel = ds.cells;
     uint32_t r16 = ds.r16acc;
+    (void)lane;
+    // scalar temporaries and constants
     int d1, rem, p0, p1, rb1, re1, ra1, x, y, z, beg, end, cb0, spm, pc0, pc1, tlo, pkb, pke, base1, mp, besti, r, pwb,
-        i0, c20002, c128, cr16, cq, cth;
-    uint32_t va, vd1, vrem, vp0, vp1, t, J, q, iw, a0, w0, w0p, inv, m1, m2, m3, sel, S, Hd, X1, X2, Hd1,
-        X11, X21, MK, K1, K2, M, H0, G1, G2, Ga, Gb, inc, amk, t1, Pa, Pb, P1, P2, F1, F2, H, X1e, Ho1, X2e, Ho2, E1,
-        E2, d0, dd, x01, x23, x45, x67, voff;
-    const uint32_t csel0 = 0x05040100u, csel1 = 0x07060302u, cseltb = 0x0B0A0908u, cselkp = 0x0C0C0200u;
-    const uint32_t m01 = 0x02020101u, m23 = 0x08080404u, m45 = 0x20201010u, m67 = 0x80804040u, v0c0c = 0x0C000C00u;
+        i0, c20002, c128, cr16, cq, cth, csel0, csel1, cseltb, cselkp, m01, m23, m45, m67;
+    // vector temporaries (several names of the row share a register where their lifetimes do not
+    // overlap: the address and descriptor words of the row head live in the G / P registers of the F
+    // scan, the read's code and selector in S, ... -- 34 registers instead of 57, so the block leaves
+    // the kernel's other values in registers) and the lane constants, set at the block's entry
+    uint32_t Ga, Gb, Pa, Pb, inc, S, M, H0, E1, t1, F1, P1, P2, iw, a0, inv, m1, m2, Hd, X1, X2, MK, K1, K2, G1, G2,
+        amk, H, X1e, Ho1, X2e, Ho2, E2, voff, vlane, vlane2, vlane8, LJ1, LJ2, FJ1, FJ2, clo, chi, vkneg, v10000,
+        v0c0c;
     asm volatile(
         "s_nop 4\n"
         "s_waitcnt lgkmcnt(0)\n"
@@ -2151,6 +2146,28 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "s_movk_i32 %[cr16], 0x7918\n"
         "s_mov_b32 %[cq], 0xf000f\n"
         "s_mov_b32 %[cth], 0x4040404\n"
+        "s_mov_b32 %[csel0], 0x5040100\n"
+        "s_mov_b32 %[csel1], 0x7060302\n"
+        "s_mov_b32 %[cseltb], 0xb0a0908\n"
+        "s_mov_b32 %[cselkp], 0xc0c0200\n"
+        "s_mov_b32 %[m01], 0x2020101\n"
+        "s_mov_b32 %[m23], 0x8080404\n"
+        "s_mov_b32 %[m45], 0x20201010\n"
+        "s_mov_b32 %[m67], 0x80804040\n"
+        "v_mbcnt_lo_u32_b32 %[vlane], -1, 0\n"
+        "v_mbcnt_hi_u32_b32 %[vlane], -1, %[vlane]\n"
+        "v_lshlrev_b32 %[vlane2], 1, %[vlane]\n"
+        "v_lshlrev_b32 %[vlane8], 3, %[vlane]\n"
+        "v_mul_u32_u24 %[LJ2], 0x10001, %[vlane2]\n"
+        "v_add_u32 %[LJ2], 0x10000, %[LJ2]\n"
+        "v_lshlrev_b32 %[LJ1], 1, %[LJ2]\n"
+        "v_add_u32 %[FJ1], 0x40004, %[LJ1]\n"
+        "v_add_u32 %[FJ2], 0x180018, %[LJ2]\n"
+        "v_sub_u32 %[clo], 0x7f, %[vlane2]\n"
+        "v_sub_u32 %[chi], 0x7e, %[vlane2]\n"
+        "v_mov_b32 %[vkneg], 0x80008000\n"
+        "v_mov_b32 %[v10000], 0x10000\n"
+        "v_mov_b32 %[v0c0c], 0xc000c00\n"
         "s_mov_b32 %[i0], %[i]\n"
         "s_and_b32 %[x], %[pr], 7\n"
         "s_mulk_i32 %[x], 0x300\n"
@@ -2160,15 +2177,15 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "s_cbranch_scc1 L_out%=\n"
         "s_lshl_b32 %[x], %[i], 5\n"
         "s_add_u32 %[x], %[x], %[Ldesc]\n"
-        "v_mov_b32 %[va], %[x]\n"
-        "ds_read_b32 %[vd1], %[va] offset:4\n"
-        "ds_read_b32 %[vrem], %[va] offset:8\n"
-        "ds_read_b32 %[vp0], %[va] offset:12\n"
-        "ds_read_b32 %[vp1], %[va] offset:16\n"
+        "v_mov_b32 %[Ga], %[x]\n"
+        "ds_read_b32 %[Gb], %[Ga] offset:4\n"
+        "ds_read_b32 %[Pa], %[Ga] offset:8\n"
+        "ds_read_b32 %[Pb], %[Ga] offset:12\n"
+        "ds_read_b32 %[inc], %[Ga] offset:16\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_readfirstlane_b32 %[d1], %[vd1]\n"
-        "v_readfirstlane_b32 %[p0], %[vp0]\n"
-        "v_readfirstlane_b32 %[rem], %[vrem]\n"
+        "v_readfirstlane_b32 %[d1], %[Gb]\n"
+        "v_readfirstlane_b32 %[p0], %[Pb]\n"
+        "v_readfirstlane_b32 %[rem], %[Pa]\n"
         "s_and_b32 %[y], %[d1], 0xffffc000\n"
         "s_cmp_eq_u32 %[y], 0x18000\n"
         "s_cbranch_scc0 L_two%=\n"
@@ -2177,17 +2194,17 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "s_and_b32 %[x], %[p0], 31\n"
         "s_lshl_b32 %[x], %[x], 4\n"
         "s_add_u32 %[x], %[x], %[Lrrow]\n"
-        "v_mov_b32 %[va], %[x]\n"
-        "ds_read_b32 %[vd1], %[va]\n"
-        "ds_read_b32 %[vrem], %[va] offset:4\n"
-        "ds_read_b32 %[vp0], %[va] offset:8\n"
+        "v_mov_b32 %[Ga], %[x]\n"
+        "ds_read_b32 %[Gb], %[Ga]\n"
+        "ds_read_b32 %[Pa], %[Ga] offset:4\n"
+        "ds_read_b32 %[Pb], %[Ga] offset:8\n"
         "s_and_b32 %[x], %[p0], 7\n"
         "s_mulk_i32 %[x], 0x300\n"
         "s_add_u32 %[pwb], %[x], %[Lring]\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_readfirstlane_b32 %[pb], %[vd1]\n"
-        "v_readfirstlane_b32 %[pe], %[vrem]\n"
-        "v_readfirstlane_b32 %[pa], %[vp0]\n"
+        "v_readfirstlane_b32 %[pb], %[Gb]\n"
+        "v_readfirstlane_b32 %[pe], %[Pa]\n"
+        "v_readfirstlane_b32 %[pa], %[Pb]\n"
         "s_mov_b32 %[pr], %[p0]\n"
         "L_p0ok1%=:\n"
         "s_sub_i32 %[x], %[qlen], %[rem]\n"
@@ -2213,26 +2230,26 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "s_pack_ll_b32_b16 %[pkb], %[beg], %[beg]\n"
         "s_pack_ll_b32_b16 %[pke], %[end], %[end]\n"
         "s_bfe_u32 %[x], %[cb0], 0xf0001\n"
-        "v_add_u32 %[t], %[x], %[vlane]\n"
-        "v_mad_u32_u24 %[J], %[t], %[c20002], %[v10000]\n"
-        "v_add_u32 %[va], %[Lq], %[t]\n"
-        "ds_read_u8 %[q], %[va]\n"
-        "v_and_b32 %[iw], 63, %[t]\n"
+        "v_add_u32 %[M], %[x], %[vlane]\n"
+        "v_mad_u32_u24 %[H0], %[M], %[c20002], %[v10000]\n"
+        "v_add_u32 %[Ga], %[Lq], %[M]\n"
+        "ds_read_u8 %[S], %[Ga]\n"
+        "v_and_b32 %[iw], 63, %[M]\n"
         "v_lshl_add_u32 %[a0], %[iw], 2, %[pwb]\n"
-        "ds_read_b32 %[w0], %[a0]\n"
+        "ds_read_b32 %[E1], %[a0]\n"
         "ds_read_b32 %[X1], %[a0] offset:256\n"
         "ds_read_b32 %[X2], %[a0] offset:512\n"
-        "v_pk_sub_i16 %[m1], %[J], %[pkb]\n"
-        "v_pk_sub_i16 %[m2], %[pke], %[J]\n"
+        "v_pk_sub_i16 %[m1], %[H0], %[pkb]\n"
+        "v_pk_sub_i16 %[m2], %[pke], %[H0]\n"
         "v_or_b32 %[m1], %[m1], %[m2]\n"
         "v_pk_ashrrev_i16 %[inv], 15, %[m1] op_sel_hi:[0,1]\n"
         "s_waitcnt lgkmcnt(3)\n"
-        "v_mul_u32_u24 %[sel], 0x1001, %[q]\n"
-        "v_and_or_b32 %[sel], %[sel], %[cq], %[v0c0c]\n"
-        "v_perm_b32 %[S], 4, %[tlo], %[sel]\n"
+        "v_mul_u32_u24 %[S], 0x1001, %[S]\n"
+        "v_and_or_b32 %[S], %[S], %[cq], %[v0c0c]\n"
+        "v_perm_b32 %[S], 4, %[tlo], %[S]\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_mov_b32_dpp %[w0p], %[w0] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
-        "v_alignbit_b32 %[Hd], %[w0], %[w0p], 16\n"
+        "v_mov_b32_dpp %[t1], %[E1] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
+        "v_alignbit_b32 %[Hd], %[E1], %[t1], 16\n"
         "s_cmp_le_i32 %[beg], %[pc0]\n"
         "s_cbranch_scc1 L_mask1%=\n"
         "s_add_u32 %[x], %[pc0], 0x7f\n"
@@ -2241,14 +2258,14 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "L_mask1%=:\n"
         "s_pack_ll_b32_b16 %[x], %[pb], %[pb]\n"
         "s_pack_ll_b32_b16 %[y], %[pe], %[pe]\n"
-        "v_pk_add_u16 %[m3], %[J], -1\n"
-        "v_pk_sub_i16 %[m1], %[m3], %[x]\n"
-        "v_pk_sub_i16 %[m2], %[y], %[m3]\n"
+        "v_pk_add_u16 %[t1], %[H0], -1\n"
+        "v_pk_sub_i16 %[m1], %[t1], %[x]\n"
+        "v_pk_sub_i16 %[m2], %[y], %[t1]\n"
         "v_or_b32 %[m1], %[m1], %[m2]\n"
         "v_pk_ashrrev_i16 %[m1], 15, %[m1] op_sel_hi:[0,1]\n"
-        "v_pk_sub_i16 %[m2], %[J], %[x]\n"
-        "v_pk_sub_i16 %[m3], %[y], %[J]\n"
-        "v_or_b32 %[m2], %[m2], %[m3]\n"
+        "v_pk_sub_i16 %[m2], %[H0], %[x]\n"
+        "v_pk_sub_i16 %[t1], %[y], %[H0]\n"
+        "v_or_b32 %[m2], %[m2], %[t1]\n"
         "v_pk_ashrrev_i16 %[m2], 15, %[m2] op_sel_hi:[0,1]\n"
         "v_bfi_b32 %[Hd], %[m1], %[vkneg], %[Hd]\n"
         "v_bfi_b32 %[X1], %[m2], %[vkneg], %[X1]\n"
@@ -2299,8 +2316,8 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "v_perm_b32 %[P1], %[Pb], %[Pa], %[csel0]\n"
         "v_perm_b32 %[P2], %[Pb], %[Pa], %[csel1]\n"
         "v_pk_sub_i16 %[F1], %[P1], %[FJ1] clamp\n"
-        "v_pk_sub_i16 %[F2], %[P2], %[FJ2] clamp\n"
-        "v_pk_max_i16 %[H], %[F1], %[F2]\n"
+        "v_pk_sub_i16 %[S], %[P2], %[FJ2] clamp\n"
+        "v_pk_max_i16 %[H], %[F1], %[S]\n"
         "v_pk_max_i16 %[H], %[H0], %[H]\n"
         "v_pk_add_i16 %[X1e], %[X1], -2 op_sel_hi:[1,0] clamp\n"
         "v_pk_add_i16 %[Ho1], %[H], -6 op_sel_hi:[1,0] clamp\n"
@@ -2308,25 +2325,25 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "v_pk_sub_i16 %[Ho2], %[H], 25 op_sel_hi:[1,0] clamp\n"
         "v_pk_max_i16 %[E1], %[X1e], %[Ho1]\n"
         "v_pk_max_i16 %[E2], %[X2e], %[Ho2]\n"
-        "v_pk_sub_i16 %[d0], %[M], %[H] clamp\n"
-        "v_pk_sub_i16 %[dd], %[X1], %[H] clamp\n"
-        "v_perm_b32 %[x01], %[dd], %[d0], %[cseltb]\n"
-        "v_pk_sub_i16 %[d0], %[X2], %[H] clamp\n"
-        "v_pk_sub_i16 %[dd], %[F1], %[H] clamp\n"
-        "v_perm_b32 %[x23], %[dd], %[d0], %[cseltb]\n"
-        "v_pk_sub_i16 %[d0], %[Ho1], %[X1e] clamp\n"
-        "v_pk_sub_i16 %[dd], %[Ho2], %[X2e] clamp\n"
-        "v_perm_b32 %[x45], %[dd], %[d0], %[cseltb]\n"
-        "v_pk_sub_i16 %[d0], %[G1], %[P1] clamp\n"
-        "v_pk_sub_i16 %[dd], %[G2], %[P2] clamp\n"
-        "v_perm_b32 %[x67], %[dd], %[d0], %[cseltb]\n"
-        "v_and_b32 %[x67], %[x67], %[m67]\n"
-        "v_and_or_b32 %[x67], %[x45], %[m45], %[x67]\n"
-        "v_and_or_b32 %[x67], %[x23], %[m23], %[x67]\n"
-        "v_and_or_b32 %[x67], %[x01], %[m01], %[x67]\n"
-        "v_or_b32_sdwa %[x67], %[x67], %[x67] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
+        "v_pk_sub_i16 %[Ga], %[M], %[H] clamp\n"
+        "v_pk_sub_i16 %[Gb], %[X1], %[H] clamp\n"
+        "v_perm_b32 %[Pa], %[Gb], %[Ga], %[cseltb]\n"
+        "v_pk_sub_i16 %[Ga], %[X2], %[H] clamp\n"
+        "v_pk_sub_i16 %[Gb], %[F1], %[H] clamp\n"
+        "v_perm_b32 %[Pb], %[Gb], %[Ga], %[cseltb]\n"
+        "v_pk_sub_i16 %[Ga], %[Ho1], %[X1e] clamp\n"
+        "v_pk_sub_i16 %[Gb], %[Ho2], %[X2e] clamp\n"
+        "v_perm_b32 %[inc], %[Gb], %[Ga], %[cseltb]\n"
+        "v_pk_sub_i16 %[Ga], %[G1], %[P1] clamp\n"
+        "v_pk_sub_i16 %[Gb], %[G2], %[P2] clamp\n"
+        "v_perm_b32 %[amk], %[Gb], %[Ga], %[cseltb]\n"
+        "v_and_b32 %[amk], %[m67], %[amk]\n"
+        "v_and_or_b32 %[amk], %[inc], %[m45], %[amk]\n"
+        "v_and_or_b32 %[amk], %[Pb], %[m23], %[amk]\n"
+        "v_and_or_b32 %[amk], %[Pa], %[m01], %[amk]\n"
+        "v_or_b32_sdwa %[amk], %[amk], %[amk] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
         "v_add_u32 %[voff], %[tbu], %[vlane2]\n"
-        "global_store_short %[voff], %[x67], %[tbp]\n"
+        "global_store_short %[voff], %[amk], %[tbp]\n"
         "v_bfi_b32 %[Hd], %[inv], %[vkneg], %[H]\n"
         "v_bfi_b32 %[m1], %[inv], %[vkneg], %[E1]\n"
         "v_bfi_b32 %[m2], %[inv], %[vkneg], %[E2]\n"
@@ -2422,7 +2439,7 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "L_two%=:\n"
         "s_cmp_lg_u32 %[y], 0x28000\n"
         "s_cbranch_scc1 L_out%=\n"
-        "v_readfirstlane_b32 %[p1], %[vp1]\n"
+        "v_readfirstlane_b32 %[p1], %[inc]\n"
         "s_cmp_eq_u32 %[p1], %[pr]\n"
         "s_cbranch_scc0 L_p1lds%=\n"
         "s_mov_b32 %[rb1], %[pb]\n"
@@ -2434,34 +2451,34 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "s_and_b32 %[x], %[p1], 31\n"
         "s_lshl_b32 %[x], %[x], 4\n"
         "s_add_u32 %[x], %[x], %[Lrrow]\n"
-        "v_mov_b32 %[va], %[x]\n"
-        "ds_read_b32 %[vd1], %[va]\n"
-        "ds_read_b32 %[vrem], %[va] offset:4\n"
-        "ds_read_b32 %[vp0], %[va] offset:8\n"
+        "v_mov_b32 %[Ga], %[x]\n"
+        "ds_read_b32 %[Gb], %[Ga]\n"
+        "ds_read_b32 %[Pa], %[Ga] offset:4\n"
+        "ds_read_b32 %[Pb], %[Ga] offset:8\n"
         "s_and_b32 %[x], %[p1], 7\n"
         "s_mulk_i32 %[x], 0x300\n"
         "s_add_u32 %[base1], %[x], %[Lring]\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_readfirstlane_b32 %[rb1], %[vd1]\n"
-        "v_readfirstlane_b32 %[re1], %[vrem]\n"
-        "v_readfirstlane_b32 %[ra1], %[vp0]\n"
+        "v_readfirstlane_b32 %[rb1], %[Gb]\n"
+        "v_readfirstlane_b32 %[re1], %[Pa]\n"
+        "v_readfirstlane_b32 %[ra1], %[Pb]\n"
         "L_p1ok%=:\n"
         "s_cmp_eq_u32 %[p0], %[pr]\n"
         "s_cbranch_scc1 L_p0ok2%=\n"
         "s_and_b32 %[x], %[p0], 31\n"
         "s_lshl_b32 %[x], %[x], 4\n"
         "s_add_u32 %[x], %[x], %[Lrrow]\n"
-        "v_mov_b32 %[va], %[x]\n"
-        "ds_read_b32 %[vd1], %[va]\n"
-        "ds_read_b32 %[vrem], %[va] offset:4\n"
-        "ds_read_b32 %[vp0], %[va] offset:8\n"
+        "v_mov_b32 %[Ga], %[x]\n"
+        "ds_read_b32 %[Gb], %[Ga]\n"
+        "ds_read_b32 %[Pa], %[Ga] offset:4\n"
+        "ds_read_b32 %[Pb], %[Ga] offset:8\n"
         "s_and_b32 %[x], %[p0], 7\n"
         "s_mulk_i32 %[x], 0x300\n"
         "s_add_u32 %[pwb], %[x], %[Lring]\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_readfirstlane_b32 %[pb], %[vd1]\n"
-        "v_readfirstlane_b32 %[pe], %[vrem]\n"
-        "v_readfirstlane_b32 %[pa], %[vp0]\n"
+        "v_readfirstlane_b32 %[pb], %[Gb]\n"
+        "v_readfirstlane_b32 %[pe], %[Pa]\n"
+        "v_readfirstlane_b32 %[pa], %[Pb]\n"
         "s_mov_b32 %[pr], %[p0]\n"
         "L_p0ok2%=:\n"
         "s_sub_i32 %[x], %[qlen], %[rem]\n"
@@ -2493,26 +2510,26 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "s_pack_ll_b32_b16 %[pkb], %[beg], %[beg]\n"
         "s_pack_ll_b32_b16 %[pke], %[end], %[end]\n"
         "s_bfe_u32 %[x], %[cb0], 0xf0001\n"
-        "v_add_u32 %[t], %[x], %[vlane]\n"
-        "v_mad_u32_u24 %[J], %[t], %[c20002], %[v10000]\n"
-        "v_add_u32 %[va], %[Lq], %[t]\n"
-        "ds_read_u8 %[q], %[va]\n"
-        "v_and_b32 %[iw], 63, %[t]\n"
+        "v_add_u32 %[M], %[x], %[vlane]\n"
+        "v_mad_u32_u24 %[H0], %[M], %[c20002], %[v10000]\n"
+        "v_add_u32 %[Ga], %[Lq], %[M]\n"
+        "ds_read_u8 %[S], %[Ga]\n"
+        "v_and_b32 %[iw], 63, %[M]\n"
         "v_lshl_add_u32 %[a0], %[iw], 2, %[pwb]\n"
-        "ds_read_b32 %[w0], %[a0]\n"
+        "ds_read_b32 %[E1], %[a0]\n"
         "ds_read_b32 %[X1], %[a0] offset:256\n"
         "ds_read_b32 %[X2], %[a0] offset:512\n"
-        "v_pk_sub_i16 %[m1], %[J], %[pkb]\n"
-        "v_pk_sub_i16 %[m2], %[pke], %[J]\n"
+        "v_pk_sub_i16 %[m1], %[H0], %[pkb]\n"
+        "v_pk_sub_i16 %[m2], %[pke], %[H0]\n"
         "v_or_b32 %[m1], %[m1], %[m2]\n"
         "v_pk_ashrrev_i16 %[inv], 15, %[m1] op_sel_hi:[0,1]\n"
         "s_waitcnt lgkmcnt(3)\n"
-        "v_mul_u32_u24 %[sel], 0x1001, %[q]\n"
-        "v_and_or_b32 %[sel], %[sel], %[cq], %[v0c0c]\n"
-        "v_perm_b32 %[S], 4, %[tlo], %[sel]\n"
+        "v_mul_u32_u24 %[S], 0x1001, %[S]\n"
+        "v_and_or_b32 %[S], %[S], %[cq], %[v0c0c]\n"
+        "v_perm_b32 %[S], 4, %[tlo], %[S]\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_mov_b32_dpp %[w0p], %[w0] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
-        "v_alignbit_b32 %[Hd], %[w0], %[w0p], 16\n"
+        "v_mov_b32_dpp %[t1], %[E1] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
+        "v_alignbit_b32 %[Hd], %[E1], %[t1], 16\n"
         "s_max_i32 %[x], %[pc0], %[pc1]\n"
         "s_cmp_le_i32 %[beg], %[x]\n"
         "s_cbranch_scc1 L_mask2%=\n"
@@ -2523,58 +2540,58 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "L_mask2%=:\n"
         "s_pack_ll_b32_b16 %[x], %[pb], %[pb]\n"
         "s_pack_ll_b32_b16 %[y], %[pe], %[pe]\n"
-        "v_pk_add_u16 %[m3], %[J], -1\n"
-        "v_pk_sub_i16 %[m1], %[m3], %[x]\n"
-        "v_pk_sub_i16 %[m2], %[y], %[m3]\n"
+        "v_pk_add_u16 %[t1], %[H0], -1\n"
+        "v_pk_sub_i16 %[m1], %[t1], %[x]\n"
+        "v_pk_sub_i16 %[m2], %[y], %[t1]\n"
         "v_or_b32 %[m1], %[m1], %[m2]\n"
         "v_pk_ashrrev_i16 %[m1], 15, %[m1] op_sel_hi:[0,1]\n"
-        "v_pk_sub_i16 %[m2], %[J], %[x]\n"
-        "v_pk_sub_i16 %[m3], %[y], %[J]\n"
-        "v_or_b32 %[m2], %[m2], %[m3]\n"
+        "v_pk_sub_i16 %[m2], %[H0], %[x]\n"
+        "v_pk_sub_i16 %[t1], %[y], %[H0]\n"
+        "v_or_b32 %[m2], %[m2], %[t1]\n"
         "v_pk_ashrrev_i16 %[m2], 15, %[m2] op_sel_hi:[0,1]\n"
         "v_bfi_b32 %[Hd], %[m1], %[vkneg], %[Hd]\n"
         "v_bfi_b32 %[X1], %[m2], %[vkneg], %[X1]\n"
         "v_bfi_b32 %[X2], %[m2], %[vkneg], %[X2]\n"
         "v_lshl_add_u32 %[a0], %[iw], 2, %[base1]\n"
-        "ds_read_b32 %[w0], %[a0]\n"
-        "ds_read_b32 %[X11], %[a0] offset:256\n"
-        "ds_read_b32 %[X21], %[a0] offset:512\n"
+        "ds_read_b32 %[E1], %[a0]\n"
+        "ds_read_b32 %[P1], %[a0] offset:256\n"
+        "ds_read_b32 %[P2], %[a0] offset:512\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_mov_b32_dpp %[w0p], %[w0] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
-        "v_alignbit_b32 %[Hd1], %[w0], %[w0p], 16\n"
+        "v_mov_b32_dpp %[t1], %[E1] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
+        "v_alignbit_b32 %[F1], %[E1], %[t1], 16\n"
         "s_pack_ll_b32_b16 %[x], %[rb1], %[rb1]\n"
         "s_pack_ll_b32_b16 %[y], %[re1], %[re1]\n"
-        "v_pk_add_u16 %[m3], %[J], -1\n"
-        "v_pk_sub_i16 %[m1], %[m3], %[x]\n"
-        "v_pk_sub_i16 %[m2], %[y], %[m3]\n"
+        "v_pk_add_u16 %[t1], %[H0], -1\n"
+        "v_pk_sub_i16 %[m1], %[t1], %[x]\n"
+        "v_pk_sub_i16 %[m2], %[y], %[t1]\n"
         "v_or_b32 %[m1], %[m1], %[m2]\n"
         "v_pk_ashrrev_i16 %[m1], 15, %[m1] op_sel_hi:[0,1]\n"
-        "v_pk_sub_i16 %[m2], %[J], %[x]\n"
-        "v_pk_sub_i16 %[m3], %[y], %[J]\n"
-        "v_or_b32 %[m2], %[m2], %[m3]\n"
+        "v_pk_sub_i16 %[m2], %[H0], %[x]\n"
+        "v_pk_sub_i16 %[t1], %[y], %[H0]\n"
+        "v_or_b32 %[m2], %[m2], %[t1]\n"
         "v_pk_ashrrev_i16 %[m2], 15, %[m2] op_sel_hi:[0,1]\n"
-        "v_bfi_b32 %[Hd1], %[m1], %[vkneg], %[Hd1]\n"
-        "v_bfi_b32 %[X11], %[m2], %[vkneg], %[X11]\n"
-        "v_bfi_b32 %[X21], %[m2], %[vkneg], %[X21]\n"
+        "v_bfi_b32 %[F1], %[m1], %[vkneg], %[F1]\n"
+        "v_bfi_b32 %[P1], %[m2], %[vkneg], %[P1]\n"
+        "v_bfi_b32 %[P2], %[m2], %[vkneg], %[P2]\n"
         "s_branch L_merge2%=\n"
         "L_nomask2%=:\n"
         "v_lshl_add_u32 %[a0], %[iw], 2, %[base1]\n"
-        "ds_read_b32 %[w0], %[a0]\n"
-        "ds_read_b32 %[X11], %[a0] offset:256\n"
-        "ds_read_b32 %[X21], %[a0] offset:512\n"
+        "ds_read_b32 %[E1], %[a0]\n"
+        "ds_read_b32 %[P1], %[a0] offset:256\n"
+        "ds_read_b32 %[P2], %[a0] offset:512\n"
         "s_waitcnt lgkmcnt(0)\n"
-        "v_mov_b32_dpp %[w0p], %[w0] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
-        "v_alignbit_b32 %[Hd1], %[w0], %[w0p], 16\n"
+        "v_mov_b32_dpp %[t1], %[E1] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
+        "v_alignbit_b32 %[F1], %[E1], %[t1], 16\n"
         "L_merge2%=:\n"
-        "v_pk_sub_i16 %[MK], %[Hd], %[Hd1] clamp\n"
+        "v_pk_sub_i16 %[MK], %[Hd], %[F1] clamp\n"
         "v_pk_lshrrev_b16 %[MK], 15, %[MK] op_sel_hi:[0,1]\n"
-        "v_pk_sub_i16 %[K1], %[X1], %[X11] clamp\n"
+        "v_pk_sub_i16 %[K1], %[X1], %[P1] clamp\n"
         "v_pk_lshrrev_b16 %[K1], 15, %[K1] op_sel_hi:[0,1]\n"
-        "v_pk_sub_i16 %[K2], %[X2], %[X21] clamp\n"
+        "v_pk_sub_i16 %[K2], %[X2], %[P2] clamp\n"
         "v_pk_lshrrev_b16 %[K2], 15, %[K2] op_sel_hi:[0,1]\n"
-        "v_pk_max_i16 %[Hd], %[Hd], %[Hd1]\n"
-        "v_pk_max_i16 %[X1], %[X1], %[X11]\n"
-        "v_pk_max_i16 %[X2], %[X2], %[X21]\n"
+        "v_pk_max_i16 %[Hd], %[Hd], %[F1]\n"
+        "v_pk_max_i16 %[X1], %[X1], %[P1]\n"
+        "v_pk_max_i16 %[X2], %[X2], %[P2]\n"
         "v_pk_add_i16 %[M], %[Hd], %[S] clamp\n"
         "v_pk_add_i16 %[M], %[M], -4 op_sel_hi:[1,0] clamp\n"
         "v_pk_max_i16 %[t1], %[X1], %[X2]\n"
@@ -2620,8 +2637,8 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "v_perm_b32 %[P1], %[Pb], %[Pa], %[csel0]\n"
         "v_perm_b32 %[P2], %[Pb], %[Pa], %[csel1]\n"
         "v_pk_sub_i16 %[F1], %[P1], %[FJ1] clamp\n"
-        "v_pk_sub_i16 %[F2], %[P2], %[FJ2] clamp\n"
-        "v_pk_max_i16 %[H], %[F1], %[F2]\n"
+        "v_pk_sub_i16 %[S], %[P2], %[FJ2] clamp\n"
+        "v_pk_max_i16 %[H], %[F1], %[S]\n"
         "v_pk_max_i16 %[H], %[H0], %[H]\n"
         "v_pk_add_i16 %[X1e], %[X1], -2 op_sel_hi:[1,0] clamp\n"
         "v_pk_add_i16 %[Ho1], %[H], -6 op_sel_hi:[1,0] clamp\n"
@@ -2629,25 +2646,25 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
         "v_pk_sub_i16 %[Ho2], %[H], 25 op_sel_hi:[1,0] clamp\n"
         "v_pk_max_i16 %[E1], %[X1e], %[Ho1]\n"
         "v_pk_max_i16 %[E2], %[X2e], %[Ho2]\n"
-        "v_pk_sub_i16 %[d0], %[M], %[H] clamp\n"
-        "v_pk_sub_i16 %[dd], %[X1], %[H] clamp\n"
-        "v_perm_b32 %[x01], %[dd], %[d0], %[cseltb]\n"
-        "v_pk_sub_i16 %[d0], %[X2], %[H] clamp\n"
-        "v_pk_sub_i16 %[dd], %[F1], %[H] clamp\n"
-        "v_perm_b32 %[x23], %[dd], %[d0], %[cseltb]\n"
-        "v_pk_sub_i16 %[d0], %[Ho1], %[X1e] clamp\n"
-        "v_pk_sub_i16 %[dd], %[Ho2], %[X2e] clamp\n"
-        "v_perm_b32 %[x45], %[dd], %[d0], %[cseltb]\n"
-        "v_pk_sub_i16 %[d0], %[G1], %[P1] clamp\n"
-        "v_pk_sub_i16 %[dd], %[G2], %[P2] clamp\n"
-        "v_perm_b32 %[x67], %[dd], %[d0], %[cseltb]\n"
-        "v_and_b32 %[x67], %[x67], %[m67]\n"
-        "v_and_or_b32 %[x67], %[x45], %[m45], %[x67]\n"
-        "v_and_or_b32 %[x67], %[x23], %[m23], %[x67]\n"
-        "v_and_or_b32 %[x67], %[x01], %[m01], %[x67]\n"
-        "v_or_b32_sdwa %[x67], %[x67], %[x67] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
+        "v_pk_sub_i16 %[Ga], %[M], %[H] clamp\n"
+        "v_pk_sub_i16 %[Gb], %[X1], %[H] clamp\n"
+        "v_perm_b32 %[Pa], %[Gb], %[Ga], %[cseltb]\n"
+        "v_pk_sub_i16 %[Ga], %[X2], %[H] clamp\n"
+        "v_pk_sub_i16 %[Gb], %[F1], %[H] clamp\n"
+        "v_perm_b32 %[Pb], %[Gb], %[Ga], %[cseltb]\n"
+        "v_pk_sub_i16 %[Ga], %[Ho1], %[X1e] clamp\n"
+        "v_pk_sub_i16 %[Gb], %[Ho2], %[X2e] clamp\n"
+        "v_perm_b32 %[inc], %[Gb], %[Ga], %[cseltb]\n"
+        "v_pk_sub_i16 %[Ga], %[G1], %[P1] clamp\n"
+        "v_pk_sub_i16 %[Gb], %[G2], %[P2] clamp\n"
+        "v_perm_b32 %[amk], %[Gb], %[Ga], %[cseltb]\n"
+        "v_and_b32 %[amk], %[m67], %[amk]\n"
+        "v_and_or_b32 %[amk], %[inc], %[m45], %[amk]\n"
+        "v_and_or_b32 %[amk], %[Pb], %[m23], %[amk]\n"
+        "v_and_or_b32 %[amk], %[Pa], %[m01], %[amk]\n"
+        "v_or_b32_sdwa %[amk], %[amk], %[amk] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
         "v_add_u32 %[voff], %[tbu], %[vlane2]\n"
-        "global_store_short %[voff], %[x67], %[tbp]\n"
+        "global_store_short %[voff], %[amk], %[tbp]\n"
         "v_lshlrev_b32 %[K1], 2, %[K1]\n"
         "v_lshlrev_b32 %[K2], 4, %[K2]\n"
         "v_or3_b32 %[MK], %[MK], %[K1], %[K2]\n"
@@ -2759,23 +2776,19 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
           [cb0] "=&s"(cb0), [spm] "=&s"(spm), [pc0] "=&s"(pc0), [pc1] "=&s"(pc1), [tlo] "=&s"(tlo), [pkb] "=&s"(pkb),
           [pke] "=&s"(pke), [base1] "=&s"(base1), [mp] "=&s"(mp), [besti] "=&s"(besti), [r] "=&s"(r),
           [pwb] "=&s"(pwb), [i0] "=&s"(i0), [c20002] "=&s"(c20002), [c128] "=&s"(c128), [cr16] "=&s"(cr16),
-          [cq] "=&s"(cq), [cth] "=&s"(cth),
-          [va] "=&v"(va), [vd1] "=&v"(vd1), [vrem] "=&v"(vrem), [vp0] "=&v"(vp0), [vp1] "=&v"(vp1), [t] "=&v"(t),
-          [J] "=&v"(J), [q] "=&v"(q), [iw] "=&v"(iw), [a0] "=&v"(a0),
-          [w0] "=&v"(w0), [w0p] "=&v"(w0p), [inv] "=&v"(inv), [m1] "=&v"(m1), [m2] "=&v"(m2), [m3] "=&v"(m3),
-          [sel] "=&v"(sel), [S] "=&v"(S), [Hd] "=&v"(Hd), [X1] "=&v"(X1), [X2] "=&v"(X2), [Hd1] "=&v"(Hd1),
-          [X11] "=&v"(X11), [X21] "=&v"(X21), [MK] "=&v"(MK), [K1] "=&v"(K1), [K2] "=&v"(K2), [M] "=&v"(M),
-          [H0] "=&v"(H0), [G1] "=&v"(G1), [G2] "=&v"(G2), [Ga] "=&v"(Ga), [Gb] "=&v"(Gb), [inc] "=&v"(inc),
-          [amk] "=&v"(amk), [t1] "=&v"(t1), [Pa] "=&v"(Pa), [Pb] "=&v"(Pb), [P1] "=&v"(P1), [P2] "=&v"(P2),
-          [F1] "=&v"(F1), [F2] "=&v"(F2), [H] "=&v"(H), [X1e] "=&v"(X1e), [Ho1] "=&v"(Ho1), [X2e] "=&v"(X2e),
-          [Ho2] "=&v"(Ho2), [E1] "=&v"(E1), [E2] "=&v"(E2), [d0] "=&v"(d0), [dd] "=&v"(dd), [x01] "=&v"(x01),
-          [x23] "=&v"(x23), [x45] "=&v"(x45), [x67] "=&v"(x67), [voff] "=&v"(voff)
+          [cq] "=&s"(cq), [cth] "=&s"(cth), [csel0] "=&s"(csel0), [csel1] "=&s"(csel1), [cseltb] "=&s"(cseltb),
+          [cselkp] "=&s"(cselkp), [m01] "=&s"(m01), [m23] "=&s"(m23), [m45] "=&s"(m45), [m67] "=&s"(m67),
+          [Ga] "=&v"(Ga), [Gb] "=&v"(Gb), [Pa] "=&v"(Pa), [Pb] "=&v"(Pb), [inc] "=&v"(inc), [S] "=&v"(S),
+          [M] "=&v"(M), [H0] "=&v"(H0), [E1] "=&v"(E1), [t1] "=&v"(t1), [F1] "=&v"(F1), [P1] "=&v"(P1),
+          [P2] "=&v"(P2), [iw] "=&v"(iw), [a0] "=&v"(a0), [inv] "=&v"(inv), [m1] "=&v"(m1), [m2] "=&v"(m2),
+          [Hd] "=&v"(Hd), [X1] "=&v"(X1), [X2] "=&v"(X2), [MK] "=&v"(MK), [K1] "=&v"(K1), [K2] "=&v"(K2),
+          [G1] "=&v"(G1), [G2] "=&v"(G2), [amk] "=&v"(amk), [H] "=&v"(H), [X1e] "=&v"(X1e), [Ho1] "=&v"(Ho1),
+          [X2e] "=&v"(X2e), [Ho2] "=&v"(Ho2), [E2] "=&v"(E2), [voff] "=&v"(voff), [vlane] "=&v"(vlane),
+          [vlane2] "=&v"(vlane2), [vlane8] "=&v"(vlane8), [LJ1] "=&v"(LJ1), [LJ2] "=&v"(LJ2), [FJ1] "=&v"(FJ1),
+          [FJ2] "=&v"(FJ2), [clo] "=&v"(clo), [chi] "=&v"(chi), [vkneg] "=&v"(vkneg), [v10000] "=&v"(v10000),
+          [v0c0c] "=&v"(v0c0c)
         : [iend] "s"(iend), [b0] "s"(b0), [qlen] "s"(qlen), [w] "s"(w), [Ldesc] "s"(Ldesc), [Lrrow] "s"(Lrrow),
-          [Lring] "s"(Lring), [Lq] "s"(Lq), [tbp] "s"(tbp), [kpp] "s"(kpp), [svp] "s"(svp), [rip] "s"(rip),
-          [vlane] "v"(vlane), [vlane2] "v"(vlane2), [vlane8] "v"(vlane8), [LJ1] "v"(LJ1), [LJ2] "v"(LJ2),
-          [FJ1] "v"(FJ1), [FJ2] "v"(FJ2), [clo] "v"(clo), [chi] "v"(chi), [vkneg] "v"(vkneg), [v10000] "v"(v10000),
-          [csel0] "v"(csel0), [csel1] "v"(csel1), [cseltb] "v"(cseltb), [cselkp] "v"(cselkp), [m01] "v"(m01),
-          [m23] "v"(m23), [m45] "v"(m45), [m67] "v"(m67), [v0c0c] "v"(v0c0c)
+          [Lring] "s"(Lring), [Lq] "s"(Lq), [tbp] "s"(tbp), [kpp] "s"(kpp), [svp] "s"(svp), [rip] "s"(rip)
         : "memory", "scc", "v120", "v121", "v122", "v123", "v124", "v125");
     prv_r = pr;
     prv_beg = pb;

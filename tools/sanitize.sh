@@ -16,8 +16,8 @@ tar -C "$ROOT" --exclude=./.git --exclude=./gpurun_out --exclude=./build --exclu
 LLVM=/opt/rocm/lib/llvm/bin
 make -s -j8 -C "$W/mandalorion_amd/csrc" SAN=$MODE
 make -s -C "$W/oracle" CC=$LLVM/clang CXX=$LLVM/clang++ SAN=$MODE
-RT=$($LLVM/clang -print-file-name=libclang_rt.${MODE/address/asan}-x86_64.so)
-RT=${RT/thread-x86_64/tsan-x86_64}
+case $MODE in address) RTN=asan ;; thread) RTN=tsan ;; *) echo "mode: address or thread"; exit 1 ;; esac
+RT=$($LLVM/clang -print-file-name=libclang_rt.$RTN-x86_64.so)
 [ -f "$RT" ] || { echo "no sanitizer runtime $RT"; exit 1; }
 cd "$W"
 export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=1:symbolize=1
