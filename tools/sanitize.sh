@@ -21,5 +21,5 @@ RT=$($LLVM/clang -print-file-name=libclang_rt.$RTN-x86_64.so)
 [ -f "$RT" ] || { echo "no sanitizer runtime $RT"; exit 1; }
 cd "$W"
 export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=1:symbolize=1
-export TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0:second_deadlock_stack=1
+export TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0:second_deadlock_stack=1:suppressions=$ROOT/tools/tsan.supp
 LD_PRELOAD="$RT${LD_PRELOAD:+:$LD_PRELOAD}" python -m pytest tests -m "not gpu" -x -q -p no:cacheprovider "$@"
