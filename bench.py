@@ -310,20 +310,62 @@ def shard_plan(data: str, world: int) -> list:
     return [{"rank": k, "loci": int(cnt[k]), "cost_share": float(load[k] / max(load.sum(), 1e-9))} for k in range(world)]
 
 
+def _prefix_sha(path: str, nbytes: int) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as fh:
+        left = nbytes
+        while left > 0:
+            blk = fh.read(min(left, 1 << 24))
+            if not blk:
+                break
+            h.update(blk)
+            left -= len(blk)
+    return h.hexdigest()
+
+
+def _headers_sha(path: str, limit: int = -1) -> str:
+    """sha256 over the FASTA's first `limit` header lines (all: -1), newlines included."""
+    h, n = hashlib.sha256(), 0
+    with open(path, "rb") as fh:
+        for line in fh:
+            if line.startswith(b">"):
+                if n == limit:
+                    break
+                h.update(line)
+                n += 1
+    return h.hexdigest()
+
+
 def fullsize_check(data: str, key: str):
-    """Both output files of the last step against the oracle's full-size hashes (None: no entry)."""
+    """Both output files of the last step against the oracle's full-size hashes, and the clustering half
+    (reads2isoforms.txt, the isoform header list) against the unmodified reference's own run on the same
+    data (tests/golden/make_reference_fullsize.py: all loci, or a sorted-root prefix of them).  Returns
+    (oracle ok, reference scope) or (None, None) without an entry; a mismatch fails the run."""
     if not os.path.exists(FULLSIZE_HASHES):
-        return None
+        return None, None
     ref = json.load(open(FULLSIZE_HASHES)).get(key)
     if ref is None:
-        return None
-    got = {"isoform_consensi_sha256": sha(os.path.join(data, "Isoform_Consensi.fasta")),
-           "reads2isoforms_sha256": sha(os.path.join(data, "reads2isoforms.txt"))}
+        return None, None
+    fa, r2 = os.path.join(data, "Isoform_Consensi.fasta"), os.path.join(data, "reads2isoforms.txt")
+    got = {"isoform_consensi_sha256": sha(fa), "reads2isoforms_sha256": sha(r2)}
     ok = all(got[k] == ref[k] for k in got)
     if not ok:
         raise SystemExit(f"GPU D-module output of {key} differs from the oracle's full-size hashes: {got} vs "
                          f"{ {k: ref[k] for k in got} }")
-    return True
+    scope = None
+    if "reference_reads2isoforms_sha256" in ref:
+        hs = _headers_sha(fa)
+        if got["reads2isoforms_sha256"] != ref["reference_reads2isoforms_sha256"] or hs != ref["reference_headers_sha256"]:
+            raise SystemExit(f"GPU clustering of {key} differs from the reference's own run (reads2isoforms / headers)")
+        scope = f"all {ref['loci']} loci"
+    elif "reference_prefix" in ref:
+        px = ref["reference_prefix"]
+        if (_prefix_sha(r2, px["reads2isoforms_bytes"]) != px["reads2isoforms_sha256"]
+                or _headers_sha(fa, px["isoforms"]) != px["headers_sha256"]):
+            raise SystemExit(f"GPU clustering of {key} differs from the reference's own run on its first "
+                             f"{px['loci']} loci (reads2isoforms prefix / headers)")
+        scope = f"first {px['loci']} of {ref['loci']} loci (sorted roots)"
+    return True, scope
 
 
 def main():
@@ -411,7 +453,8 @@ def main():
     st = stats[-1]
 
     # the whole output of the last timed step against the oracle's full-size hashes (rank 0 wrote it)
-    full_parity = fullsize_check(data, f"{args.workload}:{n_loci}") if rank == 0 and SHARE is None else None
+    full_parity, ref_scope = (fullsize_check(data, f"{args.workload}:{n_loci}") if rank == 0 and SHARE is None
+                              else (None, None))
     if SHARE is not None:  # one rank's load: its own records
         records = stats[-1]["records"]
 
@@ -499,6 +542,8 @@ def main():
             },
             "gpu_equals_cpu_on_sample": parity,
             "full_output_equals_oracle": full_parity,
+            # reads2isoforms.txt and the isoform headers (clustering only) against the unmodified reference
+            "clustering_equals_reference": ref_scope,
             # per timed step (rank 0): the D module's own wall time and its POA kernels' event time, so a
             # slow step shows where it lost its time
             "steps_s": [round(x["t_total"], 4) for x in stats],

@@ -18,7 +18,14 @@ The data are regenerated from the workload's parameters (libmando_synth is a pur
 the hashes refer to the same bytes bench.py generates on the GPU box.  Nothing from the reference is
 copied into the repository: it is run, and only hashes are kept.
 
-Usage: python tests/golden/make_reference_fullsize.py config3 [config4] [--procs 8] [--data-dir /tmp]
+With --prefix-loci N the reference runs on the first N loci of the workload (sorted roots, the
+reference's own order, defineIsoforms.py:126) -- config 4's 200,000 loci take ~12 h of the reference's
+Python on this container's cores, its first 20,000 about 1 h.  Isoforms are numbered in sorted-root
+order from 1, so the reference's files over that prefix are byte prefixes of the full run's files: the
+entry's `reference_prefix` holds their sizes and sha256 (reads2isoforms.txt bytes, header list).
+
+Usage: python tests/golden/make_reference_fullsize.py config3 [config4 --prefix-loci 20000] [--procs 8]
+       [--data-dir /tmp]
 """
 from __future__ import annotations
 
@@ -107,6 +114,7 @@ def main():
     ap.add_argument("workloads", nargs="+")
     ap.add_argument("--procs", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--data-dir", default="/tmp")
+    ap.add_argument("--prefix-loci", type=int, default=0)
     a = ap.parse_args()
     with tempfile.TemporaryDirectory(dir="/tmp") as tools:
         os.makedirs(os.path.join(tools, "stub", "mappy"))
@@ -118,21 +126,32 @@ def main():
             d = os.path.join(a.data_dir, f"mando_bench_{name}_{wl['loci']}")
             os.makedirs(d, exist_ok=True)
             records = bench.gen_data(d, wl, wl["loci"], a.procs)
-            wall = run_reference(d, tools, a.procs)
-            r2i = sha_file(os.path.join(d, "reads2isoforms.txt"))
-            hsha, n_iso = headers_sha(os.path.join(d, "Isoform_Consensi.fasta"))
+            run_dir = d
+            if a.prefix_loci:
+                run_dir = os.path.join(a.data_dir, f"mando_refprefix_{name}_{a.prefix_loci}")
+                sub_records = bench.sample_dir(d, run_dir, a.prefix_loci)
+            wall = run_reference(run_dir, tools, a.procs)
+            r2_path = os.path.join(run_dir, "reads2isoforms.txt")
+            r2i = sha_file(r2_path)
+            hsha, n_iso = headers_sha(os.path.join(run_dir, "Isoform_Consensi.fasta"))
             out = json.load(open(DST))
             ent = out.setdefault(key, {})
             if ent.get("records", records) != records:
                 raise SystemExit(f"{key}: {records} records generated, the entry says {ent['records']}")
-            ent.update(reference_reads2isoforms_sha256=r2i, reference_headers_sha256=hsha,
-                       reference_isoforms=n_iso,
-                       reference_generated_by=f"unmodified /root/reference defineIsoforms.py (seeded parent, "
-                                              f"forward-only mappy stand-in, abpoa=/bin/true) on {a.procs} "
-                                              f"processes, {wall:.0f} s; tests/golden/make_reference_fullsize.py")
+            how = (f"unmodified /root/reference defineIsoforms.py (seeded parent, forward-only mappy stand-in, "
+                   f"abpoa=/bin/true) on {a.procs} processes, {wall:.0f} s; tests/golden/make_reference_fullsize.py")
+            if a.prefix_loci:
+                ent["reference_prefix"] = {"loci": a.prefix_loci, "records": sub_records, "isoforms": n_iso,
+                                           "reads2isoforms_bytes": os.path.getsize(r2_path),
+                                           "reads2isoforms_sha256": r2i, "headers_sha256": hsha,
+                                           "generated_by": how}
+            else:
+                ent.update(reference_reads2isoforms_sha256=r2i, reference_headers_sha256=hsha,
+                           reference_isoforms=n_iso, reference_generated_by=how)
             json.dump(out, open(DST, "w"), indent=1, sort_keys=True)
             print(name, records, "records;", n_iso, "isoforms; reads2isoforms", r2i,
-                  "(oracle:", ent.get("reads2isoforms_sha256"), ")", f"{wall:.0f} s", flush=True)
+                  "(oracle:", ent.get("reads2isoforms_sha256"), ")", f"{wall:.0f} s",
+                  "prefix" if a.prefix_loci else "", flush=True)
 
 
 if __name__ == "__main__":

@@ -118,3 +118,19 @@ def test_define_gpu_hbm_plan_after_a_larger_call(gpu_ctx, tmp_path):
     free0, total = _lib.device_memory(0)
     assert 0 < free0 <= total
     assert pctx.memory()[1] <= st1["hbm"]["poa_budget"]
+
+
+@pytest.mark.gpu
+def test_gpu_config3_clustering_equals_reference_run(gpu_ctx, tmp_path):
+    """BASELINE configs[2] at full size (20,000 loci, 1M records): the GPU run's reads2isoforms.txt and
+    isoform header list equal the UNMODIFIED reference's own run on the same data
+    (tests/golden/make_reference_fullsize.py: defineIsoforms.py under a seeded parent, 70 min of its Python
+    here), and both files equal the oracle's full-size hashes (bench.fullsize_check)."""
+    import bench
+
+    wl = bench.WORKLOADS["config3"]
+    d = str(tmp_path / "c3")
+    bench.gen_data(d, wl, wl["loci"], 16)
+    define.define_isoforms(d, threads=16, device=0)
+    ok, scope = bench.fullsize_check(d, f"config3:{wl['loci']}")
+    assert ok and scope == f"all {wl['loci']} loci"
