@@ -252,6 +252,18 @@ int mando_gather_bytes(mando_comm *comm, const uint8_t *send, int64_t n, uint8_t
 int mando_allreduce_max_f64(mando_comm *comm, double *v);
 int mando_comm_barrier(mando_comm *comm);
 void mando_comm_destroy(mando_comm *comm);
+/* The RCCL paths' argument marshalling, exposed so a CPU run can replay it (no device needed).
+ * All-gather: RCCL has no allgatherv, so every rank sends *maxc bytes (the largest count, >= 1) to one
+ * ncclAllGather; rank r's bytes land at dev_off[r] = r * maxc of the padded receive buffer and are
+ * compacted to host_off[r] (the prefix sum of recv_counts).
+ * Gather to rank 0: on rank 0, peer p's bytes are received at peer_off[p] (their offset in the
+ * concatenation), peer_len[p] = recv_counts[p] for p > 0, and the device range [d2h_off, d2h_off +
+ * d2h_len) is copied back (rank 0's own bytes stay on the host); on rank r > 0, peer_len[0] =
+ * recv_counts[r] (its send to rank 0) and every other entry is 0. */
+int mando_rccl_allgather_plan(int nranks, const int64_t *recv_counts, int64_t *maxc, int64_t *dev_off,
+                              int64_t *host_off);
+int mando_rccl_gather_plan(int nranks, int rank, const int64_t *recv_counts, int64_t *peer_off, int64_t *peer_len,
+                           int64_t *d2h_off, int64_t *d2h_len);
 
 /* Host helper of the D driver (FASTA / read-group assembly without per-read interpreter work):
  * segment i = src[sel[i]] + starts[i], lens[i] bytes (sel may be NULL: src[0]), reverse-complemented

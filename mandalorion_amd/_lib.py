@@ -50,6 +50,8 @@ EXPORTED = (
     "mando_allreduce_max_f64",
     "mando_comm_barrier",
     "mando_comm_destroy",
+    "mando_rccl_allgather_plan",
+    "mando_rccl_gather_plan",
     "mando_pack_segments",
     "mando_format_outputs",
     "mando_write_blocks",
@@ -238,6 +240,8 @@ def load(path: str | None = None):
         lib.mando_comm_barrier.argtypes = [_P]
         lib.mando_comm_destroy.argtypes = [_P]
         lib.mando_comm_destroy.restype = None
+        lib.mando_rccl_allgather_plan.argtypes = [ctypes.c_int, _P, _P, _P, _P]
+        lib.mando_rccl_gather_plan.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P]
         if hasattr(lib, "mando_selftest"):
             lib.mando_selftest.argtypes = [_P, _P]
         if path is None:

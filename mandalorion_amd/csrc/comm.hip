@@ -294,6 +294,43 @@ int mando_allgather_counts(mando_comm *c, int64_t n, int64_t *counts) {
     return MANDO_OK;
 }
 
+// The RCCL paths' marshalling, kept apart from the transfers so that the CPU suite can replay it
+// against the host transport (tests/test_comm.py) without a device.
+int mando_rccl_allgather_plan(int nranks, const int64_t *recv_counts, int64_t *maxc, int64_t *dev_off,
+                              int64_t *host_off) {
+    if (nranks < 1 || !recv_counts || !maxc || !dev_off || !host_off)
+        return mando::set_error(MANDO_E_ARG, "mando_rccl_allgather_plan: bad argument");
+    int64_t m = 1, o = 0;
+    for (int r = 0; r < nranks; ++r) {
+        if (recv_counts[r] < 0) return mando::set_error(MANDO_E_ARG, "mando_rccl_allgather_plan: negative count");
+        m = std::max(m, recv_counts[r]);
+    }
+    for (int r = 0; r < nranks; ++r) {
+        dev_off[r] = (int64_t)r * m;  // ncclAllGather places rank r's padded slice at r * maxc
+        host_off[r] = o;
+        o += recv_counts[r];
+    }
+    *maxc = m;
+    return MANDO_OK;
+}
+
+int mando_rccl_gather_plan(int nranks, int rank, const int64_t *recv_counts, int64_t *peer_off, int64_t *peer_len,
+                           int64_t *d2h_off, int64_t *d2h_len) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || !recv_counts || !peer_off || !peer_len || !d2h_off || !d2h_len)
+        return mando::set_error(MANDO_E_ARG, "mando_rccl_gather_plan: bad argument");
+    int64_t o = 0;
+    for (int r = 0; r < nranks; ++r) {
+        if (recv_counts[r] < 0) return mando::set_error(MANDO_E_ARG, "mando_rccl_gather_plan: negative count");
+        // rank 0 receives peer p's bytes at their offset in the concatenation; a peer sends its own to 0
+        peer_off[r] = rank == 0 && r > 0 ? o : 0;
+        peer_len[r] = rank == 0 ? (r > 0 ? recv_counts[r] : 0) : (r == 0 ? recv_counts[rank] : 0);
+        o += recv_counts[r];
+    }
+    *d2h_off = rank == 0 ? recv_counts[0] : 0;
+    *d2h_len = rank == 0 ? o - recv_counts[0] : 0;
+    return MANDO_OK;
+}
+
 int mando_allgather_bytes(mando_comm *c, const uint8_t *send, int64_t n, uint8_t *recv, const int64_t *recv_counts) {
     if (!c || !recv_counts || n < 0 || (n > 0 && !send)) return mando::set_error(MANDO_E_ARG, "mando_allgather_bytes: bad argument");
     const int R = c->nranks;
@@ -323,9 +360,10 @@ int mando_allgather_bytes(mando_comm *c, const uint8_t *send, int64_t n, uint8_t
     // RCCL has no allgatherv: one ncclAllGather of every rank's bytes padded to the largest count
     // (SURVEY.md §8(e)), then each rank's slice is compacted on the way back to the host
     if (hipSetDevice(c->device) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: hipSetDevice failed");
-    int64_t maxc = 1;
-    for (int r = 0; r < R; ++r) maxc = std::max(maxc, recv_counts[r]);
-    int rc = ensure_dev(&c->dsend, &c->dsend_cap, (size_t)maxc);
+    int64_t maxc = 0;
+    std::vector<int64_t> dev_off((size_t)R), host_off((size_t)R);
+    int rc = mando_rccl_allgather_plan(R, recv_counts, &maxc, dev_off.data(), host_off.data());
+    if (!rc) rc = ensure_dev(&c->dsend, &c->dsend_cap, (size_t)maxc);
     if (!rc) rc = ensure_dev(&c->drecv, &c->drecv_cap, (size_t)maxc * (size_t)R);
     if (rc) return rc;
     if (n > 0 && hipMemcpyAsync(c->dsend, send, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
@@ -334,7 +372,7 @@ int mando_allgather_bytes(mando_comm *c, const uint8_t *send, int64_t n, uint8_t
     if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
     for (int root = 0; root < R; ++root) {
         if (recv_counts[root] == 0) continue;
-        if (hipMemcpyAsync(recv + off[(size_t)root], static_cast<uint8_t *>(c->drecv) + (size_t)root * (size_t)maxc,
+        if (hipMemcpyAsync(recv + host_off[(size_t)root], static_cast<uint8_t *>(c->drecv) + dev_off[(size_t)root],
                            (size_t)recv_counts[root], hipMemcpyDeviceToHost, c->stream) != hipSuccess)
             return mando::set_error(MANDO_E_HIP, "comm: D2H copy failed");
     }
@@ -371,20 +409,21 @@ int mando_gather_bytes(mando_comm *c, const uint8_t *send, int64_t n, uint8_t *r
     // RCCL: point-to-point sends to rank 0 in one group (rank 0 receives each rank's bytes at its
     // offset); no rank but 0 holds more than its own bytes, unlike the padded all-gather
     if (hipSetDevice(c->device) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: hipSetDevice failed");
-    int rc = ensure_dev(&c->dsend, &c->dsend_cap, (size_t)std::max<int64_t>(n, 1));
+    std::vector<int64_t> peer_off((size_t)R), peer_len((size_t)R);
+    int64_t d2h_off = 0, d2h_len = 0;
+    int rc = mando_rccl_gather_plan(R, c->rank, recv_counts, peer_off.data(), peer_len.data(), &d2h_off, &d2h_len);
+    if (!rc) rc = ensure_dev(&c->dsend, &c->dsend_cap, (size_t)std::max<int64_t>(n, 1));
     if (!rc && root) rc = ensure_dev(&c->drecv, &c->drecv_cap, (size_t)std::max<int64_t>(tot, 1));
     if (rc) return rc;
     if (n > 0 && hipMemcpyAsync(c->dsend, send, (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return mando::set_error(MANDO_E_HIP, "comm: H2D copy failed");
     ncclResult_t r = ncclGroupStart();
     if (r == ncclSuccess) {
-        if (root) {
-            for (int p = 1; p < R && r == ncclSuccess; ++p)
-                if (recv_counts[p] > 0)
-                    r = ncclRecv(static_cast<uint8_t *>(c->drecv) + off[(size_t)p], (size_t)recv_counts[p], ncclUint8, p,
-                                 c->nccl, c->stream);
-        } else if (n > 0) {
-            r = ncclSend(c->dsend, (size_t)n, ncclUint8, 0, c->nccl, c->stream);
+        for (int p = 0; p < R && r == ncclSuccess; ++p) {
+            if (peer_len[(size_t)p] == 0) continue;
+            r = root ? ncclRecv(static_cast<uint8_t *>(c->drecv) + peer_off[(size_t)p], (size_t)peer_len[(size_t)p],
+                                ncclUint8, p, c->nccl, c->stream)
+                     : ncclSend(c->dsend, (size_t)peer_len[(size_t)p], ncclUint8, p, c->nccl, c->stream);
         }
         const ncclResult_t e = ncclGroupEnd();
         if (r == ncclSuccess) r = e;
@@ -392,8 +431,8 @@ int mando_gather_bytes(mando_comm *c, const uint8_t *send, int64_t n, uint8_t *r
     if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv gather");
     if (root) {
         if (n > 0) memcpy(recv, send, (size_t)n);  // rank 0's own bytes never leave the host
-        if (tot > n && hipMemcpyAsync(recv + n, static_cast<uint8_t *>(c->drecv) + n, (size_t)(tot - n),
-                                      hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        if (d2h_len > 0 && hipMemcpyAsync(recv + d2h_off, static_cast<uint8_t *>(c->drecv) + d2h_off, (size_t)d2h_len,
+                                          hipMemcpyDeviceToHost, c->stream) != hipSuccess)
             return mando::set_error(MANDO_E_HIP, "comm: D2H copy failed");
     }
     if (hipStreamSynchronize(c->stream) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: stream sync failed");
