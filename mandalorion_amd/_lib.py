@@ -240,8 +240,9 @@ def load(path: str | None = None):
         lib.mando_comm_barrier.argtypes = [_P]
         lib.mando_comm_destroy.argtypes = [_P]
         lib.mando_comm_destroy.restype = None
-        lib.mando_rccl_allgather_plan.argtypes = [ctypes.c_int, _P, _P, _P, _P]
-        lib.mando_rccl_gather_plan.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P]
+        if hasattr(lib, "mando_rccl_gather_plan"):  # (dev A/B builds of older trees lack them)
+            lib.mando_rccl_allgather_plan.argtypes = [ctypes.c_int, _P, _P, _P, _P]
+            lib.mando_rccl_gather_plan.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P]
         if hasattr(lib, "mando_selftest"):
             lib.mando_selftest.argtypes = [_P, _P]
         if path is None:

@@ -18,7 +18,10 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <cerrno>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <sys/mman.h>
 #include <thread>
@@ -265,8 +268,8 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     const bool timing = getenv("MANDO_CL_TIME") != nullptr;
     const auto t_0 = std::chrono::steady_clock::now();
     auto secs = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_0).count(); };
-    int nth = prm->threads > 0 ? prm->threads : mando::usable_threads();
-    nth = (int)std::min<int64_t>(nth, std::max<int64_t>(1, n_loci));
+    const int nth_all = prm->threads > 0 ? prm->threads : mando::usable_threads();
+    int nth = (int)std::min<int64_t>(nth_all, std::max<int64_t>(1, n_loci));
     // read every locus file into one buffer: sizes first (stat, on the reader threads), then reads
     vector<int64_t> fsize((size_t)n_loci, 0), foff((size_t)n_loci + 1, 0);
     vector<int32_t> fstatus((size_t)n_loci, cl::kOk);
@@ -299,26 +302,50 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     res->ctx = ctx;
     res->d_text = d_text;
     res->d_cap = d_cap;
+    // Files are read in pieces of at most kReadPiece bytes, pieces dealt to the reader threads in file
+    // order: a few large loci (config 2: seven ~22 MB files) keep every reader busy instead of one
+    // thread per file.  The thread that finishes a locus's last piece marks it done.
+    constexpr int64_t kReadPiece = int64_t(4) << 20;
+    vector<int64_t> pfirst((size_t)n_loci + 1, 0);
+    for (int64_t i = 0; i < n_loci; ++i)
+        pfirst[(size_t)i + 1] = pfirst[(size_t)i] + std::max<int64_t>(1, (fsize[(size_t)i] + kReadPiece - 1) / kReadPiece);
+    const int64_t n_pieces = pfirst[(size_t)n_loci];
+    nth = (int)std::min<int64_t>(nth_all, std::max<int64_t>(1, n_pieces));
     std::atomic<int64_t> next{0};
-    vector<std::atomic<uint8_t>> done((size_t)n_loci);
-    for (auto &d : done) d.store(0);
+    vector<std::atomic<uint8_t>> done((size_t)n_loci), ioerr((size_t)n_loci);
+    vector<std::atomic<int32_t>> left((size_t)n_loci);
+    for (int64_t i = 0; i < n_loci; ++i) {
+        done[(size_t)i].store(0);
+        ioerr[(size_t)i].store(0);
+        left[(size_t)i].store((int32_t)(pfirst[(size_t)i + 1] - pfirst[(size_t)i]));
+    }
     std::mutex mu;
     std::condition_variable cv;
     auto reader = [&]() {
         while (true) {
-            const int64_t i = next.fetch_add(1);
-            if (i >= n_loci) break;
-            if (fsize[(size_t)i] < 0) {
-                fstatus[(size_t)i] = cl::kIO;
-            } else if (FILE *fh = fopen(psl_paths[i], "rb")) {
-                const size_t got = fread(res->text_p + foff[(size_t)i], 1, (size_t)fsize[(size_t)i], fh);
-                fclose(fh);
-                if ((int64_t)got != fsize[(size_t)i]) fstatus[(size_t)i] = cl::kIO;
-            } else {
-                fstatus[(size_t)i] = cl::kIO;
+            const int64_t p = next.fetch_add(1);
+            if (p >= n_pieces) break;
+            const size_t i = (size_t)(std::upper_bound(pfirst.begin(), pfirst.end(), p) - pfirst.begin() - 1);
+            bool ok = fsize[i] >= 0;
+            if (ok) {
+                const int64_t a = (p - pfirst[i]) * kReadPiece, len = std::min(kReadPiece, fsize[i] - a);
+                const int fd = open(psl_paths[i], O_RDONLY | O_CLOEXEC);
+                ok = fd >= 0;
+                for (int64_t got = 0; ok && got < len;) {
+                    const ssize_t r = pread(fd, res->text_p + foff[i] + a + got, (size_t)(len - got), (off_t)(a + got));
+                    if (r < 0 && errno == EINTR) continue;
+                    ok = r > 0;
+                    got += r > 0 ? r : 0;
+                }
+                if (fd >= 0) close(fd);
             }
-            done[(size_t)i].store(1, std::memory_order_release);
-            cv.notify_one();
+            if (!ok) ioerr[i].store(1, std::memory_order_relaxed);
+            // acq_rel: the last piece's thread sees every other piece's bytes and error flag
+            if (left[i].fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                if (ioerr[i].load(std::memory_order_relaxed)) fstatus[i] = cl::kIO;
+                done[i].store(1, std::memory_order_release);
+                cv.notify_one();
+            }
         }
     };
     in.text = res->text_p;
@@ -441,7 +468,7 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
             if (copy_rc != MANDO_OK) break;
         }
         if (copy_rc != MANDO_OK) {
-            next.store(n_loci);  // stop the readers
+            next.store(n_pieces);  // stop the readers
             std::lock_guard<std::mutex> g(pmu);
             copy_failed = true;
             pcv.notify_all();

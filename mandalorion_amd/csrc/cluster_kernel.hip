@@ -1,8 +1,8 @@
 // cluster_kernel.hip — per-locus read clustering of the D module on the GPU (gfx950).
 //
 // Restates the clustering half of the reference's process_locus (/root/reference/defineIsoforms.py:55-91)
-// as two kernels, one 64-lane wave per locus (the workgroup is that one wave, so __syncthreads() is a
-// wave-local barrier + fence):
+// as two kernels, one 64-lane wave per locus (large loci: a workgroup of kMwWaves waves, whose helper
+// waves join wave 0 for the data-parallel phases, see LocusRun::par):
 //   cluster_parse  PSL text -> records (SDC:278-331 field use), blocks, and every cs string tokenised
 //                  into run-length records (getCSaroundSS, SDC:107-161)
 //   cluster_locus  collect_reads (SDC:278-331), make_genome_bins (:392-438), find_peaks /
@@ -41,7 +41,8 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 // wave helpers (one workgroup == one wave of 64 lanes)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int ln() { return (int)threadIdx.x; }
+__device__ __forceinline__ int ln() { return (int)(threadIdx.x & 63); }
+__device__ __forceinline__ int wv() { return (int)(threadIdx.x >> 6); }
 
 template <class T>
 __device__ __forceinline__ T wsum(T v) {
@@ -74,7 +75,10 @@ __device__ __forceinline__ T wincl(T v) {
     return v;
 }
 __device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
-__device__ __forceinline__ void wsync() { __syncthreads(); }
+// A wave's barrier: its own memory operations complete (lanes exchange data through LDS and the locus
+// scratch).  The large-locus kernel's workgroup has several waves; they meet only at gsync().
+__device__ __forceinline__ void wsync() { __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void gsync() { __syncthreads(); }
 
 __host__ __device__ __forceinline__ int64_t al256(int64_t x) { return (x + 255) & ~int64_t(255); }
 
@@ -1009,6 +1013,10 @@ __device__ void mt_refill(uint32_t *key) {
 struct MT {
     uint32_t *key;
     int pos;
+#ifdef MANDO_CL_PHASES  // dev build: where a permutation's cycles go
+    uint64_t pq_acc = 0, pq_swap = 0;
+    int32_t pq_blocks = 0, pq_arounds = 0, pq_srounds = 0;
+#endif
     __device__ static uint32_t temper(uint32_t y) {
         y ^= (y >> 11);
         y ^= (y << 7) & 0x9d2c5680u;
@@ -1040,17 +1048,31 @@ struct MT {
     // permutation(n): Fisher-Yates from the top (numpy's shuffle: for i = n-1 .. 1, j = interval(i),
     // swap(perm[i], perm[j])), 64 stream outputs at a time, one per lane.
     // Draws: lane t's output serves draw i - (outputs accepted before t); random_interval accepts it iff
-    // (output & mask(i)) <= i.  Assuming every lane from `start` on is accepted, the first lane that
-    // fails is rejected (consumed, the rest shift by one) or lies past i = 1 (not consumed); each ballot
-    // round settles one rejection, consuming exactly the outputs interval() would.
+    // (output & mask(i)) <= i.  A block takes mf <= 64 lanes such that the draws it can serve,
+    // i - mf + 1 .. i, stay at or above the top power of two of i, so one mask serves them all: an
+    // output u = y & mask with u > i is rejected whatever draw it serves, u <= i - mf + 1 accepted
+    // whatever draw it serves; only the rare u in between depend on how many lanes before them were
+    // accepted, and they are settled in lane order on the scalar unit.  Every lane of the block is
+    // consumed (no draw index falls below 1 inside it), exactly the outputs interval() would consume.
     // Swaps: the accepted lanes' swaps (d, v) run in lane order; a prefix of lanes that touch no
-    // position an earlier lane of the block touches (v_s == d_t or v_s == v_t for s < t; d_s == v_t
-    // is impossible since v_t <= d_t < d_s) run at once, then the rest.
-    __device__ void permutation(int32_t n, int32_t *perm) {
+    // position an earlier pending lane touches (v_s == d_t or v_s == v_t for s < t; d_s == v_t is
+    // impossible since v_t <= d_t < d_s) runs at once, then the rest.  Conflicts are found through a
+    // table of `slots` words in free LDS (tab): every pending lane posts its lane into slot v & (slots-1)
+    // with an atomic min (tagged by round, so the table is cleared once per permutation), and lane t
+    // conflicts when slot(d_t) or slot(v_t) holds an earlier lane of this round -- a hash collision can
+    // only split a round early, never hide a conflict.
+    __device__ void permutation(int32_t n, int32_t *perm, uint32_t *tab, int slots) {
         for (int i = ln(); i < n; i += 64) perm[i] = i;
+        for (int i = ln(); i < slots; i += 64) tab[i] = 0xffffffffu;
         wsync();
+        const uint64_t below = (1ull << ln()) - 1;  // (lane 0: 0)
+        uint32_t round = 0;
         int32_t i = n - 1;
         while (i >= 1) {
+#ifdef MANDO_CL_PHASES
+            const uint64_t tq0 = clock64();
+            ++pq_blocks;
+#endif
             if (pos == 624) {
                 mt_refill(key);
                 pos = 0;
@@ -1060,37 +1082,55 @@ struct MT {
             int start = 0, cur = i;
             int32_t dl = 0, vl = 0;
             uint64_t acc = 0;
-            while (start < m) {
-                const int d = cur - (ln() - start);
-                const uint32_t v = y & (0xffffffffu >> __clz(d > 1 ? d : 1));
-                const bool in = ln() >= start && ln() < m;
-                const uint64_t bad = __ballot(in && (d < 1 || v > (uint32_t)d));
-                const int f = bad ? (int)__ffsll((unsigned long long)bad) - 1 : m;
-                if (ln() >= start && ln() < f) {
-                    dl = d;
-                    vl = (int32_t)v;
+            const uint32_t mask = 0xffffffffu >> __clz(cur);
+            // the block's lanes: at most the draws down to the top power of two of i, so that one mask
+            // serves them all (the next block starts under it with the next mask)
+            const int mf = min(m, cur - (int)((mask >> 1) + 1) + 1);
+            {
+                const uint64_t livef = mf >= 64 ? ~0ull : ((1ull << mf) - 1);
+                const uint32_t u = y & mask;
+                acc = __ballot(u <= (uint32_t)(cur - (mf - 1))) & livef;
+                uint64_t amb = __ballot(u > (uint32_t)(cur - (mf - 1)) && u <= (uint32_t)cur) & livef;
+                while (amb) {  // lane order: each one's draw index counts the accepted lanes before it
+                    const int l = (int)__ffsll((unsigned long long)amb) - 1;
+                    const uint32_t ul = (uint32_t)__builtin_amdgcn_readlane((int)u, l);
+                    if (ul <= (uint32_t)(cur - __popcll(acc & ((1ull << l) - 1)))) acc |= 1ull << l;
+                    amb &= amb - 1;
                 }
-                acc |= (f >= 64 ? ~0ull : ((1ull << f) - 1)) & ~((1ull << start) - 1);
-                cur -= f - start;
-                if (f >= m || cur < 1) {  // block used up, or every draw made (lane f not consumed)
-                    start = f;
-                    break;
-                }
-                start = f + 1;  // rejected: consumed
+                dl = cur - __popcll(acc & below);
+                vl = (int32_t)u;
+                start = mf;
+                cur -= __popcll(acc);
+#ifdef MANDO_CL_PHASES
+                ++pq_arounds;
+#endif
             }
             pos += start;
             i = cur;
+#ifdef MANDO_CL_PHASES
+            const uint64_t tq1 = clock64();
+            pq_acc += tq1 - tq0;
+#endif
             uint64_t rem = acc;
+            const uint32_t hm = (uint32_t)slots - 1;
             while (rem) {
+#ifdef MANDO_CL_PHASES
+                ++pq_srounds;
+#endif
+                ++round;
+                const uint32_t tag = (0xffffffu - round) << 8;
+                const bool pend = (rem >> ln()) & 1ull;
+                if (pend) atomicMin(&tab[(uint32_t)vl & hm], tag | (uint32_t)ln());
+                wsync();
                 bool conf = false;
-                for (uint64_t it = rem; it; it &= it - 1) {
-                    const int sl = (int)__ffsll((unsigned long long)it) - 1;
-                    const int32_t vs = __builtin_amdgcn_readlane(vl, sl);
-                    conf |= ln() > sl && (dl == vs || vl == vs);
+                if (pend) {
+                    const uint32_t a = tab[(uint32_t)dl & hm], b = tab[(uint32_t)vl & hm];
+                    conf = ((a >> 8) == (tag >> 8) && (int)(a & 255u) < ln()) ||
+                           ((b >> 8) == (tag >> 8) && (int)(b & 255u) < ln());
                 }
-                const uint64_t cb = __ballot(conf && ((rem >> ln()) & 1ull));
+                const uint64_t cb = __ballot(conf);
                 const int c = cb ? (int)__ffsll((unsigned long long)cb) - 1 : 64;
-                const bool mine = ((rem >> ln()) & 1ull) && ln() < c;
+                const bool mine = pend && ln() < c;
                 int32_t pa = 0, pb = 0;
                 if (mine) {
                     pa = perm[dl];
@@ -1104,6 +1144,9 @@ struct MT {
                 if (rem) wsync();
             }
             wsync();
+#ifdef MANDO_CL_PHASES
+            pq_swap += clock64() - tq1;
+#endif
         }
     }
 };
@@ -1143,7 +1186,23 @@ __device__ double round3(int64_t best, int64_t cov) {
 // ---------------------------------------------------------------------------------------------
 // K2: one locus
 // ---------------------------------------------------------------------------------------------
-constexpr int kLdsPerm = 2048;
+constexpr int kLdsPerm = 4096;
+
+// Large loci (>= kMwMinRecs records: config 2's SIRV-sized loci) run on a workgroup of kMwWaves waves.
+// Wave 0 runs the locus exactly as the one-wave kernel does; the helper waves wait in
+// LocusRun::helper() and join it for the data-parallel phases (coverage sets, the coverage merge),
+// each wave taking a contiguous share of the records / winners.  MwX is their LDS exchange: the phase
+// and its arguments, and per-wave partials in two banks that alternate between exchanges (a wave that
+// runs ahead cannot overwrite a partial another wave has yet to read).
+constexpr int kMwWaves = 8;
+constexpr int kMwMinRecs = 2048;
+constexpr int kOpExit = 0, kOpCovSets = 1, kOpDetCov = 2;
+struct MwX {
+    int32_t op;
+    int32_t i32[4];
+    int64_t i64[4];
+    int64_t part[2][kMwWaves][4];
+};
 constexpr int64_t kPosBias = int64_t(1) << 39;  // sort keys hold position + bias in 40 bits
 
 struct LocusRun {
@@ -1163,6 +1222,9 @@ struct LocusRun {
     int32_t ctr[2];  // spliceDict per-side counters
     int32_t n_iso, n_mem, n_sub;
     int32_t hcb_ok;  // every coverage bin lies in the map, so B.hcb answers histo_cov
+    int W;           // waves of the workgroup (1: the one-wave kernel)
+    MwX *X;          // their exchange (LDS)
+    int64_t xcov;    // determine_cov's result (wave 0)
 #ifdef MANDO_CL_PHASES  // dev build: cycles inside find_peaks (coverage merge, permutation, cs queries)
     uint64_t pc_cov = 0, pc_perm = 0, pc_cs = 0, pc_csof = 0, pc_bins = 0, pc_side = 0;
     uint64_t pc_sd_sort = 0, pc_sd_keys = 0, pc_sd_cand = 0;
@@ -1174,11 +1236,68 @@ struct LocusRun {
     __device__ int32_t *perm_buf(int32_t m) const {
         return m <= kLdsPerm ? lperm : m <= 2 * kSortTile ? reinterpret_cast<int32_t *>(g_sort_lds) : B.perm;
     }
+    // the permutation's conflict table: whichever of the two LDS buffers the permutation does not use,
+    // as many slots as positions where it fits (no collisions then), cleared once per permutation
+    __device__ void permute(int32_t m, int32_t *perm) {
+        int slots = 64;
+        while (slots < m && slots < (m <= kLdsPerm ? 2 * (int)kSortTile : kLdsPerm)) slots <<= 1;
+        mt.permutation(m, perm, m <= kLdsPerm ? reinterpret_cast<uint32_t *>(g_sort_lds) : reinterpret_cast<uint32_t *>(lperm),
+                       slots);
+    }
     __device__ bool in_map(int64_t p) const { return p >= L.map_lo && p < L.map_lo + L.map_n; }
     __device__ int64_t mi(int64_t p) const { return p - L.map_lo; }
 
     __device__ void fail(int code) {
         if (status == kOk) status = code;
+    }
+
+    // --- several waves per locus ----------------------------------------------------------------
+    // wave 0: run a data-parallel phase on every wave of the workgroup (its arguments are in X)
+    __device__ void par(int op) {
+        if (W > 1) {
+            if (ln() == 0) X->op = op;
+            gsync();
+        }
+        exec(op, 0, W);
+        if (W > 1)
+            gsync();
+        else
+            wsync();
+    }
+    __device__ void exec(int op, int w, int nw) {
+        if (op == kOpCovSets)
+            cov_sets(w, nw);
+        else if (op == kOpDetCov)
+            det_cov(w, nw);
+    }
+    // the helper waves: phases until wave 0 posts kOpExit
+    __device__ void helper() {
+        while (true) {
+            gsync();
+            const int op = X->op;
+            if (op == kOpExit) break;
+            exec(op, wv(), W);
+            gsync();
+        }
+    }
+    // one exchange between nw waves: wave w posts (a, b); after one barrier every wave holds the sum
+    // of the a's and the min (or max) of the b's
+    __device__ void xchg(int &ph, int w, int nw, int64_t &a, int64_t &b, bool bmax) {
+        if (nw == 1) return;
+        if (ln() == 0) {
+            X->part[ph][w][0] = a;
+            X->part[ph][w][1] = b;
+        }
+        gsync();
+        int64_t sa = 0, sb = bmax ? INT64_MIN : INT64_MAX;
+        for (int v = 0; v < nw; ++v) {
+            sa += X->part[ph][v][0];
+            const int64_t t = X->part[ph][v][1];
+            sb = bmax ? (t > sb ? t : sb) : (t < sb ? t : sb);
+        }
+        a = sa;
+        b = sb;
+        ph ^= 1;
     }
 
     // --- collect_reads (SDC:278-331) -----------------------------------------------------------
@@ -1231,32 +1350,104 @@ struct LocusRun {
         pc_csof = tc1 - tc0;
 #endif
         // coverage bins per record: myround over each block at stride 10 plus the block's tail, sorted
-        // and made unique (cov_set)
-        int64_t carry = 0, lo = INT64_MAX, hi = INT64_MIN;
-        int bad = 0, oob = 0;
+        // and made unique (cov_set); on every wave of the workgroup (cov_sets)
         const int64_t hist_n = L.map_n / 10 + 2;
         const bool hist_lds = hist_n <= 2 * kSortTile;  // the sort tile is free until build_side
         if (hist_lds) {
             for (int64_t i = ln(); i < hist_n; i += 64) reinterpret_cast<int32_t *>(g_sort_lds)[i] = 0;
-            wsync();
         }
+        if (ln() == 0) X->i32[0] = hist_lds ? 1 : 0;
+        wsync();
+        par(kOpCovSets);
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        int b = 0, oob = 0;
+        for (int v = 0; v < W; ++v) {
+            const int64_t *q = X->part[1][v];
+            lo = q[0] < lo ? q[0] : lo;
+            hi = q[1] > hi ? q[1] : hi;
+            b = (int)q[2] > b ? (int)q[2] : b;
+            oob |= (int)q[3];
+        }
+        if (b) {
+            fail(b == 1 ? kParse : kRange);
+            return;
+        }
+        bin_lo = lo;
+        bin_hi = hi;
+        hcb_ok = !oob;
+        wsync();
+        if (hist_lds)
+            for (int64_t i = ln(); i < hist_n; i += 64) B.hcb[i] = reinterpret_cast<int32_t *>(g_sort_lds)[i];
+        nbins = bin_lo <= bin_hi ? (bin_hi - bin_lo) / 10 + 1 : 0;
+        wsync();
+#ifdef MANDO_CL_PHASES
+        const uint64_t tc2 = clock64();
+        pc_bins = tc2 - tc1;
+#endif
+        for (int k = 0; k < 2; ++k) build_side(B.s[k]);
+#ifdef MANDO_CL_PHASES
+        pc_side = clock64() - tc2;
+#endif
+    }
+
+    // coverage sets (cov_set), the histogram entries of both sides and histo_cov of wave w's share of
+    // the records (collect_reads, SDC:300-331), for nw waves
+    __device__ void cov_sets(int w, int nw) {
+        const int r_lo = (int)((int64_t)n * w / nw), r_hi = (int)((int64_t)n * (w + 1) / nw);
+        const bool hist_lds = X->i32[0] != 0;
+        // the coverage-set capacity and histogram entries of a record
+        auto sizes = [&](const Rec &R, int64_t &capr, int32_t &nl, int32_t &nr) {
+            capr = 0;
+            nl = nr = 0;
+            for (int x = 0; x < R.nblk; ++x) {
+                const int64_t sz = A.blk[2 * (R.blk_off + x)], bs = A.blk[2 * (R.blk_off + x) + 1];
+                capr += (sz > 0 ? (sz + 9) / 10 : 0) + 11;
+                if (!R.acc_lt) {
+                    nl += (bs + sz) != R.tend;
+                    nr += bs != R.tstart;
+                }
+            }
+        };
+        // offsets continue the shares of the waves before this one (record order, as one wave would)
+        int64_t carry = 0;
         int32_t hl_carry = 0, hr_carry = 0;
-        for (int r0 = 0; r0 < n; r0 += 64) {
+        if (nw > 1) {
+            int64_t sc = 0, sl = 0, sr = 0;
+            for (int r0 = r_lo; r0 < r_hi; r0 += 64) {
+                const int r = r0 + ln();
+                if (r < r_hi && A.recs[r].same_chrom) {
+                    int64_t c;
+                    int32_t x, y;
+                    sizes(A.recs[r], c, x, y);
+                    sc += c;
+                    sl += x;
+                    sr += y;
+                }
+            }
+            sc = wsum(sc);
+            sl = wsum(sl);
+            sr = wsum(sr);
+            if (ln() == 0) {
+                X->part[0][w][0] = sc;
+                X->part[0][w][1] = sl;
+                X->part[0][w][2] = sr;
+            }
+            gsync();
+            for (int v = 0; v < w; ++v) {
+                carry += X->part[0][v][0];
+                hl_carry += (int32_t)X->part[0][v][1];
+                hr_carry += (int32_t)X->part[0][v][2];
+            }
+        }
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        int bad = 0, oob = 0;
+        for (int r0 = r_lo; r0 < r_hi; r0 += 64) {
             const int r = r0 + ln();
-            const bool act = r < n && A.recs[r].same_chrom;
+            const bool act = r < r_hi && A.recs[r].same_chrom;
             const Rec R = act ? A.recs[r] : Rec{};
             int64_t capr = 0;
             int32_t nl = 0, nr = 0;
-            if (act) {
-                for (int x = 0; x < R.nblk; ++x) {
-                    const int64_t sz = A.blk[2 * (R.blk_off + x)], bs = A.blk[2 * (R.blk_off + x) + 1];
-                    capr += (sz > 0 ? (sz + 9) / 10 : 0) + 11;
-                    if (!R.acc_lt) {
-                        nl += (bs + sz) != R.tend;
-                        nr += bs != R.tstart;
-                    }
-                }
-            }
+            if (act) sizes(R, capr, nl, nr);
             const int64_t ci = wincl(capr);
             const int64_t coff = carry + ci - capr;
             carry += __shfl(ci, 63);
@@ -1336,32 +1527,21 @@ struct LocusRun {
                         hi = v[u - 1] > hi ? v[u - 1] : hi;
                     }
                 }
-            } else if (r < n) {
+            } else if (r < r_hi) {
                 A.recs[r].cov_off = 0;
                 A.recs[r].cov_n = 0;
             }
         }
-        const int b = wmax(bad);
-        if (b) {
-            fail(b == 1 ? kParse : kRange);
-            return;
+        lo = wmin(lo);
+        hi = wmax(hi);
+        bad = wmax(bad);
+        oob = wany(oob != 0) ? 1 : 0;
+        if (ln() == 0) {
+            X->part[1][w][0] = lo;
+            X->part[1][w][1] = hi;
+            X->part[1][w][2] = bad;
+            X->part[1][w][3] = oob;
         }
-        bin_lo = wmin(lo);
-        bin_hi = wmax(hi);
-        hcb_ok = !wany(oob != 0);
-        wsync();
-        if (hist_lds)
-            for (int64_t i = ln(); i < hist_n; i += 64) B.hcb[i] = reinterpret_cast<int32_t *>(g_sort_lds)[i];
-        nbins = bin_lo <= bin_hi ? (bin_hi - bin_lo) / 10 + 1 : 0;
-        wsync();
-#ifdef MANDO_CL_PHASES
-        const uint64_t tc2 = clock64();
-        pc_bins = tc2 - tc1;
-#endif
-        for (int k = 0; k < 2; ++k) build_side(B.s[k]);
-#ifdef MANDO_CL_PHASES
-        pc_side = clock64() - tc2;
-#endif
     }
 
     __device__ static int64_t myround(int64_t x) {
@@ -1643,24 +1823,49 @@ struct LocusRun {
     }
 
     __device__ int64_t determine_cov(int32_t nn, int64_t center, bool reverse) {
+        if (ln() == 0) {
+            X->i32[0] = nn;
+            X->i32[1] = reverse ? 1 : 0;
+            X->i64[0] = center;
+            X->i64[1] = bin_lo;
+            X->i64[2] = nbins;
+        }
+        wsync();
+        if (W > 1 && nn >= 64 * W)
+            par(kOpDetCov);
+        else
+            det_cov(0, 1);
+        return xcov;
+    }
+
+    // the coverage merge of determine_cov over wave w's share of the nn winners (B.names), nw waves;
+    // wave 0 keeps the result in xcov
+    __device__ void det_cov(int w, int nw) {
+        const int32_t nn = X->i32[0];
+        const bool reverse = X->i32[1] != 0;
+        const int64_t center = X->i64[0], blo = X->i64[1], nbn = X->i64[2];
         int64_t kstart;
         if (reverse) {
-            const int64_t k = center - 1 - bin_lo;
-            kstart = k < 0 ? -1 : (k / 10 < nbins - 1 ? k / 10 : nbins - 1);
-            if (kstart < 0) return 0;
+            const int64_t k = center - 1 - blo;
+            kstart = k < 0 ? -1 : (k / 10 < nbn - 1 ? k / 10 : nbn - 1);
         } else {
-            const int64_t k = center + 1 - bin_lo;
+            const int64_t k = center + 1 - blo;
             kstart = k <= 0 ? 0 : (k + 9) / 10;
-            if (kstart >= nbins) return 0;
+            if (kstart >= nbn) kstart = -1;
         }
-        const int64_t bound = bin_lo + 10 * kstart;
+        if (kstart < 0) {
+            if (w == 0) xcov = 0;
+            return;
+        }
+        const int c_lo = (int)((int64_t)nn * w / nw), c_hi = (int)((int64_t)nn * (w + 1) / nw);
+        const int64_t bound = blo + 10 * kstart;
         const int64_t none = reverse ? INT64_MIN : INT64_MAX;
         // each winner's head: the absolute index of its first set element at / after the bound (the
         // last at / before it for the left side) in B.cur, its value in B.hv
         int64_t best = none;
-        for (int c0 = 0; c0 < nn; c0 += 64) {
+        for (int c0 = c_lo; c0 < c_hi; c0 += 64) {
             const int c = c0 + ln();
-            if (c < nn) {
+            if (c < c_hi) {
                 const Rec &R = A.recs[B.names[c]];
                 const int64_t *v = B.cov + R.cov_off;
                 int lo = 0, hi = R.cov_n;
@@ -1691,17 +1896,22 @@ struct LocusRun {
             }
         }
         int64_t top = reverse ? wmax(best) : wmin(best);
+        int ph = 0;
+        {
+            int64_t z = 0;
+            xchg(ph, w, nw, z, top, reverse);
+        }
         wsync();
         int64_t cov = 0;
         int counter = 0;
         // merge step: the winners at the extreme head (`top`) advance; the next extreme is taken in the
-        // same pass
+        // same pass (count and next extreme exchanged between the waves once per step)
         while (counter < 4 && top != none) {
-            int32_t count = 0;
+            int64_t count = 0;
             int64_t nb = none;
-            for (int c0 = 0; c0 < nn; c0 += 64) {
+            for (int c0 = c_lo; c0 < c_hi; c0 += 64) {
                 const int c = c0 + ln();
-                if (c < nn) {
+                if (c < c_hi) {
                     int64_t h = B.hv[c];
                     if (h == top) {
                         ++count;
@@ -1716,15 +1926,19 @@ struct LocusRun {
                 }
             }
             count = wsum(count);
+            nb = reverse ? wmax(nb) : wmin(nb);
+            xchg(ph, w, nw, count, nb, reverse);
             wsync();
             if (count > 1) {
                 ++counter;
-                const int64_t hc = hcov(top);
-                cov = hc > cov ? hc : cov;
+                if (w == 0) {
+                    const int64_t hc = hcov(top);
+                    cov = hc > cov ? hc : cov;
+                }
             }
-            top = reverse ? wmax(nb) : wmin(nb);
+            top = nb;
         }
-        return cov;
+        if (w == 0) xcov = cov;
     }
 
     // --- getCSaroundSS on the tokenised cs (cluster.cpp cs_around) --------------------------------
@@ -1819,12 +2033,12 @@ struct LocusRun {
         int32_t *perm = perm_buf(nn);
 #ifdef MANDO_CL_PHASES
         const uint64_t tq0 = clock64();
-        mt.permutation(nn, perm);
+        permute(nn, perm);
         const uint64_t tq1 = clock64();
         pc_perm += tq1 - tq0;
         ++pc_char;
 #else
-        mt.permutation(nn, perm);
+        permute(nn, perm);
 #endif
         int32_t allowed = 0, bad = 0;
         int32_t lc[6] = {0, 0, 0, 0, 0, 0}, rc[6] = {0, 0, 0, 0, 0, 0};
@@ -2353,7 +2567,7 @@ struct LocusRun {
             const int lo = B.id_lo[id], m = B.id_hi[id] - lo;
             const int32_t k = m < 10000 ? m : 10000;
             int32_t *perm = perm_buf(m);
-            mt.permutation(m, perm);
+            permute(m, perm);
             const int64_t pk = pow2ge(k);
             int64_t tlo = INT64_MAX, thi = INT64_MIN;
             for (int64_t i = ln(); i < pk; i += 64) {
@@ -2439,7 +2653,7 @@ struct LocusRun {
             const int32_t m = O.iso_nmem[iso];
             const int32_t k = m < P->sub_k ? m : P->sub_k;
             int32_t *perm = perm_buf(m);
-            mt.permutation(m, perm);
+            permute(m, perm);
             for (int i = ln(); i < k; i += 64) O.sub[n_sub + i] = O.mem[moff + perm[i]];
             if (ln() == 0) O.iso_nsub[iso] = k;
             n_sub += k;
@@ -2507,6 +2721,9 @@ struct LocusRun {
                    "%.2f bins %.2f sides %.2f\n", n, pc_cand, pc_char, pc_cov * 1e-6, pc_perm * 1e-6, pc_cs * 1e-6,
                    pc_csof * 1e-6, pc_bins * 1e-6, pc_side * 1e-6);
         if (ln() == 0)
+            printf("[K2 perm] n %d: blocks %d accept rounds %d swap rounds %d | accept %.2f swap %.2f Mcyc\n", n,
+                   mt.pq_blocks, mt.pq_arounds, mt.pq_srounds, mt.pq_acc * 1e-6, mt.pq_swap * 1e-6);
+        if (ln() == 0)
             printf("[K2 sides] n %d: H %d %d | sort %.2f keys %.2f cand %.2f Mcyc\n", n, B.s[0].H, B.s[1].H,
                    pc_sd_sort * 1e-6, pc_sd_keys * 1e-6, pc_sd_cand * 1e-6);
 #endif
@@ -2514,14 +2731,19 @@ struct LocusRun {
     }
 };
 
-__global__ __launch_bounds__(64) void cluster_locus(Args G) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void cluster_locus(Args G) {
     __shared__ uint32_t mtk[624];
     __shared__ int32_t lperm[kLdsPerm];
+    __shared__ MwX mwx;
     const int li = G.order[blockIdx.x];
     Stats *st = G.stats + li;
     LocusRun R;
     R.S = *st;
-    if (R.S.status != kOk) return;
+    if (R.S.status != kOk) return;  // (every wave of the workgroup)
+    R.W = NW;
+    R.X = &mwx;
+    R.xcov = 0;
     R.L = G.loci[li];
     R.T = G.text + R.L.text_off;
     R.P = G.prm;
@@ -2533,13 +2755,21 @@ __global__ __launch_bounds__(64) void cluster_locus(Args G) {
     R.n_peaks = 0;
     R.n_iso = R.n_mem = R.n_sub = 0;
     R.n_ids = R.n_members = 0;
-    for (int i = ln(); i < 624; i += 64) mtk[i] = R.P->mt_init[i];
     R.mt.key = mtk;
     R.mt.pos = 624;
     R.lperm = lperm;
+    if (NW > 1 && wv() > 0) {
+        R.helper();
+        return;
+    }
+    for (int i = ln(); i < 624; i += 64) mtk[i] = R.P->mt_init[i];
     wsync();
     R.run(G);
     wsync();
+    if (NW > 1) {  // the helpers leave their loop
+        if (ln() == 0) mwx.op = kOpExit;
+        gsync();
+    }
     if (ln() == 0) {
         st->status = R.status;
         st->n_peaks = R.n_peaks;
@@ -2562,9 +2792,15 @@ hipError_t launch_parse(const Args &a, int n_blocks, int n_work, hipStream_t s) 
     hipLaunchKernelGGL(cluster_cs_runs, dim3(n_work), dim3(64), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_locus(const Args &a, int n_blocks, hipStream_t s) {
-    if (n_blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(cluster_locus, dim3(n_blocks), dim3(64), kSortTile * 8, s, a);
+// K2 over the loci a.order[0, n_big) on kMwWaves-wave workgroups, then a.order[n_big, n_blocks) on
+// one wave each
+hipError_t launch_locus(const Args &a, int n_blocks, int n_big, hipStream_t s) {
+    if (n_big > 0) hipLaunchKernelGGL(cluster_locus<kMwWaves>, dim3(n_big), dim3(64 * kMwWaves), kSortTile * 8, s, a);
+    if (n_blocks > n_big) {
+        Args b = a;
+        b.order = a.order + n_big;
+        hipLaunchKernelGGL(cluster_locus<1>, dim3(n_blocks - n_big), dim3(64), kSortTile * 8, s, b);
+    }
     return hipGetLastError();
 }
 int64_t b_bytes(const Stats &S, const Locus &L, int w) {
@@ -2893,11 +3129,15 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
             if (out.status[(size_t)i] != kOk && st[(size_t)i].status == kOk) st[(size_t)i].status = out.status[(size_t)i];
         CL_TRY(hipMemcpyAsync(d_stats.p, st.data(), (size_t)nl * sizeof(Stats), hipMemcpyHostToDevice, s));
         CL_TRY(hipMemcpyAsync(d_loci.p, L.data(), (size_t)nl * sizeof(Locus), hipMemcpyHostToDevice, s));
+        // loci of kMwMinRecs records or more first: they take the several-wave kernel
+        const int n_big = (int)(std::stable_partition(k2_order.begin(), k2_order.end(),
+                                                      [&](int32_t i) { return st[(size_t)i].n_rec >= kMwMinRecs; }) -
+                                k2_order.begin());
         CL_TRY(hipMemcpyAsync(d_order.p, k2_order.data(), k2_order.size() * 4, hipMemcpyHostToDevice, s));
         G.scratch_b = d_b.as<uint8_t>();
         G.out = d_o.as<uint8_t>();
         G.rec_text = d_rec.as<int64_t>();
-        CL_TRY(launch_locus(G, (int)k2_order.size(), s));
+        CL_TRY(launch_locus(G, (int)k2_order.size(), n_big, s));
         uint8_t *ho = nullptr;
         CL_TRY(pinned_host(ctx, 0, (size_t)o_tot + 256, ho));
         out.rec_text.resize((size_t)recs * 4);

@@ -2113,7 +2113,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
 }
 
 #define MANDO_FR_OPERANDS \
-        : [i] "+s"(i), [pr] "+s"(pr), [pb] "+s"(pb), [pe] "+s"(pe), [pa] "+s"(pa), [tbu] "+s"(tbu), [split] "+s"(split), \
+        : [i] "+s"(i), [pr] "+s"(pr), [pb] "+s"(pb), [pe] "+s"(pe), [pa] "+s"(pa), [tbu] "+s"(tbu), \
           [kpu] "+s"(kpu), [svu] "+s"(svu), [cel] "+s"(cel), [r16] "+v"(r16), \
           [d1] "=&s"(d1), [rem] "=&s"(rem), [p0] "=&s"(p0), [p1] "=&s"(p1), [rb1] "=&s"(rb1), [re1] "=&s"(re1), \
           [ra1] "=&s"(ra1), [x] "=&s"(x), [y] "=&s"(y), [z] "=&s"(z), [beg] "=&s"(beg), [end] "=&s"(end), \
@@ -2132,36 +2132,24 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
           [FJ2] "=&v"(FJ2), [clo] "=&v"(clo), [chi] "=&v"(chi), [vkneg] "=&v"(vkneg), [v10000] "=&v"(v10000), \
           [v0c0c] "=&v"(v0c0c) \
         : [iend] "s"(iend), [b0] "s"(b0), [qlen] "s"(qlen), [w] "s"(w), [Ldesc] "s"(Ldesc), [Lrrow] "s"(Lrrow), \
-          [Lring] "s"(Lring), [Lq] "s"(Lq), [tbp] "s"(tbp), [kpp] "s"(kpp), [svp] "s"(svp), [rip] "s"(rip), [Lw2] "s"(Lw2) \
+          [Lring] "s"(Lring), [Lq] "s"(Lq), [tbp] "s"(tbp), [kpp] "s"(kpp), [svp] "s"(svp), [rip] "s"(rip) \
         : "memory", "scc", "v120", "v121", "v122", "v123", "v124", "v125"
 
-template <int RW, int NW>
 __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb, gu8 *kp, gint *sv, gint *rinfo,
                                              int b0, int i, int iend, int qlen, int w, int &prv_r, int &prv_beg,
-                                             int &prv_end, int &prv_am, DpState &ds, int &split) {
+                                             int &prv_end, int &prv_am, DpState &ds) {
+    constexpr int RW = kChunk;
     using SC = DefaultScores;
     static_assert(SC::match == 5 && SC::mismatch == 4 && SC::o1 == 4 && SC::e1 == 2 && SC::o2 == 24 && SC::e2 == 1,
                   "the constants below are abPOA's defaults");
-    static_assert(kRing16 == 8 && kChunk == 128 && kRowRing == 32 && kDescInts == 8 && kRowInfoInts == 8 &&
-                      (RW == kChunk || RW == kWideRing) && kWideRing == 256 && kW2Nop == 2,
+    static_assert(kRing16 == 8 && kChunk == 128 && kRowRing == 32 && kDescInts == 8 && kRowInfoInts == 8,
                   "LDS / HBM geometry the block assumes");
     const uint32_t Ldesc = lds_addr(&sh.desc[0][0]), Lrrow = lds_addr(&sh.rrow[0]);
     const uint32_t Lring = lds_addr(ring16_row<RW>(sh, 0)), Lq = lds_addr(qnib<RW>());
-    uint32_t Lw2 = 0;  // a two-wave wide workgroup: wave 1's command word (a row after a split row syncs first)
-    if constexpr (NW > 1) Lw2 = lds_addr(&w2lds().cmd.op);
-    Lw2 = (uint32_t)bcast0((int)Lw2);
-    split = bcast0(split);
     const uint64_t tbp = (uint64_t)uni64((int64_t)tb), kpp = (uint64_t)uni64((int64_t)kp);
     const uint64_t svp = (uint64_t)uni64((int64_t)sv), rip = (uint64_t)uni64((int64_t)rinfo);
-    // the block's scalar operands must be provably wave-uniform (two-wave workgroups: the compiler cannot
-    // tell that wave 0's copies of these are)
-    int pr = bcast0(prv_r), pb = bcast0(prv_beg), pe = bcast0(prv_end), pa = bcast0(prv_am);
-    int tbu = bcast0(ds.tb_used), kpu = bcast0(ds.kp_used), svu = bcast0(ds.sv_used), cel = bcast0(ds.cells);
-    i = bcast0(i);
-    iend = bcast0(iend);
-    b0 = bcast0(b0);
-    qlen = bcast0(qlen);
-    w = bcast0(w);
+    int pr = prv_r, pb = prv_beg, pe = prv_end, pa = prv_am;
+    int tbu = ds.tb_used, kpu = ds.kp_used, svu = ds.sv_used, cel = ds.cells;
     uint32_t r16 = ds.r16acc;
     (void)lane;
     // scalar temporaries and constants
@@ -2174,7 +2162,7 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
     uint32_t Ga, Gb, Pa, Pb, inc, S, M, H0, E1, t1, F1, P1, P2, iw, a0, inv, m1, m2, Hd, X1, X2, MK, K1, K2, G1, G2,
         amk, H, X1e, Ho1, X2e, Ho2, E2, voff, vlane, vlane2, vlane8, LJ1, LJ2, FJ1, FJ2, clo, chi, vkneg, v10000,
         v0c0c;
-    if constexpr (RW == kChunk) {
+    {
         asm volatile(
             "s_nop 4\n"
             "s_waitcnt lgkmcnt(0)\n"
@@ -2807,645 +2795,6 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_add_i32 %[cel], %[cel], %[x]\n"
             "s_nop 1\n"
             MANDO_FR_OPERANDS);
-    } else {
-        asm volatile(
-            "s_nop 4\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "s_mov_b32 %[c20002], 0x20002\n"
-            "s_movk_i32 %[c128], 0x80\n"
-            "s_movk_i32 %[cr16], 0x7918\n"
-            "s_mov_b32 %[cq], 0xf000f\n"
-            "s_mov_b32 %[cth], 0x4040404\n"
-            "s_mov_b32 %[csel0], 0x5040100\n"
-            "s_mov_b32 %[csel1], 0x7060302\n"
-            "s_mov_b32 %[cseltb], 0xb0a0908\n"
-            "s_mov_b32 %[cselkp], 0xc0c0200\n"
-            "s_mov_b32 %[m01], 0x2020101\n"
-            "s_mov_b32 %[m23], 0x8080404\n"
-            "s_mov_b32 %[m45], 0x20201010\n"
-            "s_mov_b32 %[m67], 0x80804040\n"
-            "v_mbcnt_lo_u32_b32 %[vlane], -1, 0\n"
-            "v_mbcnt_hi_u32_b32 %[vlane], -1, %[vlane]\n"
-            "v_lshlrev_b32 %[vlane2], 1, %[vlane]\n"
-            "v_lshlrev_b32 %[vlane8], 3, %[vlane]\n"
-            "v_mul_u32_u24 %[LJ2], 0x10001, %[vlane2]\n"
-            "v_add_u32 %[LJ2], 0x10000, %[LJ2]\n"
-            "v_lshlrev_b32 %[LJ1], 1, %[LJ2]\n"
-            "v_add_u32 %[FJ1], 0x40004, %[LJ1]\n"
-            "v_add_u32 %[FJ2], 0x180018, %[LJ2]\n"
-            "v_sub_u32 %[clo], 0x7f, %[vlane2]\n"
-            "v_sub_u32 %[chi], 0x7e, %[vlane2]\n"
-            "v_mov_b32 %[vkneg], 0x80008000\n"
-            "v_mov_b32 %[v10000], 0x10000\n"
-            "v_mov_b32 %[v0c0c], 0xc000c00\n"
-            "s_mov_b32 %[i0], %[i]\n"
-            "s_and_b32 %[x], %[pr], 7\n"
-            "s_mulk_i32 %[x], 0x600\n"
-            "s_add_u32 %[pwb], %[x], %[Lring]\n"
-            "L_top%=:\n"
-            "s_cmp_ge_i32 %[i], %[iend]\n"
-            "s_cbranch_scc1 L_out%=\n"
-            "s_lshl_b32 %[x], %[i], 5\n"
-            "s_add_u32 %[x], %[x], %[Ldesc]\n"
-            "v_mov_b32 %[Ga], %[x]\n"
-            "ds_read_b32 %[Gb], %[Ga] offset:4\n"
-            "ds_read_b32 %[Pa], %[Ga] offset:8\n"
-            "ds_read_b32 %[Pb], %[Ga] offset:12\n"
-            "ds_read_b32 %[inc], %[Ga] offset:16\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "v_readfirstlane_b32 %[d1], %[Gb]\n"
-            "v_readfirstlane_b32 %[p0], %[Pb]\n"
-            "v_readfirstlane_b32 %[rem], %[Pa]\n"
-            "s_and_b32 %[y], %[d1], 0xffffc000\n"
-            "s_cmp_eq_u32 %[y], 0x18000\n"
-            "s_cbranch_scc0 L_two%=\n"
-            "s_cmp_eq_u32 %[p0], %[pr]\n"
-            "s_cbranch_scc1 L_p0ok1%=\n"
-            "s_and_b32 %[x], %[p0], 31\n"
-            "s_lshl_b32 %[x], %[x], 4\n"
-            "s_add_u32 %[x], %[x], %[Lrrow]\n"
-            "v_mov_b32 %[Ga], %[x]\n"
-            "ds_read_b32 %[Gb], %[Ga]\n"
-            "ds_read_b32 %[Pa], %[Ga] offset:4\n"
-            "ds_read_b32 %[Pb], %[Ga] offset:8\n"
-            "s_and_b32 %[x], %[p0], 7\n"
-            "s_mulk_i32 %[x], 0x600\n"
-            "s_add_u32 %[pwb], %[x], %[Lring]\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "v_readfirstlane_b32 %[pb], %[Gb]\n"
-            "v_readfirstlane_b32 %[pe], %[Pa]\n"
-            "v_readfirstlane_b32 %[pa], %[Pb]\n"
-            "s_mov_b32 %[pr], %[p0]\n"
-            "L_p0ok1%=:\n"
-            "s_sub_i32 %[x], %[qlen], %[rem]\n"
-            "s_add_i32 %[z], %[pa], 1\n"
-            "s_min_i32 %[y], %[z], %[x]\n"
-            "s_max_i32 %[z], %[z], %[x]\n"
-            "s_sub_i32 %[y], %[y], %[w]\n"
-            "s_add_i32 %[z], %[z], %[w]\n"
-            "s_max_i32 %[beg], %[y], 0\n"
-            "s_min_i32 %[end], %[z], %[qlen]\n"
-            "s_and_b32 %[cb0], %[beg], -2\n"
-            "s_sub_i32 %[spm], %[end], %[cb0]\n"
-            "s_and_b32 %[pc0], %[pb], -2\n"
-            "s_sub_i32 %[x], %[pe], %[pc0]\n"
-            "s_cmpk_gt_i32 %[spm], 0x7f\n"
-            "s_cbranch_scc1 L_out%=\n"
-            "s_cmpk_gt_i32 %[x], 0xff\n"
-            "s_cbranch_scc1 L_out%=\n"
-            "s_cmp_eq_u32 %[split], 0\n"
-            "s_cbranch_scc1 L_nosync1%=\n"
-            "v_mov_b32 %[a0], %[Lw2]\n"
-            "v_mov_b32 %[voff], 2\n"
-            "s_mov_b64 exec, 1\n"
-            "ds_write_b32 %[a0], %[voff]\n"
-            "s_mov_b64 exec, -1\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "s_barrier\n"
-            "s_mov_b32 %[split], 0\n"
-            "L_nosync1%=:\n"
-            "s_bfe_u32 %[z], %[d1], 0x80000\n"
-            "s_lshl_b32 %[x], %[z], 3\n"
-            "s_lshl_b32 %[tlo], 9, %[x]\n"
-            "s_cmp_gt_u32 %[z], 3\n"
-            "s_cselect_b32 %[tlo], %[cth], %[tlo]\n"
-            "s_pack_ll_b32_b16 %[pkb], %[beg], %[beg]\n"
-            "s_pack_ll_b32_b16 %[pke], %[end], %[end]\n"
-            "s_bfe_u32 %[x], %[cb0], 0xf0001\n"
-            "v_add_u32 %[M], %[x], %[vlane]\n"
-            "v_mad_u32_u24 %[H0], %[M], %[c20002], %[v10000]\n"
-            "v_add_u32 %[Ga], %[Lq], %[M]\n"
-            "ds_read_u8 %[S], %[Ga]\n"
-            "v_and_b32 %[iw], 127, %[M]\n"
-            "v_lshl_add_u32 %[a0], %[iw], 2, %[pwb]\n"
-            "ds_read_b32 %[E1], %[a0]\n"
-            "ds_read_b32 %[X1], %[a0] offset:512\n"
-            "ds_read_b32 %[X2], %[a0] offset:1024\n"
-            "v_add_u32 %[Gb], -1, %[M]\n"
-            "v_and_b32 %[Gb], 127, %[Gb]\n"
-            "v_lshl_add_u32 %[Pa], %[Gb], 2, %[pwb]\n"
-            "ds_read_b32 %[t1], %[Pa]\n"
-            "v_pk_sub_i16 %[m1], %[H0], %[pkb]\n"
-            "v_pk_sub_i16 %[m2], %[pke], %[H0]\n"
-            "v_or_b32 %[m1], %[m1], %[m2]\n"
-            "v_pk_ashrrev_i16 %[inv], 15, %[m1] op_sel_hi:[0,1]\n"
-            "s_waitcnt lgkmcnt(4)\n"
-            "v_mul_u32_u24 %[S], 0x1001, %[S]\n"
-            "v_and_or_b32 %[S], %[S], %[cq], %[v0c0c]\n"
-            "v_perm_b32 %[S], 4, %[tlo], %[S]\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "v_alignbit_b32 %[Hd], %[E1], %[t1], 16\n"
-            "s_pack_ll_b32_b16 %[x], %[pb], %[pb]\n"
-            "s_pack_ll_b32_b16 %[y], %[pe], %[pe]\n"
-            "v_pk_add_u16 %[t1], %[H0], -1\n"
-            "v_pk_sub_i16 %[m1], %[t1], %[x]\n"
-            "v_pk_sub_i16 %[m2], %[y], %[t1]\n"
-            "v_or_b32 %[m1], %[m1], %[m2]\n"
-            "v_pk_ashrrev_i16 %[m1], 15, %[m1] op_sel_hi:[0,1]\n"
-            "v_pk_sub_i16 %[m2], %[H0], %[x]\n"
-            "v_pk_sub_i16 %[t1], %[y], %[H0]\n"
-            "v_or_b32 %[m2], %[m2], %[t1]\n"
-            "v_pk_ashrrev_i16 %[m2], 15, %[m2] op_sel_hi:[0,1]\n"
-            "v_bfi_b32 %[Hd], %[m1], %[vkneg], %[Hd]\n"
-            "v_bfi_b32 %[X1], %[m2], %[vkneg], %[X1]\n"
-            "v_bfi_b32 %[X2], %[m2], %[vkneg], %[X2]\n"
-            "v_pk_add_i16 %[M], %[Hd], %[S] clamp\n"
-            "v_pk_add_i16 %[M], %[M], -4 op_sel_hi:[1,0] clamp\n"
-            "v_pk_max_i16 %[t1], %[X1], %[X2]\n"
-            "v_pk_max_i16 %[t1], %[M], %[t1]\n"
-            "v_bfi_b32 %[H0], %[inv], %[vkneg], %[t1]\n"
-            "v_pk_add_i16 %[G1], %[H0], %[LJ1] clamp\n"
-            "v_pk_add_i16 %[G2], %[H0], %[LJ2] clamp\n"
-            "v_perm_b32 %[Ga], %[G2], %[G1], %[csel0]\n"
-            "v_perm_b32 %[Gb], %[G2], %[G1], %[csel1]\n"
-            "v_pk_max_i16 %[inc], %[Ga], %[Gb]\n"
-            "v_xor_b32 %[inc], 0x80008000, %[inc]\n"
-            "v_mad_i32_i16 %[amk], %[H0], %[c128], %[clo]\n"
-            "v_mad_i32_i16 %[t1], %[H0], %[c128], %[chi] op_sel:[1,0,0,0]\n"
-            "v_max_i32 %[amk], %[amk], %[t1]\n"
-            "s_nop 1\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:1 row_mask:0xf bank_mask:0xf\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "s_nop 0\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:2 row_mask:0xf bank_mask:0xf\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:4 row_mask:0xf bank_mask:0xf\n"
-            "s_nop 0\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "s_nop 0\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:8 row_mask:0xf bank_mask:0xf\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-            "s_nop 0\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-            "s_nop 0\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "s_nop 1\n"
-            "v_readlane_b32 %[mp], %[amk], 63\n"
-            "v_xor_b32_dpp %[Pa], %[inc], %[vkneg] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_pk_max_i16 %[Pb], %[Pa], %[Ga]\n"
-            "v_perm_b32 %[P1], %[Pb], %[Pa], %[csel0]\n"
-            "v_perm_b32 %[P2], %[Pb], %[Pa], %[csel1]\n"
-            "v_pk_sub_i16 %[F1], %[P1], %[FJ1] clamp\n"
-            "v_pk_sub_i16 %[S], %[P2], %[FJ2] clamp\n"
-            "v_pk_max_i16 %[H], %[F1], %[S]\n"
-            "v_pk_max_i16 %[H], %[H0], %[H]\n"
-            "v_pk_add_i16 %[X1e], %[X1], -2 op_sel_hi:[1,0] clamp\n"
-            "v_pk_add_i16 %[Ho1], %[H], -6 op_sel_hi:[1,0] clamp\n"
-            "v_pk_add_i16 %[X2e], %[X2], -1 clamp\n"
-            "v_pk_sub_i16 %[Ho2], %[H], 25 op_sel_hi:[1,0] clamp\n"
-            "v_pk_max_i16 %[E1], %[X1e], %[Ho1]\n"
-            "v_pk_max_i16 %[E2], %[X2e], %[Ho2]\n"
-            "v_pk_sub_i16 %[Ga], %[M], %[H] clamp\n"
-            "v_pk_sub_i16 %[Gb], %[X1], %[H] clamp\n"
-            "v_perm_b32 %[Pa], %[Gb], %[Ga], %[cseltb]\n"
-            "v_pk_sub_i16 %[Ga], %[X2], %[H] clamp\n"
-            "v_pk_sub_i16 %[Gb], %[F1], %[H] clamp\n"
-            "v_perm_b32 %[Pb], %[Gb], %[Ga], %[cseltb]\n"
-            "v_pk_sub_i16 %[Ga], %[Ho1], %[X1e] clamp\n"
-            "v_pk_sub_i16 %[Gb], %[Ho2], %[X2e] clamp\n"
-            "v_perm_b32 %[inc], %[Gb], %[Ga], %[cseltb]\n"
-            "v_pk_sub_i16 %[Ga], %[G1], %[P1] clamp\n"
-            "v_pk_sub_i16 %[Gb], %[G2], %[P2] clamp\n"
-            "v_perm_b32 %[amk], %[Gb], %[Ga], %[cseltb]\n"
-            "v_and_b32 %[amk], %[m67], %[amk]\n"
-            "v_and_or_b32 %[amk], %[inc], %[m45], %[amk]\n"
-            "v_and_or_b32 %[amk], %[Pb], %[m23], %[amk]\n"
-            "v_and_or_b32 %[amk], %[Pa], %[m01], %[amk]\n"
-            "v_or_b32_sdwa %[amk], %[amk], %[amk] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
-            "v_add_u32 %[voff], %[tbu], %[vlane2]\n"
-            "global_store_short %[voff], %[amk], %[tbp]\n"
-            "v_bfi_b32 %[Hd], %[inv], %[vkneg], %[H]\n"
-            "v_bfi_b32 %[m1], %[inv], %[vkneg], %[E1]\n"
-            "v_bfi_b32 %[m2], %[inv], %[vkneg], %[E2]\n"
-            "s_add_u32 %[r], %[b0], %[i]\n"
-            "s_and_b32 %[y], %[r], 7\n"
-            "s_mulk_i32 %[y], 0x600\n"
-            "s_add_u32 %[y], %[y], %[Lring]\n"
-            "v_lshl_add_u32 %[a0], %[iw], 2, %[y]\n"
-            "ds_write_b32 %[a0], %[Hd]\n"
-            "ds_write_b32 %[a0], %[m1] offset:512\n"
-            "ds_write_b32 %[a0], %[m2] offset:1024\n"
-            "v_pk_add_u16 %[t1], %[Hd], %[cr16] op_sel_hi:[1,0]\n"
-            "v_pk_min_u16 %[r16], %[r16], %[t1]\n"
-            "s_and_b32 %[x], %[mp], 0x7f\n"
-            "s_sub_i32 %[besti], %[cb0], %[x]\n"
-            "s_addk_i32 %[besti], 0x7f\n"
-            "s_bitcmp1_b32 %[d1], 8\n"
-            "s_cbranch_scc1 L_far1%=\n"
-            "s_sub_i32 %[x], %[tbu], %[cb0]\n"
-            "s_sub_i32 %[z], %[kpu], %[cb0]\n"
-            "v_mov_b32 v120, %[beg]\n"
-            "v_mov_b32 v121, %[end]\n"
-            "v_mov_b32 v122, %[x]\n"
-            "v_mov_b32 v123, %[z]\n"
-            "v_mov_b32 v124, %[besti]\n"
-            "s_and_b32 %[x], %[r], 31\n"
-            "s_lshl_b32 %[x], %[x], 4\n"
-            "s_add_u32 %[x], %[x], %[Lrrow]\n"
-            "v_mov_b32 %[a0], %[x]\n"
-            "s_lshl_b32 %[x], %[r], 5\n"
-            "v_mov_b32 %[voff], %[x]\n"
-            "v_mov_b32 v125, -1\n"
-            "s_mov_b64 exec, 1\n"
-            "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
-            "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
-            "s_mov_b64 exec, -1\n"
-            "s_sub_i32 %[x], %[end], %[beg]\n"
-            "s_add_i32 %[cel], %[cel], %[x]\n"
-            "s_add_i32 %[x], %[spm], 4\n"
-            "s_and_b32 %[x], %[x], -4\n"
-            "s_add_i32 %[tbu], %[tbu], %[x]\n"
-            "s_mov_b32 %[pr], %[r]\n"
-            "s_mov_b32 %[pb], %[beg]\n"
-            "s_mov_b32 %[pe], %[end]\n"
-            "s_mov_b32 %[pa], %[besti]\n"
-            "s_mov_b32 %[pwb], %[y]\n"
-            "s_add_i32 %[i], %[i], 1\n"
-            "s_branch L_top%=\n"
-            "L_far1%=:\n"
-            "s_lshl_b32 %[x], %[svu], 2\n"
-            "v_add_u32 %[voff], %[x], %[vlane8]\n"
-            "v_bfe_i32 v120, %[H], 0, 16\n"
-            "v_ashrrev_i32 v121, 16, %[H]\n"
-            "v_bfe_i32 v122, %[E1], 0, 16\n"
-            "v_ashrrev_i32 v123, 16, %[E1]\n"
-            "v_bfe_i32 v124, %[E2], 0, 16\n"
-            "v_ashrrev_i32 v125, 16, %[E2]\n"
-            "global_store_dwordx2 %[voff], v[120:121], %[svp]\n"
-            "global_store_dwordx2 %[voff], v[122:123], %[svp] offset:512\n"
-            "global_store_dwordx2 %[voff], v[124:125], %[svp] offset:1024\n"
-            "s_sub_i32 %[x], %[tbu], %[cb0]\n"
-            "s_sub_i32 %[z], %[kpu], %[cb0]\n"
-            "v_mov_b32 v120, %[beg]\n"
-            "v_mov_b32 v121, %[end]\n"
-            "v_mov_b32 v122, %[x]\n"
-            "v_mov_b32 v123, %[z]\n"
-            "v_mov_b32 v124, %[besti]\n"
-            "s_and_b32 %[x], %[r], 31\n"
-            "s_lshl_b32 %[x], %[x], 4\n"
-            "s_add_u32 %[x], %[x], %[Lrrow]\n"
-            "v_mov_b32 %[a0], %[x]\n"
-            "s_lshl_b32 %[x], %[r], 5\n"
-            "v_mov_b32 %[voff], %[x]\n"
-            "v_mov_b32 v125, %[svu]\n"
-            "s_mov_b64 exec, 1\n"
-            "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
-            "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
-            "global_store_dwordx2 %[voff], v[124:125], %[rip] offset:16\n"
-            "s_addk_i32 %[svu], 0x180\n"
-            "s_mov_b64 exec, -1\n"
-            "s_sub_i32 %[x], %[end], %[beg]\n"
-            "s_add_i32 %[cel], %[cel], %[x]\n"
-            "s_add_i32 %[x], %[spm], 4\n"
-            "s_and_b32 %[x], %[x], -4\n"
-            "s_add_i32 %[tbu], %[tbu], %[x]\n"
-            "s_mov_b32 %[pr], %[r]\n"
-            "s_mov_b32 %[pb], %[beg]\n"
-            "s_mov_b32 %[pe], %[end]\n"
-            "s_mov_b32 %[pa], %[besti]\n"
-            "s_mov_b32 %[pwb], %[y]\n"
-            "s_add_i32 %[i], %[i], 1\n"
-            "s_branch L_top%=\n"
-            "L_two%=:\n"
-            "s_cmp_lg_u32 %[y], 0x28000\n"
-            "s_cbranch_scc1 L_out%=\n"
-            "v_readfirstlane_b32 %[p1], %[inc]\n"
-            "s_cmp_eq_u32 %[p1], %[pr]\n"
-            "s_cbranch_scc0 L_p1lds%=\n"
-            "s_mov_b32 %[rb1], %[pb]\n"
-            "s_mov_b32 %[re1], %[pe]\n"
-            "s_mov_b32 %[ra1], %[pa]\n"
-            "s_mov_b32 %[base1], %[pwb]\n"
-            "s_branch L_p1ok%=\n"
-            "L_p1lds%=:\n"
-            "s_and_b32 %[x], %[p1], 31\n"
-            "s_lshl_b32 %[x], %[x], 4\n"
-            "s_add_u32 %[x], %[x], %[Lrrow]\n"
-            "v_mov_b32 %[Ga], %[x]\n"
-            "ds_read_b32 %[Gb], %[Ga]\n"
-            "ds_read_b32 %[Pa], %[Ga] offset:4\n"
-            "ds_read_b32 %[Pb], %[Ga] offset:8\n"
-            "s_and_b32 %[x], %[p1], 7\n"
-            "s_mulk_i32 %[x], 0x600\n"
-            "s_add_u32 %[base1], %[x], %[Lring]\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "v_readfirstlane_b32 %[rb1], %[Gb]\n"
-            "v_readfirstlane_b32 %[re1], %[Pa]\n"
-            "v_readfirstlane_b32 %[ra1], %[Pb]\n"
-            "L_p1ok%=:\n"
-            "s_cmp_eq_u32 %[p0], %[pr]\n"
-            "s_cbranch_scc1 L_p0ok2%=\n"
-            "s_and_b32 %[x], %[p0], 31\n"
-            "s_lshl_b32 %[x], %[x], 4\n"
-            "s_add_u32 %[x], %[x], %[Lrrow]\n"
-            "v_mov_b32 %[Ga], %[x]\n"
-            "ds_read_b32 %[Gb], %[Ga]\n"
-            "ds_read_b32 %[Pa], %[Ga] offset:4\n"
-            "ds_read_b32 %[Pb], %[Ga] offset:8\n"
-            "s_and_b32 %[x], %[p0], 7\n"
-            "s_mulk_i32 %[x], 0x600\n"
-            "s_add_u32 %[pwb], %[x], %[Lring]\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "v_readfirstlane_b32 %[pb], %[Gb]\n"
-            "v_readfirstlane_b32 %[pe], %[Pa]\n"
-            "v_readfirstlane_b32 %[pa], %[Pb]\n"
-            "s_mov_b32 %[pr], %[p0]\n"
-            "L_p0ok2%=:\n"
-            "s_sub_i32 %[x], %[qlen], %[rem]\n"
-            "s_min_i32 %[y], %[pa], %[ra1]\n"
-            "s_max_i32 %[z], %[pa], %[ra1]\n"
-            "s_add_i32 %[y], %[y], 1\n"
-            "s_add_i32 %[z], %[z], 1\n"
-            "s_min_i32 %[y], %[y], %[x]\n"
-            "s_max_i32 %[z], %[z], %[x]\n"
-            "s_sub_i32 %[y], %[y], %[w]\n"
-            "s_add_i32 %[z], %[z], %[w]\n"
-            "s_max_i32 %[beg], %[y], 0\n"
-            "s_min_i32 %[end], %[z], %[qlen]\n"
-            "s_and_b32 %[cb0], %[beg], -2\n"
-            "s_sub_i32 %[spm], %[end], %[cb0]\n"
-            "s_and_b32 %[pc0], %[pb], -2\n"
-            "s_sub_i32 %[x], %[pe], %[pc0]\n"
-            "s_and_b32 %[pc1], %[rb1], -2\n"
-            "s_sub_i32 %[y], %[re1], %[pc1]\n"
-            "s_max_i32 %[x], %[x], %[y]\n"
-            "s_cmpk_gt_i32 %[spm], 0x7f\n"
-            "s_cbranch_scc1 L_out%=\n"
-            "s_cmpk_gt_i32 %[x], 0xff\n"
-            "s_cbranch_scc1 L_out%=\n"
-            "s_cmp_eq_u32 %[split], 0\n"
-            "s_cbranch_scc1 L_nosync2%=\n"
-            "v_mov_b32 %[a0], %[Lw2]\n"
-            "v_mov_b32 %[voff], 2\n"
-            "s_mov_b64 exec, 1\n"
-            "ds_write_b32 %[a0], %[voff]\n"
-            "s_mov_b64 exec, -1\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "s_barrier\n"
-            "s_mov_b32 %[split], 0\n"
-            "L_nosync2%=:\n"
-            "s_bfe_u32 %[z], %[d1], 0x80000\n"
-            "s_lshl_b32 %[x], %[z], 3\n"
-            "s_lshl_b32 %[tlo], 9, %[x]\n"
-            "s_cmp_gt_u32 %[z], 3\n"
-            "s_cselect_b32 %[tlo], %[cth], %[tlo]\n"
-            "s_pack_ll_b32_b16 %[pkb], %[beg], %[beg]\n"
-            "s_pack_ll_b32_b16 %[pke], %[end], %[end]\n"
-            "s_bfe_u32 %[x], %[cb0], 0xf0001\n"
-            "v_add_u32 %[M], %[x], %[vlane]\n"
-            "v_mad_u32_u24 %[H0], %[M], %[c20002], %[v10000]\n"
-            "v_add_u32 %[Ga], %[Lq], %[M]\n"
-            "ds_read_u8 %[S], %[Ga]\n"
-            "v_and_b32 %[iw], 127, %[M]\n"
-            "v_lshl_add_u32 %[a0], %[iw], 2, %[pwb]\n"
-            "ds_read_b32 %[E1], %[a0]\n"
-            "ds_read_b32 %[X1], %[a0] offset:512\n"
-            "ds_read_b32 %[X2], %[a0] offset:1024\n"
-            "v_add_u32 %[Gb], -1, %[M]\n"
-            "v_and_b32 %[Gb], 127, %[Gb]\n"
-            "v_lshl_add_u32 %[Pa], %[Gb], 2, %[pwb]\n"
-            "ds_read_b32 %[t1], %[Pa]\n"
-            "v_pk_sub_i16 %[m1], %[H0], %[pkb]\n"
-            "v_pk_sub_i16 %[m2], %[pke], %[H0]\n"
-            "v_or_b32 %[m1], %[m1], %[m2]\n"
-            "v_pk_ashrrev_i16 %[inv], 15, %[m1] op_sel_hi:[0,1]\n"
-            "s_waitcnt lgkmcnt(4)\n"
-            "v_mul_u32_u24 %[S], 0x1001, %[S]\n"
-            "v_and_or_b32 %[S], %[S], %[cq], %[v0c0c]\n"
-            "v_perm_b32 %[S], 4, %[tlo], %[S]\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "v_alignbit_b32 %[Hd], %[E1], %[t1], 16\n"
-            "s_pack_ll_b32_b16 %[x], %[pb], %[pb]\n"
-            "s_pack_ll_b32_b16 %[y], %[pe], %[pe]\n"
-            "v_pk_add_u16 %[t1], %[H0], -1\n"
-            "v_pk_sub_i16 %[m1], %[t1], %[x]\n"
-            "v_pk_sub_i16 %[m2], %[y], %[t1]\n"
-            "v_or_b32 %[m1], %[m1], %[m2]\n"
-            "v_pk_ashrrev_i16 %[m1], 15, %[m1] op_sel_hi:[0,1]\n"
-            "v_pk_sub_i16 %[m2], %[H0], %[x]\n"
-            "v_pk_sub_i16 %[t1], %[y], %[H0]\n"
-            "v_or_b32 %[m2], %[m2], %[t1]\n"
-            "v_pk_ashrrev_i16 %[m2], 15, %[m2] op_sel_hi:[0,1]\n"
-            "v_bfi_b32 %[Hd], %[m1], %[vkneg], %[Hd]\n"
-            "v_bfi_b32 %[X1], %[m2], %[vkneg], %[X1]\n"
-            "v_bfi_b32 %[X2], %[m2], %[vkneg], %[X2]\n"
-            "v_lshl_add_u32 %[a0], %[iw], 2, %[base1]\n"
-            "ds_read_b32 %[E1], %[a0]\n"
-            "ds_read_b32 %[P1], %[a0] offset:512\n"
-            "ds_read_b32 %[P2], %[a0] offset:1024\n"
-            "v_lshl_add_u32 %[Pa], %[Gb], 2, %[base1]\n"
-            "ds_read_b32 %[t1], %[Pa]\n"
-            "s_waitcnt lgkmcnt(0)\n"
-            "v_alignbit_b32 %[F1], %[E1], %[t1], 16\n"
-            "s_pack_ll_b32_b16 %[x], %[rb1], %[rb1]\n"
-            "s_pack_ll_b32_b16 %[y], %[re1], %[re1]\n"
-            "v_pk_add_u16 %[t1], %[H0], -1\n"
-            "v_pk_sub_i16 %[m1], %[t1], %[x]\n"
-            "v_pk_sub_i16 %[m2], %[y], %[t1]\n"
-            "v_or_b32 %[m1], %[m1], %[m2]\n"
-            "v_pk_ashrrev_i16 %[m1], 15, %[m1] op_sel_hi:[0,1]\n"
-            "v_pk_sub_i16 %[m2], %[H0], %[x]\n"
-            "v_pk_sub_i16 %[t1], %[y], %[H0]\n"
-            "v_or_b32 %[m2], %[m2], %[t1]\n"
-            "v_pk_ashrrev_i16 %[m2], 15, %[m2] op_sel_hi:[0,1]\n"
-            "v_bfi_b32 %[F1], %[m1], %[vkneg], %[F1]\n"
-            "v_bfi_b32 %[P1], %[m2], %[vkneg], %[P1]\n"
-            "v_bfi_b32 %[P2], %[m2], %[vkneg], %[P2]\n"
-            "v_pk_sub_i16 %[MK], %[Hd], %[F1] clamp\n"
-            "v_pk_lshrrev_b16 %[MK], 15, %[MK] op_sel_hi:[0,1]\n"
-            "v_pk_sub_i16 %[K1], %[X1], %[P1] clamp\n"
-            "v_pk_lshrrev_b16 %[K1], 15, %[K1] op_sel_hi:[0,1]\n"
-            "v_pk_sub_i16 %[K2], %[X2], %[P2] clamp\n"
-            "v_pk_lshrrev_b16 %[K2], 15, %[K2] op_sel_hi:[0,1]\n"
-            "v_pk_max_i16 %[Hd], %[Hd], %[F1]\n"
-            "v_pk_max_i16 %[X1], %[X1], %[P1]\n"
-            "v_pk_max_i16 %[X2], %[X2], %[P2]\n"
-            "v_pk_add_i16 %[M], %[Hd], %[S] clamp\n"
-            "v_pk_add_i16 %[M], %[M], -4 op_sel_hi:[1,0] clamp\n"
-            "v_pk_max_i16 %[t1], %[X1], %[X2]\n"
-            "v_pk_max_i16 %[t1], %[M], %[t1]\n"
-            "v_bfi_b32 %[H0], %[inv], %[vkneg], %[t1]\n"
-            "v_pk_add_i16 %[G1], %[H0], %[LJ1] clamp\n"
-            "v_pk_add_i16 %[G2], %[H0], %[LJ2] clamp\n"
-            "v_perm_b32 %[Ga], %[G2], %[G1], %[csel0]\n"
-            "v_perm_b32 %[Gb], %[G2], %[G1], %[csel1]\n"
-            "v_pk_max_i16 %[inc], %[Ga], %[Gb]\n"
-            "v_xor_b32 %[inc], 0x80008000, %[inc]\n"
-            "v_mad_i32_i16 %[amk], %[H0], %[c128], %[clo]\n"
-            "v_mad_i32_i16 %[t1], %[H0], %[c128], %[chi] op_sel:[1,0,0,0]\n"
-            "v_max_i32 %[amk], %[amk], %[t1]\n"
-            "s_nop 1\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:1 row_mask:0xf bank_mask:0xf\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "s_nop 0\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:2 row_mask:0xf bank_mask:0xf\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:4 row_mask:0xf bank_mask:0xf\n"
-            "s_nop 0\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "s_nop 0\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_shr:8 row_mask:0xf bank_mask:0xf\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-            "s_nop 0\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "v_max_i32_dpp %[amk], %[amk], %[amk] row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-            "s_nop 0\n"
-            "v_mov_b32_dpp %[t1], %[inc] row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-            "v_pk_max_u16 %[inc], %[inc], %[t1]\n"
-            "s_nop 1\n"
-            "v_readlane_b32 %[mp], %[amk], 63\n"
-            "v_xor_b32_dpp %[Pa], %[inc], %[vkneg] wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-            "v_pk_max_i16 %[Pb], %[Pa], %[Ga]\n"
-            "v_perm_b32 %[P1], %[Pb], %[Pa], %[csel0]\n"
-            "v_perm_b32 %[P2], %[Pb], %[Pa], %[csel1]\n"
-            "v_pk_sub_i16 %[F1], %[P1], %[FJ1] clamp\n"
-            "v_pk_sub_i16 %[S], %[P2], %[FJ2] clamp\n"
-            "v_pk_max_i16 %[H], %[F1], %[S]\n"
-            "v_pk_max_i16 %[H], %[H0], %[H]\n"
-            "v_pk_add_i16 %[X1e], %[X1], -2 op_sel_hi:[1,0] clamp\n"
-            "v_pk_add_i16 %[Ho1], %[H], -6 op_sel_hi:[1,0] clamp\n"
-            "v_pk_add_i16 %[X2e], %[X2], -1 clamp\n"
-            "v_pk_sub_i16 %[Ho2], %[H], 25 op_sel_hi:[1,0] clamp\n"
-            "v_pk_max_i16 %[E1], %[X1e], %[Ho1]\n"
-            "v_pk_max_i16 %[E2], %[X2e], %[Ho2]\n"
-            "v_pk_sub_i16 %[Ga], %[M], %[H] clamp\n"
-            "v_pk_sub_i16 %[Gb], %[X1], %[H] clamp\n"
-            "v_perm_b32 %[Pa], %[Gb], %[Ga], %[cseltb]\n"
-            "v_pk_sub_i16 %[Ga], %[X2], %[H] clamp\n"
-            "v_pk_sub_i16 %[Gb], %[F1], %[H] clamp\n"
-            "v_perm_b32 %[Pb], %[Gb], %[Ga], %[cseltb]\n"
-            "v_pk_sub_i16 %[Ga], %[Ho1], %[X1e] clamp\n"
-            "v_pk_sub_i16 %[Gb], %[Ho2], %[X2e] clamp\n"
-            "v_perm_b32 %[inc], %[Gb], %[Ga], %[cseltb]\n"
-            "v_pk_sub_i16 %[Ga], %[G1], %[P1] clamp\n"
-            "v_pk_sub_i16 %[Gb], %[G2], %[P2] clamp\n"
-            "v_perm_b32 %[amk], %[Gb], %[Ga], %[cseltb]\n"
-            "v_and_b32 %[amk], %[m67], %[amk]\n"
-            "v_and_or_b32 %[amk], %[inc], %[m45], %[amk]\n"
-            "v_and_or_b32 %[amk], %[Pb], %[m23], %[amk]\n"
-            "v_and_or_b32 %[amk], %[Pa], %[m01], %[amk]\n"
-            "v_or_b32_sdwa %[amk], %[amk], %[amk] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
-            "v_add_u32 %[voff], %[tbu], %[vlane2]\n"
-            "global_store_short %[voff], %[amk], %[tbp]\n"
-            "v_lshlrev_b32 %[K1], 2, %[K1]\n"
-            "v_lshlrev_b32 %[K2], 4, %[K2]\n"
-            "v_or3_b32 %[MK], %[MK], %[K1], %[K2]\n"
-            "v_perm_b32 %[MK], 0, %[MK], %[cselkp]\n"
-            "v_add_u32 %[voff], %[kpu], %[vlane2]\n"
-            "global_store_short %[voff], %[MK], %[kpp]\n"
-            "v_bfi_b32 %[Hd], %[inv], %[vkneg], %[H]\n"
-            "v_bfi_b32 %[m1], %[inv], %[vkneg], %[E1]\n"
-            "v_bfi_b32 %[m2], %[inv], %[vkneg], %[E2]\n"
-            "s_add_u32 %[r], %[b0], %[i]\n"
-            "s_and_b32 %[y], %[r], 7\n"
-            "s_mulk_i32 %[y], 0x600\n"
-            "s_add_u32 %[y], %[y], %[Lring]\n"
-            "v_lshl_add_u32 %[a0], %[iw], 2, %[y]\n"
-            "ds_write_b32 %[a0], %[Hd]\n"
-            "ds_write_b32 %[a0], %[m1] offset:512\n"
-            "ds_write_b32 %[a0], %[m2] offset:1024\n"
-            "v_pk_add_u16 %[t1], %[Hd], %[cr16] op_sel_hi:[1,0]\n"
-            "v_pk_min_u16 %[r16], %[r16], %[t1]\n"
-            "s_and_b32 %[x], %[mp], 0x7f\n"
-            "s_sub_i32 %[besti], %[cb0], %[x]\n"
-            "s_addk_i32 %[besti], 0x7f\n"
-            "s_bitcmp1_b32 %[d1], 8\n"
-            "s_cbranch_scc1 L_far2%=\n"
-            "s_sub_i32 %[x], %[tbu], %[cb0]\n"
-            "s_sub_i32 %[z], %[kpu], %[cb0]\n"
-            "v_mov_b32 v120, %[beg]\n"
-            "v_mov_b32 v121, %[end]\n"
-            "v_mov_b32 v122, %[x]\n"
-            "v_mov_b32 v123, %[z]\n"
-            "v_mov_b32 v124, %[besti]\n"
-            "s_and_b32 %[x], %[r], 31\n"
-            "s_lshl_b32 %[x], %[x], 4\n"
-            "s_add_u32 %[x], %[x], %[Lrrow]\n"
-            "v_mov_b32 %[a0], %[x]\n"
-            "s_lshl_b32 %[x], %[r], 5\n"
-            "v_mov_b32 %[voff], %[x]\n"
-            "v_mov_b32 v125, -1\n"
-            "s_mov_b64 exec, 1\n"
-            "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
-            "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
-            "s_mov_b64 exec, -1\n"
-            "s_sub_i32 %[x], %[end], %[beg]\n"
-            "s_add_i32 %[cel], %[cel], %[x]\n"
-            "s_add_i32 %[x], %[spm], 4\n"
-            "s_and_b32 %[x], %[x], -4\n"
-            "s_add_i32 %[tbu], %[tbu], %[x]\n"
-            "s_add_i32 %[kpu], %[kpu], %[x]\n"
-            "s_mov_b32 %[pr], %[r]\n"
-            "s_mov_b32 %[pb], %[beg]\n"
-            "s_mov_b32 %[pe], %[end]\n"
-            "s_mov_b32 %[pa], %[besti]\n"
-            "s_mov_b32 %[pwb], %[y]\n"
-            "s_add_i32 %[i], %[i], 1\n"
-            "s_branch L_top%=\n"
-            "L_far2%=:\n"
-            "s_lshl_b32 %[x], %[svu], 2\n"
-            "v_add_u32 %[voff], %[x], %[vlane8]\n"
-            "v_bfe_i32 v120, %[H], 0, 16\n"
-            "v_ashrrev_i32 v121, 16, %[H]\n"
-            "v_bfe_i32 v122, %[E1], 0, 16\n"
-            "v_ashrrev_i32 v123, 16, %[E1]\n"
-            "v_bfe_i32 v124, %[E2], 0, 16\n"
-            "v_ashrrev_i32 v125, 16, %[E2]\n"
-            "global_store_dwordx2 %[voff], v[120:121], %[svp]\n"
-            "global_store_dwordx2 %[voff], v[122:123], %[svp] offset:512\n"
-            "global_store_dwordx2 %[voff], v[124:125], %[svp] offset:1024\n"
-            "s_sub_i32 %[x], %[tbu], %[cb0]\n"
-            "s_sub_i32 %[z], %[kpu], %[cb0]\n"
-            "v_mov_b32 v120, %[beg]\n"
-            "v_mov_b32 v121, %[end]\n"
-            "v_mov_b32 v122, %[x]\n"
-            "v_mov_b32 v123, %[z]\n"
-            "v_mov_b32 v124, %[besti]\n"
-            "s_and_b32 %[x], %[r], 31\n"
-            "s_lshl_b32 %[x], %[x], 4\n"
-            "s_add_u32 %[x], %[x], %[Lrrow]\n"
-            "v_mov_b32 %[a0], %[x]\n"
-            "s_lshl_b32 %[x], %[r], 5\n"
-            "v_mov_b32 %[voff], %[x]\n"
-            "v_mov_b32 v125, %[svu]\n"
-            "s_mov_b64 exec, 1\n"
-            "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
-            "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
-            "global_store_dwordx2 %[voff], v[124:125], %[rip] offset:16\n"
-            "s_addk_i32 %[svu], 0x180\n"
-            "s_mov_b64 exec, -1\n"
-            "s_sub_i32 %[x], %[end], %[beg]\n"
-            "s_add_i32 %[cel], %[cel], %[x]\n"
-            "s_add_i32 %[x], %[spm], 4\n"
-            "s_and_b32 %[x], %[x], -4\n"
-            "s_add_i32 %[tbu], %[tbu], %[x]\n"
-            "s_add_i32 %[kpu], %[kpu], %[x]\n"
-            "s_mov_b32 %[pr], %[r]\n"
-            "s_mov_b32 %[pb], %[beg]\n"
-            "s_mov_b32 %[pe], %[end]\n"
-            "s_mov_b32 %[pa], %[besti]\n"
-            "s_mov_b32 %[pwb], %[y]\n"
-            "s_add_i32 %[i], %[i], 1\n"
-            "s_branch L_top%=\n"
-            "L_out%=:\n"
-            "s_sub_i32 %[x], %[i], %[i0]\n"
-            "s_add_i32 %[cel], %[cel], %[x]\n"
-            "s_nop 1\n"
-            MANDO_FR_OPERANDS);
     }
     prv_r = pr;
     prv_beg = pb;
@@ -3544,12 +2893,11 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         auto rows = [&](auto capchk) -> int {
         constexpr bool CAP = decltype(capchk)::value;
     for (int i = i0; i < iend; ++i) {
-        if constexpr (((RW == kChunk && NW == 1) || RW == kWideRing) && !CAP &&
-                      std::is_same<SC, DefaultScores>::value) {
+        if constexpr (RW == kChunk && NW == 1 && !CAP && std::is_same<SC, DefaultScores>::value) {
             // the one-chunk fast rows with one or two predecessors in the ring, hand-scheduled (~90 % of a
-            // narrow launch's rows; a wide launch's one-chunk rows, on wave 0 alone)
-            const int j = fast_rows_asm<RW, NW>(sh, lane, tb, kp, sv, rinfo, b0, i, iend, qlen, w, prv_r, prv_beg,
-                                                prv_end, prv_am, ds, split);
+            // narrow launch's rows)
+            const int j = fast_rows_asm(sh, lane, tb, kp, sv, rinfo, b0, i, iend, qlen, w, prv_r, prv_beg, prv_end,
+                                        prv_am, ds);
             if (j != i) {
                 nfast += j - i;
                 i = j;

@@ -624,7 +624,7 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
             # go back to their pools, so a many-chunk run holds only the chunks in flight
             pl, res = poa_fut.result()
             tw = time.perf_counter()
-            n = _write_payload(pl, fa, None, counter0)
+            n = _write_payload(pl, fa, None, counter0, threads)
             timeline.append(("write", tw - t0, time.perf_counter() - t0))
             r2_fut.result()
             del pl
@@ -633,7 +633,7 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
 
         def write_r2i(res, ix, counter0):
             tw = time.perf_counter()
-            _write_payload(_names_payload(res, mine_a[ix]), None, r2, counter0)
+            _write_payload(_names_payload(res, mine_a[ix]), None, r2, counter0, threads)
             timeline.append(("write_r2i", tw - t0, time.perf_counter() - t0))
         def close_outputs():
             if fa is not None:
@@ -667,7 +667,7 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
                 # every chunk is clustered: number this rank's isoforms and place its reads2isoforms.txt
                 # blocks (writer thread) while the POA runs
                 place_fut = writer.submit(_place_r2i, [names_parts[k] for k in range(len(parts))], comm,
-                                          len(roots), out_path, timeline, t0)
+                                          len(roots), out_path, timeline, t0, threads)
         except BaseException:
             close_outputs()
             _close_all(cl, poa_futs)
@@ -704,7 +704,7 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
         cons = _merge_cons(payloads)
         timeline.append(("merge", tm - t0, time.perf_counter() - t0))
         tw = time.perf_counter()
-        stats["written_isoforms"] = _place_fasta(cons, place_fut.result(), comm, len(roots), out_path)
+        stats["written_isoforms"] = _place_fasta(cons, place_fut.result(), comm, len(roots), out_path, threads)
         timeline.append(("write", tw - t0, time.perf_counter() - t0))
         del cons
     elif not stream_out:
@@ -717,7 +717,7 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
             tw = time.perf_counter()
             with open(out_path + "/Isoform_Consensi.fasta", "wb") as fa, \
                     open(out_path + "/reads2isoforms.txt", "wb") as r2:
-                stats["written_isoforms"] = _write_payload(payload, fa, r2, 0)
+                stats["written_isoforms"] = _write_payload(payload, fa, r2, 0, threads)
             timeline.append(("write", tw - t0, time.perf_counter() - t0))
         del payload
     stats["t_total"] = time.perf_counter() - t0
@@ -780,7 +780,7 @@ def _close_all(cluster_futs, poa_futs) -> None:
             res.close()
 
 
-def _write_payload(payload: dict, fa, r2, counter0: int) -> int:
+def _write_payload(payload: dict, fa, r2, counter0: int, threads: int = 0) -> int:
     """Appends a payload's isoforms to both files in output order (sorted roots x IsoDict order,
     defineIsoforms.py:155-166), numbering from counter0 + 1; returns the isoform count.  fa or r2 None:
     that file is skipped (reads2isoforms needs only the clustering, so one rank writes it ahead).  The
@@ -791,7 +791,7 @@ def _write_payload(payload: dict, fa, r2, counter0: int) -> int:
         cons = (payload["cons_src"], payload["c_sel"], payload["c_start"], payload["c_len"], payload["c_rc"])
     if r2 is not None:
         names = (payload["name_src"], payload["n_sel"], payload["n_start"], payload["n_len"])
-    fasta, r2i = _lib.format_outputs(order, payload["mem_off"], counter0, cons, names)
+    fasta, r2i = _lib.format_outputs(order, payload["mem_off"], counter0, cons, names, threads=threads)
     if fa is not None:
         _write_big(fa, fasta)
     if r2 is not None:
@@ -920,21 +920,23 @@ def _exchange_per_root(comm, n_roots: int, roots: np.ndarray, *vals: np.ndarray)
 
 
 def _place(path: str, buf: np.ndarray, src: np.ndarray, roots: np.ndarray, sizes: np.ndarray,
-           g_sizes: np.ndarray) -> None:
+           g_sizes: np.ndarray, threads: int = 0) -> None:
     """Writes this rank's per-root blocks of buf at their offsets in the shared file (its size the total
     of every rank's blocks: each rank sets it, and the blocks of all ranks tile it, so no rank truncates
-    another's bytes and no stale byte survives)."""
+    another's bytes and no stale byte survives).  threads: the rank's host-thread budget (N ranks share
+    the node's cores; 0 lets the library take its default)."""
     goff = np.zeros(len(g_sizes) + 1, np.int64)
     np.cumsum(g_sizes, out=goff[1:])
     fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o644)  # read-write: mando_write_blocks maps the file
     try:
         os.ftruncate(fd, int(goff[-1]))
-        _lib.write_blocks(fd, buf, src, goff[roots], sizes)
+        _lib.write_blocks(fd, buf, src, goff[roots], sizes, threads=threads)
     finally:
         os.close(fd)
 
 
-def _place_r2i(parts: list, comm, n_roots: int, out_path: str, timeline: list, t0: float) -> tuple:
+def _place_r2i(parts: list, comm, n_roots: int, out_path: str, timeline: list, t0: float,
+               threads: int = 0) -> tuple:
     """Placement reassembly, clustering half (defineIsoforms.py:155-166 numbers isoforms in sorted-root
     order across all loci): the ranks exchange per-root isoform counts, number their own isoforms from
     them and place their reads2isoforms.txt blocks.  Returns what the FASTA half needs."""
@@ -955,22 +957,22 @@ def _place_r2i(parts: list, comm, n_roots: int, out_path: str, timeline: list, t
     kbase = np.zeros(n_roots + 1, np.int64)
     np.cumsum(g_cnt, out=kbase[1:])
     k = kbase[rs] + 1 + (np.arange(len(rs), dtype=np.int64) - np.repeat(first, cnt))
-    _, r2i, _, ro = _lib.format_outputs(order, mem_off, 0, None, names, iso_k=k, offsets=True)
+    _, r2i, _, ro = _lib.format_outputs(order, mem_off, 0, None, names, threads=threads, iso_k=k, offsets=True)
     sz = ro[first + cnt] - ro[first]
     g_sz, = _exchange_per_root(comm, n_roots, ur, sz)
-    _place(out_path + "/reads2isoforms.txt", r2i, ro[first], ur, sz, g_sz)
+    _place(out_path + "/reads2isoforms.txt", r2i, ro[first], ur, sz, g_sz, threads)
     timeline.append(("write_r2i", tw - t0, time.perf_counter() - t0))
     return order, mem_off, k, ur, first, cnt
 
 
-def _place_fasta(cons: tuple, numbered: tuple, comm, n_roots: int, out_path: str) -> int:
+def _place_fasta(cons: tuple, numbered: tuple, comm, n_roots: int, out_path: str, threads: int = 0) -> int:
     """Placement reassembly, POA half: per-root FASTA sizes exchanged, blocks placed, then one barrier
     (every rank's blocks of both files are written when any rank returns)."""
     order, mem_off, k, ur, first, cnt = numbered
-    fasta, _, fo, _ = _lib.format_outputs(order, mem_off, 0, cons, None, iso_k=k, offsets=True)
+    fasta, _, fo, _ = _lib.format_outputs(order, mem_off, 0, cons, None, threads=threads, iso_k=k, offsets=True)
     sz = fo[first + cnt] - fo[first]
     g_sz, = _exchange_per_root(comm, n_roots, ur, sz)
-    _place(out_path + "/Isoform_Consensi.fasta", fasta, fo[first], ur, sz, g_sz)
+    _place(out_path + "/Isoform_Consensi.fasta", fasta, fo[first], ur, sz, g_sz, threads)
     comm.barrier()
     return int(len(order))
 

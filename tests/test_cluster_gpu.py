@@ -124,6 +124,20 @@ def test_sub_batched_calls_equal_the_restatement(tmp_path, monkeypatch, sub):
     assert n_ok == 300
 
 
+def test_mixed_large_and_small_loci(tmp_path):
+    """Loci of >= 2,048 records run on the several-wave kernel (helper waves join wave 0 for the coverage
+    sets and the coverage merge), the others on one wave each, in the same call: both launches (and the
+    order split between them) equal the restatement locus by locus."""
+    d = str(tmp_path)
+    synth.write_loci(os.path.join(d, "big", "tmp_SS"), 3, reads=(2100, 2600), exons=(6, 10), exon_len=(60, 200),
+                     isoforms=(4, 8), threads=8, seed=31, rev_frac=0.3)
+    synth.write_loci(os.path.join(d, "small", "tmp_SS"), 40, reads=(10, 60), threads=8, seed=32, rev_frac=0.3)
+    _, pb, cb, _ = _inputs(os.path.join(d, "big"))
+    _, ps, cs, _ = _inputs(os.path.join(d, "small"))
+    n_ok, _ = _compare(ps[:20] + pb + ps[20:], cs[:20] + cb + cs[20:], seed=4)
+    assert n_ok == len(pb) + len(ps)
+
+
 def _edit_lines(src, dst, fn):
     lines = open(src).read().split("\n")
     if lines and lines[-1] == "":

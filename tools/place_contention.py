@@ -1,35 +1,95 @@
-# Dev tool: 8 processes place ~1 GB of blocks into one file through mando_write_blocks at once, with the
-# roots interleaved (the snake plan), in contiguous ranges, or dealt in blocks of B roots.
-import os, sys, time, numpy as np, multiprocessing as mp
-sys.path.insert(0, "/root/repo")
-from mandalorion_amd import _lib
-N, NB = 8, 200000
-rng = np.random.default_rng(1)
-sizes = rng.integers(2000, 8000, NB).astype(np.int64)   # ~1 GB of FASTA blocks
-off = np.concatenate([[0], np.cumsum(sizes)])
-total = int(off[-1])
-def run(rank, mode, path, q, barrier):
-    if mode == "scatter":
-        idx = np.arange(rank, NB, N)            # interleaved roots (LPT-like)
-    elif mode.startswith("blk"):
-        B = int(mode[3:]); b = np.arange(NB) // B
-        idx = np.nonzero(b % N == rank)[0]
-    else:
-        idx = np.arange(rank * NB // N, (rank + 1) * NB // N)   # contiguous range
-    ln = sizes[idx]; src = np.concatenate([[0], np.cumsum(ln)[:-1]])
-    buf = np.full(int(ln.sum()), 65 + rank, np.uint8)
-    fd = os.open(path, os.O_RDWR)
-    barrier.wait()
+"""Concurrent placement of an N-rank plan's real output blocks, no GPU work.
+
+tools/rank_rehearsal.py with PLACE_DUMP=<dir> saves, for every rank of an N-rank plan, the blocks it
+places into reads2isoforms.txt and Isoform_Consensi.fasta (define._place's arguments: the rank's
+formatted bytes, per-root source offsets, its roots, their sizes and the all-rank size table).  This
+tool places them the way N rank processes on one node do: N processes, each with `threads` host
+threads, a barrier, every rank's reads2isoforms.txt blocks at once, a barrier, every rank's FASTA blocks
+at once (the driver's order: reads2isoforms during the POA, the FASTA after it).  For comparison each
+rank's blocks are also placed alone, one rank after another.  Rounds alternate concurrent / alone, the
+first of each untimed (files created, page cache warm, as in a later bench step).
+
+usage: python tools/place_contention.py <dump dir> <out dir> [threads=2] [rounds=3]
+prints one JSON line: per file, the max over ranks of the concurrent placement and the sum / max of
+the ranks placed alone.
+"""
+from __future__ import annotations
+
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+FILES = ("reads2isoforms.txt", "Isoform_Consensi.fasta")
+
+
+def _load(dump: str, rank: int, f: str):
+    z = np.load(os.path.join(dump, f"r{rank}_{f}.npz"))
+    return {k: z[k] for k in ("buf", "src", "roots", "sizes", "g_sizes")}
+
+
+def _place(out: str, f: str, b: dict, threads: int) -> float:
+    """define._place's work for one rank and file, timed."""
+    from mandalorion_amd import _lib
+
+    goff = np.zeros(len(b["g_sizes"]) + 1, np.int64)
+    np.cumsum(b["g_sizes"], out=goff[1:])
     t = time.perf_counter()
-    _lib.write_blocks(fd, buf, src, off[idx], ln, threads=2)
-    q.put(time.perf_counter() - t)
-    os.close(fd)
-for mode in ("scatter", "contig", "blk256", "blk1024", "blk64", "contig", "blk256"):
-    path = "/tmp/place_test.bin"
-    fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o644); os.ftruncate(fd, total); os.close(fd)
-    q = mp.Queue(); b = mp.Barrier(N)
-    ps = [mp.Process(target=run, args=(r, mode, path, q, b)) for r in range(N)]
-    [p.start() for p in ps]; [p.join() for p in ps]
-    ts = [q.get() for _ in range(N)]
-    print(mode, "max %.3f s" % max(ts), "GB %.2f" % (total / 1e9))
-    os.unlink(path)
+    fd = os.open(os.path.join(out, f), os.O_RDWR | os.O_CREAT, 0o644)
+    try:
+        os.ftruncate(fd, int(goff[-1]))
+        _lib.write_blocks(fd, b["buf"], b["src"], goff[b["roots"]], b["sizes"], threads=threads)
+    finally:
+        os.close(fd)
+    return time.perf_counter() - t
+
+
+def _rank(rank, dump, out, threads, rounds, bar, q):
+    blocks = {f: _load(dump, rank, f) for f in FILES}
+    for _ in range(rounds):
+        ts = {}
+        for f in FILES:
+            bar.wait()
+            ts[f] = _place(out, f, blocks[f], threads)
+        q.put((rank, ts))
+
+
+def main():
+    dump, out = sys.argv[1], sys.argv[2]
+    threads = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    n = 1 + max(int(x[1:].split("_", 1)[0]) for x in os.listdir(dump) if x.startswith("r") and x.endswith(".npz"))
+    os.makedirs(out, exist_ok=True)
+    ctx = mp.get_context("spawn")
+    res = {"ranks": n, "threads_per_rank": threads, "rounds": rounds, "concurrent_s": {f: [] for f in FILES},
+           "alone_sum_s": {f: [] for f in FILES}, "alone_max_s": {f: [] for f in FILES},
+           "bytes": {f: int(_load(dump, 0, f)["g_sizes"].sum()) for f in FILES}}
+    for rd in range(rounds + 1):
+        # concurrent: N processes, barrier per file
+        q, bar = ctx.Queue(), ctx.Barrier(n)
+        ps = [ctx.Process(target=_rank, args=(r, dump, out, threads, 1, bar, q)) for r in range(n)]
+        for p in ps:
+            p.start()
+        got = [q.get(timeout=600) for _ in range(n)]
+        for p in ps:
+            p.join(60)
+            assert p.exitcode == 0
+        # alone: one rank at a time, in this process
+        alone = {f: [_place(out, f, _load(dump, r, f), threads) for r in range(n)] for f in FILES}
+        if rd == 0:
+            continue
+        for f in FILES:
+            res["concurrent_s"][f].append(round(max(ts[f] for _, ts in got), 4))
+            res["alone_sum_s"][f].append(round(sum(alone[f]), 4))
+            res["alone_max_s"][f].append(round(max(alone[f]), 4))
+    res["concurrent_median_s"] = {f: float(np.median(v)) for f, v in res["concurrent_s"].items()}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

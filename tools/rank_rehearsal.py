@@ -14,6 +14,9 @@ estimated RCCL transfer for gather).  Placement: the ranks' FASTA blocks go into
 time in a real run, and buffered writes to one file serialise in the kernel, so the prediction also
 reports the step with every rank's FASTA placement serialised (an upper bound).
 
+With PLACE_DUMP=<dir> a fourth, untimed pass saves each rank's placement blocks there (real sizes and
+offsets of the N-rank plan), for tools/place_contention.py to place from N processes at once.
+
 usage: python tools/rank_rehearsal.py <data dir with tmp_SS> N [threads]
 """
 from __future__ import annotations
@@ -82,15 +85,36 @@ def _span(st, name):
     return sum(b - a for n, a, b in st["timeline"] if n == name)
 
 
+def _dump_place(define, dump: str, cur: list):
+    """Wraps define._place so that the dump pass saves every rank's real blocks (the buffer, per-root
+    source offsets, roots, sizes and the all-rank size table) for tools/place_contention.py."""
+    inner = define._place
+
+    def place(path, buf, src, roots, sizes, g_sizes, threads=0):
+        if cur[0] is not None:
+            np.savez(os.path.join(dump, f"r{cur[0]}_{os.path.basename(path)}.npz"), buf=buf, src=src,
+                     roots=roots, sizes=sizes, g_sizes=g_sizes)
+        return inner(path, buf, src, roots, sizes, g_sizes, threads)
+
+    define._place = place
+
+
 def main_place(d, n, threads, ref, files):
     from mandalorion_amd import define
 
     store: dict = {}
-    out = {"ranks": n, "reassembly": "place", "rank_s": {}, "rank_phases_s": {}}
-    for p in range(3):
+    cur = [None]
+    dump = os.environ.get("PLACE_DUMP")
+    if dump:
+        os.makedirs(dump, exist_ok=True)
+        _dump_place(define, dump, cur)
+    out = {"ranks": n, "reassembly": "place", "threads": threads, "rank_s": {}, "rank_phases_s": {}}
+    for p in range(4 if dump else 3):  # the dump pass comes after the timed one
         for r in range(n):
+            cur[0] = r if p == 3 else None
             t0 = time.perf_counter()
             st = define.define_isoforms(d, threads=threads, comm=_Place(r, n, store))
+            print(f"[rehearsal] pass {p} rank {r}: {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
             if p == 2:
                 out["rank_s"][r] = round(time.perf_counter() - t0, 4)
                 ph = {k: round(st[k], 4) for k in ("t_ingest", "t_cluster", "t_orient", "t_poa", "t_merge", "t_total")}
