@@ -12,6 +12,8 @@ first of each untimed (files created, page cache warm, as in a later bench step)
 usage: python tools/place_contention.py <dump dir> <out dir> [threads=2] [rounds=3]
 prints one JSON line: per file, the max over ranks of the concurrent placement and the sum / max of
 the ranks placed alone.
+       python tools/place_contention.py --ranges <out dir> <ranks> <bytes> [threads=2] [rounds=3]
+the same for a layout where each rank's blocks are one contiguous range (bytes split evenly).
 """
 from __future__ import annotations
 
@@ -59,7 +61,39 @@ def _rank(rank, dump, out, threads, rounds, bar, q):
         q.put((rank, ts))
 
 
+def _range_rank(rank, n, total, out, threads, bar, q):
+    part = total // n
+    b = {"buf": np.full(part, 65 + rank, np.uint8), "src": np.zeros(1, np.int64), "roots": np.array([rank]),
+         "sizes": np.array([part], np.int64), "g_sizes": np.full(n, part, np.int64)}
+    bar.wait()
+    q.put((rank, {"ranges": _place(out, "ranges.bin", b, threads)}))
+
+
+def main_ranges():
+    out, n, total = sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    threads = int(sys.argv[5]) if len(sys.argv) > 5 else 2
+    rounds = int(sys.argv[6]) if len(sys.argv) > 6 else 3
+    os.makedirs(out, exist_ok=True)
+    ctx = mp.get_context("spawn")
+    ts = []
+    for rd in range(rounds + 1):
+        q, bar = ctx.Queue(), ctx.Barrier(n)
+        ps = [ctx.Process(target=_range_rank, args=(r, n, total, out, threads, bar, q)) for r in range(n)]
+        for p in ps:
+            p.start()
+        got = [q.get(timeout=600) for _ in range(n)]
+        for p in ps:
+            p.join(60)
+            assert p.exitcode == 0
+        if rd:
+            ts.append(round(max(t["ranges"] for _, t in got), 4))
+    print(json.dumps({"ranks": n, "threads_per_rank": threads, "bytes": total, "layout": "contiguous range per rank",
+                      "concurrent_s": ts, "concurrent_median_s": float(np.median(ts))}), flush=True)
+
+
 def main():
+    if sys.argv[1] == "--ranges":
+        return main_ranges()
     dump, out = sys.argv[1], sys.argv[2]
     threads = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 3
