@@ -248,6 +248,13 @@ int mando_allgather_bytes(mando_comm *comm, const uint8_t *send, int64_t n, uint
  * NULL on the other ranks): RCCL point-to-point sends to rank 0 between GPUs (xGMI), the TCP star without
  * a device.  The D driver's reassembly (defineIsoforms.py:155-166's writer is rank 0). */
 int mando_gather_bytes(mando_comm *comm, const uint8_t *send, int64_t n, uint8_t *recv, const int64_t *recv_counts);
+/* Personalised exchange: send holds the parts for ranks 0..nranks-1 back to back (send_counts[r] bytes
+ * for rank r), recv receives the parts from ranks 0..nranks-1 back to back (recv_counts[r] bytes from
+ * rank r; every rank must know what it receives, e.g. from an all-gather of the send counts).  RCCL
+ * point-to-point sends / receives in one group; the host transport returns MANDO_E_UNSUPPORTED (callers
+ * all-gather instead).  The D driver's range placement of the output files (defineIsoforms.py:155-166). */
+int mando_alltoallv_bytes(mando_comm *comm, const uint8_t *send, const int64_t *send_counts, uint8_t *recv,
+                          const int64_t *recv_counts);
 /* *v = max over ranks of *v (the benchmark's max-over-ranks wall time) */
 int mando_allreduce_max_f64(mando_comm *comm, double *v);
 int mando_comm_barrier(mando_comm *comm);
@@ -264,6 +271,9 @@ int mando_rccl_allgather_plan(int nranks, const int64_t *recv_counts, int64_t *m
                               int64_t *host_off);
 int mando_rccl_gather_plan(int nranks, int rank, const int64_t *recv_counts, int64_t *peer_off, int64_t *peer_len,
                            int64_t *d2h_off, int64_t *d2h_len);
+/* mando_alltoallv_bytes: the offsets of each rank's part in send and in recv (prefix sums). */
+int mando_rccl_alltoallv_plan(int nranks, const int64_t *send_counts, const int64_t *recv_counts, int64_t *send_off,
+                              int64_t *recv_off);
 
 /* Host helper of the D driver (FASTA / read-group assembly without per-read interpreter work):
  * segment i = src[sel[i]] + starts[i], lens[i] bytes (sel may be NULL: src[0]), reverse-complemented

@@ -52,6 +52,8 @@ EXPORTED = (
     "mando_comm_destroy",
     "mando_rccl_allgather_plan",
     "mando_rccl_gather_plan",
+    "mando_rccl_alltoallv_plan",
+    "mando_alltoallv_bytes",
     "mando_pack_segments",
     "mando_format_outputs",
     "mando_write_blocks",
@@ -243,6 +245,9 @@ def load(path: str | None = None):
         if hasattr(lib, "mando_rccl_gather_plan"):  # (dev A/B builds of older trees lack them)
             lib.mando_rccl_allgather_plan.argtypes = [ctypes.c_int, _P, _P, _P, _P]
             lib.mando_rccl_gather_plan.argtypes = [ctypes.c_int, ctypes.c_int, _P, _P, _P, _P, _P]
+        if hasattr(lib, "mando_alltoallv_bytes"):
+            lib.mando_rccl_alltoallv_plan.argtypes = [ctypes.c_int, _P, _P, _P, _P]
+            lib.mando_alltoallv_bytes.argtypes = [_P, _P, _P, _P, _P]
         if hasattr(lib, "mando_selftest"):
             lib.mando_selftest.argtypes = [_P, _P]
         if path is None:
@@ -270,18 +275,25 @@ def ptr(a: np.ndarray | None) -> int | None:
 
 
 def pack_segments(srcs: list[np.ndarray], starts: np.ndarray, lens: np.ndarray, sel: np.ndarray | None = None,
-                  rc: np.ndarray | None = None, threads: int = 0) -> tuple[np.ndarray, np.ndarray]:
+                  rc: np.ndarray | None = None, threads: int = 0, out: np.ndarray | None = None,
+                  out_off: np.ndarray | None = None) -> tuple[np.ndarray, np.ndarray]:
     """Concatenate byte segments of the uint8 arrays in srcs (see mando_pack_segments); returns
-    (bytes uint8 array, offsets int64 with n+1 entries)."""
+    (bytes uint8 array, offsets int64 with n+1 entries).  With out / out_off: segment i goes to
+    out[out_off[i]:] instead (a scatter; out is returned as is)."""
     lib = load()
     n = int(len(starts))
     lens = np.ascontiguousarray(lens, dtype=np.int64)
-    off = np.zeros(n + 1, dtype=np.int64)
-    if n:
-        np.cumsum(lens, out=off[1:])
-    out = np.empty(max(int(off[-1]), 1), dtype=np.uint8)
+    if out is not None:
+        off = np.ascontiguousarray(out_off, dtype=np.int64)
+        if len(off) != n or (n and int((off + lens).max()) > out.size) or (n and int(off.min()) < 0):
+            raise ValueError("pack_segments: a segment falls outside out")
+    else:
+        off = np.zeros(n + 1, dtype=np.int64)
+        if n:
+            np.cumsum(lens, out=off[1:])
+        out = np.empty(max(int(off[-1]), 1), dtype=np.uint8)
     if n == 0:
-        return out[:0], off
+        return (out if out_off is not None else out[:0]), off
     if len(srcs) > 127:
         raise ValueError("pack_segments: at most 127 sources (int8 selectors)")
     keep = [np.ascontiguousarray(s, dtype=np.uint8) for s in srcs]
@@ -290,6 +302,8 @@ def pack_segments(srcs: list[np.ndarray], starts: np.ndarray, lens: np.ndarray, 
     sel_a = None if sel is None else np.ascontiguousarray(sel, dtype=np.int8)
     rc_a = None if rc is None else np.ascontiguousarray(rc, dtype=np.int8)
     check(lib.mando_pack_segments(ptrs, ptr(sel_a), ptr(starts), ptr(lens), ptr(rc_a), n, ptr(out), ptr(off), threads))
+    if out_off is not None:
+        return out, off
     return out[:int(off[-1])], off
 
 

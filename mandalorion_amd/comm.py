@@ -74,6 +74,33 @@ class Comm:
                                                _lib.ptr(counts)))
         return (out[:int(counts.sum())] if out is not None else None), counts
 
+    def alltoallv(self, parts: list) -> list:
+        """Personalised exchange: parts[r] (uint8) goes to rank r; returns, by rank, what every rank sent
+        to this one.  The send counts are all-gathered first (each rank learns what it receives); the bytes
+        go over RCCL point-to-point (mando_alltoallv_bytes), or over the host transport as one all-gather
+        of every rank's parts of which each rank keeps its own."""
+        parts = [np.ascontiguousarray(p, dtype=np.uint8).ravel() for p in parts]
+        if len(parts) != self.world:
+            raise ValueError("alltoallv: one part per rank")
+        sc = np.array([p.size for p in parts], dtype=np.int64)
+        allc, _ = self.allgather_bytes(sc.view(np.uint8))
+        mat = allc.view(np.int64).reshape(self.world, self.world)
+        rc = np.ascontiguousarray(mat[:, self.rank])
+        roff = np.concatenate([[0], np.cumsum(rc)])
+        send = np.concatenate(parts) if sc.sum() else np.zeros(1, dtype=np.uint8)
+        if self.backend == "rccl" or self.world == 1:
+            recv = np.empty(max(int(rc.sum()), 1), dtype=np.uint8)
+            _lib.check(self.lib.mando_alltoallv_bytes(self.handle, _lib.ptr(send), _lib.ptr(sc), _lib.ptr(recv),
+                                                      _lib.ptr(rc)))
+            return [recv[roff[r]:roff[r + 1]] for r in range(self.world)]
+        allb, cnt = self.allgather_bytes(send[:int(sc.sum())])
+        base = np.concatenate([[0], np.cumsum(cnt)])
+        out = []
+        for r in range(self.world):
+            a = int(base[r] + mat[r, :self.rank].sum())
+            out.append(allb[a:a + int(mat[r, self.rank])])
+        return out
+
     def max(self, v: float) -> float:
         x = ctypes.c_double(float(v))
         _lib.check(self.lib.mando_allreduce_max_f64(self.handle, ctypes.byref(x)))

@@ -806,6 +806,18 @@ __host__ __device__ inline int32_t peak_cap_of(const Stats &S, const Locus &L) {
     return S.n_hist_l + S.n_hist_r + n_ann_of(L) + 8;
 }
 
+// Large loci (>= kMwMinRecs records: config 2's SIRV-sized loci) run on a workgroup of kMwWaves waves.
+// Wave 0 runs the locus exactly as the one-wave kernel does; the helper waves wait in
+// LocusRun::helper() and join it for the data-parallel phases (coverage sets, the coverage merge),
+// each wave taking a contiguous share of the records / winners.  MwX is their LDS exchange: the phase
+// and its arguments, and per-wave partials in two banks that alternate between exchanges (a wave that
+// runs ahead cannot overwrite a partial another wave has yet to read).
+constexpr int kMwWaves = 8;
+constexpr int kMwMinRecs = 2048;
+constexpr int kOpExit = 0, kOpCovSets = 1, kOpDetCov = 2, kOpCountSort = 3, kOpKeys = 4;
+// waves of a locus's K2 workgroup (the host splits the launch on the same rule)
+__host__ __device__ inline int mw_waves(const Stats &S) { return S.n_rec >= kMwMinRecs ? kMwWaves : 1; }
+
 __host__ __device__ inline void carve_b(uint8_t *base, const Stats &S, const Locus &L, int w, BPtr &B) {
     int64_t off = 0;
     auto take = [&](int64_t bytes) -> uint8_t * {
@@ -842,7 +854,7 @@ __host__ __device__ inline void carve_b(uint8_t *base, const Stats &S, const Loc
     B.areas[0] = take(L.map_n);
     B.areas[1] = take(L.map_n);
     B.splice = (int32_t *)take(L.map_n * 4);
-    B.sc = (int32_t *)take(L.map_n * 4);
+    B.sc = (int32_t *)take(L.map_n * 4 * mw_waves(S));  // several waves: one count column per wave
     B.ec = (int32_t *)take(L.map_n * 4);
     B.sp = (int32_t *)take(L.map_n * 4);
     B.ep = (int32_t *)take(L.map_n * 4);
@@ -1188,15 +1200,6 @@ __device__ double round3(int64_t best, int64_t cov) {
 // ---------------------------------------------------------------------------------------------
 constexpr int kLdsPerm = 4096;
 
-// Large loci (>= kMwMinRecs records: config 2's SIRV-sized loci) run on a workgroup of kMwWaves waves.
-// Wave 0 runs the locus exactly as the one-wave kernel does; the helper waves wait in
-// LocusRun::helper() and join it for the data-parallel phases (coverage sets, the coverage merge),
-// each wave taking a contiguous share of the records / winners.  MwX is their LDS exchange: the phase
-// and its arguments, and per-wave partials in two banks that alternate between exchanges (a wave that
-// runs ahead cannot overwrite a partial another wave has yet to read).
-constexpr int kMwWaves = 8;
-constexpr int kMwMinRecs = 2048;
-constexpr int kOpExit = 0, kOpCovSets = 1, kOpDetCov = 2;
 struct MwX {
     int32_t op;
     int32_t i32[4];
@@ -1269,6 +1272,10 @@ struct LocusRun {
             cov_sets(w, nw);
         else if (op == kOpDetCov)
             det_cov(w, nw);
+        else if (op == kOpCountSort)
+            count_sort_part(X->i32[0], w, nw);
+        else if (op == kOpKeys)
+            keys_part(X->i32[0], w, nw);
     }
     // the helper waves: phases until wave 0 posts kOpExit
     __device__ void helper() {
@@ -1297,6 +1304,23 @@ struct LocusRun {
         }
         a = sa;
         b = sb;
+        ph ^= 1;
+    }
+    // exclusive prefix over the waves of v (excl: the waves before w) and the total
+    __device__ void xprefix(int &ph, int w, int nw, int64_t v, int64_t &excl, int64_t &total) {
+        if (nw == 1) {
+            excl = 0;
+            total = v;
+            return;
+        }
+        if (ln() == 0) X->part[ph][w][0] = v;
+        gsync();
+        excl = total = 0;
+        for (int u = 0; u < nw; ++u) {
+            const int64_t t = X->part[ph][u][0];
+            total += t;
+            if (u < w) excl += t;
+        }
         ph ^= 1;
     }
 
@@ -1384,7 +1408,7 @@ struct LocusRun {
         const uint64_t tc2 = clock64();
         pc_bins = tc2 - tc1;
 #endif
-        for (int k = 0; k < 2; ++k) build_side(B.s[k]);
+        for (int k = 0; k < 2; ++k) build_side(k);
 #ifdef MANDO_CL_PHASES
         pc_side = clock64() - tc2;
 #endif
@@ -1587,36 +1611,74 @@ struct LocusRun {
     // map position in B.sc (zero outside start_end_sites), an exclusive scan over the map, then the
     // entries placed in rank order, ties inside a step ranked by lane.  Returns false (nothing
     // changed) when a position falls outside the map.
-    __device__ bool count_sort_side(Side &d) {
+    // Over nw waves: wave w takes the entries [H*w/nw, H*(w+1)/nw) and counts them in its own column
+    // of B.sc (column v of position x at B.sc[x * nw + v]); the scan turns a position's columns into
+    // the waves' cursors (the position's start, then the entries of the waves before), so each wave
+    // places its entries in insertion order exactly where one wave would.
+    __device__ bool count_sort_part(int side_i, int w, int nw) {
+        Side &d = B.s[side_i];
         const int H = d.H;
         int32_t *C = B.sc;
+        const int e_lo = (int)((int64_t)H * w / nw), e_hi = (int)((int64_t)H * (w + 1) / nw);
         int oob = 0;
-        for (int i0 = 0; i0 < H; i0 += 64) {
+        for (int i0 = e_lo; i0 < e_hi; i0 += 64) {
             const int i = i0 + ln();
-            if (i < H) {
+            if (i < e_hi) {
                 const int64_t x = mi((int64_t)(d.sk[i] >> 24) - kPosBias);
                 if (x < 0 || x >= L.map_n)
                     oob = 1;
                 else
-                    atomicAdd(&C[x], 1);
+                    atomicAdd(&C[x * nw + w], 1);
             }
         }
         wsync();
-        const bool bad = wany(oob != 0);
+        int ph = 0;
+        int64_t nbad = wany(oob != 0) ? 1 : 0, unused = 0;
+        xchg(ph, w, nw, nbad, unused, true);
+        const bool bad = nbad != 0;
         if (!bad) {
-            // exclusive scan of the counts (read with agent-scope loads: they were made by L2 atomics)
+            // exclusive scan of the counts over the map (read with agent-scope loads: they were made by
+            // L2 atomics), the map split between the waves: this wave's total first, then its range
+            const int64_t m_lo = L.map_n * w / nw, m_hi = L.map_n * (w + 1) / nw;
+            auto count_at = [&](int64_t x, int v) {
+                return __hip_atomic_load(&C[x * nw + v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
             int64_t carry = 0;
-            for (int64_t x0 = 0; x0 < L.map_n; x0 += 64) {
+            if (nw > 1) {
+                int64_t tot = 0;
+                for (int64_t x0 = m_lo; x0 < m_hi; x0 += 64) {
+                    const int64_t x = x0 + ln();
+                    if (x < m_hi)
+                        for (int v = 0; v < nw; ++v) tot += count_at(x, v);
+                }
+                tot = wsum(tot);
+                if (ln() == 0) X->part[ph][w][0] = tot;
+                gsync();
+                for (int v = 0; v < w; ++v) carry += X->part[ph][v][0];
+                ph ^= 1;
+            }
+            for (int64_t x0 = m_lo; x0 < m_hi; x0 += 64) {
                 const int64_t x = x0 + ln();
-                const int32_t c = x < L.map_n ? __hip_atomic_load(&C[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                int32_t c = 0;
+                if (x < m_hi)
+                    for (int v = 0; v < nw; ++v) c += count_at(x, v);
                 const int32_t ci = wincl(c);
-                if (x < L.map_n && c) C[x] = (int32_t)(carry + ci - c);
+                if (x < m_hi && c) {  // the cursor of each wave's column: the start, then the waves before
+                    int32_t at = (int32_t)(carry + ci - c);
+                    for (int v = 0; v < nw; ++v) {
+                        const int32_t cv = count_at(x, v);
+                        C[x * nw + v] = at;
+                        at += cv;
+                    }
+                }
                 carry += __shfl(ci, 63);
             }
             wsync();
-            for (int i0 = 0; i0 < H; i0 += 64) {
+            if (nw > 1) gsync();
+            // this wave's entries, in insertion order, each at its column's cursor
+            for (int i0 = e_lo; i0 < e_hi; i0 += 64) {
                 const int i = i0 + ln();
-                const bool act = i < H;
+                const bool act = i < e_hi;
                 const uint64_t k = act ? d.sk[i] : ~0ull;
                 const int64_t x = act ? mi((int64_t)(k >> 24) - kPosBias) : -1;
                 int32_t rank = 0, later = 0;
@@ -1627,29 +1689,42 @@ struct LocusRun {
                     later |= (same && t > ln()) ? 1 : 0;
                 }
                 if (act) {
-                    const int32_t dst = C[x] + rank;
+                    const int32_t dst = C[x * nw + w] + rank;
                     d.cand[dst] = k;
-                    if (!later) C[x] = dst + 1;
+                    if (!later) C[x * nw + w] = dst + 1;
                 }
                 wsync();
             }
+            if (nw > 1) gsync();  // every entry placed before any wave clears the counts
             uint64_t *t = d.sk;
             d.sk = d.cand;
             d.cand = t;
         }
         // B.sc back to zero where this side touched it
-        for (int i0 = 0; i0 < H; i0 += 64) {
+        for (int i0 = e_lo; i0 < e_hi; i0 += 64) {
             const int i = i0 + ln();
-            if (i < H) {
+            if (i < e_hi) {
                 const int64_t x = mi((int64_t)(d.sk[i] >> 24) - kPosBias);
-                if (x >= 0 && x < L.map_n) C[x] = 0;
+                if (x >= 0 && x < L.map_n)
+                    for (int v = 0; v < nw; ++v) C[x * nw + v] = 0;
             }
         }
         wsync();
         return !bad;
     }
 
-    __device__ void build_side(Side &d) {
+    // the counting sort of side side_i on every wave of the workgroup; false: a position outside the map
+    __device__ bool count_sort_side(int side_i) {
+        if (W == 1) return count_sort_part(side_i, 0, 1);
+        if (ln() == 0) X->i32[0] = side_i;
+        wsync();
+        const uint64_t *before = B.s[side_i].sk;
+        par(kOpCountSort);
+        return B.s[side_i].sk != before;  // sorted: the entries moved to the other buffer
+    }
+
+    __device__ void build_side(int side_i) {
+        Side &d = B.s[side_i];
         const int H = d.H;
         for (int64_t i = H + ln(); i < d.P; i += 64) d.sk[i] = ~0ull;
         wsync();
@@ -1658,43 +1733,20 @@ struct LocusRun {
 #ifdef MANDO_CL_PHASES
         const uint64_t ts0 = clock64();
 #endif
-        if (H <= kSortTile || !count_sort_side(d)) sort_u64(d.sk, d.P);
+        if (H <= kSortTile || !count_sort_side(side_i)) sort_u64(d.sk, d.P);
 #ifdef MANDO_CL_PHASES
         const uint64_t ts1 = clock64();
         pc_sd_sort += ts1 - ts0;
 #endif
-        // records in sorted order; distinct-key flags; strand counts per key (lane per entry: the key
-        // index of entry i is the number of distinct keys up to i, minus one)
-        for (int64_t i = ln(); i < 3 * (int64_t)H; i += 64) d.upmb[i] = 0;
-        wsync();
-        int32_t kc = 0;
-        for (int i0 = 0; i0 < H; i0 += 64) {
-            const int i = i0 + ln();
-            int first = 0;
-            int64_t pos = 0;
-            int32_t seq = 0;
-            if (i < H) {
-                const uint64_t k = d.sk[i];
-                pos = (int64_t)(k >> 24) - kPosBias;
-                seq = (int32_t)(k & 0xffffffu);
-                d.erec[i] = d.etmp[seq];
-                first = (i == 0 || (int64_t)(d.sk[i - 1] >> 24) - kPosBias != pos) ? 1 : 0;
-            }
-            const int32_t fi = wincl(first);
-            if (i < H) {
-                const int32_t u = kc + fi - 1;
-                if (first) {
-                    d.ukey[u] = pos;
-                    d.ulo[u] = i;
-                    d.ufirst[u] = seq;
-                }
-                const int8_t dn = A.recs[d.etmp[seq]].dirn;
-                atomicAdd(&d.upmb[3 * u + (dn == 0 ? 0 : dn == 1 ? 1 : 2)], 1);
-            }
-            kc += __shfl(fi, 63);
+        // records in sorted order; distinct-key flags; strand counts per key (keys_part)
+        if (W > 1 && H >= 64 * W) {
+            if (ln() == 0) X->i32[0] = side_i;
+            wsync();
+            par(kOpKeys);
+        } else {
+            keys_part(side_i, 0, 1);
         }
-        d.nkeys = kc;
-        wsync();
+        const int32_t kc = d.nkeys;
 #ifdef MANDO_CL_PHASES
         const uint64_t ts2 = clock64();
         pc_sd_keys += ts2 - ts1;
@@ -1723,6 +1775,56 @@ struct LocusRun {
 #ifdef MANDO_CL_PHASES
         pc_sd_cand += clock64() - ts2;
 #endif
+    }
+
+    // distinct keys of side side_i's sorted entries, wave w of nw taking the entries [H*w/nw,
+    // H*(w+1)/nw): lane per entry, the key index of entry i is the number of distinct keys up to i,
+    // minus one (the waves before w count theirs first)
+    __device__ void keys_part(int side_i, int w, int nw) {
+        Side &d = B.s[side_i];
+        const int H = d.H;
+        const int e_lo = (int)((int64_t)H * w / nw), e_hi = (int)((int64_t)H * (w + 1) / nw);
+        for (int64_t i = 3 * (int64_t)e_lo + ln(); i < 3 * (int64_t)e_hi; i += 64) d.upmb[i] = 0;
+        auto pos_of = [&](int i) { return (int64_t)(d.sk[i] >> 24) - kPosBias; };
+        int64_t kc = 0, total = 0;
+        {
+            int64_t f = 0;
+            if (nw > 1)
+                for (int i0 = e_lo; i0 < e_hi; i0 += 64) {
+                    const int i = i0 + ln();
+                    if (i < e_hi) f += (i == 0 || pos_of(i - 1) != pos_of(i)) ? 1 : 0;
+                }
+            int ph = 0;
+            xprefix(ph, w, nw, wsum(f), kc, total);  // (one wave: both 0, set below)
+        }
+        wsync();
+        for (int i0 = e_lo; i0 < e_hi; i0 += 64) {
+            const int i = i0 + ln();
+            int first = 0;
+            int64_t pos = 0;
+            int32_t seq = 0;
+            if (i < e_hi) {
+                const uint64_t k = d.sk[i];
+                pos = (int64_t)(k >> 24) - kPosBias;
+                seq = (int32_t)(k & 0xffffffu);
+                d.erec[i] = d.etmp[seq];
+                first = (i == 0 || pos_of(i - 1) != pos) ? 1 : 0;
+            }
+            const int32_t fi = wincl(first);
+            if (i < e_hi) {
+                const int32_t u = (int32_t)kc + fi - 1;
+                if (first) {
+                    d.ukey[u] = pos;
+                    d.ulo[u] = i;
+                    d.ufirst[u] = seq;
+                }
+                const int8_t dn = A.recs[d.etmp[seq]].dirn;
+                atomicAdd(&d.upmb[3 * u + (dn == 0 ? 0 : dn == 1 ? 1 : 2)], 1);
+            }
+            kc += __shfl(fi, 63);
+        }
+        d.nkeys = (int32_t)(nw > 1 ? total : kc);
+        wsync();
     }
 
     __device__ int find_key(const Side &d, int64_t pos) const {
@@ -2677,7 +2779,7 @@ struct LocusRun {
             if (p % 10 == 0) B.hcb[p / 10] = 0;
             B.areas[1][p] = 0;
             B.splice[p] = -1;
-            B.sc[p] = 0;
+            for (int v = 0; v < W; ++v) B.sc[p * W + v] = 0;
             B.ec[p] = 0;
             B.sp[p] = -1;
             B.ep[p] = -1;

@@ -439,6 +439,67 @@ int mando_gather_bytes(mando_comm *c, const uint8_t *send, int64_t n, uint8_t *r
     return MANDO_OK;
 }
 
+int mando_rccl_alltoallv_plan(int nranks, const int64_t *send_counts, const int64_t *recv_counts, int64_t *send_off,
+                              int64_t *recv_off) {
+    if (nranks < 1 || !send_counts || !recv_counts || !send_off || !recv_off)
+        return mando::set_error(MANDO_E_ARG, "mando_rccl_alltoallv_plan: bad argument");
+    int64_t so = 0, ro = 0;
+    for (int r = 0; r < nranks; ++r) {
+        if (send_counts[r] < 0 || recv_counts[r] < 0)
+            return mando::set_error(MANDO_E_ARG, "mando_rccl_alltoallv_plan: negative count");
+        send_off[r] = so;  // the send buffer holds the parts for ranks 0..R-1 in order, so does recv
+        recv_off[r] = ro;
+        so += send_counts[r];
+        ro += recv_counts[r];
+    }
+    return MANDO_OK;
+}
+
+int mando_alltoallv_bytes(mando_comm *c, const uint8_t *send, const int64_t *send_counts, uint8_t *recv,
+                          const int64_t *recv_counts) {
+    if (!c || !send_counts || !recv_counts) return mando::set_error(MANDO_E_ARG, "mando_alltoallv_bytes: bad argument");
+    const int R = c->nranks, me = c->rank;
+    std::vector<int64_t> soff((size_t)R), roff((size_t)R);
+    int rc = mando_rccl_alltoallv_plan(R, send_counts, recv_counts, soff.data(), roff.data());
+    if (rc) return rc;
+    const int64_t stot = soff[(size_t)R - 1] + send_counts[R - 1], rtot = roff[(size_t)R - 1] + recv_counts[R - 1];
+    if ((stot > 0 && !send) || (rtot > 0 && !recv)) return mando::set_error(MANDO_E_ARG, "mando_alltoallv_bytes: null buffer");
+    if (send_counts[me] != recv_counts[me]) return mando::set_error(MANDO_E_ARG, "mando_alltoallv_bytes: own part sizes differ");
+    if (send_counts[me] > 0) memcpy(recv + roff[(size_t)me], send + soff[(size_t)me], (size_t)send_counts[me]);
+    if (R == 1) return MANDO_OK;
+    if (!c->nccl)  // the host transport has no point-to-point exchange: the caller all-gathers instead
+        return mando::set_error(MANDO_E_UNSUPPORTED, "mando_alltoallv_bytes: RCCL communicators only");
+    // RCCL: one group of point-to-point sends and receives with every other rank (the own part never
+    // leaves the host)
+    if (hipSetDevice(c->device) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: hipSetDevice failed");
+    rc = ensure_dev(&c->dsend, &c->dsend_cap, (size_t)std::max<int64_t>(stot, 1));
+    if (!rc) rc = ensure_dev(&c->drecv, &c->drecv_cap, (size_t)std::max<int64_t>(rtot, 1));
+    if (rc) return rc;
+    if (stot > 0 && hipMemcpyAsync(c->dsend, send, (size_t)stot, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return mando::set_error(MANDO_E_HIP, "comm: H2D copy failed");
+    ncclResult_t r = ncclGroupStart();
+    for (int p = 0; p < R && r == ncclSuccess; ++p) {
+        if (p == me) continue;
+        if (send_counts[p] > 0)
+            r = ncclSend(static_cast<uint8_t *>(c->dsend) + soff[(size_t)p], (size_t)send_counts[p], ncclUint8, p, c->nccl,
+                         c->stream);
+        if (r == ncclSuccess && recv_counts[p] > 0)
+            r = ncclRecv(static_cast<uint8_t *>(c->drecv) + roff[(size_t)p], (size_t)recv_counts[p], ncclUint8, p, c->nccl,
+                         c->stream);
+    }
+    const ncclResult_t e = ncclGroupEnd();
+    if (r == ncclSuccess) r = e;
+    if (r != ncclSuccess) return nccl_fail(r, "ncclSend/ncclRecv alltoallv");
+    for (int p = 0; p < R; ++p) {
+        if (p == me || recv_counts[p] == 0) continue;
+        if (hipMemcpyAsync(recv + roff[(size_t)p], static_cast<uint8_t *>(c->drecv) + roff[(size_t)p],
+                           (size_t)recv_counts[p], hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+            return mando::set_error(MANDO_E_HIP, "comm: D2H copy failed");
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return mando::set_error(MANDO_E_HIP, "comm: stream sync failed");
+    return MANDO_OK;
+}
+
 int mando_allreduce_max_f64(mando_comm *c, double *v) {
     if (!c || !v) return mando::set_error(MANDO_E_ARG, "mando_allreduce_max_f64: bad argument");
     if (c->nranks == 1) return MANDO_OK;

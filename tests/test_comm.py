@@ -187,6 +187,67 @@ def test_rccl_plan_edge_cases():
                                          P(b.ctypes.data)) != 0
 
 
+def _a2a_part(src: int, dst: int) -> np.ndarray:
+    """The alltoallv tests' part from rank src to rank dst (ragged; rank 1 sends nothing to rank 0)."""
+    if (src, dst) == (1, 0):
+        return np.zeros(0, np.uint8)
+    return ((np.arange(src * 3001 + dst * 17 + 5) * (src + 2 * dst + 1)) % 251).astype(np.uint8)
+
+
+def _host_a2a_rank(rank, world, port, q):
+    from mandalorion_amd.comm import Comm
+
+    with Comm(world, rank, "127.0.0.1", port, timeout_s=60) as c:
+        got = c.alltoallv([_a2a_part(rank, d) for d in range(world)])
+        q.put((rank, [g.tobytes() for g in got]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_alltoallv_and_rccl_plan(world):
+    """alltoallv over the host transport (one all-gather, each rank keeps its parts), and the RCCL path's
+    marshalling (mando_rccl_alltoallv_plan: offsets of each rank's part in the send and receive buffers)
+    replayed on host buffers: the same bytes."""
+    import ctypes
+
+    from mandalorion_amd import _lib
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_host_a2a_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    lib = _lib.load()
+    P = ctypes.c_void_p
+    # the RCCL path: every rank's send buffer and offsets from the plan; rank d receives from rank s the
+    # bytes at send_off[s][d] of s's buffer, into recv_off[d][s] of its own
+    sends, soffs, roffs, rcs = [], [], [], []
+    for r in range(world):
+        parts = [_a2a_part(r, d) for d in range(world)]
+        sc = np.array([p.size for p in parts], np.int64)
+        rc = np.array([_a2a_part(s, r).size for s in range(world)], np.int64)
+        so, ro = np.zeros(world, np.int64), np.zeros(world, np.int64)
+        assert lib.mando_rccl_alltoallv_plan(world, P(sc.ctypes.data), P(rc.ctypes.data), P(so.ctypes.data),
+                                             P(ro.ctypes.data)) == 0
+        sends.append(np.concatenate(parts))
+        soffs.append(so)
+        roffs.append(ro)
+        rcs.append(rc)
+    for d in range(world):
+        recv = np.full(int(rcs[d].sum()), 0xEE, np.uint8)
+        for s_ in range(world):
+            n = int(rcs[d][s_])
+            recv[roffs[d][s_]:roffs[d][s_] + n] = sends[s_][soffs[s_][d]:soffs[s_][d] + n]
+        replay = [recv[roffs[d][s_]:roffs[d][s_] + rcs[d][s_]].tobytes() for s_ in range(world)]
+        want = [_a2a_part(s_, d).tobytes() for s_ in range(world)]
+        assert out[d] == want
+        assert replay == want
+
+
 @pytest.mark.gpu
 def test_rccl_backend_single_rank(gpu_ctx):
     """The RCCL path of mando_comm_init on the box's one GPU (ncclUniqueId drawn by rank 0,
@@ -199,6 +260,8 @@ def test_rccl_backend_single_rank(gpu_ctx):
         assert cnt.tolist() == [1000] and b.tolist() == [i % 251 for i in range(1000)]
         g, gc = c.gather_bytes((np.arange(999) % 13).astype(np.uint8))
         assert gc.tolist() == [999] and g.tolist() == [i % 13 for i in range(999)]
+        a = c.alltoallv([(np.arange(777) % 7).astype(np.uint8)])
+        assert len(a) == 1 and a[0].tolist() == [i % 7 for i in range(777)]
         c.barrier()
 
 
@@ -219,6 +282,8 @@ def _rccl_rank(rank, world, port, q):
         assert gc.tolist() == counts.tolist()
         assert (g is None) == (rank != 0) and (g is None or g.tobytes() == allb.tobytes())
         m = c.max(float(rank) * 1.5)
+        a2a = c.alltoallv([_a2a_part(rank, d) for d in range(world)])
+        assert [x.tobytes() for x in a2a] == [_a2a_part(s, rank).tobytes() for s in range(world)]
         c.barrier()
         q.put((rank, counts.tolist(), allb.tobytes(), m, c.backend))
     finally:

@@ -145,9 +145,10 @@ def test_driver_three_rank_reassembly_in_one_process(tmp_path, monkeypatch):
 class PlaceRehearsal:
     """In-process stand-in for a communicator under placement reassembly: call c of allgather_bytes
     returns every rank's latest contribution to call c (ranks that have not made it yet: an empty one).
-    Ranks run one after another, so three passes over the ranks make every exchange complete: the counts
-    (call 0) after the first, the sizes computed from them after the second, the placed bytes after the
-    third (tools/rank_rehearsal.py uses the same scheme)."""
+    Ranks run one after another, so an exchange whose inputs depend on k earlier exchanges is complete
+    in pass k + 2: the counts in the second pass, the sizes computed from them in the third, the range
+    placement's pieces (sent to the ranks that own their bytes of each file) in the fourth
+    (tools/rank_rehearsal.py uses the same scheme)."""
 
     def __init__(self, rank, world, store):
         self.rank, self.world, self.store, self.calls = rank, world, store, 0
@@ -176,7 +177,7 @@ def test_driver_three_rank_placement_in_one_process(tmp_path):
     kw = dict(orient_fn=lambda s, o, g: oref.orient_packed(s, o, g),
               consensus_fn=lambda s, o, g, sd: opoa.consensus_packed(s, o, g, seeding=sd), cluster_fn=ocl.cluster_loci)
     store = {}
-    for _ in range(3):
+    for _ in range(4):
         groups = 0
         for r in range(3):
             st = _run(d, comm=PlaceRehearsal(r, 3, store), **kw)

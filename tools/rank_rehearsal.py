@@ -2,10 +2,11 @@
 this process, each on its own share of the LPT plan, exactly as define_isoforms runs them under a real
 communicator -- except the transport, an in-process stand-in.
 
-* placement reassembly (the default): allgather_bytes call c returns every rank's latest contribution to
-  call c.  Three passes over the ranks: the first warms each rank's share (its own process in a real run:
-  files cached, device buffers sized) and completes the count exchange, the second completes the size
-  exchanges, the third is timed and its placed files are checked against the one-rank run.
+* placement reassembly (the default): allgather_bytes / alltoallv call c returns every rank's latest
+  contribution to call c.  Four passes over the ranks: the first warms each rank's share (its own process
+  in a real run: files cached, device buffers sized) and completes the count exchange, the second the size
+  exchanges, the third the range placement's pieces, the fourth is timed and its placed files are checked
+  against the one-rank run.
 * gather reassembly (MANDO_REASSEMBLY=gather): ranks 1..N-1 hand their compacted payload to a recording
   stand-in for mando_gather_bytes, and rank 0 receives those bytes from it, then merges and writes.
 
@@ -45,6 +46,13 @@ class _Place:
         empty = np.zeros(1, np.int64).view(np.uint8)
         parts = [c.get(r, empty) for r in range(self.world)]
         return np.concatenate(parts), np.array([p.size for p in parts], dtype=np.int64)
+
+    def alltoallv(self, parts):
+        """call c returns, by rank, each rank's latest part addressed to this one for call c"""
+        c = self.store.setdefault(("a2a", self.calls), {})
+        self.calls += 1
+        c[self.rank] = [np.array(p, dtype=np.uint8, copy=True).ravel() for p in parts]
+        return [c[r][self.rank] if r in c else np.zeros(0, np.uint8) for r in range(self.world)]
 
     def barrier(self):
         pass
@@ -90,11 +98,11 @@ def _dump_place(define, dump: str, cur: list):
     source offsets, roots, sizes and the all-rank size table) for tools/place_contention.py."""
     inner = define._place
 
-    def place(path, buf, src, roots, sizes, g_sizes, threads=0):
+    def place(path, buf, src, roots, sizes, g_sizes, comm, threads=0):
         if cur[0] is not None:
             np.savez(os.path.join(dump, f"r{cur[0]}_{os.path.basename(path)}.npz"), buf=buf, src=src,
                      roots=roots, sizes=sizes, g_sizes=g_sizes)
-        return inner(path, buf, src, roots, sizes, g_sizes, threads)
+        return inner(path, buf, src, roots, sizes, g_sizes, comm, threads)
 
     define._place = place
 
@@ -109,13 +117,13 @@ def main_place(d, n, threads, ref, files):
         os.makedirs(dump, exist_ok=True)
         _dump_place(define, dump, cur)
     out = {"ranks": n, "reassembly": "place", "threads": threads, "rank_s": {}, "rank_phases_s": {}}
-    for p in range(4 if dump else 3):  # the dump pass comes after the timed one
+    for p in range(5 if dump else 4):  # the dump pass comes after the timed one
         for r in range(n):
-            cur[0] = r if p == 3 else None
+            cur[0] = r if p == 4 else None
             t0 = time.perf_counter()
             st = define.define_isoforms(d, threads=threads, comm=_Place(r, n, store))
             print(f"[rehearsal] pass {p} rank {r}: {time.perf_counter() - t0:.2f} s", file=sys.stderr, flush=True)
-            if p == 2:
+            if p == 3:
                 out["rank_s"][r] = round(time.perf_counter() - t0, 4)
                 ph = {k: round(st[k], 4) for k in ("t_ingest", "t_cluster", "t_orient", "t_poa", "t_merge", "t_total")}
                 ph["place_r2i"] = round(_span(st, "write_r2i"), 4)     # overlapped with the POA
