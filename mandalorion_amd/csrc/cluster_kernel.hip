@@ -79,6 +79,9 @@ __device__ __forceinline__ bool wany(bool p) { return __ballot(p) != 0ull; }
 // scratch).  The large-locus kernel's workgroup has several waves; they meet only at gsync().
 __device__ __forceinline__ void wsync() { __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void gsync() { __syncthreads(); }
+// the large-locus kernels' waves per workgroup (K2: loci of kMwMinRecs records or more; K1: kK1MwBytes)
+constexpr int kMwWaves = 8;
+constexpr int kMwMinRecs = 2048;
 
 __host__ __device__ __forceinline__ int64_t al256(int64_t x) { return (x + 255) & ~int64_t(255); }
 
@@ -341,13 +344,41 @@ __device__ __forceinline__ ALayout a_layout(uint8_t *base, const Locus &L) {
     return A;
 }
 
-__global__ __launch_bounds__(64) void cluster_parse(Args G) {
+// K1 for a locus file of kK1MwBytes or more runs on a workgroup of kMwWaves waves: wave w scans the
+// w-th share of the text and parses the w-th share of the records, the offsets of each share (line ends,
+// blocks) continuing those of the shares before it (one exchange each), so the results are the one-wave
+// kernel's.  The parse is then two passes over a wave's records: fields (the block columns' starts
+// parked in the record's op / run offsets, which steps 3-4 set later), then the blocks at their offsets.
+constexpr int64_t kK1MwBytes = int64_t(4) << 20;
+struct K1X {
+    int64_t part[2][kMwWaves][4];
+};
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void cluster_parse(Args G) {
+    __shared__ K1X kx;
+    const int w = NW > 1 ? wv() : 0;
     const int li = G.order[blockIdx.x];
     const Locus L = G.loci[li];
     Stats *st = G.stats + li;
     // the locus' statistics start from zero here rather than by a memset on the stream: a fill kernel
     // queued behind a running POA grid waited ~0.28 s for CUs
-    if (ln() == 0) *st = Stats{};
+    if (w == 0 && ln() == 0) *st = Stats{};
+    // exchanges between the waves: each posts up to four values; after one barrier every wave reads all
+    // posts (banks alternate, so no wave overwrites a post another has yet to read)
+    int ph = 0;
+    auto post = [&](int64_t v0, int64_t v1 = 0, int64_t v2 = 0, int64_t v3 = 0) {
+        if (ln() == 0) {
+            kx.part[ph][w][0] = v0;
+            kx.part[ph][w][1] = v1;
+            kx.part[ph][w][2] = v2;
+            kx.part[ph][w][3] = v3;
+        }
+        gsync();
+        const int b = ph;
+        ph ^= 1;
+        return b;
+    };
     const uint8_t *T = G.text + L.text_off;
     const int64_t n = L.text_len;
     ALayout A = a_layout(G.scratch_a + L.a_off, L);
@@ -363,19 +394,43 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
     const uintptr_t base = (uintptr_t)T & ~(uintptr_t)15;
     const int pad0 = (int)((uintptr_t)T - base);
     const int64_t nch = (pad0 + n + 15) >> 4;
-    int32_t nl = 0;
-    for (int64_t c00 = 0; c00 < nch; c00 += 64 * kLineUnroll) {
+    // this wave's chunks; several waves: their newlines counted first, the line ends of the waves
+    // before come first
+    const int64_t c_lo = nch * w / NW, c_hi = nch * (w + 1) / NW;
+    int32_t nl = 0, nl_all = 0;
+    if (NW > 1) {
+        int64_t cnt = 0;
+        for (int64_t c00 = c_lo; c00 < c_hi; c00 += 64 * kLineUnroll) {
+            uint4 vv[kLineUnroll];
+#pragma unroll
+            for (int u = 0; u < kLineUnroll; ++u) {
+                const int64_t c = c00 + u * 64 + ln();
+                vv[u] = c < c_hi ? ((const uint4 *)base)[c] : uint4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < kLineUnroll; ++u) {
+                const int64_t c = c00 + u * 64 + ln();
+                cnt += c < c_hi ? __popc(byte_mask16(vv[u], 0x0a0a0a0au) & span_mask16(pad0 - c * 16, pad0 + n - c * 16)) : 0;
+            }
+        }
+        const int bk = post(wsum(cnt));
+        for (int v = 0; v < NW; ++v) {
+            if (v < w) nl += (int32_t)kx.part[bk][v][0];
+            nl_all += (int32_t)kx.part[bk][v][0];
+        }
+    }
+    for (int64_t c00 = c_lo; c00 < c_hi; c00 += 64 * kLineUnroll) {
         uint4 vv[kLineUnroll];
 #pragma unroll
         for (int u = 0; u < kLineUnroll; ++u) {
             const int64_t c = c00 + u * 64 + ln();
-            vv[u] = c < nch ? ((const uint4 *)base)[c] : uint4{0, 0, 0, 0};
+            vv[u] = c < c_hi ? ((const uint4 *)base)[c] : uint4{0, 0, 0, 0};
         }
 #pragma unroll
         for (int u = 0; u < kLineUnroll; ++u) {
             const int64_t c = c00 + u * 64 + ln();
             // newline bytes at text positions [0, n) of the chunk (bytes k with 0 <= c * 16 + k - pad0 < n)
-            uint32_t m = c < nch ? byte_mask16(vv[u], 0x0a0a0a0au) & span_mask16(pad0 - c * 16, pad0 + n - c * 16) : 0u;
+            uint32_t m = c < c_hi ? byte_mask16(vv[u], 0x0a0a0a0au) & span_mask16(pad0 - c * 16, pad0 + n - c * 16) : 0u;
             const int cnt = __popc(m);
             const int incl = wincl(cnt);
             int idx = nl + incl - cnt;
@@ -388,11 +443,12 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
             nl += __shfl(incl, 63);
         }
     }
+    if (NW > 1) nl = nl_all;
     const bool tail = n > 0 && T[n - 1] != '\n';
     const int32_t nrec = nl + (tail ? 1 : 0);
-    if (tail && nl < L.line_cap && ln() == 0) A.line_end[nl] = (int32_t)n;
+    if (tail && nl < L.line_cap && w == 0 && ln() == 0) A.line_end[nl] = (int32_t)n;
     if (nrec > L.line_cap) {
-        if (ln() == 0) {
+        if (w == 0 && ln() == 0) {
             st->status = kCapacity;
             st->n_rec = nrec;
             st->n_ops = 0;
@@ -401,6 +457,7 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
         return;
     }
     wsync();
+    if (NW > 1) gsync();  // every line end written
 
 #ifdef MANDO_CL_PHASES
     const uint64_t k1t1 = clock64();
@@ -410,12 +467,10 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
     int64_t blk_carry = 0, cov_cap = 0, ident_cap = 0;
     int64_t span_lo = INT64_MAX, span_hi = INT64_MIN;
     int32_t hist_l = 0, hist_r = 0, max_nblk = 0;
-    for (int r0 = 0; r0 < nrec; r0 += 64) {
-        const int r = r0 + ln();
-        const bool act = r < nrec;
-        Rec R = {};
-        int nb = 0;
-        int f18a = 0, f18b = 0, f20a = 0, f20b = 0;
+    const int r_lo = (int)((int64_t)nrec * w / NW), r_hi = (int)((int64_t)nrec * (w + 1) / NW);
+    // the fields of record r (act: a record of this lane); the block columns' starts and their count
+    auto fields = [&](int r, bool act, Rec &R, int &nb, int &f18a, int &f20a) {
+        int f18b = 0, f20b = 0;
         if (act) {
             int a = r == 0 ? 0 : A.line_end[r - 1] + 1, b = A.line_end[r];
             while (a < b && is_space6(T[a])) ++a;
@@ -488,13 +543,9 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
                 if (!ok) err = 1;
             }
         }
-        // block offsets: prefix over the lanes
-        const int nbi = act && !err ? nb : 0;
-        const int incl = wincl(nbi);
-        const int64_t boff = blk_carry + incl - nbi;
-        blk_carry += __shfl(incl, 63);
-        R.blk_off = (int32_t)boff;
-        R.nblk = nbi;
+    };
+    // the blocks of record r at boff, and its statistics
+    auto blocks = [&](int r, bool act, Rec &R, int nb, int f18a, int f20a, int64_t boff) {
         if (act && !err) {
             // blocks: str.split(',')[:-1] of columns 18 (sizes) and 20 (starts)
             const bool room = boff + nb <= L.blk_cap;
@@ -531,14 +582,83 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
             max_nblk = nb > max_nblk ? nb : max_nblk;
             A.recs[r] = R;
         }
+    };
+    if (NW == 1) {
+        for (int r0 = 0; r0 < nrec; r0 += 64) {
+            const int r = r0 + ln();
+            const bool act = r < nrec;
+            Rec R = {};
+            int nb = 0, f18a = 0, f20a = 0;
+            fields(r, act, R, nb, f18a, f20a);
+            // block offsets: prefix over the lanes
+            const int nbi = act && !err ? nb : 0;
+            const int incl = wincl(nbi);
+            const int64_t boff = blk_carry + incl - nbi;
+            blk_carry += __shfl(incl, 63);
+            R.blk_off = (int32_t)boff;
+            R.nblk = nbi;
+            blocks(r, act, R, nb, f18a, f20a, boff);
+        }
+    } else {
+        // pass 1: fields of this wave's records, block counts summed
+        int64_t nbs = 0;
+        for (int r0 = r_lo; r0 < r_hi; r0 += 64) {
+            const int r = r0 + ln();
+            const bool act = r < r_hi;
+            Rec R = {};
+            int nb = 0, f18a = 0, f20a = 0;
+            fields(r, act, R, nb, f18a, f20a);
+            if (act) {
+                R.nblk = !err ? nb : 0;
+                R.op_off = f18a;
+                R.run_off = f20a;
+                A.recs[r] = R;
+                nbs += R.nblk;
+            }
+        }
+        const int bk = post(wsum(nbs), wany(err != 0) ? 1 : 0);
+        int64_t all_blk = 0, any_err = 0;
+        for (int v = 0; v < NW; ++v) {
+            if (v < w) blk_carry += kx.part[bk][v][0];
+            all_blk += kx.part[bk][v][0];
+            any_err |= kx.part[bk][v][1];
+        }
+        if (any_err) {
+            if (w == 0 && ln() == 0) st->status = kParse;
+            return;
+        }
+        // pass 2: the blocks at the offsets after the waves before this one
+        for (int r0 = r_lo; r0 < r_hi; r0 += 64) {
+            const int r = r0 + ln();
+            const bool act = r < r_hi;
+            Rec R = act ? A.recs[r] : Rec{};
+            const int nb = R.nblk, f18a = R.op_off, f20a = R.run_off;
+            R.op_off = R.run_off = 0;
+            const int nbi = act && !err ? nb : 0;
+            const int incl = wincl(nbi);
+            const int64_t boff = blk_carry + incl - nbi;
+            blk_carry += __shfl(incl, 63);
+            R.blk_off = (int32_t)boff;
+            R.nblk = nbi;
+            blocks(r, act, R, nb, f18a, f20a, boff);
+        }
+        blk_carry = all_blk;
     }
-    if (wany(err != 0)) {
-        if (ln() == 0) st->status = kParse;
-        return;
+    {
+        int64_t e = wany(err != 0) ? 1 : 0;
+        if (NW > 1) {
+            const int bk = post(e);
+            e = 0;
+            for (int v = 0; v < NW; ++v) e |= kx.part[bk][v][0];
+        }
+        if (e) {
+            if (w == 0 && ln() == 0) st->status = kParse;
+            return;
+        }
     }
     const int64_t n_blk = blk_carry;
     if (n_blk > L.blk_cap) {
-        if (ln() == 0) {
+        if (w == 0 && ln() == 0) {
             st->status = kCapacity;
             st->n_rec = nrec;
             st->n_blk = (int32_t)n_blk;
@@ -565,7 +685,27 @@ __global__ __launch_bounds__(64) void cluster_parse(Args G) {
     span_lo = wmin(span_lo);
     span_hi = wmax(span_hi);
     max_nblk = wmax(max_nblk);
-    if (ln() == 0) {
+    if (NW > 1) {
+        const int b1 = post(cov_cap, ident_cap, hist_l, hist_r);
+        int64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        for (int v = 0; v < NW; ++v) {
+            s0 += kx.part[b1][v][0];
+            s1 += kx.part[b1][v][1];
+            s2 += kx.part[b1][v][2];
+            s3 += kx.part[b1][v][3];
+        }
+        const int b2 = post(span_lo, span_hi, max_nblk);
+        for (int v = 0; v < NW; ++v) {
+            span_lo = kx.part[b2][v][0] < span_lo ? kx.part[b2][v][0] : span_lo;
+            span_hi = kx.part[b2][v][1] > span_hi ? kx.part[b2][v][1] : span_hi;
+            max_nblk = (int32_t)kx.part[b2][v][2] > max_nblk ? (int32_t)kx.part[b2][v][2] : max_nblk;
+        }
+        cov_cap = s0;
+        ident_cap = s1;
+        hist_l = (int32_t)s2;
+        hist_r = (int32_t)s3;
+    }
+    if (w == 0 && ln() == 0) {
         st->status = kOk;
         st->n_rec = nrec;
         st->n_ops = 0;  // cluster_cs_scan
@@ -812,8 +952,6 @@ __host__ __device__ inline int32_t peak_cap_of(const Stats &S, const Locus &L) {
 // each wave taking a contiguous share of the records / winners.  MwX is their LDS exchange: the phase
 // and its arguments, and per-wave partials in two banks that alternate between exchanges (a wave that
 // runs ahead cannot overwrite a partial another wave has yet to read).
-constexpr int kMwWaves = 8;
-constexpr int kMwMinRecs = 2048;
 constexpr int kOpExit = 0, kOpCovSets = 1, kOpDetCov = 2, kOpCountSort = 3, kOpKeys = 4;
 // waves of a locus's K2 workgroup (the host splits the launch on the same rule)
 __host__ __device__ inline int mw_waves(const Stats &S) { return S.n_rec >= kMwMinRecs ? kMwWaves : 1; }
@@ -2886,9 +3024,15 @@ __global__ __launch_bounds__(64 * NW) void cluster_locus(Args G) {
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-hipError_t launch_parse(const Args &a, int n_blocks, int n_work, hipStream_t s) {
+// K1 over the loci a.order[0, n_blocks): the first n_big (files of kK1MwBytes or more) on several waves each
+hipError_t launch_parse(const Args &a, int n_blocks, int n_big, int n_work, hipStream_t s) {
     if (n_blocks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(cluster_parse, dim3(n_blocks), dim3(64), 0, s, a);
+    if (n_big > 0) hipLaunchKernelGGL(cluster_parse<kMwWaves>, dim3(n_big), dim3(64 * kMwWaves), 0, s, a);
+    if (n_blocks > n_big) {
+        Args b = a;
+        b.order = a.order + n_big;
+        hipLaunchKernelGGL(cluster_parse<1>, dim3(n_blocks - n_big), dim3(64), 0, s, b);
+    }
     hipLaunchKernelGGL(cluster_cs_count, dim3(n_work), dim3(64), 0, s, a);
     hipLaunchKernelGGL(cluster_cs_scan, dim3(n_blocks), dim3(64), 0, s, a);
     hipLaunchKernelGGL(cluster_cs_runs, dim3(n_work), dim3(64), 0, s, a);
@@ -3132,6 +3276,9 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     G.stats = d_stats.as<Stats>();
     G.prm = d_prm.as<Params>();
 
+    // run_order is by text size, descending: the large files lead
+    int k1_big = 0;
+    while (k1_big < nrun && L[(size_t)run_order[(size_t)k1_big]].text_len >= kK1MwBytes) ++k1_big;
     // K1, re-run with the reported sizes while a locus outgrows its scratch
     const bool timing = getenv("MANDO_CL_TIME") != nullptr;
     const auto tk0 = std::chrono::steady_clock::now();
@@ -3149,7 +3296,7 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         a_last = a_tot;
         CL_TRY(hipMemcpyAsync(d_loci.p, L.data(), (size_t)nl * sizeof(Locus), hipMemcpyHostToDevice, s));
         G.scratch_a = d_a.as<uint8_t>();
-        CL_TRY(launch_parse(G, nrun, n_work, s));
+        CL_TRY(launch_parse(G, nrun, k1_big, n_work, s));
         CL_TRY(hipMemcpyAsync(st.data(), d_stats.p, (size_t)nl * sizeof(Stats), hipMemcpyDeviceToHost, s));
         CL_TRY(hipStreamSynchronize(s));
         bool again = false;

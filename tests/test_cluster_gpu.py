@@ -193,6 +193,27 @@ def test_edge_cases(tmp_path):
     _compare(paths + ["/nonexistent/x.psl"], chroms + ["chrA"], seed=2)
 
 
+def test_large_files_on_several_waves(tmp_path):
+    """Locus files of 4 MB or more are parsed by several waves (K1: line ends and records split between
+    them): such files without a trailing newline, with CRLF ends, and with a malformed line in the middle
+    (a parse error, wherever the split falls) equal the restatement."""
+    d = str(tmp_path)
+    synth.write_loci(os.path.join(d, "src"), 1, reads=(7000, 7000), exons=(10, 14), exon_len=(60, 200),
+                     isoforms=(9, 11), threads=8, seed=41, rev_frac=0.3)
+    src = os.path.join(d, "src", sorted(os.listdir(os.path.join(d, "src")))[0])
+    assert os.path.getsize(src) >= 4 << 20
+    tmp = os.path.join(d, "tmp_SS")
+    os.makedirs(tmp)
+    chrom = open(src).readline().split("\t")[13]
+    _edit_lines(src, os.path.join(tmp, f"{chrom}~1~2.psl"), lambda L: "\n".join(L))  # no trailing newline
+    _edit_lines(src, os.path.join(tmp, f"{chrom}~3~4.psl"), lambda L: "\r\n".join(L) + "\r\n")
+    _edit_lines(src, os.path.join(tmp, f"{chrom}~5~6.psl"),
+                lambda L: "\n".join(L[:4321] + ["a\tb\tc"] + L[4321:]) + "\n")  # short line
+    roots = define._roots(tmp)
+    paths = [os.path.join(tmp, r + ".psl") for r in roots]
+    _compare(paths, [chrom] * len(paths), seed=6)
+
+
 def test_repeated_calls_reuse_buffers(tmp_path):
     """Back-to-back calls reuse the host and device text buffers and the per-context scratch; every call
     must equal the restatement (a refilled, recycled buffer once handed the kernels stale bytes)."""

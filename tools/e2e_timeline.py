@@ -1,13 +1,15 @@
-"""Dev helper: whole D module on the bench's config-3 loci with the stage timeline (cluster chunks on
-the host worker thread vs orientation / POA chunks on the GPU).  CHUNKS=<n> fixes the chunk count."""
+"""Dev helper: whole D module on one of the bench's workloads with the stage timeline (cluster chunks on
+the host worker thread vs orientation / POA chunks on the GPU).  CHUNKS=<n> fixes the chunk count.
+usage: python tools/e2e_timeline.py [workload=config3] [loci]"""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench
 from mandalorion_amd import define
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
-d = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mando_bench_config3_{n}")
+wl = sys.argv[1] if len(sys.argv) > 1 else "config3"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else bench.WORKLOADS[wl]["loci"]
+d = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mando_bench_{wl}_{n}")
 os.makedirs(d, exist_ok=True)
-t = time.time(); bench.gen_data(d, bench.WORKLOADS["config3"], n, 16); print(f"data {time.time()-t:.1f}s")
+t = time.time(); bench.gen_data(d, bench.WORKLOADS[wl], n, 16); print(f"data {time.time()-t:.1f}s", flush=True)
 for nc in [int(x) for x in os.environ.get("CHUNKS", "0").split(",")]:
     define.define_isoforms(d, threads=16, n_chunks=nc)
     st = define.define_isoforms(d, threads=16, n_chunks=nc)
