@@ -121,6 +121,7 @@ struct Args {
     uint8_t *out;
     int64_t *rec_text;  // per global record: name_off, name_len, seq_off, seq_len (text-absolute)
     const Params *prm;
+    int64_t sort_tile;  // K2: keys of the launch's dynamic LDS (the sort tile; a power of two)
 };
 
 // host side (cluster_kernel.hip): both kernels over a batch of loci whose text is in host memory

@@ -1040,8 +1040,8 @@ __host__ __device__ inline void carve_o(uint8_t *base, const Stats &S, const Loc
 // ---------------------------------------------------------------------------------------------
 // wave sorts (bitonic, in global scratch; P a power of two >= 64)
 // ---------------------------------------------------------------------------------------------
-// The bitonic network's exchanges with partner distance j < kSortTile stay inside aligned tiles of
-// kSortTile keys, so they run in LDS (cluster_locus's dynamic LDS): a tile is loaded once, takes every
+// The bitonic network's exchanges with partner distance j < the tile stay inside aligned tiles of
+// that many keys (kSortTile at most), so they run in LDS (cluster_locus's dynamic LDS): a tile is loaded once, takes every
 // such pass of the current stage, and is written back; only the passes with j >= kSortTile go through
 // global memory (for 2^17 keys: 10 global passes instead of 153).
 constexpr int64_t kSortTile = 4096;
@@ -1086,8 +1086,9 @@ __device__ void sort_tile_lds(uint64_t *a, int64_t t0, int64_t T, int64_t k, int
     wsync();
 }
 
-__device__ void sort_u64(uint64_t *a, int64_t P) {
-    const int64_t T = P < kSortTile ? P : kSortTile;
+// tile: the keys the launch's dynamic LDS holds (Args::sort_tile, at most kSortTile)
+__device__ void sort_u64(uint64_t *a, int64_t P, int64_t tile) {
+    const int64_t T = P < tile ? P : tile;
     // stages k <= T: every pass inside the tile
     for (int64_t t0 = 0; t0 < P; t0 += T) {
         for (int64_t i = ln(); i < T; i += 64) g_sort_lds[i] = a[t0 + i];
@@ -1336,7 +1337,13 @@ __device__ double round3(int64_t best, int64_t cov) {
 // ---------------------------------------------------------------------------------------------
 // K2: one locus
 // ---------------------------------------------------------------------------------------------
-constexpr int kLdsPerm = 4096;
+// the static permutation buffer: 8 KB in the one-wave kernel (its LDS limits how many loci share a CU
+// with the POA grids), 16 KB in the large-locus kernel (whose permutations reach 7k entries)
+#ifdef MANDO_K2_LITE  // dev A/B build: a one-wave K2 workgroup about as large as a POA workgroup
+constexpr int kLdsPerm = 512, kLdsPermBig = 4096;
+#else
+constexpr int kLdsPerm = 2048, kLdsPermBig = 4096;
+#endif
 
 struct MwX {
     int32_t op;
@@ -1356,6 +1363,8 @@ struct LocusRun {
     OPtr O;
     MT mt;
     int32_t *lperm;
+    int lperm_cap;  // its entries
+    int64_t tile;   // keys of the dynamic LDS (g_sort_lds)
     int n;
     int status;
     int64_t bin_lo, bin_hi, nbins;
@@ -1375,14 +1384,14 @@ struct LocusRun {
     // a permutation's buffer: static LDS, else the sort tile's dynamic LDS (free between sorts; each
     // permutation is consumed before the next sort), else global scratch
     __device__ int32_t *perm_buf(int32_t m) const {
-        return m <= kLdsPerm ? lperm : m <= 2 * kSortTile ? reinterpret_cast<int32_t *>(g_sort_lds) : B.perm;
+        return m <= lperm_cap ? lperm : m <= 2 * tile ? reinterpret_cast<int32_t *>(g_sort_lds) : B.perm;
     }
     // the permutation's conflict table: whichever of the two LDS buffers the permutation does not use,
     // as many slots as positions where it fits (no collisions then), cleared once per permutation
     __device__ void permute(int32_t m, int32_t *perm) {
         int slots = 64;
-        while (slots < m && slots < (m <= kLdsPerm ? 2 * (int)kSortTile : kLdsPerm)) slots <<= 1;
-        mt.permutation(m, perm, m <= kLdsPerm ? reinterpret_cast<uint32_t *>(g_sort_lds) : reinterpret_cast<uint32_t *>(lperm),
+        while (slots < m && slots < (m <= lperm_cap ? 2 * (int)tile : lperm_cap)) slots <<= 1;
+        mt.permutation(m, perm, m <= lperm_cap ? reinterpret_cast<uint32_t *>(g_sort_lds) : reinterpret_cast<uint32_t *>(lperm),
                        slots);
     }
     __device__ bool in_map(int64_t p) const { return p >= L.map_lo && p < L.map_lo + L.map_n; }
@@ -1484,7 +1493,7 @@ struct LocusRun {
         for (int64_t r = ln(); r < pn; r += 64)
             B.isort[r] = (r < n && A.recs[r].same_chrom) ? ((B.ihash[r] & ~0xffffffull) | (uint64_t)r) : ~0ull;
         wsync();
-        sort_u64(B.isort, pn);
+        sort_u64(B.isort, pn, tile);
         for (int64_t i0 = 0; i0 < n; i0 += 64) {
             const int64_t i = i0 + ln();
             const uint64_t k = i < n ? B.isort[i] : ~0ull;
@@ -1514,7 +1523,7 @@ struct LocusRun {
         // coverage bins per record: myround over each block at stride 10 plus the block's tail, sorted
         // and made unique (cov_set); on every wave of the workgroup (cov_sets)
         const int64_t hist_n = L.map_n / 10 + 2;
-        const bool hist_lds = hist_n <= 2 * kSortTile;  // the sort tile is free until build_side
+        const bool hist_lds = hist_n <= 2 * tile;  // the sort tile is free until build_side
         if (hist_lds) {
             for (int64_t i = ln(); i < hist_n; i += 64) reinterpret_cast<int32_t *>(g_sort_lds)[i] = 0;
         }
@@ -1871,7 +1880,7 @@ struct LocusRun {
 #ifdef MANDO_CL_PHASES
         const uint64_t ts0 = clock64();
 #endif
-        if (H <= kSortTile || !count_sort_side(side_i)) sort_u64(d.sk, d.P);
+        if (H <= kSortTile || !count_sort_side(side_i)) sort_u64(d.sk, d.P, tile);
 #ifdef MANDO_CL_PHASES
         const uint64_t ts1 = clock64();
         pc_sd_sort += ts1 - ts0;
@@ -1909,7 +1918,7 @@ struct LocusRun {
         d.ncand = cc;
         for (int64_t i = cc + ln(); i < d.P; i += 64) d.cand[i] = ~0ull;
         wsync();
-        sort_u64(d.cand, pow2ge(cc));
+        sort_u64(d.cand, pow2ge(cc), tile);
 #ifdef MANDO_CL_PHASES
         pc_sd_cand += clock64() - ts2;
 #endif
@@ -2596,7 +2605,7 @@ struct LocusRun {
             B.isort[i] = k;
         }
         wsync();
-        sort_u64(B.isort, pn);
+        sort_u64(B.isort, pn, tile);
         // valid entries and hash-run starts (max-scan of run-start flags)
         int32_t nv = 0, carry = 0;
         for (int i0 = 0; i0 < n; i0 += 64) {
@@ -2640,7 +2649,7 @@ struct LocusRun {
             B.isort[i] = k;
         }
         wsync();
-        sort_u64(B.isort, pn);
+        sort_u64(B.isort, pn, tile);
         for (int i = ln(); i < nv; i += 64) B.msort[i] = (int32_t)(B.isort[i] & 0xffffffu);
         wsync();
         n_members = nv;
@@ -2835,8 +2844,8 @@ struct LocusRun {
                 atomicAdd(&B.ec[mi((int64_t)B.isort[i] - kPosBias)], 1);
             }
             wsync();
-            sort_u64(B.ss, pk);
-            sort_u64(B.isort, pk);
+            sort_u64(B.ss, pk, tile);
+            sort_u64(B.isort, pk, tile);
             ends_side(B.sp, B.sc, B.ss, k, true);
             if (status != kOk) return;
             ends_side(B.ep, B.ec, B.isort, k, false);
@@ -2971,10 +2980,16 @@ struct LocusRun {
     }
 };
 
+#ifdef MANDO_K2_LITE  // dev A/B build: K2 capped at 128 VGPRs (4 waves per SIMD)
+#define MANDO_K2_WPE __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define MANDO_K2_WPE
+#endif
 template <int NW>
-__global__ __launch_bounds__(64 * NW) void cluster_locus(Args G) {
+__global__ __launch_bounds__(64 * NW) MANDO_K2_WPE void cluster_locus(Args G) {
     __shared__ uint32_t mtk[624];
-    __shared__ int32_t lperm[kLdsPerm];
+    constexpr int kPerm = NW > 1 ? kLdsPermBig : kLdsPerm;
+    __shared__ int32_t lperm[kPerm];
     __shared__ MwX mwx;
     const int li = G.order[blockIdx.x];
     Stats *st = G.stats + li;
@@ -2998,6 +3013,8 @@ __global__ __launch_bounds__(64 * NW) void cluster_locus(Args G) {
     R.mt.key = mtk;
     R.mt.pos = 624;
     R.lperm = lperm;
+    R.lperm_cap = kPerm;
+    R.tile = G.sort_tile;
     if (NW > 1 && wv() > 0) {
         R.helper();
         return;
@@ -3041,11 +3058,15 @@ hipError_t launch_parse(const Args &a, int n_blocks, int n_big, int n_work, hipS
 // K2 over the loci a.order[0, n_big) on kMwWaves-wave workgroups, then a.order[n_big, n_blocks) on
 // one wave each
 hipError_t launch_locus(const Args &a, int n_blocks, int n_big, hipStream_t s) {
-    if (n_big > 0) hipLaunchKernelGGL(cluster_locus<kMwWaves>, dim3(n_big), dim3(64 * kMwWaves), kSortTile * 8, s, a);
+    if (n_big > 0) {
+        Args b = a;
+        b.sort_tile = kSortTile;
+        hipLaunchKernelGGL(cluster_locus<kMwWaves>, dim3(n_big), dim3(64 * kMwWaves), kSortTile * 8, s, b);
+    }
     if (n_blocks > n_big) {
         Args b = a;
         b.order = a.order + n_big;
-        hipLaunchKernelGGL(cluster_locus<1>, dim3(n_blocks - n_big), dim3(64), kSortTile * 8, s, b);
+        hipLaunchKernelGGL(cluster_locus<1>, dim3(n_blocks - n_big), dim3(64), b.sort_tile * 8, s, b);
     }
     return hipGetLastError();
 }
@@ -3386,6 +3407,11 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         G.scratch_b = d_b.as<uint8_t>();
         G.out = d_o.as<uint8_t>();
         G.rec_text = d_rec.as<int64_t>();
+        // the one-wave launch's sort tile (its dynamic LDS: 8 bytes a key)
+        G.sort_tile = kSortTile;
+#ifdef MANDO_K2_LITE  // dev A/B build: 4 KB (larger sorts and histograms go through global memory)
+        G.sort_tile = 512;
+#endif
         CL_TRY(launch_locus(G, (int)k2_order.size(), n_big, s));
         uint8_t *ho = nullptr;
         CL_TRY(pinned_host(ctx, 0, (size_t)o_tot + 256, ho));
