@@ -628,6 +628,11 @@ int mando_ctx_create(int device_ordinal, mando_ctx **out) {
     if (device_ordinal < 0 || device_ordinal >= n)
         return fail(MANDO_E_ARG, "device ordinal out of range");
     HIP_TRY(hipSetDevice(device_ordinal));
+    // host threads waiting on the device sleep on the completion signal instead of spinning: one GPU's
+    // waits took ~20 s of CPU per config-4 step (1.6 cores) for no gain in time
+    // (profiles/r05q_ab_blocking_sync.txt), cores the other ranks of a node need (2 per rank at N = 8)
+    (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
+    (void)hipGetLastError();  // (refused when the device was initialised before: keep its flags)
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device_ordinal));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)

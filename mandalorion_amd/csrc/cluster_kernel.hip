@@ -1337,13 +1337,11 @@ __device__ double round3(int64_t best, int64_t cov) {
 // ---------------------------------------------------------------------------------------------
 // K2: one locus
 // ---------------------------------------------------------------------------------------------
-// the static permutation buffer: 8 KB in the one-wave kernel (its LDS limits how many loci share a CU
+// the static permutation buffer: 2 KB in the one-wave kernel (its LDS limits how many loci share a CU
 // with the POA grids), 16 KB in the large-locus kernel (whose permutations reach 7k entries)
-#ifdef MANDO_K2_LITE  // dev A/B build: a one-wave K2 workgroup about as large as a POA workgroup
+// (one-wave: the large loci whose permutations need more run on several waves; a longer one goes to the
+// sort tile's LDS or to global scratch)
 constexpr int kLdsPerm = 512, kLdsPermBig = 4096;
-#else
-constexpr int kLdsPerm = 2048, kLdsPermBig = 4096;
-#endif
 
 struct MwX {
     int32_t op;
@@ -2980,13 +2978,12 @@ struct LocusRun {
     }
 };
 
-#ifdef MANDO_K2_LITE  // dev A/B build: K2 capped at 128 VGPRs (4 waves per SIMD)
-#define MANDO_K2_WPE __attribute__((amdgpu_waves_per_eu(4)))
-#else
-#define MANDO_K2_WPE
-#endif
+// K2 runs beside the POA grids of the chunk before (config 4): at most 128 VGPRs (a POA wave's share of
+// a SIMD) and, one-wave, 9 KB of LDS (a POA workgroup's 10 KB), so a freed POA slot fits a K2
+// workgroup: config 4 12.60 -> 12.23 s per step with the orientation kernel's cap
+// (profiles/r05l_ab_side_kernels_lite.txt; K2 alone 12.69 -> 12.50 s, r05n_ab_k2_lite.txt)
 template <int NW>
-__global__ __launch_bounds__(64 * NW) MANDO_K2_WPE void cluster_locus(Args G) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void cluster_locus(Args G) {
     __shared__ uint32_t mtk[624];
     constexpr int kPerm = NW > 1 ? kLdsPermBig : kLdsPerm;
     __shared__ int32_t lperm[kPerm];
@@ -3407,11 +3404,9 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
         G.scratch_b = d_b.as<uint8_t>();
         G.out = d_o.as<uint8_t>();
         G.rec_text = d_rec.as<int64_t>();
-        // the one-wave launch's sort tile (its dynamic LDS: 8 bytes a key)
-        G.sort_tile = kSortTile;
-#ifdef MANDO_K2_LITE  // dev A/B build: 4 KB (larger sorts and histograms go through global memory)
+        // the one-wave launch's sort tile: 4 KB of dynamic LDS (larger sorts and histograms go through
+        // global memory; the large loci's launch keeps kSortTile)
         G.sort_tile = 512;
-#endif
         CL_TRY(launch_locus(G, (int)k2_order.size(), n_big, s));
         uint8_t *ho = nullptr;
         CL_TRY(pinned_host(ctx, 0, (size_t)o_tot + 256, ho));

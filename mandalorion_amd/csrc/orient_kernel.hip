@@ -647,12 +647,9 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
 }
 
 template <bool G>
-#ifdef MANDO_K2_LITE  // dev A/B build (with the clustering's): at most 128 VGPRs beside the POA grids
-#define MANDO_OR_WPE __attribute__((amdgpu_waves_per_eu(4)))
-#else
-#define MANDO_OR_WPE
-#endif
-__global__ __launch_bounds__(64) MANDO_OR_WPE void orient_kernel(OrientArgs a) {
+// at most 128 VGPRs: the orientation runs beside the POA grids of the chunk before (cluster_kernel.hip,
+// cluster_locus)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void orient_kernel(OrientArgs a) {
     __shared__ OrientLds sh;
     const int lane = lane_id();
     if (lane == 0) {

@@ -132,10 +132,15 @@ def test_mixed_large_and_small_loci(tmp_path):
     synth.write_loci(os.path.join(d, "big", "tmp_SS"), 3, reads=(2100, 2600), exons=(6, 10), exon_len=(60, 200),
                      isoforms=(4, 8), threads=8, seed=31, rev_frac=0.3)
     synth.write_loci(os.path.join(d, "small", "tmp_SS"), 40, reads=(10, 60), threads=8, seed=32, rev_frac=0.3)
+    # one-wave loci whose permutations, sorts and histogram bins outgrow the one-wave kernel's LDS
+    # (global-memory permutation, sort passes and bins)
+    synth.write_loci(os.path.join(d, "mid", "tmp_SS"), 3, reads=(1100, 1900), exons=(6, 10), exon_len=(60, 200),
+                     isoforms=(4, 8), threads=8, seed=33, rev_frac=0.3)
     _, pb, cb, _ = _inputs(os.path.join(d, "big"))
     _, ps, cs, _ = _inputs(os.path.join(d, "small"))
-    n_ok, _ = _compare(ps[:20] + pb + ps[20:], cs[:20] + cb + cs[20:], seed=4)
-    assert n_ok == len(pb) + len(ps)
+    _, pm, cm, _ = _inputs(os.path.join(d, "mid"))
+    n_ok, _ = _compare(ps[:20] + pb + pm + ps[20:], cs[:20] + cb + cm + cs[20:], seed=4)
+    assert n_ok == len(pb) + len(ps) + len(pm)
 
 
 def _edit_lines(src, dst, fn):
