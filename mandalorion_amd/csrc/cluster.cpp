@@ -290,15 +290,18 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     const double t_size = secs();
     for (int64_t i = 0; i < n_loci; ++i) foff[(size_t)i + 1] = foff[(size_t)i] + std::max<int64_t>(0, fsize[(size_t)i]);
     res->text_len = (size_t)foff[(size_t)n_loci];
+    const double t_acq0 = secs();
     res->text_buf = pool().acquire(res->text_len + 64);
+    const double t_acq = secs() - t_acq0;
     res->text_p = res->text_buf.p;
     if (!res->text_p) return mando::set_error(MANDO_E_NOMEM, "cluster: host text buffer");
     // device copy of the text, filled piecewise while later files are still being read
-    hipStream_t stream = mando::ctx_stream(ctx);
+    hipStream_t stream = cl::cluster_stream(ctx);
     size_t d_cap = 0;
     void *d_text = hipSetDevice(mando::ctx_device(ctx)) == hipSuccess
                        ? mando::cl::acquire_text(ctx, res->text_len + 64, d_cap) : nullptr;
     if (!d_text) return mando::set_error(MANDO_E_NOMEM, "cluster: device text buffer");
+    const double t_dacq = secs() - t_acq0 - t_acq;
     res->ctx = ctx;
     res->d_text = d_text;
     res->d_cap = d_cap;
@@ -321,7 +324,16 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
     }
     std::mutex mu;
     std::condition_variable cv;
+    std::atomic<int64_t> reader_ns{0};
     auto reader = [&]() {
+        const auto r0 = std::chrono::steady_clock::now();
+        struct Busy {  // this reader's time, added at its end
+            std::atomic<int64_t> &sum;
+            std::chrono::steady_clock::time_point t0;
+            ~Busy() {
+                sum.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+            }
+        } busy{reader_ns, r0};
         while (true) {
             const int64_t p = next.fetch_add(1);
             if (p >= n_pieces) break;
@@ -426,6 +438,7 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
         }
     };
     int copy_rc = MANDO_OK;
+    double copy_call_s = 0;  // (MANDO_CL_TIME: time inside the copy calls)
     {
         vector<std::thread> th;
         for (int t = 0; t < nth; ++t) th.emplace_back(reader);
@@ -446,8 +459,11 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
             // a sub-batch's last file read: its text goes out now, whatever the piece size
             const bool edge = nsub > 1 && copied < nsub && upto >= bounds[(size_t)copied + 1];
             if (avail - sent >= kPiece || (edge && avail > sent) || (upto == n_loci && avail > sent)) {
-                if (hipMemcpyAsync((char *)d_text + sent, res->text_p + sent, (size_t)(avail - sent),
-                                   hipMemcpyHostToDevice, cstream) != hipSuccess) {
+                const auto tc0 = std::chrono::steady_clock::now();
+                const hipError_t ce = hipMemcpyAsync((char *)d_text + sent, res->text_p + sent, (size_t)(avail - sent),
+                                                     hipMemcpyHostToDevice, cstream);
+                copy_call_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tc0).count();
+                if (ce != hipSuccess) {
                     copy_rc = mando::set_error(MANDO_E_HIP, "cluster: text copy to the device");
                     break;
                 }
@@ -604,8 +620,10 @@ int mando_cluster_loci(mando_ctx *ctx, const mando_cluster_params *prm, const ch
         }
     }
     if (timing)
-        fprintf(stderr, "[cluster] %lld loci, %.1f MB: sizes %.3f s, read + copy %.3f s, kernels %.3f s, flatten %.3f s\n",
-                (long long)n_loci, res->text_len / 1e6, t_size, t_read - t_size, t_gpu - t_read, secs() - t_gpu);
+        fprintf(stderr, "[cluster] %lld loci, %.1f MB: sizes %.3f s, read + copy %.3f s (buffers %.3f + %.3f s, "
+                        "readers %.3f s each on %d threads, copy calls %.3f s), kernels %.3f s, flatten %.3f s\n",
+                (long long)n_loci, res->text_len / 1e6, t_size, t_read - t_size, t_acq, t_dacq,
+                reader_ns.load() * 1e-9 / std::max(1, nth), nth, copy_call_s, t_gpu - t_read, secs() - t_gpu);
     *out = res.release();
     return MANDO_OK;
 }

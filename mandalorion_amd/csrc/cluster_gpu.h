@@ -157,6 +157,8 @@ CL_HD inline int64_t scratch_a_bytes(int64_t line_cap, int64_t op_cap, int64_t b
 }
 
 int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out);
+// the stream the clustering of ctx runs on (its kernels and the copies they wait for)
+hipStream_t cluster_stream(mando_ctx *ctx);
 // the device copy of the locus text (cached whole buffers; the result keeps one until it is freed)
 void *acquire_text(mando_ctx *ctx, size_t need, size_t &cap);
 void release_text(mando_ctx *ctx, void *d_text, size_t cap);
