@@ -3443,23 +3443,9 @@ int cluster_gpu(mando_ctx *ctx, const ClusterIn &in, ClusterOut &out) {
     return MANDO_OK;
 }
 
-hipStream_t cluster_stream(mando_ctx *ctx) {
-#ifdef MANDO_CL_PRIO  // dev A/B build: the clustering kernels on a high-priority stream per device
-    static std::mutex mu;
-    static std::vector<hipStream_t> streams;
-    const int dev = mando::ctx_device(ctx);
-    std::lock_guard<std::mutex> g(mu);
-    if ((int)streams.size() <= dev) streams.resize((size_t)dev + 1, nullptr);
-    if (!streams[(size_t)dev]) {
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if (hipStreamCreateWithPriority(&streams[(size_t)dev], hipStreamNonBlocking, hi) != hipSuccess)
-            streams[(size_t)dev] = nullptr;
-    }
-    if (streams[(size_t)dev]) return streams[(size_t)dev];
-#endif
-    return mando::ctx_stream(ctx);
-}
+// (a high-priority stream of its own was measured neutral: profiles/r05v_ab_cluster_priority.txt; so was
+// a hardware queue of its own, r05w_ab_hw_queues.txt)
+hipStream_t cluster_stream(mando_ctx *ctx) { return mando::ctx_stream(ctx); }
 
 void *acquire_text(mando_ctx *ctx, size_t need, size_t &cap) {
     const int dev = mando::ctx_device(ctx);
