@@ -2103,7 +2103,10 @@ __device__ __forceinline__ void w2_helper(SharedState &sh, int lane) {
 // run_dp16 / row16_vec exactly (same band, masks, traceback and predecessor bytes, ring and spill
 // planes, row records); tests/test_poa_gpu.py compares the bytes with the oracle.
 // The loop leaves at the batch end or at the first row it does not take (the C++ row handles it):
-// nothing of that row has been written then.  Hazards (gfx950) are padded inside the string: DPP
+// nothing of that row has been written then.  The next row's descriptor words are read from the LDS
+// batch once the row's traceback is stored (into the registers the row is done with), so the row head
+// finds them loaded instead of waiting on the LDS round trip; at the batch end that read is past the
+// batch and unused, and the loop drains it before it leaves.  Hazards (gfx950) are padded inside the string: DPP
 // reads two wait states after a VALU write, v_readlane after the scans, VMEM reads of SGPRs written
 // by a VALU before the block (s_nop 4).  Exec is the whole wave here (run_dp16 runs wave-uniform);
 // the row records are stored with exec = lane 0 and exec is restored to all lanes.
@@ -2197,9 +2200,6 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_and_b32 %[x], %[pr], 7\n"
             "s_mulk_i32 %[x], 0x300\n"
             "s_add_u32 %[pwb], %[x], %[Lring]\n"
-            "L_top%=:\n"
-            "s_cmp_ge_i32 %[i], %[iend]\n"
-            "s_cbranch_scc1 L_out%=\n"
             "s_lshl_b32 %[x], %[i], 5\n"
             "s_add_u32 %[x], %[x], %[Ldesc]\n"
             "v_mov_b32 %[Ga], %[x]\n"
@@ -2207,6 +2207,9 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "ds_read_b32 %[Pa], %[Ga] offset:8\n"
             "ds_read_b32 %[Pb], %[Ga] offset:12\n"
             "ds_read_b32 %[inc], %[Ga] offset:16\n"
+            "L_top%=:\n"
+            "s_cmp_ge_i32 %[i], %[iend]\n"
+            "s_cbranch_scc1 L_out%=\n"
             "s_waitcnt lgkmcnt(0)\n"
             "v_readfirstlane_b32 %[d1], %[Gb]\n"
             "v_readfirstlane_b32 %[p0], %[Pb]\n"
@@ -2369,6 +2372,13 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "v_or_b32_sdwa %[amk], %[amk], %[amk] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
             "v_add_u32 %[voff], %[tbu], %[vlane2]\n"
             "global_store_short %[voff], %[amk], %[tbp]\n"
+            "s_lshl_b32 %[x], %[i], 5\n"
+            "s_add_u32 %[x], %[x], %[Ldesc]\n"
+            "v_mov_b32 %[Ga], %[x]\n"
+            "ds_read_b32 %[Gb], %[Ga] offset:36\n"
+            "ds_read_b32 %[Pa], %[Ga] offset:40\n"
+            "ds_read_b32 %[Pb], %[Ga] offset:44\n"
+            "ds_read_b32 %[inc], %[Ga] offset:48\n"
             "v_bfi_b32 %[Hd], %[inv], %[vkneg], %[H]\n"
             "v_bfi_b32 %[m1], %[inv], %[vkneg], %[E1]\n"
             "v_bfi_b32 %[m2], %[inv], %[vkneg], %[E2]\n"
@@ -2690,6 +2700,13 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "v_or_b32_sdwa %[amk], %[amk], %[amk] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
             "v_add_u32 %[voff], %[tbu], %[vlane2]\n"
             "global_store_short %[voff], %[amk], %[tbp]\n"
+            "s_lshl_b32 %[x], %[i], 5\n"
+            "s_add_u32 %[x], %[x], %[Ldesc]\n"
+            "v_mov_b32 %[Ga], %[x]\n"
+            "ds_read_b32 %[Gb], %[Ga] offset:36\n"
+            "ds_read_b32 %[Pa], %[Ga] offset:40\n"
+            "ds_read_b32 %[Pb], %[Ga] offset:44\n"
+            "ds_read_b32 %[inc], %[Ga] offset:48\n"
             "v_lshlrev_b32 %[K1], 2, %[K1]\n"
             "v_lshlrev_b32 %[K2], 4, %[K2]\n"
             "v_or3_b32 %[MK], %[MK], %[K1], %[K2]\n"
@@ -2791,6 +2808,7 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_add_i32 %[i], %[i], 1\n"
             "s_branch L_top%=\n"
             "L_out%=:\n"
+            "s_waitcnt lgkmcnt(0)\n"
             "s_sub_i32 %[x], %[i], %[i0]\n"
             "s_add_i32 %[cel], %[cel], %[x]\n"
             "s_nop 1\n"
