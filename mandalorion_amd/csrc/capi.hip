@@ -153,7 +153,7 @@ struct mando_ctx {
     DevBuf gorder_w;                                                       // wide-launch groups
     DevBuf g_off, g_len, g_rc, g_dst;                                      // segment gather
     DevBuf cons_txt;                                                       // decoded consensi
-    DevBuf o_scratch;                                                      // long-read orientation slabs
+    DevBuf o_scratch;                                                      // orientation slabs (per wave)
     // extra POA lanes: a batch's launches of different kinds (narrow, wide, seeded) run side by side,
     // each with its own stream and workspace
     hipStream_t lane_stream[2] = {nullptr, nullptr};
@@ -1150,6 +1150,10 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
         const int64_t ng = first ? n_groups : (int64_t)redo.size();
         a.n_groups = (int32_t)ng;
         const int slots = (int)std::min<int64_t>(ng, (int64_t)ctx->n_cu * mando::orient_blocks_per_cu(a.cap));
+        // one HBM slab per launched wave: the reference keys and chain table, or (past the LDS capacity)
+        // every per-read array
+        if ((rc = ctx->o_scratch.ensure((size_t)slots * mando::orient_slab_words(a.cap) * 8)) != MANDO_OK) return rc;
+        a.gscratch = ctx->o_scratch.as<uint64_t>();
         HIP_TRY(hipMemsetAsync(ctx->counter.p, 0, sizeof(int32_t), ctx->stream));
         HIP_TRY(mando::launch_orient(a, slots, ctx->stream));
         ++ctx->last_launches;
@@ -1185,10 +1189,6 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
             int cap2 = a.cap * 2;
             while (cap2 < mando::kOrientCapMax && ml * 26 / 110 > cap2) cap2 *= 2;
             a.cap = cap2;
-            const int64_t slots = std::min<int64_t>((int64_t)redo.size(), (int64_t)ctx->n_cu * mando::orient_blocks_per_cu(a.cap));
-            if ((rc = ctx->o_scratch.ensure((size_t)slots * (size_t)(3 * (int64_t)a.cap + a.cap / 64) * 8)) != MANDO_OK)
-                return rc;
-            a.gscratch = ctx->o_scratch.as<uint64_t>();
         }
     }
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));

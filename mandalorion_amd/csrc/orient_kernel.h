@@ -20,11 +20,13 @@ struct OrientArgs {
     int32_t *counter;         // work-queue head (zeroed before launch)
     const int32_t *gidx;      // optional: the group indices to process (a re-run of overflowed groups)
     int32_t cap;              // per-read capacity of this launch (power of two; > kOrientCap: HBM slabs)
-    uint64_t *gscratch;       // HBM slabs, (3 * cap + cap / 64) words per launched block (cap > kOrientCap)
+    uint64_t *gscratch;       // per launched block an HBM slab of orient_slab_words(cap) words: the
+                              // reference keys and the chain table (cap <= kOrientCap), or every array
 };
 
 size_t orient_dyn_bytes(int cap);
 int orient_blocks_per_cu(int cap);
+size_t orient_slab_words(int cap);
 hipError_t launch_orient(const OrientArgs &a, int n_slots, hipStream_t stream);
 
 }  // namespace mando

@@ -8,18 +8,19 @@
 // extraction and mask_level-0.5 primary selection (see oracle/orient_ref.c for the exact rules and
 // the known differences from minimap2; parity with mappy itself is unpinned).
 //
-// Layout: one 64-lane wave per isoform group (persistent over groups); everything stays in LDS.
-// The two per-read arrays hold `cap` entries (a power of two chosen per launch, 1024 for R2C2-length
-// reads: 16 KB of dynamic LDS, so 8 waves fit per CU, the VGPR limit; groups that overflow are re-run
-// by the host at the next capacity):
-//   refk  sorted reference minimizer keys  (h << 33 | pos << 1 | strand)          8 B x cap
+// Layout: one 64-lane wave per isoform group (persistent over groups).  Two per-read arrays hold `cap`
+// entries (a power of two chosen per launch, 1024 for R2C2-length reads; groups that overflow are
+// re-run by the host at the next capacity):
+//   refk  sorted reference minimizer keys  (h << 33 | pos << 1 | strand)   8 B x cap, the wave's HBM slab
 //   an    anchor keys (rev << 62 | x << 31 | y), bitonic-sorted in LDS; after the chaining DP each
-//         slot is rewritten as used << 63 | f << 48 | (p + 1) << 32 | rev << 31 | y   8 B x cap
+//         slot is rewritten as used << 63 | f << 48 | (p + 1) << 32 | rev << 31 | y   8 B x cap, dynamic LDS
+// With the keys in HBM (a bucket index over their top hash bits stays in LDS) a wave takes 10 KB of
+// LDS and 16 waves fit per CU, the VGPR limit (both arrays in LDS: 20 KB, 8 waves; 1.47x slower).
 // The query's minimizers are not stored: each 64-position batch of them is looked up in refk as it is
 // found and its anchors appended.  Beyond kOrientCap (2048, ~10 kb reads) the same code runs with the
-// arrays in a per-wave HBM slab (orient_kernel<true>), with f[] / p[] and a used bitmap of their own,
+// anchors in the HBM slab too (orient_kernel<true>), with f[] / p[] and a used bitmap of their own,
 // so long reads are oriented instead of refused.
-// Minimizers are computed in 256-position tiles (k-mer hashes -> window minima -> marks -> ballot
+// Minimizers are computed in 128-position tiles (k-mer hashes -> window minima -> marks -> ballot
 // compaction); the chaining DP is sequential over anchors with the 64-anchor look-back spread over the
 // 64 lanes and a DPP max-reduction per anchor.
 #include <hip/hip_runtime.h>
@@ -31,8 +32,11 @@ namespace mando {
 namespace {
 
 constexpr int K = 15, W = 10, MAX_OCC = 10, MAX_GAP = 5000, BW = 500, MIN_CNT = 3, MIN_SCORE = 40;
-constexpr int TILE = 256;
+// 128-position minimizer tiles: the tile buffers are half of a 256-position tile's, which with the
+// keys in HBM brings a wave to 10 KB of LDS (16 waves per CU; 256: 14, 62.0 against 58.0 ms)
+constexpr int TILE = 128;
 constexpr int MAXCH = 64;
+constexpr int kChWords = 4 * MAXCH / 2;  // the chain table in 64-bit words (slabs of the LDS variant: cap + kChWords)
 constexpr int kBucketShift = 2 * K - 8, kBuckets = 1 << 8;  // refk index over the top 8 hash bits
 constexpr uint64_t INF = ~0ull;
 constexpr uint32_t INF32 = ~0u;
@@ -53,7 +57,6 @@ struct OrientLds {
     uint64_t nm[NNM];           // staged non-ACGT mask
     uint32_t hb[TILE + 2 * W];  // (hash << 1 | z) of the tile's k-mers (30-bit hashes), INF32 when invalid
     uint32_t mb[TILE + W];      // window minima (hash only)
-    int32_t ch_score[MAXCH], ch_rev[MAXCH], ch_qs[MAXCH], ch_qe[MAXCH];
     int32_t misc[8];
     uint16_t bst[kBuckets + 1];  // LDS variant: first refk index of each top-8-bit hash bucket
 #ifdef MANDO_ORIENT_PROF
@@ -77,18 +80,14 @@ extern __shared__ __attribute__((aligned(16))) uint64_t g_orient_dyn[];  // 2 * 
 // views into the dynamic buffer (LDS address space kept: the base is the LDS symbol itself)
 // G: the arrays live in a per-wave HBM slab (reads beyond the LDS capacity) instead of dynamic LDS
 __device__ __forceinline__ int o_cap(const OrientLds &sh) { return __builtin_amdgcn_readfirstlane(sh.cap); }
+// the reference keys: always in the wave's HBM slab (read by the query lookups, a few dependent loads
+// per 64 query positions); the anchors: in dynamic LDS, or (G) in the slab past the keys.  With only
+// the anchors in LDS a wave takes 10 KB instead of 20 KB: 16 waves per CU instead of 8 (orientation
+// kernel 85.6 -> 58 ms on 32,000 groups x 25 reads x 3 kb, profiles/r06f_ab_orient_ref_hbm.txt)
 template <bool G>
-__device__ __forceinline__ uint64_t *o_base(const OrientLds &sh) {
-    if constexpr (G) {
-        return sh.gdyn;
-    } else {
-        return g_orient_dyn;
-    }
-}
+__device__ __forceinline__ uint64_t *o_refk(const OrientLds &sh) { return sh.gdyn; }
 template <bool G>
-__device__ __forceinline__ uint64_t *o_refk(const OrientLds &sh) { return o_base<G>(sh); }
-template <bool G>
-__device__ __forceinline__ uint64_t *o_an(const OrientLds &sh) { return o_base<G>(sh) + (G ? 2 : 1) * o_cap(sh); }
+__device__ __forceinline__ uint64_t *o_an(const OrientLds &sh) { return G ? sh.gdyn + 2 * o_cap(sh) : g_orient_dyn; }
 // HBM variant only: f[] / p[] of the chaining DP and the used bitmap
 __device__ __forceinline__ int32_t *o_f(const OrientLds &sh) { return reinterpret_cast<int32_t *>(sh.gdyn + o_cap(sh)); }
 __device__ __forceinline__ int32_t *o_p(const OrientLds &sh) { return o_f(sh) + o_cap(sh); }
@@ -416,9 +415,12 @@ __device__ __forceinline__ int lower_bound_h(const uint64_t *a, int lo, int hi, 
 __device__ __forceinline__ int ilog2_u32(uint32_t v) { return 31 - __clz((int)v); }
 
 // one query read; returns 0 or -1 (over CAP)
+// ch: the extracted chains' score / strand / query start / query end, MAXCH each (LDS, or the wave's
+// HBM slab: lane 0 alone writes and reads them)
 template <bool G>
-__device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t qlen, int8_t *hits, int max_hits,
-                           int32_t *n_hits, int lane) {
+__device__ int orient_read(OrientLds &sh, int32_t *ch, int nref, const uint8_t *q, int64_t qlen, int8_t *hits,
+                           int max_hits, int32_t *n_hits, int lane) {
+    int32_t *ch_score = ch, *ch_rev = ch + MAXCH, *ch_qs = ch + 2 * MAXCH, *ch_qe = ch + 3 * MAXCH;
     const uint64_t *refk = o_refk<G>(sh);
     uint64_t *an = o_an<G>(sh);
     const int cap = o_cap(sh);
@@ -589,11 +591,11 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
                     // G: anchor keys (rev << 62 | x << 31 | y); LDS: slots (rev << 31 | y)
                     const uint64_t sb = an[bi], sf = an[first];
                     const int rev = G ? (int)(sb >> 62) : (int)((sb >> 31) & 1);
-                    sh.ch_score[nch] = score;
-                    sh.ch_rev[nch] = rev;
+                    ch_score[nch] = score;
+                    ch_rev[nch] = rev;
                     const int ys = (int)(sf & 0x7fffffff) - K + 1, ye = (int)(sb & 0x7fffffff) + 1;
-                    sh.ch_qs[nch] = rev ? (int)qlen - ye : ys;
-                    sh.ch_qe[nch] = rev ? (int)qlen - ys : ye;
+                    ch_qs[nch] = rev ? (int)qlen - ye : ys;
+                    ch_qe[nch] = rev ? (int)qlen - ys : ye;
                     ok = 1;
                 }
             }
@@ -611,7 +613,7 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         int idx[MAXCH];
         for (int c = 0; c < nch; ++c) {
             int t = c;
-            while (t > 0 && sh.ch_score[idx[t - 1]] < sh.ch_score[c]) {
+            while (t > 0 && ch_score[idx[t - 1]] < ch_score[c]) {
                 idx[t] = idx[t - 1];
                 --t;
             }
@@ -623,7 +625,7 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
         int pqs[9], pqe[9];
         for (int c = 0; c < nch && np <= max_hits && np < 9; ++c) {
             const int id = idx[c];
-            const int qs = sh.ch_qs[id], qe = sh.ch_qe[id];
+            const int qs = ch_qs[id], qe = ch_qe[id];
             bool prim = true;
             for (int t = 0; t < np; ++t) {
                 const int ov = min(qe, pqe[t]) - max(qs, pqs[t]);
@@ -636,7 +638,7 @@ __device__ int orient_read(OrientLds &sh, int nref, const uint8_t *q, int64_t ql
             if (!prim) continue;
             pqs[np] = qs;
             pqe[np] = qe;
-            if (np < max_hits) hits[np] = sh.ch_rev[id] ? -1 : 1;
+            if (np < max_hits) hits[np] = ch_rev[id] ? -1 : 1;
             ++np;
         }
         *n_hits = np;
@@ -658,7 +660,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void or
         sh.tlast = wall_clock64();
 #endif
         sh.cap = a.cap;
-        sh.gdyn = G ? a.gscratch + (int64_t)blockIdx.x * (3 * (int64_t)a.cap + a.cap / 64) : nullptr;
+        sh.gdyn = a.gscratch + (int64_t)blockIdx.x * (G ? 3 * (int64_t)a.cap + a.cap / 64 : (int64_t)a.cap + kChWords);
+    }
+    int32_t *ch;
+    if constexpr (G) {
+        __shared__ int32_t ch_lds[4 * MAXCH];
+        ch = ch_lds;
+    } else {
+        ch = reinterpret_cast<int32_t *>(a.gscratch + (int64_t)blockIdx.x * ((int64_t)a.cap + kChWords) + a.cap);
     }
     wsync();
     for (;;) {
@@ -686,6 +695,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void or
                 st = -1;
             } else {
                 bitonic_sort(o_refk<G>(sh), nref, lane);
+                // (HBM keys: the sorted stores complete before any lane reads another lane's keys)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 OPROF(6)
                 if constexpr (!G) {
                     for (int b = lane; b <= kBuckets; b += 64)
@@ -693,7 +704,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void or
                     wsync();
                 }
                 for (int64_t r = r0; r < r1; ++r) {
-                    const int rc = orient_read<G>(sh, nref, a.seq + a.seq_off[r], a.seq_off[r + 1] - a.seq_off[r],
+                    const int rc = orient_read<G>(sh, ch, nref, a.seq + a.seq_off[r], a.seq_off[r + 1] - a.seq_off[r],
                                                a.hits + r * a.max_hits, a.max_hits, a.n_hits + r, lane);
                     if (rc < 0) {
                         st = -1;
@@ -719,18 +730,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void or
 
 }  // namespace
 
-size_t orient_dyn_bytes(int cap) { return (size_t)(2 * cap) * sizeof(uint64_t); }
+size_t orient_dyn_bytes(int cap) { return (size_t)cap * sizeof(uint64_t); }
 
 int orient_blocks_per_cu(int cap) {
     int nb = 0;
-    if (cap > kOrientCap) {  // HBM variant: no dynamic LDS
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, orient_kernel<true>, 64, 0) != hipSuccess || nb < 1) nb = 1;
-        return nb;
-    }
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, orient_kernel<false>, 64, orient_dyn_bytes(cap)) != hipSuccess ||
-        nb < 1)
-        nb = 1;
+    const hipError_t e = cap > kOrientCap  // HBM variant: no dynamic LDS
+                             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, orient_kernel<true>, 64, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, orient_kernel<false>, 64,
+                                                                            orient_dyn_bytes(cap));
+    if (e != hipSuccess || nb < 1) nb = 1;
     return nb;
+}
+
+size_t orient_slab_words(int cap) {
+    return cap > kOrientCap ? 3 * (size_t)cap + (size_t)cap / 64 : (size_t)cap + kChWords;
 }
 
 hipError_t launch_orient(const OrientArgs &a, int n_slots, hipStream_t stream) {
