@@ -187,8 +187,13 @@ DevBuf &kind_ws(mando_ctx *ctx, int kind) { return kind == 0 ? ctx->ws : ctx->la
 
 constexpr int kMaxWavesPerCu = 16;  // upper bound on resident POA waves per CU
 // groups whose band 2w + 1 (at their mean read length) is wider than this run in the wide-ring
-// launch: their rows mostly exceed one 128-column chunk (the band also drifts with the argmax)
-constexpr int64_t kWideBand = 112;
+// launch: their rows mostly exceed one 128-column chunk (the band also drifts with the argmax).  Below
+// it a group runs on one wave (16 per CU) with rows of one chunk; a row that drifts past the chunk
+// takes the generic row.  Config 4 per step (profiles/r06k_ab_wide_band.txt): 96: 16.7 s, 104: 14.1,
+// 108: 15.0, 112: 12.0-12.4, 114-118: 11.7-11.9, 120: 12.1, 124: 13.9, 140: 19.5 -- the bands 113 and
+// 115 (mean reads of 4.6-4.8 kb) still fit a chunk often enough to be cheaper on one wave than on the
+// two-wave wide kernel (8 waves per CU)
+constexpr int64_t kWideBand = 116;
 #ifndef MANDO_WS_SHARE
 #define MANDO_WS_SHARE 0.8
 #endif

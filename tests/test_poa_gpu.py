@@ -122,6 +122,14 @@ def test_grid_modes_and_launch_kinds(gpu_ctx, persistent):
         ctx.set_poa_budget(0)
 
 
+def test_narrow_groups_at_the_band_threshold(gpu_ctx):
+    """Mean reads of 4.5-5.0 kb: bands 2w + 1 of 111-121 columns, on both sides of the narrow / wide split
+    (kWideBand); the narrow ones (113, 115) run rows of one chunk whose drift past 128 columns takes the
+    generic row and its HBM spill.  Same consensi as the restatement."""
+    _, groups = poa_cases.noisy_groups(12, (4500, 5000), (4, 8), seed=84)
+    _check(groups)
+
+
 @pytest.mark.parametrize("waves", ["0", "2"])
 def test_wide_launch_waves_per_group(monkeypatch, waves):
     """Wide launches with one or two waves per group (MANDO_POA_W2=0: one wave; 2, the default: every
