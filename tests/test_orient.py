@@ -134,3 +134,16 @@ def test_orient_gpu_reads_beyond_lds_capacity(gpu_ctx):
     truth = short_truth[:4] + long_truth + short_truth[4:]
     got = orient.orient_batch(groups)
     assert got == oref.orient_batch(groups) == truth
+
+
+@pytest.mark.gpu
+def test_orient_gpu_more_groups_than_waves(gpu_ctx):
+    """More groups than the launch has waves (4,096 on MI355X at 16 per CU), so every wave reuses its HBM
+    slab of reference keys for several groups: same hit lists as the restatement."""
+    from mandalorion_amd import orient
+    from oracle import orient as oref
+
+    groups, truth = _groups(9000, 61, lens=(300, 700), depth=(2, 4), unrelated=False)
+    got = orient.orient_batch(groups)
+    assert got == oref.orient_batch(groups)
+    assert got == truth
