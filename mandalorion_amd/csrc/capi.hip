@@ -1132,6 +1132,7 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
     a.gidx = nullptr;
     a.cap = cap;
     a.gscratch = nullptr;
+    a.cap_fb = cap < mando::kOrientCap ? mando::kOrientCap : 0;
     std::vector<int32_t> st((size_t)n_groups);
     std::vector<int32_t> redo;
     // the first launch takes the groups largest first (bases of the group's reads): the waves pull
@@ -1157,7 +1158,8 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
         const int slots = (int)std::min<int64_t>(ng, (int64_t)ctx->n_cu * mando::orient_blocks_per_cu(a.cap));
         // one HBM slab per launched wave: the reference keys and chain table, or (past the LDS capacity)
         // every per-read array
-        if ((rc = ctx->o_scratch.ensure((size_t)slots * mando::orient_slab_words(a.cap) * 8)) != MANDO_OK) return rc;
+        if ((rc = ctx->o_scratch.ensure((size_t)slots * mando::orient_slab_words(a.cap, a.cap_fb) * 8)) != MANDO_OK)
+            return rc;
         a.gscratch = ctx->o_scratch.as<uint64_t>();
         HIP_TRY(hipMemsetAsync(ctx->counter.p, 0, sizeof(int32_t), ctx->stream));
         HIP_TRY(mando::launch_orient(a, slots, ctx->stream));
@@ -1176,6 +1178,9 @@ int orient_impl(mando_ctx *ctx, const std::vector<int64_t> &soff, const int64_t 
         }
         first = false;
         if (redo.empty()) break;
+        // (over the in-kernel fallback's capacity too: the re-run starts past it)
+        if (a.cap_fb > a.cap) a.cap = a.cap_fb;
+        a.cap_fb = 0;
         if (a.cap >= mando::kOrientCapMax)
             return fail(MANDO_E_UNSUPPORTED, "orientation: group " + std::to_string(redo[0]) + " has a read with more than " +
                                                  std::to_string(mando::kOrientCapMax) + " minimizers or anchors");

@@ -20,13 +20,15 @@ struct OrientArgs {
     int32_t *counter;         // work-queue head (zeroed before launch)
     const int32_t *gidx;      // optional: the group indices to process (a re-run of overflowed groups)
     int32_t cap;              // per-read capacity of this launch (power of two; > kOrientCap: HBM slabs)
-    uint64_t *gscratch;       // per launched block an HBM slab of orient_slab_words(cap) words: the
-                              // reference keys and the chain table (cap <= kOrientCap), or every array
+    uint64_t *gscratch;       // per launched block an HBM slab of orient_slab_words(cap, cap_fb) words:
+                              // the reference keys and the chain table (cap <= kOrientCap), or every array
+    int32_t cap_fb;           // cap <= kOrientCap: a group over `cap` is re-run at once in the kernel with
+                              // every array in the slab at this capacity (0: left to a host re-run)
 };
 
 size_t orient_dyn_bytes(int cap);
 int orient_blocks_per_cu(int cap);
-size_t orient_slab_words(int cap);
+size_t orient_slab_words(int cap, int cap_fb);
 hipError_t launch_orient(const OrientArgs &a, int n_slots, hipStream_t stream);
 
 }  // namespace mando

@@ -99,6 +99,13 @@ __device__ __forceinline__ int slot_p(uint64_t s) { return (int)((s >> 32) & 0xf
 static_assert(kOrientCap * K < (1 << 15) && kOrientCap < (1 << 16), "packed f / p fields");
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+// words of a wave's HBM slab: every array at `cap` (cap > kOrientCap), else the keys at cap, plus the
+// arrays of the in-kernel fallback at cap_fb (0: none) and the chain table
+__host__ __device__ __forceinline__ int64_t slab_words(int cap, int cap_fb) {
+    if (cap > kOrientCap) return 3 * (int64_t)cap + cap / 64;
+    const int64_t keys = cap_fb > 0 ? 3 * (int64_t)cap_fb + cap_fb / 64 : (int64_t)cap;
+    return keys + kChWords;
+}
 // the workgroup is one wave, and a wave's LDS accesses complete in order: waiting for its own LDS
 // traffic (with a compiler memory barrier) is the whole sync.  __syncthreads() would also wait for
 // every outstanding global load (its workgroup-scope fence), e.g. the next tile's bases.
@@ -648,26 +655,65 @@ __device__ int orient_read(OrientLds &sh, int32_t *ch, int nref, const uint8_t *
     return 0;
 }
 
+// one group: 0, or -1 when a read is over the capacity o_cap(sh) (its outputs are then rewritten in full
+// by the re-run)
+template <bool G>
+__device__ int orient_group(OrientLds &sh, int32_t *ch, const OrientArgs &a, int g, int lane) {
+    const int64_t r0 = a.grp_off[g], r1 = a.grp_off[g + 1];
+    if (r1 <= r0) return 0;
+    uint64_t *refk = o_refk<G>(sh);
+    int nref = 0;
+    const bool fits = minimizers(sh, a.seq + a.seq_off[r0], a.seq_off[r0 + 1] - a.seq_off[r0], lane,
+                                 [&](bool mark, uint64_t key) -> bool {
+                                     const unsigned long long m = __ballot(mark);
+                                     const int cnt = __popcll(m);
+                                     if (nref + cnt > o_cap(sh)) return false;
+                                     if (mark) refk[nref + __popcll(m & lanemask_lt(lane))] = key;
+                                     nref += cnt;
+                                     return true;
+                                 });
+    wsync();
+    if (!fits) return -1;
+    bitonic_sort(o_refk<G>(sh), nref, lane);
+    // (HBM keys: the sorted stores complete before any lane reads another lane's keys)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    OPROF(6)
+    if constexpr (!G) {
+        for (int b = lane; b <= kBuckets; b += 64)
+            sh.bst[b] = (uint16_t)lower_bound_h(refk, 0, nref, (uint64_t)b << kBucketShift);
+        wsync();
+    }
+    for (int64_t r = r0; r < r1; ++r) {
+        const int rc = orient_read<G>(sh, ch, nref, a.seq + a.seq_off[r], a.seq_off[r + 1] - a.seq_off[r],
+                                      a.hits + r * a.max_hits, a.max_hits, a.n_hits + r, lane);
+        if (rc < 0) return -1;
+    }
+    return 0;
+}
+
 template <bool G>
 // at most 128 VGPRs: the orientation runs beside the POA grids of the chunk before (cluster_kernel.hip,
 // cluster_locus)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void orient_kernel(OrientArgs a) {
     __shared__ OrientLds sh;
     const int lane = lane_id();
+    // the wave's HBM slab: G's arrays at a.cap; the LDS variant's keys, its fallback's arrays at a.cap_fb
+    // and the chain table at the end
+    const int64_t slab = slab_words(a.cap, G ? 0 : a.cap_fb);
     if (lane == 0) {
 #ifdef MANDO_ORIENT_PROF
         for (int k = 0; k < 8; ++k) sh.prof[k] = 0;
         sh.tlast = wall_clock64();
 #endif
         sh.cap = a.cap;
-        sh.gdyn = a.gscratch + (int64_t)blockIdx.x * (G ? 3 * (int64_t)a.cap + a.cap / 64 : (int64_t)a.cap + kChWords);
+        sh.gdyn = a.gscratch + (int64_t)blockIdx.x * slab;
     }
     int32_t *ch;
     if constexpr (G) {
         __shared__ int32_t ch_lds[4 * MAXCH];
         ch = ch_lds;
     } else {
-        ch = reinterpret_cast<int32_t *>(a.gscratch + (int64_t)blockIdx.x * ((int64_t)a.cap + kChWords) + a.cap);
+        ch = reinterpret_cast<int32_t *>(a.gscratch + (int64_t)blockIdx.x * slab + slab - kChWords);
     }
     wsync();
     for (;;) {
@@ -676,41 +722,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void or
         gi = __builtin_amdgcn_readfirstlane(gi);
         if (gi >= a.n_groups) break;
         const int g = a.gidx ? __builtin_amdgcn_readfirstlane(a.gidx[gi]) : gi;
-        const int64_t r0 = a.grp_off[g], r1 = a.grp_off[g + 1];
-        int st = 0;
-        if (r1 > r0) {
-            uint64_t *refk = o_refk<G>(sh);
-            int nref = 0;
-            const bool fits = minimizers(sh, a.seq + a.seq_off[r0], a.seq_off[r0 + 1] - a.seq_off[r0], lane,
-                                         [&](bool mark, uint64_t key) -> bool {
-                                             const unsigned long long m = __ballot(mark);
-                                             const int cnt = __popcll(m);
-                                             if (nref + cnt > o_cap(sh)) return false;
-                                             if (mark) refk[nref + __popcll(m & lanemask_lt(lane))] = key;
-                                             nref += cnt;
-                                             return true;
-                                         });
-            wsync();
-            if (!fits) {
-                st = -1;
-            } else {
-                bitonic_sort(o_refk<G>(sh), nref, lane);
-                // (HBM keys: the sorted stores complete before any lane reads another lane's keys)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                OPROF(6)
-                if constexpr (!G) {
-                    for (int b = lane; b <= kBuckets; b += 64)
-                        sh.bst[b] = (uint16_t)lower_bound_h(refk, 0, nref, (uint64_t)b << kBucketShift);
-                    wsync();
-                }
-                for (int64_t r = r0; r < r1; ++r) {
-                    const int rc = orient_read<G>(sh, ch, nref, a.seq + a.seq_off[r], a.seq_off[r + 1] - a.seq_off[r],
-                                               a.hits + r * a.max_hits, a.max_hits, a.n_hits + r, lane);
-                    if (rc < 0) {
-                        st = -1;
-                        break;
-                    }
-                }
+        int st = orient_group<G>(sh, ch, a, g, lane);
+        if constexpr (!G) {
+            // over the LDS capacity: the group again at once with every array in the slab (capacity
+            // a.cap_fb), instead of in a re-run launch after this one (a few long-read groups, one wave
+            // each: 10-30 ms per config-4 chunk on the pipeline's critical path)
+            if (st != 0 && a.cap_fb > a.cap) {
+                if (lane == 0) sh.cap = a.cap_fb;
+                wsync();
+                st = orient_group<true>(sh, ch, a, g, lane);
+                if (lane == 0) sh.cap = a.cap;
+                wsync();
             }
         }
         if (lane == 0) a.status[g] = st;
@@ -742,9 +764,8 @@ int orient_blocks_per_cu(int cap) {
     return nb;
 }
 
-size_t orient_slab_words(int cap) {
-    return cap > kOrientCap ? 3 * (size_t)cap + (size_t)cap / 64 : (size_t)cap + kChWords;
-}
+
+size_t orient_slab_words(int cap, int cap_fb) { return (size_t)slab_words(cap, cap_fb); }
 
 hipError_t launch_orient(const OrientArgs &a, int n_slots, hipStream_t stream) {
     if (a.cap > kOrientCap) {
