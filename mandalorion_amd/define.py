@@ -241,19 +241,22 @@ class Assembly:
         n_iso = len(sub_off) - 1
         n_sub = int(sub_off[-1])
         hits = np.asarray(hits).reshape(n_sub, -1) if n_sub else np.zeros((0, 1), np.int8)
-        nh = np.asarray(n_hits, dtype=np.int64)[:n_sub]
         H = hits.shape[1]
-        valid = np.arange(H)[None, :] < nh[:, None]
-        # running product of the hit strands (+1 / -1) along each read's hits, one column at a time
-        # (np.cumprod along the short axis took ~45 ms on a config-3 chunk)
-        signs = np.empty((n_sub, H), dtype=np.int8)
-        acc = np.ones(n_sub, dtype=np.int8)
-        for c in range(min(H, int(nh.max()) if n_sub else 0)):
-            acc = acc * np.where(valid[:, c], hits[:, c], 1).astype(np.int8)
-            signs[:, c] = acc
-        signs[:, min(H, int(nh.max()) if n_sub else 0):] = 1
+        nh = np.minimum(np.asarray(n_hits)[:n_sub], H)
         self.e_read = np.repeat(np.arange(n_sub), nh)            # emission -> subsample slot
-        self.e_sign = signs[valid]                                # row-major = hit order per read
+        # emission j of a read is its hit j, re-bound by the hits before it: the running product of the
+        # read's hit strands (+1 / -1) up to j.  Most reads have one hit, so the product starts from
+        # column 0 and only the emissions at column >= c take column c (entries past a read's hit count
+        # are never read: the kernel does not write them)
+        first = np.cumsum(nh) - nh
+        e_col = np.arange(len(self.e_read)) - np.repeat(first, nh)
+        e_sign = hits[self.e_read, 0] if len(self.e_read) else np.zeros(0, np.int8)
+        for c in range(1, H):
+            m = np.nonzero(e_col >= c)[0]
+            if not len(m):
+                break
+            e_sign[m] = e_sign[m] * hits[self.e_read[m], c]
+        self.e_sign = e_sign                                      # row-major = hit order per read
         iso_of_sub = np.repeat(np.arange(n_iso), np.diff(sub_off))
         self.e_iso = iso_of_sub[self.e_read] if n_sub else np.zeros(0, np.int64)
         self.n_emit = np.bincount(self.e_iso, minlength=n_iso) if n_iso else np.zeros(0, np.int64)
@@ -268,7 +271,8 @@ class Assembly:
         # -S when the median subsample length (all subsampled reads, mapped or not) is >= 8000
         # (np.median of a group = mean of its two middle values: sort inside groups, pick them)
         self.seeding = np.zeros(len(self.poa_iso), dtype=np.uint8)
-        if len(self.poa_iso):
+        # (no read of 8,000 or more anywhere: no median can reach it)
+        if len(self.poa_iso) and len(res.seq_len) and int(res.seq_len.max()) >= 8000:
             lens = res.seq_len[res.sub].astype(np.int64)
             m = np.diff(sub_off)
             # the median can reach 8000 only when the upper middle value does, i.e. when at least

@@ -151,6 +151,33 @@ def test_rebinding_and_fallbacks(dataset):
         run([[] for _ in sub])
 
 
+def test_assembly_emission_strands_random():
+    """Emission strands on random hit tables (0-8 hits per read, garbage past each read's hit count, as
+    the orientation kernel leaves it): equal to the running product of each read's hits, the column-wise
+    form of the earlier build (per read, over all columns, masked)."""
+    from types import SimpleNamespace
+
+    rng = np.random.default_rng(5)
+    for H in (4, 8):
+        n_iso = 300
+        m = rng.integers(1, 12, n_iso)
+        sub_off = np.zeros(n_iso + 1, np.int64)
+        np.cumsum(m, out=sub_off[1:])
+        n_sub = int(sub_off[-1])
+        nh = rng.integers(0, H + 1, n_sub).astype(np.int32)
+        nh[sub_off[:-1]] = np.maximum(nh[sub_off[:-1]], 1)  # every isoform has an emission
+        hits = rng.integers(-128, 128, (n_sub, H)).astype(np.int8)  # garbage ...
+        valid = np.arange(H)[None, :] < nh[:, None]
+        hits[valid] = np.where(rng.random(int(valid.sum())) < 0.5, 1, -1)  # ... except the hits
+        res = SimpleNamespace(sub_off=sub_off, sub=np.arange(n_sub, dtype=np.int64),
+                              seq_off=np.arange(n_sub, dtype=np.int64) * 10, seq_len=np.full(n_sub, 9, np.int32))
+        a = define.Assembly(res, hits, nh)
+        signs = np.cumprod(np.where(valid, hits, 1).astype(np.int64), axis=1)
+        assert np.array_equal(a.e_read, np.repeat(np.arange(n_sub), nh))
+        assert np.array_equal(a.e_sign, signs[valid].astype(np.int8))
+        assert a.e_sign.dtype == np.int8
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
