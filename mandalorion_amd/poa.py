@@ -106,6 +106,29 @@ def poa_consensus_packed(seqs: np.ndarray, seq_off: np.ndarray, grp_off: np.ndar
     return cons[:int(cons_off[-1])], cons_off
 
 
+_MADV_POPULATE_WRITE = 23  # Linux >= 5.14: fault pages in writable without changing their contents
+_libc = None
+
+
+def _prefault(buf: np.ndarray, nbytes: int):
+    """Map the first nbytes of buf's pages in a helper thread (madvise MADV_POPULATE_WRITE; contents are
+    left alone, so it may overlap writes into buf).  Returns the thread, or None."""
+    global _libc
+    if nbytes < (8 << 20):
+        return None
+    import ctypes
+    import threading
+
+    if _libc is None:
+        _libc = ctypes.CDLL(None, use_errno=True)
+        _libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    start = (buf.ctypes.data + 4095) & ~4095
+    n = (buf.ctypes.data + nbytes - start) & ~4095
+    t = threading.Thread(target=_libc.madvise, args=(start, n, _MADV_POPULATE_WRITE), daemon=True)
+    t.start()
+    return t
+
+
 def poa_consensus_segments(d_text: int, text_len: int, off: np.ndarray, length: np.ndarray, rc: np.ndarray | None,
                            grp_off: np.ndarray, seeding=None, device: int = 0, params: _lib.PoaParams | None = None,
                            info: dict | None = None, slot: int = 0):
@@ -119,15 +142,25 @@ def poa_consensus_segments(d_text: int, text_len: int, off: np.ndarray, length: 
     rc = None if rc is None else np.ascontiguousarray(rc, dtype=np.int8)
     grp_off = np.ascontiguousarray(grp_off, dtype=np.int64)
     seed_arr = None if seeding is None else np.ascontiguousarray(np.asarray(seeding, dtype=np.uint8))
-    cap = int(length.sum()) * 2 + 1024
+    total = int(length.sum())
+    cap = total * 2 + 1024
     cons = np.empty(cap, dtype=np.uint8)
     cons_off = np.zeros(n + 1, dtype=np.int64)
     cells = np.zeros(max(n, 1), dtype=np.int64) if info is not None else None
     if n > 0:
-        _lib.check(ctx.lib.mando_poa_segments(ctx.handle, _lib.ctypes.byref(p), _lib.ctypes.c_void_p(d_text),
-                                              int(text_len), _lib.ptr(off), _lib.ptr(length), _lib.ptr(rc),
-                                              _lib.ptr(grp_off), n, _lib.ptr(seed_arr), _lib.ptr(cons), cap,
-                                              _lib.ptr(cons_off), _lib.ptr(cells)))
+        # the consensi land in fresh pages of `cons` when the launch ends; faulting them in then took
+        # ~20 ms per 100 MB on the path from one chunk's POA to the next, so a helper thread maps the
+        # expected span (about one read per group, with margin) while the kernels run (config 4: step
+        # medians 11.57 -> 11.45 s, profiles/r07d_ab_cons_prefault.txt)
+        pre = _prefault(cons, min(cap, total // max(1, len(length) // n) * 5 // 4 + (1 << 20)))
+        try:
+            _lib.check(ctx.lib.mando_poa_segments(ctx.handle, _lib.ctypes.byref(p), _lib.ctypes.c_void_p(d_text),
+                                                  int(text_len), _lib.ptr(off), _lib.ptr(length), _lib.ptr(rc),
+                                                  _lib.ptr(grp_off), n, _lib.ptr(seed_arr), _lib.ptr(cons), cap,
+                                                  _lib.ptr(cons_off), _lib.ptr(cells)))
+        finally:
+            if pre is not None:
+                pre.join()
         if info is not None:
             info["cells"] = int(cells[:n].sum())
             info["kernel_ms"] = ctx.last_kernel_ms()
