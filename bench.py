@@ -41,6 +41,7 @@ import argparse
 import hashlib
 import json
 import os
+import resource
 import shutil
 import sys
 import time
@@ -176,9 +177,11 @@ def gen_data(d: str, wl: dict, n_loci: int, threads: int) -> int:
     return n
 
 
-def cpu_fns(threads: int):
+def cpu_fns(threads: int, simd: bool = True, poa_stats: dict | None = None):
     """orient_fn / consensus_fn over the CPU restatements (oracle/), groups split over host threads
-    (ctypes drops the GIL inside the C calls)."""
+    (ctypes drops the GIL inside the C calls).  simd: the POA restatement's AVX2 int16 build
+    (oracle/poa_simd.c, byte-identical to poa_ref.c); poa_stats (optional) accumulates the POA calls'
+    wall seconds and DP cells."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import orient as oref
@@ -207,12 +210,23 @@ def cpu_fns(threads: int):
         return np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res])
 
     def consensus_fn(seqs, seq_off, grp_off, seeding):
+        t0 = time.perf_counter()
+        cells = np.zeros(max(1, len(grp_off) - 1), dtype=np.int64)
         parts = split(seq_off, grp_off, 4 * threads)
         if not parts:
-            return opoa.consensus_packed(seqs, seq_off, grp_off)
-        res = list(pool.map(lambda ab: opoa.consensus_packed(*sub(seqs, seq_off, grp_off, *ab),
-                                                             seeding=None if seeding is None else seeding[ab[0]:ab[1]]),
-                            parts))
+            return opoa.consensus_packed(seqs, seq_off, grp_off, simd=simd)
+
+        def one(ab):
+            c = np.zeros(max(1, ab[1] - ab[0]), dtype=np.int64)
+            r = opoa.consensus_packed(*sub(seqs, seq_off, grp_off, *ab), simd=simd, cells_out=c,
+                                      seeding=None if seeding is None else seeding[ab[0]:ab[1]])
+            cells[ab[0]:ab[1]] = c[:ab[1] - ab[0]]
+            return r
+
+        res = list(pool.map(one, parts))
+        if poa_stats is not None:
+            poa_stats["s"] = poa_stats.get("s", 0.0) + time.perf_counter() - t0
+            poa_stats["cells"] = poa_stats.get("cells", 0) + int(cells[:len(grp_off) - 1].sum())
         cons = np.concatenate([c[:int(o[-1])] for c, o in res])
         off = [np.zeros(1, dtype=np.int64)]
         base = 0
@@ -260,7 +274,8 @@ def cpu_baseline(data: str, n_loci: int, threads: int):
     POA on `threads` host threads, on the first n_loci loci of the same data set."""
     d = os.path.join(data, "cpu_sample")
     recs = sample_dir(data, d, n_loci)
-    of, cf, pool = cpu_fns(threads)
+    ps: dict = {}
+    of, cf, pool = cpu_fns(threads, simd=True, poa_stats=ps)
     try:
         t0 = time.perf_counter()
         from oracle import cluster as ocl
@@ -269,11 +284,16 @@ def cpu_baseline(data: str, n_loci: int, threads: int):
         wall = time.perf_counter() - t0
     finally:
         pool.shutdown()
-    out = {"value": recs / wall, "unit": "records/s", "cores": threads, "kind": "port",
+    gcups = ps.get("cells", 0) / ps["s"] / 1e9 if ps.get("s") else None
+    out = {"value": recs / wall, "unit": "records/s", "cores": threads, "kind": "simd-port",
            "sample": f"first {n_loci} loci ({recs} PSL records, {st['poa_reads']} POA reads) of this workload through "
-                     f"the same D driver with oracle/orient_ref.c + oracle/poa_ref.c (C restatements of mappy "
-                     f"map-ont and abPOA v1.4.1) and oracle/cluster_ref.cpp (clustering) on {threads} host threads; "
-                     f"{wall:.1f} s wall"}
+                     f"the same D driver with oracle/orient_ref.c (C restatement of mappy map-ont), "
+                     f"oracle/poa_simd.c (the abPOA v1.4.1 restatement with its DP rows in AVX2 int16 lanes, as "
+                     f"abPOA vectorises them; byte-identical to oracle/poa_ref.c) and oracle/cluster_ref.cpp "
+                     f"(clustering) on {threads} host threads; {wall:.1f} s wall",
+           # the POA stage alone: its wall seconds on the host threads and its DP cells per second
+           "poa_s": round(ps.get("s", 0.0), 3), "poa_gcups": gcups,
+           "poa_gcups_per_core": gcups / threads if gcups else None}
     hashes = (sha(os.path.join(d, "Isoform_Consensi.fasta")), sha(os.path.join(d, "reads2isoforms.txt")))
     return out, d, hashes
 
@@ -295,6 +315,59 @@ def spawn_ranks(n: int) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     codes = [p.wait() for p in procs]
     return max(codes, key=abs) if any(codes) else 0
+
+
+def page_cache_resident(files: list, stride: int = 1) -> dict:
+    """Share of the locus files' pages resident in the page cache (mincore over a read-only mapping of
+    every stride-th file; the mapping faults nothing in), plus the cgroup's file-cache bytes: the timed
+    steps read the locus text from the page cache, so a box with less free RAM would read from disk."""
+    import ctypes
+    import mmap
+
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    libc.mincore.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    pg = os.sysconf("SC_PAGE_SIZE")
+    fail = ctypes.c_void_p(-1).value
+    tot = res = nf = 0
+    for f in files[::max(1, stride)]:
+        fd = os.open(f, os.O_RDONLY)
+        try:
+            n = os.fstat(fd).st_size
+            if n == 0:
+                continue
+            a = libc.mmap(None, n, mmap.PROT_READ, mmap.MAP_SHARED, fd, 0)
+            if a is None or a == fail:
+                continue
+            npg = (n + pg - 1) // pg
+            vec = (ctypes.c_ubyte * npg)()
+            if libc.mincore(a, n, vec) == 0:
+                res += int((np.frombuffer(vec, np.uint8) & 1).sum())
+                tot += npg
+                nf += 1
+            libc.munmap(a, n)
+        finally:
+            os.close(fd)
+    out = {"files_sampled": nf, "pages": tot, "resident_frac": round(res / tot, 4) if tot else None}
+    try:
+        for line in open("/sys/fs/cgroup/memory.stat"):
+            k, v = line.split()
+            if k in ("file", "anon"):
+                out[f"cgroup_{k}_GB"] = round(int(v) / 1e9, 2)
+        mx = open("/sys/fs/cgroup/memory.max").read().strip()
+        out["cgroup_memory_max_GB"] = None if mx == "max" else round(int(mx) / 1e9, 2)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def locus_files(data: str) -> list:
+    from mandalorion_amd import define
+
+    tmp = os.path.join(data, "tmp_SS")
+    return [os.path.join(tmp, r + ".psl") for r in define._roots(tmp)]
 
 
 def shard_plan(data: str, world: int) -> list:
@@ -437,8 +510,12 @@ def main():
         run_define(data, threads, local, comm)
         if rank == 0:
             log(f"warmup step {k}: {time.perf_counter() - tw:.3f} s")
+    # page-cache residency of the locus text right before and after the timed steps (outside them)
+    files = locus_files(data) if rank == 0 else []
+    pc_before = page_cache_resident(files, stride=8) if rank == 0 else None
     if comm is not None:
         comm.barrier()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     stats = []
     for k in range(args.steps):
@@ -448,9 +525,12 @@ def main():
     if comm is not None:
         comm.barrier()
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    host_cpu = (ru1.ru_utime - ru0.ru_utime + ru1.ru_stime - ru0.ru_stime) / max(1, args.steps)
     if comm is not None:
         elapsed = comm.max(elapsed)
     st = stats[-1]
+    pc_after = page_cache_resident(files, stride=8) if rank == 0 else None
 
     # the whole output of the last timed step against the oracle's full-size hashes (rank 0 wrote it)
     full_parity, ref_scope = (fullsize_check(data, f"{args.workload}:{n_loci}") if rank == 0 and SHARE is None
@@ -529,6 +609,9 @@ def main():
             "parallelism": f"loci sharded over {n_gpus} GPU(s) (LPT on the DP-cost estimate), one all-gather "
                           f"({comm.backend if comm else 'none'}) to the writer on rank 0",
             "host_threads_per_rank": threads,
+            # user + system CPU seconds of this rank's process per timed step (host waits sleep on the
+            # device's completion signal, so this is the host work itself)
+            "host_cpu_s_per_step_rank0": round(host_cpu, 2),
             "host_cores": cores,
             "phases_rank0_s": {k: round(st[k], 4) for k in ("t_ingest", "t_cluster", "t_orient", "t_assemble", "t_poa",
                                                              "t_merge", "t_write", "t_total") if k in st},
@@ -548,6 +631,8 @@ def main():
             # slow step shows where it lost its time
             "steps_s": [round(x["t_total"], 4) for x in stats],
             "steps_poa_kernel_ms": [round(sum(y["kernel_ms"] for y in x["poa_launches"]), 1) for x in stats],
+            # the locus text's pages in the page cache (every 8th file) before / after the timed steps
+            "page_cache": {"before": pc_before, "after": pc_after},
         },
         "roofline": {
             "bound": bound,

@@ -62,8 +62,17 @@ void mando_poa_default_params(mando_poa_params *p);
 /* Number of visible HIP devices (0 on a machine without a GPU; never fails for that reason). */
 int mando_device_count(int *out);
 
+/* A context: one device, its streams, cached device buffers and POA workspaces.  Creating one sets
+ * the device's schedule flag to hipDeviceScheduleBlockingSync (host threads waiting on the device
+ * sleep on its completion signal instead of spinning; spinning cost ~1.6 cores per GPU on config 4).
+ * That flag is process-wide for the device: it also applies to the host application's own waits on
+ * that device, and HIP refuses it when the application has already initialised the device with other
+ * flags (the application's flags are then kept); mando_ctx_blocking_sync() reports which. */
 int mando_ctx_create(int device_ordinal, mando_ctx **out);
 void mando_ctx_destroy(mando_ctx *ctx);
+/* 1 when the ctx's device waits with blocking sync, 0 when it spins (flags set before the ctx), <0 on
+ * error. */
+int mando_ctx_blocking_sync(mando_ctx *ctx);
 
 /* Batched POA consensus, host buffers.
  *   n_groups groups; group g = reads [grp_off[g], grp_off[g+1]) in FINAL abPOA input order

@@ -22,6 +22,7 @@ EXPORTED = (
     "mando_device_count",
     "mando_ctx_create",
     "mando_ctx_destroy",
+    "mando_ctx_blocking_sync",
     "mando_poa_batch",
     "mando_poa_batch_device",
     "mando_ctx_sync",

@@ -89,15 +89,34 @@ __device__ __forceinline__ uint8_t comp_base(uint8_t c) {
     }
 }
 
+// base -> POA code 0..4 (A, C, G, T any case; anything else 4), as mando::encode_kernel
+__device__ __forceinline__ uint8_t base_code(uint32_t c) {
+    c |= 0x20;
+    return c == 'a' ? 0 : c == 'c' ? 1 : c == 'g' ? 2 : c == 't' ? 3 : 4;
+}
+
+// segment r of the device text -> dst[dst_off[r] ..], reverse-complemented where rc[r]; encode: as POA
+// codes (the complement of code c < 4 is 3 - c, of anything else 4: comp_base maps the IUPAC letters
+// among themselves), which spares the POA batch its separate encoding pass over the gathered bytes
 __global__ __launch_bounds__(256) void gather_kernel(const uint8_t *__restrict__ text, const int64_t *__restrict__ off,
                                                      const int32_t *__restrict__ len, const int8_t *__restrict__ rc,
                                                      const int64_t *__restrict__ dst_off, int64_t n,
-                                                     uint8_t *__restrict__ dst) {
+                                                     uint8_t *__restrict__ dst, int encode) {
     for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
         const uint8_t *src = text + off[r];
         uint8_t *d = dst + dst_off[r];
         const int L = len[r];
-        if (rc && rc[r]) {
+        const bool rev = rc && rc[r];
+        if (encode) {
+            if (rev) {
+                for (int k = threadIdx.x; k < L; k += 256) {
+                    const uint8_t c = base_code(src[L - 1 - k]);
+                    d[k] = c < 4 ? (uint8_t)(3 - c) : (uint8_t)4;
+                }
+            } else {
+                for (int k = threadIdx.x; k < L; k += 256) d[k] = base_code(src[k]);
+            }
+        } else if (rev) {
             for (int k = threadIdx.x; k < L; k += 256) d[k] = comp_base(src[L - 1 - k]);
         } else {
             for (int k = threadIdx.x; k < L; k += 256) d[k] = src[k];
@@ -144,6 +163,7 @@ struct mando_ctx {
     bool timed = false;
     int64_t total_mem = 0;    // device HBM (hipDeviceProp_t::totalGlobalMem)
     int64_t poa_budget = 0;   // mando_ctx_set_poa_budget: explicit cap on the POA workspaces (0: default policy)
+    bool staged_encoded = false;       // the last POA stage wrote POA codes (gather_stage), not ASCII
     int64_t last_slots[3] = {0, 0, 0};  // slots of the last batch's launches by kind (narrow, wide, seeded)
     int64_t last_budget[3] = {0, 0, 0}; // the workspace budget each of them was sized with
     DevBuf ws, counter, prof, o_gidx;
@@ -635,9 +655,14 @@ int mando_ctx_create(int device_ordinal, mando_ctx **out) {
     HIP_TRY(hipSetDevice(device_ordinal));
     // host threads waiting on the device sleep on the completion signal instead of spinning: one GPU's
     // waits took ~20 s of CPU per config-4 step (1.6 cores) for no gain in time
-    // (profiles/r05q_ab_blocking_sync.txt), cores the other ranks of a node need (2 per rank at N = 8)
+    // (profiles/r05q_ab_blocking_sync.txt), cores the other ranks of a node need (2 per rank at N = 8).
+    // hipEventBlockingSync events on the library's own waits instead of this device flag were measured
+    // in round 6: 56 s of host CPU per config-4 step and 12.29 s per step (profiles/r08a_*), i.e. the
+    // waits still spin.  The flag is the device's (process-wide): include/mando.h says so, and
+    // mando_ctx_blocking_sync() reports whether it took effect (refused when the application initialised
+    // the device first with other flags).
     (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
-    (void)hipGetLastError();  // (refused when the device was initialised before: keep its flags)
+    (void)hipGetLastError();
     hipDeviceProp_t prop;
     HIP_TRY(hipGetDeviceProperties(&prop, device_ordinal));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
@@ -661,6 +686,14 @@ void mando_ctx_destroy(mando_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     delete ctx;
+}
+
+int mando_ctx_blocking_sync(mando_ctx *ctx) {
+    if (!ctx) return fail(MANDO_E_ARG, "null ctx");
+    HIP_TRY(hipSetDevice(ctx->device));
+    unsigned int f = 0;
+    HIP_TRY(hipGetDeviceFlags(&f));
+    return (f & hipDeviceScheduleMask) == hipDeviceScheduleBlockingSync ? 1 : 0;
 }
 
 int mando_ctx_sync(mando_ctx *ctx) {
@@ -795,8 +828,9 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
     std::vector<int64_t> goff((size_t)n_groups + 1);
     for (int64_t g = 0; g <= n_groups; ++g) goff[(size_t)g] = grp_off[g];
     if (total > 0) {
+        ctx->staged_encoded = false;
         if ((rc = stage(ctx))) return rc;
-        HIP_TRY(mando::launch_encode(ctx->seq.as<uint8_t>(), total, ctx->stream));
+        if (!ctx->staged_encoded) HIP_TRY(mando::launch_encode(ctx->seq.as<uint8_t>(), total, ctx->stream));
     }
     HIP_TRY(hipMemcpyAsync(ctx->seq_off.p, soff.data(), soff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->grp_off.p, goff.data(), goff.size() * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -995,7 +1029,7 @@ int segment_layout(const int64_t *off, const int32_t *len, int64_t n, int64_t te
 }
 
 int gather_stage(mando_ctx *ctx, const uint8_t *d_text, const int64_t *off, const int32_t *len, const int8_t *rc,
-                 const std::vector<int64_t> &soff) {
+                 const std::vector<int64_t> &soff, bool encode = false) {
     const int64_t n = (int64_t)soff.size() - 1;
     if (n <= 0) return MANDO_OK;
     int e;
@@ -1009,8 +1043,9 @@ int gather_stage(mando_ctx *ctx, const uint8_t *d_text, const int64_t *off, cons
     const int blocks = (int)std::min<int64_t>(n, (int64_t)ctx->n_cu * 32);
     hipLaunchKernelGGL(gather_kernel, dim3(blocks), dim3(256), 0, ctx->stream, d_text, ctx->g_off.as<int64_t>(),
                        ctx->g_len.as<int32_t>(), rc ? ctx->g_rc.as<int8_t>() : nullptr, ctx->g_dst.as<int64_t>(), n,
-                       ctx->seq.as<uint8_t>());
+                       ctx->seq.as<uint8_t>(), encode ? 1 : 0);
     HIP_TRY(hipGetLastError());
+    ctx->staged_encoded = encode;
     return MANDO_OK;
 }
 
@@ -1062,7 +1097,7 @@ int mando_poa_segments(mando_ctx *ctx, const mando_poa_params *params, const uin
     std::vector<int64_t> soff;
     if ((e = segment_layout(off, len, n_reads, text_len, soff))) return e;
     return poa_batch_impl(ctx, params, soff, grp_off, n_groups, seeding_per_group, cons_out, cons_cap, cons_off,
-                          cells_out, [&](mando_ctx *c) { return gather_stage(c, d_text, off, len, rc, soff); });
+                          cells_out, [&](mando_ctx *c) { return gather_stage(c, d_text, off, len, rc, soff, true); });
 }
 
 int mando_selftest(mando_ctx *ctx, int *bad) {

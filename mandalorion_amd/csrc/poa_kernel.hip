@@ -2108,8 +2108,9 @@ __device__ __forceinline__ void w2_helper(SharedState &sh, int lane) {
 // finds them loaded instead of waiting on the LDS round trip; at the batch end that read is past the
 // batch and unused, and the loop drains it before it leaves.  Hazards (gfx950) are padded inside the string: DPP
 // reads two wait states after a VALU write, v_readlane after the scans, VMEM reads of SGPRs written
-// by a VALU before the block (s_nop 4).  Exec is the whole wave here (run_dp16 runs wave-uniform);
-// the row records are stored with exec = lane 0 and exec is restored to all lanes.
+// by a VALU before the block (s_nop 4).  Exec is the whole wave here (run_dp16 runs wave-uniform; the
+// scans need every lane; MANDO_CHECK_EXEC builds trap otherwise); the row records are stored with
+// exec = lane 0, exec saved in vcc around them and restored from it.
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(lds_u8 *)(const_cast<void *>(p));
@@ -2136,7 +2137,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
           [v0c0c] "=&v"(v0c0c) \
         : [iend] "s"(iend), [b0] "s"(b0), [qlen] "s"(qlen), [w] "s"(w), [Ldesc] "s"(Ldesc), [Lrrow] "s"(Lrrow), \
           [Lring] "s"(Lring), [Lq] "s"(Lq), [tbp] "s"(tbp), [kpp] "s"(kpp), [svp] "s"(svp), [rip] "s"(rip) \
-        : "memory", "scc", "v120", "v121", "v122", "v123", "v124", "v125"
+        : "memory", "scc", "vcc", "v120", "v121", "v122", "v123", "v124", "v125"
 
 __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb, gu8 *kp, gint *sv, gint *rinfo,
                                              int b0, int i, int iend, int qlen, int w, int &prv_r, int &prv_beg,
@@ -2411,10 +2412,11 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_lshl_b32 %[x], %[r], 5\n"
             "v_mov_b32 %[voff], %[x]\n"
             "v_mov_b32 v125, -1\n"
+            "s_mov_b64 vcc, exec\n"
             "s_mov_b64 exec, 1\n"
             "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
             "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
-            "s_mov_b64 exec, -1\n"
+            "s_mov_b64 exec, vcc\n"
             "s_sub_i32 %[x], %[end], %[beg]\n"
             "s_add_i32 %[cel], %[cel], %[x]\n"
             "s_add_i32 %[x], %[spm], 4\n"
@@ -2453,12 +2455,13 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_lshl_b32 %[x], %[r], 5\n"
             "v_mov_b32 %[voff], %[x]\n"
             "v_mov_b32 v125, %[svu]\n"
+            "s_mov_b64 vcc, exec\n"
             "s_mov_b64 exec, 1\n"
             "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
             "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
             "global_store_dwordx2 %[voff], v[124:125], %[rip] offset:16\n"
             "s_addk_i32 %[svu], 0x180\n"
-            "s_mov_b64 exec, -1\n"
+            "s_mov_b64 exec, vcc\n"
             "s_sub_i32 %[x], %[end], %[beg]\n"
             "s_add_i32 %[cel], %[cel], %[x]\n"
             "s_add_i32 %[x], %[spm], 4\n"
@@ -2745,10 +2748,11 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_lshl_b32 %[x], %[r], 5\n"
             "v_mov_b32 %[voff], %[x]\n"
             "v_mov_b32 v125, -1\n"
+            "s_mov_b64 vcc, exec\n"
             "s_mov_b64 exec, 1\n"
             "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
             "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
-            "s_mov_b64 exec, -1\n"
+            "s_mov_b64 exec, vcc\n"
             "s_sub_i32 %[x], %[end], %[beg]\n"
             "s_add_i32 %[cel], %[cel], %[x]\n"
             "s_add_i32 %[x], %[spm], 4\n"
@@ -2788,12 +2792,13 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_lshl_b32 %[x], %[r], 5\n"
             "v_mov_b32 %[voff], %[x]\n"
             "v_mov_b32 v125, %[svu]\n"
+            "s_mov_b64 vcc, exec\n"
             "s_mov_b64 exec, 1\n"
             "ds_write2_b64 %[a0], v[120:121], v[124:125] offset1:1\n"
             "global_store_dwordx4 %[voff], v[120:123], %[rip]\n"
             "global_store_dwordx2 %[voff], v[124:125], %[rip] offset:16\n"
             "s_addk_i32 %[svu], 0x180\n"
-            "s_mov_b64 exec, -1\n"
+            "s_mov_b64 exec, vcc\n"
             "s_sub_i32 %[x], %[end], %[beg]\n"
             "s_add_i32 %[cel], %[cel], %[x]\n"
             "s_add_i32 %[x], %[spm], 4\n"
@@ -2914,6 +2919,9 @@ __device__ __forceinline__ int run_dp16(SharedState &sh, const SC &sc, int qlen,
         if constexpr (RW == kChunk && NW == 1 && !CAP && std::is_same<SC, DefaultScores>::value) {
             // the one-chunk fast rows with one or two predecessors in the ring, hand-scheduled (~90 % of a
             // narrow launch's rows)
+#ifdef MANDO_CHECK_EXEC
+            if (__builtin_amdgcn_read_exec() != ~0ull) __builtin_trap();
+#endif
             const int j = fast_rows_asm(sh, lane, tb, kp, sv, rinfo, b0, i, iend, qlen, w, prv_r, prv_beg, prv_end,
                                         prv_am, ds);
             if (j != i) {

@@ -242,7 +242,13 @@ class Assembly:
         n_sub = int(sub_off[-1])
         hits = np.asarray(hits).reshape(n_sub, -1) if n_sub else np.zeros((0, 1), np.int8)
         H = hits.shape[1]
-        nh = np.minimum(np.asarray(n_hits)[:n_sub], H)
+        nh = np.asarray(n_hits)[:n_sub]
+        if len(nh) and int(nh.max()) > H:
+            # the orientation reports max_hits + 1 for a read with more primary hits than it kept: the
+            # caller must re-run such reads with room for all of them (gpu_orient* do)
+            bad = int(np.argmax(nh > H))
+            raise ValueError(f"subsampled read {bad}: {int(nh[bad])} hits reported for {H} hit columns "
+                             "(orientation overflow not re-run)")
         self.e_read = np.repeat(np.arange(n_sub), nh)            # emission -> subsample slot
         # emission j of a read is its hit j, re-bound by the hits before it: the running product of the
         # read's hit strands (+1 / -1) up to j.  Most reads have one hit, so the product starts from
@@ -975,9 +981,10 @@ def _place(path: str, buf: np.ndarray, src: np.ndarray, roots: np.ndarray, sizes
     dst, src, ln = dst[keep], src[keep], ln[keep]
     r0 = np.searchsorted(bnd, dst, side="right") - 1
     r1 = np.searchsorted(bnd, dst + ln - 1, side="right") - 1
-    if np.any(r1 > r0):  # blocks across a bound (at most world - 1 of them): one piece per range
+    cross = np.flatnonzero(r1 > r0)
+    if len(cross):  # blocks across a bound (at most world - 1 of them): one piece per range
         pd, ps, pl = [], [], []
-        for i in range(len(dst)):
+        for i in cross:
             a, b, s0 = int(dst[i]), int(dst[i] + ln[i]), int(src[i])
             for r in range(int(r0[i]), int(r1[i]) + 1):
                 lo, hi = max(a, int(bnd[r])), min(b, int(bnd[r + 1]))
@@ -985,9 +992,12 @@ def _place(path: str, buf: np.ndarray, src: np.ndarray, roots: np.ndarray, sizes
                     pd.append(lo)
                     ps.append(s0 + lo - a)
                     pl.append(hi - lo)
-        dst, src, ln = (np.array(x, dtype=np.int64) for x in (pd, ps, pl))
+        whole = np.ones(len(dst), dtype=bool)
+        whole[cross] = False
+        dst, src, ln = (np.concatenate([v[whole], np.array(x, dtype=np.int64)])
+                        for v, x in ((dst, pd), (src, ps), (ln, pl)))
     rk = np.searchsorted(bnd, dst, side="right") - 1
-    order = np.argsort(rk, kind="stable")  # by destination, file order inside
+    order = np.argsort(dst, kind="stable")  # file order, so by destination rank too
     dst, src, ln, rk = dst[order], src[order], ln[order], rk[order]
     cut = np.searchsorted(rk, np.arange(world + 1))
     payload, _ = _lib.pack_segments([buf], src, ln, threads=threads)
@@ -999,17 +1009,29 @@ def _place(path: str, buf: np.ndarray, src: np.ndarray, roots: np.ndarray, sizes
     got_data = _alltoallv(comm, data)
     lo, hi = int(bnd[me]), int(bnd[me + 1])
     rb = np.zeros(max(hi - lo, 1), dtype=np.uint8)
+    # in-process stand-in communicators (rehearsals: no alltoallv) deliver incomplete data in their early
+    # passes, whose pieces are dropped; over a real transport every piece must land inside this rank's
+    # range and the pieces must tile it, or the exchange disagreed and the file would carry zero bytes
+    standin = not hasattr(comm, "alltoallv")
     sel, starts, lens, outs = [], [], [], []
+    got = 0
     for r in range(world):
         m = np.ascontiguousarray(got_meta[r]).view(np.int64).reshape(-1, 2)
         if not len(m):
             continue
         st = np.concatenate([[0], np.cumsum(m[:, 1])[:-1]])
-        ok = (m[:, 0] >= lo) & (m[:, 0] + m[:, 1] <= hi) & (st + m[:, 1] <= got_data[r].size)  # (stand-ins' early passes)
+        ok = (m[:, 0] >= lo) & (m[:, 0] + m[:, 1] <= hi) & (st + m[:, 1] <= got_data[r].size)
+        if not standin and not ok.all():
+            raise RuntimeError(f"range placement of {os.path.basename(path)}: rank {r} sent {int((~ok).sum())} "
+                               f"piece(s) outside rank {me}'s range [{lo}, {hi}) or beyond its data")
+        got += int(m[ok, 1].sum())
         sel.append(np.full(int(ok.sum()), r, np.int8))
         starts.append(st[ok])
         lens.append(m[ok, 1])
         outs.append(m[ok, 0] - lo)
+    if not standin and got != hi - lo:
+        raise RuntimeError(f"range placement of {os.path.basename(path)}: rank {me} received {got} bytes for its "
+                           f"range [{lo}, {hi}) of {hi - lo}")
     if sel:
         _lib.pack_segments([np.ascontiguousarray(g) if g.size else np.zeros(1, np.uint8) for g in got_data],
                            np.concatenate(starts), np.concatenate(lens), sel=np.concatenate(sel), threads=threads,

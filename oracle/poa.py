@@ -14,6 +14,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "libpoa_ref.so")
+# the same restatement with AVX2 int16 DP rows (poa_simd.c): bench.py's cpu_baseline, byte-equal to LIB
+LIB_SIMD = os.path.join(HERE, "build", "libpoa_simd.so")
 
 
 class Params(ctypes.Structure):
@@ -27,7 +29,7 @@ class Params(ctypes.Structure):
         return cls(5, 4, 4, 2, 24, 1, 10, 0.01, 0, 19, 10, 500)
 
 
-_lib = None
+_libs: dict = {}
 
 
 def build() -> str:
@@ -35,20 +37,20 @@ def build() -> str:
     return LIB
 
 
-def load():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
+def load(simd: bool = False):
+    path = LIB_SIMD if simd else LIB
+    if path not in _libs:
+        if not os.path.exists(path):
             build()
-        lib = ctypes.CDLL(LIB)
+        lib = ctypes.CDLL(path)
         P = ctypes.c_void_p
         lib.poa_ref_batch.argtypes = [P, P, P, P, ctypes.c_int64, P, P, ctypes.c_int64, P, P]
         lib.poa_ref_batch.restype = ctypes.c_int
         lib.poa_ref_seed_partition.argtypes = [P, ctypes.c_int, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int, P, P, ctypes.c_int]
         lib.poa_ref_seed_partition.restype = ctypes.c_int
-        _lib = lib
-    return _lib
+        _libs[path] = lib
+    return _libs[path]
 
 
 _ENC = np.full(256, 4, dtype=np.uint8)
@@ -71,8 +73,8 @@ def seed_partition(t: str, q: str, params: Params | None = None) -> list[tuple[i
 
 
 def consensus_batch(groups: Sequence[Sequence[str]], params: Params | None = None,
-                    return_cells: bool = False, seeding: Sequence[bool] | None = None):
-    lib = load()
+                    return_cells: bool = False, seeding: Sequence[bool] | None = None, simd: bool = False):
+    lib = load(simd)
     p = params or Params.defaults()
     parts, lens, grp = [], [], [0]
     for g in groups:
@@ -102,9 +104,11 @@ def consensus_batch(groups: Sequence[Sequence[str]], params: Params | None = Non
     return (cons, cells[:n].copy()) if return_cells else cons
 
 
-def consensus_packed(seqs, seq_off, grp_off, params: Params | None = None, seeding=None):
-    """Packed form of consensus_batch (mirrors mandalorion_amd.poa.poa_consensus_packed)."""
-    lib = load()
+def consensus_packed(seqs, seq_off, grp_off, params: Params | None = None, seeding=None, simd: bool = False,
+                     cells_out=None):
+    """Packed form of consensus_batch (mirrors mandalorion_amd.poa.poa_consensus_packed); cells_out (an
+    int64 array of one entry per group, optional) receives the DP cell counts."""
+    lib = load(simd)
     p = params or Params.defaults()
     seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
     if seqs.size == 0:
@@ -119,7 +123,7 @@ def consensus_packed(seqs, seq_off, grp_off, params: Params | None = None, seedi
     if n > 0:
         rc = lib.poa_ref_batch(ctypes.addressof(p), seqs.ctypes.data, seq_off.ctypes.data, grp_off.ctypes.data, n,
                                None if sd is None else sd.ctypes.data, out.ctypes.data, cap, cons_off.ctypes.data,
-                               None)
+                               None if cells_out is None else cells_out.ctypes.data)
         if rc != 0:
             raise RuntimeError(f"poa_ref_batch failed: {rc}")
     return out, cons_off

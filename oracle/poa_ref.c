@@ -241,8 +241,20 @@ static int band_w(const mando_poa_params *p, int qlen) {
  * Predecessors outside the subgraph are ignored.  Fills qnode[0..qlen) with the aligned node of every
  * query position (-1 = inserted).  B = SRC, E = SINK is the whole-graph alignment of the default mode.
  * Returns the number of DP cells evaluated, or -1 on an internal inconsistency. */
+#ifdef POA_SIMD
+/* oracle/poa_simd.c (the cpu_baseline's vectorised build of this file): the same window alignment with
+ * the DP rows in AVX2 int16 lanes; returns -2 when the window must take the scalar code below */
+static int64_t align_window_simd(const graph_t *g, const int *order, const int *pos, const int *remain, int B,
+                                 int E, const uint8_t *q, int qlen, const scorer *sc, int *qnode);
+#endif
 static int64_t align_window(const graph_t *g, const int *order, const int *pos, const int *remain, int B, int E,
                             const uint8_t *q, int qlen, const scorer *sc, int *qnode) {
+#ifdef POA_SIMD
+    {
+        const int64_t c = align_window_simd(g, order, pos, remain, B, E, q, qlen, sc, qnode);
+        if (c != -2) return c;
+    }
+#endif
     const int pB = pos[B], pE = pos[E];
     if (pE <= pB) return -1;
     const int span = pE - pB + 1;

@@ -4,6 +4,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 from mandalorion_amd import _lib
 
@@ -56,3 +57,12 @@ def test_bad_arguments_rejected():
     ks = np.array([6], dtype=np.int64)  # k > n
     assert lib.mando_mt_permutation(0, ns.ctypes.data, ks.ctypes.data, 1, out.ctypes.data, 4) == -1
     assert lib.mando_poa_batch(None, None, None, None, None, 0, None, None, 0, None, None) == -1
+
+
+@pytest.mark.gpu
+def test_ctx_sets_blocking_sync():
+    """mando_ctx_create puts the device's host waits on blocking sync (include/mando.h), and says so."""
+    from mandalorion_amd import _lib
+
+    c = _lib.context(0)
+    assert c.lib.mando_ctx_blocking_sync(c.handle) == 1
