@@ -347,6 +347,11 @@ int mando_root_sizes(const char *dir, const char *names, int64_t n, int32_t thre
  * the accuracy / cs / read-sequence columns when mando_mode != 0.  threads <= 0: all cores. */
 int mando_sam_to_psl(const char *sam_path, const char *psl_path, int32_t mando_mode, int32_t threads,
                      int64_t *n_records);
+/* The same conversion on the ctx's GPU (sam_kernel.hip: one wave per record, two launches), byte-identical
+ * to mando_sam_to_psl; MANDO_E_ARG where emtrey raises, MANDO_E_UNSUPPORTED for a record of more than
+ * 1,024 columns or an accuracy outside [1e-8, 1e9]. */
+int mando_sam_to_psl_device(mando_ctx *ctx, const char *sam_path, const char *psl_path, int32_t mando_mode,
+                            int64_t *n_records);
 
 /* clean_psl (SpliceDefineConsensus.py:14-92, called at Mando.py:343): target gaps < 10 nt merged into
  * their blocks; primary != 0 keeps only the first line per read name. */

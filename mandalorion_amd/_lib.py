@@ -63,6 +63,7 @@ EXPORTED = (
     "mando_list_root_names",
     "mando_root_sizes",
     "mando_sam_to_psl",
+    "mando_sam_to_psl_device",
     "mando_clean_psl",
     "mando_filter_default_params",
     "mando_filter_sam",
@@ -222,6 +223,7 @@ def load(path: str | None = None):
         lib.mando_list_root_names.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64, _P, _P]
         lib.mando_root_sizes.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, _P]
         lib.mando_sam_to_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, _P]
+        lib.mando_sam_to_psl_device.argtypes = [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, _P]
         lib.mando_clean_psl.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, _P]
         lib.mando_filter_default_params.argtypes = [_P]
         lib.mando_filter_default_params.restype = None

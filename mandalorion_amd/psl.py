@@ -21,13 +21,23 @@ def split_loci(clean_psl: str, tmp_ss: str, sort_lines: bool = True, sorted_out:
     return nr.value, nl.value
 
 
-def sam_to_psl(sam: str, psl: str, mando: bool = True, threads: int = 0) -> int:
+def sam_to_psl(sam: str, psl: str, mando: bool = True, threads: int = 0, device: int | None | str = "auto") -> int:
     """emtrey.py -i sam -o psl [-m] (/root/reference/emtrey.py:31-193); returns PSL lines written.
     Raises MandoError where emtrey raises (unknown chromosome, missing cs tag in -m mode, zero-length
-    alignment, malformed CIGAR)."""
+    alignment, malformed CIGAR).  device: a GPU ordinal runs the conversion there
+    (mando_sam_to_psl_device, sam_kernel.hip); "auto" uses GPU 0 when one is visible; None the host C++
+    threads (mando_sam_to_psl).  Both write the same bytes."""
     n = ctypes.c_int64()
-    _lib.check(_lib.load().mando_sam_to_psl(sam.encode(), psl.encode(), 1 if mando else 0, int(threads),
-                                            ctypes.byref(n)))
+    lib = _lib.load()
+    if device == "auto":
+        device = 0 if _lib.device_count() > 0 else None
+    if device is not None:
+        ctx = _lib.context(int(device), slot=4)
+        _lib.check(lib.mando_sam_to_psl_device(ctx.handle, sam.encode(), psl.encode(), 1 if mando else 0,
+                                               ctypes.byref(n)))
+    else:
+        _lib.check(lib.mando_sam_to_psl(sam.encode(), psl.encode(), 1 if mando else 0, int(threads),
+                                        ctypes.byref(n)))
     return n.value
 
 

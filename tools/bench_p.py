@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Module P throughput (SAM -> PSL -> clean PSL -> sorted + locus split), native vs the reference.
 
-usage: python tools/bench_p.py [n_reads] [threads] [--ref]
+usage: python tools/bench_p.py [n_reads] [threads] [--ref] [--gpu]
 Input: tests/golden/make_sam_vectors.make_input with n_reads reads (~1.3 records each).  With --ref
 (this container only; /root/reference does not exist on the GPU box) the reference's
 `python3 emtrey.py -m -t T` + clean_psl + `sort` + get_chromosomes run on the same file under a stand-in
@@ -35,9 +35,17 @@ def main():
         out["records"] = m.make_input(sam, n_reads=n_reads)
         out["gen_s"] = round(time.perf_counter() - t, 2)
         out["sam_mb"] = round(os.path.getsize(sam) / 1e6, 1)
+        if "--gpu" in sys.argv:
+            # the GPU conversion (sam_kernel.hip) beside the host threads' one: same bytes, both timed
+            psl.sam_to_psl(sam, os.path.join(tmp, "g.psl"), mando=True, device=0)  # warm (context, code)
+            tg = time.perf_counter()
+            psl.sam_to_psl(sam, os.path.join(tmp, "g.psl"), mando=True, device=0)
+            out["sam_to_psl_gpu_s"] = round(time.perf_counter() - tg, 3)
         t0 = time.perf_counter()
-        psl.sam_to_psl(sam, os.path.join(tmp, "a.psl"), mando=True, threads=threads)
+        psl.sam_to_psl(sam, os.path.join(tmp, "a.psl"), mando=True, threads=threads, device=None)
         t1 = time.perf_counter()
+        if "--gpu" in sys.argv:
+            out["gpu_equals_host"] = open(os.path.join(tmp, "g.psl"), "rb").read() == open(os.path.join(tmp, "a.psl"), "rb").read()
         psl.clean_psl(os.path.join(tmp, "a.psl"), os.path.join(tmp, "a.clean.psl"), True)
         t2 = time.perf_counter()
         psl.split_loci(os.path.join(tmp, "a.clean.psl"), os.path.join(tmp, "ss"), True, os.path.join(tmp, "a.sorted.psl"))
