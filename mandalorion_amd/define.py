@@ -523,6 +523,13 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
     # with several chunks in flight, two cores stay with the GPU driver, assembly and compaction threads
     n_cpu = threads if threads > 0 else (os.cpu_count() or 1)
     cl_threads = max(1, n_cpu - 2) if len(parts) > 1 and n_cpu > 4 else threads
+    if world > 1:
+        # several ranks on one node read their locus files from one page cache at once: 8 ranks x 2
+        # reader threads read their real 8-rank config-4 shares in 0.59 s (104 GB/s in all), 8 x 16 in
+        # 1.16-1.40 s (48 GB/s: the readers contend; profiles/r08a_read_contention_*).  So a rank's
+        # clustering reads with its share of 16 readers per node, at least 2.
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "0")) or world
+        cl_threads = min(cl_threads if cl_threads > 0 else n_cpu, max(2, 16 // max(1, local_world)))
 
     # backpressure: at most _MAX_INFLIGHT chunks hold their buffers (locus text on host and device,
     # clustering results) at once -- clustering runs ahead of the POA otherwise, and a many-chunk input
