@@ -320,6 +320,11 @@ int mando_write_blocks(int32_t fd, const uint8_t *buf, const int64_t *src_off, c
  * get_chromosomes (SpliceDefineConsensus.py:442-495): one <out_dir>/<chrom>~<start>~<end>.psl per locus. */
 int mando_split_loci(const char *psl_path, const char *out_dir, int32_t sort_lines, const char *sorted_out,
                      int64_t *n_records, int64_t *n_loci);
+/* The same with the parse and the sort on the ctx's GPU (psl_kernel.hip: a wave per line, a chain of
+ * stable radix sorts over the line order; the file writes stay on the host), byte-identical to
+ * mando_split_loci; MANDO_E_UNSUPPORTED for a chromosome name over 32 bytes. */
+int mando_split_loci_device(mando_ctx *ctx, const char *psl_path, const char *out_dir, int32_t sort_lines,
+                            const char *sorted_out, int64_t *n_records, int64_t *n_loci);
 
 /* The D module's locus roots (defineIsoforms.py:130-139, `roots` of main): every entry of `dir` that is a
  * regular file whose name holds ".psl", cut at the first ".psl", deduplicated, sorted by

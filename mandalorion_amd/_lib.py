@@ -59,6 +59,7 @@ EXPORTED = (
     "mando_format_outputs",
     "mando_write_blocks",
     "mando_split_loci",
+    "mando_split_loci_device",
     "mando_list_roots",
     "mando_list_root_names",
     "mando_root_sizes",
@@ -218,6 +219,8 @@ def load(path: str | None = None):
         lib.mando_orient_segments.argtypes = [_P, _P, _I64, _P, _P, _P, _I64, _P, ctypes.c_int32, _P]
         lib.mando_poa_segments.argtypes = [_P, _P, _P, _I64, _P, _P, _P, _P, _I64, _P, _P, _I64, _P, _P]
         lib.mando_split_loci.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p, _P, _P]
+        lib.mando_split_loci_device.argtypes = [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p,
+                                                _P, _P]
         lib.mando_list_roots.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64, _P,
                                          ctypes.c_int64, _P, _P]
         lib.mando_list_root_names.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64, _P, _P]

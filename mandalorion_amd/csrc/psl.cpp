@@ -28,14 +28,11 @@
 
 #include "../../include/mando.h"
 
+#include "psl_split.h"
+
 namespace {
 
-struct Line {
-    std::string_view text;  // without the trailing newline
-    std::string_view chrom; // field 14 (index 13)
-    int64_t start = 0, end = 0;
-    bool start_ok = false;
-};
+using mando::psl::Line;
 
 // leading number of a field the way `sort -n` reads it in the C locale (no thousands separator)
 int64_t sort_num(std::string_view s, bool &ok) {
@@ -109,6 +106,14 @@ extern "C" int mando_split_loci(const char *psl_path, const char *out_dir, int32
             return a.text < b.text;  // GNU sort's last-resort comparison (whole line, bytes)
         });
     }
+    return mando::psl::split_write_ordered(lines, out_dir, sorted_out, n_records, n_loci);
+}
+
+namespace mando {
+namespace psl {
+
+int split_write_ordered(const std::vector<Line> &lines, const char *out_dir, const char *sorted_out,
+                        int64_t *n_records, int64_t *n_loci) {
     if (sorted_out) {  // clean.sorted.psl, as the reference's sort writes it
         FILE *o = fopen(sorted_out, "wb");
         if (!o) return MANDO_E_ARG;
@@ -160,6 +165,9 @@ extern "C" int mando_split_loci(const char *psl_path, const char *out_dir, int32
     if (n_loci) *n_loci = nloc;
     return MANDO_OK;
 }
+
+}  // namespace psl
+}  // namespace mando
 
 // The directory scan of defineIsoforms.py:130-139 (+ the file sizes the D driver plans its chunks
 // with) without a Python stat per file.  with_sizes == false (mando_list_root_names): the entry type

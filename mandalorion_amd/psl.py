@@ -10,14 +10,25 @@ import os
 from . import _lib
 
 
-def split_loci(clean_psl: str, tmp_ss: str, sort_lines: bool = True, sorted_out: str | None = None) -> tuple[int, int]:
-    """Writes <tmp_ss>/<chrom>~<start>~<end>.psl per locus; returns (records, loci)."""
+def split_loci(clean_psl: str, tmp_ss: str, sort_lines: bool = True, sorted_out: str | None = None,
+               device: int | None | str = "auto") -> tuple[int, int]:
+    """Writes <tmp_ss>/<chrom>~<start>~<end>.psl per locus; returns (records, loci).  device: a GPU
+    ordinal parses and sorts there (mando_split_loci_device, psl_kernel.hip); "auto" uses GPU 0 when one
+    is visible; None the host C++ (mando_split_loci).  Both write the same bytes."""
     os.makedirs(tmp_ss, exist_ok=True)
     nr = ctypes.c_int64()
     nl = ctypes.c_int64()
-    _lib.check(_lib.load().mando_split_loci(clean_psl.encode(), tmp_ss.encode(), 1 if sort_lines else 0,
-                                            sorted_out.encode() if sorted_out else None, ctypes.byref(nr),
-                                            ctypes.byref(nl)))
+    lib = _lib.load()
+    if device == "auto":
+        device = 0 if _lib.device_count() > 0 else None
+    srt = sorted_out.encode() if sorted_out else None
+    if device is not None:
+        ctx = _lib.context(int(device), slot=4)
+        _lib.check(lib.mando_split_loci_device(ctx.handle, clean_psl.encode(), tmp_ss.encode(), 1 if sort_lines else 0,
+                                               srt, ctypes.byref(nr), ctypes.byref(nl)))
+    else:
+        _lib.check(lib.mando_split_loci(clean_psl.encode(), tmp_ss.encode(), 1 if sort_lines else 0, srt,
+                                        ctypes.byref(nr), ctypes.byref(nl)))
     return nr.value, nl.value
 
 

@@ -48,8 +48,18 @@ def main():
             out["gpu_equals_host"] = open(os.path.join(tmp, "g.psl"), "rb").read() == open(os.path.join(tmp, "a.psl"), "rb").read()
         psl.clean_psl(os.path.join(tmp, "a.psl"), os.path.join(tmp, "a.clean.psl"), True)
         t2 = time.perf_counter()
-        psl.split_loci(os.path.join(tmp, "a.clean.psl"), os.path.join(tmp, "ss"), True, os.path.join(tmp, "a.sorted.psl"))
+        psl.split_loci(os.path.join(tmp, "a.clean.psl"), os.path.join(tmp, "ss"), True, os.path.join(tmp, "a.sorted.psl"),
+                       device=None)
         t3 = time.perf_counter()
+        if "--gpu" in sys.argv:
+            tg = time.perf_counter()
+            psl.split_loci(os.path.join(tmp, "a.clean.psl"), os.path.join(tmp, "ssg"), True,
+                           os.path.join(tmp, "g.sorted.psl"), device=0)
+            out["sort_split_gpu_s"] = round(time.perf_counter() - tg, 3)
+            out["split_gpu_equals_host"] = (open(os.path.join(tmp, "g.sorted.psl"), "rb").read() ==
+                                            open(os.path.join(tmp, "a.sorted.psl"), "rb").read() and
+                                            sorted(os.listdir(os.path.join(tmp, "ssg"))) ==
+                                            sorted(os.listdir(os.path.join(tmp, "ss"))))
         out["native_s"] = {"sam_to_psl": round(t1 - t0, 3), "clean": round(t2 - t1, 3), "sort_split": round(t3 - t2, 3)}
         out["native_records_per_s"] = round(out["records"] / (t3 - t0))
         if "--ref" in sys.argv:
