@@ -337,6 +337,10 @@ _BIG_CHUNK_BYTES = _CHUNK_BYTES if "MANDO_CHUNK_BYTES" in os.environ else 6 << 3
 _TWO_CHUNK_BYTES = 8 << 30
 # fewer loci than this always run in one chunk (a few large loci: SIRV-like, config 5)
 _MIN_LOCI_CHUNKED = 1024
+# the first chunk of a many-chunk plan, as a share of one chunk: small, so the first POA launch starts
+# early, large enough to fill the chip (config 4: 0.4 against 0.6 / 0.75 in r07f; MANDO_FIRST_FRAC is the
+# A/B knob)
+_FIRST_FRAC = float(os.environ.get("MANDO_FIRST_FRAC", "0.4"))
 def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0,
                 fracs: list | None = None) -> tuple[int, list | None]:
     """(chunks, cumulative byte fractions of the cuts or None for equal chunks).  n_chunks > 0 (or
@@ -352,7 +356,7 @@ def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0,
         else:
             k = -(-text_bytes // (_BIG_CHUNK_BYTES if text_bytes >= _BIG_INPUT_BYTES else _CHUNK_BYTES))
             if k > 1:
-                fracs = [(0.4 + i) / k for i in range(k)]
+                fracs = [(_FIRST_FRAC + i) / k for i in range(k)]
                 n_chunks = k + 1
             else:
                 n_chunks = 2
@@ -1016,10 +1020,11 @@ def _place(path: str, buf: np.ndarray, src: np.ndarray, roots: np.ndarray, sizes
     got_data = _alltoallv(comm, data)
     lo, hi = int(bnd[me]), int(bnd[me + 1])
     rb = np.zeros(max(hi - lo, 1), dtype=np.uint8)
-    # in-process stand-in communicators (rehearsals: no alltoallv) deliver incomplete data in their early
-    # passes, whose pieces are dropped; over a real transport every piece must land inside this rank's
-    # range and the pieces must tile it, or the exchange disagreed and the file would carry zero bytes
-    standin = not hasattr(comm, "alltoallv")
+    # in-process stand-in communicators (tests without alltoallv, tools/rank_rehearsal.py's `standin`
+    # transport) deliver incomplete data in their early passes, whose pieces are dropped; over a real
+    # transport every piece must land inside this rank's range and the pieces must tile it, or the
+    # exchange disagreed and the file would carry zero bytes
+    standin = getattr(comm, "standin", False) or not hasattr(comm, "alltoallv")
     sel, starts, lens, outs = [], [], [], []
     got = 0
     for r in range(world):
