@@ -67,7 +67,13 @@ int mando_device_count(int *out);
  * sleep on its completion signal instead of spinning; spinning cost ~1.6 cores per GPU on config 4).
  * That flag is process-wide for the device: it also applies to the host application's own waits on
  * that device, and HIP refuses it when the application has already initialised the device with other
- * flags (the application's flags are then kept); mando_ctx_blocking_sync() reports which. */
+ * flags (the application's flags are then kept); mando_ctx_blocking_sync() reports which.
+ * Each context's stream (and each internal stream: POA lanes, the clustering's copy stream) runs on a
+ * hardware queue of its own -- a CU-masked stream with every CU enabled -- so two contexts' work
+ * overlaps however many streams the process holds (HIP shares 4 hardware queues among plain streams).
+ * Such streams are blocking with respect to the legacy null stream: an application's null-stream
+ * commands on the same device wait for the library's queued work.  MANDO_SHARED_QUEUES=1 makes them
+ * plain non-blocking streams. */
 int mando_ctx_create(int device_ordinal, mando_ctx **out);
 void mando_ctx_destroy(mando_ctx *ctx);
 /* 1 when the ctx's device waits with blocking sync, 0 when it spins (flags set before the ctx), <0 on

@@ -1,10 +1,12 @@
 // capi.hip — C-ABI of libmando (declared in include/mando.h): contexts, device buffers, batch
 // planning for the POA kernel (capacity estimates, LPT work order, overflow re-runs).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <chrono>
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <numeric>
@@ -612,6 +614,32 @@ namespace mando {
 int set_error(int code, const std::string &msg) { return fail(code, msg); }
 int ctx_device(const mando_ctx *ctx) { return ctx->device; }
 hipStream_t ctx_stream(const mando_ctx *ctx) { return ctx->stream; }
+
+// Every stream of the library gets a hardware queue of its own.  HIP maps plain streams onto at most
+// GPU_MAX_HW_QUEUES (4) hardware queues per process and, past that, puts a new stream on an existing
+// queue, where its work waits behind everything queued before it whatever the streams' dependencies:
+// one D call creates six (POA context, POA lanes x2, orientation context, clustering context and copy
+// stream; a multi-rank run adds the communicator's), and the config-4 trace showed the orientation
+// context sharing the narrow POA lane's queue -- each chunk's orientation started only when the previous
+// chunk's narrow POA grid ended, 64 ms on the path between POA launches (profiles/r08a_trace_*,
+// r08h_queue_probe_*).  A stream created with a CU mask always gets a new queue; the mask here enables
+// every CU, so it changes nothing else.  MANDO_SHARED_QUEUES=1 goes back to plain streams (A/B).
+hipError_t create_stream(hipStream_t *out) {
+    static const bool shared = [] {
+        const char *e = std::getenv("MANDO_SHARED_QUEUES");
+        return e && std::atoi(e) != 0;
+    }();
+    if (shared) return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    int n_cu = 0;
+    e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    std::vector<uint32_t> mask((size_t)(n_cu + 31) / 32, 0xffffffffu);
+    if (n_cu % 32) mask.back() = (1u << (n_cu % 32)) - 1u;
+    return hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data());
+}
 }  // namespace mando
 
 extern "C" {
@@ -672,7 +700,7 @@ int mando_ctx_create(int device_ordinal, mando_ctx **out) {
     c->n_cu = prop.multiProcessorCount;
     c->n_cu_act = c->n_cu;
     c->total_mem = (int64_t)prop.totalGlobalMem;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    if (mando::create_stream(&c->stream) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return fail(MANDO_E_HIP, "stream/event creation failed");
@@ -870,7 +898,7 @@ int poa_batch_impl(mando_ctx *ctx, const mando_poa_params *params, const std::ve
             if (!ctx->ev_fork) {
                 HIP_TRY(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
                 for (int k = 0; k < 2; ++k) {
-                    HIP_TRY(hipStreamCreateWithFlags(&ctx->lane_stream[k], hipStreamNonBlocking));
+                    HIP_TRY(mando::create_stream(&ctx->lane_stream[k]));
                     HIP_TRY(hipEventCreateWithFlags(&ctx->ev_lane[k], hipEventDisableTiming));
                 }
             }

@@ -100,7 +100,7 @@ hipStream_t copy_stream(int device) {
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(device);
-        if (hipStreamCreateWithFlags(&streams[(size_t)device], hipStreamNonBlocking) != hipSuccess)
+        if (mando::create_stream(&streams[(size_t)device]) != hipSuccess)
             streams[(size_t)device] = nullptr;
         (void)hipSetDevice(cur);
     }

@@ -11,4 +11,6 @@ namespace mando {
 int set_error(int code, const std::string &msg);
 int ctx_device(const mando_ctx *ctx);
 hipStream_t ctx_stream(const mando_ctx *ctx);
+// a non-blocking stream on a hardware queue of its own (see capi.hip); the current device's
+hipError_t create_stream(hipStream_t *out);
 }  // namespace mando
