@@ -3853,6 +3853,20 @@ __device__ __forceinline__ int update_graph(SharedState &sh, const uint8_t *q, i
                             int &ng, int lane) {
     const PoaRunArgs a = args_of(sh);
     Slot s = slot_of(sh);
+#ifdef MANDO_UPD_PROF
+    // dev build: cycles of the update's passes in prof phases 8..11 (1, 2, 3, 4 + 5)
+    uint64_t upd_t = clock64();
+#define MANDO_UPD_MARK(k)                                                                \
+    do {                                                                                 \
+        const uint64_t t_ = clock64();                                                   \
+        if (a.prof && lane == 0) a.prof[(int64_t)blockIdx.x * kProfPhases + (k)] += (int64_t)(t_ - upd_t); \
+        upd_t = t_;                                                                      \
+    } while (0)
+#else
+#define MANDO_UPD_MARK(k) \
+    do {                  \
+    } while (0)
+#endif
     // Path kinds per query position: 0 = existing node (matched, or a reused aligned node),
     // 1 = new node aligned to the DP row's node (mismatch), 2 = new inserted node.
     // Topological order invariant kept here: every aligned group occupies a contiguous block of
@@ -3943,6 +3957,7 @@ __device__ __forceinline__ int update_graph(SharedState &sh, const uint8_t *q, i
     err = bcast0(err);
     if (err != kStOk) return err;
     wave_sync();
+    MANDO_UPD_MARK(8);
     // pass 2 (backwards): slot (old row) each new node is inserted in front of
     int nxt_q = qlen, nxt_R = n_old - 1;
     for (int c = nch - 1; c >= 0; --c) {
@@ -3972,6 +3987,7 @@ __device__ __forceinline__ int update_graph(SharedState &sh, const uint8_t *q, i
         }
     }
     wave_sync();
+    MANDO_UPD_MARK(9);
     // pass 3: shift old rows by the number of new nodes inserted before (and at) them
     int carry = 0;
     for (int c = 0; c * kWave < n_old; ++c) {
@@ -3988,6 +4004,7 @@ __device__ __forceinline__ int update_graph(SharedState &sh, const uint8_t *q, i
         }
     }
     wave_sync();
+    MANDO_UPD_MARK(10);
     // pass 4: place the new nodes (mismatch node first, then the insertion run, before row R)
     for (int c = 0; c < nch; ++c) {
         const int qi = c * kWave + lane;
@@ -4016,6 +4033,8 @@ __device__ __forceinline__ int update_graph(SharedState &sh, const uint8_t *q, i
         sh.slot.order2 = s.order;
     }
     wave_sync();
+    MANDO_UPD_MARK(11);
+#undef MANDO_UPD_MARK
     return kStOk;
 }
 
