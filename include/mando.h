@@ -402,6 +402,12 @@ int mando_psl_to_gtf(const char *psl_path, const char *gtf_path);
  * every isoform of the filtered PSL, from reads2isoforms.txt and the read files (FASTA/FASTQ, gz). */
 int mando_quantify(const char *const *fasta_paths, int32_t n_fasta, const char *r2i_path,
                    const char *filtered_psl, const char *out_quant, const char *out_tpm);
+/* mando_quantify with its two joins on the GPU of ctx (quant_kernel.hip): read name -> read file for every
+ * reads2isoforms.txt line and isoform -> its lines' files for every filtered isoform, as radix sorts and
+ * binary searches over 64-bit name hashes with every hit confirmed byte for byte.  The host reads the
+ * files and writes the tables exactly as mando_quantify does (same outputs, same errors). */
+int mando_quantify_device(mando_ctx *ctx, const char *const *fasta_paths, int32_t n_fasta, const char *r2i_path,
+                          const char *filtered_psl, const char *out_quant, const char *out_tpm);
 
 #ifdef __cplusplus
 }

@@ -71,6 +71,7 @@ EXPORTED = (
     "mando_filter_isoforms",
     "mando_psl_to_gtf",
     "mando_quantify",
+    "mando_quantify_device",
 )
 
 STATUS = {
@@ -234,6 +235,7 @@ def load(path: str | None = None):
         lib.mando_filter_isoforms.argtypes = [_P] + [ctypes.c_char_p] * 7 + [_P]
         lib.mando_psl_to_gtf.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         lib.mando_quantify.argtypes = [_P, ctypes.c_int32] + [ctypes.c_char_p] * 4
+        lib.mando_quantify_device.argtypes = [_P, _P, ctypes.c_int32] + [ctypes.c_char_p] * 4
         lib.mando_pack_segments.argtypes = [_P, _P, _P, _P, _P, _I64, _P, _P, ctypes.c_int32]
         lib.mando_format_outputs.argtypes = [_I64, _I64] + [_P] * 12 + [_P, _I64, _P, _P, _I64, _P, _P, _P,
                                                                          ctypes.c_int32]

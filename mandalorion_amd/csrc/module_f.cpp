@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/mando.h"
+#include "quant.h"
 
 namespace {
 
@@ -65,10 +66,8 @@ bool read_any(const char *path, string &out) {
 }
 
 // mappy.fastx_read: FASTA or FASTQ records, name = header up to the first blank
-template <class F>
-bool fastx_each(const char *path, F &&fn) {
-    string buf;
-    if (!read_any(path, buf)) return false;
+template <bool kSeq = true, class F>
+bool fastx_each_in(const string &buf, F &&fn) {
     size_t p = 0;
     const size_t n = buf.size();
     auto line_end = [&](size_t a) {
@@ -86,17 +85,19 @@ bool fastx_each(const char *path, F &&fn) {
         const string_view name = head.substr(0, sp);
         p = e + 1;
         string seq;
+        size_t seqlen = 0;
         while (p < n && buf[p] != '>' && buf[p] != '@' && !(fq && buf[p] == '+')) {
             e = line_end(p);
             string_view l(buf.data() + p, e - p);
             if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
-            seq.append(l.data(), l.size());
+            if (kSeq) seq.append(l.data(), l.size());
+            seqlen += l.size();
             p = e + 1;
         }
         if (fq && p < n && buf[p] == '+') {
             p = line_end(p) + 1;  // '+' line
             size_t q = 0;
-            while (p < n && q < seq.size()) {
+            while (p < n && q < seqlen) {
                 e = line_end(p);
                 q += e - p;
                 p = e + 1;
@@ -105,6 +106,12 @@ bool fastx_each(const char *path, F &&fn) {
         fn(name, std::move(seq));
     }
     return true;
+}
+template <class F>
+bool fastx_each(const char *path, F &&fn) {
+    string buf;
+    if (!read_any(path, buf)) return false;
+    return fastx_each_in(buf, std::forward<F>(fn));
 }
 
 void split(string_view s, char sep, vector<string_view> &out) {
@@ -528,6 +535,73 @@ void process_chr(const mando_filter_params &P, const string &chrom, vector<Iso> 
 
 }  // namespace
 
+namespace mando {
+namespace modq {
+
+bool fastx_names(const char *path, std::string &buf, std::vector<std::pair<int64_t, int32_t>> &names) {
+    names.clear();
+    if (!read_any(path, buf)) return false;
+    const char *base = buf.data();
+    return fastx_each_in<false>(buf, [&](string_view nm, string &&) {
+        names.push_back({(int64_t)(nm.data() - base), (int32_t)nm.size()});
+    });
+}
+
+bool psl_isoforms(const std::string &buf, std::vector<std::string_view> &isos) {
+    vector<string_view> a;
+    size_t p = 0;
+    while (p < buf.size()) {
+        size_t e = buf.find('\n', p);
+        if (e == string::npos) e = buf.size();
+        const string_view ln(buf.data() + p, e - p);
+        p = e + 1;
+        split(strip(ln), '\t', a);
+        if (a.size() < 10) return false;
+        isos.push_back(a[9]);
+    }
+    return true;
+}
+
+int write_tables(const std::vector<std::string> &samples, const std::vector<int64_t> &total,
+                 const std::vector<std::string_view> &isos, const std::vector<int64_t> &counts, const char *out_quant,
+                 const char *out_tpm) {
+    string q = "Isoform\t", t = "Isoform\t";
+    for (auto &s : samples) {
+        q += s + "\t";
+        t += s + "\t";
+    }
+    q += "\n";
+    t += "\n";
+    const size_t ns = samples.size();
+    for (size_t k = 0; k < isos.size(); ++k) {
+        q += string(isos[k]) + "\t";
+        t += string(isos[k]) + "\t";
+        for (size_t s = 0; s < ns; ++s) {
+            if (total[s] == 0) return MANDO_E_ARG;  // ZeroDivisionError in the reference
+            const int64_t c = counts[k * ns + s];
+            q += std::to_string(c) + "\t";
+            t += py_repr(py_round3((double)c / (double)total[s] * 1000000.0)) + "\t";
+        }
+        q += "\n";
+        t += "\n";
+    }
+    FILE *fq = fopen(out_quant, "wb");
+    FILE *ft = fopen(out_tpm, "wb");
+    if (!fq || !ft) {
+        if (fq) fclose(fq);
+        if (ft) fclose(ft);
+        return MANDO_E_ARG;
+    }
+    fwrite(q.data(), 1, q.size(), fq);
+    fwrite(t.data(), 1, t.size(), ft);
+    fclose(fq);
+    fclose(ft);
+    return MANDO_OK;
+}
+
+}  // namespace modq
+}  // namespace mando
+
 extern "C" {
 
 void mando_filter_default_params(mando_filter_params *p) {
@@ -739,7 +813,9 @@ int mando_quantify(const char *const *fasta_paths, int32_t n_fasta, const char *
         samples.push_back(loc);
         total.push_back(0);
         const int si = (int)samples.size() - 1;
-        if (!fastx_each(loc.c_str(), [&](string_view nm, string &&) {
+        string fbuf;
+        if (!read_any(loc.c_str(), fbuf)) return MANDO_E_ARG;
+        if (!fastx_each_in<false>(fbuf, [&](string_view nm, string &&) {
                 read_sample[string(nm)] = si;
                 ++total[(size_t)si];
             }))
@@ -761,49 +837,16 @@ int mando_quantify(const char *const *fasta_paths, int32_t n_fasta, const char *
         if (it == read_sample.end()) return MANDO_E_ARG;  // KeyError in the reference
         r2i[string(a[1])].push_back(it->second);
     }
-    string q = "Isoform\t", t = "Isoform\t";
-    for (auto &s : samples) {
-        q += s + "\t";
-        t += s + "\t";
-    }
-    q += "\n";
-    t += "\n";
-    if (!read_file(filtered_psl, buf)) return MANDO_E_ARG;
-    p = 0;
-    while (p < buf.size()) {
-        size_t e = buf.find('\n', p);
-        if (e == string::npos) e = buf.size();
-        const string_view ln(buf.data() + p, e - p);
-        p = e + 1;
-        split(strip(ln), '\t', a);
-        if (a.size() < 10) return MANDO_E_ARG;
-        const string iso(a[9]);
-        auto it = r2i.find(iso);
+    string pbuf;
+    vector<string_view> isos;
+    if (!read_file(filtered_psl, pbuf) || !mando::modq::psl_isoforms(pbuf, isos)) return MANDO_E_ARG;
+    vector<int64_t> counts(isos.size() * samples.size(), 0);
+    for (size_t k = 0; k < isos.size(); ++k) {
+        auto it = r2i.find(string(isos[k]));
         if (it == r2i.end()) return MANDO_E_ARG;  // KeyError in the reference
-        vector<int64_t> cnt(samples.size(), 0);
-        for (int s : it->second) ++cnt[(size_t)s];
-        q += iso + "\t";
-        t += iso + "\t";
-        for (size_t s = 0; s < samples.size(); ++s) {
-            if (total[s] == 0) return MANDO_E_ARG;  // ZeroDivisionError in the reference
-            q += std::to_string(cnt[s]) + "\t";
-            t += py_repr(py_round3((double)cnt[s] / (double)total[s] * 1000000.0)) + "\t";
-        }
-        q += "\n";
-        t += "\n";
+        for (int s : it->second) ++counts[k * samples.size() + (size_t)s];
     }
-    FILE *fq = fopen(out_quant, "wb");
-    FILE *ft = fopen(out_tpm, "wb");
-    if (!fq || !ft) {
-        if (fq) fclose(fq);
-        if (ft) fclose(ft);
-        return MANDO_E_ARG;
-    }
-    fwrite(q.data(), 1, q.size(), fq);
-    fwrite(t.data(), 1, t.size(), ft);
-    fclose(fq);
-    fclose(ft);
-    return MANDO_OK;
+    return mando::modq::write_tables(samples, total, isos, counts, out_quant, out_tpm);
 }
 
 }  // extern "C"

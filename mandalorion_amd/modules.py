@@ -78,10 +78,16 @@ def module_f(path: str, isoform_fasta: str, genome_fasta: str, params: FilterPar
     return n
 
 
-def quantify(folder: str, fasta_files: list[str]) -> None:
-    """assignReadsToIsoforms.py -m folder -f files: Isoforms.filtered.clean.quant / .tpm in folder."""
+def quantify(folder: str, fasta_files: list[str], device="auto") -> None:
+    """assignReadsToIsoforms.py -m folder -f files: Isoforms.filtered.clean.quant / .tpm in folder.
+    device: a GPU ordinal (the joins on the GPU, mando_quantify_device), None (host C++, mando_quantify) or
+    "auto" (GPU 0 when one is visible)."""
     arr = (ctypes.c_char_p * len(fasta_files))(*[f.encode() for f in fasta_files])
-    _lib.check(_lib.load().mando_quantify(arr, len(fasta_files), os.path.join(folder, "reads2isoforms.txt").encode(),
-                                          os.path.join(folder, "Isoforms.filtered.clean.psl").encode(),
-                                          os.path.join(folder, "Isoforms.filtered.clean.quant").encode(),
-                                          os.path.join(folder, "Isoforms.filtered.clean.tpm").encode()))
+    paths = [os.path.join(folder, f).encode() for f in ("reads2isoforms.txt", "Isoforms.filtered.clean.psl",
+                                                          "Isoforms.filtered.clean.quant", "Isoforms.filtered.clean.tpm")]
+    dev = (0 if _lib.device_count() > 0 else None) if device == "auto" else device
+    lib = _lib.load()
+    if dev is None:
+        _lib.check(lib.mando_quantify(arr, len(fasta_files), *paths))
+    else:
+        _lib.check(lib.mando_quantify_device(_lib.context(int(dev), slot=4).handle, arr, len(fasta_files), *paths))
