@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/mando.h"
+#include "modf.h"
 #include "quant.h"
 
 namespace {
@@ -215,13 +216,10 @@ int64_t abundance_of(string_view name, bool &ok) {
     return v;
 }
 
-struct Iso {
-    string name;
-    vector<string> fields;       // the clean PSL line, split on tabs
-    vector<int64_t> coords;      // block start, block end, ...
-    char dir = '+';
-    int64_t abundance = 0;
-};
+using mando::modf::ChrState;
+using mando::modf::Contain;
+using mando::modf::Iso;
+using mando::modf::Ivs;
 
 struct ChrOut {
     vector<int> kept;  // indices into isos, output order
@@ -229,8 +227,6 @@ struct ChrOut {
     int err = 0;
 };
 
-// merged [s, e) intervals
-using Ivs = vector<std::pair<int64_t, int64_t>>;
 Ivs merged_extended(const vector<int64_t> &c, int sw) {
     Ivs v;
     for (size_t k = 0; k + 1 < c.size(); k += 2) v.push_back({c[k] - sw, c[k + 1] + sw});
@@ -257,15 +253,15 @@ int64_t ivs_count(const Ivs &m, int64_t s, int64_t e) {  // bases of [s, e) cove
     return n;
 }
 
-// filterIsoforms.process_chr for one chromosome
-void process_chr(const mando_filter_params &P, const string &chrom, vector<Iso> &isos,
-                 const vector<std::pair<string_view, string_view>> &lines_raw, const string *chr_seq,
-                 const std::set<int64_t> *wl_plus, const std::set<int64_t> *wl_minus, ChrOut &out) {
+// filterIsoforms.process_chr for one chromosome, part 1: parse_clean_psl (absolute filters), get_count and
+// filter_isoforms (relative expression), and the candidate index of look_for_contained_isoforms
+void chr_stage1(const mando_filter_params &P, const string &chrom, vector<Iso> &isos,
+                const vector<std::pair<string_view, string_view>> &lines_raw, ChrState &S, ChrOut &out) {
     string &R = out.reasons;
     R += chrom + "\n";
     // parse_clean_psl (absolute filters), input order
     std::unordered_set<string> done;
-    vector<int> listed;  // names passing parse, in line order (psl_dict)
+    vector<int> &listed = S.listed;  // names passing parse, in line order (psl_dict)
     vector<string_view> a, bs, bt;
     for (auto &lr : lines_raw) {
         split(strip(lr.second), '\t', a);
@@ -357,7 +353,7 @@ void process_chr(const mando_filter_params &P, const string &chrom, vector<Iso> 
     // filter_isoforms: sorted names, relative expression
     vector<int> order = listed;
     std::sort(order.begin(), order.end(), [&](int x, int y) { return isos[(size_t)x].name < isos[(size_t)y].name; });
-    vector<int> kept1;
+    vector<int> &kept1 = S.kept1;
     for (int k : order) {
         const Iso &I = isos[(size_t)k];
         int64_t s0, e0;
@@ -392,19 +388,111 @@ void process_chr(const mando_filter_params &P, const string &chrom, vector<Iso> 
     }
     // look_for_contained_isoforms
     const int sw = P.splice_window;
-    vector<Ivs> ext(isos.size());
+    vector<Ivs> &ext = S.ext;
+    ext.assign(isos.size(), Ivs());
     for (int k : kept1) ext[(size_t)k] = merged_extended(isos[(size_t)k].coords, sw);
     // candidates by direction, sorted by span start for the overlap search
-    vector<int> bydir[2];
+    auto &bydir = S.bydir;
     for (int k : kept1) bydir[isos[(size_t)k].dir == '-'].push_back(k);
     for (auto &v : bydir)
         std::sort(v.begin(), v.end(), [&](int x, int y) {
             return ext[(size_t)x].front().first < ext[(size_t)y].front().first;
         });
-    int64_t maxspan[2] = {0, 0};
+    auto &maxspan = S.maxspan;
     for (int d = 0; d < 2; ++d)
         for (int k : bydir[d])
             maxspan[d] = std::max(maxspan[d], ext[(size_t)k].back().second - ext[(size_t)k].front().first);
+}
+
+// trimmed block coordinates of look_for_contained_isoforms (the first start +20, the last end -20,
+// each clamped by its block's other end; for one block the end clamps against the trimmed start)
+void trimmed(const vector<int64_t> &co, vector<int64_t> &c) {
+    c = co;
+    c[0] = std::min(c[0] + 20, c[1]);
+    c[c.size() - 1] = std::max(c[c.size() - 1] - 20, c[c.size() - 2]);
+}
+
+// every junction of c (trimmed, isoform A) matches one of mc (isoform B): the reference's dd table keeps,
+// for a base1 position, the window of B's LAST junction whose base1 window holds it
+bool junctions_contained(const vector<int64_t> &c, const vector<int64_t> &mc, int sw) {
+    std::unordered_map<int64_t, std::pair<int64_t, int64_t>> dd;  // base1 -> [b2lo, b2hi)
+    for (size_t jn = 1; jn + 1 < mc.size(); jn += 2)
+        for (int64_t b1 = mc[jn] - sw; b1 < mc[jn] + sw; ++b1) dd[b1] = {mc[jn + 1] - sw, mc[jn + 1] + sw};
+    for (size_t jn = 1; jn + 1 < c.size(); jn += 2) {
+        bool hit = false;
+        for (int64_t b1 = c[jn] - sw; b1 < c[jn] + sw && !hit; ++b1) {
+            auto it = dd.find(b1);
+            if (it == dd.end()) continue;
+            const int64_t a2lo = c[jn + 1] - sw, a2hi = c[jn + 1] + sw;
+            if (std::max(a2lo, it->second.first) < std::min(a2hi, it->second.second)) hit = true;
+        }
+        if (!hit) return false;
+    }
+    return true;
+}
+
+// look_for_contained_isoforms' candidate search for isoform k on the host (modf.h Contain)
+Contain contain_host(const mando_filter_params &P, const vector<Iso> &isos, const ChrState &S, int k) {
+    const Iso &I = isos[(size_t)k];
+    const int d = I.dir == '-';
+    vector<int64_t> c;
+    trimmed(I.coords, c);
+    const int64_t start = I.coords.front(), end = I.coords.back();
+    const int64_t pa0 = I.dir == '+' ? end + 3 : start - 23;
+    const int64_t lo = std::min(c.front(), pa0), hi = std::max(c.back(), pa0 + 20);
+    bool any_base = false;
+    for (size_t q = 0; q + 1 < c.size(); q += 2)
+        if (c[q] < c[q + 1]) any_base = true;
+    Contain r;
+    vector<int> status;
+    const auto &cand = S.bydir[d];
+    auto first = std::lower_bound(cand.begin(), cand.end(), lo - S.maxspan[d] - 1, [&](int x, int64_t v) {
+        return S.ext[(size_t)x].front().first < v;
+    });
+    for (auto it = first; it != cand.end(); ++it) {
+        const Ivs &m = S.ext[(size_t)*it];
+        if (m.front().first >= hi) break;
+        if (m.back().second <= lo) continue;
+        if (ivs_count(m, pa0, pa0 + 20) >= 10) {
+            ++r.n_extend;
+            if (r.ext_first < 0 || isos[(size_t)*it].name < isos[(size_t)r.ext_first].name) r.ext_first = *it;
+        }
+        if (any_base) {
+            bool all = true;
+            for (size_t q = 0; q + 1 < c.size() && all; q += 2)
+                if (c[q] < c[q + 1] && !ivs_cover(m, c[q], c[q + 1])) all = false;
+            if (all) status.push_back(*it);
+        }
+    }
+    if (!any_base) status = S.listed;  // no base to intersect over: every parsed isoform of the chromosome
+    r.n_status = (int64_t)status.size();
+    for (int mk : status) {
+        if (mk == k) continue;
+        const Iso &Mt = isos[(size_t)mk];
+        if (r.trig >= 0 && !(Mt.name < isos[(size_t)r.trig].name)) continue;
+        if (!junctions_contained(c, Mt.coords, P.splice_window)) continue;
+        int kind = 0;
+        if (Mt.abundance == 0)
+            kind = 3;
+        else if ((double)I.abundance / (double)Mt.abundance < P.internal_ratio)
+            kind = 1;
+        else if (std::llabs(I.coords.front() - Mt.coords.front()) < P.downstream_buffer &&
+                 std::llabs(I.coords.back() - Mt.coords.back()) < P.downstream_buffer && I.abundance < Mt.abundance)
+            kind = 2;
+        if (kind) {
+            r.trig = mk;
+            r.kind = kind;
+        }
+    }
+    return r;
+}
+
+// part 3: the polyA test and the containment decisions of kept1, in order, into the kept list and the
+// reason texts (filterIsoforms.py:125-278)
+void chr_stage3(const mando_filter_params &P, const vector<Iso> &isos, const ChrState &S, const vector<Contain> &dec,
+                const string *chr_seq, const std::set<int64_t> *wl_plus, const std::set<int64_t> *wl_minus,
+                ChrOut &out) {
+    string &R = out.reasons;
     const int64_t L = chr_seq ? (int64_t)chr_seq->size() : 0;
     auto py_slice_count = [&](int64_t s, int64_t e, char ch) {
         // chr_sequence[s:e].upper().count(ch) with Python slice semantics
@@ -412,125 +500,81 @@ void process_chr(const mando_filter_params &P, const string &chrom, vector<Iso> 
         if (e < 0) e = std::max<int64_t>(0, e + L);
         s = std::min(s, L);
         e = std::min(e, L);
-        int64_t c = 0;
-        for (int64_t x = s; x < e; ++x) c += (toupper((unsigned char)(*chr_seq)[(size_t)x]) == ch);
-        return c;
+        int64_t n = 0;
+        for (int64_t x = s; x < e; ++x) n += (toupper((unsigned char)(*chr_seq)[(size_t)x]) == ch);
+        return n;
     };
-    for (int k : kept1) {
+    for (size_t t = 0; t < S.kept1.size(); ++t) {
+        const int k = S.kept1[t];
         const Iso &I = isos[(size_t)k];
-        const int d = I.dir == '-';
-        vector<int64_t> c = I.coords;
-        const int64_t start = c.front(), end = c.back();
-        c[0] = std::min(c[0] + 20, c[1]);
-        c[c.size() - 1] = std::max(c[c.size() - 1] - 20, c[c.size() - 2]);
-        double Acontent;
-        int64_t pa0, polyApos;
+        const Contain &D = dec[t];
         if (!chr_seq) {
             out.err = MANDO_E_ARG;  // KeyError: chromosome not in the genome
             return;
         }
+        const int64_t start = I.coords.front(), end = I.coords.back();
+        double Acontent;
+        int64_t polyApos;
         if (I.dir == '+') {
             Acontent = (double)py_slice_count(end, end + 15, 'A') / 15.0;
-            pa0 = end + 3;
             polyApos = end;
         } else {
             Acontent = (double)py_slice_count(start - 15, start, 'T') / 15.0;
-            pa0 = start - 23;
             polyApos = start;
         }
-        // candidates: same direction, overlapping [min(blocks, polyA range) ...]
-        const int64_t lo = std::min(c.front(), pa0), hi = std::max(c.back(), pa0 + 20);
-        vector<int> extend, status;
-        bool any_base = false;
-        for (size_t q = 0; q + 1 < c.size(); q += 2)
-            if (c[q] < c[q + 1]) any_base = true;
-        const auto &cand = bydir[d];
-        auto first = std::lower_bound(cand.begin(), cand.end(), lo - maxspan[d] - 1, [&](int x, int64_t v) {
-            return ext[(size_t)x].front().first < v;
-        });
-        for (auto it = first; it != cand.end(); ++it) {
-            const Ivs &m = ext[(size_t)*it];
-            if (m.front().first >= hi) break;
-            if (m.back().second <= lo) continue;
-            if (ivs_count(m, pa0, pa0 + 20) >= 10) extend.push_back(*it);
-            if (any_base) {
-                bool all = true;
-                for (size_t q = 0; q + 1 < c.size() && all; q += 2)
-                    if (c[q] < c[q + 1] && !ivs_cover(m, c[q], c[q + 1])) all = false;
-                if (all) status.push_back(*it);
-            }
-        }
-        if (!any_base) status = listed;  // no base to intersect over: every parsed isoform of the chromosome
-        if (status.size() + extend.size() == 1) {
+        if (D.n_status + D.n_extend == 1) {
             out.kept.push_back(k);
             continue;
         }
         bool decision = true;
-        auto first_name = [&](const vector<int> &v) {
-            string b = isos[(size_t)v[0]].name;
-            for (int x : v) b = std::min(b, isos[(size_t)x].name);
-            return b;
-        };
-        if (!extend.empty() && Acontent > P.Acutoff) {
+        if (D.n_extend > 0 && Acontent > P.Acutoff) {
             const std::set<int64_t> *wl = I.dir == '+' ? wl_plus : wl_minus;
+            const string &fname = isos[(size_t)D.ext_first].name;
             if (wl && wl->count(polyApos)) {
-                R += I.name + " would have been filtered because at least one isoform (including " + first_name(extend) +
+                R += I.name + " would have been filtered because at least one isoform (including " + fname +
                      ") is extending beyond its polyA site and the genomic A content at its putative polyA site is " +
                      py_repr(Acontent) + " which is higher than the cutoff set to " + py_repr(P.Acutoff) +
                      "but it was kept because its polyA site was part of the polyA site whitelist\n";
             } else {
                 decision = false;
-                R += I.name + " filtered because at least one isoform (including " + first_name(extend) +
+                R += I.name + " filtered because at least one isoform (including " + fname +
                      ") is extending beyond its polyA site and the genomic A content at its putative polyA site is " +
                      py_repr(Acontent) + " which is higher than the cutoff set to " + py_repr(P.Acutoff) + "\n";
             }
         }
-        if (decision) {
-            std::sort(status.begin(), status.end(), [&](int x, int y) { return isos[(size_t)x].name < isos[(size_t)y].name; });
-            for (int mk : status) {
-                if (mk == k) continue;
-                const Iso &Mt = isos[(size_t)mk];
-                const vector<int64_t> &mc = Mt.coords;
-                // junction table of the match: base1 rows of a later junction replace earlier ones
-                std::unordered_map<int64_t, std::pair<int64_t, int64_t>> dd;  // base1 -> [b2lo, b2hi)
-                for (size_t jn = 1; jn + 1 < mc.size(); jn += 2)
-                    for (int64_t b1 = mc[jn] - sw; b1 < mc[jn] + sw; ++b1) dd[b1] = {mc[jn + 1] - sw, mc[jn + 1] + sw};
-                bool allm = true;
-                for (size_t jn = 1; jn + 1 < c.size() && allm; jn += 2) {
-                    bool hit = false;
-                    for (int64_t b1 = c[jn] - sw; b1 < c[jn] + sw && !hit; ++b1) {
-                        auto it = dd.find(b1);
-                        if (it == dd.end()) continue;
-                        const int64_t a2lo = c[jn + 1] - sw, a2hi = c[jn + 1] + sw;
-                        if (std::max(a2lo, it->second.first) < std::min(a2hi, it->second.second)) hit = true;
-                    }
-                    if (!hit) allm = false;
-                }
-                if (!allm) continue;
-                if (Mt.abundance == 0) {  // ZeroDivisionError in the reference
-                    out.err = MANDO_E_ARG;
-                    return;
-                }
-                if ((double)I.abundance / (double)Mt.abundance < P.internal_ratio) {
-                    R += I.name + " filtered because it is internal to (all bases and splice junctions contained in) " +
-                         Mt.name + " and expressed at " + std::to_string(I.abundance) + " reads compared to " +
-                         std::to_string(Mt.abundance) +
-                         " reads for the isoform containing it which is below that internal ratio of " +
-                         py_repr(P.internal_ratio) + "\n";
-                    decision = false;
-                    break;
-                } else if (std::llabs(I.coords.front() - mc.front()) < P.downstream_buffer &&
-                           std::llabs(I.coords.back() - mc.back()) < P.downstream_buffer &&
-                           I.abundance < Mt.abundance) {
-                    R += I.name + " filtered because it is internal (all bases and splice junctions contained in) and almost identical to " +
-                         Mt.name + "\n";
-                    decision = false;
-                    break;
-                }
+        if (decision && D.trig >= 0) {
+            const Iso &Mt = isos[(size_t)D.trig];
+            if (D.kind == 3) {  // ZeroDivisionError in the reference
+                out.err = MANDO_E_ARG;
+                return;
             }
+            if (D.kind == 1) {
+                R += I.name + " filtered because it is internal to (all bases and splice junctions contained in) " +
+                     Mt.name + " and expressed at " + std::to_string(I.abundance) + " reads compared to " +
+                     std::to_string(Mt.abundance) +
+                     " reads for the isoform containing it which is below that internal ratio of " +
+                     py_repr(P.internal_ratio) + "\n";
+            } else {
+                R += I.name + " filtered because it is internal (all bases and splice junctions contained in) and almost identical to " +
+                     Mt.name + "\n";
+            }
+            decision = false;
         }
         if (decision) out.kept.push_back(k);
     }
+}
+
+// filterIsoforms.process_chr for one chromosome on the host
+void process_chr(const mando_filter_params &P, const string &chrom, vector<Iso> &isos,
+                 const vector<std::pair<string_view, string_view>> &lines_raw, const string *chr_seq,
+                 const std::set<int64_t> *wl_plus, const std::set<int64_t> *wl_minus, ChrOut &out) {
+    ChrState S;
+    chr_stage1(P, chrom, isos, lines_raw, S, out);
+    if (out.err) return;
+    vector<Contain> dec;
+    dec.reserve(S.kept1.size());
+    for (int k : S.kept1) dec.push_back(contain_host(P, isos, S, k));
+    chr_stage3(P, isos, S, dec, chr_seq, wl_plus, wl_minus, out);
 }
 
 }  // namespace
@@ -600,6 +644,147 @@ int write_tables(const std::vector<std::string> &samples, const std::vector<int6
 }
 
 }  // namespace modq
+
+namespace modf {
+
+int filter_isoforms_impl(const mando_filter_params *P, const char *isoform_fasta, const char *genome_fasta,
+                         const char *clean_psl, const char *whitelist_bed, const char *out_fasta, const char *out_psl,
+                         const char *reasons_path, int64_t *n_kept, const ContainStage *stage) {
+    if (!P || !isoform_fasta || !genome_fasta || !clean_psl || !out_fasta || !out_psl) return MANDO_E_ARG;
+    std::unordered_map<string, string> isoforms, genome;
+    if (!fastx_each(isoform_fasta, [&](string_view n, string &&s) { isoforms[string(n)] = std::move(s); }))
+        return MANDO_E_ARG;
+    if (!fastx_each(genome_fasta, [&](string_view n, string &&s) { genome[string(n)] = std::move(s); }))
+        return MANDO_E_ARG;
+    string pbuf;
+    if (!read_file(clean_psl, pbuf)) return MANDO_E_ARG;
+    // collect_chromosomes (sorted) and the per-chromosome line lists (file order)
+    std::map<string, vector<std::pair<string_view, string_view>>> bychr;
+    {
+        size_t p = 0;
+        vector<string_view> a;
+        while (p < pbuf.size()) {
+            size_t e = pbuf.find('\n', p);
+            if (e == string::npos) e = pbuf.size();
+            const string_view ln(pbuf.data() + p, e - p);
+            p = e + 1;
+            split(strip(ln), '\t', a);
+            if (a.size() < 14) return MANDO_E_ARG;
+            bychr[string(a[13])].push_back({a[13], ln});
+        }
+    }
+    // readWhiteList: bed [start, end) positions per chromosome and strand (column 6)
+    std::unordered_map<string, std::set<int64_t>> wlp, wlm;
+    if (whitelist_bed) {
+        string wbuf;
+        if (read_file(whitelist_bed, wbuf)) {
+            size_t p = 0;
+            vector<string_view> a;
+            while (p < wbuf.size()) {
+                size_t e = wbuf.find('\n', p);
+                if (e == string::npos) e = wbuf.size();
+                const string_view ln(wbuf.data() + p, e - p);
+                p = e + 1;
+                split(strip(ln), '\t', a);
+                if (a.size() < 6) continue;
+                int64_t s0, e0;
+                if (!to_i64(a[1], s0) || !to_i64(a[2], e0)) return MANDO_E_ARG;
+                auto &st = a[5] == "+" ? wlp[string(a[0])] : wlm[string(a[0])];
+                for (int64_t x = s0; x < e0; ++x) st.insert(x);
+            }
+        } else {
+            return MANDO_E_ARG;  // open() fails in the reference
+        }
+    }
+    vector<string> chroms;
+    for (auto &kv : bychr) {
+        chroms.push_back(kv.first);
+        if (!genome.count(kv.first)) return MANDO_E_ARG;  // KeyError on genome_sequence[chromosome]
+    }
+    vector<vector<Iso>> isos(chroms.size());
+    vector<ChrOut> outs(chroms.size());
+    std::atomic<size_t> next{0};
+    int nth = P->threads > 0 ? P->threads : mando::usable_threads();
+    nth = (int)std::min<size_t>((size_t)nth, std::max<size_t>(1, chroms.size()));
+    auto run = [&](auto &&fn) {
+        next = 0;
+        auto work = [&]() {
+            for (size_t i; (i = next.fetch_add(1)) < chroms.size();) fn(i);
+        };
+        vector<std::thread> th;
+        for (int t = 0; t < nth; ++t) th.emplace_back(work);
+        for (auto &t : th) t.join();
+    };
+    auto seq_of = [&](size_t i) {
+        auto g = genome.find(chroms[i]);
+        return g == genome.end() ? nullptr : &g->second;
+    };
+    auto wl_of = [&](std::unordered_map<string, std::set<int64_t>> &w, size_t i) {
+        auto it = w.find(chroms[i]);
+        return it == w.end() ? nullptr : &it->second;
+    };
+    if (!stage) {
+        run([&](size_t i) {
+            process_chr(*P, chroms[i], isos[i], bychr[chroms[i]], seq_of(i), wl_of(wlp, i), wl_of(wlm, i), outs[i]);
+        });
+    } else {
+        // the parse and the ratio filter per chromosome, then every chromosome's containment search at
+        // once, then the decisions
+        vector<ChrState> states(chroms.size());
+        run([&](size_t i) { chr_stage1(*P, chroms[i], isos[i], bychr[chroms[i]], states[i], outs[i]); });
+        for (auto &o : outs)
+            if (o.err) return o.err;
+        vector<vector<Contain>> dec(chroms.size());
+        const int rc = (*stage)(*P, isos, states, dec);
+        if (rc) return rc;
+        run([&](size_t i) {
+            chr_stage3(*P, isos[i], states[i], dec[i], seq_of(i), wl_of(wlp, i), wl_of(wlm, i), outs[i]);
+        });
+    }
+    for (auto &o : outs)
+        if (o.err) return o.err;
+    FILE *fa = fopen(out_fasta, "wb");
+    FILE *fp = fopen(out_psl, "wb");
+    if (!fa || !fp) {
+        if (fa) fclose(fa);
+        if (fp) fclose(fp);
+        return MANDO_E_ARG;
+    }
+    int64_t kept = 0;
+    int rc = MANDO_OK;
+    for (size_t i = 0; i < chroms.size() && rc == MANDO_OK; ++i) {
+        for (int k : outs[i].kept) {
+            const Iso &I = isos[i][(size_t)k];
+            auto it = isoforms.find(I.name);
+            if (it == isoforms.end()) {  // KeyError in the reference
+                rc = MANDO_E_ARG;
+                break;
+            }
+            fprintf(fa, ">%s\n%s\n", I.name.c_str(), it->second.c_str());
+            string line;
+            for (size_t f = 0; f < I.fields.size(); ++f) {
+                if (f) line += '\t';
+                line += I.fields[f];
+            }
+            line += '\n';
+            fwrite(line.data(), 1, line.size(), fp);
+            ++kept;
+        }
+    }
+    fclose(fa);
+    fclose(fp);
+    if (rc) return rc;
+    if (reasons_path) {
+        FILE *fr = fopen(reasons_path, "wb");
+        if (!fr) return MANDO_E_ARG;
+        for (auto &o : outs) fwrite(o.reasons.data(), 1, o.reasons.size(), fr);
+        fclose(fr);
+    }
+    if (n_kept) *n_kept = kept;
+    return MANDO_OK;
+}
+
+}  // namespace modf
 }  // namespace mando
 
 extern "C" {
@@ -690,115 +875,8 @@ int mando_psl_to_gtf(const char *psl_path, const char *gtf_path) {
 int mando_filter_isoforms(const mando_filter_params *P, const char *isoform_fasta, const char *genome_fasta,
                           const char *clean_psl, const char *whitelist_bed, const char *out_fasta, const char *out_psl,
                           const char *reasons_path, int64_t *n_kept) {
-    if (!P || !isoform_fasta || !genome_fasta || !clean_psl || !out_fasta || !out_psl) return MANDO_E_ARG;
-    std::unordered_map<string, string> isoforms, genome;
-    if (!fastx_each(isoform_fasta, [&](string_view n, string &&s) { isoforms[string(n)] = std::move(s); }))
-        return MANDO_E_ARG;
-    if (!fastx_each(genome_fasta, [&](string_view n, string &&s) { genome[string(n)] = std::move(s); }))
-        return MANDO_E_ARG;
-    string pbuf;
-    if (!read_file(clean_psl, pbuf)) return MANDO_E_ARG;
-    // collect_chromosomes (sorted) and the per-chromosome line lists (file order)
-    std::map<string, vector<std::pair<string_view, string_view>>> bychr;
-    {
-        size_t p = 0;
-        vector<string_view> a;
-        while (p < pbuf.size()) {
-            size_t e = pbuf.find('\n', p);
-            if (e == string::npos) e = pbuf.size();
-            const string_view ln(pbuf.data() + p, e - p);
-            p = e + 1;
-            split(strip(ln), '\t', a);
-            if (a.size() < 14) return MANDO_E_ARG;
-            bychr[string(a[13])].push_back({a[13], ln});
-        }
-    }
-    // readWhiteList: bed [start, end) positions per chromosome and strand (column 6)
-    std::unordered_map<string, std::set<int64_t>> wlp, wlm;
-    if (whitelist_bed) {
-        string wbuf;
-        if (read_file(whitelist_bed, wbuf)) {
-            size_t p = 0;
-            vector<string_view> a;
-            while (p < wbuf.size()) {
-                size_t e = wbuf.find('\n', p);
-                if (e == string::npos) e = wbuf.size();
-                const string_view ln(wbuf.data() + p, e - p);
-                p = e + 1;
-                split(strip(ln), '\t', a);
-                if (a.size() < 6) continue;
-                int64_t s0, e0;
-                if (!to_i64(a[1], s0) || !to_i64(a[2], e0)) return MANDO_E_ARG;
-                auto &st = a[5] == "+" ? wlp[string(a[0])] : wlm[string(a[0])];
-                for (int64_t x = s0; x < e0; ++x) st.insert(x);
-            }
-        } else {
-            return MANDO_E_ARG;  // open() fails in the reference
-        }
-    }
-    vector<string> chroms;
-    for (auto &kv : bychr) {
-        chroms.push_back(kv.first);
-        if (!genome.count(kv.first)) return MANDO_E_ARG;  // KeyError on genome_sequence[chromosome]
-    }
-    vector<vector<Iso>> isos(chroms.size());
-    vector<ChrOut> outs(chroms.size());
-    std::atomic<size_t> next{0};
-    int nth = P->threads > 0 ? P->threads : mando::usable_threads();
-    nth = (int)std::min<size_t>((size_t)nth, std::max<size_t>(1, chroms.size()));
-    auto work = [&]() {
-        for (size_t i; (i = next.fetch_add(1)) < chroms.size();) {
-            auto g = genome.find(chroms[i]);
-            auto wp = wlp.find(chroms[i]);
-            auto wm = wlm.find(chroms[i]);
-            process_chr(*P, chroms[i], isos[i], bychr[chroms[i]], g == genome.end() ? nullptr : &g->second,
-                        wp == wlp.end() ? nullptr : &wp->second, wm == wlm.end() ? nullptr : &wm->second, outs[i]);
-        }
-    };
-    vector<std::thread> th;
-    for (int t = 0; t < nth; ++t) th.emplace_back(work);
-    for (auto &t : th) t.join();
-    for (auto &o : outs)
-        if (o.err) return o.err;
-    FILE *fa = fopen(out_fasta, "wb");
-    FILE *fp = fopen(out_psl, "wb");
-    if (!fa || !fp) {
-        if (fa) fclose(fa);
-        if (fp) fclose(fp);
-        return MANDO_E_ARG;
-    }
-    int64_t kept = 0;
-    int rc = MANDO_OK;
-    for (size_t i = 0; i < chroms.size() && rc == MANDO_OK; ++i) {
-        for (int k : outs[i].kept) {
-            const Iso &I = isos[i][(size_t)k];
-            auto it = isoforms.find(I.name);
-            if (it == isoforms.end()) {  // KeyError in the reference
-                rc = MANDO_E_ARG;
-                break;
-            }
-            fprintf(fa, ">%s\n%s\n", I.name.c_str(), it->second.c_str());
-            string line;
-            for (size_t f = 0; f < I.fields.size(); ++f) {
-                if (f) line += '\t';
-                line += I.fields[f];
-            }
-            line += '\n';
-            fwrite(line.data(), 1, line.size(), fp);
-            ++kept;
-        }
-    }
-    fclose(fa);
-    fclose(fp);
-    if (rc) return rc;
-    if (reasons_path) {
-        FILE *fr = fopen(reasons_path, "wb");
-        if (!fr) return MANDO_E_ARG;
-        for (auto &o : outs) fwrite(o.reasons.data(), 1, o.reasons.size(), fr);
-        fclose(fr);
-    }
-    if (n_kept) *n_kept = kept;
-    return MANDO_OK;
+    return mando::modf::filter_isoforms_impl(P, isoform_fasta, genome_fasta, clean_psl, whitelist_bed, out_fasta,
+                                             out_psl, reasons_path, n_kept, nullptr);
 }
 
 // assignReadsToIsoforms.py: per-sample read counts (.quant) and TPM (.tpm) of every filtered isoform
