@@ -394,6 +394,13 @@ int mando_filter_sam(const char *sam_path, const char *out_path, int64_t *n_kept
 int mando_filter_isoforms(const mando_filter_params *p, const char *isoform_fasta, const char *genome_fasta,
                           const char *clean_psl, const char *whitelist_bed, const char *out_fasta,
                           const char *out_psl, const char *reasons_path, int64_t *n_kept);
+/* mando_filter_isoforms with look_for_contained_isoforms' candidate search (filterIsoforms.py:125-278) on the
+ * GPU of ctx (modf_kernel.hip: one thread per isoform, all chromosomes in one launch); the parse, the
+ * counts, the polyA test and the reason texts are the host path's, and so are the outputs, byte for byte. */
+int mando_filter_isoforms_device(mando_ctx *ctx, const mando_filter_params *P, const char *isoform_fasta,
+                                 const char *genome_fasta, const char *clean_psl, const char *whitelist_bed,
+                                 const char *out_fasta, const char *out_psl, const char *reasons_path,
+                                 int64_t *n_kept);
 
 /* psl_to_gtf (filterIsoforms.py:413-433). */
 int mando_psl_to_gtf(const char *psl_path, const char *gtf_path);

@@ -69,6 +69,7 @@ EXPORTED = (
     "mando_filter_default_params",
     "mando_filter_sam",
     "mando_filter_isoforms",
+    "mando_filter_isoforms_device",
     "mando_psl_to_gtf",
     "mando_quantify",
     "mando_quantify_device",
@@ -233,6 +234,7 @@ def load(path: str | None = None):
         lib.mando_filter_default_params.restype = None
         lib.mando_filter_sam.argtypes = [ctypes.c_char_p, ctypes.c_char_p, _P]
         lib.mando_filter_isoforms.argtypes = [_P] + [ctypes.c_char_p] * 7 + [_P]
+        lib.mando_filter_isoforms_device.argtypes = [_P, _P] + [ctypes.c_char_p] * 7 + [_P]
         lib.mando_psl_to_gtf.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         lib.mando_quantify.argtypes = [_P, ctypes.c_int32] + [ctypes.c_char_p] * 4
         lib.mando_quantify_device.argtypes = [_P, _P, ctypes.c_int32] + [ctypes.c_char_p] * 4

@@ -41,18 +41,31 @@ def psl_to_gtf(psl_file: str, gtf_file: str) -> None:
     _lib.check(_lib.load().mando_psl_to_gtf(psl_file.encode(), gtf_file.encode()))
 
 
+def _device(device):
+    return (0 if _lib.device_count() > 0 else None) if device == "auto" else device
+
+
 def filter_isoforms(params: FilterParams, isoform_fasta: str, genome_fasta: str, clean_psl: str,
-                    whitelist_bed: str | None, out_fasta: str, out_psl: str, reasons: str | None = None) -> int:
+                    whitelist_bed: str | None, out_fasta: str, out_psl: str, reasons: str | None = None,
+                    device="auto") -> int:
+    """filterIsoforms.process_chr over every chromosome + write_isoforms.  device: a GPU ordinal runs the
+    containment search there (mando_filter_isoforms_device), None the host C++ (mando_filter_isoforms),
+    "auto" GPU 0 when one is visible; both write the same bytes."""
     n = ctypes.c_int64()
     enc = lambda x: x.encode() if x else None  # noqa: E731
-    _lib.check(_lib.load().mando_filter_isoforms(ctypes.byref(params), enc(isoform_fasta), enc(genome_fasta),
-                                                 enc(clean_psl), enc(whitelist_bed), enc(out_fasta), enc(out_psl),
-                                                 enc(reasons), ctypes.byref(n)))
+    args = (ctypes.byref(params), enc(isoform_fasta), enc(genome_fasta), enc(clean_psl), enc(whitelist_bed),
+            enc(out_fasta), enc(out_psl), enc(reasons), ctypes.byref(n))
+    dev = _device(device)
+    lib = _lib.load()
+    if dev is None:
+        _lib.check(lib.mando_filter_isoforms(*args))
+    else:
+        _lib.check(lib.mando_filter_isoforms_device(_lib.context(int(dev), slot=4).handle, *args))
     return n.value
 
 
 def module_f(path: str, isoform_fasta: str, genome_fasta: str, params: FilterParams,
-             minimap2: str | None = None, threads: int = 8) -> int:
+             minimap2: str | None = None, threads: int = 8, device="auto") -> int:
     """filterIsoforms.main (filterIsoforms.py:456-510) in `path`.  The alignment of the consensi is the
     reference's minimap2 command when `minimap2` is given; otherwise `path`/Isoforms.aligned.out.sam
     must already exist."""
@@ -73,7 +86,7 @@ def module_f(path: str, isoform_fasta: str, genome_fasta: str, params: FilterPar
     out_psl = os.path.join(path, "Isoforms.filtered.clean.psl")
     wl = os.path.join(path, "polyAWhiteList.bed")
     n = filter_isoforms(params, isoform_fasta, genome_fasta, clean, wl, out_fa, out_psl,
-                        os.path.join(path, "filter_reasons.txt"))
+                        os.path.join(path, "filter_reasons.txt"), device=device)
     psl_to_gtf(out_psl, os.path.join(path, "Isoforms.filtered.clean.gtf"))
     return n
 
@@ -85,7 +98,7 @@ def quantify(folder: str, fasta_files: list[str], device="auto") -> None:
     arr = (ctypes.c_char_p * len(fasta_files))(*[f.encode() for f in fasta_files])
     paths = [os.path.join(folder, f).encode() for f in ("reads2isoforms.txt", "Isoforms.filtered.clean.psl",
                                                           "Isoforms.filtered.clean.quant", "Isoforms.filtered.clean.tpm")]
-    dev = (0 if _lib.device_count() > 0 else None) if device == "auto" else device
+    dev = _device(device)
     lib = _lib.load()
     if dev is None:
         _lib.check(lib.mando_quantify(arr, len(fasta_files), *paths))

@@ -4,28 +4,30 @@ near-identical ends, polyA extension and the whitelist all fire), and a polyA wh
 import os
 import random
 
+import numpy as np
+
 
 def write_inputs(d, n_loci=300, seed=3, chroms=3):
     rng = random.Random(seed)
+    nrg = np.random.default_rng(seed)
     genome = {}
+    per = n_loci // chroms
     for c in range(chroms):
-        seq = [rng.choice("ACGT") for _ in range(n_loci * 4000 + 20000)]
-        # A-rich (and T-rich) stretches after some exon ends, for the polyA extension test
-        for _ in range(n_loci // 2):
-            p = rng.randrange(100, len(seq) - 100)
-            for k in range(20):
-                seq[p + k] = rng.choice("AAAAT") if rng.random() < 0.5 else rng.choice("TTTTA")
-        genome[f"chr{c + 1}"] = "".join(seq)
+        seq = np.frombuffer(b"ACGT", dtype=np.uint8)[nrg.integers(0, 4, size=per * 4000 + 20000)].copy()
+        # A-rich (and T-rich) stretches, some at exon ends, for the polyA extension test
+        for p in nrg.integers(100, len(seq) - 100, size=max(1, per // 2)):
+            base = b"AAAAT" if nrg.random() < 0.5 else b"TTTTA"
+            seq[p:p + 20] = np.frombuffer(base, dtype=np.uint8)[nrg.integers(0, 5, size=20)]
+        genome[f"chr{c + 1}"] = seq.tobytes().decode()
     with open(os.path.join(d, "genome.fa"), "w") as fh:
         for name, seq in genome.items():
             fh.write(f">{name}\n")
-            for k in range(0, len(seq), 80):
-                fh.write(seq[k:k + 80] + "\n")
+            fh.write("\n".join(seq[k:k + 80] for k in range(0, len(seq), 80)) + "\n")
     lines, cons, wl = [], [], []
     iso_id = 0
     for c in range(chroms):
         chrom = f"chr{c + 1}"
-        for loc in range(n_loci // chroms):
+        for loc in range(per):
             base = 5000 + loc * 4000
             nex = rng.randrange(1, 6)
             exons, p = [], base
