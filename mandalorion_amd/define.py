@@ -76,6 +76,19 @@ def gpu_consensus(seqs, seq_off, grp_off, seeding, device: int = 0, info: dict |
     return poa.poa_consensus_packed(seqs, seq_off, grp_off, seeding=seeding, device=device, info=info, slot=slot)
 
 
+def usable_cores() -> int:
+    """The host CPUs this process may use: its affinity, capped by the cgroup's CPU quota (cpu.max);
+    os.cpu_count() is the whole machine, on a GPU box many times this process's share."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def _roots(out_tmp: str, sizes: dict | None = None, size_array: list | None = None) -> list[str]:
     """Locus roots of tmp_SS (defineIsoforms.py:130-139); sizes (optional) receives each root's
     <root>.psl size from the same directory scan, size_array (a list, optional) one int64 array of them
@@ -525,15 +538,16 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
         pctx.set_poa_budget(hbm["poa_budget"])
 
     # with several chunks in flight, two cores stay with the GPU driver, assembly and compaction threads
-    n_cpu = threads if threads > 0 else (os.cpu_count() or 1)
+    n_cpu = threads if threads > 0 else usable_cores()
     cl_threads = max(1, n_cpu - 2) if len(parts) > 1 and n_cpu > 4 else threads
     if world > 1:
-        # several ranks on one node read their locus files from one page cache at once: 8 ranks x 2
-        # reader threads read their real 8-rank config-4 shares in 0.59 s (104 GB/s in all), 8 x 16 in
-        # 1.16-1.40 s (48 GB/s: the readers contend; profiles/r08a_read_contention_*).  So a rank's
-        # clustering reads with its share of 16 readers per node, at least 2.
+        # several ranks on one node read their locus files at once, a CPU copy out of one page cache:
+        # a rank's clustering reads with its share of the node's usable cores (at least 2).  On the
+        # one-GPU box (a 16-core quota) 8 ranks x 2 readers read their real 8-rank config-4 shares in
+        # 0.59 s (104 GB/s in all) and 8 x 16 in 1.16-1.40 s (48 GB/s: 128 threads on 16 cores;
+        # profiles/r08a_read_contention_*)
         local_world = int(os.environ.get("LOCAL_WORLD_SIZE", "0")) or world
-        cl_threads = min(cl_threads if cl_threads > 0 else n_cpu, max(2, 16 // max(1, local_world)))
+        cl_threads = min(cl_threads if cl_threads > 0 else n_cpu, max(2, usable_cores() // max(1, local_world)))
 
     # backpressure: at most _MAX_INFLIGHT chunks hold their buffers (locus text on host and device,
     # clustering results) at once -- clustering runs ahead of the POA otherwise, and a many-chunk input
