@@ -5,6 +5,7 @@ every compute entry point raises instead of falling back to a CPU implementation
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -439,6 +440,18 @@ class Context:
 
 
 _ctx_cache: dict[tuple[int, int], Context] = {}
+
+
+def close_contexts() -> None:
+    """Destroys the cached contexts (their streams, events and device buffers).  Registered at exit: the
+    library's streams each own a hardware queue, and the process should hand them back while the HIP
+    runtime is still whole (a profiler that tears the runtime down first crashed on them otherwise)."""
+    for c in list(_ctx_cache.values()):
+        c.close()
+    _ctx_cache.clear()
+
+
+atexit.register(close_contexts)
 
 
 def context(device: int = 0, slot: int = 0) -> Context:

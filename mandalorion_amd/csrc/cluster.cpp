@@ -91,9 +91,19 @@ int orient_part(mando_ctx *octx, const void *d_text, int64_t text_len, const man
     }
 }
 
+// the copy streams live until the library is unloaded (each owns a hardware queue: handed back then)
+struct CopyStreams {
+    std::vector<hipStream_t> s;
+    ~CopyStreams() {
+        for (hipStream_t x : s)
+            if (x) (void)hipStreamDestroy(x);
+    }
+};
+
 hipStream_t copy_stream(int device) {
     static std::mutex mu;
-    static std::vector<hipStream_t> streams;
+    static CopyStreams holder;
+    std::vector<hipStream_t> &streams = holder.s;
     std::lock_guard<std::mutex> g(mu);
     if ((int)streams.size() <= device) streams.resize((size_t)device + 1, nullptr);
     if (!streams[(size_t)device]) {
