@@ -386,7 +386,7 @@ def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0,
 # (0.42x each)
 _HBM_USABLE = 0.92
 # chunks whose buffers may be alive at once (clustering k+2 while k+1 waits for the POA and k is written)
-_MAX_INFLIGHT = 3
+_MAX_INFLIGHT = int(os.environ.get("MANDO_INFLIGHT", "4"))
 # multi-rank reassembly: "place" -- the ranks exchange per-root isoform counts and byte sizes (two small
 # all-gathers), send each block of their roots' output bytes to the rank that owns that range of the file
 # (one personalised exchange per file) and each writes its own contiguous range of the shared output
@@ -405,6 +405,55 @@ def poa_budget(total_hbm: int, span_text: list) -> int:
     return max(4 << 30, int(_HBM_USABLE * total_hbm) - reserve)
 
 
+# The wide groups of a chunk (bands over one 128-column chunk: the two-wave instantiation) run as a batch
+# of their own on this context slot and a host thread of their own, beside the chunk's other groups: the
+# next chunk's narrow launch then no longer waits for this chunk's wide one (a wide launch now and then
+# takes twice its time).  Every group's consensus is the same either way: the library splits
+# each batch by the same rule itself, so a group on the other side of the split here would only run in
+# the other batch as its own kind.
+_WIDE_SLOT = 5
+_SPLIT_WIDE = os.environ.get("MANDO_SPLIT_WIDE", "1") != "0"
+# the library's launch split (capi.hip poa_batch_impl): abPOA's adaptive band w = b + f * mean read
+# length (float, truncated), wide when 2w + 1 exceeds one 128-column chunk's 116 usable columns
+_BAND_B, _BAND_F, _WIDE_BAND = 10, np.float32(0.01), 116
+
+
+def _wide_groups(length, grp_off, seeding) -> np.ndarray:
+    n = np.diff(grp_off)
+    cs = np.zeros(len(length) + 1, dtype=np.int64)
+    np.cumsum(np.maximum(np.asarray(length, dtype=np.int64), 0), out=cs[1:])
+    mean = (cs[grp_off[1:]] - cs[grp_off[:-1]]) // np.maximum(n, 1)
+    w = _BAND_B + (_BAND_F * mean.astype(np.float32)).astype(np.int64)
+    wide = 2 * w + 1 > _WIDE_BAND
+    if seeding is not None:
+        wide &= np.asarray(seeding) == 0
+    return wide
+
+
+class _Pending:
+    """A part of a chunk's consensi still running on the wide context: a future of (cons, cons_off, info)
+    and the part's group indices."""
+
+    def __init__(self, fut, gidx):
+        self.fut, self.gidx = fut, gidx
+
+    def result(self):
+        cons, cons_off, info = self.fut.result()
+        return cons, cons_off, self.gidx, info
+
+
+def _group_subset(off, length, rc, grp_off, seeding, mask):
+    """The groups where mask holds, as (their indices, off, length, rc, grp_off, seeding) of a batch."""
+    gidx = np.flatnonzero(mask)
+    n = np.diff(grp_off)[gidx]
+    starts = grp_off[:-1][gidx]
+    g2 = np.zeros(len(gidx) + 1, dtype=np.int64)
+    np.cumsum(n, out=g2[1:])
+    ridx = np.repeat(starts - g2[:-1], n) + np.arange(int(g2[-1]), dtype=np.int64)
+    sd = None if seeding is None else np.asarray(seeding)[gidx]
+    return gidx, off[ridx], length[ridx], (None if rc is None else rc[ridx]), g2, sd
+
+
 def define_isoforms(path: str, *args, device: int = 0, consensus_fn: Callable | None = None, **kw) -> dict:
     """Runs the D module on <path>/tmp_SS/*.psl (arguments: _define_isoforms).  The POA context's workspace
     budget is the call's own: it goes back to the library's default policy when the call returns, so a
@@ -412,9 +461,10 @@ def define_isoforms(path: str, *args, device: int = 0, consensus_fn: Callable | 
     try:
         return _define_isoforms(path, *args, device=device, consensus_fn=consensus_fn, **kw)
     finally:
-        c = _lib._ctx_cache.get((device, 0)) if consensus_fn is None else None
-        if c is not None and c.handle is not None:
-            c.set_poa_budget(0)
+        for slot in (0, _WIDE_SLOT):
+            c = _lib._ctx_cache.get((device, slot)) if consensus_fn is None else None
+            if c is not None and c.handle is not None:
+                c.set_poa_budget(0)
 
 
 def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", splice_site_width: int = 1,
@@ -442,13 +492,15 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
     poa_slots: dict = {}
     slot_lock = threading.Lock()
 
-    def _gpu_poa(res, off, length, rc, g, sd):
-        # one device context (stream + buffers) per POA host thread: slots 0 and 3 (1: orientation)
+    def _gpu_poa(res, off, length, rc, g, sd, slot=None, record=True):
+        # one device context (stream + buffers) per POA host thread: slots 0 and 3 (1: orientation,
+        # _WIDE_SLOT: the wide groups of a split chunk)
         from . import poa
 
-        tid = threading.get_ident()
-        with slot_lock:
-            slot = poa_slots.setdefault(tid, 3 * len(poa_slots))
+        if slot is None:
+            tid = threading.get_ident()
+            with slot_lock:
+                slot = poa_slots.setdefault(tid, 3 * len(poa_slots))
         info = {}
         d, n = res.device_text()
         out = poa.poa_consensus_segments(d, n, off, length, rc, g, seeding=sd, device=device, info=info, slot=slot)
@@ -456,14 +508,28 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
             info["read_bytes"] = int(np.asarray(length, dtype=np.int64).sum())
             info["cons_bytes"] = int(out[1][-1])
             info["reads"] = int(g[-1])
-            poa_launches.append(info)
-        return out
+            if record:
+                poa_launches.append(info)
+        return out + (info,)
 
     def run_poa(res, prep):
+        """The chunk's consensi as parts [(cons, cons_off, group index or None), or _Pending]."""
         asm = prep[0]
-        if dev_poa:
-            return _gpu_poa(res, *prep[1:], asm.seeding)
-        return consensus_fn(*prep[1:], asm.seeding)
+        if not dev_poa:
+            return [consensus_fn(*prep[1:], asm.seeding) + (None,)]
+        off, length, rc, gro = prep[1:]
+        if split_wide:
+            wide = _wide_groups(length, gro, asm.seeding)
+            if wide.any() and not wide.all():
+                # the wide groups run as their own batch on their own context and thread, so that the
+                # next chunk's narrow launch does not wait for this chunk's wide one
+                sub = [_group_subset(off, length, rc, gro, asm.seeding, m) for m in (~wide, wide)]
+                add("split_wide_groups", int(wide.sum()))
+                fut = gpu_wide.submit(_gpu_poa, res, *sub[1][1:], slot=_WIDE_SLOT, record=False)
+                a = _gpu_poa(res, *sub[0][1:], record=False)
+                return [(a[0], a[1], sub[0][0], a[2]), _Pending(fut, sub[1][0])]
+        a = _gpu_poa(res, off, length, rc, gro, asm.seeding)
+        return [(a[0], a[1], None)]
     out_path = path + "/"
     out_tmp = out_path + "/tmp_SS"
     wl = list(white_list_polyA)
@@ -531,11 +597,21 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
         held = _lib.cache_trim(device, text_cap_max=big + (512 << 20),
                                scratch_max=int(1.25 * _CLUSTER_SCRATCH_PER_TEXT * big) + (1 << 30))
         hbm = {"cache_held_start": held}
+    # one rank, several chunks: each chunk's wide groups run as a separate batch (_WIDE_SLOT)
+    split_wide = dev_poa and world == 1 and len(parts) > 1 and _SPLIT_WIDE
     if dev_poa:
         pctx = _lib.context(device, 0)
         total_hbm = pctx.memory()[0]
         hbm.update(total=total_hbm, poa_budget=poa_budget(total_hbm, span_text))
-        pctx.set_poa_budget(hbm["poa_budget"])
+        if split_wide:
+            # the wide batches' context takes an eighth of the POA budget (their launches held 6-17 GB
+            # of config 4's ~195 GB), the chunk's own context the rest
+            wb = hbm["poa_budget"] // 8
+            _lib.context(device, _WIDE_SLOT).set_poa_budget(wb)
+            pctx.set_poa_budget(hbm["poa_budget"] - wb)
+            hbm["wide_budget"] = wb
+        else:
+            pctx.set_poa_budget(hbm["poa_budget"])
 
     # with several chunks in flight, two cores stay with the GPU driver, assembly and compaction threads
     n_cpu = threads if threads > 0 else usable_cores()
@@ -598,7 +674,7 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
 
     stats = {"loci": len(roots), "isoforms": 0, "poa_groups": 0, "records": 0, "poa_reads": 0,
              "t_ingest": t1 - t0, "t_cluster": 0.0, "t_pack": 0.0, "t_orient": 0.0, "t_assemble": 0.0,
-             "t_poa": 0.0, "chunks": len(parts), "poa_launches": poa_launches}
+             "t_poa": 0.0, "chunks": len(parts), "poa_launches": poa_launches, "split_wide_groups": 0}
     payloads = []
     stats["timeline"] = timeline
     stats["hbm"] = hbm
@@ -624,7 +700,7 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
     def poa_job(res, asm_fut, ix):
         prep = asm_fut.result()
         tp = time.perf_counter()
-        pl = _poa_chunk(res, mine_a[ix], prep, run_poa, stats, lock)
+        pl = _poa_chunk(res, mine_a[ix], prep, run_poa, stats, lock, poa_launches)
         timeline.append(("poa", tp - t0, time.perf_counter() - t0))
         if world > 1:
             # several ranks: the chunk's results are gathered at the end, so its referenced bytes are
@@ -639,7 +715,7 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
     # first one left free -- a quarter of the slots, the persistent grid, 2.9 s, in 3 of 30 config-3 steps)
     with ThreadPoolExecutor(max_workers=1) as ex, ThreadPoolExecutor(max_workers=1) as host, \
             ThreadPoolExecutor(max_workers=1) as writer, \
-            ThreadPoolExecutor(max_workers=1) as gpu_poa:
+            ThreadPoolExecutor(max_workers=1) as gpu_poa, ThreadPoolExecutor(max_workers=1) as gpu_wide:
         cl = [ex.submit(run_cluster, k, ix) for k, ix in enumerate(parts)]
         poa_futs = []
         # one rank: reads2isoforms.txt needs only the clustering, so each chunk's part of it is written
@@ -659,6 +735,8 @@ def _define_isoforms(path: str, cutoff: float = 0.1, genome_file: str = "None", 
             # once both of its parts are written the chunk's buffers (locus text on host and device)
             # go back to their pools, so a many-chunk run holds only the chunks in flight
             pl, res = poa_fut.result()
+            if "_finish" in pl:  # the chunk's wide groups ran beside the next chunk's POA
+                pl = pl["_finish"]()
             tw = time.perf_counter()
             n = _write_payload(pl, fa, None, counter0, threads)
             timeline.append(("write", tw - t0, time.perf_counter() - t0))
@@ -860,35 +938,62 @@ def _write_big(fh, arr: np.ndarray, piece: int = 64 << 20) -> None:
     fh.seek(at + n)
 
 
-def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, run_poa, stats: dict, lock):
-    """POA of one oriented chunk; returns its writer payload."""
+def _poa_chunk(res: cluster.ClusterResult, root_idx: Sequence[int], prep, run_poa, stats: dict, lock,
+               launches: list | None = None):
+    """POA of one oriented chunk; returns its writer payload, or {"_finish": f} when a part still runs on
+    the wide context (f() waits for it and returns the payload)."""
     asm, p_grp = prep[0], prep[-1]
     t3 = time.perf_counter()
-    cons, cons_off = run_poa(res, prep)
+    parts = run_poa(res, prep)
     t4 = time.perf_counter()
-    # consensus of every isoform as a byte segment: POA output, else (<=2 sequences, or an empty POA
-    # result) the first emission, re-bound (SDC:911-926)
-    n_iso = res.n_isoforms
-    fe = asm.first_emit
-    c_sel = np.zeros(n_iso, dtype=np.int8)                      # 0: read text, 1: POA output
-    c_start = res.seq_off[asm.e_rec[fe]] if n_iso else np.zeros(0, np.int64)
-    c_len = res.seq_len[asm.e_rec[fe]].astype(np.int64) if n_iso else np.zeros(0, np.int64)
-    c_rc = (asm.e_sign[fe] == -1).astype(np.int8) if n_iso else np.zeros(0, np.int8)
-    plen = np.diff(cons_off)
-    use = plen > 0
-    pi = asm.poa_iso[use]
-    c_sel[pi] = 1
-    c_start[pi] = cons_off[:-1][use]
-    c_len[pi] = plen[use]
-    c_rc[pi] = 0
     with lock:
-        stats["isoforms"] += n_iso
         stats["poa_groups"] += int(len(asm.poa_iso))
         stats["records"] += int(res.n_records)
         stats["poa_reads"] += int(p_grp[-1])
         stats["t_poa"] += t4 - t3
-    return dict(_names_payload(res, root_idx), cons_src=[res.text, cons], c_sel=c_sel.astype(np.int16),
-                c_start=c_start, c_len=c_len, c_rc=c_rc)
+    base = _names_payload(res, root_idx)
+
+    def finish():
+        # consensus of every isoform as a byte segment: POA output, else (<=2 sequences, or an empty POA
+        # result) the first emission, re-bound (SDC:911-926)
+        n_iso = res.n_isoforms
+        fe = asm.first_emit
+        c_sel = np.zeros(n_iso, dtype=np.int16)                     # 0: read text, k: POA part k
+        c_start = res.seq_off[asm.e_rec[fe]] if n_iso else np.zeros(0, np.int64)
+        c_len = res.seq_len[asm.e_rec[fe]].astype(np.int64) if n_iso else np.zeros(0, np.int64)
+        c_rc = (asm.e_sign[fe] == -1).astype(np.int8) if n_iso else np.zeros(0, np.int8)
+        src, infos = [res.text], []
+        for part in parts:
+            got = part.result() if isinstance(part, _Pending) else part
+            cons, cons_off, gidx = got[:3]
+            if len(got) > 3 and got[3] is not None:
+                infos.append(got[3])
+            plen = np.diff(cons_off)
+            use = plen > 0
+            g = np.flatnonzero(use) if gidx is None else gidx[use]
+            pi = asm.poa_iso[g]
+            c_sel[pi] = len(src)
+            c_start[pi] = cons_off[:-1][use]
+            c_len[pi] = plen[use]
+            c_rc[pi] = 0
+            src.append(cons)
+        if infos and launches is not None:
+            # the split chunk's parts as one entry: their launches started together, so the pair's time
+            # is the longer one's (as for the kinds of one batch)
+            with lock:
+                launches.append({"cells": sum(x.get("cells", 0) for x in infos),
+                                 "kernel_ms": max(x["kernel_ms"] for x in infos),
+                                 "launches": sum(x.get("launches", 0) for x in infos),
+                                 "read_bytes": sum(x["read_bytes"] for x in infos),
+                                 "cons_bytes": sum(x["cons_bytes"] for x in infos),
+                                 "reads": sum(x["reads"] for x in infos)})
+        with lock:
+            stats["isoforms"] += n_iso
+        return dict(base, cons_src=src, c_sel=c_sel, c_start=c_start, c_len=c_len, c_rc=c_rc)
+
+    if any(isinstance(p, _Pending) for p in parts):
+        return {"_finish": finish}
+    return finish()
 
 
 def _names_payload(res: cluster.ClusterResult, root_idx: Sequence[int]) -> dict:
