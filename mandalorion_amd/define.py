@@ -385,7 +385,8 @@ def _chunk_plan(text_bytes: int, n_loci: int, n_chunks: int = 0,
 # per call, reused, allocated with 1/4 headroom) and the reads gathered for orientation and for the POA
 # (0.42x each)
 _HBM_USABLE = 0.92
-# chunks whose buffers may be alive at once (clustering k+2 while k+1 waits for the POA and k is written)
+# chunks whose buffers may be alive at once: clustering k+2 while k+1 waits for the POA, k runs it and
+# k-1's wide part finishes and is written (the pool of locus-text buffers in poa_budget counts four)
 _MAX_INFLIGHT = int(os.environ.get("MANDO_INFLIGHT", "4"))
 # multi-rank reassembly: "place" -- the ranks exchange per-root isoform counts and byte sizes (two small
 # all-gathers), send each block of their roots' output bytes to the rank that owns that range of the file
