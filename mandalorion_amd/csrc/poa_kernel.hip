@@ -2111,6 +2111,11 @@ __device__ __forceinline__ void w2_helper(SharedState &sh, int lane) {
 // by a VALU before the block (s_nop 4).  Exec is the whole wave here (run_dp16 runs wave-uniform; the
 // scans need every lane; MANDO_CHECK_EXEC builds trap otherwise); the row records are stored with
 // exec = lane 0, exec saved in vcc around them and restored from it.
+// A row's head -- descriptor words to SGPRs, the scalar band, the ring addresses and reads up to the
+// diagonal of the (first) predecessor -- runs at wave priority 2 (the rest of the row at 0, the serial
+// phases at 3): it is the latency-bound start of the row's dependent stream, and a wave there issues
+// ahead of the co-resident waves' bulk cell work (kernel -0.7 % / -1.8 % on the config-3 / config-4
+// group shapes, profiles/r08ah_*; the scans at 2 as well, or the window up to them, gain less).
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(lds_u8 *)(const_cast<void *>(p));
@@ -2212,6 +2217,7 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_cmp_ge_i32 %[i], %[iend]\n"
             "s_cbranch_scc1 L_out%=\n"
             "s_waitcnt lgkmcnt(0)\n"
+            "s_setprio 2\n"
             "v_readfirstlane_b32 %[d1], %[Gb]\n"
             "v_readfirstlane_b32 %[p0], %[Pb]\n"
             "v_readfirstlane_b32 %[rem], %[Pa]\n"
@@ -2279,6 +2285,7 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_waitcnt lgkmcnt(0)\n"
             "v_mov_b32_dpp %[t1], %[E1] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
             "v_alignbit_b32 %[Hd], %[E1], %[t1], 16\n"
+            "s_setprio 0\n"
             "s_cmp_le_i32 %[beg], %[pc0]\n"
             "s_cbranch_scc1 L_mask1%=\n"
             "s_add_u32 %[x], %[pc0], 0x7f\n"
@@ -2568,6 +2575,7 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_waitcnt lgkmcnt(0)\n"
             "v_mov_b32_dpp %[t1], %[E1] wave_ror:1 row_mask:0xf bank_mask:0xf\n"
             "v_alignbit_b32 %[Hd], %[E1], %[t1], 16\n"
+            "s_setprio 0\n"
             "s_max_i32 %[x], %[pc0], %[pc1]\n"
             "s_cmp_le_i32 %[beg], %[x]\n"
             "s_cbranch_scc1 L_mask2%=\n"
@@ -2813,6 +2821,7 @@ __device__ __forceinline__ int fast_rows_asm(SharedState &sh, int lane, gu8 *tb,
             "s_add_i32 %[i], %[i], 1\n"
             "s_branch L_top%=\n"
             "L_out%=:\n"
+            "s_setprio 0\n"
             "s_waitcnt lgkmcnt(0)\n"
             "s_sub_i32 %[x], %[i], %[i0]\n"
             "s_add_i32 %[cel], %[cel], %[x]\n"
@@ -3269,7 +3278,9 @@ __device__ __forceinline__ int run_dp(SharedState &sh, const SC &sc, const uint8
 // is read from row i itself, so every step reads only the current row's window entry.
 // ---------------------------------------------------------------------------------------------
 constexpr int kKpNone = -2147483647 - 1;
-constexpr int kSerialPrio = 1;  // wave priority of the non-DP phases (see the read loop)
+// wave priority of the non-DP phases (see the read loop); above the fast rows' head (2, fast_rows_asm),
+// which is above the rest of a DP row (0)
+constexpr int kSerialPrio = 3;
 
 struct BtWin {
     int lo, hi, glob;  // rows [lo, hi] are in the window; glob: single row read from HBM
@@ -4613,8 +4624,9 @@ __global__ __launch_bounds__(kWave * NW, NW > 1 ? 2 : (RW == kWideRing ? MANDO_W
                     sc = SC{aa.match, aa.mismatch, aa.o1, aa.e1, aa.o2, aa.e2};
                 }
                 // The serial, latency-bound phases (descriptors, backtrack, graph update, consensus) issue
-                // ahead of the co-resident waves' DP rows (s_setprio 1; the DP runs at 0): those waves
-                // return to their DP sooner, the SIMD's issue slots stay busy (config-3 kernel -3.5 %).
+                // ahead of the co-resident waves' DP rows (s_setprio 3; the DP runs at 0, a fast row's head
+                // at 2): those waves return to their DP sooner, the SIMD's issue slots stay busy (config-3
+                // kernel -3.5 % at 1 over 0, r01).
                 // (Running a wide launch's waves two levels higher changed neither the mean step nor
                 // the slow steps: 10-step lines interleaved twice, r03 prio1.)
                 prio_serial();
